@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: correlative scan matching on MI355X (BASELINE.json config 2).
+
+Step = one ScanMatcher::OptimizePose(query) through the C-ABI
+(lgs_rtcsm_optimize_pose_query): coarse-map precompute of the 1000x1000 @ 5 cm
+grid, exhaustive +-2 m / +-30 deg correlative search for a 1081-beam scan,
+greedy-endpoint cost and covariance.  Grid and scans are resident in HBM
+before the timed region.  With --gpus N (one process per GPU, torchrun) every
+rank matches its own scans (weak scaling) and the winning poses are
+all-gathered over RCCL at the end of the timed region, as the loop-closure
+batch does.
+
+Rank 0 prints ONE JSON line (see DESIGN.md §Measurement for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "my-lidar-graph-slam_amd"))
+
+from lgs_amd import abi, scene  # noqa: E402
+
+METRIC = "scans/sec + p50 scan-match ms, 1081-beam vs 1000×1000@5cm grid, 1/2/4/8 GPU"
+PARAMS = (5, 4.0, 4.0, 1.0471976, 20.0)          # LowRes, rangeX, rangeY, rangeTheta, ScanRangeMax
+COST = (0.01, 20.0, 0.075, 0.1, 1, 0.05, 1.0)    # launcher-built CostGreedyEndpoint members
+HBM_PEAK_GBS = 8000.0                            # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
+    return ap.parse_args()
+
+
+def make_inputs(rank: int, n_scans: int):
+    world = scene.make_world()
+    ang = scene.beam_angles(1081)
+    w, h, mx, my = scene.map_geometry(1000, 100, 0.05)
+    cells = scene.approx_occupancy_map(world, scene.arc_poses(10), ang, w, h, mx, my, 0.05)
+    rng = np.random.default_rng(1000 + rank)
+    scans, inits, truths = [], [], []
+    for _ in range(n_scans):
+        true = (rng.uniform(-1.5, 1.5), rng.uniform(-1.5, 1.5), rng.uniform(-np.pi, np.pi))
+        r = scene.ray_cast(world, true, ang)
+        init = (true[0] + rng.uniform(-0.3, 0.3), true[1] + rng.uniform(-0.3, 0.3),
+                true[2] + rng.uniform(-0.2, 0.2))
+        scans.append(r)
+        inits.append(init)
+        truths.append(true)
+    return cells, (mx, my), ang, scans, inits, truths
+
+
+def cpu_baseline(cells, origin, ang, scans, inits, budget_s):
+    """Oracle (CPU restatement of the reference, 1 thread) on a bounded sample."""
+    import ctypes as C
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as ob
+    g = ob.OGrid(cells, origin[0], origin[1], 0.05)
+    prm = ob.RtcsmParams(*PARAMS)
+    cost = ob.CostGE(*COST)
+    times = []
+    t_start = time.perf_counter()
+    for r, init in zip(scans, inits):
+        osc = ob.OScan(r, ang)
+        out = ob.Summary()
+        t0 = time.perf_counter()
+        ob.lib().orc_rtcsm_optimize_pose_query(C.byref(g.g), C.byref(prm), C.byref(cost), C.byref(osc.s),
+                                               ob.Pose(*init), C.byref(out))
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s and len(times) >= 3:
+            break
+    return len(times) / sum(times), times
+
+
+def main():
+    args = parse()
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world_size > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = tdist
+
+    n_scans = args.warmup + args.steps
+    cells, origin, ang, scans, inits, truths = make_inputs(rank, min(n_scans, 256))
+
+    ctx = abi.Context(local_rank)
+    grid = ctx.grid_from_array(cells, origin[0], origin[1], 0.05)
+    dscans = [ctx.scan(r, ang) for r in scans]
+    P = abi.RtcsmParams(*PARAMS)
+    cost = abi.CostGEParams(*COST)
+    pick = lambda k: (dscans[k % len(dscans)], inits[k % len(dscans)])
+
+    for k in range(args.warmup):
+        s, i = pick(k)
+        ctx.optimize_pose_query(grid, P, cost, s, i)
+    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
+    ctx.reset_stats()
+
+    results = np.zeros((args.steps, 4))
+    lat = []
+    if dist:
+        dist.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        s, i = pick(args.warmup + k)
+        ts = time.perf_counter()
+        out = ctx.optimize_pose_query(grid, P, cost, s, i)
+        lat.append(time.perf_counter() - ts)
+        e = out.estimated_pose
+        results[k] = (e.x, e.y, e.theta, out.score_max)
+    if dist:
+        import torch
+        local = torch.from_numpy(results).to(f"cuda:{local_rank}")
+        gathered = torch.empty((world_size,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(gathered, local)
+        torch.cuda.synchronize()
+    ctx.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+
+    stats = ctx.kernel_stats()
+    ctx.set_option(abi.LGS_OPT_PROFILE, 0)
+
+    # accuracy sanity (not a parity claim): recovered pose vs ground truth
+    err = []
+    for k in range(args.steps):
+        tr = truths[(args.warmup + k) % len(truths)]
+        err.append(max(abs(results[k, 0] - tr[0]), abs(results[k, 1] - tr[1])))
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    total_scans = args.steps * world_size
+    value = total_scans / elapsed
+    kc = stats.get("k_coarse")
+    roofline = None
+    if kc and kc["launches"]:
+        per_launch_bytes = kc["algo_bytes"] / kc["launches"]
+        avg_ms = kc["total_ms"] / kc["launches"]
+        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.pmc):
+            try:
+                traffic = json.load(open(args.pmc)).get("k_coarse", {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                        kernel="k_coarse", avg_launch_ms=round(avg_ms, 5),
+                        algo_bytes_per_launch=per_launch_bytes)
+
+    cpu = None
+    if not args.no_cpu and world_size == 1:
+        cs = scans[: min(len(scans), 24)]
+        ci = inits[: len(cs)]
+        rate, times = cpu_baseline(cells, origin, ang, cs, ci, args.cpu_seconds)
+        cpu = dict(value=round(rate, 4), unit="scans/s", cores=1, kind="port",
+                   sample=f"{len(times)} config-2 scans through the oracle's OptimizePose(query) "
+                          f"(C restatement, -O2 -ffp-contract=off), p50 {1e3 * float(np.median(times)):.1f} ms",
+                   speedup=round(value / rate, 1))
+
+    lat_ms = np.array(lat) * 1e3
+    line = dict(
+        metric=METRIC, value=round(value, 2), unit="scans/s", n_gpus=world_size, steps=args.steps,
+        warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 4), higher_is_better=True,
+        scaling="weak", vs_baseline=None, dtype="f64",
+        data="synthetic: 24 m room + 40 boxes, analytic ray-cast 1081-beam scans, 10-scan occupancy map",
+        config=dict(workload="config2: 1081-beam scan, +-2 m/+-30 deg correlative match (OptimizePose(query)) "
+                             "vs 1000x1000@5cm grid, PatchSize 100",
+                    beams=1081, grid=[1000, 1000], resolution=0.05, low_resolution=5,
+                    search_range=[4.0, 4.0, 1.0471976], scans_per_rank=args.steps,
+                    parallelism=f"replicas x{world_size} (independent scans per rank) + RCCL all-gather of poses"),
+        p50_scan_match_ms=round(float(np.percentile(lat_ms, 50)), 4),
+        p90_scan_match_ms=round(float(np.percentile(lat_ms, 90)), 4),
+        roofline=roofline, cpu_baseline=cpu,
+        kernels={k: dict(launches=v["launches"], avg_ms=round(v["total_ms"] / max(1, v["launches"]), 5))
+                 for k, v in stats.items()},
+        pose_err_max_m=round(float(max(err)), 4),
+    )
+    print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,208 @@
+/*
+ * lgs_hip.h -- C-ABI of the MI355X-native scan-matching + grid-update hot path.
+ *
+ * This is the drop-in boundary.  Every entry point is plain C:
+ * opaque handles, plain pointers and sizes, an int status (LGS_OK == 0), no
+ * exceptions and no torch/HIP types in the signatures.  A C++ adapter above this
+ * ABI mirrors the reference's plugin interface (my-lidar-graph-slam_amd/host/);
+ * INTEGRATION.md shows the reference-side registration.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference root; H/ = include/my_lidar_graph_slam/, C/ = src/my_lidar_graph_slam/):
+ *
+ *   lgs_grid_precompute_max      PrecomputeGridMap(gridMap, winSize)
+ *                                C/mapping/grid_map_builder.cpp:518-536 (via
+ *                                ScanMatcherRealTimeCorrelative::ComputeCoarserMap
+ *                                C/mapping/scan_matcher_real_time_correlative.cpp:148-153)
+ *   lgs_rtcsm_optimize_pose      ScanMatcherRealTimeCorrelative::OptimizePose(
+ *                                gridMap, precompMap, scanData, initialPose, thr) const
+ *                                C/mapping/scan_matcher_real_time_correlative.cpp:50-145
+ *   lgs_rtcsm_optimize_pose_query  ScanMatcherRealTimeCorrelative::OptimizePose(query)
+ *                                C/mapping/scan_matcher_real_time_correlative.cpp:31-47
+ *                                (the ScanMatcher plugin entry, H/mapping/scan_matcher.hpp:198-199)
+ *   lgs_rtcsm_optimize_pose_batch  LoopDetectorRealTimeCorrelative::Detect's per-node
+ *                                loop C/mapping/loop_detector_real_time_correlative.cpp:66-92
+ *   lgs_cost_greedy_endpoint     CostGreedyEndpoint::Cost
+ *                                C/mapping/cost_function_greedy_endpoint.cpp:32-111
+ *   lgs_grid_integrate_scans     GridMapBuilder's per-beam ray-cast + Bayes update
+ *                                C/mapping/grid_map_builder.cpp:167-186 and :292-329
+ *   lgs_linsolve_optimize_pose   ScanMatcherLinearSolver::OptimizePose(query)
+ *                                C/mapping/scan_matcher_linear_solver.cpp:38-148
+ *
+ * Threading: one lgs_ctx per matcher instance (the reference's frontend and
+ * loop detector own distinct matchers, C/slam_launcher.cpp:774-775, :835).  A
+ * context owns one HIP stream and its scratch; calls on one context must not
+ * overlap, calls on different contexts may.
+ *
+ * Numerics: fp64 throughout.  Cell indices, hit/miss counts and the correlative
+ * argmax are bit-exact with the reference CPU path; costs/covariances agree to
+ * within 1e-5 (device exp/sin/cos differ from glibc in the last ulp).
+ */
+#ifndef LGS_HIP_H
+#define LGS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LGS_ABI_VERSION 1
+
+/* status codes */
+#define LGS_OK               0
+#define LGS_ERR_INVALID_ARG  1
+#define LGS_ERR_HIP          2
+#define LGS_ERR_NO_DEVICE    3
+#define LGS_ERR_OOM          4
+#define LGS_ERR_INTERNAL     5
+
+typedef struct lgs_ctx  lgs_ctx;   /* device, stream, scratch arena */
+typedef struct lgs_grid lgs_grid;  /* device-resident dense fp64 grid */
+typedef struct lgs_scan lgs_scan;  /* device-resident scan (ScanData<double>) */
+
+/* RobotPose2D<double> (H/pose.hpp:14-42) */
+typedef struct { double x, y, theta; } lgs_pose2d;
+
+/* Host view of a ScanData<double> (H/sensor/sensor_data.hpp:65-158) */
+typedef struct {
+    const double* ranges;        /* n */
+    const double* angles;        /* n */
+    int n;
+    lgs_pose2d rel_sensor_pose;  /* RelativeSensorPose() */
+    double min_range, max_range; /* MinRange(), MaxRange() */
+} lgs_scan_host;
+
+/* ScanMatcherRealTimeCorrelative ctor arguments
+ * (H/mapping/scan_matcher_real_time_correlative.hpp:19-25) */
+typedef struct {
+    int low_resolution;
+    double range_x, range_y, range_theta;
+    double scan_range_max;
+} lgs_rtcsm_params;
+
+/* CostGreedyEndpoint *member* values (C/mapping/cost_function_greedy_endpoint.cpp:10-28).
+ * The reference launcher passes (stddev, scale) into the (scale, stddev) slots
+ * (C/slam_launcher.cpp:70-72); callers fill these with the members as constructed. */
+typedef struct {
+    double usable_range_min, usable_range_max;
+    double hit_and_missed_dist, occupancy_threshold;
+    int kernel_size;
+    double scaling_factor;
+    double standard_deviation;
+} lgs_cost_ge_params;
+
+/* ScanMatchingSummary (H/mapping/scan_matcher.hpp:147-174) + diagnostics */
+typedef struct {
+    int pose_found;
+    double normalized_cost;
+    lgs_pose2d initial_pose;
+    lgs_pose2d estimated_pose;
+    double covariance[9];         /* row-major 3x3 */
+    /* diagnostics */
+    double score_max;             /* best (fine) score, sequential fp64 beam-order sum */
+    double score_threshold;       /* normalizedScoreThreshold * NumOfScans() */
+    int best_win[3];              /* x, y, theta window indices of the argmax */
+    int win[3];                   /* winX, winY, winTheta */
+    double steps[3];              /* stepX, stepY, stepTheta */
+    lgs_pose2d best_sensor_pose;
+    int64_t coarse_blocks;        /* coarse poses scored (all of them) */
+    int64_t fine_blocks;          /* coarse blocks refined on the fine map */
+    int guard_hits;               /* projections near a cell boundary re-checked on host */
+    int fixups;                   /* 1 if any device index differed from glibc and was patched */
+    int slow_path;                /* 1 if the exact dense fallback was taken */
+} lgs_rtcsm_summary;
+
+/* ---- context ---- */
+int  lgs_ctx_create(int device, lgs_ctx** out);
+void lgs_ctx_destroy(lgs_ctx* ctx);
+const char* lgs_ctx_last_error(const lgs_ctx* ctx);
+int  lgs_ctx_synchronize(lgs_ctx* ctx);
+void* lgs_ctx_stream(lgs_ctx* ctx);       /* hipStream_t, for interop (torch) */
+int  lgs_abi_version(void);
+
+/* Test/diagnostic knobs (never needed in production):
+ *  LGS_OPT_GUARD_EPS     boundary guard in cells (default 1e-9)
+ *  LGS_OPT_FORCE_DENSE   1 = refine every coarse block above threshold
+ *  LGS_OPT_INJECT_INDEX  1 = corrupt every guarded device index (exercises the fix-up path)
+ *  LGS_OPT_GUARD_CAP     max guard records inspected before full host re-projection */
+#define LGS_OPT_GUARD_EPS     1
+#define LGS_OPT_FORCE_DENSE   2
+#define LGS_OPT_INJECT_INDEX  3
+#define LGS_OPT_GUARD_CAP     4
+#define LGS_OPT_PROFILE       5   /* 1 = time every kernel launch with HIP events on the ctx stream */
+int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
+
+/* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is
+ * the algorithmic byte count of DESIGN.md §Roofline (e.g. 8 B per coarse-score
+ * lookup), summed over launches; total_ms sums hipEventElapsedTime. */
+typedef struct {
+    char name[32];
+    int64_t launches;
+    double total_ms;
+    double algo_bytes;
+} lgs_kernel_stat;
+int  lgs_ctx_kernel_stats(lgs_ctx* ctx, lgs_kernel_stat* out, int cap);  /* returns count (>=0) or -status */
+int  lgs_ctx_reset_stats(lgs_ctx* ctx);
+
+/* ---- grids: dense row-major fp64, cell (x,y) at y*w+x, 0.0 = unknown ---- */
+int  lgs_grid_create(lgs_ctx* ctx, int w, int h, double min_x, double min_y,
+                     double resolution, lgs_grid** out);
+/* non-owning view over existing device memory (e.g. a torch tensor) */
+int  lgs_grid_wrap(lgs_ctx* ctx, double* device_cells, int w, int h, double min_x,
+                   double min_y, double resolution, lgs_grid** out);
+void lgs_grid_destroy(lgs_grid* grid);
+int  lgs_grid_upload(lgs_ctx* ctx, lgs_grid* grid, const double* host_cells);
+int  lgs_grid_download(lgs_ctx* ctx, const lgs_grid* grid, double* host_cells);
+int  lgs_grid_fill(lgs_ctx* ctx, lgs_grid* grid, double value);
+int  lgs_grid_info(const lgs_grid* grid, int* w, int* h, double* min_x, double* min_y,
+                   double* resolution);
+double* lgs_grid_device_ptr(lgs_grid* grid);
+
+/* PrecomputeGridMap(grid, win) into `out` (same geometry). */
+int  lgs_grid_precompute_max(lgs_ctx* ctx, const lgs_grid* in, int win, lgs_grid* out);
+
+/* ---- scans: uploaded once, resident in HBM ---- */
+int  lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* host, lgs_scan** out);
+void lgs_scan_destroy(lgs_scan* scan);
+
+/* ---- correlative scan matcher ---- */
+int  lgs_rtcsm_optimize_pose(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
+                             const lgs_rtcsm_params* params,
+                             const lgs_cost_ge_params* cost,
+                             const lgs_scan* scan, lgs_pose2d initial_pose,
+                             double normalized_score_threshold,
+                             lgs_rtcsm_summary* out);
+/* OptimizePose(query): coarse map computed on device, threshold DBL_MIN */
+int  lgs_rtcsm_optimize_pose_query(lgs_ctx* ctx, const lgs_grid* grid,
+                                   const lgs_rtcsm_params* params,
+                                   const lgs_cost_ge_params* cost,
+                                   const lgs_scan* scan, lgs_pose2d initial_pose,
+                                   lgs_rtcsm_summary* out);
+/* n independent matches against one grid, enqueued back to back with one
+ * host synchronisation (loop-closure candidates, C/.../loop_detector_real_time_correlative.cpp:66) */
+int  lgs_rtcsm_optimize_pose_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
+                                   const lgs_rtcsm_params* params,
+                                   const lgs_cost_ge_params* cost,
+                                   const lgs_scan* const* scans, const lgs_pose2d* initial_poses,
+                                   int n, double normalized_score_threshold,
+                                   lgs_rtcsm_summary* out);
+/* Every coarse and fine score of the search window (kernel-level parity).
+ * dims[7] = {winX, winY, winTheta, ncx, ncy, nfx, nfy}; pass NULL score
+ * buffers to query dims.  coarse_scores[T][ncx][ncy], fine_scores[T][nfx][nfy]. */
+int  lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
+                            const lgs_rtcsm_params* params, const lgs_scan* scan,
+                            lgs_pose2d initial_pose, double* coarse_scores,
+                            double* fine_scores, int* dims);
+
+/* CostGreedyEndpoint::Cost at one sensor pose */
+int  lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
+                              const lgs_cost_ge_params* cost, const lgs_scan* scan,
+                              lgs_pose2d sensor_pose, double* out_cost);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LGS_HIP_H */

@@ -1,0 +1,520 @@
+// lgs_core.hip -- context, device arena, grids, scans and the coarse-map
+// precompute kernel (K2) of the MI355X hot-path library.
+//
+// K2 restates PrecomputeGridMap (C/mapping/grid_map_builder.cpp:518-536):
+// SlidingWindowMaxRow (:403-434) then SlidingWindowMaxCol (:437-468), each a
+// forward window max out[i] = max(in[s(i) .. s(i)+w-1]) with s(i) = min(i, n-w)
+// (the tail repeats the last full window, H/util.hpp:250-252) and 0.0 read past
+// the end when n < w.  Max is exact, so the separable pair equals one 2-D
+// window max over zero-padded input; it is computed here from an LDS tile.
+#include "lgs_internal.hpp"
+
+#include <cstring>
+
+using namespace lgs;
+
+// ---------------------------------------------------------------------------
+// context + arena
+// ---------------------------------------------------------------------------
+void* lgs_ctx::ensure(int slot, size_t bytes)
+{
+    if (bytes == 0) bytes = 16;
+    if (buf_bytes[slot] >= bytes) return buf[slot];
+    if (buf[slot]) {
+        LGS_HIP_CHECK(hipStreamSynchronize(stream));
+        LGS_HIP_CHECK(hipFree(buf[slot]));
+        buf[slot] = nullptr;
+        buf_bytes[slot] = 0;
+    }
+    size_t want = bytes + bytes / 4;  // grow with headroom
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) throw Error(LGS_ERR_OOM, "hipMalloc failed for scratch slot");
+    buf[slot] = p;
+    buf_bytes[slot] = want;
+    return p;
+}
+
+void* lgs_ctx::ensure_pinned(size_t bytes)
+{
+    if (pinned_bytes >= bytes) return pinned;
+    if (pinned) {
+        LGS_HIP_CHECK(hipStreamSynchronize(stream));
+        LGS_HIP_CHECK(hipHostFree(pinned));
+        pinned = nullptr;
+        pinned_bytes = 0;
+    }
+    size_t want = bytes + bytes / 4;
+    LGS_HIP_CHECK(hipHostMalloc(&pinned, want, hipHostMallocDefault));
+    pinned_bytes = want;
+    return pinned;
+}
+
+namespace lgs {
+const char* const kKernelNames[K_NUM_KERNELS] = { "k_project", "k_coarse", "k_seed", "k_select",
+                                                  "k_fine", "k_replay", "k_cost", "k_precompute" };
+}
+
+int lgs_ctx::timing_begin(int kernel, double algo_bytes)
+{
+    if (!profile) return -1;
+    hipEvent_t ev[2];
+    for (int i = 0; i < 2; ++i) {
+        if (!event_pool.empty()) {
+            ev[i] = event_pool.back();
+            event_pool.pop_back();
+        } else {
+            LGS_HIP_CHECK(hipEventCreate(&ev[i]));
+        }
+    }
+    LGS_HIP_CHECK(hipEventRecord(ev[0], stream));
+    pending.push_back({ kernel, ev[0], ev[1], algo_bytes });
+    return (int)pending.size() - 1;
+}
+
+void lgs_ctx::timing_end(int token)
+{
+    if (token < 0) return;
+    LGS_HIP_CHECK(hipEventRecord(pending[token].b, stream));
+}
+
+void lgs_ctx::harvest()
+{
+    for (auto& p : pending) {
+        float ms = 0.f;
+        LGS_HIP_CHECK(hipEventSynchronize(p.b));
+        LGS_HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+        stat_launches[p.kernel] += 1;
+        stat_ms[p.kernel] += ms;
+        stat_bytes[p.kernel] += p.algo_bytes;
+        event_pool.push_back(p.a);
+        event_pool.push_back(p.b);
+    }
+    pending.clear();
+}
+
+void lgs_ctx::release()
+{
+    if (stream) hipStreamSynchronize(stream);
+    for (int i = 0; i < S_NUM_SLOTS; ++i) {
+        if (buf[i]) hipFree(buf[i]);
+        buf[i] = nullptr;
+        buf_bytes[i] = 0;
+    }
+    if (pinned) hipHostFree(pinned);
+    pinned = nullptr;
+    for (auto& p : pending) {
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    pending.clear();
+    for (auto e : event_pool) hipEventDestroy(e);
+    event_pool.clear();
+    if (coarse_scratch) {
+        if (coarse_scratch->owned && coarse_scratch->d) hipFree(coarse_scratch->d);
+        delete coarse_scratch;
+        coarse_scratch = nullptr;
+    }
+    if (stream) hipStreamDestroy(stream);
+    stream = nullptr;
+}
+
+extern "C" int lgs_abi_version(void) { return LGS_ABI_VERSION; }
+
+extern "C" int lgs_ctx_create(int device, lgs_ctx** out)
+{
+    if (!out) return LGS_ERR_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return LGS_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return LGS_ERR_INVALID_ARG;
+    lgs_ctx* ctx = new lgs_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return LGS_ERR_HIP;
+    }
+    *out = ctx;
+    return LGS_OK;
+}
+
+extern "C" void lgs_ctx_destroy(lgs_ctx* ctx)
+{
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    ctx->release();
+    delete ctx;
+}
+
+extern "C" const char* lgs_ctx_last_error(const lgs_ctx* ctx)
+{
+    return ctx ? ctx->last_error.c_str() : "null context";
+}
+
+extern "C" int lgs_ctx_synchronize(lgs_ctx* ctx)
+{
+    if (!ctx) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] { LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream)); });
+}
+
+extern "C" int lgs_ctx_kernel_stats(lgs_ctx* ctx, lgs_kernel_stat* out, int cap)
+{
+    if (!ctx) return -LGS_ERR_INVALID_ARG;
+    int rc = guarded(ctx, [&] {
+        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->harvest();
+    });
+    if (rc != LGS_OK) return -rc;
+    int n = 0;
+    for (int k = 0; k < K_NUM_KERNELS; ++k) {
+        if (ctx->stat_launches[k] == 0) continue;
+        if (out && n < cap) {
+            std::memset(&out[n], 0, sizeof(out[n]));
+            std::strncpy(out[n].name, kKernelNames[k], sizeof(out[n].name) - 1);
+            out[n].launches = ctx->stat_launches[k];
+            out[n].total_ms = ctx->stat_ms[k];
+            out[n].algo_bytes = ctx->stat_bytes[k];
+        }
+        ++n;
+    }
+    return n;
+}
+
+extern "C" int lgs_ctx_reset_stats(lgs_ctx* ctx)
+{
+    if (!ctx) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->harvest();
+        for (int k = 0; k < K_NUM_KERNELS; ++k) {
+            ctx->stat_launches[k] = 0;
+            ctx->stat_ms[k] = 0;
+            ctx->stat_bytes[k] = 0;
+        }
+    });
+}
+
+extern "C" void* lgs_ctx_stream(lgs_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
+{
+    if (!ctx) return LGS_ERR_INVALID_ARG;
+    switch (option) {
+    case LGS_OPT_GUARD_EPS: ctx->guard_eps = value; return LGS_OK;
+    case LGS_OPT_FORCE_DENSE: ctx->force_dense = value != 0.0; return LGS_OK;
+    case LGS_OPT_INJECT_INDEX: ctx->inject_index = value != 0.0; return LGS_OK;
+    case LGS_OPT_PROFILE: ctx->profile = value != 0.0; return LGS_OK;
+    case LGS_OPT_GUARD_CAP:
+        ctx->guard_cap = (int)value;
+        if (ctx->guard_cap < 0) ctx->guard_cap = 0;
+        if (ctx->guard_cap > kGuardInline) ctx->guard_cap = kGuardInline;
+        return LGS_OK;
+    default: ctx->last_error = "unknown option"; return LGS_ERR_INVALID_ARG;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// grids
+// ---------------------------------------------------------------------------
+__global__ void k_fill(double* __restrict__ d, size_t n, double v)
+{
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) d[i] = v;
+}
+
+extern "C" int lgs_grid_create(lgs_ctx* ctx, int w, int h, double min_x, double min_y,
+                               double res, lgs_grid** out)
+{
+    if (!ctx || !out) return LGS_ERR_INVALID_ARG;
+    *out = nullptr;
+    return guarded(ctx, [&] {
+        LGS_REQUIRE(w >= 0 && h >= 0 && res > 0.0, "invalid grid geometry");
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        lgs_grid* g = new lgs_grid();
+        g->ctx = ctx;
+        g->w = w;
+        g->h = h;
+        g->min_x = min_x;
+        g->min_y = min_y;
+        g->res = res;
+        g->owned = true;
+        size_t bytes = (size_t)w * (size_t)h * sizeof(double);
+        if (bytes == 0) bytes = sizeof(double);
+        if (hipMalloc(&g->d, bytes) != hipSuccess) {
+            delete g;
+            throw Error(LGS_ERR_OOM, "hipMalloc failed for grid");
+        }
+        LGS_HIP_CHECK(hipMemsetAsync(g->d, 0, bytes, ctx->stream));
+        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        *out = g;
+    });
+}
+
+extern "C" int lgs_grid_wrap(lgs_ctx* ctx, double* dev, int w, int h, double min_x,
+                             double min_y, double res, lgs_grid** out)
+{
+    if (!ctx || !out) return LGS_ERR_INVALID_ARG;
+    *out = nullptr;
+    return guarded(ctx, [&] {
+        LGS_REQUIRE(dev != nullptr && w >= 0 && h >= 0 && res > 0.0, "invalid grid view");
+        lgs_grid* g = new lgs_grid();
+        g->ctx = ctx;
+        g->d = dev;
+        g->w = w;
+        g->h = h;
+        g->min_x = min_x;
+        g->min_y = min_y;
+        g->res = res;
+        g->owned = false;
+        *out = g;
+    });
+}
+
+extern "C" void lgs_grid_destroy(lgs_grid* g)
+{
+    if (!g) return;
+    if (g->owned && g->d) {
+        if (g->ctx) {
+            hipSetDevice(g->ctx->device);
+            hipStreamSynchronize(g->ctx->stream);
+        }
+        hipFree(g->d);
+    }
+    delete g;
+}
+
+extern "C" int lgs_grid_upload(lgs_ctx* ctx, lgs_grid* g, const double* host)
+{
+    if (!ctx || !g || !host) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        size_t bytes = (size_t)g->w * (size_t)g->h * sizeof(double);
+        if (!bytes) return;
+        LGS_HIP_CHECK(hipMemcpyAsync(g->d, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+extern "C" int lgs_grid_download(lgs_ctx* ctx, const lgs_grid* g, double* host)
+{
+    if (!ctx || !g || !host) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        size_t bytes = (size_t)g->w * (size_t)g->h * sizeof(double);
+        if (!bytes) return;
+        LGS_HIP_CHECK(hipMemcpyAsync(host, g->d, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+extern "C" int lgs_grid_fill(lgs_ctx* ctx, lgs_grid* g, double v)
+{
+    if (!ctx || !g) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        size_t n = (size_t)g->w * (size_t)g->h;
+        if (!n) return;
+        unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, ctx->stream, g->d, n, v);
+        LGS_HIP_CHECK(hipGetLastError());
+    });
+}
+
+extern "C" int lgs_grid_info(const lgs_grid* g, int* w, int* h, double* min_x, double* min_y,
+                             double* res)
+{
+    if (!g) return LGS_ERR_INVALID_ARG;
+    if (w) *w = g->w;
+    if (h) *h = g->h;
+    if (min_x) *min_x = g->min_x;
+    if (min_y) *min_y = g->min_y;
+    if (res) *res = g->res;
+    return LGS_OK;
+}
+
+extern "C" double* lgs_grid_device_ptr(lgs_grid* g) { return g ? g->d : nullptr; }
+
+// ---------------------------------------------------------------------------
+// K2: coarse-map precompute (2-D forward window max), LDS tiled
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kTileX = 64;
+constexpr int kTileY = 16;
+constexpr int kMaxWinTiled = 32;
+
+// window start of output i over n cells with window w (SlidingWindowMax)
+__device__ __forceinline__ int win_start(int i, int n, int w) { return (n >= w) ? min(i, n - w) : 0; }
+
+__device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b : a; }
+
+// One workgroup computes a kTileX x kTileY block of outputs.  The input
+// footprint [sx0, sx1) x [sy0, sy1) is staged in LDS (zero outside the grid),
+// then the y-pass (SlidingWindowMaxRow) and x-pass (SlidingWindowMaxCol) run
+// from LDS.
+__global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restrict__ in,
+                                                          double* __restrict__ out, int W,
+                                                          int H, int w)
+{
+    extern __shared__ double lds[];
+    const int x0 = blockIdx.x * kTileX, y0 = blockIdx.y * kTileY;
+    const int x1 = min(x0 + kTileX, W), y1 = min(y0 + kTileY, H);
+    const int sx0 = win_start(x0, W, w), sy0 = win_start(y0, H, w);
+    const int sx1 = win_start(x1 - 1, W, w) + w, sy1 = win_start(y1 - 1, H, w) + w;
+    const int fw = sx1 - sx0, fh = sy1 - sy0;  // footprint (<= tile + w - 1)
+    double* tile = lds;                          // [fh][fw]
+    double* m1 = lds + fh * fw;                  // [y1-y0][fw]
+    const int tid = threadIdx.x;
+    for (int k = tid; k < fh * fw; k += blockDim.x) {
+        const int yy = sy0 + k / fw, xx = sx0 + k % fw;
+        tile[k] = (xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;
+    }
+    __syncthreads();
+    const int oh = y1 - y0;
+    for (int k = tid; k < oh * fw; k += blockDim.x) {
+        const int oy = k / fw, cx = k % fw;
+        const int s = win_start(y0 + oy, H, w) - sy0;
+        double m = tile[s * fw + cx];
+        for (int j = 1; j < w; ++j) m = dmax(m, tile[(s + j) * fw + cx]);
+        m1[oy * fw + cx] = m;
+    }
+    __syncthreads();
+    const int ow = x1 - x0;
+    for (int k = tid; k < oh * ow; k += blockDim.x) {
+        const int oy = k / ow, ox = k % ow;
+        const int s = win_start(x0 + ox, W, w) - sx0;
+        double m = m1[oy * fw + s];
+        for (int j = 1; j < w; ++j) m = dmax(m, m1[oy * fw + s + j]);
+        out[(size_t)(y0 + oy) * W + (x0 + ox)] = m;
+    }
+}
+
+// Fallback for large windows: direct 2-D window per output.
+__global__ void k_precompute_direct(const double* __restrict__ in, double* __restrict__ out,
+                                    int W, int H, int w)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    const int sx = win_start(x, W, w), sy = win_start(y, H, w);
+    double m = 0.0;
+    bool first = true;
+    for (int yy = sy; yy < sy + w; ++yy)
+        for (int xx = sx; xx < sx + w; ++xx) {
+            const double v = (xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;
+            m = first ? v : dmax(m, v);
+            first = false;
+        }
+    out[(size_t)y * W + x] = m;
+}
+
+}  // namespace
+
+namespace lgs {
+void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out)
+{
+    if (in->w == 0 || in->h == 0) return;
+    // algorithmic bytes: two separable passes, each reading and
+    // writing one fp64 per cell = 32 B/cell
+    const int tok = ctx->timing_begin(K_PRECOMPUTE, 32.0 * (double)in->w * (double)in->h);
+    if (win <= kMaxWinTiled) {
+        const int fw = kTileX + win - 1, fh = kTileY + win - 1;
+        const size_t lds = (size_t)(fh * fw + kTileY * fw) * sizeof(double);
+        dim3 grid((in->w + kTileX - 1) / kTileX, (in->h + kTileY - 1) / kTileY);
+        hipLaunchKernelGGL(k_precompute_tiled, grid, dim3(256), lds, ctx->stream, in->d, out,
+                           in->w, in->h, win);
+    } else {
+        dim3 grid((in->w + 255) / 256, in->h);
+        hipLaunchKernelGGL(k_precompute_direct, grid, dim3(256), 0, ctx->stream, in->d, out,
+                           in->w, in->h, win);
+    }
+    ctx->timing_end(tok);
+    LGS_HIP_CHECK(hipGetLastError());
+}
+}  // namespace lgs
+
+extern "C" int lgs_grid_precompute_max(lgs_ctx* ctx, const lgs_grid* in, int win, lgs_grid* out)
+{
+    if (!ctx || !in || !out) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        LGS_REQUIRE(win >= 1, "window must be >= 1");
+        LGS_REQUIRE(out->w == in->w && out->h == in->h, "precompute output geometry mismatch");
+        LGS_REQUIRE(out->d != in->d, "precompute cannot run in place");
+        out->min_x = in->min_x;
+        out->min_y = in->min_y;
+        out->res = in->res;
+        launch_precompute(ctx, in, win, out->d);
+    });
+}
+
+// ---------------------------------------------------------------------------
+// scans
+// ---------------------------------------------------------------------------
+extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan** out)
+{
+    if (!ctx || !hs || !out) return LGS_ERR_INVALID_ARG;
+    *out = nullptr;
+    return guarded(ctx, [&] {
+        LGS_REQUIRE(hs->n >= 1 && hs->ranges && hs->angles, "scan must have >= 1 beam");
+        lgs_scan* s = new lgs_scan();
+        s->ctx = ctx;
+        s->n = hs->n;
+        s->rel = hs->rel_sensor_pose;
+        s->min_range = hs->min_range;
+        s->max_range = hs->max_range;
+        s->h_ranges.assign(hs->ranges, hs->ranges + hs->n);
+        s->h_angles.assign(hs->angles, hs->angles + hs->n);
+        double m = hs->ranges[0];  // std::max_element: first maximum
+        for (int i = 1; i < hs->n; ++i)
+            if (m < hs->ranges[i]) m = hs->ranges[i];
+        s->max_elem = m;
+        const size_t bytes = sizeof(double) * (size_t)hs->n;
+        if (hipMalloc(&s->d_ranges, bytes) != hipSuccess ||
+            hipMalloc(&s->d_angles, bytes) != hipSuccess ||
+            hipMalloc(&s->d_vidx, sizeof(int) * (size_t)hs->n) != hipSuccess) {
+            hipFree(s->d_ranges);
+            hipFree(s->d_angles);
+            delete s;
+            throw Error(LGS_ERR_OOM, "hipMalloc failed for scan");
+        }
+        LGS_HIP_CHECK(hipMemcpyAsync(s->d_ranges, hs->ranges, bytes, hipMemcpyHostToDevice, ctx->stream));
+        LGS_HIP_CHECK(hipMemcpyAsync(s->d_angles, hs->angles, bytes, hipMemcpyHostToDevice, ctx->stream));
+        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        *out = s;
+    });
+}
+
+extern "C" void lgs_scan_destroy(lgs_scan* s)
+{
+    if (!s) return;
+    if (s->ctx) {
+        hipSetDevice(s->ctx->device);
+        hipStreamSynchronize(s->ctx->stream);
+    }
+    hipFree(s->d_ranges);
+    hipFree(s->d_angles);
+    hipFree(s->d_vidx);
+    delete s;
+}
+
+namespace lgs {
+// Beams with range < ScanRangeMax in beam order (ComputeScanIndices filter,
+// C/mapping/scan_matcher_real_time_correlative.cpp:189-193).  Cached per
+// ScanRangeMax; the upload happens once per (scan, matcher).
+const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* s, double rmax, int* nv)
+{
+    if (!(s->cached_rmax == rmax)) {
+        s->h_vidx.clear();
+        for (int i = 0; i < s->n; ++i)
+            if (!(s->h_ranges[i] >= rmax)) s->h_vidx.push_back(i);
+        s->nv = (int)s->h_vidx.size();
+        if (s->nv > 0) {
+            LGS_HIP_CHECK(hipMemcpyAsync(s->d_vidx, s->h_vidx.data(), sizeof(int) * s->nv,
+                                         hipMemcpyHostToDevice, ctx->stream));
+            LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        }
+        s->cached_rmax = rmax;
+    }
+    *nv = s->nv;
+    return s->d_vidx;
+}
+}  // namespace lgs

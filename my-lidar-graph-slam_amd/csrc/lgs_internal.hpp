@@ -1,0 +1,227 @@
+// lgs_internal.hpp -- internal types of the MI355X hot-path library (not part of the ABI).
+//
+// Device layout (DESIGN.md §Data layout):
+//   grid      dense fp64, row-major, cell (x,y) at y*w + x, 0.0 = unknown/unallocated
+//   scan      ranges[n], angles[n] fp64 (SoA, as ScanData<double>)
+//   indices   int2 idx[T][Nv] projected hit cells per search angle (ComputeScanIndices)
+//   scores    coarse fp64 cscore[T*ncx*ncy] in reference block order (t, xc, yc)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "lgs_hip.h"
+
+namespace lgs {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define LGS_HIP_CHECK(expr)                                                              \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            throw ::lgs::Error(LGS_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define LGS_REQUIRE(cond, msg)                                                           \
+    do {                                                                                 \
+        if (!(cond))                                                                     \
+            throw ::lgs::Error(LGS_ERR_INVALID_ARG, msg);                                \
+    } while (0)
+
+// Scratch slots of the per-context device arena.
+enum Slot {
+    S_IDX = 0,      // int2 [T*Nv]
+    S_CSCORE,       // double [K]
+    S_CFLAG,        // uint8 [K]
+    S_SEL,          // uint8 [K]
+    S_LIST,         // int [K]
+    S_FVAL,         // double [K]
+    S_FPOS,         // int [K]
+    S_PART_C,       // double [parts]
+    S_PART_K,       // int64 [parts]
+    S_CUB_TEMP,     // hipcub temp
+    S_COUNT,        // int [4]
+    S_RECORDS,      // RtcsmRecord [batch]
+    S_POSES7,       // double [7*3]
+    S_COST_IDX,     // int4 [7*N]
+    S_COST_TERM,    // double [7*N]
+    S_PATCH,        // int4 [patches]
+    S_DENSE_FINE,   // double (dense diagnostics)
+    S_COARSE_GRID,  // double (coarse map for OptimizePose(query))
+    S_RAY0, S_RAY1, S_RAY2, S_RAY3, S_RAY4, S_RAY5, S_RAY6, S_RAY7,
+    S_LS0, S_LS1,
+    S_NUM_SLOTS
+};
+
+constexpr int kGuardInline = 64;
+
+struct GuardRec { int t, v, ix, iy; };        // projection near a cell boundary
+struct CostGuardRec { int pose_which, beam, ix, iy; };
+
+// Device-written per-scan result record (copied to host once per batch).
+struct RtcsmRecord {
+    int status;           // bit0: dangerous unsafe block -> dense rerun
+    int guard_count;
+    int cost_guard_count;
+    int found;
+    long long n_eval;     // coarse blocks refined on the fine map
+    int best[3];
+    int pad0;
+    double score_max;
+    double L;             // lower bound used for pruning
+    double costs[7];
+    GuardRec guard[kGuardInline];
+    CostGuardRec cost_guard[kGuardInline];
+};
+
+enum RecordStatus { REC_DANGEROUS = 1 };
+
+// Host-side search plan: everything the reference computes on the host before
+// the loops, evaluated with glibc (bit-exact), then shipped to kernels by value.
+struct RtcsmPlan {
+    double sx, sy, st;          // sensor pose (Compound(initialPose, relPose))
+    double step_x, step_y, step_t;
+    double min_x, min_y, res;   // grid geometry
+    double thr;                 // normalizedScoreThreshold * NumOfScans()
+    int W, H;
+    int win_x, win_y, win_t;
+    int T, ncx, ncy, P;         // angles, coarse grid per angle, P = ncx*ncy
+    int low_res;
+    int Nv;                     // beams with range < ScanRangeMax
+    int N;                      // all beams
+    long long K;                // T * P coarse blocks
+};
+
+struct CostPlan {
+    double min_range, max_range;   // filter (open interval)
+    double hit_and_missed_dist, occupancy_threshold;
+    double variance, scaling_factor;
+    double min_x, min_y, res;
+    int W, H, kernel_size, N;
+};
+
+}  // namespace lgs
+
+namespace lgs {
+enum KernelId { K_PROJECT = 0, K_COARSE, K_SEED, K_SELECT, K_FINE, K_REPLAY, K_COST, K_PRECOMPUTE, K_NUM_KERNELS };
+extern const char* const kKernelNames[K_NUM_KERNELS];
+struct PendingTiming {
+    int kernel;
+    hipEvent_t a, b;
+    double algo_bytes;
+};
+}  // namespace lgs
+
+struct lgs_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    // options
+    double guard_eps = 1e-9;
+    bool force_dense = false;
+    bool inject_index = false;
+    int guard_cap = lgs::kGuardInline;
+    // arena
+    void* buf[lgs::S_NUM_SLOTS] = {};
+    size_t buf_bytes[lgs::S_NUM_SLOTS] = {};
+    void* pinned = nullptr;
+    size_t pinned_bytes = 0;
+    lgs_grid* coarse_scratch = nullptr;
+    // profiling (LGS_OPT_PROFILE)
+    bool profile = false;
+    std::vector<lgs::PendingTiming> pending;
+    std::vector<hipEvent_t> event_pool;
+    int64_t stat_launches[lgs::K_NUM_KERNELS] = {};
+    double stat_ms[lgs::K_NUM_KERNELS] = {};
+    double stat_bytes[lgs::K_NUM_KERNELS] = {};
+
+    // profiling helpers: begin() before a launch, end() after it, harvest()
+    // after a stream synchronisation.
+    int timing_begin(int kernel, double algo_bytes);
+    void timing_end(int token);
+    void harvest();
+
+    void* ensure(int slot, size_t bytes);
+    void* ensure_pinned(size_t bytes);
+    void release();
+};
+
+struct lgs_grid {
+    lgs_ctx* ctx = nullptr;
+    double* d = nullptr;
+    int w = 0, h = 0;
+    double min_x = 0, min_y = 0, res = 0;
+    bool owned = false;
+};
+
+struct lgs_scan {
+    lgs_ctx* ctx = nullptr;
+    double* d_ranges = nullptr;
+    double* d_angles = nullptr;
+    int n = 0;
+    lgs_pose2d rel{0, 0, 0};
+    double min_range = 0, max_range = 0;
+    double max_elem = 0;                 // *std::max_element(ranges)
+    std::vector<double> h_ranges, h_angles;
+    // compaction cache: beams with range < scan_range_max, in beam order
+    double cached_rmax = NAN;
+    int nv = 0;
+    int* d_vidx = nullptr;
+    std::vector<int> h_vidx;
+};
+
+namespace lgs {
+
+// Host pose algebra restated from H/pose.hpp (glibc sin/cos, no contraction).
+inline lgs_pose2d compound(lgs_pose2d s, lgs_pose2d d)
+{
+    const double sinT = std::sin(s.theta);
+    const double cosT = std::cos(s.theta);
+    return { cosT * d.x - sinT * d.y + s.x, sinT * d.x + cosT * d.y + s.y, s.theta + d.theta };
+}
+inline lgs_pose2d move_backward(lgs_pose2d e, lgs_pose2d d)
+{
+    const double theta = e.theta - d.theta;
+    const double sinT = std::sin(theta);
+    const double cosT = std::cos(theta);
+    return { e.x - cosT * d.x + sinT * d.y, e.y - sinT * d.x - cosT * d.y, theta };
+}
+inline lgs_pose2d inverse_compound(lgs_pose2d s, lgs_pose2d e)
+{
+    const double sinT = std::sin(s.theta);
+    const double cosT = std::cos(s.theta);
+    const double dx = e.x - s.x, dy = e.y - s.y;
+    return { cosT * dx + sinT * dy, -sinT * dx + cosT * dy, e.theta - s.theta };
+}
+
+const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* scan, double scan_range_max, int* nv);
+
+// C-ABI guard: run f, map exceptions to status codes + ctx->last_error.
+template <class F>
+int guarded(lgs_ctx* ctx, F&& f)
+{
+    try {
+        f();
+        return LGS_OK;
+    } catch (const Error& e) {
+        if (ctx) ctx->last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        if (ctx) ctx->last_error = "out of host memory";
+        return LGS_ERR_OOM;
+    } catch (const std::exception& e) {
+        if (ctx) ctx->last_error = e.what();
+        return LGS_ERR_INTERNAL;
+    }
+}
+
+}  // namespace lgs

@@ -1,0 +1,329 @@
+"""ctypes binding of the C-ABI in include/lgs_hip.h (liblgs_hip.so).
+
+This is plumbing for tests and bench.py: every compute call goes through the
+HIP library.  There is no CPU fallback -- if liblgs_hip.so is missing or no
+device is present, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblgs_hip.so")
+
+LGS_OK = 0
+LGS_OPT_GUARD_EPS = 1
+LGS_OPT_FORCE_DENSE = 2
+LGS_OPT_INJECT_INDEX = 3
+LGS_OPT_GUARD_CAP = 4
+LGS_OPT_PROFILE = 5
+
+
+class Pose2D(C.Structure):
+    _fields_ = [("x", C.c_double), ("y", C.c_double), ("theta", C.c_double)]
+
+    def tuple(self):
+        return (self.x, self.y, self.theta)
+
+
+class ScanHost(C.Structure):
+    _fields_ = [
+        ("ranges", C.POINTER(C.c_double)),
+        ("angles", C.POINTER(C.c_double)),
+        ("n", C.c_int),
+        ("rel_sensor_pose", Pose2D),
+        ("min_range", C.c_double),
+        ("max_range", C.c_double),
+    ]
+
+
+class RtcsmParams(C.Structure):
+    _fields_ = [
+        ("low_resolution", C.c_int),
+        ("range_x", C.c_double),
+        ("range_y", C.c_double),
+        ("range_theta", C.c_double),
+        ("scan_range_max", C.c_double),
+    ]
+
+
+class CostGEParams(C.Structure):
+    _fields_ = [
+        ("usable_range_min", C.c_double),
+        ("usable_range_max", C.c_double),
+        ("hit_and_missed_dist", C.c_double),
+        ("occupancy_threshold", C.c_double),
+        ("kernel_size", C.c_int),
+        ("scaling_factor", C.c_double),
+        ("standard_deviation", C.c_double),
+    ]
+
+
+class RtcsmSummary(C.Structure):
+    _fields_ = [
+        ("pose_found", C.c_int),
+        ("normalized_cost", C.c_double),
+        ("initial_pose", Pose2D),
+        ("estimated_pose", Pose2D),
+        ("covariance", C.c_double * 9),
+        ("score_max", C.c_double),
+        ("score_threshold", C.c_double),
+        ("best_win", C.c_int * 3),
+        ("win", C.c_int * 3),
+        ("steps", C.c_double * 3),
+        ("best_sensor_pose", Pose2D),
+        ("coarse_blocks", C.c_int64),
+        ("fine_blocks", C.c_int64),
+        ("guard_hits", C.c_int),
+        ("fixups", C.c_int),
+        ("slow_path", C.c_int),
+    ]
+
+
+class KernelStat(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double),
+                ("algo_bytes", C.c_double)]
+
+
+# (name, restype, argtypes) for every symbol of include/lgs_hip.h
+_P = C.c_void_p
+_PROTOS = [
+    ("lgs_abi_version", C.c_int, []),
+    ("lgs_ctx_create", C.c_int, [C.c_int, C.POINTER(_P)]),
+    ("lgs_ctx_destroy", None, [_P]),
+    ("lgs_ctx_last_error", C.c_char_p, [_P]),
+    ("lgs_ctx_synchronize", C.c_int, [_P]),
+    ("lgs_ctx_stream", _P, [_P]),
+    ("lgs_ctx_set_option", C.c_int, [_P, C.c_int, C.c_double]),
+    ("lgs_ctx_kernel_stats", C.c_int, [_P, C.POINTER(KernelStat), C.c_int]),
+    ("lgs_ctx_reset_stats", C.c_int, [_P]),
+    ("lgs_grid_create", C.c_int, [_P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.POINTER(_P)]),
+    ("lgs_grid_wrap", C.c_int, [_P, _P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.POINTER(_P)]),
+    ("lgs_grid_destroy", None, [_P]),
+    ("lgs_grid_upload", C.c_int, [_P, _P, C.POINTER(C.c_double)]),
+    ("lgs_grid_download", C.c_int, [_P, _P, C.POINTER(C.c_double)]),
+    ("lgs_grid_fill", C.c_int, [_P, _P, C.c_double]),
+    ("lgs_grid_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
+                                 C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    ("lgs_grid_device_ptr", _P, [_P]),
+    ("lgs_grid_precompute_max", C.c_int, [_P, _P, C.c_int, _P]),
+    ("lgs_scan_create", C.c_int, [_P, C.POINTER(ScanHost), C.POINTER(_P)]),
+    ("lgs_scan_destroy", None, [_P]),
+    ("lgs_rtcsm_optimize_pose", C.c_int, [_P, _P, _P, C.POINTER(RtcsmParams), C.POINTER(CostGEParams), _P,
+                                          Pose2D, C.c_double, C.POINTER(RtcsmSummary)]),
+    ("lgs_rtcsm_optimize_pose_query", C.c_int, [_P, _P, C.POINTER(RtcsmParams), C.POINTER(CostGEParams), _P,
+                                                Pose2D, C.POINTER(RtcsmSummary)]),
+    ("lgs_rtcsm_optimize_pose_batch", C.c_int, [_P, _P, _P, C.POINTER(RtcsmParams), C.POINTER(CostGEParams),
+                                                C.POINTER(_P), C.POINTER(Pose2D), C.c_int, C.c_double,
+                                                C.POINTER(RtcsmSummary)]),
+    ("lgs_rtcsm_dense_scores", C.c_int, [_P, _P, _P, C.POINTER(RtcsmParams), _P, Pose2D,
+                                         C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+    ("lgs_cost_greedy_endpoint", C.c_int, [_P, _P, C.POINTER(CostGEParams), _P, Pose2D,
+                                           C.POINTER(C.c_double)]),
+]
+
+SYMBOLS = [p[0] for p in _PROTOS]
+
+_lib: Optional[C.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load liblgs_hip.so and bind prototypes.  Raises if missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"HIP extension missing: {path} (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    for name, res, args in _PROTOS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class LgsError(RuntimeError):
+    pass
+
+
+class Context:
+    """One lgs_ctx: a device + HIP stream + scratch arena."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = _P()
+        rc = self.lib.lgs_ctx_create(device, C.byref(h))
+        if rc != LGS_OK:
+            raise LgsError(f"lgs_ctx_create(device={device}) failed with status {rc}")
+        self.h = h
+
+    def check(self, rc: int, what: str):
+        if rc != LGS_OK:
+            msg = self.lib.lgs_ctx_last_error(self.h)
+            raise LgsError(f"{what}: status {rc}: {msg.decode() if msg else ''}")
+
+    def set_option(self, opt: int, value: float):
+        self.check(self.lib.lgs_ctx_set_option(self.h, opt, float(value)), "set_option")
+
+    def kernel_stats(self) -> dict:
+        """{name: dict(launches, total_ms, algo_bytes)} since the last reset."""
+        buf = (KernelStat * 16)()
+        n = self.lib.lgs_ctx_kernel_stats(self.h, buf, 16)
+        if n < 0:
+            self.check(-n, "kernel_stats")
+        return {buf[i].name.decode(): dict(launches=buf[i].launches, total_ms=buf[i].total_ms,
+                                           algo_bytes=buf[i].algo_bytes) for i in range(n)}
+
+    def reset_stats(self):
+        self.check(self.lib.lgs_ctx_reset_stats(self.h), "reset_stats")
+
+    def synchronize(self):
+        self.check(self.lib.lgs_ctx_synchronize(self.h), "synchronize")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.lgs_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- grids ----
+    def grid(self, w: int, h: int, min_x: float, min_y: float, res: float) -> "Grid":
+        g = _P()
+        self.check(self.lib.lgs_grid_create(self.h, w, h, min_x, min_y, res, C.byref(g)), "grid_create")
+        return Grid(self, g, w, h, min_x, min_y, res)
+
+    def grid_from_array(self, cells: np.ndarray, min_x: float, min_y: float, res: float) -> "Grid":
+        cells = np.ascontiguousarray(cells, dtype=np.float64)
+        h, w = cells.shape
+        g = self.grid(w, h, min_x, min_y, res)
+        g.upload(cells)
+        return g
+
+    def wrap_device(self, ptr: int, w: int, h: int, min_x: float, min_y: float, res: float) -> "Grid":
+        g = _P()
+        self.check(self.lib.lgs_grid_wrap(self.h, _P(ptr), w, h, min_x, min_y, res, C.byref(g)), "grid_wrap")
+        return Grid(self, g, w, h, min_x, min_y, res, owned=False)
+
+    def precompute_max(self, src: "Grid", win: int, out: Optional["Grid"] = None) -> "Grid":
+        if out is None:
+            out = self.grid(src.w, src.h, src.min_x, src.min_y, src.res)
+        self.check(self.lib.lgs_grid_precompute_max(self.h, src.h, int(win), out.h), "precompute_max")
+        return out
+
+    # ---- scans ----
+    def scan(self, ranges, angles, rel_pose=(0.0, 0.0, 0.0), min_range=0.0, max_range=30.0) -> "Scan":
+        r = np.ascontiguousarray(ranges, dtype=np.float64)
+        a = np.ascontiguousarray(angles, dtype=np.float64)
+        hs = ScanHost(dptr(r), dptr(a), len(r), Pose2D(*rel_pose), min_range, max_range)
+        s = _P()
+        self.check(self.lib.lgs_scan_create(self.h, C.byref(hs), C.byref(s)), "scan_create")
+        return Scan(self, s, r, a, rel_pose, min_range, max_range)
+
+    # ---- matcher ----
+    def optimize_pose(self, grid, coarse, params: RtcsmParams, cost: CostGEParams, scan, init,
+                      thr: float) -> RtcsmSummary:
+        out = RtcsmSummary()
+        rc = self.lib.lgs_rtcsm_optimize_pose(self.h, grid.h, coarse.h, C.byref(params), C.byref(cost), scan.h,
+                                              Pose2D(*init), float(thr), C.byref(out))
+        self.check(rc, "rtcsm_optimize_pose")
+        return out
+
+    def optimize_pose_query(self, grid, params: RtcsmParams, cost: CostGEParams, scan, init) -> RtcsmSummary:
+        out = RtcsmSummary()
+        rc = self.lib.lgs_rtcsm_optimize_pose_query(self.h, grid.h, C.byref(params), C.byref(cost), scan.h,
+                                                    Pose2D(*init), C.byref(out))
+        self.check(rc, "rtcsm_optimize_pose_query")
+        return out
+
+    def optimize_pose_batch(self, grid, coarse, params, cost, scans: Sequence["Scan"], inits, thr: float):
+        n = len(scans)
+        arr = (_P * n)(*[s.h for s in scans])
+        poses = (Pose2D * n)(*[Pose2D(*p) for p in inits])
+        out = (RtcsmSummary * n)()
+        rc = self.lib.lgs_rtcsm_optimize_pose_batch(self.h, grid.h, coarse.h, C.byref(params), C.byref(cost),
+                                                    arr, poses, n, float(thr), out)
+        self.check(rc, "rtcsm_optimize_pose_batch")
+        return list(out)
+
+    def dense_scores(self, grid, coarse, params, scan, init):
+        dims = (C.c_int * 7)()
+        self.check(self.lib.lgs_rtcsm_dense_scores(self.h, grid.h, coarse.h, C.byref(params), scan.h,
+                                                   Pose2D(*init), None, None, dims), "dense_scores(dims)")
+        wx, wy, wt, ncx, ncy, nfx, nfy = list(dims)
+        T = 2 * wt + 1
+        cs = np.zeros((T, ncx, ncy))
+        fs = np.zeros((T, nfx, nfy))
+        self.check(self.lib.lgs_rtcsm_dense_scores(self.h, grid.h, coarse.h, C.byref(params), scan.h,
+                                                   Pose2D(*init), dptr(cs), dptr(fs), dims), "dense_scores")
+        return list(dims), cs, fs
+
+    def cost_greedy_endpoint(self, grid, cost: CostGEParams, scan, pose) -> float:
+        v = C.c_double()
+        self.check(self.lib.lgs_cost_greedy_endpoint(self.h, grid.h, C.byref(cost), scan.h, Pose2D(*pose),
+                                                     C.byref(v)), "cost_greedy_endpoint")
+        return v.value
+
+
+class Grid:
+    def __init__(self, ctx: Context, h, w, hh, min_x, min_y, res, owned=True):
+        self.ctx, self.h = ctx, h
+        self.w, self.hgt = w, hh
+        self.min_x, self.min_y, self.res = min_x, min_y, res
+        self.owned = owned
+
+    def upload(self, cells: np.ndarray):
+        cells = np.ascontiguousarray(cells, dtype=np.float64)
+        assert cells.shape == (self.hgt, self.w)
+        self.ctx.check(self.ctx.lib.lgs_grid_upload(self.ctx.h, self.h, dptr(cells)), "grid_upload")
+
+    def download(self) -> np.ndarray:
+        out = np.zeros((self.hgt, self.w))
+        self.ctx.check(self.ctx.lib.lgs_grid_download(self.ctx.h, self.h, dptr(out)), "grid_download")
+        return out
+
+    def device_ptr(self) -> int:
+        return self.ctx.lib.lgs_grid_device_ptr(self.h)
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.lgs_grid_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Scan:
+    def __init__(self, ctx, h, ranges, angles, rel_pose, min_range, max_range):
+        self.ctx, self.h = ctx, h
+        self.ranges, self.angles = ranges, angles
+        self.rel_pose, self.min_range, self.max_range = rel_pose, min_range, max_range
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.lgs_scan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

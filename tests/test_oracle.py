@@ -1,0 +1,208 @@
+"""CPU tests of the oracle (oracle/lgs_oracle.c) against the known-answer
+vectors in tests/golden/kat.json, plus property tests of the restatement.
+
+No GPU needed.  See tests/golden/make_kat.py for where the vectors come from
+("parity unpinned": the reference has no tests and is not buildable here).
+"""
+import ctypes as C
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+
+KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kat.json")))
+DBL_MIN = 2.2250738585072014e-308
+
+
+@pytest.mark.parametrize("case", KAT["bresenham_hand"] + KAT["bresenham_py"])
+def test_bresenham_kat(case):
+    assert [list(p) for p in ob.bresenham(*case["args"])] == case["pts"]
+
+
+@pytest.mark.parametrize("case", KAT["swm_hand"] + KAT["swm_py"])
+def test_sliding_window_max_kat(case):
+    v = np.array(case["in"], dtype=np.float64)
+    out = np.zeros_like(v)
+    ob.lib().orc_sliding_window_max(ob.dp(v), 1, ob.dp(out), 1, len(v), case["win"])
+    assert out.tolist() == case["out"]
+
+
+@pytest.mark.parametrize("case", KAT["precompute_py"])
+def test_precompute_kat(case):
+    out = ob.precompute(np.array(case["grid"]), case["win"])
+    assert out.tolist() == case["out"]
+
+
+def test_bayes_kat():
+    L = ob.lib()
+    for s in KAT["bayes_py"]:
+        v = 0.0
+        for o, want in zip(s["obs"], s["values"]):
+            v = L.orc_bayes_update(v, s["p_hit"] if o == "h" else s["p_miss"])
+            assert v == want
+    for h in KAT["bayes_hand"]:
+        assert L.orc_bayes_update(h["v"], h["p"]) == h["out"]
+
+
+def test_pose_algebra_kat():
+    L = ob.lib()
+    for c in KAT["pose_py"]:
+        r = L.orc_compound(ob.Pose(*c["s"]), ob.Pose(*c["d"]))
+        assert (r.x, r.y, r.theta) == tuple(c["compound"])
+        r = L.orc_move_backward(ob.Pose(*c["s"]), ob.Pose(*c["d"]))
+        assert (r.x, r.y, r.theta) == tuple(c["move_backward"])
+
+
+@pytest.mark.parametrize("i", range(len(KAT["rtcsm_py"])))
+def test_rtcsm_search_kat(i):
+    c = KAT["rtcsm_py"][i]
+    grid = np.array(c["grid"])
+    g = ob.OGrid(grid, 0.0, 0.0, c["res"])
+    cg = ob.OGrid(ob.precompute(grid, c["low_res"]), 0.0, 0.0, c["res"])
+    sc = ob.OScan(c["ranges"], c["angles"])
+    prm = ob.RtcsmParams(c["low_res"], *c["range"], c["scan_range_max"])
+    out = ob.Summary()
+    cost = ob.CostGE(0.01, 20.0, 0.075, 0.1, 1, 0.05, 1.0)
+    ob.lib().orc_rtcsm_optimize_pose(C.byref(g.g), C.byref(cg.g), C.byref(prm), C.byref(cost), C.byref(sc.s),
+                                     ob.Pose(*c["sensor"]), c["nthr"], C.byref(out))
+    assert bool(out.pose_found) == c["found"]
+    assert out.score_max == c["score"]
+    assert list(out.best_win) == c["best"]
+    assert list(out.win) == c["win"]
+    assert out.steps[2] == c["step_t"]
+
+
+def _small_scene(seed, n=64, w=80):
+    rng = np.random.default_rng(seed)
+    grid = np.zeros((w, w))
+    k = rng.integers(0, w * w, size=w * w // 6)
+    grid.reshape(-1)[k] = rng.choice([0.45, 0.3, 0.6, 0.8, 0.999, 0.02], size=len(k))
+    ranges = rng.uniform(0.3, 1.5, size=n)
+    angles = -np.pi + np.arange(n) * (2 * np.pi / n)
+    return grid, ranges, angles
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_pruned_search_equals_dense_first_argmax(seed):
+    """SURVEY §0 finding 3, checked on the restatement: when no coarse read
+    falls left/below the map, the reference's pruned loop returns the first
+    maximum of the dense fine scores in (t, x, y) order."""
+    grid, ranges, angles = _small_scene(seed)
+    res = 0.05
+    g = ob.OGrid(grid, -2.0, -2.0, res)
+    cg = ob.OGrid(ob.precompute(grid, 5), -2.0, -2.0, res)
+    sc = ob.OScan(ranges, angles)
+    prm = ob.RtcsmParams(5, 0.6, 0.6, 0.3, 20.0)
+    init = ob.Pose(0.1, -0.05, 0.2)
+    dims = (C.c_int * 7)()
+    ob.lib().orc_rtcsm_dense_scores(C.byref(g.g), C.byref(cg.g), C.byref(prm), C.byref(sc.s), init, None, None,
+                                    dims)
+    wx, wy, wt, ncx, ncy, nfx, nfy = list(dims)
+    T = 2 * wt + 1
+    fine = np.zeros((T, nfx, nfy))
+    coarse = np.zeros((T, ncx, ncy))
+    ob.lib().orc_rtcsm_dense_scores(C.byref(g.g), C.byref(cg.g), C.byref(prm), C.byref(sc.s), init,
+                                    ob.dp(coarse), ob.dp(fine), dims)
+    out = ob.Summary()
+    cost = ob.CostGE(0.01, 20.0, 0.075, 0.1, 1, 0.05, 1.0)
+    ob.lib().orc_rtcsm_optimize_pose(C.byref(g.g), C.byref(cg.g), C.byref(prm), C.byref(cost), C.byref(sc.s),
+                                     init, DBL_MIN, C.byref(out))
+    # dense order (t, xc, yc, xf, yf): reorder fine scores block-wise
+    best = None
+    for t in range(T):
+        for jx in range(ncx):
+            for jy in range(ncy):
+                blk = fine[t, jx * 5:(jx + 1) * 5, jy * 5:(jy + 1) * 5]
+                m = blk.max()
+                if best is None or m > best[0]:
+                    xo, yo = np.argwhere(blk == m)[0]  # row-major = x outer, y inner
+                    best = (m, t - wt, -wx + jx * 5 + xo, -wy + jy * 5 + yo)
+    assert out.score_max == best[0]
+    assert list(out.best_win) == [best[2], best[3], best[1]]
+    # coarse bound property
+    for t in range(T):
+        for jx in range(ncx):
+            for jy in range(ncy):
+                assert coarse[t, jx, jy] >= fine[t, jx * 5:(jx + 1) * 5, jy * 5:(jy + 1) * 5].max()
+
+
+def test_patch_index_negative_quirk():
+    """GridCellIndexToPatchIndex (H/grid_map/grid_map.hpp:905-915): exact negative
+    multiples map one patch too low, so Resize allocates one extra patch."""
+    m = ob.OMap(0.05, 64, 0, 0)
+    assert m.geometry()["w"] == 0
+    # cell -192 = -3 * 64 -> patch -4 (not -3)
+    ob.lib().orc_map_resize(C.byref(m.m), -192 * 0.05, 0.0, 0.01, 0.01)
+    g = m.geometry()
+    assert g["npx"] == 5 and abs(g["min_x"] - (-256 * 0.05)) < 1e-12
+
+
+def test_map_init_geometry():
+    m = ob.OMap(0.05, 100, 1000, 1000)
+    assert m.geometry() == dict(w=1000, h=1000, min_x=-25.0, min_y=-25.0, npx=10, npy=10)
+    m = ob.OMap(0.05, 64, 1000, 1000)
+    g = m.geometry()
+    assert g["w"] == 1024 and abs(g["min_x"] + 25.6) < 1e-12
+
+
+def test_integrate_scan_counts(world):
+    from lgs_amd import scene
+    ang = scene.beam_angles(181)
+    pose = (0.3, -0.2, 0.4)
+    r = scene.ray_cast(world, pose, ang)
+    m = ob.OMap(0.05, 100, 600, 600)
+    bp = ob.BuilderParams(0.01, 20.0, 0.6, 0.45)
+    m.integrate(pose, ob.OScan(r, ang), bp)
+    hits = m.hits()
+    valid = ((r > 0.01) & (r < 20.0)).sum()
+    assert hits.sum() == valid
+    cells = m.cells()
+    assert ((cells > 0) == ((hits + m.misses()) > 0)).all()
+    assert cells.max() <= 0.999 and cells[cells > 0].min() >= 1e-3
+
+
+def test_construct_map_from_scans_topright_quirk():
+    """topRight starts at numeric_limits<double>::min() (C/mapping/grid_map_builder.cpp:236-237):
+    with every point at negative x/y the map still reaches x = y = 0."""
+    ang = np.linspace(np.pi, 1.5 * np.pi, 9)
+    r = np.full(9, 1.0)
+    m = ob.OMap(0.05, 16, 0, 0)
+    bp = ob.BuilderParams(0.01, 20.0, 0.6, 0.45)
+    m.construct([(-3.0, -3.0, 0.0)], [ob.OScan(r, ang)], bp)
+    g = m.geometry()
+    assert g["min_x"] + g["w"] * 0.05 > 0.0 and g["min_y"] + g["h"] * 0.05 > 0.0
+
+
+def test_linsolve_converges(world):
+    from lgs_amd import scene
+    ang = scene.beam_angles(361)
+    m = ob.OMap(0.05, 100, 600, 600)
+    bp = ob.BuilderParams(0.01, 20.0, 0.6, 0.45)
+    for p in scene.arc_poses(6):
+        m.integrate(p, ob.OScan(scene.ray_cast(world, p, ang), ang), bp)
+    g = ob.OGrid(m.cells(), m.m.min_x, m.m.min_y, 0.05)
+    true = (1.0, 0.2, 1.7)
+    sc = ob.OScan(scene.ray_cast(world, true, ang), ang)
+    lp = ob.LinsolveParams(20, 0.0, 0.01, 20.0, 1e-3, 1e-3, 0.01, 20.0)
+    out = ob.Summary()
+    traj = (ob.Pose * 20)()
+    ob.lib().orc_linsolve_optimize_pose(C.byref(g.g), C.byref(lp), C.byref(sc.s), ob.Pose(1.03, 0.18, 1.71),
+                                        C.byref(out), traj)
+    e = out.estimated_pose
+    assert abs(e.x - true[0]) < 0.03 and abs(e.y - true[1]) < 0.03 and abs(e.theta - true[2]) < 0.02
+    assert out.best_win[0] == 20
+
+
+def test_colpiv_qr_solves():
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        A = rng.normal(size=(3, 3))
+        H = A @ A.T + 1e-3 * np.eye(3)
+        b = rng.normal(size=3)
+        x = np.zeros(3)
+        ob.lib().orc_solve3_colpiv_qr(ob.dp(np.ascontiguousarray(H)), ob.dp(b), ob.dp(x))
+        assert np.allclose(H @ x, b, rtol=1e-9, atol=1e-9)
