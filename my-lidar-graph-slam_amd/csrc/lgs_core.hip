@@ -234,6 +234,7 @@ extern "C" int lgs_grid_create(lgs_ctx* ctx, int w, int h, double min_x, double 
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         lgs_grid* g = new lgs_grid();
         g->ctx = ctx;
+        g->device = ctx->device;
         g->w = w;
         g->h = h;
         g->min_x = min_x;
@@ -261,6 +262,7 @@ extern "C" int lgs_grid_wrap(lgs_ctx* ctx, double* dev, int w, int h, double min
         LGS_REQUIRE(dev != nullptr && w >= 0 && h >= 0 && res > 0.0, "invalid grid view");
         lgs_grid* g = new lgs_grid();
         g->ctx = ctx;
+        g->device = ctx->device;
         g->d = dev;
         g->w = w;
         g->h = h;
@@ -275,11 +277,10 @@ extern "C" int lgs_grid_wrap(lgs_ctx* ctx, double* dev, int w, int h, double min
 extern "C" void lgs_grid_destroy(lgs_grid* g)
 {
     if (!g) return;
+    // hipFree synchronises with the device; the creating context may already
+    // be gone, so it is not touched here.
     if (g->owned && g->d) {
-        if (g->ctx) {
-            hipSetDevice(g->ctx->device);
-            hipStreamSynchronize(g->ctx->stream);
-        }
+        hipSetDevice(g->device);
         hipFree(g->d);
     }
     delete g;
@@ -457,6 +458,7 @@ extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan**
         LGS_REQUIRE(hs->n >= 1 && hs->ranges && hs->angles, "scan must have >= 1 beam");
         lgs_scan* s = new lgs_scan();
         s->ctx = ctx;
+        s->device = ctx->device;
         s->n = hs->n;
         s->rel = hs->rel_sensor_pose;
         s->min_range = hs->min_range;
@@ -486,10 +488,7 @@ extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan**
 extern "C" void lgs_scan_destroy(lgs_scan* s)
 {
     if (!s) return;
-    if (s->ctx) {
-        hipSetDevice(s->ctx->device);
-        hipStreamSynchronize(s->ctx->stream);
-    }
+    hipSetDevice(s->device);
     hipFree(s->d_ranges);
     hipFree(s->d_angles);
     hipFree(s->d_vidx);

@@ -156,7 +156,8 @@ struct lgs_ctx {
 };
 
 struct lgs_grid {
-    lgs_ctx* ctx = nullptr;
+    lgs_ctx* ctx = nullptr;   // creating context (not used after its destruction)
+    int device = 0;
     double* d = nullptr;
     int w = 0, h = 0;
     double min_x = 0, min_y = 0, res = 0;
@@ -164,7 +165,8 @@ struct lgs_grid {
 };
 
 struct lgs_scan {
-    lgs_ctx* ctx = nullptr;
+    lgs_ctx* ctx = nullptr;   // creating context (not used after its destruction)
+    int device = 0;
     double* d_ranges = nullptr;
     double* d_angles = nullptr;
     int n = 0;

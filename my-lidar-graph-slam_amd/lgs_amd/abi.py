@@ -221,7 +221,7 @@ class Context:
 
     def precompute_max(self, src: "Grid", win: int, out: Optional["Grid"] = None) -> "Grid":
         if out is None:
-            out = self.grid(src.w, src.h, src.min_x, src.min_y, src.res)
+            out = self.grid(src.w, src.hgt, src.min_x, src.min_y, src.res)
         self.check(self.lib.lgs_grid_precompute_max(self.h, src.h, int(win), out.h), "precompute_max")
         return out
 
