@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--coarse-planes", type=int, default=1, help="A/B: 1 phase-plane coarse layout, 0 plain")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
     return ap.parse_args()
 
@@ -101,6 +102,7 @@ def main():
     cells, origin, ang, scans, inits, truths = make_inputs(rank, min(n_scans, 256))
 
     ctx = abi.Context(local_rank)
+    ctx.set_option(abi.LGS_OPT_COARSE_PLANES, args.coarse_planes)
     grid = ctx.grid_from_array(cells, origin[0], origin[1], 0.05)
     dscans = [ctx.scan(r, ang) for r in scans]
     P = abi.RtcsmParams(*PARAMS)

@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstring>
+#include <type_traits>
 
 using namespace lgs;
 
@@ -41,7 +42,6 @@ void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out);
 
 namespace {
 
-constexpr int kCoarseBlock = 256;
 
 __device__ __forceinline__ bool near_boundary(double q, double eps)
 {
@@ -53,11 +53,27 @@ __device__ __forceinline__ bool near_boundary(double q, double eps)
 // --------------------------------------------------------------------------
 // k_project: idx[t][v] = WorldCoordinateToGridCellIndex(HitPoint(pose_t, beam))
 // --------------------------------------------------------------------------
+__device__ __forceinline__ int floor_div(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+// Per (angle, beam) addressing of the coarse stage in the phase-plane layout
+// (see k_decimate): the beam's lattice starts at bx = ix - winX, by = iy - winY,
+// which lies in plane (bx mod lr, by mod lr) at (floor(bx/lr), floor(by/lr)).
+__device__ __forceinline__ int4 coarse_info(int ix, int iy, int win_x, int win_y, int lr, int Wq,
+                                            int Hq)
+{
+    const int bx = ix - win_x, by = iy - win_y;
+    const int qx0 = floor_div(bx, lr), qy0 = floor_div(by, lr);
+    const int rx = bx - lr * qx0, ry = by - lr * qy0;
+    return make_int4(qx0, qy0, (ry * lr + rx) * Wq * Hq, rx | (ry << 16));
+}
+
 __global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __restrict__ ranges,
                                                  const double* __restrict__ angles,
                                                  const int* __restrict__ vidx,
-                                                 int2* __restrict__ idx, RtcsmRecord* rec,
-                                                 int guard_cap, double guard_eps, int inject)
+                                                 int2* __restrict__ idx, int4* __restrict__ cinfo,
+                                                 int Wq, int Hq, int* __restrict__ tedge, int gen,
+                                                 RtcsmRecord* rec, int guard_cap, double guard_eps,
+                                                 int inject)
 {
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
     const int tt = blockIdx.y;
@@ -89,16 +105,36 @@ __global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __r
         }
         ix += inject;
     }
-    idx[(size_t)tt * pl.Nv + v] = make_int2(ix, iy);
+    const size_t o = (size_t)tt * pl.Nv + v;
+    idx[o] = make_int2(ix, iy);
+    cinfo[o] = coarse_info(ix, iy, pl.win_x, pl.win_y, pl.low_res, Wq, Hq);
+    // this angle has a beam whose coarse lattice starts left of / below the
+    // map: k_coarse must run its unsafe-block check (generation-stamped flag)
+    if (ix - pl.win_x < 0 || iy - pl.win_y < 0) tedge[tt] = gen;
 }
 
-__global__ void k_patch(RtcsmPlan pl, int2* __restrict__ idx, const int4* __restrict__ patches,
+__global__ void k_patch(RtcsmPlan pl, int2* __restrict__ idx, int4* __restrict__ cinfo, int Wq,
+                        int Hq, int* __restrict__ tedge, int gen, const int4* __restrict__ patches,
                         int n)
 {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const int4 p = patches[k];
-    idx[(size_t)p.x * pl.Nv + p.y] = make_int2(p.z, p.w);
+    const size_t o = (size_t)p.x * pl.Nv + p.y;
+    idx[o] = make_int2(p.z, p.w);
+    cinfo[o] = coarse_info(p.z, p.w, pl.win_x, pl.win_y, pl.low_res, Wq, Hq);
+    if (p.z - pl.win_x < 0 || p.w - pl.win_y < 0) tedge[p.x] = gen;
+}
+
+// full host projection -> coarse info
+__global__ void k_cinfo(RtcsmPlan pl, const int2* __restrict__ idx, int4* __restrict__ cinfo,
+                        int Wq, int Hq, int* __restrict__ tedge, int gen)
+{
+    const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= (size_t)pl.T * pl.Nv) return;
+    const int2 q = idx[o];
+    cinfo[o] = coarse_info(q.x, q.y, pl.win_x, pl.win_y, pl.low_res, Wq, Hq);
+    if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0) tedge[o / pl.Nv] = gen;
 }
 
 __global__ void k_cost_patch(int4* __restrict__ cidx, const int4* __restrict__ pairs, int n)
@@ -150,41 +186,138 @@ __device__ void block_argmax(double& v, long long& k, double* sv, long long* sk)
 }
 
 // --------------------------------------------------------------------------
-// k_coarse: one lane per coarse block (t, jx, jy); lanes of a wave share t
-// and sweep jx fastest, so the gathered cells of one beam are 5 cells apart.
+// Phase-plane ("decimated") coarse map.  Coarse reads of one beam are at
+// x = ix - winX + lr*jx, y = iy - winY + lr*jy: a stride-lr lattice.  Storing
+// the coarse map as lr*lr planes D[ry][rx][qy][qx] = C[lr*qy+ry][lr*qx+rx]
+// turns that lattice into a dense block of one plane, so the lanes of a wave
+// (consecutive jx) gather consecutive doubles.  Cells past the map are 0.0,
+// exactly what GridMap::Value returns out of bounds.
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(kCoarseBlock) void k_coarse(
-    RtcsmPlan pl, const double* __restrict__ cgrid, const int2* __restrict__ idx,
-    double* __restrict__ cscore, uint8_t* __restrict__ cflag, double* __restrict__ part_c,
-    long long* __restrict__ part_k)
+__global__ __launch_bounds__(256) void k_decimate(const double* __restrict__ C, int W, int H, int lr,
+                                                  int Wq, int Hq, double* __restrict__ D)
 {
-    __shared__ double sv[kCoarseBlock / 64];
-    __shared__ long long sk[kCoarseBlock / 64];
+    const int qx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int qy = blockIdx.y;
+    const int plane = blockIdx.z;  // ry * lr + rx
+    if (qx >= Wq) return;
+    const int rx = plane % lr, ry = plane / lr;
+    const int x = lr * qx + rx, y = lr * qy + ry;
+    const double v = (x < W && y < H) ? C[(size_t)y * W + x] : 0.0;
+    D[((size_t)plane * Hq + qy) * Wq + qx] = v;
+}
+
+// --------------------------------------------------------------------------
+// Sequential fp64 sum in beam order with the gathers software-pipelined:
+// batch k+1's loads are issued before batch k's values are added, so two
+// batches of loads are always in flight per lane while the add chain (the
+// reference's order, :217-221) runs.  load(v) issues one gather; beam
+// indices are wave-uniform (scalar loads).
+// --------------------------------------------------------------------------
+constexpr int kPipe = 16;
+
+// load(v) must be safe for v < n + 2*kPipe (index arrays are padded) and must
+// not branch: out-of-map lanes read a zero cell.  Adding 0.0 to the running
+// sum is an exact no-op (the sum starts at +0.0 and can never become -0.0),
+// and is exactly what GridMap::Value's default contributes for those cells.
+// fetch(v): the beam's (wave-uniform) index record; addr(rec): this lane's
+// cell address (or the zero cell).  Index records of a batch are fetched
+// together (merged scalar loads) before any address is formed.
+template <class Rec, class Fetch, class Addr>
+__device__ __forceinline__ void issue_batch(int v0, Fetch& fetch, Addr& addr, double (&buf)[kPipe])
+{
+    Rec rc[kPipe];
+#pragma unroll
+    for (int j = 0; j < kPipe; ++j) rc[j] = fetch(v0 + j);
+#pragma unroll
+    for (int j = 0; j < kPipe; ++j) buf[j] = *addr(rc[j]);
+}
+
+__device__ __forceinline__ void add_batch(double& s, const double (&buf)[kPipe], int left)
+{
+    if (left >= kPipe) {
+#pragma unroll
+        for (int j = 0; j < kPipe; ++j) s += buf[j];
+    } else {
+        for (int j = 0; j < left; ++j) s += buf[j];
+    }
+}
+
+// Two register buffers alternate roles (no copies), so while batch k is being
+// added, batch k+1's gathers are in flight.
+template <class Rec, class Fetch, class Addr>
+__device__ __forceinline__ double seq_sum(int n, Fetch fetch, Addr addr)
+{
+    double a[kPipe], b[kPipe];
+    double s = 0.0;
+    issue_batch<Rec>(0, fetch, addr, a);
+    for (int v0 = 0; v0 < n; v0 += 2 * kPipe) {
+        issue_batch<Rec>(v0 + kPipe, fetch, addr, b);
+        add_batch(s, a, n - v0);
+        if (v0 + kPipe >= n) break;
+        issue_batch<Rec>(v0 + 2 * kPipe, fetch, addr, a);
+        add_batch(s, b, n - v0 - kPipe);
+    }
+    return s;
+}
+
+// --------------------------------------------------------------------------
+// k_coarse: one lane per coarse block (t, jx, jy) of one search angle t per
+// workgroup (blockDim = P rounded up to 64); lanes sweep jx fastest.  Each lane
+// walks the beams in order: the reference's sequential fp64 sum.
+//   PLANES = 1: phase-plane coarse map (k_decimate), lanes gather consecutive
+//               doubles of one plane;
+//   PLANES = 0: the coarse map as is (stride lr between lanes).
+// --------------------------------------------------------------------------
+template <int PLANES>
+__global__ __launch_bounds__(1024) void k_coarse(
+    RtcsmPlan pl, const double* __restrict__ cmap, int Wq, int Hq, const int2* __restrict__ idx,
+    const int4* __restrict__ cinfo, const double* __restrict__ zero,
+    const int* __restrict__ tedge, int gen, double* __restrict__ cscore,
+    uint8_t* __restrict__ cflag, double* __restrict__ part_c, long long* __restrict__ part_k)
+{
+    __shared__ double sv[16];
+    __shared__ long long sk[16];
     const int tt = blockIdx.y;
-    const int p = blockIdx.x * kCoarseBlock + threadIdx.x;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = p < pl.P;
     const int jx = active ? p % pl.ncx : 0;
     const int jy = active ? p / pl.ncx : 0;
-    const int xc = -pl.win_x + jx * pl.low_res;
-    const int yc = -pl.win_y + jy * pl.low_res;
+    const int lr = pl.low_res;
     const int W = pl.W, H = pl.H;
-    const int lo = -(pl.low_res - 1);
-    const int xmin = -pl.win_x, ymin = -pl.win_y;
-    const int2* __restrict__ id = idx + (size_t)tt * pl.Nv;
+    const size_t o = (size_t)tt * pl.Nv;
+    const int2* __restrict__ id = idx + o;
+    const int4* __restrict__ ci = cinfo + o;
 
-    double sum = 0.0;
+    double sum;
+    if (PLANES) {
+        sum = seq_sum<int4>(pl.Nv, [&](int v) { return ci[v]; }, [&](const int4& c) {
+            const int qx = c.x + jx, qy = c.y + jy;
+            const bool inb = ((unsigned)qx < (unsigned)Wq) & ((unsigned)qy < (unsigned)Hq);
+            const unsigned off = (unsigned)(c.z + qy * Wq + qx);
+            return inb ? cmap + off : zero;
+        });
+    } else {
+        const int xc = -pl.win_x + jx * lr, yc = -pl.win_y + jy * lr;
+        sum = seq_sum<int2>(pl.Nv, [&](int v) { return id[v]; }, [&](const int2& q) {
+            const int x = q.x + xc, y = q.y + yc;
+            const bool inb = ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
+            const unsigned off = (unsigned)(y * W + x);
+            return inb ? cmap + off : zero;
+        });
+    }
+    // unsafe: some coarse read left of / below the map while the block's fine
+    // reads can land inside (x, y >= -(lr-1)); rare, so a separate pass
     bool unsafe = false;
-#pragma unroll 8
-    for (int v = 0; v < pl.Nv; ++v) {
-        const int2 q = id[v];
-        const int x = q.x + xc;
-        const int y = q.y + yc;
-        const bool inb = ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
-        const size_t off = inb ? (size_t)y * (size_t)W + (size_t)x : 0;
-        const double val = cgrid[off];
-        sum += inb ? val : 0.0;
-        if (q.x + xmin < 0 || q.y + ymin < 0)  // wave-uniform pre-check
-            unsafe |= (x >= lo) & (x < W) & (y >= lo) & (y < H) & ((x < 0) | (y < 0));
+    if (tedge[tt] == gen) {
+        const int lo = -(lr - 1);
+        const int x0 = -pl.win_x + jx * lr, y0 = -pl.win_y + jy * lr;
+        for (int v = 0; v < pl.Nv; ++v) {
+            const int2 q = id[v];
+            if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0) {  // wave-uniform
+                const int x = q.x + x0, y = q.y + y0;
+                unsafe |= (x >= lo) & (x < W) & (y >= lo) & (y < H) & ((x < 0) | (y < 0));
+            }
+        }
     }
     const long long k = (long long)tt * pl.P + (long long)jx * pl.ncy + jy;
     if (active) {
@@ -201,63 +334,189 @@ __global__ __launch_bounds__(kCoarseBlock) void k_coarse(
     }
 }
 
-// Fine scores of one block for lanes q in [0, lr*lr): lane q -> (xo = q % lr,
-// yo = q / lr); reference order index o = xo*lr + yo (x outer, y inner, :239-240).
-__device__ __forceinline__ double fine_score(const RtcsmPlan& pl, const double* __restrict__ grid,
-                                             const int2* __restrict__ id, int xf, int yf)
-{
-    const int W = pl.W, H = pl.H;
-    double sum = 0.0;
-#pragma unroll 8
-    for (int v = 0; v < pl.Nv; ++v) {
-        const int2 q = id[v];
-        const int x = q.x + xf;
-        const int y = q.y + yf;
-        const bool inb = ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
-        const size_t off = inb ? (size_t)y * (size_t)W + (size_t)x : 0;
-        const double val = grid[off];
-        sum += inb ? val : 0.0;
-    }
-    return sum;
-}
-
+// Fine scores of one block by one wave: lane q owns pose (xo = q % lr,
+// yo = q / lr) and runs the pipelined sequential sum over the beams.  The
+// reference visits x outer, y inner (:239-240), so its order index is
+// o = xo*lr + yo; ties resolve to the smallest o.  The block's angle row of
+// beam indices is staged in LDS first (sidx, Nv + 2*kPipe entries), so the
+// per-batch index fetch is an LDS broadcast instead of a scalar-cache miss.
+// The workgroup is this one wave.
 __device__ void eval_block(const RtcsmPlan& pl, const double* __restrict__ grid,
-                           const int2* __restrict__ idx, long long k, double* sv,
-                           long long* sk, double& f, int& pos)
+                           const int2* __restrict__ idx, const double* __restrict__ zero,
+                           long long k, int2* sidx, double& f, int& pos)
 {
     const int tt = (int)(k / pl.P);
     const int rem = (int)(k % pl.P);
     const int jx = rem / pl.ncy, jy = rem % pl.ncy;
-    const int xc = -pl.win_x + jx * pl.low_res;
-    const int yc = -pl.win_y + jy * pl.low_res;
     const int lr = pl.low_res;
+    const int npose = lr * lr;
+    const int W = pl.W, H = pl.H;
     const int2* __restrict__ id = idx + (size_t)tt * pl.Nv;
+    const int lane = threadIdx.x & 63;
+    __syncthreads();
+    for (int v = lane; v < pl.Nv + 2 * kPipe; v += 64)
+        sidx[v] = (v < pl.Nv) ? id[v] : make_int2(-(1 << 28), -(1 << 28));
+    __syncthreads();
     double bv = -1.0;
     long long bo = LLONG_MAX;
-    for (int q = threadIdx.x; q < lr * lr; q += blockDim.x) {
+    for (int q = lane; q - lane < npose; q += 64) {   // wave-uniform trip count
+        const bool act = q < npose;
         const int xo = q % lr, yo = q / lr;
-        const double s = fine_score(pl, grid, id, xc + xo, yc + yo);
+        const int xf = -pl.win_x + jx * lr + xo, yf = -pl.win_y + jy * lr + yo;
+        const double s = seq_sum<int2>(pl.Nv, [&](int v) { return sidx[v]; }, [&](const int2& c) {
+            const int x = c.x + xf, y = c.y + yf;
+            const bool inb = act & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
+            const unsigned off = (unsigned)(y * W + x);
+            return inb ? grid + off : zero;
+        });
         const long long o = (long long)xo * lr + yo;
-        if (better(s, o, bv, bo)) {
+        if (act && better(s, o, bv, bo)) {
             bv = s;
             bo = o;
         }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(bv, off, 64);
+        const long long ok = __shfl_xor(bo, off, 64);
+        if (better(ov, ok, bv, bo)) {
+            bv = ov;
+            bo = ok;
+        }
+    }
+    f = bv;
+    pos = (int)bo;
+}
+
+// Transposed block evaluation for a compile-time window LR (LR <= 16): the
+// workgroup has LR waves, wave w owns block row yo = w (poses xo = 0..LR-1).
+// lane = beam of a 64-beam chunk: it gathers the LR cells of its beam in the
+// wave's row (independent loads), stores them to LDS row xo, and lanes
+// xo < LR then add their row in beam order (the reference's sequential sum).
+// Two chunks of gathers are kept in flight ahead of the adds (ping-pong, no
+// register copies).  Beam indices of the angle row are staged in LDS first.
+// Ties resolve to the smallest reference order index o = xo*LR + yo.
+constexpr int kMaxChunks = 32;   // transposed evaluator handles Nv <= 2048
+
+// compile-time loop C = 0, 2, 4, ... < MAXC; f returns false to stop
+template <int C, int MAXC, class F>
+__device__ __forceinline__ void static_for_step2(F&& f)
+{
+    if constexpr (C < MAXC) {
+        if (!f(std::integral_constant<int, C>{})) return;
+        static_for_step2<C + 2, MAXC>(f);
+    }
+}
+
+template <int LR>
+__device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ grid,
+                             const int2* __restrict__ idx, const double* __restrict__ zero,
+                             long long k, char* smem, double* sv, long long* sk, double& f,
+                             int& pos)
+{
+    constexpr int LD = 65;
+    const int tt = (int)(k / pl.P);
+    const int rem = (int)(k % pl.P);
+    const int jx = rem / pl.ncy, jy = rem % pl.ncy;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int xc = -pl.win_x + jx * LR, yr = -pl.win_y + jy * LR + wave;
+    const int W = pl.W, H = pl.H, Nv = pl.Nv;
+    const int2* __restrict__ id = idx + (size_t)tt * Nv;
+    int2* sidx = (int2*)smem;                                        // [Nv]
+    double* bufs = (double*)(smem + sizeof(int2) * (size_t)((Nv + 1) & ~1)) + wave * 2 * LR * LD;
+    const int nchunk = (Nv + 63) / 64;
+
+    __syncthreads();
+    for (int v = threadIdx.x; v < Nv; v += blockDim.x) sidx[v] = id[v];
+    __syncthreads();
+
+    double ra[LR], rb[LR];
+    auto gather = [&](int c, double (&r)[LR]) {
+        const int b = c * 64 + lane;
+        const int2 ij = sidx[min(b, Nv - 1)];
+        const bool bv = b < Nv;
+#pragma unroll
+        for (int q = 0; q < LR; ++q) {
+            const int x = ij.x + xc + q, y = ij.y + yr;
+            const bool inb = bv & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
+            const unsigned off = (unsigned)(y * W + x);
+            r[q] = *(inb ? grid + off : zero);
+        }
+    };
+    auto store = [&](const double (&r)[LR], double* buf) {
+#pragma unroll
+        for (int q = 0; q < LR; ++q) buf[q * LD + lane] = r[q];
+        // no fence: a wave's LDS operations execute in order, and a release
+        // fence here would also wait for the prefetch gathers in flight
+        __builtin_amdgcn_wave_barrier();
+    };
+    double acc = 0.0;
+    auto add_chunk = [&](int c, const double* buf) {
+        if (lane < LR) {
+            const double* row = buf + lane * LD;
+            const int cnt = min(64, Nv - c * 64);
+            double s = acc;
+            if (cnt == 64) {
+#pragma unroll 16
+                for (int b = 0; b < 64; ++b) s += row[b];
+            } else {
+                for (int b = 0; b < cnt; ++b) s += row[b];
+            }
+            acc = s;
+        }
+    };
+    // Ping-pong, fully unrolled over at most kMaxChunks chunks: without a
+    // loop header there are no phi copies of in-flight registers, so each
+    // store waits only for the older batch; sched_barrier keeps each batch's
+    // gathers contiguous and in program order.
+    gather(0, ra);
+    __builtin_amdgcn_sched_barrier(0);
+    gather(1, rb);
+    __builtin_amdgcn_sched_barrier(0);
+    static_for_step2<0, kMaxChunks>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if (c >= nchunk) return false;
+        store(ra, bufs);
+        __builtin_amdgcn_sched_barrier(0);
+        gather(c + 2, ra);
+        __builtin_amdgcn_sched_barrier(0);
+        add_chunk(c, bufs);
+        if (c + 1 >= nchunk) return false;
+        store(rb, bufs + LR * LD);
+        __builtin_amdgcn_sched_barrier(0);
+        gather(c + 3, rb);
+        __builtin_amdgcn_sched_barrier(0);
+        add_chunk(c + 1, bufs + LR * LD);
+        return true;
+    });
+    double bv = -1.0;
+    long long bo = LLONG_MAX;
+    if (lane < LR) {
+        bv = acc;
+        bo = (long long)lane * LR + wave;
     }
     block_argmax(bv, bo, sv, sk);
     f = bv;
     pos = (int)bo;
 }
 
+template <int LR>
+constexpr size_t eval_t_smem(int Nv)
+{
+    return sizeof(int2) * (size_t)((Nv + 1) & ~1) + sizeof(double) * 2 * LR * LR * 65;
+}
+
 // k_seed: best safe coarse block -> its fine max is a lower bound of the
 // final score (every safe block's fine max is <= the reference's final score).
-__global__ __launch_bounds__(256) void k_seed(RtcsmPlan pl, const double* __restrict__ grid,
-                                              const int2* __restrict__ idx,
-                                              const double* __restrict__ part_c,
-                                              const long long* __restrict__ part_k, int nparts,
-                                              double* __restrict__ Lout, int force_dense)
+// LR > 0: transposed evaluation with LR waves; LR == 0: generic one-wave path.
+template <int LR>
+__global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_seed(
+    RtcsmPlan pl, const double* __restrict__ grid, const int2* __restrict__ idx,
+    const double* __restrict__ zero, const double* __restrict__ part_c,
+    const long long* __restrict__ part_k, int nparts, double* __restrict__ Lout, int force_dense)
 {
-    __shared__ double sv[4];
-    __shared__ long long sk[4];
+    extern __shared__ char smem[];
+    __shared__ double sv[16];
+    __shared__ long long sk[16];
     double bv = -1.0;
     long long bk = LLONG_MAX;
     for (int i = threadIdx.x; i < nparts; i += blockDim.x)
@@ -277,7 +536,10 @@ __global__ __launch_bounds__(256) void k_seed(RtcsmPlan pl, const double* __rest
     }
     double f;
     int pos;
-    eval_block(pl, grid, idx, bk, sv, sk, f, pos);
+    if constexpr (LR > 0)
+        eval_block_t<LR>(pl, grid, idx, zero, bk, smem, sv, sk, f, pos);
+    else
+        eval_block(pl, grid, idx, zero, bk, (int2*)smem, f, pos);
     if (threadIdx.x == 0) *Lout = f;
 }
 
@@ -292,24 +554,28 @@ __global__ void k_select(RtcsmPlan pl, const double* __restrict__ cscore,
     sel[k] = (c > pl.thr) && (cflag[k] || c >= L) ? 1 : 0;
 }
 
-__global__ __launch_bounds__(64) void k_fine(RtcsmPlan pl, const double* __restrict__ grid,
-                                             const int2* __restrict__ idx,
-                                             const int* __restrict__ list,
-                                             const int* __restrict__ count,
-                                             double* __restrict__ fval, int* __restrict__ fpos)
+// k_fine: one workgroup per listed block (grid-stride); LR as in k_seed.
+template <int LR>
+__global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_fine(
+    RtcsmPlan pl, const double* __restrict__ grid, const int2* __restrict__ idx,
+    const double* __restrict__ zero, const int* __restrict__ list, const int* __restrict__ count,
+    double* __restrict__ fval, int* __restrict__ fpos)
 {
-    __shared__ double sv[1];
-    __shared__ long long sk[1];
+    extern __shared__ char smem[];
+    __shared__ double sv[16];
+    __shared__ long long sk[16];
     const int n = *count;
     for (int b = blockIdx.x; b < n; b += gridDim.x) {
         double f;
         int pos;
-        eval_block(pl, grid, idx, list[b], sv, sk, f, pos);
+        if constexpr (LR > 0)
+            eval_block_t<LR>(pl, grid, idx, zero, list[b], smem, sv, sk, f, pos);
+        else
+            eval_block(pl, grid, idx, zero, list[b], (int2*)smem, f, pos);
         if (threadIdx.x == 0) {
             fval[b] = f;
             fpos[b] = pos;
         }
-        __syncthreads();
     }
 }
 
@@ -368,99 +634,136 @@ __global__ void k_replay(RtcsmPlan pl, const double* __restrict__ cscore,
 }
 
 // --------------------------------------------------------------------------
-// greedy-endpoint cost: cell indices per (pose, beam), then per-pose terms
-// summed sequentially in beam order (the reference's `costValue -= exp(..)`).
+// greedy-endpoint cost, one workgroup per pose: every thread computes the
+// cells and the exp() term of its beams into LDS, then lane 0 performs the
+// reference's `costValue -= exp(..)` in beam order (filtered beams add an
+// exact -0.0 no-op), and `costValue *= scale`.
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_cost_idx(CostPlan cp, const double* __restrict__ ranges,
-                                                  const double* __restrict__ angles,
-                                                  const double* __restrict__ poses,
-                                                  int4* __restrict__ cidx, RtcsmRecord* rec,
-                                                  int guard_cap, double guard_eps, int inject)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int pi = blockIdx.y;
-    if (i >= cp.N) return;
-    const double r = ranges[i];
-    int4 out = make_int4(INT_MIN, 0, 0, 0);
-    if (!(r >= cp.max_range || r <= cp.min_range)) {
-        const double px = poses[3 * pi], py = poses[3 * pi + 1], pt = poses[3 * pi + 2];
-        const double c = cos(pt + angles[i]);
-        const double s = sin(pt + angles[i]);
-        const double q[4] = {
-            (px + r * c - cp.min_x) / cp.res,
-            (py + r * s - cp.min_y) / cp.res,
-            (px + (r - cp.hit_and_missed_dist) * c - cp.min_x) / cp.res,
-            (py + (r - cp.hit_and_missed_dist) * s - cp.min_y) / cp.res,
-        };
-        int cell[4];
-        for (int j = 0; j < 4; ++j) {
-            cell[j] = (int)floor(q[j]);
-            if (near_boundary(q[j], guard_eps)) {
-                cell[j] += inject;
-                const int slot = atomicAdd(&rec->cost_guard_count, 1);
-                if (slot < guard_cap) {
-                    CostGuardRec g;
-                    g.pose_which = pi * 4 + j;
-                    g.beam = i;
-                    g.ix = cell[j];
-                    g.iy = 0;
-                    rec->cost_guard[slot] = g;
-                }
-            }
-        }
-        out = make_int4(cell[0], cell[1], cell[2], cell[3]);
-    }
-    cidx[(size_t)pi * cp.N + i] = out;
-}
+constexpr int kCostThreads = 1024;
+constexpr int kCostLdsTerms = 8192;
 
 __device__ __forceinline__ double gval(const CostPlan& cp, const double* __restrict__ g, int x,
                                        int y)
 {
     const bool inb = ((unsigned)x < (unsigned)cp.W) & ((unsigned)y < (unsigned)cp.H);
-    return inb ? g[(size_t)y * cp.W + x] : 0.0;
+    const size_t off = inb ? (size_t)y * cp.W + x : 0;
+    const double v = g[off];
+    return inb ? v : 0.0;
 }
 
-__global__ __launch_bounds__(256) void k_cost_eval(CostPlan cp, const double* __restrict__ grid,
-                                                   const int4* __restrict__ cidx,
-                                                   double* __restrict__ terms,
-                                                   double* __restrict__ costs_out)
+// mode 0: compute cells (+ guard records) and store them in cidx;
+// mode 1: read cells from cidx (after host patches).
+__global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double* __restrict__ grid,
+                                                       const double* __restrict__ ranges,
+                                                       const double* __restrict__ angles,
+                                                       const double* __restrict__ poses,
+                                                       int4* __restrict__ cidx,
+                                                       double* __restrict__ gterms,
+                                                       RtcsmRecord* rec, int guard_cap,
+                                                       double guard_eps, int inject, int mode)
 {
+    __shared__ double lterms[kCostLdsTerms];
     const int pi = blockIdx.x;
-    const int4* __restrict__ ci = cidx + (size_t)pi * cp.N;
-    double* __restrict__ tm = terms + (size_t)pi * cp.N;
+    const bool in_lds = cp.N <= kCostLdsTerms;
+    double* __restrict__ tm = in_lds ? lterms : gterms + (size_t)pi * cp.N;
+    const double px = poses[3 * pi], py = poses[3 * pi + 1], pt = poses[3 * pi + 2];
     const int K = cp.kernel_size;
     const double lim = (K + 1) * cp.res;
     const double minSq0 = lim * lim + lim * lim;
     for (int i = threadIdx.x; i < cp.N; i += blockDim.x) {
-        const int4 c = ci[i];
-        if (c.x == INT_MIN) continue;
-        double minSq = minSq0;
-        for (int ky = -K; ky <= K; ++ky)
-            for (int kx = -K; kx <= K; ++kx) {
-                const double hv = gval(cp, grid, c.x + kx, c.y + ky);
-                const double mv = gval(cp, grid, c.z + kx, c.w + ky);
-                if (hv == 0.0 || mv == 0.0) continue;
-                if (hv < cp.occupancy_threshold || mv > cp.occupancy_threshold) continue;
-                const double dX = kx * cp.res;
-                const double dY = ky * cp.res;
-                const double sq = dX * dX + dY * dY;
-                minSq = (minSq < sq) ? minSq : sq;
+        int4 c;
+        if (mode == 0) {
+            c = make_int4(INT_MIN, 0, 0, 0);
+            const double r = ranges[i];
+            if (!(r >= cp.max_range || r <= cp.min_range)) {
+                const double cs = cos(pt + angles[i]);
+                const double sn = sin(pt + angles[i]);
+                const double q[4] = {
+                    (px + r * cs - cp.min_x) / cp.res,
+                    (py + r * sn - cp.min_y) / cp.res,
+                    (px + (r - cp.hit_and_missed_dist) * cs - cp.min_x) / cp.res,
+                    (py + (r - cp.hit_and_missed_dist) * sn - cp.min_y) / cp.res,
+                };
+                int cell[4];
+                for (int j = 0; j < 4; ++j) {
+                    cell[j] = (int)floor(q[j]);
+                    if (near_boundary(q[j], guard_eps)) {
+                        cell[j] += inject;
+                        const int slot = atomicAdd(&rec->cost_guard_count, 1);
+                        if (slot < guard_cap) {
+                            CostGuardRec g;
+                            g.pose_which = pi * 4 + j;
+                            g.beam = i;
+                            g.ix = cell[j];
+                            g.iy = 0;
+                            rec->cost_guard[slot] = g;
+                        }
+                    }
+                }
+                c = make_int4(cell[0], cell[1], cell[2], cell[3]);
             }
-        tm[i] = exp(-0.5 * minSq / cp.variance);
+            cidx[(size_t)pi * cp.N + i] = c;
+        } else {
+            c = cidx[(size_t)pi * cp.N + i];
+        }
+        double term = 0.0;
+        if (c.x != INT_MIN) {
+            double minSq = minSq0;
+            for (int ky = -K; ky <= K; ++ky)
+                for (int kx = -K; kx <= K; ++kx) {
+                    const double hv = gval(cp, grid, c.x + kx, c.y + ky);
+                    const double mv = gval(cp, grid, c.z + kx, c.w + ky);
+                    if (hv == 0.0 || mv == 0.0) continue;
+                    if (hv < cp.occupancy_threshold || mv > cp.occupancy_threshold) continue;
+                    const double dX = kx * cp.res;
+                    const double dY = ky * cp.res;
+                    const double sq = dX * dX + dY * dY;
+                    minSq = (minSq < sq) ? minSq : sq;
+                }
+            term = exp(-0.5 * minSq / cp.variance);
+        }
+        tm[i] = term;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        // costValue -= exp(..) in beam order; reads batched so that only the
+        // subtraction chain is serial
         double cost = 0.0;
-        for (int i = 0; i < cp.N; ++i)
-            if (ci[i].x != INT_MIN) cost -= tm[i];
+        int i = 0;
+        for (; i + 16 <= cp.N; i += 16) {
+            double t[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) t[j] = tm[i + j];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) cost -= t[j];
+        }
+        for (; i < cp.N; ++i) cost -= tm[i];
         cost *= cp.scaling_factor;
-        costs_out[pi] = cost;
+        rec->costs[pi] = cost;
     }
 }
 
 // --------------------------------------------------------------------------
-// dense diagnostics: every fine score of the window
+// dense diagnostics: every fine score of the window (one lane per pose)
 // --------------------------------------------------------------------------
+__device__ __forceinline__ double fine_score(const RtcsmPlan& pl, const double* __restrict__ grid,
+                                             const int2* __restrict__ id, int xf, int yf)
+{
+    const int W = pl.W, H = pl.H;
+    double sum = 0.0;
+#pragma unroll 8
+    for (int v = 0; v < pl.Nv; ++v) {
+        const int2 q = id[v];
+        const int x = q.x + xf;
+        const int y = q.y + yf;
+        const bool inb = ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
+        const size_t off = inb ? (size_t)y * (size_t)W + (size_t)x : 0;
+        const double val = grid[off];
+        sum += inb ? val : 0.0;
+    }
+    return sum;
+}
+
 __global__ __launch_bounds__(256) void k_fine_dense(RtcsmPlan pl, const double* __restrict__ grid,
                                                     const int2* __restrict__ idx, int nfx,
                                                     int nfy, double* __restrict__ out)
@@ -534,6 +837,7 @@ CostPlan make_cost_plan(const lgs_grid* grid, const lgs_cost_ge_params* c, const
 
 struct Workspace {
     int2* idx;
+    int4* cinfo;
     double* cscore;
     uint8_t* cflag;
     uint8_t* sel;
@@ -550,15 +854,30 @@ struct Workspace {
     void* cub_temp;
     size_t cub_bytes;
     int nparts;
+    double* decim;
+    int Wq, Hq;
+    double* zero;
+    int* tedge;
 };
+
+inline size_t sidx_bytes(const RtcsmPlan& pl) { return sizeof(int2) * (size_t)(pl.Nv + 2 * kPipe); }
+
+inline int coarse_block(const RtcsmPlan& pl) { return std::min(1024, ((pl.P + 63) / 64) * 64); }
 
 Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
 {
     Workspace w{};
-    const int tiles = (pl.P + kCoarseBlock - 1) / kCoarseBlock;
+    const int cb = coarse_block(pl);
+    const int tiles = (pl.P + cb - 1) / cb;
     w.nparts = tiles * pl.T;
+    w.Wq = (pl.W + pl.low_res - 1) / pl.low_res;
+    w.Hq = (pl.H + pl.low_res - 1) / pl.low_res;
+    w.decim = (double*)ctx->ensure(S_DECIM, sizeof(double) * std::max<size_t>(1, (size_t)pl.low_res * pl.low_res * w.Wq * w.Hq));
     const size_t K = (size_t)pl.K;
-    w.idx = (int2*)ctx->ensure(S_IDX, sizeof(int2) * (size_t)pl.T * std::max(pl.Nv, 1));
+    // index arrays padded by 2*kPipe entries: seq_sum's look-ahead loads
+    const size_t nidx = (size_t)pl.T * std::max(pl.Nv, 1) + 2 * kPipe;
+    w.idx = (int2*)ctx->ensure(S_IDX, sizeof(int2) * nidx);
+    w.cinfo = (int4*)ctx->ensure(S_CINFO, sizeof(int4) * nidx);
     w.cscore = (double*)ctx->ensure(S_CSCORE, sizeof(double) * K);
     w.cflag = (uint8_t*)ctx->ensure(S_CFLAG, K);
     w.sel = (uint8_t*)ctx->ensure(S_SEL, K);
@@ -567,9 +886,11 @@ Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
     w.fpos = (int*)ctx->ensure(S_FPOS, sizeof(int) * K);
     w.part_c = (double*)ctx->ensure(S_PART_C, sizeof(double) * (size_t)w.nparts);
     w.part_k = (long long*)ctx->ensure(S_PART_K, sizeof(long long) * (size_t)w.nparts);
-    char* cnt = (char*)ctx->ensure(S_COUNT, 64);
+    char* cnt = (char*)ctx->ensure(S_COUNT, 128);
     w.count = (int*)cnt;
     w.Lp = (double*)(cnt + 16);
+    w.zero = ctx->zero;  // zero cell for out-of-map gathers
+    w.tedge = (int*)ctx->ensure(S_TEDGE, sizeof(int) * (size_t)pl.T);
     w.poses7 = (double*)ctx->ensure(S_POSES7, sizeof(double) * 21);
     w.cidx = (int4*)ctx->ensure(S_COST_IDX, sizeof(int4) * 7 * (size_t)N);
     w.terms = (double*)ctx->ensure(S_COST_TERM, sizeof(double) * 7 * (size_t)N);
@@ -579,6 +900,67 @@ Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
     w.cub_temp = ctx->ensure(S_CUB_TEMP, bytes);
     w.cub_bytes = bytes;
     return w;
+}
+
+// Coarse stage: (phase-plane copy of the caller's coarse map, re-done per call
+// since the caller owns that map) + one lane per coarse block.
+void launch_coarse(lgs_ctx* ctx, const RtcsmPlan& pl, const Workspace& w, const double* coarse,
+                   int gen, hipStream_t st)
+{
+    const int cb = coarse_block(pl);
+    dim3 g((pl.P + cb - 1) / cb, pl.T);
+    if (ctx->coarse_planes) {
+        dim3 gd((w.Wq + 255) / 256, w.Hq, pl.low_res * pl.low_res);
+        hipLaunchKernelGGL(k_decimate, gd, dim3(256), 0, st, coarse, pl.W, pl.H, pl.low_res, w.Wq, w.Hq,
+                           w.decim);
+        LGS_HIP_CHECK(hipGetLastError());
+        const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
+        hipLaunchKernelGGL(k_coarse<1>, g, dim3(cb), 0, st, pl, w.decim, w.Wq, w.Hq, w.idx, w.cinfo,
+                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
+        ctx->timing_end(tok);
+    } else {
+        const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
+        hipLaunchKernelGGL(k_coarse<0>, g, dim3(cb), 0, st, pl, coarse, w.Wq, w.Hq, w.idx, w.cinfo,
+                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
+        ctx->timing_end(tok);
+    }
+    LGS_HIP_CHECK(hipGetLastError());
+}
+
+// Block evaluation dispatch: transposed multi-wave kernels for the window
+// size the launcher JSON uses (LowRes 5; its LDS need stays < 64 KB), the
+// generic one-wave kernels otherwise.
+template <int LR>
+void launch_seed_t(const RtcsmPlan& pl, const double* grid, const Workspace& w, int dense, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_seed<LR>, dim3(1), dim3(64 * LR), eval_t_smem<LR>(pl.Nv), st, pl, grid, w.idx,
+                       w.zero, w.part_c, w.part_k, w.nparts, w.Lp, dense);
+}
+void launch_seed(const RtcsmPlan& pl, const double* grid, const Workspace& w, int dense, hipStream_t st)
+{
+    switch (pl.Nv <= 64 * kMaxChunks ? pl.low_res : 0) {
+    case 5: launch_seed_t<5>(pl, grid, w, dense, st); break;
+    default:
+        hipLaunchKernelGGL(k_seed<0>, dim3(1), dim3(64), sidx_bytes(pl), st, pl, grid, w.idx, w.zero,
+                           w.part_c, w.part_k, w.nparts, w.Lp, dense);
+    }
+    LGS_HIP_CHECK(hipGetLastError());
+}
+template <int LR>
+void launch_fine_t(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_fine<LR>, dim3(1024), dim3(64 * LR), eval_t_smem<LR>(pl.Nv), st, pl, grid,
+                       w.idx, w.zero, w.list, w.count, w.fval, w.fpos);
+}
+void launch_fine(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
+{
+    switch (pl.Nv <= 64 * kMaxChunks ? pl.low_res : 0) {
+    case 5: launch_fine_t<5>(pl, grid, w, st); break;
+    default:
+        hipLaunchKernelGGL(k_fine<0>, dim3(1024), dim3(64), sidx_bytes(pl), st, pl, grid, w.idx, w.zero,
+                           w.list, w.count, w.fval, w.fpos);
+    }
+    LGS_HIP_CHECK(hipGetLastError());
 }
 
 struct ScanOptions {
@@ -595,18 +977,24 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
 {
     Workspace w = ensure_workspace(ctx, pl, scan->n);
     hipStream_t st = ctx->stream;
+    const int gen = ++ctx->generation;
     LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0, sizeof(RtcsmRecord), st));
     const int inject = ctx->inject_index ? 1 : 0;
     if (pl.Nv > 0) {
         if (opt.host_idx) {
             LGS_HIP_CHECK(hipMemcpyAsync(w.idx, opt.host_idx->data(), sizeof(int2) * opt.host_idx->size(),
                                          hipMemcpyHostToDevice, st));
+            const size_t n = (size_t)pl.T * pl.Nv;
+            hipLaunchKernelGGL(k_cinfo, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pl, w.idx,
+                               w.cinfo, w.Wq, w.Hq, w.tedge, gen);
+            LGS_HIP_CHECK(hipGetLastError());
         } else {
             dim3 g((pl.Nv + 255) / 256, pl.T);
             {
-                const int tok_ = ctx->timing_begin(K_PROJECT, 16.0 * (double)pl.T * pl.Nv);
+                const int tok_ = ctx->timing_begin(K_PROJECT, 24.0 * (double)pl.T * pl.Nv);
                 hipLaunchKernelGGL(k_project, g, dim3(256), 0, st, pl, scan->d_ranges, scan->d_angles,
-                                   d_vidx, w.idx, d_rec, ctx->guard_cap, ctx->guard_eps, inject);
+                                   d_vidx, w.idx, w.cinfo, w.Wq, w.Hq, w.tedge, gen, d_rec,
+                                   ctx->guard_cap, ctx->guard_eps, inject);
                 ctx->timing_end(tok_);
             }
             LGS_HIP_CHECK(hipGetLastError());
@@ -615,25 +1003,16 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                 LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.patches->data(), sizeof(int4) * opt.patches->size(),
                                              hipMemcpyHostToDevice, st));
                 const int np = (int)opt.patches->size();
-                hipLaunchKernelGGL(k_patch, dim3((np + 255) / 256), dim3(256), 0, st, pl, w.idx, dp, np);
+                hipLaunchKernelGGL(k_patch, dim3((np + 255) / 256), dim3(256), 0, st, pl, w.idx, w.cinfo,
+                                   w.Wq, w.Hq, w.tedge, gen, dp, np);
                 LGS_HIP_CHECK(hipGetLastError());
             }
         }
     }
-    {
-        dim3 g((pl.P + kCoarseBlock - 1) / kCoarseBlock, pl.T);
-        {
-            const int tok_ = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-            hipLaunchKernelGGL(k_coarse, g, dim3(kCoarseBlock), 0, st, pl, coarse->d, w.idx, w.cscore,
-                               w.cflag, w.part_c, w.part_k);
-            ctx->timing_end(tok_);
-        }
-        LGS_HIP_CHECK(hipGetLastError());
-    }
+    launch_coarse(ctx, pl, w, coarse->d, gen, st);
     {
         const int tok_ = ctx->timing_begin(K_SEED, 8.0 * pl.low_res * pl.low_res * (double)pl.Nv);
-        hipLaunchKernelGGL(k_seed, dim3(1), dim3(256), 0, st, pl, grid->d, w.idx, w.part_c, w.part_k,
-                           w.nparts, w.Lp, (opt.dense || ctx->force_dense) ? 1 : 0);
+        launch_seed(pl, grid->d, w, (opt.dense || ctx->force_dense) ? 1 : 0, st);
         ctx->timing_end(tok_);
     }
     LGS_HIP_CHECK(hipGetLastError());
@@ -649,8 +1028,7 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                                                 w.sel, w.list, w.count, (int)pl.K, st));
     {
         const int tok_ = ctx->timing_begin(K_FINE, 0.0);
-        hipLaunchKernelGGL(k_fine, dim3(2048), dim3(64), 0, st, pl, grid->d, w.idx, w.list, w.count,
-                           w.fval, w.fpos);
+        launch_fine(pl, grid->d, w, st);
         ctx->timing_end(tok_);
     }
     LGS_HIP_CHECK(hipGetLastError());
@@ -663,27 +1041,26 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
     LGS_HIP_CHECK(hipGetLastError());
     // cost + covariance terms at the 7 poses
     CostPlan cp = make_cost_plan(grid, cost, scan);
+    const double kk = (2.0 * cost->kernel_size + 1) * (2.0 * cost->kernel_size + 1);
     {
-        dim3 g((scan->n + 255) / 256, 7);
-        hipLaunchKernelGGL(k_cost_idx, g, dim3(256), 0, st, cp, scan->d_ranges, scan->d_angles,
-                           w.poses7, w.cidx, d_rec, ctx->guard_cap, ctx->guard_eps, inject);
+        const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * (double)scan->n);
+        hipLaunchKernelGGL(k_cost, dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
+                           scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
+                           ctx->guard_eps, inject, 0);
+        ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
-        if (opt.cost_patches && !opt.cost_patches->empty()) {
-            // (key, cells) pairs: cidx[key.x] = cells, computed on the host with glibc
-            const int np = (int)(opt.cost_patches->size() / 2);
-            int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * opt.cost_patches->size());
-            LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.cost_patches->data(),
-                                         sizeof(int4) * opt.cost_patches->size(),
-                                         hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, st, w.cidx, dp, np);
-            LGS_HIP_CHECK(hipGetLastError());
-        }
-        {
-            const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * (2 * cost->kernel_size + 1) * (2 * cost->kernel_size + 1) * (double)scan->n);
-            hipLaunchKernelGGL(k_cost_eval, dim3(7), dim3(256), 0, st, cp, grid->d, w.cidx, w.terms,
-                               d_rec->costs);
-            ctx->timing_end(tok_);
-        }
+    }
+    if (opt.cost_patches && !opt.cost_patches->empty()) {
+        // (key, cells) pairs: cidx[key.x] = cells, computed on the host with glibc
+        const int np = (int)(opt.cost_patches->size() / 2);
+        int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * opt.cost_patches->size());
+        LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.cost_patches->data(), sizeof(int4) * opt.cost_patches->size(),
+                                     hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, st, w.cidx, dp, np);
+        LGS_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_cost, dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
+                           scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
+                           ctx->guard_eps, 0, 1);
         LGS_HIP_CHECK(hipGetLastError());
     }
 }
@@ -845,6 +1222,7 @@ void check_args(const lgs_grid* grid, const lgs_grid* coarse, const lgs_rtcsm_pa
     LGS_REQUIRE(p->low_resolution >= 1 && p->low_resolution <= 32, "low_resolution must be in [1, 32]");
     LGS_REQUIRE(p->range_x >= 0 && p->range_y >= 0 && p->range_theta >= 0, "negative search range");
     LGS_REQUIRE(s->n >= 1, "empty scan");
+    LGS_REQUIRE(s->n <= 16384, "at most 16384 beams per scan (LDS-staged index rows)");
     LGS_REQUIRE(c->kernel_size >= 0, "negative kernel size");
 }
 
@@ -1013,19 +1391,17 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
         }
         if (!coarse_scores && !fine_scores) return;
         Workspace w = ensure_workspace(ctx, pl, s->n);
+        const int gen = ++ctx->generation;
         RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord));
         LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0, sizeof(RtcsmRecord), ctx->stream));
         if (nv > 0) {
             dim3 g((nv + 255) / 256, pl.T);
             hipLaunchKernelGGL(k_project, g, dim3(256), 0, ctx->stream, pl, s->d_ranges, s->d_angles,
-                               vidx, w.idx, d_rec, 0, -1.0, 0);
+                               vidx, w.idx, w.cinfo, w.Wq, w.Hq, w.tedge, gen, d_rec, 0, -1.0, 0);
             LGS_HIP_CHECK(hipGetLastError());
         }
         if (coarse_scores) {
-            dim3 g((pl.P + kCoarseBlock - 1) / kCoarseBlock, pl.T);
-            hipLaunchKernelGGL(k_coarse, g, dim3(kCoarseBlock), 0, ctx->stream, pl, coarse->d, w.idx,
-                               w.cscore, w.cflag, w.part_c, w.part_k);
-            LGS_HIP_CHECK(hipGetLastError());
+            launch_coarse(ctx, pl, w, coarse->d, gen, ctx->stream);
             LGS_HIP_CHECK(hipMemcpyAsync(coarse_scores, w.cscore, sizeof(double) * (size_t)pl.K,
                                          hipMemcpyDeviceToHost, ctx->stream));
         }
@@ -1059,38 +1435,28 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
         double hp[3] = { pose.x, pose.y, pose.theta };
         LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0, sizeof(RtcsmRecord), ctx->stream));
         LGS_HIP_CHECK(hipMemcpyAsync(poses, hp, sizeof(hp), hipMemcpyHostToDevice, ctx->stream));
-        hipLaunchKernelGGL(k_cost_idx, dim3((scan->n + 255) / 256, 1), dim3(256), 0, ctx->stream, cp,
-                           scan->d_ranges, scan->d_angles, poses, cidx, d_rec, ctx->guard_cap,
-                           ctx->guard_eps, 0);
-        LGS_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_cost_eval, dim3(1), dim3(256), 0, ctx->stream, cp, grid->d, cidx, terms,
-                           d_rec->costs);
+        hipLaunchKernelGGL(k_cost, dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
+                           scan->d_ranges, scan->d_angles, poses, cidx, terms, d_rec, ctx->guard_cap,
+                           ctx->guard_eps, 0, 0);
         LGS_HIP_CHECK(hipGetLastError());
         LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                      ctx->stream));
         LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
         if (h_rec->cost_guard_count > 0) {
-            // exact host recomputation of the guarded cells, then re-evaluate
-            std::vector<int4> fix;
+            // exact host recomputation of every cell row, then re-evaluate
+            std::vector<int4> row((size_t)cp.N, make_int4(INT_MIN, 0, 0, 0));
             for (int b = 0; b < cp.N; ++b) {
                 const double r = scan->h_ranges[b];
                 if (r >= cp.max_range || r <= cp.min_range) continue;
                 int cells[4];
                 host_cost_cells(cp, scan, hp, b, cells);
-                fix.push_back(make_int4(cells[0], cells[1], cells[2], cells[3]));
-            }
-            // rebuild the full index row on the host (N entries)
-            std::vector<int4> row((size_t)cp.N, make_int4(INT_MIN, 0, 0, 0));
-            size_t k = 0;
-            for (int b = 0; b < cp.N; ++b) {
-                const double r = scan->h_ranges[b];
-                if (r >= cp.max_range || r <= cp.min_range) continue;
-                row[b] = fix[k++];
+                row[b] = make_int4(cells[0], cells[1], cells[2], cells[3]);
             }
             LGS_HIP_CHECK(hipMemcpyAsync(cidx, row.data(), sizeof(int4) * row.size(),
                                          hipMemcpyHostToDevice, ctx->stream));
-            hipLaunchKernelGGL(k_cost_eval, dim3(1), dim3(256), 0, ctx->stream, cp, grid->d, cidx,
-                               terms, d_rec->costs);
+            hipLaunchKernelGGL(k_cost, dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
+                               scan->d_ranges, scan->d_angles, poses, cidx, terms, d_rec,
+                               ctx->guard_cap, ctx->guard_eps, 0, 1);
             LGS_HIP_CHECK(hipGetLastError());
             LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                          ctx->stream));

@@ -103,6 +103,8 @@ void lgs_ctx::release()
     }
     if (pinned) hipHostFree(pinned);
     pinned = nullptr;
+    if (zero) hipFree(zero);
+    zero = nullptr;
     for (auto& p : pending) {
         hipEventDestroy(p.a);
         hipEventDestroy(p.b);
@@ -131,7 +133,9 @@ extern "C" int lgs_ctx_create(int device, lgs_ctx** out)
     lgs_ctx* ctx = new lgs_ctx();
     ctx->device = device;
     if (hipSetDevice(device) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&ctx->zero, 32 * sizeof(double)) != hipSuccess ||
+        hipMemset(ctx->zero, 0, 32 * sizeof(double)) != hipSuccess) {
         delete ctx;
         return LGS_ERR_HIP;
     }
@@ -205,6 +209,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_FORCE_DENSE: ctx->force_dense = value != 0.0; return LGS_OK;
     case LGS_OPT_INJECT_INDEX: ctx->inject_index = value != 0.0; return LGS_OK;
     case LGS_OPT_PROFILE: ctx->profile = value != 0.0; return LGS_OK;
+    case LGS_OPT_COARSE_PLANES: ctx->coarse_planes = value != 0.0; return LGS_OK;
     case LGS_OPT_GUARD_CAP:
         ctx->guard_cap = (int)value;
         if (ctx->guard_cap < 0) ctx->guard_cap = 0;

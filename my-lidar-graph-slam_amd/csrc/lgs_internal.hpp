@@ -57,6 +57,9 @@ enum Slot {
     S_PATCH,        // int4 [patches]
     S_DENSE_FINE,   // double (dense diagnostics)
     S_COARSE_GRID,  // double (coarse map for OptimizePose(query))
+    S_DECIM,        // double (phase-plane coarse map)
+    S_CINFO,        // int4 [T*Nv] phase-plane addressing per (angle, beam)
+    S_TEDGE,        // int [T] generation-stamped 'angle touches the low map edge' flags
     S_RAY0, S_RAY1, S_RAY2, S_RAY3, S_RAY4, S_RAY5, S_RAY6, S_RAY7,
     S_LS0, S_LS1,
     S_NUM_SLOTS
@@ -130,12 +133,15 @@ struct lgs_ctx {
     bool force_dense = false;
     bool inject_index = false;
     int guard_cap = lgs::kGuardInline;
+    bool coarse_planes = true;   // phase-plane coarse layout (LGS_OPT_COARSE_PLANES)
+    int generation = 0;          // per-enqueue stamp (edge flags need no memset)
     // arena
     void* buf[lgs::S_NUM_SLOTS] = {};
     size_t buf_bytes[lgs::S_NUM_SLOTS] = {};
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
     lgs_grid* coarse_scratch = nullptr;
+    double* zero = nullptr;      // 32 zero doubles: target of out-of-map gathers
     // profiling (LGS_OPT_PROFILE)
     bool profile = false;
     std::vector<lgs::PendingTiming> pending;

@@ -21,6 +21,7 @@ LGS_OPT_FORCE_DENSE = 2
 LGS_OPT_INJECT_INDEX = 3
 LGS_OPT_GUARD_CAP = 4
 LGS_OPT_PROFILE = 5
+LGS_OPT_COARSE_PLANES = 6
 
 
 class Pose2D(C.Structure):

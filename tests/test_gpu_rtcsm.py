@@ -114,6 +114,24 @@ def test_optimize_pose_small_scenes(ctx, world, seed):
     assert gpu.fine_blocks <= ora.fine_blocks
 
 
+@pytest.mark.parametrize("low_res", [1, 3, 5, 10])
+def test_optimize_pose_low_resolutions(ctx, world, low_res):
+    """LowRes 5 (JSON) takes the multi-wave transposed block evaluator, other
+    values (10 = factory default) the generic one-wave evaluator."""
+    rng = np.random.default_rng(low_res)
+    cells, mx, my = build_map(world, 400, 0.05, 100, scene.arc_poses(5), n_beams=541)
+    ang = scene.beam_angles(541)
+    true = (0.3, -0.4, 0.9)
+    r = scene.ray_cast(world, true, ang)
+    init = (true[0] + rng.uniform(-0.2, 0.2), true[1] + rng.uniform(-0.2, 0.2), true[2] + 0.1)
+    params = (low_res, 0.8, 0.8, 0.4, 20.0)
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    sc = ctx.scan(r, ang)
+    gpu = ctx.optimize_pose_query(g, abi.RtcsmParams(*params), launcher_cost(), sc, init)
+    ora = oracle_match(cells, mx, my, 0.05, params, r, ang, init)
+    assert_same(gpu, ora, f"lowres{low_res}")
+
+
 def test_config1_launcher_json_window(ctx, world):
     """Config 1: 360 beams, 400x400 @ 10 cm, JSON ScanMatcherRealTimeCorrelative
     (launcher_settings_default.json:42-50: LowRes 5, 0.2/0.2/0.5, 20 m)."""
