@@ -197,6 +197,54 @@ int  lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* 
                             lgs_pose2d initial_pose, double* coarse_scores,
                             double* fine_scores, int* dims);
 
+/* ---- occupancy-grid maps: GridMap<BinaryBayesGridCell<double>> ----
+ * Geometry follows the reference exactly (H/grid_map/grid_map.hpp): square
+ * patches of patch_size cells, minPos anchoring, Resize/Expand with the
+ * negative patch-index quirk (:905-915).  Cells live on the device (dense,
+ * row-major over the whole patch grid, 0.0 = unknown); the per-beam
+ * Bresenham ray-cast and binary Bayes update run on the device in the
+ * reference's update order (beam order; misses along a ray before its hit),
+ * so every cell value is bit-exact. */
+typedef struct lgs_map lgs_map;
+
+/* GridMapBuilder ctor arguments used by the ray-cast (C/mapping/grid_map_builder.cpp:20-45) */
+typedef struct {
+    double usable_range_min, usable_range_max;
+    double prob_hit, prob_miss;
+} lgs_builder_params;
+
+typedef struct {
+    double resolution;
+    int patch_size;
+    int num_patches_x, num_patches_y;
+    int num_cells_x, num_cells_y;
+    double min_x, min_y;
+} lgs_map_geometry;
+
+/* GridMap(res, patchSize, numCellsX, numCellsY, centerPos) (H/grid_map/grid_map.hpp:337-391) */
+int  lgs_map_create(lgs_ctx* ctx, double resolution, int patch_size, int num_cells_x,
+                    int num_cells_y, double center_x, double center_y, lgs_map** out);
+void lgs_map_destroy(lgs_map* map);
+int  lgs_map_get_geometry(const lgs_map* map, lgs_map_geometry* out);
+/* Non-owning grid view of the map's cells (valid until the next geometry change
+ * or lgs_map_destroy); lgs_grid_destroy on a view is a no-op. */
+int  lgs_map_grid(lgs_map* map, lgs_grid** out);
+/* One scan into the map as GridMapBuilder::UpdateGridMap does after choosing
+ * the local map (C/mapping/grid_map_builder.cpp:149-186): bounding box,
+ * Expand(.., 5.0), then the ray-cast update. */
+int  lgs_map_update_scan(lgs_ctx* ctx, lgs_map* map, const lgs_scan* scan, lgs_pose2d robot_pose,
+                         const lgs_builder_params* params);
+/* GridMapBuilder::ConstructMapFromScans (C/mapping/grid_map_builder.cpp:227-332):
+ * Resize to the bounding box of all scans (topRight starts at DBL_MIN), Reset,
+ * then ray-cast every scan in order. */
+int  lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* map, const lgs_scan* const* scans,
+                                  const lgs_pose2d* robot_poses, int n,
+                                  const lgs_builder_params* params);
+/* Copy cells and per-cell hit/miss update counts (since create/construct) to
+ * the host; any pointer may be NULL.  Sizes: num_cells_x * num_cells_y. */
+int  lgs_map_download(lgs_ctx* ctx, const lgs_map* map, double* cells, uint32_t* hit_count,
+                      uint32_t* miss_count);
+
 /* CostGreedyEndpoint::Cost at one sensor pose */
 int  lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
                               const lgs_cost_ge_params* cost, const lgs_scan* scan,

@@ -1071,8 +1071,8 @@ void host_project(const RtcsmPlan& pl, const lgs_scan* scan, int vbeam, int tt, 
     const double r = scan->h_ranges[vbeam];
     const double a = scan->h_angles[vbeam];
     const double th = pl.st + pl.step_t * (double)(tt - pl.win_t);
-    const double c = std::cos(th + a);
-    const double s = std::sin(th + a);
+    double s, c;
+    ref_sincos(th + a, s, c);
     const double hx = pl.sx + r * c;
     const double hy = pl.sy + r * s;
     ix = (int)std::floor((hx - pl.min_x) / pl.res);
@@ -1083,8 +1083,8 @@ void host_cost_cells(const CostPlan& cp, const lgs_scan* scan, const double pose
                      int cells[4])
 {
     const double r = scan->h_ranges[beam];
-    const double c = std::cos(pose[2] + scan->h_angles[beam]);
-    const double s = std::sin(pose[2] + scan->h_angles[beam]);
+    double s, c;
+    ref_sincos(pose[2] + scan->h_angles[beam], s, c);
     const double hx = pose[0] + r * c;
     const double hy = pose[1] + r * s;
     const double mx = pose[0] + (r - cp.hit_and_missed_dist) * c;

@@ -281,7 +281,7 @@ extern "C" int lgs_grid_wrap(lgs_ctx* ctx, double* dev, int w, int h, double min
 
 extern "C" void lgs_grid_destroy(lgs_grid* g)
 {
-    if (!g) return;
+    if (!g || g->map_view) return;  // map views live and die with their lgs_map
     // hipFree synchronises with the device; the creating context may already
     // be gone, so it is not touched here.
     if (g->owned && g->d) {

@@ -167,7 +167,8 @@ struct lgs_grid {
     double* d = nullptr;
     int w = 0, h = 0;
     double min_x = 0, min_y = 0, res = 0;
-    bool owned = false;
+    bool owned = false;       // device cells freed by lgs_grid_destroy
+    bool map_view = false;    // handle embedded in an lgs_map: destroy is a no-op
 };
 
 struct lgs_scan {
@@ -187,26 +188,35 @@ struct lgs_scan {
     std::vector<int> h_vidx;
 };
 
+extern "C" void sincos(double x, double* s, double* c);  // glibc
+
 namespace lgs {
 
-// Host pose algebra restated from H/pose.hpp (glibc sin/cos, no contraction).
+// The reference is built with GCC, which fuses sin(x) and cos(x) of the same
+// argument into one glibc sincos() call; glibc's sincos differs from separate
+// sin/cos in ~0.1% of inputs.  Every host recomputation that must be
+// bit-exact therefore calls sincos() explicitly wherever the reference
+// evaluates both (HitPoint, Compound, MoveBackward, ...).
+inline void ref_sincos(double x, double& s, double& c) { ::sincos(x, &s, &c); }
+
+// Host pose algebra restated from H/pose.hpp (glibc sincos, no contraction).
 inline lgs_pose2d compound(lgs_pose2d s, lgs_pose2d d)
 {
-    const double sinT = std::sin(s.theta);
-    const double cosT = std::cos(s.theta);
+    double sinT, cosT;
+    ref_sincos(s.theta, sinT, cosT);
     return { cosT * d.x - sinT * d.y + s.x, sinT * d.x + cosT * d.y + s.y, s.theta + d.theta };
 }
 inline lgs_pose2d move_backward(lgs_pose2d e, lgs_pose2d d)
 {
     const double theta = e.theta - d.theta;
-    const double sinT = std::sin(theta);
-    const double cosT = std::cos(theta);
+    double sinT, cosT;
+    ref_sincos(theta, sinT, cosT);
     return { e.x - cosT * d.x + sinT * d.y, e.y - sinT * d.x - cosT * d.y, theta };
 }
 inline lgs_pose2d inverse_compound(lgs_pose2d s, lgs_pose2d e)
 {
-    const double sinT = std::sin(s.theta);
-    const double cosT = std::cos(s.theta);
+    double sinT, cosT;
+    ref_sincos(s.theta, sinT, cosT);
     const double dx = e.x - s.x, dy = e.y - s.y;
     return { cosT * dx + sinT * dy, -sinT * dx + cosT * dy, e.theta - s.theta };
 }

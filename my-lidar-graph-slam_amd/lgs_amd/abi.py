@@ -85,6 +85,24 @@ class RtcsmSummary(C.Structure):
     ]
 
 
+class BuilderParams(C.Structure):
+    _fields_ = [("usable_range_min", C.c_double), ("usable_range_max", C.c_double),
+                ("prob_hit", C.c_double), ("prob_miss", C.c_double)]
+
+
+class MapGeometry(C.Structure):
+    _fields_ = [("resolution", C.c_double), ("patch_size", C.c_int), ("num_patches_x", C.c_int),
+                ("num_patches_y", C.c_int), ("num_cells_x", C.c_int), ("num_cells_y", C.c_int),
+                ("min_x", C.c_double), ("min_y", C.c_double)]
+
+    def dict(self):
+        return dict(w=self.num_cells_x, h=self.num_cells_y, min_x=self.min_x, min_y=self.min_y,
+                    npx=self.num_patches_x, npy=self.num_patches_y)
+
+    def res(self):
+        return self.resolution
+
+
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double),
                 ("algo_bytes", C.c_double)]
@@ -125,6 +143,16 @@ _PROTOS = [
                                          C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     ("lgs_cost_greedy_endpoint", C.c_int, [_P, _P, C.POINTER(CostGEParams), _P, Pose2D,
                                            C.POINTER(C.c_double)]),
+    ("lgs_map_create", C.c_int, [_P, C.c_double, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
+                                 C.POINTER(_P)]),
+    ("lgs_map_destroy", None, [_P]),
+    ("lgs_map_get_geometry", C.c_int, [_P, C.POINTER(MapGeometry)]),
+    ("lgs_map_grid", C.c_int, [_P, C.POINTER(_P)]),
+    ("lgs_map_update_scan", C.c_int, [_P, _P, _P, Pose2D, C.POINTER(BuilderParams)]),
+    ("lgs_map_construct_from_scans", C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(Pose2D), C.c_int,
+                                               C.POINTER(BuilderParams)]),
+    ("lgs_map_download", C.c_int, [_P, _P, C.POINTER(C.c_double), C.POINTER(C.c_uint32),
+                                   C.POINTER(C.c_uint32)]),
 ]
 
 SYMBOLS = [p[0] for p in _PROTOS]
@@ -273,6 +301,13 @@ class Context:
                                                    Pose2D(*init), dptr(cs), dptr(fs), dims), "dense_scores")
         return list(dims), cs, fs
 
+    # ---- occupancy maps (K3) ----
+    def map(self, res: float, patch_size: int, ncx: int, ncy: int, center=(0.0, 0.0)) -> "Map":
+        h = _P()
+        self.check(self.lib.lgs_map_create(self.h, res, patch_size, ncx, ncy, center[0], center[1],
+                                           C.byref(h)), "map_create")
+        return Map(self, h)
+
     def cost_greedy_endpoint(self, grid, cost: CostGEParams, scan, pose) -> float:
         v = C.c_double()
         self.check(self.lib.lgs_cost_greedy_endpoint(self.h, grid.h, C.byref(cost), scan.h, Pose2D(*pose),
@@ -281,8 +316,9 @@ class Context:
 
 
 class Grid:
-    def __init__(self, ctx: Context, h, w, hh, min_x, min_y, res, owned=True):
+    def __init__(self, ctx: Context, h, w, hh, min_x, min_y, res, owned=True, map_view=None):
         self.ctx, self.h = ctx, h
+        self.map_view = map_view      # owning Map for lgs_map_grid views (handle not ours)
         self.w, self.hgt = w, hh
         self.min_x, self.min_y, self.res = min_x, min_y, res
         self.owned = owned
@@ -302,7 +338,62 @@ class Grid:
 
     def close(self):
         if self.h:
-            self.ctx.lib.lgs_grid_destroy(self.h)
+            if self.map_view is None:
+                self.ctx.lib.lgs_grid_destroy(self.h)  # frees the handle; cells only if owned
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Map:
+    """lgs_map: GridMap<BinaryBayesGridCell<double>> with device-resident cells."""
+
+    def __init__(self, ctx: Context, h):
+        self.ctx, self.h = ctx, h
+
+    def geometry(self) -> dict:
+        g = MapGeometry()
+        self.ctx.check(self.ctx.lib.lgs_map_get_geometry(self.h, C.byref(g)), "map_geometry")
+        return g.dict()
+
+    def grid(self) -> "Grid":
+        """Non-owning grid view (valid until the next geometry change)."""
+        gh = _P()
+        self.ctx.check(self.ctx.lib.lgs_map_grid(self.h, C.byref(gh)), "map_grid")
+        mg = MapGeometry()
+        self.ctx.check(self.ctx.lib.lgs_map_get_geometry(self.h, C.byref(mg)), "map_geometry")
+        return Grid(self.ctx, gh, mg.num_cells_x, mg.num_cells_y, mg.min_x, mg.min_y, mg.resolution,
+                    owned=False, map_view=self)
+
+    def update_scan(self, scan: "Scan", robot_pose, bp: BuilderParams):
+        self.ctx.check(self.ctx.lib.lgs_map_update_scan(self.ctx.h, self.h, scan.h, Pose2D(*robot_pose),
+                                                        C.byref(bp)), "map_update_scan")
+
+    def construct(self, scans, poses, bp: BuilderParams):
+        n = len(scans)
+        arr = (_P * n)(*[s.h for s in scans])
+        ps = (Pose2D * n)(*[Pose2D(*p) for p in poses])
+        self.ctx.check(self.ctx.lib.lgs_map_construct_from_scans(self.ctx.h, self.h, arr, ps, n, C.byref(bp)),
+                       "map_construct_from_scans")
+
+    def download(self):
+        g = self.geometry()
+        cells = np.zeros((g["h"], g["w"]))
+        hits = np.zeros((g["h"], g["w"]), dtype=np.uint32)
+        misses = np.zeros((g["h"], g["w"]), dtype=np.uint32)
+        self.ctx.check(self.ctx.lib.lgs_map_download(self.ctx.h, self.h, dptr(cells),
+                                                     hits.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                     misses.ctypes.data_as(C.POINTER(C.c_uint32))),
+                       "map_download")
+        return cells, hits, misses
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.lgs_map_destroy(self.h)
             self.h = None
 
     def __del__(self):

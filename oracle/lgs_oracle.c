@@ -9,7 +9,12 @@
  * source), so that with -ffp-contract=off and glibc libm the results are the
  * ones the reference computes.  Citations: H/ = include/my_lidar_graph_slam/,
  * C/ = src/my_lidar_graph_slam/ under /root/reference.
+ *
+ * sin/cos: the reference is built with GCC -O3, which fuses a sin(x)/cos(x)
+ * pair into one glibc sincos() call; sincos differs from separate sin/cos in
+ * ~0.1% of inputs (last ulp), so every paired site here calls sincos().
  */
+#define _GNU_SOURCE 1
 #include "lgs_oracle.h"
 
 #include <float.h>
@@ -53,8 +58,8 @@ static inline void world_to_cell(double min_x, double min_y, double res,
 orc_pose orc_compound(orc_pose s, orc_pose d)
 {
     /* H/pose.hpp:150-161 */
-    double sinT = sin(s.theta);
-    double cosT = cos(s.theta);
+    double sinT, cosT;
+    sincos(s.theta, &sinT, &cosT);
     orc_pose r;
     r.x = cosT * d.x - sinT * d.y + s.x;
     r.y = sinT * d.x + cosT * d.y + s.y;
@@ -65,8 +70,8 @@ orc_pose orc_compound(orc_pose s, orc_pose d)
 orc_pose orc_inverse_compound(orc_pose s, orc_pose e)
 {
     /* H/pose.hpp:165-180 */
-    double sinT = sin(s.theta);
-    double cosT = cos(s.theta);
+    double sinT, cosT;
+    sincos(s.theta, &sinT, &cosT);
     double dx = e.x - s.x;
     double dy = e.y - s.y;
     double dt = e.theta - s.theta;
@@ -81,8 +86,8 @@ orc_pose orc_move_backward(orc_pose e, orc_pose d)
 {
     /* H/pose.hpp:195-206 */
     double theta = e.theta - d.theta;
-    double sinT = sin(theta);
-    double cosT = cos(theta);
+    double sinT, cosT;
+    sincos(theta, &sinT, &cosT);
     orc_pose r;
     r.x = e.x - cosT * d.x + sinT * d.y;
     r.y = e.y - sinT * d.x - cosT * d.y;
@@ -232,8 +237,8 @@ int orc_rtcsm_scan_indices(const orc_grid* g, orc_pose sp, const orc_scan* scan,
         const double range = scan->ranges[i];
         if (range >= scan_range_max)
             continue;
-        const double cosT = cos(sp.theta + scan->angles[i]);
-        const double sinT = sin(sp.theta + scan->angles[i]);
+        double sinT, cosT;
+        sincos(sp.theta + scan->angles[i], &sinT, &cosT);
         const double hx = sp.x + range * cosT;
         const double hy = sp.y + range * sinT;
         world_to_cell(g->min_x, g->min_y, g->res, hx, hy, &ixy[2 * n], &ixy[2 * n + 1]);
@@ -421,8 +426,8 @@ double orc_cost_ge_cost(const orc_grid* g, const orc_cost_ge* c, const orc_scan*
         if (scanRange >= maxRange || scanRange <= minRange)
             continue;
         /* HitAndMissedPoint (H/sensor/sensor_data.hpp:177-198) */
-        const double cosT = cos(sp.theta + scan->angles[i]);
-        const double sinT = sin(sp.theta + scan->angles[i]);
+        double sinT, cosT;
+        sincos(sp.theta + scan->angles[i], &sinT, &cosT);
         const double hx = sp.x + scanRange * cosT;
         const double hy = sp.y + scanRange * sinT;
         const double mx = sp.x + (scanRange - c->hit_and_missed_dist) * cosT;
@@ -635,8 +640,8 @@ int orc_integrate_scan(orc_map* m, orc_pose robotPose, const orc_scan* scan,
         const double r = scan->ranges[i];
         if (r >= maxRange || r <= minRange)
             continue;
-        const double cosT = cos(sp.theta + scan->angles[i]);
-        const double sinT = sin(sp.theta + scan->angles[i]);
+        double sinT, cosT;
+        sincos(sp.theta + scan->angles[i], &sinT, &cosT);
         const double hx = sp.x + r * cosT;
         const double hy = sp.y + r * sinT;
         hp[2 * nh] = hx;
@@ -684,8 +689,8 @@ int orc_construct_map_from_scans(orc_map* m, const orc_node* nodes, int n_nodes,
             const double r = scan->ranges[i];
             if (r >= maxRange || r <= minRange)
                 continue;
-            const double cosT = cos(sp.theta + scan->angles[i]);
-            const double sinT = sin(sp.theta + scan->angles[i]);
+            double sinT, cosT;
+            sincos(sp.theta + scan->angles[i], &sinT, &cosT);
             const double hx = sp.x + r * cosT;
             const double hy = sp.y + r * sinT;
             hps[k][2 * nhs[k]] = hx;
@@ -789,8 +794,8 @@ double orc_sq_cost(const orc_grid* g, double umin, double umax, const orc_scan* 
         const double r = scan->ranges[i];
         if (r >= maxRange || r <= minRange)
             continue;
-        const double cosT = cos(sp.theta + scan->angles[i]);
-        const double sinT = sin(sp.theta + scan->angles[i]);
+        double sinT, cosT;
+        sincos(sp.theta + scan->angles[i], &sinT, &cosT);
         const double hx = sp.x + r * cosT;
         const double hy = sp.y + r * sinT;
         const double fx = (hx - g->min_x) / g->res;
@@ -805,8 +810,8 @@ double orc_sq_cost(const orc_grid* g, double umin, double umax, const orc_scan* 
  * ComputeMapGradient(gridMap, mapPos) (:172-199) */
 static void sq_map_gradient(const orc_grid* g, orc_pose sp, double r, double a, double out[3])
 {
-    const double cosT = cos(sp.theta + a);
-    const double sinT = sin(sp.theta + a);
+    double sinT, cosT;
+    sincos(sp.theta + a, &sinT, &cosT);
     const double hx = sp.x + r * cosT;
     const double hy = sp.y + r * sinT;
     const double deltaIdx = 0.1;
@@ -981,8 +986,8 @@ static orc_pose linsolve_step(const orc_grid* g, const orc_linsolve_params* p,
         const double a = scan->angles[i];
         if (r >= maxRange || r <= minRange)
             continue;
-        const double cosT = cos(sp.theta + a);
-        const double sinT = sin(sp.theta + a);
+        double sinT, cosT;
+        sincos(sp.theta + a, &sinT, &cosT);
         const double hx = sp.x + r * cosT;
         const double hy = sp.y + r * sinT;
         const double fx = (hx - g->min_x) / g->res;
@@ -1044,8 +1049,8 @@ int orc_linsolve_optimize_pose(const orc_grid* g, const orc_linsolve_params* p,
             const double a = scan->angles[i];
             if (r >= maxRange || r <= minRange)
                 continue;
-            const double cosT = cos(best.theta + a);
-            const double sinT = sin(best.theta + a);
+            double sinT, cosT;
+            sincos(best.theta + a, &sinT, &cosT);
             const double hx = best.x + r * cosT;
             const double hy = best.y + r * sinT;
             const double fx = (hx - g->min_x) / g->res;

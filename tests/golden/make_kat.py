@@ -9,7 +9,10 @@ two sources independent of oracle/lgs_oracle.c:
     is recorded next to each case);
   * "py" cases: a second, pure-Python restatement of the same reference
     functions below (Python floats are IEEE binary64 without FMA contraction and
-    math.sin/cos/exp/acos call glibc, like the reference's build).
+    math.exp/acos and the ctypes-bound glibc sincos() below are glibc's, like
+    the reference's build: GCC -O3 fuses each sin(x)/cos(x) pair of the
+    reference into one sincos() call, which differs from separate sin/cos in
+    ~0.1% of inputs, so paired sites here call sincos()).
 
 Agreement of the C oracle with both pins the oracle against restatement bugs;
 it does not pin it to the reference binary ("parity unpinned").
@@ -18,12 +21,25 @@ Run:  python tests/golden/make_kat.py   (rewrites kat.json deterministically)
 """
 from __future__ import annotations
 
+import ctypes
+import ctypes.util
 import json
 import math
 import os
 import random
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+
+_libm = ctypes.CDLL(ctypes.util.find_library("m"))
+_libm.sincos.restype = None
+_libm.sincos.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+
+
+def sincos(x):
+    """glibc sincos(x) -> (sin, cos)."""
+    sn, cs = ctypes.c_double(), ctypes.c_double()
+    _libm.sincos(x, ctypes.byref(sn), ctypes.byref(cs))
+    return sn.value, cs.value
 
 
 # ---------------- pure-Python restatement (small cases only) ----------------
@@ -120,13 +136,13 @@ def bayes(v, p):
 
 
 def compound(s, d):
-    st, ct = math.sin(s[2]), math.cos(s[2])
+    st, ct = sincos(s[2])
     return (ct * d[0] - st * d[1] + s[0], st * d[0] + ct * d[1] + s[1], s[2] + d[2])
 
 
 def move_backward(e, d):
     th = e[2] - d[2]
-    st, ct = math.sin(th), math.cos(th)
+    st, ct = sincos(th)
     return (e[0] - ct * d[0] + st * d[1], e[1] - st * d[0] - ct * d[1], th)
 
 
@@ -157,8 +173,9 @@ def rtcsm_search(grid, coarse, min_x, min_y, res, ranges, angles, sensor, low_re
         for r, a in zip(ranges, angles):
             if r >= rmax:
                 continue
-            hx = sensor[0] + r * math.cos(th + a)
-            hy = sensor[1] + r * math.sin(th + a)
+            sn, cs = sincos(th + a)
+            hx = sensor[0] + r * cs
+            hy = sensor[1] + r * sn
             idx.append((int(math.floor((hx - min_x) / res)), int(math.floor((hy - min_y) / res))))
         for x in range(-wx, wx + 1, low_res):
             for y in range(-wy, wy + 1, low_res):
