@@ -168,7 +168,9 @@ def main():
         traffic = None
         if os.path.exists(args.pmc):
             try:
-                traffic = json.load(open(args.pmc)).get("k_coarse", {}).get("hbm_bytes_per_launch")
+                pmc = json.load(open(args.pmc))
+                key = next((k for k in pmc if k.startswith("k_coarse")), None)
+                traffic = pmc[key].get("hbm_bytes_per_launch") if key else None
             except Exception:
                 traffic = None
         roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
