@@ -250,6 +250,50 @@ int  lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
                               const lgs_cost_ge_params* cost, const lgs_scan* scan,
                               lgs_pose2d sensor_pose, double* out_cost);
 
+/* ---- K4: Gauss-Newton refine (ScanMatcherLinearSolver + CostSquareError) ----
+ * Replaces ScanMatcherLinearSolver::OptimizePose (C/mapping/scan_matcher_linear_solver.cpp:38-85,
+ * H/mapping/scan_matcher_linear_solver.hpp:15-56) with its CostSquareError
+ * (C/mapping/cost_function_square_error.cpp).  Field order follows the
+ * constructor (numOfIterationsMax, convergenceThreshold, usableRangeMin/Max,
+ * translation/rotation regularizer) then CostSquareError(usableRangeMin/Max). */
+typedef struct {
+    int    num_iterations_max;
+    double convergence_threshold;
+    double usable_range_min, usable_range_max;
+    double translation_regularizer, rotation_regularizer;
+    double cost_usable_range_min, cost_usable_range_max;
+} lgs_linsolve_params;
+
+/* ScanMatchingSummary (H/mapping/scan_matcher.hpp:26-77) plus diagnostics */
+typedef struct {
+    int pose_found;               /* always 1, as the reference */
+    int iterations;               /* OptimizeStep calls made */
+    double normalized_cost;       /* cost / NumOfScans() */
+    lgs_pose2d initial_pose;
+    lgs_pose2d estimated_pose;    /* MoveBackward(bestSensorPose, relPose) */
+    double covariance[9];         /* CostSquareError::ComputeCovariance, row-major */
+    lgs_pose2d sensor_pose;       /* Compound(initialPose, relPose) */
+    lgs_pose2d best_sensor_pose;
+    double cost;                  /* un-normalized final cost */
+} lgs_linsolve_summary;
+
+/* One refine; trajectory (may be NULL; room for 4 * max(1, num_iterations_max)
+ * doubles) receives, after every OptimizeStep, the sensor pose (x, y, theta)
+ * and the cost the convergence test sees at it. */
+int  lgs_linsolve_optimize_pose(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params* params,
+                                const lgs_scan* scan, lgs_pose2d initial_pose,
+                                lgs_linsolve_summary* out, double* trajectory);
+/* n independent refines against one grid (one workgroup each), one sync */
+int  lgs_linsolve_optimize_pose_batch(lgs_ctx* ctx, const lgs_grid* grid,
+                                      const lgs_linsolve_params* params,
+                                      const lgs_scan* const* scans, const lgs_pose2d* initial_poses,
+                                      int n, lgs_linsolve_summary* out);
+/* CostSquareError::Cost (C/mapping/cost_function_square_error.cpp:21-58) and,
+ * if out_covariance is not NULL, ComputeCovariance (:112-135) at one sensor pose */
+int  lgs_cost_square_error(lgs_ctx* ctx, const lgs_grid* grid, double usable_range_min,
+                           double usable_range_max, const lgs_scan* scan, lgs_pose2d sensor_pose,
+                           double* out_cost, double* out_covariance);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,637 @@
+// k_linsolve.hip -- K4: Gauss-Newton scan matcher (ScanMatcherLinearSolver) on MI355X.
+//
+// Restates ScanMatcherLinearSolver::OptimizePose / OptimizeStep
+// (C/mapping/scan_matcher_linear_solver.cpp:38-148) with CostSquareError
+// (C/mapping/cost_function_square_error.cpp: Cost :21-58, ComputeCovariance
+// :112-135, ComputeMapGradient :172-229, ComputeSmoothedValue :276-346).
+//
+// One workgroup runs one whole refine (all iterations) without returning to
+// the host: per iteration every thread takes beams i = tid, tid + 512, ...,
+// evaluates the bicubic smoothed value and its central-difference map
+// gradient (5 x 16 gathers per beam, all independent), and accumulates
+// b = sum res*g and H = sum g*g^T in registers; wave64 shuffle butterflies
+// plus one LDS pass reduce the 9 sums; lane 0 solves the regularised 3x3
+// system with the column-pivoting Householder QR Eigen's colPivHouseholderQr
+// uses (restated, Eigen is not vendored), updates the pose, and the cost at
+// the new pose is reduced the same way for the convergence test.  A batch
+// launches one workgroup per scan.
+//
+// Numerics: the reference's own result moves by up to ~1e-5
+// under a 1-ulp change of its input pose (ComputeSmoothedValue truncates
+// coordinates that sit on integers +- rounding), so parity with the oracle is
+// judged within the north-star tolerance, not bitwise.  Device sin/cos/pow
+// follow ocml; pow(x, 2.0) is the exact x*x GCC folds it to, pow(x, 3.0) is
+// the correctly rounded cube (glibc's pow agrees with it in 99.9% of inputs).
+#include "lgs_internal.hpp"
+
+#include <cfloat>
+#include <climits>
+#include <cstring>
+
+using namespace lgs;
+
+namespace {
+
+constexpr int kLsThreads = 512;
+
+struct LsPlan {
+    double min_x, min_y, res;
+    int W, H, N;
+    int max_iter;
+    double conv;
+    double step_min, step_max;    // OptimizeStep's beam filter (open interval)
+    double cost_min, cost_max;    // CostSquareError's beam filter
+    double reg_t, reg_r;
+};
+
+struct LsRecord {
+    double pose[3];     // best sensor pose
+    double cost;
+    double grad[3];     // CostSquareError::ComputeGradient at the best pose
+    int iterations;
+    int pad;
+};
+
+// x86-64 cvttsd2si semantics of static_cast<int>(double) (the reference's
+// host): out-of-range and NaN give INT_MIN; the GPU conversion would saturate.
+__device__ __forceinline__ int host_trunc(double x)
+{
+    return (x > -2147483649.0 && x < 2147483648.0) ? (int)x : INT_MIN;
+}
+
+// pow(a, 3.0), correctly rounded: a^3 = c + ce + pe*a exactly up to 2^-106 relative
+__device__ __forceinline__ double cube(double a)
+{
+    const double p = a * a;
+    const double pe = fma(a, a, -p);
+    const double c = p * a;
+    const double ce = fma(p, a, -c);
+    return c + (ce + pe * a);
+}
+
+// bicubic kernel h(t) (:281-295); pow(at, 2.0) is at*at after GCC folding
+__device__ __forceinline__ double bicubic_h(double t)
+{
+    const double at = fabs(t);
+    if (at <= 1.0) {
+        const double at3 = cube(at);
+        const double at2 = at * at;
+        return (at3 - 2.0 * at2 + 1.0);
+    } else if (at <= 2.0) {
+        const double at3 = cube(at);
+        const double at2 = at * at;
+        return (-at3 + 5.0 * at2 - 8.0 * at + 4.0);
+    }
+    return 0.0;
+}
+
+// One axis of ComputeSmoothedValue (:276-346) for coordinate v: the four
+// sample indices clamp(static_cast<int>(v_i), 0, n-1) of f (:298-310,
+// truncation) and the four kernel weights h(v_1..v_4).  The x axis of
+// (fx, fy +- d) and the y axis of (fx +- d, fy) are the axes of (fx, fy): the
+// reference's "+ 0.0" / "- 0.0" leave every derived quantity unchanged
+// (v + 0.0 differs from v only for v = -0.0, which yields the same floor
+// differences, indices and weights), so five smoothed values share six axes.
+struct Axis {
+    int idx[4];
+    double w[4];
+};
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (hi < v ? hi : v); }
+
+__device__ __forceinline__ Axis make_axis(double v, int n)
+{
+    const double fl = floor(v);
+    const double v1 = 1.0 + v - fl;
+    const double v2 = v - fl;
+    const double v3 = fl + 1.0 - v;
+    const double v4 = fl + 2.0 - v;
+    Axis a;
+    a.idx[0] = clampi(host_trunc(v - v1), 0, n - 1);
+    a.idx[1] = clampi(host_trunc(v - v2), 0, n - 1);
+    a.idx[2] = clampi(host_trunc(v + v3), 0, n - 1);
+    a.idx[3] = clampi(host_trunc(v + v4), 0, n - 1);
+    a.w[0] = bicubic_h(v1);
+    a.w[1] = bicubic_h(v2);
+    a.w[2] = bicubic_h(v3);
+    a.w[3] = bicubic_h(v4);
+    return a;
+}
+
+// vecX^T * M * vecY with M(i, j) = f(xs_i, ys_j), evaluated as
+// r_j = sum_i vx_i M_ij, then sum_j r_j vy_j (the oracle's order; Eigen's
+// own order is not pinned), clamped to [0, 1] (:345)
+__device__ __forceinline__ double smoothed(const double* __restrict__ g, int W, const Axis& ax,
+                                           const Axis& ay)
+{
+    double m[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const double* row = g + (size_t)ay.idx[j] * W;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m[j][i] = row[ax.idx[i]];
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double acc = ax.w[0] * m[j][0];
+#pragma unroll
+        for (int i = 1; i < 4; ++i) acc = acc + ax.w[i] * m[j][i];
+        s = (j == 0) ? acc * ay.w[0] : s + acc * ay.w[j];
+    }
+    return s < 0.0 ? 0.0 : (1.0 < s ? 1.0 : s);
+}
+
+// Per beam at one sensor pose: residual e = 1 - S(hit point) and the map
+// gradient w.r.t. the pose (ComputeMapGradient :172-229: central differences
+// of +-0.05 cells, / (0.1 res), dtheta = -r sin gx + r cos gy).
+__device__ __forceinline__ void beam_terms(const LsPlan& p, const double* __restrict__ g,
+                                           const double pose[3], double r, double a, double& e,
+                                           double gv[3])
+{
+    double sn, cs;
+    sincos(pose[2] + a, &sn, &cs);
+    const double hx = pose[0] + r * cs;
+    const double hy = pose[1] + r * sn;
+    const double fx = (hx - p.min_x) / p.res;
+    const double fy = (hy - p.min_y) / p.res;
+    const double deltaIdx = 0.1;
+    const double deltaDist = p.res * deltaIdx;
+    const double d = deltaIdx / 2.0;
+    const Axis x0 = make_axis(fx, p.W), xp = make_axis(fx + d, p.W), xm = make_axis(fx - d, p.W);
+    const Axis y0 = make_axis(fy, p.H), yp = make_axis(fy + d, p.H), ym = make_axis(fy - d, p.H);
+    const double s0 = smoothed(g, p.W, x0, y0);
+    const double sxp = smoothed(g, p.W, xp, y0);
+    const double sxm = smoothed(g, p.W, xm, y0);
+    const double syp = smoothed(g, p.W, x0, yp);
+    const double sym = smoothed(g, p.W, x0, ym);
+    const double gx = (sxp - sxm) / deltaDist;
+    const double gy = (syp - sym) / deltaDist;
+    e = 1.0 - s0;
+    gv[0] = gx;
+    gv[1] = gy;
+    gv[2] = -r * sn * gx + r * cs * gy;
+}
+
+// sum over the workgroup of NV values per thread (wave64 butterfly + LDS);
+// every thread gets the totals
+template <int NV>
+__device__ void wg_sum(double (&v)[NV], double* red)
+{
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int nw = kLsThreads / 64;
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[k * nw + wid] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        double s = red[k * nw];
+        for (int w = 1; w < nw; ++w) s += red[k * nw + w];
+        v[k] = s;
+    }
+}
+
+// Eigen ColPivHouseholderQR<Matrix3d>::compute + solve (published algorithm,
+// Eigen >= 3.3), one thread.  Every loop is unrolled and every data-dependent
+// index (pivot column, permutation) is resolved with compile-time-indexed
+// selects, so the 3x3 problem lives in registers (no scratch).
+template <class T>
+__device__ __forceinline__ void cswap(bool c, T& a, T& b)
+{
+    const T ta = a, tb = b;
+    a = c ? tb : ta;
+    b = c ? ta : tb;
+}
+
+__device__ void solve3_colpiv_qr(const double Hin[9], const double bin[3], double xout[3])
+{
+    constexpr int N = 3;
+    double A[N][N];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < N; ++j) A[i][j] = Hin[3 * i + j];
+    double hc[N], normU[N], normD[N];
+    int transp[N];
+    const double eps = DBL_EPSILON;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) s += A[i][k] * A[i][k];
+        normD[k] = sqrt(s);
+        normU[k] = normD[k];
+    }
+    double maxn = normU[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k)
+        if (normU[k] > maxn) maxn = normU[k];
+    const double thrHelper = (maxn * eps) * (maxn * eps) / (double)N;
+    const double downdateThr = sqrt(eps);
+    int nonzero = N;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        int big = k;
+        double bigv = normU[k];
+#pragma unroll
+        for (int j = k + 1; j < N; ++j)
+            if (normU[j] > bigv) {
+                bigv = normU[j];
+                big = j;
+            }
+        if (nonzero == N && bigv * bigv < thrHelper * (double)(N - k)) nonzero = k;
+        transp[k] = big;
+#pragma unroll
+        for (int j = k + 1; j < N; ++j) {
+            const bool sw = (j == big);
+#pragma unroll
+            for (int i = 0; i < N; ++i) cswap(sw, A[i][k], A[i][j]);
+            cswap(sw, normU[k], normU[j]);
+            cswap(sw, normD[k], normD[j]);
+        }
+        double tailSq = 0.0;
+#pragma unroll
+        for (int i = k + 1; i < N; ++i) tailSq += A[i][k] * A[i][k];
+        const double c0 = A[k][k];
+        double tau, beta;
+        if (tailSq <= DBL_MIN) {
+            tau = 0.0;
+            beta = c0;
+#pragma unroll
+            for (int i = k + 1; i < N; ++i) A[i][k] = 0.0;
+        } else {
+            beta = sqrt(c0 * c0 + tailSq);
+            if (c0 >= 0.0) beta = -beta;
+#pragma unroll
+            for (int i = k + 1; i < N; ++i) A[i][k] = A[i][k] / (c0 - beta);
+            tau = (beta - c0) / beta;
+        }
+        hc[k] = tau;
+        A[k][k] = beta;
+        if (tau != 0.0) {
+#pragma unroll
+            for (int j = k + 1; j < N; ++j) {
+                double tmp = 0.0;
+#pragma unroll
+                for (int i = k + 1; i < N; ++i) tmp += A[i][k] * A[i][j];
+                tmp += A[k][j];
+                A[k][j] -= tau * tmp;
+#pragma unroll
+                for (int i = k + 1; i < N; ++i) A[i][j] -= (tau * A[i][k]) * tmp;
+            }
+        }
+#pragma unroll
+        for (int j = k + 1; j < N; ++j) {
+            if (normU[j] != 0.0) {
+                double temp = fabs(A[k][j]) / normU[j];
+                temp = (1.0 + temp) * (1.0 - temp);
+                temp = temp < 0.0 ? 0.0 : temp;
+                const double q = normU[j] / normD[j];
+                if (temp * (q * q) <= downdateThr) {
+                    double s = 0.0;
+#pragma unroll
+                    for (int i = k + 1; i < N; ++i) s += A[i][j] * A[i][j];
+                    normD[j] = sqrt(s);
+                    normU[j] = normD[j];
+                } else {
+                    normU[j] *= sqrt(temp);
+                }
+            }
+        }
+    }
+    // permutation: perm = transpositions applied in order
+    int perm[N] = { 0, 1, 2 };
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+#pragma unroll
+        for (int j = k + 1; j < N; ++j) cswap(transp[k] == j, perm[k], perm[j]);
+    if (nonzero == 0) {
+        xout[0] = xout[1] = xout[2] = 0.0;
+        return;
+    }
+    double c[N] = { bin[0], bin[1], bin[2] };
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (k >= nonzero) break;
+        if (k == N - 1) {
+            c[k] *= 1.0 - hc[k];
+            continue;
+        }
+        if (hc[k] == 0.0) continue;
+        double tmp = 0.0;
+#pragma unroll
+        for (int i = k + 1; i < N; ++i) tmp += A[i][k] * c[i];
+        tmp += c[k];
+        c[k] -= hc[k] * tmp;
+#pragma unroll
+        for (int i = k + 1; i < N; ++i) c[i] -= (hc[k] * A[i][k]) * tmp;
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        if (i < nonzero && c[i] != 0.0) {
+            c[i] /= A[i][i];
+#pragma unroll
+            for (int j = 0; j < i; ++j) c[j] -= c[i] * A[j][i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (i >= nonzero) c[i] = 0.0;
+#pragma unroll
+    for (int m = 0; m < N; ++m) {
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) v = (perm[i] == m) ? c[i] : v;
+        xout[m] = v;
+    }
+}
+
+struct LsScanRef {
+    const double* ranges;
+    const double* angles;
+    double min_range, max_range;   // ScanData min/max range (filters take the max/min with usable)
+    double pose0[3];               // Compound(initialPose, relPose), glibc on the host
+    int n;
+    int pad;
+};
+
+// One pass over the beams at one sensor pose accumulates everything any
+// phase of the loop needs at that pose:
+//   [0..8]   OptimizeStep's b = sum e*g, H = sum g*g^T (upper triangle)
+//            over beams in (step_min, step_max) (:100-132);
+//   [9]      CostSquareError::Cost = sum e^2 over beams in (cost_min, cost_max);
+//   [10..12] ComputeGradient's sum 2*e*(-g) over the same beams (:61-109).
+// The reference's loop (step; cost at the new pose; convergence test) then
+// needs one pass per iteration plus the first (:48-69).
+constexpr int kAcc = 13;
+
+__device__ __forceinline__ void pass(const LsPlan& p, const double* __restrict__ grid, const LsScanRef& sc,
+                                     const double pose[3], double smin, double smax, double cmin,
+                                     double cmax, double (&acc)[kAcc])
+{
+#pragma unroll
+    for (int k = 0; k < kAcc; ++k) acc[k] = 0.0;
+    for (int i = threadIdx.x; i < sc.n; i += kLsThreads) {
+        const double r = sc.ranges[i];
+        const bool in_step = !(r >= smax || r <= smin);
+        const bool in_cost = !(r >= cmax || r <= cmin);
+        if (!in_step && !in_cost) continue;
+        double e, gv[3];
+        beam_terms(p, grid, pose, r, sc.angles[i], e, gv);
+        if (in_step) {
+            acc[0] += e * gv[0];
+            acc[1] += e * gv[1];
+            acc[2] += e * gv[2];
+            acc[3] += gv[0] * gv[0];
+            acc[4] += gv[0] * gv[1];
+            acc[5] += gv[0] * gv[2];
+            acc[6] += gv[1] * gv[1];
+            acc[7] += gv[1] * gv[2];
+            acc[8] += gv[2] * gv[2];
+        }
+        if (in_cost) {
+            acc[9] += e * e;   // pow(1.0 - S, 2.0): GCC folds it to the exact product
+            acc[10] += 2.0 * e * (-gv[0]);
+            acc[11] += 2.0 * e * (-gv[1]);
+            acc[12] += 2.0 * e * (-gv[2]);
+        }
+    }
+}
+
+// One workgroup per scan: the whole OptimizePose loop (:48-69) + covariance.
+__global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double* __restrict__ grid,
+                                                         const LsScanRef* __restrict__ scans,
+                                                         LsRecord* __restrict__ out,
+                                                         double* __restrict__ traj)
+{
+    __shared__ double red[kAcc * (kLsThreads / 64)];
+    __shared__ double spose[3];
+    const LsScanRef sc = scans[blockIdx.x];
+    const double smin = fmax(p.step_min, sc.min_range), smax = fmin(p.step_max, sc.max_range);
+    const double cmin = fmax(p.cost_min, sc.min_range), cmax = fmin(p.cost_max, sc.max_range);
+    double pose[3] = { sc.pose0[0], sc.pose0[1], sc.pose0[2] };
+    double prevCost = DBL_MAX, cost = DBL_MAX;
+    double acc[kAcc];
+    pass(p, grid, sc, pose, smin, smax, cmin, cmax, acc);
+    wg_sum(acc, red);
+    int it = 0;
+    for (;;) {
+        // OptimizeStep (:88-148): regularised normal equations, col-piv QR, pose += delta
+        if (threadIdx.x == 0) {
+            const double H[9] = { acc[3] + p.reg_t, acc[4], acc[5],
+                                  acc[4], acc[6] + p.reg_t, acc[7],
+                                  acc[5], acc[7], acc[8] + p.reg_r };
+            const double b[3] = { acc[0], acc[1], acc[2] };
+            double d[3];
+            solve3_colpiv_qr(H, b, d);
+            spose[0] = pose[0] + d[0];
+            spose[1] = pose[1] + d[1];
+            spose[2] = pose[2] + d[2];
+        }
+        __syncthreads();
+        pose[0] = spose[0];
+        pose[1] = spose[1];
+        pose[2] = spose[2];
+        // cost at the new pose (and the next step's sums, and the covariance
+        // gradient should the loop stop here)
+        pass(p, grid, sc, pose, smin, smax, cmin, cmax, acc);
+        wg_sum(acc, red);
+        cost = acc[9];
+        if (traj && threadIdx.x == 0) {
+            double* t = traj + ((size_t)blockIdx.x * max(1, p.max_iter) + it) * 4;
+            t[0] = pose[0];
+            t[1] = pose[1];
+            t[2] = pose[2];
+            t[3] = cost;
+        }
+        if (++it >= p.max_iter || fabs(prevCost - cost) < p.conv) break;
+        prevCost = cost;
+    }
+    if (threadIdx.x == 0) {
+        LsRecord rec;
+        rec.pose[0] = pose[0];
+        rec.pose[1] = pose[1];
+        rec.pose[2] = pose[2];
+        rec.cost = cost;
+        rec.grad[0] = acc[10];
+        rec.grad[1] = acc[11];
+        rec.grad[2] = acc[12];
+        rec.iterations = it;
+        rec.pad = 0;
+        out[blockIdx.x] = rec;
+    }
+}
+
+// CostSquareError::Cost and ComputeGradient sums at one pose (diagnostics):
+// out[0] = cost, out[1..3] = sum 2 e (-grad)
+__global__ __launch_bounds__(kLsThreads) void k_sq_cost(LsPlan p, const double* __restrict__ grid,
+                                                        LsScanRef sc, double* __restrict__ out)
+{
+    __shared__ double red[kAcc * (kLsThreads / 64)];
+    const double cmin = fmax(p.cost_min, sc.min_range), cmax = fmin(p.cost_max, sc.max_range);
+    double acc[kAcc];
+    // step filter empty: only the cost-side sums are accumulated
+    pass(p, grid, sc, sc.pose0, 0.0, 0.0, cmin, cmax, acc);
+    wg_sum(acc, red);
+    if (threadIdx.x == 0) {
+        out[0] = acc[9];
+        out[1] = acc[10];
+        out[2] = acc[11];
+        out[3] = acc[12];
+    }
+}
+
+LsPlan make_ls_plan(const lgs_grid* g, const lgs_linsolve_params* prm)
+{
+    LsPlan p{};
+    p.min_x = g->min_x;
+    p.min_y = g->min_y;
+    p.res = g->res;
+    p.W = g->w;
+    p.H = g->h;
+    p.max_iter = prm->num_iterations_max;
+    p.conv = prm->convergence_threshold;
+    p.step_min = prm->usable_range_min;
+    p.step_max = prm->usable_range_max;
+    p.cost_min = prm->cost_usable_range_min;
+    p.cost_max = prm->cost_usable_range_max;
+    p.reg_t = prm->translation_regularizer;
+    p.reg_r = prm->rotation_regularizer;
+    return p;
+}
+
+LsScanRef scan_ref(const lgs_scan* s, lgs_pose2d initial)
+{
+    LsScanRef r{};
+    r.ranges = s->d_ranges;
+    r.angles = s->d_angles;
+    r.min_range = s->min_range;
+    r.max_range = s->max_range;
+    const lgs_pose2d sp = compound(initial, s->rel);
+    r.pose0[0] = sp.x;
+    r.pose0[1] = sp.y;
+    r.pose0[2] = sp.theta;
+    r.n = s->n;
+    return r;
+}
+
+void check_grid(const lgs_grid* g)
+{
+    LGS_REQUIRE(g && g->d && g->w >= 1 && g->h >= 1, "grid must be non-empty");
+}
+
+void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params* prm,
+                  const lgs_scan* const* scans, const lgs_pose2d* init, int n,
+                  lgs_linsolve_summary* out, double* traj)
+{
+    check_grid(grid);
+    LGS_REQUIRE(prm, "null params");
+    LGS_HIP_CHECK(hipSetDevice(ctx->device));
+    const LsPlan p = make_ls_plan(grid, prm);
+    const int iters = std::max(1, p.max_iter);
+    std::vector<LsScanRef> refs(n);
+    for (int j = 0; j < n; ++j) {
+        LGS_REQUIRE(scans[j] && scans[j]->n >= 1, "empty scan");
+        refs[j] = scan_ref(scans[j], init[j]);
+    }
+    // pinned staging: [refs | records | trajectory]
+    const size_t b_refs = sizeof(LsScanRef) * n, b_rec = sizeof(LsRecord) * n;
+    const size_t b_traj = traj ? sizeof(double) * 4 * (size_t)iters * n : 0;
+    char* h = (char*)ctx->ensure_pinned(b_refs + b_rec + b_traj);
+    std::memcpy(h, refs.data(), b_refs);
+    char* d = (char*)ctx->ensure(S_LIN0, b_refs + b_rec + b_traj);
+    LGS_HIP_CHECK(hipMemcpyAsync(d, h, b_refs, hipMemcpyHostToDevice, ctx->stream));
+    const int tok = ctx->timing_begin(K_LINSOLVE, 0.0);
+    hipLaunchKernelGGL(k_linsolve, dim3(n), dim3(kLsThreads), 0, ctx->stream, p, grid->d,
+                       (const LsScanRef*)d, (LsRecord*)(d + b_refs),
+                       traj ? (double*)(d + b_refs + b_rec) : nullptr);
+    ctx->timing_end(tok);
+    LGS_HIP_CHECK(hipGetLastError());
+    LGS_HIP_CHECK(hipMemcpyAsync(h + b_refs, d + b_refs, b_rec + b_traj, hipMemcpyDeviceToHost,
+                                 ctx->stream));
+    LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (ctx->profile) ctx->harvest();
+    const LsRecord* rec = (const LsRecord*)(h + b_refs);
+    for (int j = 0; j < n; ++j) {
+        lgs_linsolve_summary& o = out[j];
+        std::memset(&o, 0, sizeof(o));
+        const LsRecord& r = rec[j];
+        o.pose_found = 1;
+        o.iterations = r.iterations;
+        o.cost = r.cost;
+        o.normalized_cost = r.cost / (double)scans[j]->n;
+        o.initial_pose = init[j];
+        o.sensor_pose = { refs[j].pose0[0], refs[j].pose0[1], refs[j].pose0[2] };
+        o.best_sensor_pose = { r.pose[0], r.pose[1], r.pose[2] };
+        o.estimated_pose = move_backward(o.best_sensor_pose, scans[j]->rel);
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) o.covariance[3 * a + b] = r.grad[a] * r.grad[b];
+        o.covariance[0] += 0.01;
+        o.covariance[4] += 0.01;
+        o.covariance[8] += 0.01;
+    }
+    if (traj) {
+        const double* t = (const double*)(h + b_refs + b_rec);
+        std::memcpy(traj, t, sizeof(double) * 4 * (size_t)out[0].iterations);
+    }
+}
+
+}  // namespace
+
+extern "C" int lgs_linsolve_optimize_pose(lgs_ctx* ctx, const lgs_grid* grid,
+                                          const lgs_linsolve_params* params, const lgs_scan* scan,
+                                          lgs_pose2d initial, lgs_linsolve_summary* out,
+                                          double* trajectory)
+{
+    if (!ctx || !grid || !params || !scan || !out) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] { run_linsolve(ctx, grid, params, &scan, &initial, 1, out, trajectory); });
+}
+
+extern "C" int lgs_linsolve_optimize_pose_batch(lgs_ctx* ctx, const lgs_grid* grid,
+                                                const lgs_linsolve_params* params,
+                                                const lgs_scan* const* scans,
+                                                const lgs_pose2d* initial, int n,
+                                                lgs_linsolve_summary* out)
+{
+    if (!ctx || !grid || !params || !scans || !initial || !out || n < 0) return LGS_ERR_INVALID_ARG;
+    if (n == 0) return LGS_OK;
+    return guarded(ctx, [&] { run_linsolve(ctx, grid, params, scans, initial, n, out, nullptr); });
+}
+
+extern "C" int lgs_cost_square_error(lgs_ctx* ctx, const lgs_grid* grid, double umin, double umax,
+                                     const lgs_scan* scan, lgs_pose2d sensor_pose, double* out_cost,
+                                     double* out_cov)
+{
+    if (!ctx || !grid || !scan || !out_cost) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        check_grid(grid);
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        lgs_linsolve_params prm{};
+        prm.cost_usable_range_min = umin;
+        prm.cost_usable_range_max = umax;
+        const LsPlan p = make_ls_plan(grid, &prm);
+        LsScanRef r = scan_ref(scan, { 0, 0, 0 });
+        r.pose0[0] = sensor_pose.x;
+        r.pose0[1] = sensor_pose.y;
+        r.pose0[2] = sensor_pose.theta;
+        double* d = (double*)ctx->ensure(S_LIN1, 4 * sizeof(double));
+        double* h = (double*)ctx->ensure_pinned(4 * sizeof(double));
+        hipLaunchKernelGGL(k_sq_cost, dim3(1), dim3(kLsThreads), 0, ctx->stream, p, grid->d, r, d);
+        LGS_HIP_CHECK(hipGetLastError());
+        LGS_HIP_CHECK(hipMemcpyAsync(h, d, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        *out_cost = h[0];
+        if (out_cov) {
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) out_cov[3 * a + b] = h[1 + a] * h[1 + b];
+            out_cov[0] += 0.01;
+            out_cov[4] += 0.01;
+            out_cov[8] += 0.01;
+        }
+    });
+}

@@ -331,8 +331,12 @@ void raycast(lgs_map* m, const std::vector<ScanHits>& scans, const lgs_builder_p
     LGS_HIP_CHECK(hipMemcpyAsync(d_rays, pin, rb, hipMemcpyHostToDevice, st));
     LGS_HIP_CHECK(hipMemcpyAsync(d_offs, pin + rb, ob, hipMemcpyHostToDevice, st));
     LGS_HIP_CHECK(hipMemsetAsync(d_bad, 0, sizeof(int), st));
+    // algorithmic bytes: 8 B per emitted key (emit), 8 B key +
+    // 16 B cell read/write per update (apply)
+    int tok = ctx->timing_begin(K_RAY_EMIT, 8.0 * (double)total);
     hipLaunchKernelGGL(k_emit, dim3((nrays + 63) / 64), dim3(64), 0, st, d_rays, d_offs, nrays, m->w,
                        m->h, d_keys, d_bad);
+    ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
     int cell_bits = 1;
     while (cell_bits < 32 && (1ull << cell_bits) < (unsigned long long)m->w * m->h) ++cell_bits;
@@ -342,12 +346,15 @@ void raycast(lgs_map* m, const std::vector<ScanHits>& scans, const lgs_builder_p
     void* temp = ctx->ensure(S_RAY5, tbytes);
     LGS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp, tbytes, d_keys, d_sorted, (int)total, 0,
                                                     32 + cell_bits, st));
+    tok = ctx->timing_begin(K_RAY_APPLY, 24.0 * (double)total);
     hipLaunchKernelGGL(k_apply, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d_sorted, total,
                        m->d_cells, m->d_hit, m->d_miss, bp->prob_hit, bp->prob_miss);
+    ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
     int bad = 0;
     LGS_HIP_CHECK(hipMemcpyAsync(pin, d_bad, sizeof(int), hipMemcpyDeviceToHost, st));
     LGS_HIP_CHECK(hipStreamSynchronize(st));
+    if (ctx->profile) ctx->harvest();
     std::memcpy(&bad, pin, sizeof(int));
     if (bad) throw Error(LGS_ERR_INTERNAL, "ray cell outside the map geometry");
 }

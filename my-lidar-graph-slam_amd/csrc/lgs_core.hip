@@ -52,7 +52,8 @@ void* lgs_ctx::ensure_pinned(size_t bytes)
 
 namespace lgs {
 const char* const kKernelNames[K_NUM_KERNELS] = { "k_project", "k_coarse", "k_seed", "k_select",
-                                                  "k_fine", "k_replay", "k_cost", "k_precompute" };
+                                                  "k_fine", "k_replay", "k_cost", "k_precompute",
+                                                  "k_linsolve", "k_ray_emit", "k_ray_apply" };
 }
 
 int lgs_ctx::timing_begin(int kernel, double algo_bytes)

@@ -62,6 +62,7 @@ enum Slot {
     S_TEDGE,        // int [T] generation-stamped 'angle touches the low map edge' flags
     S_RAY0, S_RAY1, S_RAY2, S_RAY3, S_RAY4, S_RAY5, S_RAY6, S_RAY7,
     S_LS0, S_LS1,
+    S_LIN0, S_LIN1,   // K4 staging
     S_NUM_SLOTS
 };
 
@@ -115,7 +116,8 @@ struct CostPlan {
 }  // namespace lgs
 
 namespace lgs {
-enum KernelId { K_PROJECT = 0, K_COARSE, K_SEED, K_SELECT, K_FINE, K_REPLAY, K_COST, K_PRECOMPUTE, K_NUM_KERNELS };
+enum KernelId { K_PROJECT = 0, K_COARSE, K_SEED, K_SELECT, K_FINE, K_REPLAY, K_COST, K_PRECOMPUTE,
+                K_LINSOLVE, K_RAY_EMIT, K_RAY_APPLY, K_NUM_KERNELS };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 struct PendingTiming {
     int kernel;

@@ -103,6 +103,20 @@ class MapGeometry(C.Structure):
         return self.resolution
 
 
+class LinsolveParams(C.Structure):
+    """lgs_linsolve_params: ScanMatcherLinearSolver ctor order, then CostSquareError's usable range."""
+    _fields_ = [("num_iterations_max", C.c_int), ("convergence_threshold", C.c_double),
+                ("usable_range_min", C.c_double), ("usable_range_max", C.c_double),
+                ("translation_regularizer", C.c_double), ("rotation_regularizer", C.c_double),
+                ("cost_usable_range_min", C.c_double), ("cost_usable_range_max", C.c_double)]
+
+
+class LinsolveSummary(C.Structure):
+    _fields_ = [("pose_found", C.c_int), ("iterations", C.c_int), ("normalized_cost", C.c_double),
+                ("initial_pose", Pose2D), ("estimated_pose", Pose2D), ("covariance", C.c_double * 9),
+                ("sensor_pose", Pose2D), ("best_sensor_pose", Pose2D), ("cost", C.c_double)]
+
+
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double),
                 ("algo_bytes", C.c_double)]
@@ -153,6 +167,12 @@ _PROTOS = [
                                                C.POINTER(BuilderParams)]),
     ("lgs_map_download", C.c_int, [_P, _P, C.POINTER(C.c_double), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32)]),
+    ("lgs_linsolve_optimize_pose", C.c_int, [_P, _P, C.POINTER(LinsolveParams), _P, Pose2D,
+                                             C.POINTER(LinsolveSummary), C.POINTER(C.c_double)]),
+    ("lgs_linsolve_optimize_pose_batch", C.c_int, [_P, _P, C.POINTER(LinsolveParams), C.POINTER(_P),
+                                                   C.POINTER(Pose2D), C.c_int, C.POINTER(LinsolveSummary)]),
+    ("lgs_cost_square_error", C.c_int, [_P, _P, C.c_double, C.c_double, _P, Pose2D, C.POINTER(C.c_double),
+                                        C.POINTER(C.c_double)]),
 ]
 
 SYMBOLS = [p[0] for p in _PROTOS]
@@ -300,6 +320,35 @@ class Context:
         self.check(self.lib.lgs_rtcsm_dense_scores(self.h, grid.h, coarse.h, C.byref(params), scan.h,
                                                    Pose2D(*init), dptr(cs), dptr(fs), dims), "dense_scores")
         return list(dims), cs, fs
+
+    # ---- Gauss-Newton refine (K4) ----
+    def linsolve(self, grid, params: LinsolveParams, scan, init, trajectory: bool = False):
+        """ScanMatcherLinearSolver::OptimizePose; returns the summary and, with
+        trajectory=True, [(x, y, theta, cost)] after every OptimizeStep."""
+        out = LinsolveSummary()
+        traj = np.zeros(4 * max(1, params.num_iterations_max)) if trajectory else None
+        self.check(self.lib.lgs_linsolve_optimize_pose(self.h, grid.h, C.byref(params), scan.h, Pose2D(*init),
+                                                       C.byref(out), dptr(traj) if trajectory else None),
+                   "linsolve_optimize_pose")
+        if trajectory:
+            return out, [tuple(traj[4 * k: 4 * k + 4]) for k in range(out.iterations)]
+        return out
+
+    def linsolve_batch(self, grid, params: LinsolveParams, scans, inits):
+        n = len(scans)
+        arr = (_P * n)(*[s.h for s in scans])
+        poses = (Pose2D * n)(*[Pose2D(*p) for p in inits])
+        out = (LinsolveSummary * n)()
+        self.check(self.lib.lgs_linsolve_optimize_pose_batch(self.h, grid.h, C.byref(params), arr, poses, n, out),
+                   "linsolve_optimize_pose_batch")
+        return list(out)
+
+    def cost_square_error(self, grid, umin: float, umax: float, scan, sensor_pose, covariance: bool = False):
+        v = C.c_double()
+        cov = (C.c_double * 9)() if covariance else None
+        self.check(self.lib.lgs_cost_square_error(self.h, grid.h, umin, umax, scan.h, Pose2D(*sensor_pose),
+                                                  C.byref(v), cov), "cost_square_error")
+        return (v.value, list(cov)) if covariance else v.value
 
     # ---- occupancy maps (K3) ----
     def map(self, res: float, patch_size: int, ncx: int, ncy: int, center=(0.0, 0.0)) -> "Map":

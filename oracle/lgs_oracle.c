@@ -830,6 +830,41 @@ static void sq_map_gradient(const orc_grid* g, orc_pose sp, double r, double a, 
     out[2] = -r * sinT * gx + r * cosT * gy;
 }
 
+/* CostSquareError::ComputeCovariance (:112-135) via ComputeGradient (:61-109):
+ * g = sum 2 e (-grad) over usable beams, cov = g g^T + 0.01 I */
+void orc_sq_covariance(const orc_grid* g, double umin, double umax, const orc_scan* scan,
+                       orc_pose sp, double cov[9])
+{
+    double gx = 0.0, gy = 0.0, gt = 0.0;
+    const double minRange = std_max(umin, scan->min_range);
+    const double maxRange = std_min(umax, scan->max_range);
+    for (int i = 0; i < scan->n; ++i) {
+        const double r = scan->ranges[i];
+        const double a = scan->angles[i];
+        if (r >= maxRange || r <= minRange)
+            continue;
+        double sinT, cosT;
+        sincos(sp.theta + a, &sinT, &cosT);
+        const double hx = sp.x + r * cosT;
+        const double hy = sp.y + r * sinT;
+        const double fx = (hx - g->min_x) / g->res;
+        const double fy = (hy - g->min_y) / g->res;
+        const double e = 1.0 - orc_sq_smoothed_value(g, fx, fy);
+        double gv[3];
+        sq_map_gradient(g, sp, r, a, gv);
+        gx += 2.0 * e * (-gv[0]);
+        gy += 2.0 * e * (-gv[1]);
+        gt += 2.0 * e * (-gv[2]);
+    }
+    const double gvv[3] = { gx, gy, gt };
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            cov[3 * i + j] = gvv[i] * gvv[j];
+    cov[0] += 0.01;
+    cov[4] += 0.01;
+    cov[8] += 0.01;
+}
+
 /* Eigen::ColPivHouseholderQR<Matrix3d>::compute + solve, restated from the
  * published algorithm (Eigen >= 3.3; not vendored in the reference). */
 void orc_solve3_colpiv_qr(const double Hin[9], const double bin[3], double xout[3])
@@ -1011,6 +1046,12 @@ static orc_pose linsolve_step(const orc_grid* g, const orc_linsolve_params* p,
     return out;
 }
 
+orc_pose orc_linsolve_step(const orc_grid* g, const orc_linsolve_params* p, const orc_scan* scan,
+                           orc_pose sensor_pose)
+{
+    return linsolve_step(g, p, scan, sensor_pose);
+}
+
 int orc_linsolve_optimize_pose(const orc_grid* g, const orc_linsolve_params* p,
                                const orc_scan* scan, orc_pose initial_pose,
                                orc_summary* out, orc_pose* traj)
@@ -1039,36 +1080,7 @@ int orc_linsolve_optimize_pose(const orc_grid* g, const orc_linsolve_params* p,
     out->sensor_pose = sensorPose;
     out->best_sensor_pose = best;
     out->best_win[0] = it;
-    /* CostSquareError::ComputeCovariance (:112-135) via ComputeGradient (:61-109) */
-    {
-        double gx = 0.0, gy = 0.0, gt = 0.0;
-        const double minRange = std_max(p->cost_usable_range_min, scan->min_range);
-        const double maxRange = std_min(p->cost_usable_range_max, scan->max_range);
-        for (int i = 0; i < scan->n; ++i) {
-            const double r = scan->ranges[i];
-            const double a = scan->angles[i];
-            if (r >= maxRange || r <= minRange)
-                continue;
-            double sinT, cosT;
-            sincos(best.theta + a, &sinT, &cosT);
-            const double hx = best.x + r * cosT;
-            const double hy = best.y + r * sinT;
-            const double fx = (hx - g->min_x) / g->res;
-            const double fy = (hy - g->min_y) / g->res;
-            const double e = 1.0 - orc_sq_smoothed_value(g, fx, fy);
-            double gv[3];
-            sq_map_gradient(g, best, r, a, gv);
-            gx += 2.0 * e * (-gv[0]);
-            gy += 2.0 * e * (-gv[1]);
-            gt += 2.0 * e * (-gv[2]);
-        }
-        const double gvv[3] = { gx, gy, gt };
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j)
-                out->covariance[3 * i + j] = gvv[i] * gvv[j];
-        out->covariance[0] += 0.01;
-        out->covariance[4] += 0.01;
-        out->covariance[8] += 0.01;
-    }
+    /* CostSquareError::ComputeCovariance (:112-135) at the best pose */
+    orc_sq_covariance(g, p->cost_usable_range_min, p->cost_usable_range_max, scan, best, out->covariance);
     return 0;
 }

@@ -188,6 +188,12 @@ double orc_sq_cost(const orc_grid* g, double umin, double umax, const orc_scan* 
 int orc_linsolve_optimize_pose(const orc_grid* g, const orc_linsolve_params* p,
                                const orc_scan* scan, orc_pose initial_pose,
                                orc_summary* out, orc_pose* trajectory /* may be NULL; max_iter sensor poses */);
+/* One OptimizeStep (:88-148) from a sensor pose */
+orc_pose orc_linsolve_step(const orc_grid* g, const orc_linsolve_params* p, const orc_scan* scan,
+                           orc_pose sensor_pose);
+/* ComputeCovariance (:112-135) at a sensor pose */
+void orc_sq_covariance(const orc_grid* g, double umin, double umax, const orc_scan* scan,
+                       orc_pose sensor_pose, double cov[9]);
 /* colPivHouseholderQr().solve() restated for 3x3 (Eigen, not vendored) */
 void orc_solve3_colpiv_qr(const double H[9], const double b[3], double x[3]);
 

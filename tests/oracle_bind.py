@@ -125,6 +125,11 @@ def lib():
         L.orc_sq_smoothed_value.argtypes = [C.POINTER(Grid), C.c_double, C.c_double]
         L.orc_sq_cost.restype = C.c_double
         L.orc_sq_cost.argtypes = [C.POINTER(Grid), C.c_double, C.c_double, C.POINTER(Scan), Pose]
+        L.orc_linsolve_step.restype = Pose
+        L.orc_linsolve_step.argtypes = [C.POINTER(Grid), C.POINTER(LinsolveParams), C.POINTER(Scan), Pose]
+        L.orc_sq_covariance.restype = None
+        L.orc_sq_covariance.argtypes = [C.POINTER(Grid), C.c_double, C.c_double, C.POINTER(Scan), Pose,
+                                        C.POINTER(C.c_double)]
         L.orc_linsolve_optimize_pose.restype = C.c_int
         L.orc_linsolve_optimize_pose.argtypes = [C.POINTER(Grid), C.POINTER(LinsolveParams), C.POINTER(Scan),
                                                  Pose, C.POINTER(Summary), C.POINTER(Pose)]
