@@ -22,21 +22,30 @@
  *                                (the ScanMatcher plugin entry, H/mapping/scan_matcher.hpp:198-199)
  *   lgs_rtcsm_optimize_pose_batch  LoopDetectorRealTimeCorrelative::Detect's per-node
  *                                loop C/mapping/loop_detector_real_time_correlative.cpp:66-92
+ *   lgs_loop_detect_rtcsm        LoopDetectorRealTimeCorrelative::Detect + FindCorrespondingPose
+ *                                C/mapping/loop_detector_real_time_correlative.cpp:26-125
  *   lgs_cost_greedy_endpoint     CostGreedyEndpoint::Cost
  *                                C/mapping/cost_function_greedy_endpoint.cpp:32-111
- *   lgs_grid_integrate_scans     GridMapBuilder's per-beam ray-cast + Bayes update
- *                                C/mapping/grid_map_builder.cpp:167-186 and :292-329
+ *   lgs_map_update_scan          GridMapBuilder::UpdateGridMap's insert of one scan
+ *                                (bounding box, Expand, per-beam Bresenham + Bayes update)
+ *                                C/mapping/grid_map_builder.cpp:149-186
+ *   lgs_map_construct_from_scans GridMapBuilder::ConstructMapFromScans
+ *                                C/mapping/grid_map_builder.cpp:227-332 (UpdateLatestMap :196-207)
  *   lgs_linsolve_optimize_pose   ScanMatcherLinearSolver::OptimizePose(query)
  *                                C/mapping/scan_matcher_linear_solver.cpp:38-148
+ *   lgs_cost_square_error        CostSquareError::Cost / ComputeCovariance
+ *                                C/mapping/cost_function_square_error.cpp:21-58, :112-135
  *
  * Threading: one lgs_ctx per matcher instance (the reference's frontend and
  * loop detector own distinct matchers, C/slam_launcher.cpp:774-775, :835).  A
  * context owns one HIP stream and its scratch; calls on one context must not
  * overlap, calls on different contexts may.
  *
- * Numerics: fp64 throughout.  Cell indices, hit/miss counts and the correlative
- * argmax are bit-exact with the reference CPU path; costs/covariances agree to
- * within 1e-5 (device exp/sin/cos differ from glibc in the last ulp).
+ * Numerics: fp64 throughout.  Cell indices, hit/miss counts, map cells and the
+ * correlative argmax/score are bit-exact with the reference CPU path; greedy-
+ * endpoint costs/covariances agree to within 1e-5 (device exp differs from glibc
+ * in the last ulp); the Gauss-Newton refine agrees per step and within 1e-5 end
+ * to end on 1081-beam scans (DESIGN.md §K4 explains why not bitwise).
  */
 #ifndef LGS_HIP_H
 #define LGS_HIP_H
@@ -249,6 +258,45 @@ int  lgs_map_download(lgs_ctx* ctx, const lgs_map* map, double* cells, uint32_t*
 int  lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
                               const lgs_cost_ge_params* cost, const lgs_scan* scan,
                               lgs_pose2d sensor_pose, double* out_cost);
+
+/* ---- loop-closure batch (LoopDetectorRealTimeCorrelative::Detect) ----
+ * C/mapping/loop_detector_real_time_correlative.cpp:26-125.  A query is one
+ * local map (LoopDetectionQuery::mLocalMapInfo / mLocalMapNode) and the
+ * contiguous range of candidates (its mPoseGraphNodes) matched against it. */
+typedef struct {
+    const lgs_grid* map;            /* local grid map */
+    const lgs_grid* coarse;         /* its cached coarse map, or NULL = compute (:52-60) */
+    lgs_pose2d local_map_node_pose; /* mLocalMapNode.Pose() */
+    int local_map_node_index;       /* mLocalMapNode.Index() */
+    int first_candidate, num_candidates;
+} lgs_loop_query;
+
+typedef struct {
+    const lgs_scan* scan;           /* poseGraphNode.ScanData() */
+    lgs_pose2d node_pose;           /* poseGraphNode.Pose() (initial pose) */
+    int node_index;                 /* poseGraphNode.Index() */
+    int pad;
+} lgs_loop_candidate;
+
+/* LoopDetectionResult (H/mapping/loop_detector.hpp:60-87) + diagnostics; a
+ * fixed 176-byte record (22 x 8 B) so shards can be all-gathered as a flat array. */
+typedef struct {
+    int found;                      /* 0: the reference appends no result */
+    int start_node_index, end_node_index;
+    int pad;
+    lgs_pose2d relative_pose;       /* InverseCompound(localMapNode.Pose(), estimated) */
+    lgs_pose2d start_node_pose;
+    lgs_pose2d estimated_pose;      /* matcher's estimate (world frame) */
+    double covariance[9];
+    double score;                   /* correlative score of the best pose */
+    double normalized_cost;
+} lgs_loop_result;
+
+/* One result per candidate, in candidate order. */
+int  lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
+                           double score_threshold, const lgs_loop_query* queries, int num_queries,
+                           const lgs_loop_candidate* candidates, int num_candidates,
+                           lgs_loop_result* results);
 
 /* ---- K4: Gauss-Newton refine (ScanMatcherLinearSolver + CostSquareError) ----
  * Replaces ScanMatcherLinearSolver::OptimizePose (C/mapping/scan_matcher_linear_solver.cpp:38-85,

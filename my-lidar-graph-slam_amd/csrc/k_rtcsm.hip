@@ -1314,6 +1314,28 @@ void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
     }
 }
 
+// ComputeCoarserMap (:148-153) into the context-owned coarse grid
+const lgs_grid* coarser_map(lgs_ctx* ctx, const lgs_grid* grid, int low_res)
+{
+    LGS_HIP_CHECK(hipSetDevice(ctx->device));
+    lgs_grid* cg = ctx->coarse_scratch;
+    if (!cg) {
+        cg = new lgs_grid();
+        cg->ctx = ctx;
+        cg->device = ctx->device;
+        cg->owned = false;
+        ctx->coarse_scratch = cg;
+    }
+    cg->d = (double*)ctx->ensure(S_COARSE_GRID, sizeof(double) * std::max<size_t>(1, (size_t)grid->w * grid->h));
+    cg->w = grid->w;
+    cg->h = grid->h;
+    cg->min_x = grid->min_x;
+    cg->min_y = grid->min_y;
+    cg->res = grid->res;
+    launch_precompute(ctx, grid, low_res, cg->d);
+    return cg;
+}
+
 }  // namespace
 
 extern "C" int lgs_rtcsm_optimize_pose(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
@@ -1352,21 +1374,7 @@ extern "C" int lgs_rtcsm_optimize_pose_query(lgs_ctx* ctx, const lgs_grid* grid,
     if (!ctx || !grid || !params || !out) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
         LGS_REQUIRE(params->low_resolution >= 1, "low_resolution must be >= 1");
-        // ComputeCoarserMap (:148-153) into a context-owned coarse grid
-        lgs_grid* cg = ctx->coarse_scratch;
-        if (!cg) {
-            cg = new lgs_grid();
-            cg->ctx = ctx;
-            cg->owned = false;
-            ctx->coarse_scratch = cg;
-        }
-        cg->d = (double*)ctx->ensure(S_COARSE_GRID, sizeof(double) * std::max<size_t>(1, (size_t)grid->w * grid->h));
-        cg->w = grid->w;
-        cg->h = grid->h;
-        cg->min_x = grid->min_x;
-        cg->min_y = grid->min_y;
-        cg->res = grid->res;
-        launch_precompute(ctx, grid, params->low_resolution, cg->d);
+        const lgs_grid* cg = coarser_map(ctx, grid, params->low_resolution);
         lgs_scan* s = const_cast<lgs_scan*>(scan);
         run_batch(ctx, grid, cg, params, cost, &s, &initial, 1, DBL_MIN, out);
     });
@@ -1463,5 +1471,67 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
             LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
         }
         *out_cost = h_rec->costs[0];
+    });
+}
+
+// LoopDetectorRealTimeCorrelative::Detect (C/mapping/loop_detector_real_time_correlative.cpp:26-92)
+// with FindCorrespondingPose (:96-125): per query, the coarse map (computed here
+// when the caller has none cached, :52-60), then every candidate node matched
+// with OptimizePose(.., ScoreThreshold) and, when found, the loop edge
+// InverseCompound(localMapNode.Pose(), estimatedPose).  One result per
+// candidate, in candidate order (found == 0 where the reference appends none).
+extern "C" int lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* params,
+                                     const lgs_cost_ge_params* cost, double score_threshold,
+                                     const lgs_loop_query* queries, int num_queries,
+                                     const lgs_loop_candidate* candidates, int num_candidates,
+                                     lgs_loop_result* results)
+{
+    if (!ctx || !params || !cost || (num_queries > 0 && !queries) || num_queries < 0 ||
+        num_candidates < 0 || (num_candidates > 0 && (!candidates || !results)))
+        return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        LGS_REQUIRE(score_threshold > 0.0 && score_threshold <= 1.0,
+                    "score threshold must be in (0, 1] (:21-22)");
+        std::vector<lgs_rtcsm_summary> sums;
+        std::vector<lgs_scan*> scans;
+        std::vector<lgs_pose2d> poses;
+        int covered = 0;
+        for (int q = 0; q < num_queries; ++q) {
+            const lgs_loop_query& Q = queries[q];
+            LGS_REQUIRE(Q.map, "loop query without a local map");
+            LGS_REQUIRE(Q.first_candidate == covered && Q.num_candidates >= 0 &&
+                            Q.first_candidate + Q.num_candidates <= num_candidates,
+                        "loop queries must cover the candidates contiguously and in order");
+            covered += Q.num_candidates;
+            if (Q.num_candidates == 0) continue;
+            const lgs_grid* coarse = Q.coarse ? Q.coarse : coarser_map(ctx, Q.map, params->low_resolution);
+            const int n = Q.num_candidates;
+            scans.resize(n);
+            poses.resize(n);
+            sums.resize(n);
+            for (int j = 0; j < n; ++j) {
+                const lgs_loop_candidate& c = candidates[Q.first_candidate + j];
+                LGS_REQUIRE(c.scan, "loop candidate without a scan");
+                scans[j] = const_cast<lgs_scan*>(c.scan);
+                poses[j] = c.node_pose;
+            }
+            run_batch(ctx, Q.map, coarse, params, cost, scans.data(), poses.data(), n, score_threshold,
+                      sums.data());
+            for (int j = 0; j < n; ++j) {
+                lgs_loop_result& r = results[Q.first_candidate + j];
+                std::memset(&r, 0, sizeof(r));
+                const lgs_rtcsm_summary& s = sums[j];
+                r.found = s.pose_found;
+                r.start_node_index = Q.local_map_node_index;
+                r.end_node_index = candidates[Q.first_candidate + j].node_index;
+                r.start_node_pose = Q.local_map_node_pose;
+                r.estimated_pose = s.estimated_pose;
+                r.score = s.score_max;
+                r.normalized_cost = s.normalized_cost;
+                if (s.pose_found) r.relative_pose = inverse_compound(Q.local_map_node_pose, s.estimated_pose);
+                std::memcpy(r.covariance, s.covariance, sizeof(r.covariance));
+            }
+        }
+        LGS_REQUIRE(covered == num_candidates, "loop queries must cover every candidate");
     });
 }

@@ -117,6 +117,24 @@ class LinsolveSummary(C.Structure):
                 ("sensor_pose", Pose2D), ("best_sensor_pose", Pose2D), ("cost", C.c_double)]
 
 
+class LoopQuery(C.Structure):
+    _fields_ = [("map", C.c_void_p), ("coarse", C.c_void_p), ("local_map_node_pose", Pose2D),
+                ("local_map_node_index", C.c_int), ("first_candidate", C.c_int), ("num_candidates", C.c_int)]
+
+
+class LoopCandidate(C.Structure):
+    _fields_ = [("scan", C.c_void_p), ("node_pose", Pose2D), ("node_index", C.c_int), ("pad", C.c_int)]
+
+
+class LoopResult(C.Structure):
+    _fields_ = [("found", C.c_int), ("start_node_index", C.c_int), ("end_node_index", C.c_int), ("pad", C.c_int),
+                ("relative_pose", Pose2D), ("start_node_pose", Pose2D), ("estimated_pose", Pose2D),
+                ("covariance", C.c_double * 9), ("score", C.c_double), ("normalized_cost", C.c_double)]
+
+
+LOOP_RESULT_DOUBLES = 22   # sizeof(lgs_loop_result) / 8
+
+
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double),
                 ("algo_bytes", C.c_double)]
@@ -167,6 +185,9 @@ _PROTOS = [
                                                C.POINTER(BuilderParams)]),
     ("lgs_map_download", C.c_int, [_P, _P, C.POINTER(C.c_double), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32)]),
+    ("lgs_loop_detect_rtcsm", C.c_int, [_P, C.POINTER(RtcsmParams), C.POINTER(CostGEParams), C.c_double,
+                                        C.POINTER(LoopQuery), C.c_int, C.POINTER(LoopCandidate), C.c_int,
+                                        C.POINTER(LoopResult)]),
     ("lgs_linsolve_optimize_pose", C.c_int, [_P, _P, C.POINTER(LinsolveParams), _P, Pose2D,
                                              C.POINTER(LinsolveSummary), C.POINTER(C.c_double)]),
     ("lgs_linsolve_optimize_pose_batch", C.c_int, [_P, _P, C.POINTER(LinsolveParams), C.POINTER(_P),
@@ -320,6 +341,21 @@ class Context:
         self.check(self.lib.lgs_rtcsm_dense_scores(self.h, grid.h, coarse.h, C.byref(params), scan.h,
                                                    Pose2D(*init), dptr(cs), dptr(fs), dims), "dense_scores")
         return list(dims), cs, fs
+
+    # ---- loop-closure batch ----
+    def loop_detect(self, params: RtcsmParams, cost: CostGEParams, thr: float, queries, candidates):
+        """queries: [(map Grid, coarse Grid|None, node_pose, node_index, first, count)];
+        candidates: [(Scan, node_pose, node_index)] -> ctypes LoopResult array (one per candidate)."""
+        qs = (LoopQuery * max(1, len(queries)))()
+        for i, (m, c, pose, idx, first, cnt) in enumerate(queries):
+            qs[i] = LoopQuery(m.h, c.h if c is not None else None, Pose2D(*pose), idx, first, cnt)
+        cs = (LoopCandidate * max(1, len(candidates)))()
+        for i, (s, pose, idx) in enumerate(candidates):
+            cs[i] = LoopCandidate(s.h, Pose2D(*pose), idx, 0)
+        out = (LoopResult * max(1, len(candidates)))()
+        self.check(self.lib.lgs_loop_detect_rtcsm(self.h, C.byref(params), C.byref(cost), float(thr), qs,
+                                                  len(queries), cs, len(candidates), out), "loop_detect_rtcsm")
+        return out
 
     # ---- Gauss-Newton refine (K4) ----
     def linsolve(self, grid, params: LinsolveParams, scan, init, trajectory: bool = False):

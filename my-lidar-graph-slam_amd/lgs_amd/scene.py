@@ -109,3 +109,34 @@ def approx_occupancy_map(segs, poses, angles, w, h, min_x, min_y, res, p_hit=0.6
     p = 1.0 / (1.0 + np.exp(-lo))
     p = np.clip(p, 1e-3, 1 - 1e-3)
     return np.where(seen, p, 0.0)
+
+
+def loop_problem(segs, build_map, n_maps: int = 32, nodes_per_map: int = 16, n_beams: int = 1081,
+                 seed: int = 5, perturb=(2.0, 0.4), arc_scans: int = 10, map_beams: int = 1081):
+    """Config-5 style loop-closure batch: `n_maps` local maps, each built by
+    `build_map(poses, angles) -> (cells, min_x, min_y, res)` from `arc_scans`
+    scans on an arc around its own centre, and `nodes_per_map` candidate
+    nodes per map whose scans are taken near that centre and whose initial
+    poses are the true poses perturbed by U(+-perturb[0] m, +-perturb[1] rad).
+    Returns (maps, candidates) as lgs_amd.loopbatch.LocalMap / Candidate lists
+    (candidates query-major)."""
+    from .loopbatch import Candidate, LocalMap
+    rng = np.random.default_rng(seed)
+    ang = beam_angles(n_beams)
+    mang = beam_angles(map_beams)
+    maps, cands = [], []
+    node = 0
+    for q in range(n_maps):
+        c = (rng.uniform(-1.5, 1.5), rng.uniform(-1.5, 1.5))
+        poses = arc_poses(arc_scans, center=c)
+        cells, mx, my, res = build_map(poses, mang)
+        maps.append(LocalMap(cells, mx, my, res, poses[0], node))
+        node += arc_scans
+        for _ in range(nodes_per_map):
+            true = (c[0] + rng.uniform(-1.0, 1.0), c[1] + rng.uniform(-1.0, 1.0), rng.uniform(-np.pi, np.pi))
+            r = ray_cast(segs, true, ang)
+            init = (true[0] + rng.uniform(-perturb[0], perturb[0]), true[1] + rng.uniform(-perturb[0], perturb[0]),
+                    true[2] + rng.uniform(-perturb[1], perturb[1]))
+            cands.append(Candidate(q, r, ang, init, node))
+            node += 1
+    return maps, cands

@@ -1,0 +1,84 @@
+"""Loop-closure batch on the GPU (lgs_loop_detect_rtcsm) vs the oracle's
+LoopDetectorRealTimeCorrelative::Detect restatement
+(C/mapping/loop_detector_real_time_correlative.cpp:26-125).
+
+found flags, node indices, estimated / relative / start poses and scores are
+bit-exact; normalized cost and covariance agree to 1e-5 relative (device exp
+vs glibc, as for every greedy-endpoint cost)."""
+import numpy as np
+import pytest
+
+import test_loopbatch_cpu as small
+from loop_oracle import oracle_detect_fn
+from lgs_amd import abi, loopbatch, scene
+
+pytestmark = pytest.mark.gpu
+
+LOOP_JSON = (5, 5.0, 5.0, 1.0, 20.0)   # launcher_settings_default.json:107-113 (LoopDetectorRealTimeCorrelative.ScanMatcher)
+
+
+def compare(dev, orc):
+    assert len(dev) == len(orc)
+    for d, o in zip(dev, orc):
+        assert (d.found, d.start_node_index, d.end_node_index) == (o.found, o.start_node_index, o.end_node_index)
+        for f in ("relative_pose", "start_node_pose", "estimated_pose"):
+            a, b = getattr(d, f), getattr(o, f)
+            assert (a.x, a.y, a.theta) == (b.x, b.y, b.theta), f
+        assert d.score == o.score
+        assert abs(d.normalized_cost - o.normalized_cost) <= 1e-5 * max(1.0, abs(o.normalized_cost))
+        assert np.allclose(list(d.covariance), list(o.covariance), rtol=1e-5, atol=1e-9)
+
+
+def test_loop_detect_small(ctx):
+    maps, cands = small.make_problem()
+    p, c = abi.RtcsmParams(*small.PARAMS), abi.CostGEParams(*small.COST)
+    dev = loopbatch.run_sharded(cands, loopbatch.hip_detect_fn(ctx, maps, cands, p, c, small.THR))
+    orc = loopbatch.run_sharded(cands, oracle_detect_fn(maps, cands, small.PARAMS, small.COST, small.THR))
+    compare(loopbatch.decode(dev), loopbatch.decode(orc))
+    found = loopbatch.loop_results(dev)
+    assert 0 < len(found) < len(cands)
+
+
+def test_loop_detect_coarse_computed_inside(ctx):
+    """coarse == NULL: the C-ABI computes ComputeCoarserMap itself (:52-60)."""
+    maps, cands = small.make_problem()
+    p, c = abi.RtcsmParams(*small.PARAMS), abi.CostGEParams(*small.COST)
+    grids = [ctx.grid_from_array(m.cells, m.min_x, m.min_y, m.res) for m in maps]
+    scans = [ctx.scan(x.ranges, x.angles) for x in cands]
+    qs, first = [], 0
+    for qi, m in enumerate(maps):
+        n = sum(1 for x in cands if x.query == qi)
+        qs.append((grids[qi], None, m.node_pose, m.node_index, first, n))
+        first += n
+    out = ctx.loop_detect(p, c, small.THR, qs, [(s, x.pose, x.node_index) for s, x in zip(scans, cands)])
+    ref = loopbatch.run_sharded(cands, loopbatch.hip_detect_fn(ctx, maps, cands, p, c, small.THR))
+    assert bytes(out)[: len(cands) * loopbatch.RECORD_BYTES] == ref.tobytes()
+
+
+def test_loop_detect_bad_queries(ctx):
+    maps, cands = small.make_problem()
+    p, c = abi.RtcsmParams(*small.PARAMS), abi.CostGEParams(*small.COST)
+    g = ctx.grid_from_array(maps[0].cells, maps[0].min_x, maps[0].min_y, 0.05)
+    s = ctx.scan(cands[0].ranges, cands[0].angles)
+    with pytest.raises(abi.LgsError):   # gap in the candidate cover
+        ctx.loop_detect(p, c, 0.6, [(g, None, (0, 0, 0), 0, 1, 1)], [(s, (0, 0, 0), 1), (s, (0, 0, 0), 2)])
+    with pytest.raises(abi.LgsError):   # threshold outside (0, 1] (:21-22)
+        ctx.loop_detect(p, c, 1.5, [(g, None, (0, 0, 0), 0, 0, 1)], [(s, (0, 0, 0), 1)])
+
+
+def test_loop_detect_config5_json_window(ctx, world):
+    """1081-beam candidates, the JSON loop window (+-2.5 m, +-0.5 rad), 500x500 maps."""
+    import oracle_bind as ob
+
+    def build(poses, ang):
+        m = ob.OMap(0.05, 100, 500, 500)
+        for q in poses:
+            m.integrate(q, ob.OScan(scene.ray_cast(world, q, ang), ang), ob.BuilderParams(0.01, 20.0, 0.6, 0.45))
+        return m.cells(), m.m.min_x, m.m.min_y, 0.05
+
+    maps, cands = scene.loop_problem(world, build, n_maps=2, nodes_per_map=2, n_beams=1081, seed=21,
+                                     perturb=(1.0, 0.3), arc_scans=8)
+    p, c = abi.RtcsmParams(*LOOP_JSON), abi.CostGEParams(*small.COST)
+    dev = loopbatch.run_sharded(cands, loopbatch.hip_detect_fn(ctx, maps, cands, p, c, 0.6))
+    orc = loopbatch.run_sharded(cands, oracle_detect_fn(maps, cands, LOOP_JSON, small.COST, 0.6))
+    compare(loopbatch.decode(dev), loopbatch.decode(orc))
