@@ -1,20 +1,31 @@
 #!/usr/bin/env python3
-"""Benchmark: correlative scan matching on MI355X (BASELINE.json config 2).
+"""Benchmark of the MI355X hot path (BASELINE.json configs 2-5).
 
-Step = one ScanMatcher::OptimizePose(query) through the C-ABI
+Default workload ("match", BASELINE.json's metric, config 2): one step = one
+ScanMatcher::OptimizePose(query) through the C-ABI
 (lgs_rtcsm_optimize_pose_query): coarse-map precompute of the 1000x1000 @ 5 cm
 grid, exhaustive +-2 m / +-30 deg correlative search for a 1081-beam scan,
-greedy-endpoint cost and covariance.  Grid and scans are resident in HBM
-before the timed region.  With --gpus N (one process per GPU, torchrun) every
-rank matches its own scans (weak scaling) and the winning poses are
-all-gathered over RCCL at the end of the timed region, as the loop-closure
-batch does.
+greedy-endpoint cost and covariance.  Grid and scans are resident in HBM before
+the timed region.  With --gpus N (one process per GPU, torchrun) every rank
+matches its own scans (replicas, weak scaling) and the winning poses are
+all-gathered over RCCL inside the timed region.
 
-Rank 0 prints ONE JSON line (see DESIGN.md §Measurement for every field).
+Other workloads (--workload):
+  refine  config 3: ScanMatcherLinearSolver, 1081 beams, 50 iterations (one
+          refine per step, synchronous; replicas across ranks)
+  loop    config 5: LoopDetectorRealTimeCorrelative::Detect over 512
+          candidates (32 local maps x 16 nodes, JSON loop window), sharded in
+          contiguous blocks across ranks + all-gather of result records
+          (strong scaling: the 512 candidates are split)
+  stream  config 4: per scan, match against the latest map + local-map insert
+          + latest-map rebuild from the last 10 scans (replicas)
+
+Rank 0 prints ONE JSON line (DESIGN.md §6 explains every field).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -29,96 +40,152 @@ from lgs_amd import abi, scene  # noqa: E402
 
 METRIC = "scans/sec + p50 scan-match ms, 1081-beam vs 1000×1000@5cm grid, 1/2/4/8 GPU"
 PARAMS = (5, 4.0, 4.0, 1.0471976, 20.0)          # LowRes, rangeX, rangeY, rangeTheta, ScanRangeMax
+LOOP_PARAMS = (5, 5.0, 5.0, 1.0, 20.0)           # launcher_settings_default.json:107-113
 COST = (0.01, 20.0, 0.075, 0.1, 1, 0.05, 1.0)    # launcher-built CostGreedyEndpoint members
+LINSOLVE = (50, 0.0, 0.01, 20.0, 1e-3, 1e-3, 0.01, 20.0)   # config 3
+BUILDER = (0.01, 20.0, 0.6, 0.45)                # GridMapBuilder usable range, pHit, pMiss
 HBM_PEAK_GBS = 8000.0                            # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=None, help="default: 200 (match/refine), 4 (loop), 500 (stream)")
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--workload", default="match", choices=["match", "refine", "loop", "stream"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--coarse-planes", type=int, default=1, help="A/B: 1 phase-plane coarse layout, 0 plain")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    d_steps = dict(match=200, refine=200, loop=4, stream=500)[a.workload]
+    d_warm = dict(match=10, refine=5, loop=1, stream=10)[a.workload]
+    a.steps = d_steps if a.steps is None else a.steps
+    a.warmup = d_warm if a.warmup is None else a.warmup
+    return a
 
 
-def make_inputs(rank: int, n_scans: int):
-    world = scene.make_world()
-    ang = scene.beam_angles(1081)
+class Dist:
+    """torch.distributed (RCCL) when launched by torchrun with WORLD_SIZE > 1."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.d = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as tdist
+            torch.cuda.set_device(self.local)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.d = tdist
+
+    def device(self):
+        return f"cuda:{self.local}" if self.d else None
+
+    def barrier(self):
+        if self.d:
+            self.d.barrier()
+
+    def max(self, v: float) -> float:
+        if not self.d:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64, device=self.device())
+        self.d.all_reduce(t, op=self.d.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_gather_rows(self, a: np.ndarray):
+        if not self.d:
+            return a
+        import torch
+        local = torch.from_numpy(np.ascontiguousarray(a)).to(self.device())
+        out = torch.empty((self.world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        self.d.all_gather_into_tensor(out, local)
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+
+    def close(self):
+        if self.d:
+            self.d.destroy_process_group()
+
+
+def roofline_from(stats, kernel, pmc_path):
+    k = stats.get(kernel)
+    if not k or not k["launches"] or not k["algo_bytes"]:
+        return None
+    per_launch = k["algo_bytes"] / k["launches"]
+    avg_ms = k["total_ms"] / k["launches"]
+    achieved = per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            key = next((n for n in pmc if n.startswith(kernel)), None)
+            traffic = pmc[key].get("hbm_bytes_per_launch") if key else None
+        except Exception:
+            traffic = None
+    return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel=kernel,
+                avg_launch_ms=round(avg_ms, 5), algo_bytes_per_launch=per_launch)
+
+
+def bench_map(world, ang):
     w, h, mx, my = scene.map_geometry(1000, 100, 0.05)
     cells = scene.approx_occupancy_map(world, scene.arc_poses(10), ang, w, h, mx, my, 0.05)
-    rng = np.random.default_rng(1000 + rank)
+    return cells, mx, my
+
+
+def random_scans(world, ang, rng, n, jitter=(0.3, 0.3, 0.2)):
     scans, inits, truths = [], [], []
-    for _ in range(n_scans):
+    for _ in range(n):
         true = (rng.uniform(-1.5, 1.5), rng.uniform(-1.5, 1.5), rng.uniform(-np.pi, np.pi))
-        r = scene.ray_cast(world, true, ang)
-        init = (true[0] + rng.uniform(-0.3, 0.3), true[1] + rng.uniform(-0.3, 0.3),
-                true[2] + rng.uniform(-0.2, 0.2))
-        scans.append(r)
-        inits.append(init)
+        scans.append(scene.ray_cast(world, true, ang))
+        inits.append((true[0] + rng.uniform(-jitter[0], jitter[0]), true[1] + rng.uniform(-jitter[1], jitter[1]),
+                      true[2] + rng.uniform(-jitter[2], jitter[2])))
         truths.append(true)
-    return cells, (mx, my), ang, scans, inits, truths
+    return scans, inits, truths
 
 
-def cpu_baseline(cells, origin, ang, scans, inits, budget_s):
-    """Oracle (CPU restatement of the reference, 1 thread) on a bounded sample."""
-    import ctypes as C
+def oracle_lib():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind as ob
-    g = ob.OGrid(cells, origin[0], origin[1], 0.05)
-    prm = ob.RtcsmParams(*PARAMS)
-    cost = ob.CostGE(*COST)
+    return ob
+
+
+def timed(budget_s, items, fn):
+    """CPU baseline: run fn over items until the budget is spent (>= 3 items)."""
     times = []
     t_start = time.perf_counter()
-    for r, init in zip(scans, inits):
-        osc = ob.OScan(r, ang)
-        out = ob.Summary()
+    for it in items:
         t0 = time.perf_counter()
-        ob.lib().orc_rtcsm_optimize_pose_query(C.byref(g.g), C.byref(prm), C.byref(cost), C.byref(osc.s),
-                                               ob.Pose(*init), C.byref(out))
+        fn(it)
         times.append(time.perf_counter() - t0)
         if time.perf_counter() - t_start > budget_s and len(times) >= 3:
             break
     return len(times) / sum(times), times
 
 
-def main():
-    args = parse()
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world_size > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        dist = tdist
-
-    n_scans = args.warmup + args.steps
-    cells, origin, ang, scans, inits, truths = make_inputs(rank, min(n_scans, 256))
-
-    ctx = abi.Context(local_rank)
+# --------------------------------------------------------------------- match
+def run_match(args, D, ctx):
+    world = scene.make_world()
+    ang = scene.beam_angles(1081)
+    cells, mx, my = bench_map(world, ang)
+    rng = np.random.default_rng(1000 + D.rank)
+    scans, inits, truths = random_scans(world, ang, rng, min(args.warmup + args.steps, 256))
     ctx.set_option(abi.LGS_OPT_COARSE_PLANES, args.coarse_planes)
-    grid = ctx.grid_from_array(cells, origin[0], origin[1], 0.05)
+    grid = ctx.grid_from_array(cells, mx, my, 0.05)
     dscans = [ctx.scan(r, ang) for r in scans]
-    P = abi.RtcsmParams(*PARAMS)
-    cost = abi.CostGEParams(*COST)
+    P, cost = abi.RtcsmParams(*PARAMS), abi.CostGEParams(*COST)
     pick = lambda k: (dscans[k % len(dscans)], inits[k % len(dscans)])
-
     for k in range(args.warmup):
         s, i = pick(k)
         ctx.optimize_pose_query(grid, P, cost, s, i)
     ctx.set_option(abi.LGS_OPT_PROFILE, 1)
     ctx.reset_stats()
-
     results = np.zeros((args.steps, 4))
     lat = []
-    if dist:
-        dist.barrier()
+    D.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -128,69 +195,33 @@ def main():
         lat.append(time.perf_counter() - ts)
         e = out.estimated_pose
         results[k] = (e.x, e.y, e.theta, out.score_max)
-    if dist:
-        import torch
-        local = torch.from_numpy(results).to(f"cuda:{local_rank}")
-        gathered = torch.empty((world_size,) + tuple(local.shape), dtype=local.dtype, device=local.device)
-        dist.all_gather_into_tensor(gathered, local)
-        torch.cuda.synchronize()
+    D.all_gather_rows(results)       # winning poses of every rank, over RCCL
     ctx.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
-
+    elapsed = D.max(time.perf_counter() - t0)
+    D.barrier()
     stats = ctx.kernel_stats()
     ctx.set_option(abi.LGS_OPT_PROFILE, 0)
-
-    # accuracy sanity (not a parity claim): recovered pose vs ground truth
-    err = []
-    for k in range(args.steps):
-        tr = truths[(args.warmup + k) % len(truths)]
-        err.append(max(abs(results[k, 0] - tr[0]), abs(results[k, 1] - tr[1])))
-
-    if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
-
-    total_scans = args.steps * world_size
-    value = total_scans / elapsed
-    kc = stats.get("k_coarse")
-    roofline = None
-    if kc and kc["launches"]:
-        per_launch_bytes = kc["algo_bytes"] / kc["launches"]
-        avg_ms = kc["total_ms"] / kc["launches"]
-        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.pmc):
-            try:
-                pmc = json.load(open(args.pmc))
-                key = next((k for k in pmc if k.startswith("k_coarse")), None)
-                traffic = pmc[key].get("hbm_bytes_per_launch") if key else None
-            except Exception:
-                traffic = None
-        roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                        kernel="k_coarse", avg_launch_ms=round(avg_ms, 5),
-                        algo_bytes_per_launch=per_launch_bytes)
-
+    err = [max(abs(results[k, 0] - truths[(args.warmup + k) % len(truths)][0]),
+               abs(results[k, 1] - truths[(args.warmup + k) % len(truths)][1])) for k in range(args.steps)]
     cpu = None
-    if not args.no_cpu and world_size == 1:
-        cs = scans[: min(len(scans), 24)]
-        ci = inits[: len(cs)]
-        rate, times = cpu_baseline(cells, origin, ang, cs, ci, args.cpu_seconds)
+    if D.rank == 0 and not args.no_cpu and D.world == 1:
+        ob = oracle_lib()
+        g = ob.OGrid(cells, mx, my, 0.05)
+        prm, oc = ob.RtcsmParams(*PARAMS), ob.CostGE(*COST)
+
+        def one(k):
+            out = ob.Summary()
+            ob.lib().orc_rtcsm_optimize_pose_query(C.byref(g.g), C.byref(prm), C.byref(oc),
+                                                   C.byref(ob.OScan(scans[k], ang).s), ob.Pose(*inits[k]),
+                                                   C.byref(out))
+        rate, times = timed(args.cpu_seconds, range(min(len(scans), 24)), one)
         cpu = dict(value=round(rate, 4), unit="scans/s", cores=1, kind="port",
                    sample=f"{len(times)} config-2 scans through the oracle's OptimizePose(query) "
-                          f"(C restatement, -O2 -ffp-contract=off), p50 {1e3 * float(np.median(times)):.1f} ms",
-                   speedup=round(value / rate, 1))
-
+                          f"(C restatement, -O2 -ffp-contract=off, 1 thread), p50 {1e3 * np.median(times):.1f} ms")
     lat_ms = np.array(lat) * 1e3
+    value = args.steps * D.world / elapsed
     line = dict(
-        metric=METRIC, value=round(value, 2), unit="scans/s", n_gpus=world_size, steps=args.steps,
+        metric=METRIC, value=round(value, 2), unit="scans/s", n_gpus=D.world, steps=args.steps,
         warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 4), higher_is_better=True,
         scaling="weak", vs_baseline=None, dtype="f64",
         data="synthetic: 24 m room + 40 boxes, analytic ray-cast 1081-beam scans, 10-scan occupancy map",
@@ -198,17 +229,209 @@ def main():
                              "vs 1000x1000@5cm grid, PatchSize 100",
                     beams=1081, grid=[1000, 1000], resolution=0.05, low_resolution=5,
                     search_range=[4.0, 4.0, 1.0471976], scans_per_rank=args.steps,
-                    parallelism=f"replicas x{world_size} (independent scans per rank) + RCCL all-gather of poses"),
+                    parallelism=f"replicas x{D.world} (independent scans per rank) + RCCL all-gather of poses"),
         p50_scan_match_ms=round(float(np.percentile(lat_ms, 50)), 4),
         p90_scan_match_ms=round(float(np.percentile(lat_ms, 90)), 4),
-        roofline=roofline, cpu_baseline=cpu,
-        kernels={k: dict(launches=v["launches"], avg_ms=round(v["total_ms"] / max(1, v["launches"]), 5))
-                 for k, v in stats.items()},
-        pose_err_max_m=round(float(max(err)), 4),
-    )
-    print(json.dumps(line))
-    if dist:
-        dist.destroy_process_group()
+        roofline=roofline_from(stats, "k_coarse", args.pmc), cpu_baseline=cpu,
+        pose_err_max_m=round(float(max(err)), 4))
+    if cpu:
+        cpu["speedup"] = round(value / cpu["value"], 1)
+    return line, stats, value
+
+
+# -------------------------------------------------------------------- refine
+def run_refine(args, D, ctx):
+    world = scene.make_world()
+    ang = scene.beam_angles(1081)
+    cells, mx, my = bench_map(world, ang)
+    rng = np.random.default_rng(2000 + D.rank)
+    scans, inits, _ = random_scans(world, ang, rng, min(args.warmup + args.steps, 256), jitter=(0.05, 0.05, 0.03))
+    grid = ctx.grid_from_array(cells, mx, my, 0.05)
+    dscans = [ctx.scan(r, ang) for r in scans]
+    lp = abi.LinsolveParams(*LINSOLVE)
+    for k in range(args.warmup):
+        ctx.linsolve(grid, lp, dscans[k % len(dscans)], inits[k % len(dscans)])
+    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
+    ctx.reset_stats()
+    lat = []
+    D.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        j = (args.warmup + k) % len(dscans)
+        ts = time.perf_counter()
+        ctx.linsolve(grid, lp, dscans[j], inits[j])
+        lat.append(time.perf_counter() - ts)
+    elapsed = D.max(time.perf_counter() - t0)
+    stats = ctx.kernel_stats()
+    ctx.set_option(abi.LGS_OPT_PROFILE, 0)
+    # batched throughput (one workgroup per refine)
+    nb = min(64, len(dscans))
+    ctx.linsolve_batch(grid, lp, dscans[:nb], inits[:nb])
+    tb = time.perf_counter()
+    ctx.linsolve_batch(grid, lp, dscans[:nb], inits[:nb])
+    batch_rate = nb / (time.perf_counter() - tb)
+    cpu = None
+    if D.rank == 0 and not args.no_cpu and D.world == 1:
+        ob = oracle_lib()
+        g = ob.OGrid(cells, mx, my, 0.05)
+        olp = ob.LinsolveParams(*LINSOLVE)
+
+        def one(k):
+            out = ob.Summary()
+            ob.lib().orc_linsolve_optimize_pose(C.byref(g.g), C.byref(olp), C.byref(ob.OScan(scans[k], ang).s),
+                                                ob.Pose(*inits[k]), C.byref(out), None)
+        rate, times = timed(args.cpu_seconds, range(min(len(scans), 64)), one)
+        cpu = dict(value=round(rate, 3), unit="refines/s", cores=1, kind="port",
+                   sample=f"{len(times)} config-3 refines through the oracle (1 thread), "
+                          f"p50 {1e3 * np.median(times):.1f} ms")
+    k = stats.get("k_linsolve", {})
+    lat_ms = np.array(lat) * 1e3
+    value = args.steps * D.world / elapsed
+    line = dict(
+        metric="refines/sec, ScanMatcherLinearSolver 1081 beams x 50 iterations vs 1000x1000@5cm",
+        value=round(value, 2), unit="refines/s", n_gpus=D.world, steps=args.steps, warmup=args.warmup,
+        ms_per_step=round(1e3 * elapsed / args.steps, 4), higher_is_better=True, scaling="weak",
+        vs_baseline=None, dtype="f64", data="synthetic (as config 2), seeds within 5 cm / 0.03 rad",
+        config=dict(workload="config3: Gauss-Newton refine (LinearSolver + CostSquareError), 50 iterations",
+                    beams=1081, grid=[1000, 1000], iterations=50, parallelism=f"replicas x{D.world}"),
+        p50_refine_ms=round(float(np.percentile(lat_ms, 50)), 4),
+        batched_refines_per_s_per_gpu=round(batch_rate, 1),
+        roofline=None, cpu_baseline=cpu,
+        kernel_avg_ms=round(k["total_ms"] / k["launches"], 5) if k.get("launches") else None)
+    return line, stats, value
+
+
+# ---------------------------------------------------------------------- loop
+def run_loop(args, D, ctx):
+    from lgs_amd import loopbatch
+    world = scene.make_world()
+    bp = abi.BuilderParams(*BUILDER)
+
+    def build(poses, ang):   # local maps built on the device (K3), 600x600 @ 5 cm
+        m = ctx.map(0.05, 100, 600, 600)
+        m.construct([ctx.scan(scene.ray_cast(world, p, ang), ang) for p in poses], poses, bp)
+        cells, _, _ = m.download()
+        g = m.geometry()
+        return cells, g["min_x"], g["min_y"], 0.05
+
+    maps, cands = scene.loop_problem(world, build, n_maps=32, nodes_per_map=16, n_beams=1081, seed=5,
+                                     perturb=(2.0, 0.4), arc_scans=10)
+    P, cost = abi.RtcsmParams(*LOOP_PARAMS), abi.CostGEParams(*COST)
+    fn = loopbatch.hip_detect_fn(ctx, maps, cands, P, cost, 0.6)
+    for _ in range(args.warmup):
+        loopbatch.run_sharded(cands, fn, D.rank, D.world, D.d, D.device())
+    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
+    ctx.reset_stats()
+    D.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rec = loopbatch.run_sharded(cands, fn, D.rank, D.world, D.d, D.device())
+    elapsed = D.max(time.perf_counter() - t0)
+    stats = ctx.kernel_stats()
+    ctx.set_option(abi.LGS_OPT_PROFILE, 0)
+    found = len(loopbatch.loop_results(rec))
+    cpu = None
+    if D.rank == 0 and not args.no_cpu and D.world == 1:
+        ob = oracle_lib()
+        grids = {}
+        prm, oc = ob.RtcsmParams(*LOOP_PARAMS), ob.CostGE(*COST)
+
+        def one(i):
+            c = cands[i]
+            if c.query not in grids:
+                m = maps[c.query]
+                grids[c.query] = (ob.OGrid(m.cells, m.min_x, m.min_y, 0.05),
+                                  ob.OGrid(ob.precompute(m.cells, 5), m.min_x, m.min_y, 0.05))
+            g, cg = grids[c.query]
+            s = ob.Summary()
+            ob.lib().orc_rtcsm_optimize_pose(C.byref(g.g), C.byref(cg.g), C.byref(prm), C.byref(oc),
+                                             C.byref(ob.OScan(c.ranges, c.angles).s), ob.Pose(*c.pose), 0.6,
+                                             C.byref(s))
+        rate, times = timed(args.cpu_seconds, range(0, len(cands), 37), one)
+        cpu = dict(value=round(rate, 4), unit="candidates/s", cores=1, kind="port",
+                   sample=f"{len(times)} config-5 candidates through the oracle's OptimizePose "
+                          f"(coarse map precomputed per map, as LocalMapInfo caches it; 1 thread), "
+                          f"p50 {1e3 * np.median(times):.1f} ms")
+    value = args.steps * len(cands) / elapsed
+    line = dict(
+        metric="loop-closure candidates/sec, 512 candidates (32 maps x 16 nodes), 1081 beams, +-2.5 m/+-0.5 rad",
+        value=round(value, 2), unit="candidates/s", n_gpus=D.world, steps=args.steps, warmup=args.warmup,
+        ms_per_step=round(1e3 * elapsed / args.steps, 4), higher_is_better=True, scaling="strong",
+        vs_baseline=None, dtype="f64", data="synthetic: 32 device-built local maps (600x600 @ 5 cm), 512 scans",
+        config=dict(workload="config5: LoopDetectorRealTimeCorrelative::Detect batch", candidates=len(cands),
+                    found=found, parallelism=f"candidates sharded in contiguous blocks over {D.world} ranks + "
+                                             "RCCL all-gather of 176-B result records"),
+        roofline=roofline_from(stats, "k_coarse", args.pmc), cpu_baseline=cpu)
+    return line, stats, value
+
+
+# -------------------------------------------------------------------- stream
+def run_stream(args, D, ctx):
+    """Config 4: odometry-driven frontend over a circular trajectory (0.1 m,
+    0.02 rad per scan, odometry noise sigma (0.01 m, 0.005 rad), seed 7)."""
+    world = scene.make_world()
+    ang = scene.beam_angles(1081)
+    rng = np.random.default_rng(7 + D.rank)
+    n = args.warmup + args.steps + 1
+    truths = [(5.0 * np.cos(0.02 * k), 5.0 * np.sin(0.02 * k), 0.02 * k + np.pi / 2) for k in range(n)]
+    ranges = [scene.ray_cast(world, t, ang) for t in truths]
+    bp = abi.BuilderParams(*BUILDER)
+    P, cost = abi.RtcsmParams(5, 0.2, 0.2, 0.5, 20.0), abi.CostGEParams(*COST)   # JSON frontend window
+    local = ctx.map(0.05, 100, 200, 200, center=truths[0][:2])
+    latest = ctx.map(0.05, 100, 200, 200, center=truths[0][:2])
+    dscans = [ctx.scan(r, ang) for r in ranges]
+    est = [truths[0]]
+    local.update_scan(dscans[0], est[0], bp)
+
+    def step(k):
+        # odometry: the true relative motion + noise, composed onto the last estimate
+        d = (0.1 + rng.normal(0, 0.01), rng.normal(0, 0.01), 0.02 + rng.normal(0, 0.005))
+        c, s = np.cos(est[-1][2]), np.sin(est[-1][2])
+        guess = (est[-1][0] + c * d[0] - s * d[1], est[-1][1] + s * d[0] + c * d[1], est[-1][2] + d[2])
+        lo = max(0, k - 10)
+        latest.construct(dscans[lo:k], est[lo:k], bp)                       # UpdateLatestMap (10 scans)
+        out = ctx.optimize_pose_query(latest.grid(), P, cost, dscans[k], guess)
+        e = out.estimated_pose
+        est.append((e.x, e.y, e.theta))
+        local.update_scan(dscans[k], est[-1], bp)                           # UpdateGridMap insert
+
+    for k in range(1, args.warmup + 1):
+        step(k)
+    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
+    ctx.reset_stats()
+    D.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.warmup + 1, n):
+        step(k)
+    elapsed = D.max(time.perf_counter() - t0)
+    stats = ctx.kernel_stats()
+    ctx.set_option(abi.LGS_OPT_PROFILE, 0)
+    steps = n - args.warmup - 1
+    drift = max(abs(est[-1][0] - truths[len(est) - 1][0]), abs(est[-1][1] - truths[len(est) - 1][1]))
+    value = steps * D.world / elapsed
+    line = dict(
+        metric="frontend scans/sec: match vs latest map + local-map insert + latest-map rebuild, 1081 beams",
+        value=round(value, 2), unit="scans/s", n_gpus=D.world, steps=steps, warmup=args.warmup,
+        ms_per_step=round(1e3 * elapsed / steps, 4), higher_is_better=True, scaling="weak", vs_baseline=None,
+        dtype="f64", data="synthetic circular trajectory, odometry noise (0.01 m, 0.005 rad)",
+        config=dict(workload="config4: streaming frontend (JSON window 0.2/0.2/0.5)", beams=1081,
+                    latest_map_scans=10, parallelism=f"replicas x{D.world}"),
+        final_drift_m=round(float(drift), 4),
+        roofline=roofline_from(stats, "k_ray_apply", args.pmc), cpu_baseline=None)
+    return line, stats, value
+
+
+def main():
+    args = parse()
+    D = Dist()
+    ctx = abi.Context(D.local)
+    line, stats, _ = dict(match=run_match, refine=run_refine, loop=run_loop, stream=run_stream)[args.workload](
+        args, D, ctx)
+    line["kernels"] = {k: dict(launches=v["launches"], avg_ms=round(v["total_ms"] / max(1, v["launches"]), 5))
+                       for k, v in stats.items()}
+    if D.rank == 0:
+        print(json.dumps(line), flush=True)
+    D.close()
 
 
 if __name__ == "__main__":

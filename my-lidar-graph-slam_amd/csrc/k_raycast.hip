@@ -118,7 +118,16 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
     if (bad) atomicAdd(outside, 1);
 }
 
-// One thread per run of equal cells in the sorted keys.
+// One thread per run of equal cells in the sorted keys.  The run is walked in
+// batches of 8 keys loaded together (one memory latency per batch instead of
+// per key).  BinaryBayesGridCell::Update is applied in order; odds(p) is the
+// same constant the reference recomputes every time, and an update that maps
+// a saturated value onto itself (v == 1e-3 under a miss with odds(pMiss) <= 1,
+// v == 1 - 1e-3 under a hit) is skipped after the kernel has checked on the
+// device that it is an exact fixed point -- long runs (cells next to the
+// sensor) are mostly such updates.
+constexpr int kApplyBatch = 8;
+
 __global__ __launch_bounds__(256) void k_apply(const unsigned long long* __restrict__ keys,
                                                long long n, double* __restrict__ cells,
                                                uint32_t* __restrict__ hits,
@@ -130,18 +139,34 @@ __global__ __launch_bounds__(256) void k_apply(const unsigned long long* __restr
     const unsigned long long k = keys[i];
     const unsigned cell = (unsigned)(k >> 32);
     if (i > 0 && (unsigned)(keys[i - 1] >> 32) == cell) return;
+    const bool miss_fixed = bayes_update(kPMin, p_miss) == kPMin;
+    const bool hit_fixed = bayes_update(kPMax, p_hit) == kPMax;
     double v = cells[cell];
     uint32_t nh = 0, nm = 0;
-    for (long long j = i; j < n; ++j) {
-        const unsigned long long kj = keys[j];
-        if ((unsigned)(kj >> 32) != cell) break;
-        if (kj & 1ull) {
-            v = bayes_update(v, p_hit);
-            ++nh;
+    for (long long j = i;; j += kApplyBatch) {
+        unsigned long long kb[kApplyBatch];
+        if (j + kApplyBatch <= n) {
+#pragma unroll
+            for (int t = 0; t < kApplyBatch; ++t) kb[t] = keys[j + t];
         } else {
-            v = bayes_update(v, p_miss);
-            ++nm;
+#pragma unroll
+            for (int t = 0; t < kApplyBatch; ++t) kb[t] = (j + t < n) ? keys[j + t] : ~0ull;
         }
+        bool end = false;
+#pragma unroll
+        for (int t = 0; t < kApplyBatch; ++t) {
+            if (!end && (unsigned)(kb[t] >> 32) != cell) end = true;
+            if (!end) {
+                if (kb[t] & 1ull) {
+                    if (!(hit_fixed && v == kPMax)) v = bayes_update(v, p_hit);
+                    ++nh;
+                } else {
+                    if (!(miss_fixed && v == kPMin)) v = bayes_update(v, p_miss);
+                    ++nm;
+                }
+            }
+        }
+        if (end) break;
     }
     cells[cell] = v;
     hits[cell] += nh;
