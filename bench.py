@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--coarse-planes", type=int, default=1, help="A/B: 1 phase-plane coarse layout, 0 plain")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
+    ap.add_argument("--timed-events", default="dominant", choices=["dominant", "all", "none"],
+                    help="HIP-event timing inside the timed region: the roofline kernel only (default), "
+                         "every kernel, or none (A/B of the event overhead)")
     a = ap.parse_args()
     d_steps = dict(match=200, refine=200, loop=4, stream=500)[a.workload]
     d_warm = dict(match=10, refine=5, loop=1, stream=10)[a.workload]
@@ -130,6 +133,14 @@ def roofline_from(stats, kernel, pmc_path):
                 avg_launch_ms=round(avg_ms, 5), algo_bytes_per_launch=per_launch)
 
 
+def set_timed_events(ctx, args, dominant):
+    """HIP-event timing during the timed region (LGS_OPT_PROFILE_MASK)."""
+    mask = {"dominant": 1 << abi.KERNEL_IDS.index(dominant), "all": (1 << len(abi.KERNEL_IDS)) - 1,
+            "none": 0}[args.timed_events]
+    ctx.set_option(abi.LGS_OPT_PROFILE_MASK, mask)
+    ctx.reset_stats()
+
+
 def bench_map(world, ang):
     w, h, mx, my = scene.map_geometry(1000, 100, 0.05)
     cells = scene.approx_occupancy_map(world, scene.arc_poses(10), ang, w, h, mx, my, 0.05)
@@ -181,8 +192,7 @@ def run_match(args, D, ctx):
     for k in range(args.warmup):
         s, i = pick(k)
         ctx.optimize_pose_query(grid, P, cost, s, i)
-    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
-    ctx.reset_stats()
+    set_timed_events(ctx, args, "k_coarse")
     results = np.zeros((args.steps, 4))
     lat = []
     D.barrier()
@@ -200,7 +210,16 @@ def run_match(args, D, ctx):
     elapsed = D.max(time.perf_counter() - t0)
     D.barrier()
     stats = ctx.kernel_stats()
+    # per-kernel table from a separate, fully event-timed pass (outside the timed region)
+    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
+    ctx.reset_stats()
+    for k in range(min(50, args.steps)):
+        s, i = pick(args.warmup + k)
+        ctx.optimize_pose_query(grid, P, cost, s, i)
+    all_stats = ctx.kernel_stats()
     ctx.set_option(abi.LGS_OPT_PROFILE, 0)
+    if "k_coarse" not in stats:
+        stats = all_stats
     err = [max(abs(results[k, 0] - truths[(args.warmup + k) % len(truths)][0]),
                abs(results[k, 1] - truths[(args.warmup + k) % len(truths)][1])) for k in range(args.steps)]
     cpu = None
@@ -233,10 +252,10 @@ def run_match(args, D, ctx):
         p50_scan_match_ms=round(float(np.percentile(lat_ms, 50)), 4),
         p90_scan_match_ms=round(float(np.percentile(lat_ms, 90)), 4),
         roofline=roofline_from(stats, "k_coarse", args.pmc), cpu_baseline=cpu,
-        pose_err_max_m=round(float(max(err)), 4))
+        pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events)
     if cpu:
         cpu["speedup"] = round(value / cpu["value"], 1)
-    return line, stats, value
+    return line, all_stats, value
 
 
 # -------------------------------------------------------------------- refine
@@ -251,8 +270,7 @@ def run_refine(args, D, ctx):
     lp = abi.LinsolveParams(*LINSOLVE)
     for k in range(args.warmup):
         ctx.linsolve(grid, lp, dscans[k % len(dscans)], inits[k % len(dscans)])
-    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
-    ctx.reset_stats()
+    set_timed_events(ctx, args, "k_linsolve")
     lat = []
     D.barrier()
     t0 = time.perf_counter()
@@ -320,8 +338,7 @@ def run_loop(args, D, ctx):
     fn = loopbatch.hip_detect_fn(ctx, maps, cands, P, cost, 0.6)
     for _ in range(args.warmup):
         loopbatch.run_sharded(cands, fn, D.rank, D.world, D.d, D.device())
-    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
-    ctx.reset_stats()
+    set_timed_events(ctx, args, "k_coarse")
     D.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -397,8 +414,7 @@ def run_stream(args, D, ctx):
 
     for k in range(1, args.warmup + 1):
         step(k)
-    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
-    ctx.reset_stats()
+    set_timed_events(ctx, args, "k_ray_apply")
     D.barrier()
     t0 = time.perf_counter()
     for k in range(args.warmup + 1, n):

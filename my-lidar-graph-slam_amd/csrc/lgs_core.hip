@@ -58,7 +58,7 @@ const char* const kKernelNames[K_NUM_KERNELS] = { "k_project", "k_coarse", "k_se
 
 int lgs_ctx::timing_begin(int kernel, double algo_bytes)
 {
-    if (!profile) return -1;
+    if (!profile || !((profile_mask >> kernel) & 1u)) return -1;
     hipEvent_t ev[2];
     for (int i = 0; i < 2; ++i) {
         if (!event_pool.empty()) {
@@ -209,7 +209,14 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_GUARD_EPS: ctx->guard_eps = value; return LGS_OK;
     case LGS_OPT_FORCE_DENSE: ctx->force_dense = value != 0.0; return LGS_OK;
     case LGS_OPT_INJECT_INDEX: ctx->inject_index = value != 0.0; return LGS_OK;
-    case LGS_OPT_PROFILE: ctx->profile = value != 0.0; return LGS_OK;
+    case LGS_OPT_PROFILE:
+        ctx->profile = value != 0.0;
+        ctx->profile_mask = ~0u;
+        return LGS_OK;
+    case LGS_OPT_PROFILE_MASK:
+        ctx->profile_mask = (unsigned)value;
+        ctx->profile = ctx->profile_mask != 0;
+        return LGS_OK;
     case LGS_OPT_COARSE_PLANES: ctx->coarse_planes = value != 0.0; return LGS_OK;
     case LGS_OPT_GUARD_CAP:
         ctx->guard_cap = (int)value;

@@ -146,6 +146,7 @@ struct lgs_ctx {
     double* zero = nullptr;      // 32 zero doubles: target of out-of-map gathers
     // profiling (LGS_OPT_PROFILE)
     bool profile = false;
+    unsigned profile_mask = ~0u;  // kernels (KernelId bits) timed while profile is on
     std::vector<lgs::PendingTiming> pending;
     std::vector<hipEvent_t> event_pool;
     int64_t stat_launches[lgs::K_NUM_KERNELS] = {};
