@@ -143,6 +143,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_PROFILE       5   /* 1 = time every kernel launch with HIP events on the ctx stream */
 #define LGS_OPT_COARSE_PLANES 6   /* 1 (default) = phase-plane coarse layout, 0 = plain layout (A/B) */
 #define LGS_OPT_PROFILE_MASK  7   /* time only the kernels whose lgs_kernel_stat index bit is set (0 = off) */
+#define LGS_OPT_SPIN_SYNC     8   /* 1 (default) = spin on the stream when waiting for results, 0 = blocking wait */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is

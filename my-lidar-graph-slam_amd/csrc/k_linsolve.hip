@@ -554,7 +554,7 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     LGS_HIP_CHECK(hipGetLastError());
     LGS_HIP_CHECK(hipMemcpyAsync(h + b_refs, d + b_refs, b_rec + b_traj, hipMemcpyDeviceToHost,
                                  ctx->stream));
-    LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->sync();
     if (ctx->profile) ctx->harvest();
     const LsRecord* rec = (const LsRecord*)(h + b_refs);
     for (int j = 0; j < n; ++j) {
@@ -624,7 +624,7 @@ extern "C" int lgs_cost_square_error(lgs_ctx* ctx, const lgs_grid* grid, double 
         hipLaunchKernelGGL(k_sq_cost, dim3(1), dim3(kLsThreads), 0, ctx->stream, p, grid->d, r, d);
         LGS_HIP_CHECK(hipGetLastError());
         LGS_HIP_CHECK(hipMemcpyAsync(h, d, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->sync();
         *out_cost = h[0];
         if (out_cov) {
             for (int a = 0; a < 3; ++a)

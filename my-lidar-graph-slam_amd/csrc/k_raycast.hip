@@ -378,7 +378,7 @@ void raycast(lgs_map* m, const std::vector<ScanHits>& scans, const lgs_builder_p
     LGS_HIP_CHECK(hipGetLastError());
     int bad = 0;
     LGS_HIP_CHECK(hipMemcpyAsync(pin, d_bad, sizeof(int), hipMemcpyDeviceToHost, st));
-    LGS_HIP_CHECK(hipStreamSynchronize(st));
+    ctx->sync();
     if (ctx->profile) ctx->harvest();
     std::memcpy(&bad, pin, sizeof(int));
     if (bad) throw Error(LGS_ERR_INTERNAL, "ray cell outside the map geometry");

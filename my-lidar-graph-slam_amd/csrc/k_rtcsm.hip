@@ -16,7 +16,9 @@
 //               reads can land inside).
 //   k_seed      lower bound L = fine max of the best safe coarse block.
 //   k_select    blocks that can influence the reference's result:
-//               (c > thr) && (unsafe || c >= L)  -> ordered list (hipcub).
+//               (c > thr) && (unsafe || c >= L)  -> ordered list, compacted per
+//               1024-block segment (ballot + LDS prefix); consumers rebuild the
+//               segment prefix in LDS, so no separate scan pass is needed.
 //   k_fine      EvaluateHighResolutionMap (:227-256) for listed blocks: block
 //               max and its first position in the reference's (x, y) order.
 //   k_replay    the reference's acceptance rule `c > s && f > s` replayed in
@@ -27,8 +29,6 @@
 //               central-difference neighbours (C/mapping/cost_function_greedy_endpoint.cpp:32-171).
 #include "lgs_internal.hpp"
 
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <cfloat>
 #include <cstring>
@@ -37,11 +37,28 @@
 using namespace lgs;
 
 namespace lgs {
-void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out);
+void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, const PlaneGeom* planes);
+bool precompute_planes_ok(const lgs_grid* in, int win);
 }
 
 namespace {
 
+
+constexpr int kPipe = 16;   // seq_sum gathers in flight per batch (index arrays padded by 2*kPipe)
+
+// Generation-tagged counter (gen << 32 | count): a word left by an earlier
+// match counts as zero, so records need no memset.  Returns this caller's slot.
+__device__ __forceinline__ int tagged_slot(unsigned long long* w, unsigned gen)
+{
+    unsigned long long cur = *(volatile unsigned long long*)w, assumed;
+    unsigned cnt;
+    do {
+        assumed = cur;
+        cnt = ((unsigned)(assumed >> 32) == gen) ? (unsigned)assumed : 0u;
+        cur = atomicCAS(w, assumed, ((unsigned long long)gen << 32) | (unsigned long long)(cnt + 1u));
+    } while (cur != assumed);
+    return (int)cnt;
+}
 
 __device__ __forceinline__ bool near_boundary(double q, double eps)
 {
@@ -55,30 +72,66 @@ __device__ __forceinline__ bool near_boundary(double q, double eps)
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int floor_div(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 
-// Per (angle, beam) addressing of the coarse stage in the phase-plane layout
-// (see k_decimate): the beam's lattice starts at bx = ix - winX, by = iy - winY,
-// which lies in plane (bx mod lr, by mod lr) at (floor(bx/lr), floor(by/lr)).
-__device__ __forceinline__ int4 coarse_info(int ix, int iy, int win_x, int win_y, int lr, int Wq,
-                                            int Hq)
+// Per (angle, beam) base offset of the coarse stage in the padded phase-plane
+// layout (see k_decimate): the beam's lattice starts at bx = ix - winX,
+// by = iy - winY, in plane (bx mod lr, by mod lr) at (floor(bx/lr),
+// floor(by/lr)).  If its ncx x ncy window touches the map, the window lies
+// inside the M-wide zero margins (M >= ncx, ncy) and the base is direct;
+// otherwise every read is 0.0 (GridMap::Value out of bounds) and the base
+// points at the all-zero top-left margin of plane 0.  The coarse lanes then
+// read base + jy * Wqp + jx with no bounds test.
+__device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
 {
-    const int bx = ix - win_x, by = iy - win_y;
+    const int lr = pl.low_res;
+    const int bx = ix - pl.win_x, by = iy - pl.win_y;
     const int qx0 = floor_div(bx, lr), qy0 = floor_div(by, lr);
     const int rx = bx - lr * qx0, ry = by - lr * qy0;
-    return make_int4(qx0, qy0, (ry * lr + rx) * Wq * Hq, rx | (ry << 16));
+    const bool touches = (qx0 < pl.Wq) & (qx0 + pl.ncx > 0) & (qy0 < pl.Hq) & (qy0 + pl.ncy > 0);
+    return touches ? (int)((ry * lr + rx) * pl.pstride + (long long)(qy0 + pl.M) * pl.Wqp + (qx0 + pl.M)) : 0;
 }
 
+// blockDim == 256.  ComputeScanIndices keeps the beams with range <
+// ScanRangeMax, in beam order (:192-193); each block finds its 256 valid
+// beams v0..v0+255 with a block-wide prefix count over the scan (no host
+// upload of the compaction).
 __global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __restrict__ ranges,
                                                  const double* __restrict__ angles,
-                                                 const int* __restrict__ vidx,
-                                                 int2* __restrict__ idx, int4* __restrict__ cinfo,
-                                                 int Wq, int Hq, int* __restrict__ tedge, int gen,
+                                                 int2* __restrict__ idx, int* __restrict__ cbase,
+                                                 int* __restrict__ tedge, int gen,
                                                  RtcsmRecord* rec, int guard_cap, double guard_eps,
                                                  int inject)
 {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ int s_map[256];
+    __shared__ int s_wsum[4];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int v0 = blockIdx.x * 256;
+    const int chunk = (pl.N + 255) / 256;
+    const int lo = min(tid * chunk, pl.N), hi = min(lo + chunk, pl.N);
+    int nvalid = 0;
+    for (int i = lo; i < hi; ++i) nvalid += !(ranges[i] >= pl.rmax);
+    int incl = nvalid;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
+    }
+    if (lane == 63) s_wsum[wid] = incl;
+    __syncthreads();
+    int pos = incl - nvalid;
+    for (int j = 0; j < wid; ++j) pos += s_wsum[j];
+    for (int i = lo; i < hi; ++i)
+        if (!(ranges[i] >= pl.rmax)) {
+            const int r = pos - v0;
+            if (r >= 0 && r < 256) s_map[r] = i;
+            ++pos;
+        }
+    __syncthreads();
+    const int v = v0 + tid;
     const int tt = blockIdx.y;
+    // seq_sum's look-ahead reads up to 2*kPipe entries past the last row:
+    // keep them at the zero margin (base 0)
+    if (blockIdx.x == 0 && tt == 0 && tid < 2 * kPipe) cbase[(size_t)pl.T * pl.Nv + tid] = 0;
     if (v >= pl.Nv) return;
-    const int i = vidx[v];
+    const int i = s_map[tid];
     const double r = ranges[i];
     const double a = angles[i];
     const int t = tt - pl.win_t;
@@ -94,7 +147,7 @@ __global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __r
     int ix = (int)floor(qx);
     int iy = (int)floor(qy);
     if (near_boundary(qx, guard_eps) || near_boundary(qy, guard_eps)) {
-        const int slot = atomicAdd(&rec->guard_count, 1);
+        const int slot = tagged_slot(&rec->guard_word, (unsigned)gen);
         if (slot < guard_cap) {
             GuardRec g;
             g.t = tt;
@@ -107,14 +160,14 @@ __global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __r
     }
     const size_t o = (size_t)tt * pl.Nv + v;
     idx[o] = make_int2(ix, iy);
-    cinfo[o] = coarse_info(ix, iy, pl.win_x, pl.win_y, pl.low_res, Wq, Hq);
+    cbase[o] = coarse_base(ix, iy, pl);
     // this angle has a beam whose coarse lattice starts left of / below the
     // map: k_coarse must run its unsafe-block check (generation-stamped flag)
     if (ix - pl.win_x < 0 || iy - pl.win_y < 0) tedge[tt] = gen;
 }
 
-__global__ void k_patch(RtcsmPlan pl, int2* __restrict__ idx, int4* __restrict__ cinfo, int Wq,
-                        int Hq, int* __restrict__ tedge, int gen, const int4* __restrict__ patches,
+__global__ void k_patch(RtcsmPlan pl, int2* __restrict__ idx, int* __restrict__ cbase,
+                        int* __restrict__ tedge, int gen, const int4* __restrict__ patches,
                         int n)
 {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -122,18 +175,19 @@ __global__ void k_patch(RtcsmPlan pl, int2* __restrict__ idx, int4* __restrict__
     const int4 p = patches[k];
     const size_t o = (size_t)p.x * pl.Nv + p.y;
     idx[o] = make_int2(p.z, p.w);
-    cinfo[o] = coarse_info(p.z, p.w, pl.win_x, pl.win_y, pl.low_res, Wq, Hq);
+    cbase[o] = coarse_base(p.z, p.w, pl);
     if (p.z - pl.win_x < 0 || p.w - pl.win_y < 0) tedge[p.x] = gen;
 }
 
 // full host projection -> coarse info
-__global__ void k_cinfo(RtcsmPlan pl, const int2* __restrict__ idx, int4* __restrict__ cinfo,
-                        int Wq, int Hq, int* __restrict__ tedge, int gen)
+__global__ void k_cinfo(RtcsmPlan pl, const int2* __restrict__ idx, int* __restrict__ cbase,
+                        int* __restrict__ tedge, int gen)
 {
     const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o < 2 * kPipe) cbase[(size_t)pl.T * pl.Nv + o] = 0;
     if (o >= (size_t)pl.T * pl.Nv) return;
     const int2 q = idx[o];
-    cinfo[o] = coarse_info(q.x, q.y, pl.win_x, pl.win_y, pl.low_res, Wq, Hq);
+    cbase[o] = coarse_base(q.x, q.y, pl);
     if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0) tedge[o / pl.Nv] = gen;
 }
 
@@ -193,8 +247,11 @@ __device__ void block_argmax(double& v, long long& k, double* sv, long long* sk)
 // (consecutive jx) gather consecutive doubles.  Cells past the map are 0.0,
 // exactly what GridMap::Value returns out of bounds.
 // --------------------------------------------------------------------------
+// Writes the interior of the padded planes only (the margins are zeroed once
+// per buffer and layout, planes_buffer).
 __global__ __launch_bounds__(256) void k_decimate(const double* __restrict__ C, int W, int H, int lr,
-                                                  int Wq, int Hq, double* __restrict__ D)
+                                                  int Wq, int M, int Wqp, long long pstride,
+                                                  double* __restrict__ D)
 {
     const int qx = blockIdx.x * blockDim.x + threadIdx.x;
     const int qy = blockIdx.y;
@@ -203,7 +260,7 @@ __global__ __launch_bounds__(256) void k_decimate(const double* __restrict__ C, 
     const int rx = plane % lr, ry = plane / lr;
     const int x = lr * qx + rx, y = lr * qy + ry;
     const double v = (x < W && y < H) ? C[(size_t)y * W + x] : 0.0;
-    D[((size_t)plane * Hq + qy) * Wq + qx] = v;
+    D[plane * pstride + (long long)(qy + M) * Wqp + qx + M] = v;
 }
 
 // --------------------------------------------------------------------------
@@ -213,7 +270,6 @@ __global__ __launch_bounds__(256) void k_decimate(const double* __restrict__ C, 
 // reference's order, :217-221) runs.  load(v) issues one gather; beam
 // indices are wave-uniform (scalar loads).
 // --------------------------------------------------------------------------
-constexpr int kPipe = 16;
 
 // load(v) must be safe for v < n + 2*kPipe (index arrays are padded) and must
 // not branch: out-of-map lanes read a zero cell.  Adding 0.0 to the running
@@ -270,8 +326,8 @@ __device__ __forceinline__ double seq_sum(int n, Fetch fetch, Addr addr)
 // --------------------------------------------------------------------------
 template <int PLANES>
 __global__ __launch_bounds__(1024) void k_coarse(
-    RtcsmPlan pl, const double* __restrict__ cmap, int Wq, int Hq, const int2* __restrict__ idx,
-    const int4* __restrict__ cinfo, const double* __restrict__ zero,
+    RtcsmPlan pl, const double* __restrict__ cmap, const int2* __restrict__ idx,
+    const int* __restrict__ cbase, const double* __restrict__ zero,
     const int* __restrict__ tedge, int gen, double* __restrict__ cscore,
     uint8_t* __restrict__ cflag, double* __restrict__ part_c, long long* __restrict__ part_k)
 {
@@ -286,16 +342,12 @@ __global__ __launch_bounds__(1024) void k_coarse(
     const int W = pl.W, H = pl.H;
     const size_t o = (size_t)tt * pl.Nv;
     const int2* __restrict__ id = idx + o;
-    const int4* __restrict__ ci = cinfo + o;
+    const int* __restrict__ cb = cbase + o;
 
     double sum;
     if (PLANES) {
-        sum = seq_sum<int4>(pl.Nv, [&](int v) { return ci[v]; }, [&](const int4& c) {
-            const int qx = c.x + jx, qy = c.y + jy;
-            const bool inb = ((unsigned)qx < (unsigned)Wq) & ((unsigned)qy < (unsigned)Hq);
-            const unsigned off = (unsigned)(c.z + qy * Wq + qx);
-            return inb ? cmap + off : zero;
-        });
+        const double* __restrict__ lane_base = cmap + (jy * pl.Wqp + jx);
+        sum = seq_sum<int>(pl.Nv, [&](int v) { return cb[v]; }, [&](const int& c) { return lane_base + c; });
     } else {
         const int xc = -pl.win_x + jx * lr, yc = -pl.win_y + jy * lr;
         sum = seq_sum<int2>(pl.Nv, [&](int v) { return id[v]; }, [&](const int2& q) {
@@ -397,13 +449,13 @@ __device__ void eval_block(const RtcsmPlan& pl, const double* __restrict__ grid,
 // Ties resolve to the smallest reference order index o = xo*LR + yo.
 constexpr int kMaxChunks = 32;   // transposed evaluator handles Nv <= 2048
 
-// compile-time loop C = 0, 2, 4, ... < MAXC; f returns false to stop
-template <int C, int MAXC, class F>
-__device__ __forceinline__ void static_for_step2(F&& f)
+// compile-time loop C = 0, STEP, 2*STEP, ... < MAXC; f returns false to stop
+template <int C, int MAXC, int STEP, class F>
+__device__ __forceinline__ void static_for_step(F&& f)
 {
     if constexpr (C < MAXC) {
         if (!f(std::integral_constant<int, C>{})) return;
-        static_for_step2<C + 2, MAXC>(f);
+        static_for_step<C + STEP, MAXC, STEP>(f);
     }
 }
 
@@ -429,6 +481,7 @@ __device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ gri
     for (int v = threadIdx.x; v < Nv; v += blockDim.x) sidx[v] = id[v];
     __syncthreads();
 
+    constexpr int kDepth = 2;   // measured: depth 4 made k_fine slower (36 vs 27 us)
     double ra[LR], rb[LR];
     auto gather = [&](int c, double (&r)[LR]) {
         const int b = c * 64 + lane;
@@ -464,28 +517,30 @@ __device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ gri
             acc = s;
         }
     };
-    // Ping-pong, fully unrolled over at most kMaxChunks chunks: without a
-    // loop header there are no phi copies of in-flight registers, so each
-    // store waits only for the older batch; sched_barrier keeps each batch's
-    // gathers contiguous and in program order.
+    // kDepth chunks of gathers in flight ahead of the adds (alternating register
+    // sets), fully unrolled over at most kMaxChunks chunks: without a loop
+    // header there are no phi copies of in-flight registers, so each store
+    // waits only for the oldest batch; sched_barrier keeps each batch's
+    // gathers contiguous and in program order.  The in-order LDS of a wave
+    // makes two row buffers enough (a store never overtakes the previous
+    // chunk's reads).
     gather(0, ra);
     __builtin_amdgcn_sched_barrier(0);
     gather(1, rb);
     __builtin_amdgcn_sched_barrier(0);
-    static_for_step2<0, kMaxChunks>([&](auto cc) {
+    auto stage = [&](int c, double (&r)[LR], double* buf) {
+        store(r, buf);
+        __builtin_amdgcn_sched_barrier(0);
+        gather(c + kDepth, r);
+        __builtin_amdgcn_sched_barrier(0);
+        add_chunk(c, buf);
+    };
+    static_for_step<0, kMaxChunks, kDepth>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
         if (c >= nchunk) return false;
-        store(ra, bufs);
-        __builtin_amdgcn_sched_barrier(0);
-        gather(c + 2, ra);
-        __builtin_amdgcn_sched_barrier(0);
-        add_chunk(c, bufs);
+        stage(c, ra, bufs);
         if (c + 1 >= nchunk) return false;
-        store(rb, bufs + LR * LD);
-        __builtin_amdgcn_sched_barrier(0);
-        gather(c + 3, rb);
-        __builtin_amdgcn_sched_barrier(0);
-        add_chunk(c + 1, bufs + LR * LD);
+        stage(c + 1, rb, bufs + LR * LD);
         return true;
     });
     double bv = -1.0;
@@ -543,35 +598,105 @@ __global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_seed(
     if (threadIdx.x == 0) *Lout = f;
 }
 
-__global__ void k_select(RtcsmPlan pl, const double* __restrict__ cscore,
-                         const uint8_t* __restrict__ cflag, const double* __restrict__ Lp,
-                         uint8_t* __restrict__ sel)
+// k_select: one workgroup per segment of kSelSeg consecutive blocks.  The
+// selected blocks of a segment are written in block order to
+// list[seg * kSelSeg + rank] (wave ballots + an LDS prefix over the 16
+// waves) and their number to segcnt[seg]; consumers rebuild the exclusive
+// prefix over segments in LDS (seg_prefix), which gives every selected block
+// its position in the reference's block order.
+constexpr int kSelSeg = 1024;
+
+__global__ __launch_bounds__(kSelSeg) void k_select(RtcsmPlan pl, const double* __restrict__ cscore,
+                                                   const uint8_t* __restrict__ cflag,
+                                                   const double* __restrict__ Lp, int* __restrict__ list,
+                                                   int* __restrict__ segcnt)
 {
-    const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= pl.K) return;
-    const double L = *Lp;
-    const double c = cscore[k];
-    sel[k] = (c > pl.thr) && (cflag[k] || c >= L) ? 1 : 0;
+    __shared__ int s_w[kSelSeg / 64];
+    const long long k = (long long)blockIdx.x * kSelSeg + threadIdx.x;
+    bool f = false;
+    if (k < pl.K) {
+        const double L = *Lp;
+        const double c = cscore[k];
+        f = (c > pl.thr) && (cflag[k] || c >= L);
+    }
+    const unsigned long long bal = __ballot(f);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) s_w[wid] = __popcll(bal);
+    __syncthreads();
+    int off = 0;
+    for (int j = 0; j < wid; ++j) off += s_w[j];
+    if (f) list[(size_t)blockIdx.x * kSelSeg + off + __popcll(bal & ((1ull << lane) - 1ull))] = (int)k;
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int j = 0; j < kSelSeg / 64; ++j) t += s_w[j];
+        segcnt[blockIdx.x] = t;
+    }
 }
 
-// k_fine: one workgroup per listed block (grid-stride); LR as in k_seed.
+// pref[0..nseg] = exclusive prefix of segcnt, built in LDS by the whole
+// workgroup (chunk per thread, wave scans, one LDS pass over the waves).
+// ws: >= 16 ints of LDS scratch.  Ends with a barrier.
+__device__ void seg_prefix(const int* __restrict__ segcnt, int nseg, int* pref, int* ws)
+{
+    const int nt = blockDim.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int chunk = (nseg + nt - 1) / nt;
+    const int lo = min(tid * chunk, nseg), hi = min(lo + chunk, nseg);
+    int c = 0;
+    for (int i = lo; i < hi; ++i) c += segcnt[i];
+    int incl = c;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
+    }
+    const int last = min(63, nt - 1 - wid * 64);
+    if (lane == last) ws[wid] = incl;
+    __syncthreads();
+    int run = incl - c;
+    for (int j = 0; j < wid; ++j) run += ws[j];
+    for (int i = lo; i < hi; ++i) {
+        pref[i] = run;
+        run += segcnt[i];
+    }
+    if (tid == nt - 1) pref[nseg] = run;
+    __syncthreads();
+}
+
+// segment holding dense position b: pref[lo] <= b < pref[lo + 1]
+__device__ __forceinline__ int seg_of(const int* pref, int nseg, int b)
+{
+    int lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pref[mid] <= b) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// k_fine: the listed blocks, dense position b = blockIdx.x, +gridDim.x, ...
+// (LR as in k_seed).  fval/fpos are indexed by dense position.
 template <int LR>
 __global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_fine(
     RtcsmPlan pl, const double* __restrict__ grid, const int2* __restrict__ idx,
-    const double* __restrict__ zero, const int* __restrict__ list, const int* __restrict__ count,
-    double* __restrict__ fval, int* __restrict__ fpos)
+    const double* __restrict__ zero, const int* __restrict__ list, const int* __restrict__ segcnt,
+    int nseg, unsigned eval_smem, double* __restrict__ fval, int* __restrict__ fpos)
 {
     extern __shared__ char smem[];
     __shared__ double sv[16];
     __shared__ long long sk[16];
-    const int n = *count;
+    __shared__ int ws[16];
+    int* pref = (int*)(smem + eval_smem);
+    seg_prefix(segcnt, nseg, pref, ws);
+    const int n = pref[nseg];
     for (int b = blockIdx.x; b < n; b += gridDim.x) {
+        const int sg = seg_of(pref, nseg, b);
+        const long long k = list[(size_t)sg * kSelSeg + (b - pref[sg])];
         double f;
         int pos;
         if constexpr (LR > 0)
-            eval_block_t<LR>(pl, grid, idx, zero, list[b], smem, sv, sk, f, pos);
+            eval_block_t<LR>(pl, grid, idx, zero, k, smem, sv, sk, f, pos);
         else
-            eval_block(pl, grid, idx, zero, list[b], (int2*)smem, f, pos);
+            eval_block(pl, grid, idx, zero, k, (int2*)smem, f, pos);
         if (threadIdx.x == 0) {
             fval[b] = f;
             fpos[b] = pos;
@@ -579,37 +704,67 @@ __global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_fine(
     }
 }
 
-// k_replay: the reference's sequential acceptance over the ordered list
-// (:98-114 with the strict update of :246), then the 7 cost poses.
-__global__ void k_replay(RtcsmPlan pl, const double* __restrict__ cscore,
-                         const uint8_t* __restrict__ cflag, const int* __restrict__ list,
-                         const int* __restrict__ count, const double* __restrict__ fval,
-                         const int* __restrict__ fpos, const double* __restrict__ Lp,
-                         RtcsmRecord* rec, double* __restrict__ poses7)
+// k_replay (one wave): the reference's sequential acceptance (:98-114 with the
+// strict update of :246) over the selected blocks in block order.  Lanes load
+// 64 consecutive entries at once; the acceptance itself walks them in lane
+// order with wave-uniform shuffles.  Then the 7 cost poses.
+__global__ __launch_bounds__(64) void k_replay(RtcsmPlan pl, const double* __restrict__ cscore,
+                                               const uint8_t* __restrict__ cflag,
+                                               const int* __restrict__ list,
+                                               const int* __restrict__ segcnt, int nseg,
+                                               const double* __restrict__ fval,
+                                               const int* __restrict__ fpos,
+                                               const double* __restrict__ Lp, RtcsmRecord* rec,
+                                               double* __restrict__ poses7)
 {
-    if (threadIdx.x != 0) return;
-    const int n = *count;
+    extern __shared__ int pref[];   // nseg + 1
+    __shared__ int ws[16];
+    seg_prefix(segcnt, nseg, pref, ws);
+    const int n = pref[nseg];
     const double L = *Lp;
+    const int lane = threadIdx.x;
     double s = pl.thr;
-    int bx = -pl.win_x, by = -pl.win_y, bt = -pl.win_t;
-    int status = 0;
-    for (int b = 0; b < n; ++b) {
-        const long long k = list[b];
-        const double c = cscore[k];
-        const double f = fval[b];
-        if (cflag[k] && c < L && f >= L) status |= REC_DANGEROUS;
-        if (c > s && f > s) {
-            s = f;
-            const int tt = (int)(k / pl.P);
-            const int rem = (int)(k % pl.P);
-            const int jx = rem / pl.ncy, jy = rem % pl.ncy;
-            const int o = fpos[b];
-            bx = -pl.win_x + jx * pl.low_res + o / pl.low_res;
-            by = -pl.win_y + jy * pl.low_res + o % pl.low_res;
-            bt = tt - pl.win_t;
+    long long bestk = -1;
+    int bestpos = 0;
+    bool dangerous = false;
+    for (int b0 = 0; b0 < n; b0 += 64) {
+        const int b = b0 + lane;
+        double c = -INFINITY, f = -INFINITY;
+        long long k = -1;
+        int pos = 0;
+        if (b < n) {
+            const int sg = seg_of(pref, nseg, b);
+            k = list[(size_t)sg * kSelSeg + (b - pref[sg])];
+            c = cscore[k];
+            f = fval[b];
+            pos = fpos[b];
+            if (cflag[k] && c < L && f >= L) dangerous = true;
+        }
+        const int cnt = min(64, n - b0);
+        for (int j = 0; j < cnt; ++j) {
+            const double cj = __shfl(c, j, 64);
+            const double fj = __shfl(f, j, 64);
+            const long long kj = __shfl(k, j, 64);
+            const int pj = __shfl(pos, j, 64);
+            if (cj > s && fj > s) {
+                s = fj;
+                bestk = kj;
+                bestpos = pj;
+            }
         }
     }
-    rec->status = status;
+    dangerous = __ballot(dangerous) != 0ull;
+    if (lane != 0) return;
+    int bx = -pl.win_x, by = -pl.win_y, bt = -pl.win_t;
+    if (bestk >= 0) {
+        const int tt = (int)(bestk / pl.P);
+        const int rem = (int)(bestk % pl.P);
+        const int jx = rem / pl.ncy, jy = rem % pl.ncy;
+        bx = -pl.win_x + jx * pl.low_res + bestpos / pl.low_res;
+        by = -pl.win_y + jy * pl.low_res + bestpos % pl.low_res;
+        bt = tt - pl.win_t;
+    }
+    rec->status = dangerous ? REC_DANGEROUS : 0;
     rec->found = s > pl.thr;
     rec->n_eval = n;
     rec->best[0] = bx;
@@ -660,7 +815,8 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double
                                                        int4* __restrict__ cidx,
                                                        double* __restrict__ gterms,
                                                        RtcsmRecord* rec, int guard_cap,
-                                                       double guard_eps, int inject, int mode)
+                                                       double guard_eps, int inject, int mode,
+                                                       int gen)
 {
     __shared__ double lterms[kCostLdsTerms];
     const int pi = blockIdx.x;
@@ -689,7 +845,7 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double
                     cell[j] = (int)floor(q[j]);
                     if (near_boundary(q[j], guard_eps)) {
                         cell[j] += inject;
-                        const int slot = atomicAdd(&rec->cost_guard_count, 1);
+                        const int slot = tagged_slot(&rec->cost_guard_word, (unsigned)gen);
                         if (slot < guard_cap) {
                             CostGuardRec g;
                             g.pose_which = pi * 4 + j;
@@ -779,6 +935,18 @@ __global__ __launch_bounds__(256) void k_fine_dense(RtcsmPlan pl, const double* 
 // --------------------------------------------------------------------------
 // host orchestration
 // --------------------------------------------------------------------------
+void set_plane_layout(RtcsmPlan& pl)
+{
+    pl.Wq = (pl.W + pl.low_res - 1) / pl.low_res;
+    pl.Hq = (pl.H + pl.low_res - 1) / pl.low_res;
+    pl.M = std::max(pl.ncx, pl.ncy);
+    pl.Wqp = pl.Wq + 2 * pl.M;
+    pl.Hqp = pl.Hq + 2 * pl.M;
+    pl.pstride = (long long)pl.Wqp * pl.Hqp;
+    LGS_REQUIRE((long long)pl.low_res * pl.low_res * pl.pstride < (1LL << 31),
+                "coarse map too large for 32-bit plane offsets");
+}
+
 RtcsmPlan make_plan(const lgs_grid* grid, const lgs_rtcsm_params* p, const lgs_scan* scan,
                     lgs_pose2d initial, double nthr, int nv)
 {
@@ -813,6 +981,23 @@ RtcsmPlan make_plan(const lgs_grid* grid, const lgs_rtcsm_params* p, const lgs_s
     pl.K = (long long)pl.T * pl.P;
     pl.Nv = nv;
     pl.N = scan->n;
+    pl.rmax = p->scan_range_max;
+    set_plane_layout(pl);
+    return pl;
+}
+
+// the plan fields the coarse-map layout depends on (no scan needed)
+RtcsmPlan layout_plan(const lgs_grid* grid, const lgs_rtcsm_params* p)
+{
+    RtcsmPlan pl{};
+    pl.W = grid->w;
+    pl.H = grid->h;
+    pl.low_res = p->low_resolution;
+    pl.win_x = (int)std::ceil(0.5 * p->range_x / grid->res);
+    pl.win_y = (int)std::ceil(0.5 * p->range_y / grid->res);
+    pl.ncx = (2 * pl.win_x) / pl.low_res + 1;
+    pl.ncy = (2 * pl.win_y) / pl.low_res + 1;
+    set_plane_layout(pl);
     return pl;
 }
 
@@ -837,11 +1022,12 @@ CostPlan make_cost_plan(const lgs_grid* grid, const lgs_cost_ge_params* c, const
 
 struct Workspace {
     int2* idx;
-    int4* cinfo;
+    int* cbase;         // [T*Nv + 2*kPipe] padded-plane base offset per (angle, beam)
     double* cscore;
     uint8_t* cflag;
-    uint8_t* sel;
-    int* list;
+    int* list;          // [nseg * kSelSeg] selected blocks, per segment
+    int* segcnt;        // [nseg]
+    int nseg;
     double* fval;
     int* fpos;
     double* part_c;
@@ -851,11 +1037,8 @@ struct Workspace {
     double* poses7;
     int4* cidx;
     double* terms;
-    void* cub_temp;
-    size_t cub_bytes;
     int nparts;
-    double* decim;
-    int Wq, Hq;
+    double* decim;      // padded phase planes
     double* zero;
     int* tedge;
 };
@@ -864,24 +1047,38 @@ inline size_t sidx_bytes(const RtcsmPlan& pl) { return sizeof(int2) * (size_t)(p
 
 inline int coarse_block(const RtcsmPlan& pl) { return std::min(1024, ((pl.P + 63) / 64) * 64); }
 
+// The padded phase-plane buffer (S_DECIM); its zero margins are written once
+// per (buffer, layout) -- the kernels only ever write the interior.
+double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl)
+{
+    const size_t bytes = sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride;
+    double* D = (double*)ctx->ensure(S_DECIM, bytes);
+    const long long key[4] = { pl.low_res, pl.Wq, pl.Hq, pl.M };
+    if (D != ctx->planes_ptr || std::memcmp(key, ctx->planes_key, sizeof(key)) != 0) {
+        LGS_HIP_CHECK(hipMemsetAsync(D, 0, bytes, ctx->stream));
+        ctx->planes_ptr = D;
+        std::memcpy(ctx->planes_key, key, sizeof(key));
+    }
+    return D;
+}
+
 Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
 {
     Workspace w{};
     const int cb = coarse_block(pl);
     const int tiles = (pl.P + cb - 1) / cb;
     w.nparts = tiles * pl.T;
-    w.Wq = (pl.W + pl.low_res - 1) / pl.low_res;
-    w.Hq = (pl.H + pl.low_res - 1) / pl.low_res;
-    w.decim = (double*)ctx->ensure(S_DECIM, sizeof(double) * std::max<size_t>(1, (size_t)pl.low_res * pl.low_res * w.Wq * w.Hq));
+    w.decim = ctx->coarse_planes ? planes_buffer(ctx, pl) : nullptr;
     const size_t K = (size_t)pl.K;
     // index arrays padded by 2*kPipe entries: seq_sum's look-ahead loads
     const size_t nidx = (size_t)pl.T * std::max(pl.Nv, 1) + 2 * kPipe;
     w.idx = (int2*)ctx->ensure(S_IDX, sizeof(int2) * nidx);
-    w.cinfo = (int4*)ctx->ensure(S_CINFO, sizeof(int4) * nidx);
+    w.cbase = (int*)ctx->ensure(S_CINFO, sizeof(int) * nidx);
     w.cscore = (double*)ctx->ensure(S_CSCORE, sizeof(double) * K);
     w.cflag = (uint8_t*)ctx->ensure(S_CFLAG, K);
-    w.sel = (uint8_t*)ctx->ensure(S_SEL, K);
-    w.list = (int*)ctx->ensure(S_LIST, sizeof(int) * K);
+    w.nseg = (int)((K + kSelSeg - 1) / kSelSeg);
+    w.segcnt = (int*)ctx->ensure(S_SEL, sizeof(int) * (size_t)w.nseg);
+    w.list = (int*)ctx->ensure(S_LIST, sizeof(int) * (size_t)w.nseg * kSelSeg);
     w.fval = (double*)ctx->ensure(S_FVAL, sizeof(double) * K);
     w.fpos = (int*)ctx->ensure(S_FPOS, sizeof(int) * K);
     w.part_c = (double*)ctx->ensure(S_PART_C, sizeof(double) * (size_t)w.nparts);
@@ -894,33 +1091,36 @@ Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
     w.poses7 = (double*)ctx->ensure(S_POSES7, sizeof(double) * 21);
     w.cidx = (int4*)ctx->ensure(S_COST_IDX, sizeof(int4) * 7 * (size_t)N);
     w.terms = (double*)ctx->ensure(S_COST_TERM, sizeof(double) * 7 * (size_t)N);
-    size_t bytes = 0;
-    LGS_HIP_CHECK(hipcub::DeviceSelect::Flagged(nullptr, bytes, hipcub::CountingInputIterator<int>(0),
-                                                w.sel, w.list, w.count, (int)K, ctx->stream));
-    w.cub_temp = ctx->ensure(S_CUB_TEMP, bytes);
-    w.cub_bytes = bytes;
     return w;
 }
 
-// Coarse stage: (phase-plane copy of the caller's coarse map, re-done per call
-// since the caller owns that map) + one lane per coarse block.
+// Phase-plane copy of a plain coarse map into the context's S_DECIM slot
+// (once per batch: every match of a batch shares the map).
+void launch_decimate(lgs_ctx* ctx, const double* coarse, const RtcsmPlan& pl, hipStream_t st)
+{
+    double* D = planes_buffer(ctx, pl);
+    dim3 gd((pl.Wq + 255) / 256, pl.Hq, pl.low_res * pl.low_res);
+    hipLaunchKernelGGL(k_decimate, gd, dim3(256), 0, st, coarse, pl.W, pl.H, pl.low_res, pl.Wq, pl.M, pl.Wqp,
+                       pl.pstride, D);
+    LGS_HIP_CHECK(hipGetLastError());
+}
+
+// Coarse stage: one lane per coarse block; with phase planes the coarse map
+// is already in w.decim (launch_decimate or the planes precompute).
 void launch_coarse(lgs_ctx* ctx, const RtcsmPlan& pl, const Workspace& w, const double* coarse,
                    int gen, hipStream_t st)
 {
     const int cb = coarse_block(pl);
     dim3 g((pl.P + cb - 1) / cb, pl.T);
     if (ctx->coarse_planes) {
-        dim3 gd((w.Wq + 255) / 256, w.Hq, pl.low_res * pl.low_res);
-        hipLaunchKernelGGL(k_decimate, gd, dim3(256), 0, st, coarse, pl.W, pl.H, pl.low_res, w.Wq, w.Hq,
-                           w.decim);
-        LGS_HIP_CHECK(hipGetLastError());
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-        hipLaunchKernelGGL(k_coarse<1>, g, dim3(cb), 0, st, pl, w.decim, w.Wq, w.Hq, w.idx, w.cinfo,
+        hipLaunchKernelGGL(k_coarse<1>, g, dim3(cb), 0, st, pl, w.decim, w.idx, w.cbase,
                            w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
         ctx->timing_end(tok);
     } else {
+        LGS_REQUIRE(coarse, "plain coarse map missing");
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-        hipLaunchKernelGGL(k_coarse<0>, g, dim3(cb), 0, st, pl, coarse, w.Wq, w.Hq, w.idx, w.cinfo,
+        hipLaunchKernelGGL(k_coarse<0>, g, dim3(cb), 0, st, pl, coarse, w.idx, w.cbase,
                            w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
         ctx->timing_end(tok);
     }
@@ -946,19 +1146,25 @@ void launch_seed(const RtcsmPlan& pl, const double* grid, const Workspace& w, in
     }
     LGS_HIP_CHECK(hipGetLastError());
 }
+// dynamic LDS: the evaluator's buffers, then the segment prefix (nseg + 1 ints)
+inline size_t pref_bytes(const Workspace& w) { return sizeof(int) * (size_t)(w.nseg + 1); }
+
 template <int LR>
 void launch_fine_t(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_fine<LR>, dim3(1024), dim3(64 * LR), eval_t_smem<LR>(pl.Nv), st, pl, grid,
-                       w.idx, w.zero, w.list, w.count, w.fval, w.fpos);
+    const size_t e = (eval_t_smem<LR>(pl.Nv) + 15) & ~size_t(15);
+    hipLaunchKernelGGL(k_fine<LR>, dim3(1024), dim3(64 * LR), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
+                       w.list, w.segcnt, w.nseg, (unsigned)e, w.fval, w.fpos);
 }
 void launch_fine(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
 {
     switch (pl.Nv <= 64 * kMaxChunks ? pl.low_res : 0) {
     case 5: launch_fine_t<5>(pl, grid, w, st); break;
-    default:
-        hipLaunchKernelGGL(k_fine<0>, dim3(1024), dim3(64), sidx_bytes(pl), st, pl, grid, w.idx, w.zero,
-                           w.list, w.count, w.fval, w.fpos);
+    default: {
+        const size_t e = (sidx_bytes(pl) + 15) & ~size_t(15);
+        hipLaunchKernelGGL(k_fine<0>, dim3(1024), dim3(64), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
+                           w.list, w.segcnt, w.nseg, (unsigned)e, w.fval, w.fpos);
+    }
     }
     LGS_HIP_CHECK(hipGetLastError());
 }
@@ -970,15 +1176,15 @@ struct ScanOptions {
     const std::vector<int4>* cost_patches = nullptr;
 };
 
-// Enqueue the whole device pipeline of one match on ctx->stream.
-void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
-                   const lgs_cost_ge_params* cost, lgs_scan* scan, const RtcsmPlan& pl,
-                   const int* d_vidx, RtcsmRecord* d_rec, const ScanOptions& opt)
+// Enqueue the whole device pipeline of one match on ctx->stream; returns the
+// generation that tags this match's guard counters in *d_rec.
+int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
+                  const lgs_cost_ge_params* cost, lgs_scan* scan, const RtcsmPlan& pl,
+                  RtcsmRecord* d_rec, const ScanOptions& opt)
 {
     Workspace w = ensure_workspace(ctx, pl, scan->n);
     hipStream_t st = ctx->stream;
     const int gen = ++ctx->generation;
-    LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0, sizeof(RtcsmRecord), st));
     const int inject = ctx->inject_index ? 1 : 0;
     if (pl.Nv > 0) {
         if (opt.host_idx) {
@@ -986,14 +1192,14 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                                          hipMemcpyHostToDevice, st));
             const size_t n = (size_t)pl.T * pl.Nv;
             hipLaunchKernelGGL(k_cinfo, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pl, w.idx,
-                               w.cinfo, w.Wq, w.Hq, w.tedge, gen);
+                               w.cbase, w.tedge, gen);
             LGS_HIP_CHECK(hipGetLastError());
         } else {
             dim3 g((pl.Nv + 255) / 256, pl.T);
             {
                 const int tok_ = ctx->timing_begin(K_PROJECT, 24.0 * (double)pl.T * pl.Nv);
                 hipLaunchKernelGGL(k_project, g, dim3(256), 0, st, pl, scan->d_ranges, scan->d_angles,
-                                   d_vidx, w.idx, w.cinfo, w.Wq, w.Hq, w.tedge, gen, d_rec,
+                                   w.idx, w.cbase, w.tedge, gen, d_rec,
                                    ctx->guard_cap, ctx->guard_eps, inject);
                 ctx->timing_end(tok_);
             }
@@ -1003,8 +1209,8 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                 LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.patches->data(), sizeof(int4) * opt.patches->size(),
                                              hipMemcpyHostToDevice, st));
                 const int np = (int)opt.patches->size();
-                hipLaunchKernelGGL(k_patch, dim3((np + 255) / 256), dim3(256), 0, st, pl, w.idx, w.cinfo,
-                                   w.Wq, w.Hq, w.tedge, gen, dp, np);
+                hipLaunchKernelGGL(k_patch, dim3((np + 255) / 256), dim3(256), 0, st, pl, w.idx, w.cbase,
+                                   w.tedge, gen, dp, np);
                 LGS_HIP_CHECK(hipGetLastError());
             }
         }
@@ -1018,14 +1224,11 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
     LGS_HIP_CHECK(hipGetLastError());
     {
         const int tok_ = ctx->timing_begin(K_SELECT, 10.0 * (double)pl.K);
-        hipLaunchKernelGGL(k_select, dim3((unsigned)((pl.K + 255) / 256)), dim3(256), 0, st, pl, w.cscore,
-                           w.cflag, w.Lp, w.sel);
+        hipLaunchKernelGGL(k_select, dim3((unsigned)w.nseg), dim3(kSelSeg), 0, st, pl, w.cscore, w.cflag,
+                           w.Lp, w.list, w.segcnt);
         ctx->timing_end(tok_);
     }
     LGS_HIP_CHECK(hipGetLastError());
-    size_t bytes = w.cub_bytes;
-    LGS_HIP_CHECK(hipcub::DeviceSelect::Flagged(w.cub_temp, bytes, hipcub::CountingInputIterator<int>(0),
-                                                w.sel, w.list, w.count, (int)pl.K, st));
     {
         const int tok_ = ctx->timing_begin(K_FINE, 0.0);
         launch_fine(pl, grid->d, w, st);
@@ -1034,8 +1237,8 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
     LGS_HIP_CHECK(hipGetLastError());
     {
         const int tok_ = ctx->timing_begin(K_REPLAY, 0.0);
-        hipLaunchKernelGGL(k_replay, dim3(1), dim3(64), 0, st, pl, w.cscore, w.cflag, w.list, w.count,
-                           w.fval, w.fpos, w.Lp, d_rec, w.poses7);
+        hipLaunchKernelGGL(k_replay, dim3(1), dim3(64), pref_bytes(w), st, pl, w.cscore, w.cflag, w.list,
+                           w.segcnt, w.nseg, w.fval, w.fpos, w.Lp, d_rec, w.poses7);
         ctx->timing_end(tok_);
     }
     LGS_HIP_CHECK(hipGetLastError());
@@ -1046,7 +1249,7 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
         const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * (double)scan->n);
         hipLaunchKernelGGL(k_cost, dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
                            scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
-                           ctx->guard_eps, inject, 0);
+                           ctx->guard_eps, inject, 0, gen);
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
     }
@@ -1060,10 +1263,25 @@ void enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
         LGS_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(k_cost, dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
                            scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
-                           ctx->guard_eps, 0, 1);
+                           ctx->guard_eps, 0, 1, gen);
         LGS_HIP_CHECK(hipGetLastError());
     }
+    return gen;
 }
+
+// Host view of a device record: the generation-tagged guard words decoded.
+inline int tagged_count(unsigned long long w, int gen)
+{
+    return ((unsigned)(w >> 32) == (unsigned)gen) ? (int)(unsigned)w : 0;
+}
+struct HostRecord : RtcsmRecord {
+    int guard_count = 0, cost_guard_count = 0;
+    HostRecord(const RtcsmRecord& r, int gen) : RtcsmRecord(r)
+    {
+        guard_count = tagged_count(r.guard_word, gen);
+        cost_guard_count = tagged_count(r.cost_guard_word, gen);
+    }
+};
 
 // glibc recomputation of one projected index (host side of the guard).
 void host_project(const RtcsmPlan& pl, const lgs_scan* scan, int vbeam, int tt, int& ix, int& iy)
@@ -1114,7 +1332,7 @@ void host_poses7(const RtcsmPlan& pl, const int best[3], double P7[7][3])
 // Verify guarded projections against glibc; returns true if the match must be
 // re-run (and fills the options for the rerun).
 bool check_projection_guards(lgs_ctx* ctx, const RtcsmPlan& pl, const lgs_scan* scan,
-                             const RtcsmRecord& rec, std::vector<int4>& patches,
+                             const HostRecord& rec, std::vector<int4>& patches,
                              std::vector<int2>& host_idx, bool& use_host_idx)
 {
     use_host_idx = false;
@@ -1142,7 +1360,7 @@ bool check_projection_guards(lgs_ctx* ctx, const RtcsmPlan& pl, const lgs_scan* 
 }
 
 bool check_cost_guards(lgs_ctx* ctx, const RtcsmPlan& pl, const CostPlan& cp,
-                       const lgs_scan* scan, const RtcsmRecord& rec, std::vector<int4>& cpatch,
+                       const lgs_scan* scan, const HostRecord& rec, std::vector<int4>& cpatch,
                        bool& full)
 {
     cpatch.clear();
@@ -1231,30 +1449,31 @@ void check_args(const lgs_grid* grid, const lgs_grid* coarse, const lgs_rtcsm_pa
 void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
                lgs_scan* const* scans, const lgs_pose2d* init, int n, double nthr,
-               lgs_rtcsm_summary* out)
+               lgs_rtcsm_summary* out, bool coarse_in_planes = false)
 {
     LGS_HIP_CHECK(hipSetDevice(ctx->device));
     std::vector<RtcsmPlan> plans(n);
-    std::vector<const int*> vidx(n);
+    std::vector<int> gens(n);
     for (int j = 0; j < n; ++j) {
         check_args(grid, coarse, params, cost, scans[j]);
         int nv = 0;
-        vidx[j] = scan_valid_indices(ctx, scans[j], params->scan_range_max, &nv);
+        scan_valid_indices(ctx, scans[j], params->scan_range_max, &nv);
         plans[j] = make_plan(grid, params, scans[j], init[j], nthr, nv);
-        LGS_REQUIRE(plans[j].K < (1LL << 31), "search window too large");
+        // the segment prefix of the selection lives in LDS next to the evaluator
+        LGS_REQUIRE(plans[j].K <= 7LL * 1024 * 1024, "search window too large (> 7M coarse blocks)");
     }
     RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord) * (size_t)n);
     RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned(sizeof(RtcsmRecord) * (size_t)n);
+    if (ctx->coarse_planes && !coarse_in_planes) launch_decimate(ctx, coarse->d, plans[0], ctx->stream);
     ScanOptions none;
-    for (int j = 0; j < n; ++j)
-        enqueue_match(ctx, grid, coarse, cost, scans[j], plans[j], vidx[j], d_rec + j, none);
+    for (int j = 0; j < n; ++j) gens[j] = enqueue_match(ctx, grid, coarse, cost, scans[j], plans[j], d_rec + j, none);
     LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n,
                                  hipMemcpyDeviceToHost, ctx->stream));
-    LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    ctx->sync();
     if (ctx->profile) ctx->harvest();
 
     for (int j = 0; j < n; ++j) {
-        RtcsmRecord rec = h_rec[j];
+        HostRecord rec(h_rec[j], gens[j]);
         int guard_hits = rec.guard_count + rec.cost_guard_count;
         int fixups = 0, slow = 0;
         // exactness loop: at most a few reruns
@@ -1300,11 +1519,11 @@ void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                 }
             }
             if (!rerun) break;
-            enqueue_match(ctx, grid, coarse, cost, scans[j], plans[j], vidx[j], d_rec + j, opt);
+            const int g = enqueue_match(ctx, grid, coarse, cost, scans[j], plans[j], d_rec + j, opt);
             LGS_HIP_CHECK(hipMemcpyAsync(&h_rec[j], d_rec + j, sizeof(RtcsmRecord),
                                          hipMemcpyDeviceToHost, ctx->stream));
-            LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-            rec = h_rec[j];
+            ctx->sync();
+            rec = HostRecord(h_rec[j], g);
             if (opt.patches || opt.host_idx) rec.guard_count = 0;  // already exact
         }
         finish_summary(plans[j], scans[j], init[j], rec, &out[j]);
@@ -1314,9 +1533,14 @@ void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
     }
 }
 
-// ComputeCoarserMap (:148-153) into the context-owned coarse grid
-const lgs_grid* coarser_map(lgs_ctx* ctx, const lgs_grid* grid, int low_res)
+// ComputeCoarserMap (:148-153) into the context-owned coarse grid.  With the
+// phase-plane layout (and W, H multiples of LowRes) the precompute writes the
+// planes directly into S_DECIM and *in_planes is set: the returned grid then
+// carries the geometry only (d == nullptr).
+const lgs_grid* coarser_map(lgs_ctx* ctx, const lgs_grid* grid, const lgs_rtcsm_params* params,
+                            bool* in_planes)
 {
+    const int low_res = params->low_resolution;
     LGS_HIP_CHECK(hipSetDevice(ctx->device));
     lgs_grid* cg = ctx->coarse_scratch;
     if (!cg) {
@@ -1332,7 +1556,15 @@ const lgs_grid* coarser_map(lgs_ctx* ctx, const lgs_grid* grid, int low_res)
     cg->min_x = grid->min_x;
     cg->min_y = grid->min_y;
     cg->res = grid->res;
-    launch_precompute(ctx, grid, low_res, cg->d);
+    *in_planes = ctx->coarse_planes && precompute_planes_ok(grid, low_res);
+    if (*in_planes) {
+        const RtcsmPlan lp = layout_plan(grid, params);
+        const PlaneGeom pg{ lp.M, lp.Wqp, lp.pstride };
+        launch_precompute(ctx, grid, low_res, planes_buffer(ctx, lp), &pg);
+        cg->d = nullptr;
+    } else {
+        launch_precompute(ctx, grid, low_res, cg->d, nullptr);
+    }
     return cg;
 }
 
@@ -1374,9 +1606,10 @@ extern "C" int lgs_rtcsm_optimize_pose_query(lgs_ctx* ctx, const lgs_grid* grid,
     if (!ctx || !grid || !params || !out) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
         LGS_REQUIRE(params->low_resolution >= 1, "low_resolution must be >= 1");
-        const lgs_grid* cg = coarser_map(ctx, grid, params->low_resolution);
+        bool planes = false;
+        const lgs_grid* cg = coarser_map(ctx, grid, params, &planes);
         lgs_scan* s = const_cast<lgs_scan*>(scan);
-        run_batch(ctx, grid, cg, params, cost, &s, &initial, 1, DBL_MIN, out);
+        run_batch(ctx, grid, cg, params, cost, &s, &initial, 1, DBL_MIN, out, planes);
     });
 }
 
@@ -1390,7 +1623,7 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         lgs_scan* s = const_cast<lgs_scan*>(scan);
         int nv = 0;
-        const int* vidx = scan_valid_indices(ctx, s, params->scan_range_max, &nv);
+        scan_valid_indices(ctx, s, params->scan_range_max, &nv);
         RtcsmPlan pl = make_plan(grid, params, s, initial, DBL_MIN, nv);
         const int nfx = pl.ncx * pl.low_res, nfy = pl.ncy * pl.low_res;
         if (dims) {
@@ -1405,10 +1638,11 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
         if (nv > 0) {
             dim3 g((nv + 255) / 256, pl.T);
             hipLaunchKernelGGL(k_project, g, dim3(256), 0, ctx->stream, pl, s->d_ranges, s->d_angles,
-                               vidx, w.idx, w.cinfo, w.Wq, w.Hq, w.tedge, gen, d_rec, 0, -1.0, 0);
+                               w.idx, w.cbase, w.tedge, gen, d_rec, 0, -1.0, 0);
             LGS_HIP_CHECK(hipGetLastError());
         }
         if (coarse_scores) {
+            if (ctx->coarse_planes) launch_decimate(ctx, coarse->d, pl, ctx->stream);
             launch_coarse(ctx, pl, w, coarse->d, gen, ctx->stream);
             LGS_HIP_CHECK(hipMemcpyAsync(coarse_scores, w.cscore, sizeof(double) * (size_t)pl.K,
                                          hipMemcpyDeviceToHost, ctx->stream));
@@ -1423,7 +1657,7 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
             LGS_HIP_CHECK(hipMemcpyAsync(fine_scores, d, sizeof(double) * nf, hipMemcpyDeviceToHost,
                                          ctx->stream));
         }
-        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->sync();
     });
 }
 
@@ -1441,16 +1675,16 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
         RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord));
         RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned(sizeof(RtcsmRecord));
         double hp[3] = { pose.x, pose.y, pose.theta };
-        LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0, sizeof(RtcsmRecord), ctx->stream));
+        const int gen = ++ctx->generation;
         LGS_HIP_CHECK(hipMemcpyAsync(poses, hp, sizeof(hp), hipMemcpyHostToDevice, ctx->stream));
         hipLaunchKernelGGL(k_cost, dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
                            scan->d_ranges, scan->d_angles, poses, cidx, terms, d_rec, ctx->guard_cap,
-                           ctx->guard_eps, 0, 0);
+                           ctx->guard_eps, 0, 0, gen);
         LGS_HIP_CHECK(hipGetLastError());
         LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                      ctx->stream));
-        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        if (h_rec->cost_guard_count > 0) {
+        ctx->sync();
+        if (tagged_count(h_rec->cost_guard_word, gen) > 0) {
             // exact host recomputation of every cell row, then re-evaluate
             std::vector<int4> row((size_t)cp.N, make_int4(INT_MIN, 0, 0, 0));
             for (int b = 0; b < cp.N; ++b) {
@@ -1464,11 +1698,11 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
                                          hipMemcpyHostToDevice, ctx->stream));
             hipLaunchKernelGGL(k_cost, dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
                                scan->d_ranges, scan->d_angles, poses, cidx, terms, d_rec,
-                               ctx->guard_cap, ctx->guard_eps, 0, 1);
+                               ctx->guard_cap, ctx->guard_eps, 0, 1, gen);
             LGS_HIP_CHECK(hipGetLastError());
             LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                          ctx->stream));
-            LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+            ctx->sync();
         }
         *out_cost = h_rec->costs[0];
     });
@@ -1504,7 +1738,8 @@ extern "C" int lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* param
                         "loop queries must cover the candidates contiguously and in order");
             covered += Q.num_candidates;
             if (Q.num_candidates == 0) continue;
-            const lgs_grid* coarse = Q.coarse ? Q.coarse : coarser_map(ctx, Q.map, params->low_resolution);
+            bool planes = false;
+            const lgs_grid* coarse = Q.coarse ? Q.coarse : coarser_map(ctx, Q.map, params, &planes);
             const int n = Q.num_candidates;
             scans.resize(n);
             poses.resize(n);
@@ -1516,7 +1751,7 @@ extern "C" int lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* param
                 poses[j] = c.node_pose;
             }
             run_batch(ctx, Q.map, coarse, params, cost, scans.data(), poses.data(), n, score_threshold,
-                      sums.data());
+                      sums.data(), planes);
             for (int j = 0; j < n; ++j) {
                 lgs_loop_result& r = results[Q.first_candidate + j];
                 std::memset(&r, 0, sizeof(r));

@@ -56,6 +56,19 @@ const char* const kKernelNames[K_NUM_KERNELS] = { "k_project", "k_coarse", "k_se
                                                   "k_linsolve", "k_ray_emit", "k_ray_apply" };
 }
 
+void lgs_ctx::sync()
+{
+    if (!spin_sync) {
+        LGS_HIP_CHECK(hipStreamSynchronize(stream));
+        return;
+    }
+    for (;;) {
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) LGS_HIP_CHECK(e);
+    }
+}
+
 int lgs_ctx::timing_begin(int kernel, double algo_bytes)
 {
     if (!profile || !((profile_mask >> kernel) & 1u)) return -1;
@@ -160,14 +173,14 @@ extern "C" const char* lgs_ctx_last_error(const lgs_ctx* ctx)
 extern "C" int lgs_ctx_synchronize(lgs_ctx* ctx)
 {
     if (!ctx) return LGS_ERR_INVALID_ARG;
-    return guarded(ctx, [&] { LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream)); });
+    return guarded(ctx, [&] { ctx->sync(); });
 }
 
 extern "C" int lgs_ctx_kernel_stats(lgs_ctx* ctx, lgs_kernel_stat* out, int cap)
 {
     if (!ctx) return -LGS_ERR_INVALID_ARG;
     int rc = guarded(ctx, [&] {
-        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->sync();
         ctx->harvest();
     });
     if (rc != LGS_OK) return -rc;
@@ -190,7 +203,7 @@ extern "C" int lgs_ctx_reset_stats(lgs_ctx* ctx)
 {
     if (!ctx) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
-        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->sync();
         ctx->harvest();
         for (int k = 0; k < K_NUM_KERNELS; ++k) {
             ctx->stat_launches[k] = 0;
@@ -213,6 +226,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
         ctx->profile = value != 0.0;
         ctx->profile_mask = ~0u;
         return LGS_OK;
+    case LGS_OPT_SPIN_SYNC: ctx->spin_sync = value != 0.0; return LGS_OK;
     case LGS_OPT_PROFILE_MASK:
         ctx->profile_mask = (unsigned)value;
         ctx->profile = ctx->profile_mask != 0;
@@ -261,7 +275,7 @@ extern "C" int lgs_grid_create(lgs_ctx* ctx, int w, int h, double min_x, double 
             throw Error(LGS_ERR_OOM, "hipMalloc failed for grid");
         }
         LGS_HIP_CHECK(hipMemsetAsync(g->d, 0, bytes, ctx->stream));
-        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->sync();
         *out = g;
     });
 }
@@ -306,7 +320,7 @@ extern "C" int lgs_grid_upload(lgs_ctx* ctx, lgs_grid* g, const double* host)
         size_t bytes = (size_t)g->w * (size_t)g->h * sizeof(double);
         if (!bytes) return;
         LGS_HIP_CHECK(hipMemcpyAsync(g->d, host, bytes, hipMemcpyHostToDevice, ctx->stream));
-        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->sync();
     });
 }
 
@@ -317,7 +331,7 @@ extern "C" int lgs_grid_download(lgs_ctx* ctx, const lgs_grid* g, double* host)
         size_t bytes = (size_t)g->w * (size_t)g->h * sizeof(double);
         if (!bytes) return;
         LGS_HIP_CHECK(hipMemcpyAsync(host, g->d, bytes, hipMemcpyDeviceToHost, ctx->stream));
-        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->sync();
     });
 }
 
@@ -365,9 +379,12 @@ __device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b 
 // footprint [sx0, sx1) x [sy0, sy1) is staged in LDS (zero outside the grid),
 // then the y-pass (SlidingWindowMaxRow) and x-pass (SlidingWindowMaxCol) run
 // from LDS.
+// pg.Wqp > 0: the output is written directly into the interior of the padded
+// phase-plane layout of k_rtcsm.hip (plane ry*w + rx, row y/w + M, column
+// x/w + M; requires W, H multiples of w).
 __global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restrict__ in,
                                                           double* __restrict__ out, int W,
-                                                          int H, int w)
+                                                          int H, int w, PlaneGeom pg)
 {
     extern __shared__ double lds[];
     const int x0 = blockIdx.x * kTileX, y0 = blockIdx.y * kTileY;
@@ -398,7 +415,13 @@ __global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restri
         const int s = win_start(x0 + ox, W, w) - sx0;
         double m = m1[oy * fw + s];
         for (int j = 1; j < w; ++j) m = dmax(m, m1[oy * fw + s + j]);
-        out[(size_t)(y0 + oy) * W + (x0 + ox)] = m;
+        const int x = x0 + ox, y = y0 + oy;
+        if (pg.Wqp > 0) {
+            const int qx = x / w, qy = y / w, rx = x - qx * w, ry = y - qy * w;
+            out[(ry * w + rx) * pg.pstride + (long long)(qy + pg.M) * pg.Wqp + qx + pg.M] = m;
+        } else {
+            out[(size_t)y * W + x] = m;
+        }
     }
 }
 
@@ -424,8 +447,15 @@ __global__ void k_precompute_direct(const double* __restrict__ in, double* __res
 }  // namespace
 
 namespace lgs {
-void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out)
+bool precompute_planes_ok(const lgs_grid* in, int win)
 {
+    return win >= 1 && win <= kMaxWinTiled && in->w % win == 0 && in->h % win == 0;
+}
+
+void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, const PlaneGeom* planes)
+{
+    LGS_REQUIRE(!planes || precompute_planes_ok(in, win), "phase-plane precompute needs W, H multiples of the window");
+    const PlaneGeom pg = planes ? *planes : PlaneGeom{ 0, 0, 0 };
     if (in->w == 0 || in->h == 0) return;
     // algorithmic bytes: two separable passes, each reading and
     // writing one fp64 per cell = 32 B/cell
@@ -435,7 +465,7 @@ void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out)
         const size_t lds = (size_t)(fh * fw + kTileY * fw) * sizeof(double);
         dim3 grid((in->w + kTileX - 1) / kTileX, (in->h + kTileY - 1) / kTileY);
         hipLaunchKernelGGL(k_precompute_tiled, grid, dim3(256), lds, ctx->stream, in->d, out,
-                           in->w, in->h, win);
+                           in->w, in->h, win, pg);
     } else {
         dim3 grid((in->w + 255) / 256, in->h);
         hipLaunchKernelGGL(k_precompute_direct, grid, dim3(256), 0, ctx->stream, in->d, out,
@@ -456,7 +486,7 @@ extern "C" int lgs_grid_precompute_max(lgs_ctx* ctx, const lgs_grid* in, int win
         out->min_x = in->min_x;
         out->min_y = in->min_y;
         out->res = in->res;
-        launch_precompute(ctx, in, win, out->d);
+        launch_precompute(ctx, in, win, out->d, nullptr);
     });
 }
 
@@ -484,8 +514,7 @@ extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan**
         s->max_elem = m;
         const size_t bytes = sizeof(double) * (size_t)hs->n;
         if (hipMalloc(&s->d_ranges, bytes) != hipSuccess ||
-            hipMalloc(&s->d_angles, bytes) != hipSuccess ||
-            hipMalloc(&s->d_vidx, sizeof(int) * (size_t)hs->n) != hipSuccess) {
+            hipMalloc(&s->d_angles, bytes) != hipSuccess) {
             hipFree(s->d_ranges);
             hipFree(s->d_angles);
             delete s;
@@ -493,7 +522,7 @@ extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan**
         }
         LGS_HIP_CHECK(hipMemcpyAsync(s->d_ranges, hs->ranges, bytes, hipMemcpyHostToDevice, ctx->stream));
         LGS_HIP_CHECK(hipMemcpyAsync(s->d_angles, hs->angles, bytes, hipMemcpyHostToDevice, ctx->stream));
-        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ctx->sync();
         *out = s;
     });
 }
@@ -504,7 +533,6 @@ extern "C" void lgs_scan_destroy(lgs_scan* s)
     hipSetDevice(s->device);
     hipFree(s->d_ranges);
     hipFree(s->d_angles);
-    hipFree(s->d_vidx);
     delete s;
 }
 
@@ -519,14 +547,10 @@ const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* s, double rmax, int* nv)
         for (int i = 0; i < s->n; ++i)
             if (!(s->h_ranges[i] >= rmax)) s->h_vidx.push_back(i);
         s->nv = (int)s->h_vidx.size();
-        if (s->nv > 0) {
-            LGS_HIP_CHECK(hipMemcpyAsync(s->d_vidx, s->h_vidx.data(), sizeof(int) * s->nv,
-                                         hipMemcpyHostToDevice, ctx->stream));
-            LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        }
         s->cached_rmax = rmax;
     }
-    *nv = s->nv;
-    return s->d_vidx;
+    (void)ctx;
+    *nv = s->nv;   // the device compacts the same beams itself (k_project)
+    return s->h_vidx.data();
 }
 }  // namespace lgs

@@ -72,11 +72,14 @@ struct GuardRec { int t, v, ix, iy; };        // projection near a cell boundary
 struct CostGuardRec { int pose_which, beam, ix, iy; };
 
 // Device-written per-scan result record (copied to host once per batch).
+// The guard counters are generation-tagged (gen << 32 | count), so the record
+// needs no memset before a match: a word carrying another generation counts
+// as zero (tagged_slot / tagged_count).
 struct RtcsmRecord {
     int status;           // bit0: dangerous unsafe block -> dense rerun
-    int guard_count;
-    int cost_guard_count;
     int found;
+    unsigned long long guard_word;
+    unsigned long long cost_guard_word;
     long long n_eval;     // coarse blocks refined on the fine map
     int best[3];
     int pad0;
@@ -102,7 +105,19 @@ struct RtcsmPlan {
     int low_res;
     int Nv;                     // beams with range < ScanRangeMax
     int N;                      // all beams
+    double rmax;                // ScanRangeMax (the compaction filter, :192-193)
+    // padded phase-plane coarse layout: lr*lr planes of
+    // (Hq + 2M) x (Wq + 2M) doubles, interior = D[ry][rx][qy][qx], margins
+    // (M = max(ncx, ncy)) all zero
+    int Wq, Hq, M, Wqp, Hqp;
+    long long pstride;
     long long K;                // T * P coarse blocks
+};
+
+// Padded phase-plane geometry handed to the precompute kernel.
+struct PlaneGeom {
+    int M, Wqp;
+    long long pstride;
 };
 
 struct CostPlan {
@@ -143,6 +158,9 @@ struct lgs_ctx {
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
     lgs_grid* coarse_scratch = nullptr;
+    // padded phase-plane buffer: margins zeroed once per (buffer, layout)
+    void* planes_ptr = nullptr;
+    long long planes_key[4] = { -1, -1, -1, -1 };
     double* zero = nullptr;      // 32 zero doubles: target of out-of-map gathers
     // profiling (LGS_OPT_PROFILE)
     bool profile = false;
@@ -158,6 +176,12 @@ struct lgs_ctx {
     int timing_begin(int kernel, double algo_bytes);
     void timing_end(int token);
     void harvest();
+
+    // wait for the stream: spin on hipStreamQuery (default; the host thread
+    // wakes within ~1 us instead of the blocking wait's interrupt latency) or
+    // hipStreamSynchronize (LGS_OPT_SPIN_SYNC 0)
+    bool spin_sync = true;
+    void sync();
 
     void* ensure(int slot, size_t bytes);
     void* ensure_pinned(size_t bytes);
@@ -187,8 +211,7 @@ struct lgs_scan {
     // compaction cache: beams with range < scan_range_max, in beam order
     double cached_rmax = NAN;
     int nv = 0;
-    int* d_vidx = nullptr;
-    std::vector<int> h_vidx;
+    std::vector<int> h_vidx;      // host copy (guard re-projection); the device compacts itself
 };
 
 extern "C" void sincos(double x, double* s, double* c);  // glibc
