@@ -448,6 +448,7 @@ __device__ void eval_block(const RtcsmPlan& pl, const double* __restrict__ grid,
 // register copies).  Beam indices of the angle row are staged in LDS first.
 // Ties resolve to the smallest reference order index o = xo*LR + yo.
 constexpr int kMaxChunks = 32;   // transposed evaluator handles Nv <= 2048
+typedef double d2a8 __attribute__((ext_vector_type(2), aligned(8)));
 
 // compile-time loop C = 0, STEP, 2*STEP, ... < MAXC; f returns false to stop
 template <int C, int MAXC, int STEP, class F>
@@ -483,16 +484,35 @@ __device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ gri
 
     constexpr int kDepth = 2;   // measured: depth 4 made k_fine slower (36 vs 27 us)
     double ra[LR], rb[LR];
+    // A lane's LR cells are consecutive doubles of one row: when the whole
+    // run is inside the map (all but the border beams) it is fetched with
+    // 16-byte loads (8-byte aligned, which gfx950 global loads accept), i.e.
+    // 3 instead of 5 memory instructions for LR = 5 -- the per-CU cache
+    // lookups, not the bytes, bound this gather.
     auto gather = [&](int c, double (&r)[LR]) {
         const int b = c * 64 + lane;
         const int2 ij = sidx[min(b, Nv - 1)];
         const bool bv = b < Nv;
+        const int x0 = ij.x + xc, y = ij.y + yr;
+        bool full = false;
+        if constexpr (LR == 5) full = bv & ((unsigned)y < (unsigned)H) & (x0 >= 0) & (x0 + LR - 1 < W);
+        if (full) {
+            const double* p = grid + (unsigned)(y * W + x0);
+            const d2a8 a = *(const d2a8*)p;
+            const d2a8 e = *(const d2a8*)(p + 2);
+            r[0] = a.x;
+            r[1] = a.y;
+            r[2] = e.x;
+            r[3] = e.y;
+            r[LR - 1] = p[4];
+        } else {
 #pragma unroll
-        for (int q = 0; q < LR; ++q) {
-            const int x = ij.x + xc + q, y = ij.y + yr;
-            const bool inb = bv & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
-            const unsigned off = (unsigned)(y * W + x);
-            r[q] = *(inb ? grid + off : zero);
+            for (int q = 0; q < LR; ++q) {
+                const int x = x0 + q;
+                const bool inb = bv & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
+                const unsigned off = (unsigned)(y * W + x);
+                r[q] = *(inb ? grid + off : zero);
+            }
         }
     };
     auto store = [&](const double (&r)[LR], double* buf) {
@@ -806,8 +826,53 @@ __device__ __forceinline__ double gval(const CostPlan& cp, const double* __restr
     return inb ? v : 0.0;
 }
 
+// The kernel-window search of CostGreedyEndpoint::Cost (:69-99) for one beam:
+// min squared distance to a cell with hit >= occThr and miss <= occThr (both
+// known).  KS > 0: compile-time kernel size, every cell value loaded before
+// any test (the loads of a beam are independent); KS == 0: runtime size.
+template <int KS>
+__device__ __forceinline__ double min_sq_dist(const CostPlan& cp, const double* __restrict__ grid, int4 c,
+                                              double minSq0)
+{
+    double minSq = minSq0;
+    if constexpr (KS > 0) {
+        constexpr int D = 2 * KS + 1;
+        double hv[D * D], mv[D * D];
+#pragma unroll
+        for (int q = 0; q < D * D; ++q) {
+            hv[q] = gval(cp, grid, c.x + q % D - KS, c.y + q / D - KS);
+            mv[q] = gval(cp, grid, c.z + q % D - KS, c.w + q / D - KS);
+        }
+#pragma unroll
+        for (int q = 0; q < D * D; ++q) {
+            const int kx = q % D - KS, ky = q / D - KS;
+            if (hv[q] == 0.0 || mv[q] == 0.0) continue;
+            if (hv[q] < cp.occupancy_threshold || mv[q] > cp.occupancy_threshold) continue;
+            const double dX = kx * cp.res;
+            const double dY = ky * cp.res;
+            const double sq = dX * dX + dY * dY;
+            minSq = (minSq < sq) ? minSq : sq;
+        }
+    } else {
+        const int K = cp.kernel_size;
+        for (int ky = -K; ky <= K; ++ky)
+            for (int kx = -K; kx <= K; ++kx) {
+                const double hv = gval(cp, grid, c.x + kx, c.y + ky);
+                const double mv = gval(cp, grid, c.z + kx, c.w + ky);
+                if (hv == 0.0 || mv == 0.0) continue;
+                if (hv < cp.occupancy_threshold || mv > cp.occupancy_threshold) continue;
+                const double dX = kx * cp.res;
+                const double dY = ky * cp.res;
+                const double sq = dX * dX + dY * dY;
+                minSq = (minSq < sq) ? minSq : sq;
+            }
+    }
+    return minSq;
+}
+
 // mode 0: compute cells (+ guard records) and store them in cidx;
 // mode 1: read cells from cidx (after host patches).
+template <int KS>
 __global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double* __restrict__ grid,
                                                        const double* __restrict__ ranges,
                                                        const double* __restrict__ angles,
@@ -823,8 +888,7 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double
     const bool in_lds = cp.N <= kCostLdsTerms;
     double* __restrict__ tm = in_lds ? lterms : gterms + (size_t)pi * cp.N;
     const double px = poses[3 * pi], py = poses[3 * pi + 1], pt = poses[3 * pi + 2];
-    const int K = cp.kernel_size;
-    const double lim = (K + 1) * cp.res;
+    const double lim = (cp.kernel_size + 1) * cp.res;
     const double minSq0 = lim * lim + lim * lim;
     for (int i = threadIdx.x; i < cp.N; i += blockDim.x) {
         int4 c;
@@ -863,21 +927,7 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double
             c = cidx[(size_t)pi * cp.N + i];
         }
         double term = 0.0;
-        if (c.x != INT_MIN) {
-            double minSq = minSq0;
-            for (int ky = -K; ky <= K; ++ky)
-                for (int kx = -K; kx <= K; ++kx) {
-                    const double hv = gval(cp, grid, c.x + kx, c.y + ky);
-                    const double mv = gval(cp, grid, c.z + kx, c.w + ky);
-                    if (hv == 0.0 || mv == 0.0) continue;
-                    if (hv < cp.occupancy_threshold || mv > cp.occupancy_threshold) continue;
-                    const double dX = kx * cp.res;
-                    const double dY = ky * cp.res;
-                    const double sq = dX * dX + dY * dY;
-                    minSq = (minSq < sq) ? minSq : sq;
-                }
-            term = exp(-0.5 * minSq / cp.variance);
-        }
+        if (c.x != INT_MIN) term = exp(-0.5 * min_sq_dist<KS>(cp, grid, c, minSq0) / cp.variance);
         tm[i] = term;
     }
     __syncthreads();
@@ -898,6 +948,9 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double
         rec->costs[pi] = cost;
     }
 }
+
+// kernel size 1 (the launcher JSON's) gets the unrolled instantiation
+#define KCOST(cp) ((cp).kernel_size == 1 ? k_cost<1> : k_cost<0>)
 
 // --------------------------------------------------------------------------
 // dense diagnostics: every fine score of the window (one lane per pose)
@@ -1247,7 +1300,7 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
     const double kk = (2.0 * cost->kernel_size + 1) * (2.0 * cost->kernel_size + 1);
     {
         const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * (double)scan->n);
-        hipLaunchKernelGGL(k_cost, dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
+        hipLaunchKernelGGL(KCOST(cp), dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
                            scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
                            ctx->guard_eps, inject, 0, gen);
         ctx->timing_end(tok_);
@@ -1261,7 +1314,7 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                                      hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, st, w.cidx, dp, np);
         LGS_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(k_cost, dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
+        hipLaunchKernelGGL(KCOST(cp), dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
                            scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
                            ctx->guard_eps, 0, 1, gen);
         LGS_HIP_CHECK(hipGetLastError());
@@ -1677,7 +1730,7 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
         double hp[3] = { pose.x, pose.y, pose.theta };
         const int gen = ++ctx->generation;
         LGS_HIP_CHECK(hipMemcpyAsync(poses, hp, sizeof(hp), hipMemcpyHostToDevice, ctx->stream));
-        hipLaunchKernelGGL(k_cost, dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
+        hipLaunchKernelGGL(KCOST(cp), dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
                            scan->d_ranges, scan->d_angles, poses, cidx, terms, d_rec, ctx->guard_cap,
                            ctx->guard_eps, 0, 0, gen);
         LGS_HIP_CHECK(hipGetLastError());
@@ -1696,7 +1749,7 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
             }
             LGS_HIP_CHECK(hipMemcpyAsync(cidx, row.data(), sizeof(int4) * row.size(),
                                          hipMemcpyHostToDevice, ctx->stream));
-            hipLaunchKernelGGL(k_cost, dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
+            hipLaunchKernelGGL(KCOST(cp), dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
                                scan->d_ranges, scan->d_angles, poses, cidx, terms, d_rec,
                                ctx->guard_cap, ctx->guard_eps, 0, 1, gen);
             LGS_HIP_CHECK(hipGetLastError());
