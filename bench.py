@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--coarse-planes", type=int, default=1, help="A/B: 1 phase-plane coarse layout, 0 plain")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="match workload: concurrent HIP streams (lgs contexts) per GPU, one host thread each")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
     ap.add_argument("--timed-events", default="dominant", choices=["dominant", "all", "none"],
                     help="HIP-event timing inside the timed region: the roofline kernel only (default), "
@@ -178,51 +180,117 @@ def timed(budget_s, items, fn):
 
 
 # --------------------------------------------------------------------- match
+def cpu_threads():
+    """Host cores the CPU baseline may use: the box's share (OMP_NUM_THREADS is
+    set to it on the GPU box), else every core."""
+    return max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+
+
+def cpu_throughput(budget_s, items, fn, threads):
+    """Oracle throughput with `threads` independent workers (ctypes releases the
+    GIL inside the C oracle, so the workers run in parallel)."""
+    import threading
+    lock = threading.Lock()
+    queue = list(items)
+    times = []
+    t_start = time.perf_counter()
+
+    def worker():
+        while True:
+            with lock:
+                if not queue or (time.perf_counter() - t_start > budget_s and len(times) >= threads):
+                    return
+                it = queue.pop(0)
+            t0 = time.perf_counter()
+            fn(it)
+            with lock:
+                times.append(time.perf_counter() - t0)
+
+    th = [threading.Thread(target=worker) for _ in range(threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t_start
+    return len(times) / wall, times
+
+
 def run_match(args, D, ctx):
+    """S concurrent streams per GPU (one lgs_ctx each, driven from its own host
+    thread), each running complete OptimizePose(query) calls on its own scans:
+    the latency-bound small kernels of one match overlap another match's."""
+    import threading
     world = scene.make_world()
     ang = scene.beam_angles(1081)
     cells, mx, my = bench_map(world, ang)
     rng = np.random.default_rng(1000 + D.rank)
     scans, inits, truths = random_scans(world, ang, rng, min(args.warmup + args.steps, 256))
-    ctx.set_option(abi.LGS_OPT_COARSE_PLANES, args.coarse_planes)
-    grid = ctx.grid_from_array(cells, mx, my, 0.05)
-    dscans = [ctx.scan(r, ang) for r in scans]
+    S = max(1, args.streams)
+    ctxs = [ctx] + [abi.Context(D.local) for _ in range(S - 1)]
+    state = []
+    for c in ctxs:
+        c.set_option(abi.LGS_OPT_COARSE_PLANES, args.coarse_planes)
+        state.append((c, c.grid_from_array(cells, mx, my, 0.05), [c.scan(r, ang) for r in scans]))
     P, cost = abi.RtcsmParams(*PARAMS), abi.CostGEParams(*COST)
-    pick = lambda k: (dscans[k % len(dscans)], inits[k % len(dscans)])
-    for k in range(args.warmup):
-        s, i = pick(k)
-        ctx.optimize_pose_query(grid, P, cost, s, i)
-    set_timed_events(ctx, args, "k_coarse")
+    n = len(scans)
+    for c, g, ds in state:
+        for k in range(args.warmup):
+            c.optimize_pose_query(g, P, cost, ds[k % n], inits[k % n])
+        set_timed_events(c, args, "k_coarse")
     results = np.zeros((args.steps, 4))
-    lat = []
+    lat = [[] for _ in range(S)]
+
+    def stream(i):
+        c, g, ds = state[i]
+        for k in range(i, args.steps, S):
+            j = (args.warmup + k) % n
+            ts = time.perf_counter()
+            out = c.optimize_pose_query(g, P, cost, ds[j], inits[j])
+            lat[i].append(time.perf_counter() - ts)
+            e = out.estimated_pose
+            results[k] = (e.x, e.y, e.theta, out.score_max)
+
     D.barrier()
-    ctx.synchronize()
+    for c, _, _ in state:
+        c.synchronize()
+    th = [threading.Thread(target=stream, args=(i,)) for i in range(S)]
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        s, i = pick(args.warmup + k)
-        ts = time.perf_counter()
-        out = ctx.optimize_pose_query(grid, P, cost, s, i)
-        lat.append(time.perf_counter() - ts)
-        e = out.estimated_pose
-        results[k] = (e.x, e.y, e.theta, out.score_max)
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
     D.all_gather_rows(results)       # winning poses of every rank, over RCCL
-    ctx.synchronize()
     elapsed = D.max(time.perf_counter() - t0)
     D.barrier()
-    stats = ctx.kernel_stats()
-    # per-kernel table from a separate, fully event-timed pass (outside the timed region)
-    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
-    ctx.reset_stats()
+    stats = {}
+    for c, _, _ in state:            # k_coarse launches of every stream, event-timed on their own streams
+        for k, v in c.kernel_stats().items():
+            a = stats.setdefault(k, dict(launches=0, total_ms=0.0, algo_bytes=0.0))
+            for f in a:
+                a[f] += v[f]
+    # single-stream latency and the per-kernel table: a separate, fully
+    # event-timed pass on one stream (outside the timed region)
+    c0, g0, ds0 = state[0]
+    c0.set_option(abi.LGS_OPT_PROFILE_MASK, 0)
+    lat1 = []
+    for k in range(min(100, args.steps)):
+        j = (args.warmup + k) % n
+        ts = time.perf_counter()
+        c0.optimize_pose_query(g0, P, cost, ds0[j], inits[j])
+        lat1.append(time.perf_counter() - ts)
+    c0.set_option(abi.LGS_OPT_PROFILE, 1)
+    c0.reset_stats()
     for k in range(min(50, args.steps)):
-        s, i = pick(args.warmup + k)
-        ctx.optimize_pose_query(grid, P, cost, s, i)
-    all_stats = ctx.kernel_stats()
-    ctx.set_option(abi.LGS_OPT_PROFILE, 0)
+        j = (args.warmup + k) % n
+        c0.optimize_pose_query(g0, P, cost, ds0[j], inits[j])
+    all_stats = c0.kernel_stats()
+    c0.set_option(abi.LGS_OPT_PROFILE, 0)
     if "k_coarse" not in stats:
         stats = all_stats
     err = [max(abs(results[k, 0] - truths[(args.warmup + k) % len(truths)][0]),
                abs(results[k, 1] - truths[(args.warmup + k) % len(truths)][1])) for k in range(args.steps)]
     cpu = None
+    value = args.steps * D.world / elapsed
     if D.rank == 0 and not args.no_cpu and D.world == 1:
         ob = oracle_lib()
         g = ob.OGrid(cells, mx, my, 0.05)
@@ -231,14 +299,18 @@ def run_match(args, D, ctx):
         def one(k):
             out = ob.Summary()
             ob.lib().orc_rtcsm_optimize_pose_query(C.byref(g.g), C.byref(prm), C.byref(oc),
-                                                   C.byref(ob.OScan(scans[k], ang).s), ob.Pose(*inits[k]),
-                                                   C.byref(out))
-        rate, times = timed(args.cpu_seconds, range(min(len(scans), 24)), one)
-        cpu = dict(value=round(rate, 4), unit="scans/s", cores=1, kind="port",
-                   sample=f"{len(times)} config-2 scans through the oracle's OptimizePose(query) "
-                          f"(C restatement, -O2 -ffp-contract=off, 1 thread), p50 {1e3 * np.median(times):.1f} ms")
-    lat_ms = np.array(lat) * 1e3
-    value = args.steps * D.world / elapsed
+                                                   C.byref(ob.OScan(scans[k % n], ang).s),
+                                                   ob.Pose(*inits[k % n]), C.byref(out))
+        T = cpu_threads()
+        rate, times = cpu_throughput(args.cpu_seconds, range(4 * T), one, T)
+        cpu = dict(value=round(rate, 4), unit="scans/s", cores=T, kind="port",
+                   sample=f"{len(times)} config-2 scans through the oracle's OptimizePose(query) (C restatement, "
+                          f"-O2 -ffp-contract=off) on {T} threads, one independent scan per thread; "
+                          f"single-scan p50 {1e3 * np.median(times):.1f} ms",
+                   speedup=round(value / rate, 1),
+                   single_core_scans_per_s=round(1.0 / float(np.median(times)), 4),
+                   speedup_vs_single_core=round(value * float(np.median(times)), 1))
+    lat_ms = np.array([x for l in lat for x in l]) * 1e3
     line = dict(
         metric=METRIC, value=round(value, 2), unit="scans/s", n_gpus=D.world, steps=args.steps,
         warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 4), higher_is_better=True,
@@ -247,14 +319,16 @@ def run_match(args, D, ctx):
         config=dict(workload="config2: 1081-beam scan, +-2 m/+-30 deg correlative match (OptimizePose(query)) "
                              "vs 1000x1000@5cm grid, PatchSize 100",
                     beams=1081, grid=[1000, 1000], resolution=0.05, low_resolution=5,
-                    search_range=[4.0, 4.0, 1.0471976], scans_per_rank=args.steps,
-                    parallelism=f"replicas x{D.world} (independent scans per rank) + RCCL all-gather of poses"),
+                    search_range=[4.0, 4.0, 1.0471976], scans_per_rank=args.steps, streams_per_gpu=S,
+                    parallelism=f"replicas x{D.world} (independent scans per rank), {S} concurrent HIP streams "
+                                f"per GPU (one OptimizePose(query) per scan each) + RCCL all-gather of poses"),
         p50_scan_match_ms=round(float(np.percentile(lat_ms, 50)), 4),
         p90_scan_match_ms=round(float(np.percentile(lat_ms, 90)), 4),
+        p50_scan_match_ms_single_stream=round(1e3 * float(np.median(lat1)), 4),
         roofline=roofline_from(stats, "k_coarse", args.pmc), cpu_baseline=cpu,
         pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events)
-    if cpu:
-        cpu["speedup"] = round(value / cpu["value"], 1)
+    for c in ctxs[1:]:
+        c.close()
     return line, all_stats, value
 
 
