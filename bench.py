@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--coarse-planes", type=int, default=1, help="A/B: 1 phase-plane coarse layout, 0 plain")
+    ap.add_argument("--spin-sync", type=int, default=1, help="1 spin on the stream when waiting, 0 blocking wait")
+    ap.add_argument("--super-prune", type=int, default=1,
+                    help="A/B: 1 superblock pruning of the coarse stage, 0 score every coarse block")
     ap.add_argument("--streams", type=int, default=3,
                     help="match workload: concurrent HIP streams (lgs contexts) per GPU, one host thread each")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
@@ -230,6 +233,8 @@ def run_match(args, D, ctx):
     state = []
     for c in ctxs:
         c.set_option(abi.LGS_OPT_COARSE_PLANES, args.coarse_planes)
+        c.set_option(abi.LGS_OPT_SUPER_PRUNE, args.super_prune)
+        c.set_option(abi.LGS_OPT_SPIN_SYNC, args.spin_sync)
         state.append((c, c.grid_from_array(cells, mx, my, 0.05), [c.scan(r, ang) for r in scans]))
     P, cost = abi.RtcsmParams(*PARAMS), abi.CostGEParams(*COST)
     n = len(scans)
@@ -237,7 +242,7 @@ def run_match(args, D, ctx):
         for k in range(args.warmup):
             c.optimize_pose_query(g, P, cost, ds[k % n], inits[k % n])
         set_timed_events(c, args, "k_coarse")
-    results = np.zeros((args.steps, 4))
+    results = np.zeros((args.steps, 6))
     lat = [[] for _ in range(S)]
 
     def stream(i):
@@ -248,7 +253,7 @@ def run_match(args, D, ctx):
             out = c.optimize_pose_query(g, P, cost, ds[j], inits[j])
             lat[i].append(time.perf_counter() - ts)
             e = out.estimated_pose
-            results[k] = (e.x, e.y, e.theta, out.score_max)
+            results[k] = (e.x, e.y, e.theta, out.score_max, out.coarse_blocks, out.fine_blocks)
 
     D.barrier()
     for c, _, _ in state:
@@ -326,7 +331,10 @@ def run_match(args, D, ctx):
         p90_scan_match_ms=round(float(np.percentile(lat_ms, 90)), 4),
         p50_scan_match_ms_single_stream=round(1e3 * float(np.median(lat1)), 4),
         roofline=roofline_from(stats, "k_coarse", args.pmc), cpu_baseline=cpu,
-        pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events)
+        pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events,
+        super_prune=bool(args.super_prune),
+        coarse_blocks_scored_mean=round(float(results[:, 4].mean()), 1),
+        fine_blocks_refined_mean=round(float(results[:, 5].mean()), 1))
     for c in ctxs[1:]:
         c.close()
     return line, all_stats, value

@@ -116,7 +116,7 @@ typedef struct {
     int win[3];                   /* winX, winY, winTheta */
     double steps[3];              /* stepX, stepY, stepTheta */
     lgs_pose2d best_sensor_pose;
-    int64_t coarse_blocks;        /* coarse poses scored (all of them) */
+    int64_t coarse_blocks;        /* coarse blocks scored: all of them, or those superblock pruning kept */
     int64_t fine_blocks;          /* coarse blocks refined on the fine map */
     int guard_hits;               /* projections near a cell boundary re-checked on host */
     int fixups;                   /* 1 if any device index differed from glibc and was patched */
@@ -144,6 +144,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_COARSE_PLANES 6   /* 1 (default) = phase-plane coarse layout, 0 = plain layout (A/B) */
 #define LGS_OPT_PROFILE_MASK  7   /* time only the kernels whose lgs_kernel_stat index bit is set (0 = off) */
 #define LGS_OPT_SPIN_SYNC     8   /* 1 (default) = spin on the stream when waiting for results, 0 = blocking wait */
+#define LGS_OPT_SUPER_PRUNE   9   /* 1 (default) = skip coarse blocks whose 4x4-superblock bound is below the seed score, 0 = evaluate every coarse block */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is

@@ -45,6 +45,7 @@ namespace {
 
 
 constexpr int kPipe = 16;   // seq_sum gathers in flight per batch (index arrays padded by 2*kPipe)
+constexpr int kPad = 4 * kPipe;   // cbase padding past the last row (seq_sum4's look-ahead)
 
 // Generation-tagged counter (gen << 32 | count): a word left by an earlier
 // match counts as zero, so records need no memset.  Returns this caller's slot.
@@ -80,6 +81,23 @@ __device__ __forceinline__ int floor_div(int a, int b) { return (a >= 0) ? a / b
 // otherwise every read is 0.0 (GridMap::Value out of bounds) and the base
 // points at the all-zero top-left margin of plane 0.  The coarse lanes then
 // read base + jy * Wqp + jx with no bounds test.
+// Superblock base of the same beam in the compact superblock planes: the
+// padded position (Qx, Qy) of its lattice start, in sub-phase (Qx & 3, Qy & 3)
+// at (Qx >> 2, Qy >> 2); superblock (a, b) is then base + b * Wq4 + a.  0 (an
+// all-zero margin corner) when the coarse window misses the map.
+__device__ __forceinline__ int super_base(int ix, int iy, const RtcsmPlan& pl)
+{
+    const int lr = pl.low_res;
+    const int bx = ix - pl.win_x, by = iy - pl.win_y;
+    const int qx0 = floor_div(bx, lr), qy0 = floor_div(by, lr);
+    const int rx = bx - lr * qx0, ry = by - lr * qy0;
+    const bool touches = (qx0 < pl.Wq) & (qx0 + pl.ncx > 0) & (qy0 < pl.Hq) & (qy0 + pl.ncy > 0);
+    const int Qx = qx0 + pl.M, Qy = qy0 + pl.M;
+    return touches ? (int)((ry * lr + rx) * pl.pstride4 + ((Qy & 3) * 4 + (Qx & 3)) * pl.sub4 +
+                           (long long)(Qy >> 2) * pl.Wq4 + (Qx >> 2))
+                   : 0;
+}
+
 __device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
 {
     const int lr = pl.low_res;
@@ -93,7 +111,10 @@ __device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
 // blockDim == 256.  ComputeScanIndices keeps the beams with range <
 // ScanRangeMax, in beam order (:192-193); each block finds its 256 valid
 // beams v0..v0+255 with a block-wide prefix count over the scan (no host
-// upload of the compaction).
+// upload of the compaction), then projects them for kProjRows search angles
+// (fewer, longer waves: the GPU's wave slots, not its ALUs, are what
+// concurrent matches compete for).
+constexpr int kProjRows = 4;
 __global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __restrict__ ranges,
                                                  const double* __restrict__ angles,
                                                  int2* __restrict__ idx, int* __restrict__ cbase,
@@ -126,14 +147,18 @@ __global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __r
         }
     __syncthreads();
     const int v = v0 + tid;
-    const int tt = blockIdx.y;
-    // seq_sum's look-ahead reads up to 2*kPipe entries past the last row:
+    // seq_sum's look-ahead reads up to kPad entries past the last row:
     // keep them at the zero margin (base 0)
-    if (blockIdx.x == 0 && tt == 0 && tid < 2 * kPipe) cbase[(size_t)pl.T * pl.Nv + tid] = 0;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid < kPad) {
+        cbase[(size_t)pl.T * pl.Nv + tid] = 0;
+        cbase[pl.sb_off + (size_t)pl.T * pl.Nv + tid] = 0;
+    }
     if (v >= pl.Nv) return;
     const int i = s_map[tid];
     const double r = ranges[i];
     const double a = angles[i];
+    const int tt1 = min(pl.T, (int)(blockIdx.y + 1) * kProjRows);
+    for (int tt = blockIdx.y * kProjRows; tt < tt1; ++tt) {
     const int t = tt - pl.win_t;
     // currentSensorPose.mTheta = sensorPose.mTheta + stepTheta * t (:90-91)
     const double th = pl.st + pl.step_t * (double)t;
@@ -161,9 +186,11 @@ __global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __r
     const size_t o = (size_t)tt * pl.Nv + v;
     idx[o] = make_int2(ix, iy);
     cbase[o] = coarse_base(ix, iy, pl);
+    cbase[pl.sb_off + o] = super_base(ix, iy, pl);
     // this angle has a beam whose coarse lattice starts left of / below the
     // map: k_coarse must run its unsafe-block check (generation-stamped flag)
     if (ix - pl.win_x < 0 || iy - pl.win_y < 0) tedge[tt] = gen;
+    }
 }
 
 __global__ void k_patch(RtcsmPlan pl, int2* __restrict__ idx, int* __restrict__ cbase,
@@ -176,6 +203,7 @@ __global__ void k_patch(RtcsmPlan pl, int2* __restrict__ idx, int* __restrict__ 
     const size_t o = (size_t)p.x * pl.Nv + p.y;
     idx[o] = make_int2(p.z, p.w);
     cbase[o] = coarse_base(p.z, p.w, pl);
+    cbase[pl.sb_off + o] = super_base(p.z, p.w, pl);
     if (p.z - pl.win_x < 0 || p.w - pl.win_y < 0) tedge[p.x] = gen;
 }
 
@@ -184,10 +212,14 @@ __global__ void k_cinfo(RtcsmPlan pl, const int2* __restrict__ idx, int* __restr
                         int* __restrict__ tedge, int gen)
 {
     const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (o < 2 * kPipe) cbase[(size_t)pl.T * pl.Nv + o] = 0;
+    if (o < kPad) {
+        cbase[(size_t)pl.T * pl.Nv + o] = 0;
+        cbase[pl.sb_off + (size_t)pl.T * pl.Nv + o] = 0;
+    }
     if (o >= (size_t)pl.T * pl.Nv) return;
     const int2 q = idx[o];
     cbase[o] = coarse_base(q.x, q.y, pl);
+    cbase[pl.sb_off + o] = super_base(q.x, q.y, pl);
     if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0) tedge[o / pl.Nv] = gen;
 }
 
@@ -201,6 +233,10 @@ __global__ void k_cost_patch(int4* __restrict__ cidx, const int4* __restrict__ p
 // --------------------------------------------------------------------------
 // wave/block argmax helpers: max value, ties -> smallest key
 // --------------------------------------------------------------------------
+__device__ __forceinline__ double dmax2(double a, double b) { return (a < b) ? b : a; }
+
+constexpr int kSB = 4;   // superblock = kSB x kSB coarse blocks
+
 __device__ __forceinline__ bool better(double a, long long ka, double b, long long kb)
 {
     return (a > b) || (a == b && ka < kb);
@@ -316,6 +352,32 @@ __device__ __forceinline__ double seq_sum(int n, Fetch fetch, Addr addr)
     return s;
 }
 
+// Four batches in flight (for kernels with few waves, where one wave's
+// latency is the kernel's duration): look-ahead up to 4*kPipe entries.
+template <class Rec, class Fetch, class Addr>
+__device__ __forceinline__ double seq_sum4(int n, Fetch fetch, Addr addr)
+{
+    double a[kPipe], b[kPipe], c[kPipe], d[kPipe];
+    double s = 0.0;
+    issue_batch<Rec>(0, fetch, addr, a);
+    issue_batch<Rec>(kPipe, fetch, addr, b);
+    issue_batch<Rec>(2 * kPipe, fetch, addr, c);
+    for (int v0 = 0; v0 < n; v0 += 4 * kPipe) {
+        issue_batch<Rec>(v0 + 3 * kPipe, fetch, addr, d);
+        add_batch(s, a, n - v0);
+        if (v0 + kPipe >= n) break;
+        issue_batch<Rec>(v0 + 4 * kPipe, fetch, addr, a);
+        add_batch(s, b, n - v0 - kPipe);
+        if (v0 + 2 * kPipe >= n) break;
+        issue_batch<Rec>(v0 + 5 * kPipe, fetch, addr, b);
+        add_batch(s, c, n - v0 - 2 * kPipe);
+        if (v0 + 3 * kPipe >= n) break;
+        issue_batch<Rec>(v0 + 6 * kPipe, fetch, addr, c);
+        add_batch(s, d, n - v0 - 3 * kPipe);
+    }
+    return s;
+}
+
 // --------------------------------------------------------------------------
 // k_coarse: one lane per coarse block (t, jx, jy) of one search angle t per
 // workgroup (blockDim = P rounded up to 64); lanes sweep jx fastest.  Each lane
@@ -324,28 +386,64 @@ __device__ __forceinline__ double seq_sum(int n, Fetch fetch, Addr addr)
 //               doubles of one plane;
 //   PLANES = 0: the coarse map as is (stride lr between lanes).
 // --------------------------------------------------------------------------
-template <int PLANES>
-__global__ __launch_bounds__(1024) void k_coarse(
+//   SBMAP = 1: superblock pruning (k_super / k_seed_super ran first): lanes
+//               are ordered superblock-major (4x4 blocks per superblock, 4
+//               superblocks per wave); a block whose superblock bound is < L
+//               is not evaluated (cscore = -inf, so k_select never takes it),
+//               and a wave with no surviving block skips the beam loop.  Rows
+//               that can hold unsafe blocks (tedge) are never pruned.
+template <int PLANES, int SBMAP>
+__global__ __launch_bounds__(SBMAP ? 256 : 1024) void k_coarse(
     RtcsmPlan pl, const double* __restrict__ cmap, const int2* __restrict__ idx,
     const int* __restrict__ cbase, const double* __restrict__ zero,
     const int* __restrict__ tedge, int gen, double* __restrict__ cscore,
-    uint8_t* __restrict__ cflag, double* __restrict__ part_c, long long* __restrict__ part_k)
+    uint8_t* __restrict__ cflag, double* __restrict__ part_c, long long* __restrict__ part_k,
+    const double* __restrict__ sbound, const double* __restrict__ Lp, RtcsmRecord* rec)
 {
     __shared__ double sv[16];
     __shared__ long long sk[16];
     const int tt = blockIdx.y;
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool active = p < pl.P;
-    const int jx = active ? p % pl.ncx : 0;
-    const int jy = active ? p / pl.ncx : 0;
+    bool active;
+    int jx, jy;
+    bool keep = true;
+    if constexpr (SBMAP) {
+        const int nsb2 = pl.nsbx * pl.nsby;
+        const int sb = p >> 4, m = p & 15;
+        const int a = sb % pl.nsbx, b = sb / pl.nsbx;
+        jx = kSB * a + (m & 3);
+        jy = kSB * b + (m >> 2);
+        active = (sb < nsb2) & (jx < pl.ncx) & (jy < pl.ncy);
+        if (!active) jx = jy = 0;
+        // safe rows only: sbound >= c for every block of the superblock
+        // (k_super); k_select takes a safe block only if c > thr and c >= L
+        if (tedge[tt] != gen && active) {
+            const double bnd = sbound[(size_t)tt * nsb2 + sb];
+            keep = (bnd > pl.thr) && (bnd >= *Lp);
+        }
+    } else {
+        active = p < pl.P;
+        jx = active ? p % pl.ncx : 0;
+        jy = active ? p / pl.ncx : 0;
+    }
     const int lr = pl.low_res;
     const int W = pl.W, H = pl.H;
     const size_t o = (size_t)tt * pl.Nv;
     const int2* __restrict__ id = idx + o;
     const int* __restrict__ cb = cbase + o;
 
-    double sum;
-    if (PLANES) {
+    double sum = 0.0;
+    if constexpr (SBMAP) {
+        const bool kp = active && keep;
+        const unsigned long long live = __ballot(kp);
+        if (live != 0ull) {
+            // dropped lanes of a live wave all read the zero cell
+            const double* __restrict__ lane_base = cmap + (jy * pl.Wqp + jx);
+            sum = seq_sum4<int>(pl.Nv, [&](int v) { return cb[v]; },
+                                [&](const int& c) { return kp ? lane_base + c : zero; });
+            if ((threadIdx.x & 63) == 0) atomicAdd(&rec->coarse_evals, (unsigned long long)__popcll(live));
+        }
+    } else if (PLANES) {
         const double* __restrict__ lane_base = cmap + (jy * pl.Wqp + jx);
         sum = seq_sum<int>(pl.Nv, [&](int v) { return cb[v]; }, [&](const int& c) { return lane_base + c; });
     } else {
@@ -373,14 +471,129 @@ __global__ __launch_bounds__(1024) void k_coarse(
     }
     const long long k = (long long)tt * pl.P + (long long)jx * pl.ncy + jy;
     if (active) {
-        cscore[k] = sum;
+        cscore[k] = keep ? sum : -INFINITY;
         cflag[k] = unsafe ? 1 : 0;
     }
-    double bv = (active && !unsafe) ? sum : -1.0;
-    long long bk = (active && !unsafe) ? k : LLONG_MAX;
-    block_argmax(bv, bk, sv, sk);
-    if (threadIdx.x == 0) {
-        const int part = blockIdx.y * gridDim.x + blockIdx.x;
+    if constexpr (!SBMAP) {
+        double bv = (active && !unsafe) ? sum : -1.0;
+        long long bk = (active && !unsafe) ? k : LLONG_MAX;
+        block_argmax(bv, bk, sv, sk);
+        if (threadIdx.x == 0) {
+            const int part = blockIdx.y * gridDim.x + blockIdx.x;
+            part_c[part] = bv;
+            part_k[part] = bk;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// Superblock pruning.  A superblock is kSB x kSB coarse
+// blocks of one angle.  Its bound, for beam v, reads the super planes (the
+// forward kSB x kSB max of the padded coarse planes) at the superblock's
+// corner, which is >= the coarse value of every member block at that beam.
+// fp64 addition is monotone, so the reference-order sum of the member's
+// coarse values is <= the reference-order sum of these super values, which is
+// <= (any-order sum) * (1 + 8 n eps) for n nonnegative terms: sbound =
+// parallel sum * pl.sb_mult bounds every member's coarse score.  A safe block
+// with c < L is never selected, so superblocks with sbound < L are skipped.
+// --------------------------------------------------------------------------
+// The bound needs nonnegative terms (occupancy probabilities are); a negative
+// cell stamps *negflag with this build's generation and k_super then keeps
+// every superblock.  NaN cells are skipped by the max: a block whose sum is
+// NaN fails c > thr and is never selected anyway.
+constexpr int kSPX = 64, kSPY = 32;   // output tile of k_super_planes
+
+__global__ __launch_bounds__(256) void k_super_planes(const double* __restrict__ P, double* __restrict__ S,
+                                                      RtcsmPlan pl, int* __restrict__ negflag, int pgen)
+{
+    const int Wqp = pl.Wqp, Hqp = pl.Hqp;
+    const long long pstride = pl.pstride;
+    constexpr int TW = kSPX + kSB - 1, TH = kSPY + kSB - 1;
+    __shared__ double tile[TH][TW];
+    __shared__ double hm[TH][kSPX];
+    const int x0 = blockIdx.x * kSPX, y0 = blockIdx.y * kSPY;
+    const double* __restrict__ base = P + blockIdx.z * pstride;
+    double* __restrict__ out = S + blockIdx.z * pl.pstride4;
+    const int tid = threadIdx.x;
+    bool neg = false;
+    for (int k = tid; k < TH * TW; k += blockDim.x) {
+        const int yy = k / TW, xx = k % TW;
+        const int x = x0 + xx, y = y0 + yy;
+        const double c = (x < Wqp && y < Hqp) ? base[(long long)y * Wqp + x] : 0.0;   // 0 past the plane
+        neg |= c < 0.0;
+        tile[yy][xx] = c;
+    }
+    __syncthreads();
+    for (int k = tid; k < TH * kSPX; k += blockDim.x) {
+        const int yy = k / kSPX, xx = k % kSPX;
+        double m = tile[yy][xx];
+#pragma unroll
+        for (int i = 1; i < kSB; ++i) m = dmax2(m, tile[yy][xx + i]);
+        hm[yy][xx] = m;
+    }
+    __syncthreads();
+    for (int k = tid; k < kSPY * kSPX; k += blockDim.x) {
+        const int yy = k / kSPX, xx = k % kSPX;
+        const int x = x0 + xx, y = y0 + yy;
+        if (x >= Wqp || y >= Hqp) continue;
+        double m = hm[yy][xx];
+#pragma unroll
+        for (int j = 1; j < kSB; ++j) m = dmax2(m, hm[yy + j][xx]);
+        out[((y & 3) * 4 + (x & 3)) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + (x >> 2)] = m;
+    }
+    if (neg) *negflag = pgen;
+}
+
+// One workgroup (kSupWaves waves) per (64 superblocks, search angle): lane =
+// superblock, wave w sums a quarter of the beams (any order: the bound
+// absorbs the rounding; four batches of gathers in flight), LDS reduction
+// over the waves.  Also the chunk's best superblock for the seed (-inf in
+// rows that may hold unsafe blocks).
+constexpr int kSupWaves = 4;
+__global__ __launch_bounds__(64 * kSupWaves) void k_super(RtcsmPlan pl, const double* __restrict__ sp,
+                                                const int* __restrict__ cbase, const double* __restrict__ zero,
+                                                const int* __restrict__ tedge, int gen,
+                                                const int* __restrict__ negflag, int pgen,
+                                                double* __restrict__ sbound, double* __restrict__ part_c,
+                                                long long* __restrict__ part_k)
+{
+    __shared__ double red[kSupWaves][64];
+    const int t = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nsb2 = pl.nsbx * pl.nsby;
+    const int sbi = blockIdx.x * 64 + lane;
+    const bool act = sbi < nsb2;
+    const int a = act ? sbi % pl.nsbx : 0, b = act ? sbi / pl.nsbx : 0;
+    const double* __restrict__ lb = sp + (b * pl.Wq4 + a);
+    // wave w: a contiguous beam range (wave-uniform index loads, pipelined
+    // gathers); cbase rows are padded for seq_sum's look-ahead
+    const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
+    const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
+    const int* __restrict__ cb = cbase + pl.sb_off + (size_t)t * pl.Nv + lo;
+    double s = 0.0;
+    if (cnt > 0)
+        s = seq_sum4<int>(cnt, [&](int v) { return cb[v]; }, [&](const int& c) { return act ? lb + c : zero; });
+    red[w][lane] = s;
+    __syncthreads();
+    if (w != 0) return;
+    double tot = 0.0;
+    for (int j = 0; j < kSupWaves; ++j) tot += red[j][lane];
+    const double bound = (*negflag == pgen) ? INFINITY : tot * pl.sb_mult;
+    if (act) sbound[(size_t)t * nsb2 + sbi] = bound;
+    // rows that may hold unsafe blocks never seed: -inf (bounds are >= 0)
+    const bool seedable = act && tedge[t] != gen;
+    double bv = seedable ? bound : -INFINITY;
+    long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(bv, off, 64);
+        const long long ok = __shfl_xor(bk, off, 64);
+        if (better(ov, ok, bv, bk)) {
+            bv = ov;
+            bk = ok;
+        }
+    }
+    if (lane == 0) {
+        const int part = t * gridDim.x + blockIdx.x;
         part_c[part] = bv;
         part_k[part] = bk;
     }
@@ -616,6 +829,182 @@ __global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_seed(
     else
         eval_block(pl, grid, idx, zero, bk, (int2*)smem, f, pos);
     if (threadIdx.x == 0) *Lout = f;
+}
+
+// k_seed_super (superblock pruning), one 1024-thread workgroup:
+//  1. the kSeedCands best superblocks above thr among k_super's per-chunk
+//     bests (rows that may hold unsafe blocks are excluded there);
+//  2. their members' coarse scores summed in any order (they only choose
+//     which block to refine: any safe block's fine max is a valid L);
+//  3. the best member's lr x lr fine scores, also summed in any order, each
+//     lowered by its rounding bound (4 (Nv + 2) eps sum|x| >= the gap to the
+//     reference-order sum), so L <= that block's exact fine max <= the
+//     reference's final score.
+// No candidate: L = -inf (k_coarse still drops superblocks with bound <= thr).
+// Every loop issues its loads in independent batches of 16: one workgroup,
+// so the kernel's duration is its latency chain.
+// Also clears the record's evaluated-block counter for k_coarse.
+// LDS: the candidate rows' cbase (kSeedCands * Nv ints), then the block's
+// index row (Nv int2) in the same space.
+constexpr int kSeedCands = 4;
+constexpr int kSeedMaxNv = 2048;   // LDS: kSeedCands * Nv ints
+constexpr int kSeedRegParts = 4;   // parts held in registers per thread
+
+__global__ __launch_bounds__(1024) void k_seed_super(
+    RtcsmPlan pl, const double* __restrict__ grid, const int2* __restrict__ idx,
+    const double* __restrict__ zero, const double* __restrict__ cmap, const int* __restrict__ cbase,
+    const double* __restrict__ part_c, const long long* __restrict__ part_k, int nparts,
+    double* __restrict__ Lout, RtcsmRecord* rec)
+{
+    extern __shared__ char smem[];
+    __shared__ double sv[16];
+    __shared__ long long sk[16];
+    __shared__ long long cand[kSeedCands];
+    __shared__ double red[1024];
+    __shared__ double reda[1024];
+    const int tid = threadIdx.x;
+    const int nsb2 = pl.nsbx * pl.nsby;
+    if (tid == 0) rec->coarse_evals = 0ull;
+    double pv[kSeedRegParts];
+    long long pk[kSeedRegParts];
+#pragma unroll
+    for (int j = 0; j < kSeedRegParts; ++j) {
+        const int i = tid + j * 1024;
+        pv[j] = (i < nparts) ? part_c[i] : -INFINITY;
+        pk[j] = (i < nparts) ? part_k[i] : LLONG_MAX;
+    }
+    int nc = 0;
+    for (; nc < kSeedCands; ++nc) {
+        double bv = -INFINITY;
+        long long bk = LLONG_MAX;
+#pragma unroll
+        for (int j = 0; j < kSeedRegParts; ++j)
+            if (better(pv[j], pk[j], bv, bk)) {
+                bv = pv[j];
+                bk = pk[j];
+            }
+        for (int i = tid + kSeedRegParts * 1024; i < nparts; i += 1024) {   // large searches only
+            bool taken = false;
+            for (int j = 0; j < nc; ++j) taken |= cand[j] == part_k[i];
+            if (!taken && better(part_c[i], part_k[i], bv, bk)) {
+                bv = part_c[i];
+                bk = part_k[i];
+            }
+        }
+        block_argmax(bv, bk, sv, sk);
+        if (bk == LLONG_MAX || bv == -INFINITY || !(bv > pl.thr)) break;   // uniform
+        if (tid == 0) cand[nc] = bk;
+#pragma unroll
+        for (int j = 0; j < kSeedRegParts; ++j)
+            if (pk[j] == bk) pv[j] = -INFINITY, pk[j] = LLONG_MAX;
+        __syncthreads();
+    }
+    if (nc == 0) {
+        if (tid == 0) *Lout = -INFINITY;
+        return;
+    }
+    // 2. member sums: member m = tid % 64 (candidate m / 16), beam group tid / 64
+    const int Nv = pl.Nv;
+    int* srow = (int*)smem;   // [kSeedCands][Nv]
+    for (int i = tid; i < nc * Nv; i += blockDim.x)
+        srow[i] = cbase[(size_t)(cand[i / Nv] / nsb2) * Nv + (i % Nv)];
+    __syncthreads();
+    {
+        const int m = tid & 63, g = tid >> 6;
+        const int ci = m >> 4, mem = m & 15;
+        bool valid = ci < nc;
+        int jx = 0, jy = 0;
+        if (valid) {
+            const int sb = (int)(cand[ci] % nsb2);
+            jx = kSB * (sb % pl.nsbx) + (mem & 3);
+            jy = kSB * (sb / pl.nsbx) + (mem >> 2);
+            valid = jx < pl.ncx && jy < pl.ncy;
+        }
+        double s = 0.0;
+        if (valid) {
+            const double* __restrict__ lb = cmap + (jy * pl.Wqp + jx);
+            const int* row = srow + ci * Nv;
+            const int cnt = (g < Nv) ? (Nv - g + 15) / 16 : 0;   // beams g, g + 16, ...
+            double acc[4] = { 0.0, 0.0, 0.0, 0.0 };
+            for (int i0 = 0; i0 < cnt; i0 += 16) {
+                double buf[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int i = min(i0 + j, cnt - 1);
+                    buf[j] = (i0 + j < cnt) ? lb[row[g + 16 * i]] : 0.0;
+                }
+#pragma unroll
+                for (int j = 0; j < 16; ++j) acc[j & 3] += buf[j];
+            }
+            s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        }
+        red[tid] = s;
+        __syncthreads();
+        double mv = -1.0;
+        long long mk = LLONG_MAX;
+        if (tid < 64) {
+            double tot = 0.0;
+            for (int j = 0; j < 16; ++j) tot += red[j * 64 + tid];
+            if (valid) {
+                mv = tot;
+                mk = (cand[ci] / nsb2) * (long long)pl.P + (long long)jx * pl.ncy + jy;
+            }
+        }
+        block_argmax(mv, mk, sv, sk);
+        if (tid == 0) cand[0] = mk;
+        __syncthreads();
+    }
+    // 3. fine scores of block cand[0], any order, rounding-bounded
+    const long long k = cand[0];
+    const int tt = (int)(k / pl.P);
+    const int rem = (int)(k % pl.P);
+    const int bjx = rem / pl.ncy, bjy = rem % pl.ncy;
+    const int lr = pl.low_res, npose = lr * lr;
+    int2* sidx = (int2*)smem;   // [Nv]
+    __syncthreads();
+    for (int v = tid; v < Nv; v += blockDim.x) sidx[v] = idx[(size_t)tt * Nv + v];
+    __syncthreads();
+    int QP = 1;
+    while (QP < npose) QP <<= 1;   // npose <= 1024
+    const int G = (int)blockDim.x / QP;
+    const int q = tid % QP, g = tid / QP;
+    double s = 0.0, a = 0.0;
+    if (q < npose) {
+        const int xo = q % lr, yo = q / lr;
+        const int xf = -pl.win_x + bjx * lr + xo, yf = -pl.win_y + bjy * lr + yo;
+        const int W = pl.W, H = pl.H;
+        const int cnt = (g < Nv) ? (Nv - g + G - 1) / G : 0;   // beams g, g + G, ...
+        for (int i0 = 0; i0 < cnt; i0 += 16) {
+            double buf[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int2 c = sidx[g + G * min(i0 + j, cnt - 1)];
+                const int x = c.x + xf, y = c.y + yf;
+                const bool inb = (i0 + j < cnt) & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
+                buf[j] = *(inb ? grid + (unsigned)(y * W + x) : zero);
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                s += buf[j];
+                a += fabs(buf[j]);
+            }
+        }
+    }
+    red[tid] = s;
+    reda[tid] = a;
+    __syncthreads();
+    double lv = -INFINITY;
+    if (tid < npose) {
+        double ts = 0.0, ta = 0.0;
+        for (int j = 0; j < G; ++j) {
+            ts += red[j * QP + tid];
+            ta += reda[j * QP + tid];
+        }
+        lv = ts - (4.0 * (double)(Nv + 2) * 0x1p-53) * ta;
+    }
+    long long dummy = tid;
+    block_argmax(lv, dummy, sv, sk);
+    if (tid == 0) *Lout = lv;
 }
 
 // k_select: one workgroup per segment of kSelSeg consecutive blocks.  The
@@ -992,11 +1381,18 @@ void set_plane_layout(RtcsmPlan& pl)
 {
     pl.Wq = (pl.W + pl.low_res - 1) / pl.low_res;
     pl.Hq = (pl.H + pl.low_res - 1) / pl.low_res;
-    pl.M = std::max(pl.ncx, pl.ncy);
+    // margins also cover the superblock reads (kSB * nsb coarse blocks per axis)
+    pl.nsbx = (pl.ncx + kSB - 1) / kSB;
+    pl.nsby = (pl.ncy + kSB - 1) / kSB;
+    pl.M = std::max(kSB * pl.nsbx, kSB * pl.nsby);
     pl.Wqp = pl.Wq + 2 * pl.M;
     pl.Hqp = pl.Hq + 2 * pl.M;
     pl.pstride = (long long)pl.Wqp * pl.Hqp;
-    LGS_REQUIRE((long long)pl.low_res * pl.low_res * pl.pstride < (1LL << 31),
+    pl.Wq4 = (pl.Wqp + 3) / 4;
+    pl.Hq4 = (pl.Hqp + 3) / 4;
+    pl.sub4 = (long long)pl.Wq4 * pl.Hq4;
+    pl.pstride4 = 16 * pl.sub4;
+    LGS_REQUIRE((long long)pl.low_res * pl.low_res * pl.pstride4 < (1LL << 31),
                 "coarse map too large for 32-bit plane offsets");
 }
 
@@ -1036,6 +1432,8 @@ RtcsmPlan make_plan(const lgs_grid* grid, const lgs_rtcsm_params* p, const lgs_s
     pl.N = scan->n;
     pl.rmax = p->scan_range_max;
     set_plane_layout(pl);
+    pl.sb_mult = 1.0 + 4.0 * (double)(nv + 1) * 0x1p-53;
+    pl.sb_off = (long long)pl.T * std::max(nv, 1) + kPad;   // == ensure_workspace's nidx
     return pl;
 }
 
@@ -1092,6 +1490,9 @@ struct Workspace {
     double* terms;
     int nparts;
     double* decim;      // padded phase planes
+    double* super;      // superblock planes (same layout)
+    double* sbound;     // [T * nsb2]
+    int* negflag;
     double* zero;
     int* tedge;
 };
@@ -1122,11 +1523,16 @@ Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
     const int tiles = (pl.P + cb - 1) / cb;
     w.nparts = tiles * pl.T;
     w.decim = ctx->coarse_planes ? planes_buffer(ctx, pl) : nullptr;
+    const int nsb2 = pl.nsbx * pl.nsby;
+    // part arrays: k_coarse's per-tile bests (w.nparts) or k_super's per-chunk bests
+    const size_t part_alloc = (size_t)std::max(w.nparts, (nsb2 + 63) / 64 * pl.T);
+    w.super = (double*)ctx->ensure(S_SUPER, sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
+    w.sbound = (double*)ctx->ensure(S_SBOUND, sizeof(double) * (size_t)pl.T * nsb2);
     const size_t K = (size_t)pl.K;
     // index arrays padded by 2*kPipe entries: seq_sum's look-ahead loads
-    const size_t nidx = (size_t)pl.T * std::max(pl.Nv, 1) + 2 * kPipe;
+    const size_t nidx = (size_t)pl.T * std::max(pl.Nv, 1) + kPad;
     w.idx = (int2*)ctx->ensure(S_IDX, sizeof(int2) * nidx);
-    w.cbase = (int*)ctx->ensure(S_CINFO, sizeof(int) * nidx);
+    w.cbase = (int*)ctx->ensure(S_CINFO, sizeof(int) * 2 * nidx);   // coarse bases, then superblock bases
     w.cscore = (double*)ctx->ensure(S_CSCORE, sizeof(double) * K);
     w.cflag = (uint8_t*)ctx->ensure(S_CFLAG, K);
     w.nseg = (int)((K + kSelSeg - 1) / kSelSeg);
@@ -1134,17 +1540,40 @@ Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
     w.list = (int*)ctx->ensure(S_LIST, sizeof(int) * (size_t)w.nseg * kSelSeg);
     w.fval = (double*)ctx->ensure(S_FVAL, sizeof(double) * K);
     w.fpos = (int*)ctx->ensure(S_FPOS, sizeof(int) * K);
-    w.part_c = (double*)ctx->ensure(S_PART_C, sizeof(double) * (size_t)w.nparts);
-    w.part_k = (long long*)ctx->ensure(S_PART_K, sizeof(long long) * (size_t)w.nparts);
+    w.part_c = (double*)ctx->ensure(S_PART_C, sizeof(double) * part_alloc);
+    w.part_k = (long long*)ctx->ensure(S_PART_K, sizeof(long long) * part_alloc);
     char* cnt = (char*)ctx->ensure(S_COUNT, 128);
     w.count = (int*)cnt;
     w.Lp = (double*)(cnt + 16);
+    w.negflag = (int*)(cnt + 32);
     w.zero = ctx->zero;  // zero cell for out-of-map gathers
     w.tedge = (int*)ctx->ensure(S_TEDGE, sizeof(int) * (size_t)pl.T);
     w.poses7 = (double*)ctx->ensure(S_POSES7, sizeof(double) * 21);
     w.cidx = (int4*)ctx->ensure(S_COST_IDX, sizeof(int4) * 7 * (size_t)N);
     w.terms = (double*)ctx->ensure(S_COST_TERM, sizeof(double) * 7 * (size_t)N);
     return w;
+}
+
+// Superblock planes of the current phase planes (after every planes build).
+void launch_super_planes(lgs_ctx* ctx, const RtcsmPlan& pl, hipStream_t st)
+{
+    double* D = planes_buffer(ctx, pl);
+    double* S = (double*)ctx->ensure(S_SUPER, sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
+    int* negflag = (int*)((char*)ctx->ensure(S_COUNT, 128) + 32);
+    const int pgen = ctx->planes_gen = ctx->next_stamp();
+    dim3 g((pl.Wqp + kSPX - 1) / kSPX, (pl.Hqp + kSPY - 1) / kSPY, pl.low_res * pl.low_res);
+    const int tok = ctx->timing_begin(K_SUPER_PLANES, 8.0 * 2.0 * (double)pl.low_res * pl.low_res * pl.pstride);
+    hipLaunchKernelGGL(k_super_planes, g, dim3(256), 0, st, D, S, pl, negflag, pgen);
+    ctx->timing_end(tok);
+    LGS_HIP_CHECK(hipGetLastError());
+    ctx->super_fresh = true;
+}
+
+// after the planes were (re)written
+void planes_written(lgs_ctx* ctx, const RtcsmPlan& pl, hipStream_t st)
+{
+    if (ctx->super_prune) launch_super_planes(ctx, pl, st);
+    else ctx->super_fresh = false;
 }
 
 // Phase-plane copy of a plain coarse map into the context's S_DECIM slot
@@ -1156,6 +1585,7 @@ void launch_decimate(lgs_ctx* ctx, const double* coarse, const RtcsmPlan& pl, hi
     hipLaunchKernelGGL(k_decimate, gd, dim3(256), 0, st, coarse, pl.W, pl.H, pl.low_res, pl.Wq, pl.M, pl.Wqp,
                        pl.pstride, D);
     LGS_HIP_CHECK(hipGetLastError());
+    planes_written(ctx, pl, st);
 }
 
 // Coarse stage: one lane per coarse block; with phase planes the coarse map
@@ -1167,16 +1597,54 @@ void launch_coarse(lgs_ctx* ctx, const RtcsmPlan& pl, const Workspace& w, const 
     dim3 g((pl.P + cb - 1) / cb, pl.T);
     if (ctx->coarse_planes) {
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-        hipLaunchKernelGGL(k_coarse<1>, g, dim3(cb), 0, st, pl, w.decim, w.idx, w.cbase,
-                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1, 0>), g, dim3(cb), 0, st, pl, w.decim, w.idx, w.cbase,
+                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k, nullptr, nullptr,
+                           nullptr);
         ctx->timing_end(tok);
     } else {
         LGS_REQUIRE(coarse, "plain coarse map missing");
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-        hipLaunchKernelGGL(k_coarse<0>, g, dim3(cb), 0, st, pl, coarse, w.idx, w.cbase,
-                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<0, 0>), g, dim3(cb), 0, st, pl, coarse, w.idx, w.cbase,
+                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k, nullptr, nullptr,
+                           nullptr);
         ctx->timing_end(tok);
     }
+    LGS_HIP_CHECK(hipGetLastError());
+}
+
+// Superblock-pruned coarse stage: k_super (bounds) -> k_seed_super (L) ->
+// k_coarse<1, 1> (superblock-major lanes, pruned blocks skipped).
+void launch_coarse_super(lgs_ctx* ctx, const RtcsmPlan& pl, const Workspace& w, const double* grid,
+                         RtcsmRecord* rec, int gen, hipStream_t st)
+{
+    const int nsb2 = pl.nsbx * pl.nsby;
+    const int chunks = (nsb2 + 63) / 64;
+    {
+        const int tok = ctx->timing_begin(K_SUPER, 8.0 * (double)pl.T * nsb2 * pl.Nv);
+        hipLaunchKernelGGL(k_super, dim3(chunks, pl.T), dim3(64 * kSupWaves), 0, st, pl, w.super, w.cbase, w.zero, w.tedge,
+                           gen, w.negflag, ctx->planes_gen, w.sbound, w.part_c, w.part_k);
+        ctx->timing_end(tok);
+        LGS_HIP_CHECK(hipGetLastError());
+    }
+    {
+        const int tok = ctx->timing_begin(K_SEED, 8.0 * (pl.low_res * pl.low_res + kSeedCands * 16.0) * pl.Nv);
+        const size_t lds = std::max(sizeof(int) * kSeedCands, sizeof(int2)) * (size_t)pl.Nv;
+        hipLaunchKernelGGL(k_seed_super, dim3(1), dim3(1024), lds, st, pl, grid, w.idx, w.zero, w.decim, w.cbase,
+                           w.part_c, w.part_k, chunks * pl.T, w.Lp, rec);
+        ctx->timing_end(tok);
+        LGS_HIP_CHECK(hipGetLastError());
+    }
+    const int lanes = nsb2 * kSB * kSB;
+    const int cb = std::min(256, ((lanes + 63) / 64) * 64);
+    dim3 g((lanes + cb - 1) / cb, pl.T);
+    const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
+    if (tok >= 0) {
+        ctx->pending[tok].dev_rec = rec;
+        ctx->pending[tok].bytes_per_eval = 8.0 * pl.Nv;
+    }
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1, 1>), g, dim3(cb), 0, st, pl, w.decim, w.idx, w.cbase, w.zero,
+                       w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k, w.sbound, w.Lp, rec);
+    ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
 }
 
@@ -1199,6 +1667,9 @@ void launch_seed(const RtcsmPlan& pl, const double* grid, const Workspace& w, in
     }
     LGS_HIP_CHECK(hipGetLastError());
 }
+// k_fine's grid: one workgroup per CU, looping over the selected blocks (the
+// count is known only on the device; idle workgroups still hold wave slots)
+constexpr int kFineGrid = 256;
 // dynamic LDS: the evaluator's buffers, then the segment prefix (nseg + 1 ints)
 inline size_t pref_bytes(const Workspace& w) { return sizeof(int) * (size_t)(w.nseg + 1); }
 
@@ -1206,7 +1677,7 @@ template <int LR>
 void launch_fine_t(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
 {
     const size_t e = (eval_t_smem<LR>(pl.Nv) + 15) & ~size_t(15);
-    hipLaunchKernelGGL(k_fine<LR>, dim3(1024), dim3(64 * LR), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
+    hipLaunchKernelGGL(k_fine<LR>, dim3(kFineGrid), dim3(64 * LR), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
                        w.list, w.segcnt, w.nseg, (unsigned)e, w.fval, w.fpos);
 }
 void launch_fine(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
@@ -1215,7 +1686,7 @@ void launch_fine(const RtcsmPlan& pl, const double* grid, const Workspace& w, hi
     case 5: launch_fine_t<5>(pl, grid, w, st); break;
     default: {
         const size_t e = (sidx_bytes(pl) + 15) & ~size_t(15);
-        hipLaunchKernelGGL(k_fine<0>, dim3(1024), dim3(64), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
+        hipLaunchKernelGGL(k_fine<0>, dim3(kFineGrid), dim3(64), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
                            w.list, w.segcnt, w.nseg, (unsigned)e, w.fval, w.fpos);
     }
     }
@@ -1229,6 +1700,13 @@ struct ScanOptions {
     const std::vector<int4>* cost_patches = nullptr;
 };
 
+// superblock pruning applies (else k_coarse scores every block)
+inline bool uses_super(const lgs_ctx* ctx, const RtcsmPlan& pl, const ScanOptions& opt)
+{
+    return !(opt.dense || ctx->force_dense) && ctx->coarse_planes && ctx->super_prune && ctx->super_fresh &&
+           pl.Nv <= kSeedMaxNv;
+}
+
 // Enqueue the whole device pipeline of one match on ctx->stream; returns the
 // generation that tags this match's guard counters in *d_rec.
 int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
@@ -1237,8 +1715,10 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
 {
     Workspace w = ensure_workspace(ctx, pl, scan->n);
     hipStream_t st = ctx->stream;
-    const int gen = ++ctx->generation;
+    const int gen = ctx->generation = ctx->next_stamp();
     const int inject = ctx->inject_index ? 1 : 0;
+    if (pl.Nv == 0)   // no beam: the look-ahead padding alone is read
+        LGS_HIP_CHECK(hipMemsetAsync(w.cbase, 0, sizeof(int) * (size_t)(pl.sb_off + kPad), st));
     if (pl.Nv > 0) {
         if (opt.host_idx) {
             LGS_HIP_CHECK(hipMemcpyAsync(w.idx, opt.host_idx->data(), sizeof(int2) * opt.host_idx->size(),
@@ -1248,7 +1728,7 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                                w.cbase, w.tedge, gen);
             LGS_HIP_CHECK(hipGetLastError());
         } else {
-            dim3 g((pl.Nv + 255) / 256, pl.T);
+            dim3 g((pl.Nv + 255) / 256, (pl.T + kProjRows - 1) / kProjRows);
             {
                 const int tok_ = ctx->timing_begin(K_PROJECT, 24.0 * (double)pl.T * pl.Nv);
                 hipLaunchKernelGGL(k_project, g, dim3(256), 0, st, pl, scan->d_ranges, scan->d_angles,
@@ -1268,10 +1748,13 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
             }
         }
     }
-    launch_coarse(ctx, pl, w, coarse->d, gen, st);
-    {
+    const bool dense = opt.dense || ctx->force_dense;
+    if (uses_super(ctx, pl, opt)) {
+        launch_coarse_super(ctx, pl, w, grid->d, d_rec, gen, st);
+    } else {
+        launch_coarse(ctx, pl, w, coarse->d, gen, st);
         const int tok_ = ctx->timing_begin(K_SEED, 8.0 * pl.low_res * pl.low_res * (double)pl.Nv);
-        launch_seed(pl, grid->d, w, (opt.dense || ctx->force_dense) ? 1 : 0, st);
+        launch_seed(pl, grid->d, w, dense ? 1 : 0, st);
         ctx->timing_end(tok_);
     }
     LGS_HIP_CHECK(hipGetLastError());
@@ -1447,7 +1930,7 @@ bool check_cost_guards(lgs_ctx* ctx, const RtcsmPlan& pl, const CostPlan& cp,
     return true;
 }
 
-void finish_summary(const RtcsmPlan& pl, const lgs_scan* scan, lgs_pose2d initial,
+void finish_summary(const RtcsmPlan& pl, const lgs_scan* scan, lgs_pose2d initial, bool pruned,
                     const RtcsmRecord& rec, lgs_rtcsm_summary* out)
 {
     std::memset(out, 0, sizeof(*out));
@@ -1479,7 +1962,7 @@ void finish_summary(const RtcsmPlan& pl, const lgs_scan* scan, lgs_pose2d initia
     out->covariance[0] += 0.01;
     out->covariance[4] += 0.01;
     out->covariance[8] += 0.01;
-    out->coarse_blocks = pl.K;
+    out->coarse_blocks = pruned ? (int64_t)rec.coarse_evals : pl.K;
     out->fine_blocks = rec.n_eval;
 }
 
@@ -1523,7 +2006,15 @@ void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
     LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n,
                                  hipMemcpyDeviceToHost, ctx->stream));
     ctx->sync();
-    if (ctx->profile) ctx->harvest();
+    if (ctx->profile) {
+        for (auto& pt : ctx->pending)
+            if (pt.dev_rec) {
+                const long long j = (const RtcsmRecord*)pt.dev_rec - d_rec;
+                if (j >= 0 && j < n) pt.algo_bytes = pt.bytes_per_eval * (double)h_rec[j].coarse_evals;
+                pt.dev_rec = nullptr;
+            }
+        ctx->harvest();
+    }
 
     for (int j = 0; j < n; ++j) {
         HostRecord rec(h_rec[j], gens[j]);
@@ -1579,7 +2070,7 @@ void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
             rec = HostRecord(h_rec[j], g);
             if (opt.patches || opt.host_idx) rec.guard_count = 0;  // already exact
         }
-        finish_summary(plans[j], scans[j], init[j], rec, &out[j]);
+        finish_summary(plans[j], scans[j], init[j], uses_super(ctx, plans[j], opt), rec, &out[j]);
         out[j].guard_hits = guard_hits;
         out[j].fixups = fixups;
         out[j].slow_path = slow;
@@ -1614,6 +2105,7 @@ const lgs_grid* coarser_map(lgs_ctx* ctx, const lgs_grid* grid, const lgs_rtcsm_
         const RtcsmPlan lp = layout_plan(grid, params);
         const PlaneGeom pg{ lp.M, lp.Wqp, lp.pstride };
         launch_precompute(ctx, grid, low_res, planes_buffer(ctx, lp), &pg);
+        planes_written(ctx, lp, ctx->stream);
         cg->d = nullptr;
     } else {
         launch_precompute(ctx, grid, low_res, cg->d, nullptr);
@@ -1685,11 +2177,11 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
         }
         if (!coarse_scores && !fine_scores) return;
         Workspace w = ensure_workspace(ctx, pl, s->n);
-        const int gen = ++ctx->generation;
+        const int gen = ctx->generation = ctx->next_stamp();
         RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord));
         LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0, sizeof(RtcsmRecord), ctx->stream));
         if (nv > 0) {
-            dim3 g((nv + 255) / 256, pl.T);
+            dim3 g((nv + 255) / 256, (pl.T + kProjRows - 1) / kProjRows);
             hipLaunchKernelGGL(k_project, g, dim3(256), 0, ctx->stream, pl, s->d_ranges, s->d_angles,
                                w.idx, w.cbase, w.tedge, gen, d_rec, 0, -1.0, 0);
             LGS_HIP_CHECK(hipGetLastError());
@@ -1728,7 +2220,7 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
         RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord));
         RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned(sizeof(RtcsmRecord));
         double hp[3] = { pose.x, pose.y, pose.theta };
-        const int gen = ++ctx->generation;
+        const int gen = ctx->generation = ctx->next_stamp();
         LGS_HIP_CHECK(hipMemcpyAsync(poses, hp, sizeof(hp), hipMemcpyHostToDevice, ctx->stream));
         hipLaunchKernelGGL(KCOST(cp), dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
                            scan->d_ranges, scan->d_angles, poses, cidx, terms, d_rec, ctx->guard_cap,

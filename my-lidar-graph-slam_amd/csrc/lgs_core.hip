@@ -9,6 +9,7 @@
 // window max over zero-padded input; it is computed here from an LDS tile.
 #include "lgs_internal.hpp"
 
+#include <atomic>
 #include <cstring>
 
 using namespace lgs;
@@ -53,7 +54,19 @@ void* lgs_ctx::ensure_pinned(size_t bytes)
 namespace lgs {
 const char* const kKernelNames[K_NUM_KERNELS] = { "k_project", "k_coarse", "k_seed", "k_select",
                                                   "k_fine", "k_replay", "k_cost", "k_precompute",
-                                                  "k_linsolve", "k_ray_emit", "k_ray_apply" };
+                                                  "k_linsolve", "k_ray_emit", "k_ray_apply",
+                                                  "k_super", "k_super_planes" };
+}
+
+int lgs_ctx::next_stamp()
+{
+    static std::atomic<int> counter{ 0 };
+    int s = counter.fetch_add(1, std::memory_order_relaxed) + 1;
+    if (s <= 0) {   // 2^31 stamps: restart above 0 (tags compare 32 bits)
+        counter.store(1);
+        s = 1;
+    }
+    return s;
 }
 
 void lgs_ctx::sync()
@@ -232,6 +245,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
         ctx->profile = ctx->profile_mask != 0;
         return LGS_OK;
     case LGS_OPT_COARSE_PLANES: ctx->coarse_planes = value != 0.0; return LGS_OK;
+    case LGS_OPT_SUPER_PRUNE: ctx->super_prune = value != 0.0; return LGS_OK;
     case LGS_OPT_GUARD_CAP:
         ctx->guard_cap = (int)value;
         if (ctx->guard_cap < 0) ctx->guard_cap = 0;
@@ -367,7 +381,7 @@ extern "C" double* lgs_grid_device_ptr(lgs_grid* g) { return g ? g->d : nullptr;
 namespace {
 
 constexpr int kTileX = 64;
-constexpr int kTileY = 16;
+constexpr int kTileY = 32;
 constexpr int kMaxWinTiled = 32;
 
 // window start of output i over n cells with window w (SlidingWindowMax)

@@ -63,6 +63,8 @@ enum Slot {
     S_RAY0, S_RAY1, S_RAY2, S_RAY3, S_RAY4, S_RAY5, S_RAY6, S_RAY7,
     S_LS0, S_LS1,
     S_LIN0, S_LIN1,   // K4 staging
+    S_SUPER,        // double: superblock planes (forward kSB x kSB max of S_DECIM)
+    S_SBOUND,       // double [T * nsb2] superblock bounds
     S_NUM_SLOTS
 };
 
@@ -86,6 +88,7 @@ struct RtcsmRecord {
     double score_max;
     double L;             // lower bound used for pruning
     double costs[7];
+    unsigned long long coarse_evals;   // blocks k_coarse evaluated (superblock pruning)
     GuardRec guard[kGuardInline];
     CostGuardRec cost_guard[kGuardInline];
 };
@@ -112,6 +115,15 @@ struct RtcsmPlan {
     int Wq, Hq, M, Wqp, Hqp;
     long long pstride;
     long long K;                // T * P coarse blocks
+    // superblocks (kSB x kSB coarse blocks of one angle)
+    int nsbx, nsby;
+    double sb_mult;             // 1 + 4 (Nv + 1) 2^-53: rounding slack of the bound
+    // superblock planes, compact: every phase plane split into 4 x 4
+    // sub-phases (padded x mod 4, y mod 4) of Wq4 x Hq4 values, so the
+    // superblocks of one beam are consecutive doubles
+    int Wq4, Hq4;
+    long long sub4, pstride4;
+    long long sb_off;           // superblock base offsets start at cbase + sb_off
 };
 
 // Padded phase-plane geometry handed to the precompute kernel.
@@ -132,12 +144,16 @@ struct CostPlan {
 
 namespace lgs {
 enum KernelId { K_PROJECT = 0, K_COARSE, K_SEED, K_SELECT, K_FINE, K_REPLAY, K_COST, K_PRECOMPUTE,
-                K_LINSOLVE, K_RAY_EMIT, K_RAY_APPLY, K_NUM_KERNELS };
+                K_LINSOLVE, K_RAY_EMIT, K_RAY_APPLY, K_SUPER, K_SUPER_PLANES, K_NUM_KERNELS };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 struct PendingTiming {
     int kernel;
     hipEvent_t a, b;
     double algo_bytes;
+    // pruned k_coarse: device record whose coarse_evals (x bytes_per_eval)
+    // replaces algo_bytes once the host copy of the record is known
+    const void* dev_rec = nullptr;
+    double bytes_per_eval = 0.0;
 };
 }  // namespace lgs
 
@@ -151,7 +167,13 @@ struct lgs_ctx {
     bool inject_index = false;
     int guard_cap = lgs::kGuardInline;
     bool coarse_planes = true;   // phase-plane coarse layout (LGS_OPT_COARSE_PLANES)
-    int generation = 0;          // per-enqueue stamp (edge flags need no memset)
+    bool super_prune = true;     // superblock pruning of k_coarse (LGS_OPT_SUPER_PRUNE)
+    int planes_gen = 0;          // stamp of the last superblock-plane build (negative-value flag)
+    // Stamps come from one process-wide counter: a context's scratch may be
+    // memory a destroyed context used, and its stale tags must never match.
+    int next_stamp();
+    bool super_fresh = false;    // superblock planes match the current phase planes
+    int generation = 0;          // per-enqueue stamp (edge flags need no memset), from next_stamp()
     // arena
     void* buf[lgs::S_NUM_SLOTS] = {};
     size_t buf_bytes[lgs::S_NUM_SLOTS] = {};

@@ -311,5 +311,127 @@ def test_config2_full_size_bit_exact(ctx, world, config2, seed):
     gpu = ctx.optimize_pose_query(g, abi.RtcsmParams(*params), launcher_cost(), sc, init)
     ora = oracle_match(config2, -25.0, -25.0, 0.05, params, r, ang, init)
     assert_same(gpu, ora, f"config2 seed{seed}")
+    # superblock pruning scores a small fraction of the 421 x 17 x 17 blocks
+    assert gpu.coarse_blocks < 0.25 * 421 * 17 * 17, gpu.coarse_blocks
     e = gpu.estimated_pose
     assert abs(e.x - true[0]) < 0.051 and abs(e.y - true[1]) < 0.051 and abs(e.theta - true[2]) < 0.01
+
+
+# ---------------------------------------------------------------- superblock pruning
+def _query_ab(ctx, g, P, sc, init):
+    """Same query with superblock pruning on (default) and off."""
+    try:
+        ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 1)
+        on = ctx.optimize_pose_query(g, P, launcher_cost(), sc, init)
+        ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 0)
+        off = ctx.optimize_pose_query(g, P, launcher_cost(), sc, init)
+    finally:
+        ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 1)
+    return on, off
+
+
+def _identical(a, b, tag):
+    assert a.pose_found == b.pose_found, tag
+    assert list(a.best_win) == list(b.best_win), tag
+    assert a.score_max == b.score_max, tag
+    assert a.normalized_cost == b.normalized_cost, tag
+    assert list(a.covariance) == list(b.covariance), tag
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_super_prune_identical_to_full_scoring(ctx, world, seed):
+    """Pruning only skips blocks k_select could never take: the result is
+    bit-identical to scoring every coarse block, and fewer blocks are scored."""
+    rng = np.random.default_rng(500 + seed)
+    cells, mx, my = build_map(world, 400, 0.05, 100, scene.arc_poses(5), n_beams=541)
+    ang = scene.beam_angles(541)
+    true = (rng.uniform(-1, 1), rng.uniform(-1, 1), rng.uniform(-np.pi, np.pi))
+    r = scene.ray_cast(world, true, ang)
+    init = (true[0] + rng.uniform(-0.3, 0.3), true[1] + rng.uniform(-0.3, 0.3), true[2] + rng.uniform(-0.2, 0.2))
+    params = (5, 1.0 + 0.5 * (seed % 3), 1.0, 0.6, 20.0)
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    sc = ctx.scan(r, ang)
+    on, off = _query_ab(ctx, g, abi.RtcsmParams(*params), sc, init)
+    _identical(on, off, f"seed{seed}")
+    if seed < 4:
+        assert_same(on, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"seed{seed}")
+    # (scans leaving this 20 m map put every angle row in the unpruned
+    # 'may hold unsafe blocks' class; config 2 checks the pruning rate)
+    assert on.coarse_blocks <= off.coarse_blocks
+    assert on.fine_blocks <= off.coarse_blocks
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_super_prune_noise_map(ctx, seed):
+    """Dense random map: superblock bounds are loose and many sums are close."""
+    rng = np.random.default_rng(900 + seed)
+    cells = rng.choice([0.0, 0.3, 0.5, 0.7, 0.9], size=(240, 260)) * rng.uniform(0.9, 1.0, size=(240, 260))
+    ang = scene.beam_angles(361)
+    r = rng.uniform(0.5, 4.0, size=361)
+    init = (rng.uniform(-1, 1), rng.uniform(-1, 1), rng.uniform(-3, 3))
+    params = (5, 0.8, 0.8, 0.3, 20.0)
+    g = ctx.grid_from_array(cells, -6.0, -6.5, 0.05)
+    sc = ctx.scan(r, ang)
+    on, off = _query_ab(ctx, g, abi.RtcsmParams(*params), sc, init)
+    _identical(on, off, f"noise{seed}")
+    assert_same(on, oracle_match(cells, -6.0, -6.5, 0.05, params, r, ang, init), f"noise{seed}")
+
+
+def test_super_prune_negative_cells(ctx, world):
+    """The bound needs nonnegative cells; a map with negative values must
+    disable pruning (every block scored) and stay exact."""
+    cells, mx, my = build_map(world, 400, 0.05, 100, scene.arc_poses(4), n_beams=361)
+    cells = cells - 0.2 * (cells == 0.0)
+    ang = scene.beam_angles(361)
+    true = (0.2, -0.1, 0.4)
+    r = scene.ray_cast(world, true, ang)
+    init = (0.25, -0.05, 0.43)
+    params = (5, 0.6, 0.6, 0.3, 20.0)
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    sc = ctx.scan(r, ang)
+    on, off = _query_ab(ctx, g, abi.RtcsmParams(*params), sc, init)
+    _identical(on, off, "negative")
+    assert on.coarse_blocks == off.coarse_blocks
+    assert_same(on, oracle_match(cells, mx, my, 0.05, params, r, ang, init), "negative")
+
+
+def test_super_prune_wide_window(ctx, world):
+    """+-4.5 m window: 37x37 coarse blocks per angle, 100 superblocks (two
+    64-superblock chunks in k_super)."""
+    cells, mx, my = build_map(world, 400, 0.05, 100, scene.arc_poses(5), n_beams=541)
+    ang = scene.beam_angles(541)
+    true = (0.6, -0.2, 1.3)
+    r = scene.ray_cast(world, true, ang)
+    init = (0.9, -0.5, 1.35)
+    params = (5, 9.0, 9.0, 0.2, 20.0)
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    sc = ctx.scan(r, ang)
+    on, off = _query_ab(ctx, g, abi.RtcsmParams(*params), sc, init)
+    assert list(on.win)[:2] == [90, 90]
+    _identical(on, off, "wide")
+    assert_same(on, oracle_match(cells, mx, my, 0.05, params, r, ang, init), "wide")
+
+
+def test_super_prune_batch_and_fixed_threshold(ctx, world):
+    """OptimizePose with a caller coarse map (decimated per batch) and a
+    fixed threshold: pruned batch == unpruned batch."""
+    cells, mx, my = build_map(world, 400, 0.05, 100, scene.arc_poses(4), n_beams=361)
+    ang = scene.beam_angles(361)
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    cg = ctx.precompute_max(g, 5)
+    P = abi.RtcsmParams(5, 0.6, 0.6, 0.4, 20.0)
+    rng = np.random.default_rng(77)
+    scans, inits = [], []
+    for _ in range(5):
+        true = (rng.uniform(-1, 1), rng.uniform(-1, 1), rng.uniform(-3, 3))
+        scans.append(ctx.scan(scene.ray_cast(world, true, ang), ang))
+        inits.append((true[0] + 0.1, true[1] - 0.05, true[2] + 0.05))
+    try:
+        ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 0)
+        off = ctx.optimize_pose_batch(g, cg, P, launcher_cost(), scans, inits, 0.5)
+        ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 1)
+        on = ctx.optimize_pose_batch(g, cg, P, launcher_cost(), scans, inits, 0.5)
+    finally:
+        ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 1)
+    for k, (a, b) in enumerate(zip(on, off)):
+        _identical(a, b, f"batch{k}")

@@ -1,19 +1,21 @@
 #!/bin/bash
-# quick A/B of bench variants (no CPU baseline), after the GPU parity tests
+# GPU-box A/B: parity tests, then the match bench with a given option on/off.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-tail -3 gpurun_out/pytest_gpu.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for v in "$@"; do
-  echo "== variant: $v"
-  timeout -k 10 300 python bench.py --steps 200 --warmup 10 --no-cpu $v > gpurun_out/ab.log 2>&1 || { tail -20 gpurun_out/ab.log; exit 3; }
-  python - <<'PY'
-import json
-l=[x for x in open('gpurun_out/ab.log') if x.startswith('{')][-1]
-d=json.loads(l)
-print('value', d['value'], 'p50', d['p50_scan_match_ms'], 'roof', d['roofline']['achieved'], d['roofline']['frac'])
-print({k: v['avg_ms'] for k, v in d['kernels'].items()})
-PY
+OUT=gpurun_out
+mkdir -p $OUT
+step() {
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 "$to" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -3 $OUT/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+[ -z "$SKIP_TESTS" ] && step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS}
+for v in ${AB_VALUES:-1 0}; do
+  step bench_${AB_FLAG:-super-prune}_$v 300 python bench.py --no-cpu --steps ${BENCH_STEPS:-200} --warmup 10 --${AB_FLAG:-super-prune} $v ${BENCH_ARGS}
 done
+echo done
