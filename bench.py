@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--coarse-planes", type=int, default=1, help="A/B: 1 phase-plane coarse layout, 0 plain")
     ap.add_argument("--spin-sync", type=int, default=1, help="1 spin on the stream when waiting, 0 blocking wait")
+    ap.add_argument("--skip-kernels", default="",
+                    help="diagnostics only: comma-separated kernel names not launched (results invalid)")
     ap.add_argument("--super-prune", type=int, default=1,
                     help="A/B: 1 superblock pruning of the coarse stage, 0 score every coarse block")
     ap.add_argument("--streams", type=int, default=3,
@@ -242,6 +244,9 @@ def run_match(args, D, ctx):
         for k in range(args.warmup):
             c.optimize_pose_query(g, P, cost, ds[k % n], inits[k % n])
         set_timed_events(c, args, "k_coarse")
+        if args.skip_kernels:   # after the warmup: skipped stages then read valid stale scratch
+            c.set_option(abi.LGS_OPT_SKIP_MASK,
+                         sum(1 << abi.KERNEL_IDS.index(k) for k in args.skip_kernels.split(",")))
     results = np.zeros((args.steps, 6))
     lat = [[] for _ in range(S)]
 

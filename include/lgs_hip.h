@@ -144,6 +144,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_COARSE_PLANES 6   /* 1 (default) = phase-plane coarse layout, 0 = plain layout (A/B) */
 #define LGS_OPT_PROFILE_MASK  7   /* time only the kernels whose lgs_kernel_stat index bit is set (0 = off) */
 #define LGS_OPT_SPIN_SYNC     8   /* 1 (default) = spin on the stream when waiting for results, 0 = blocking wait */
+#define LGS_OPT_SKIP_MASK     10  /* diagnostics only: bitmask of kernels (lgs_ctx_kernel_stats order) not launched -- results are invalid */
 #define LGS_OPT_SUPER_PRUNE   9   /* 1 (default) = skip coarse blocks whose 4x4-superblock bound is below the seed score, 0 = evaluate every coarse block */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

@@ -236,6 +236,7 @@ __global__ void k_cost_patch(int4* __restrict__ cidx, const int4* __restrict__ p
 __device__ __forceinline__ double dmax2(double a, double b) { return (a < b) ? b : a; }
 
 constexpr int kSB = 4;   // superblock = kSB x kSB coarse blocks
+constexpr int kSeedCands = 4;   // k_seed_super workgroups (candidate superblocks)
 
 __device__ __forceinline__ bool better(double a, long long ka, double b, long long kb)
 {
@@ -352,6 +353,16 @@ __device__ __forceinline__ double seq_sum(int n, Fetch fetch, Addr addr)
     return s;
 }
 
+// compile-time loop C = 0, STEP, 2*STEP, ... < MAXC; f returns false to stop
+template <int C, int MAXC, int STEP, class F>
+__device__ __forceinline__ void static_for_step(F&& f)
+{
+    if constexpr (C < MAXC) {
+        if (!f(std::integral_constant<int, C>{})) return;
+        static_for_step<C + STEP, MAXC, STEP>(f);
+    }
+}
+
 // Four batches in flight (for kernels with few waves, where one wave's
 // latency is the kernel's duration): look-ahead up to 4*kPipe entries.
 template <class Rec, class Fetch, class Addr>
@@ -386,46 +397,20 @@ __device__ __forceinline__ double seq_sum4(int n, Fetch fetch, Addr addr)
 //               doubles of one plane;
 //   PLANES = 0: the coarse map as is (stride lr between lanes).
 // --------------------------------------------------------------------------
-//   SBMAP = 1: superblock pruning (k_super / k_seed_super ran first): lanes
-//               are ordered superblock-major (4x4 blocks per superblock, 4
-//               superblocks per wave); a block whose superblock bound is < L
-//               is not evaluated (cscore = -inf, so k_select never takes it),
-//               and a wave with no surviving block skips the beam loop.  Rows
-//               that can hold unsafe blocks (tedge) are never pruned.
-template <int PLANES, int SBMAP>
-__global__ __launch_bounds__(SBMAP ? 256 : 1024) void k_coarse(
+template <int PLANES>
+__global__ __launch_bounds__(1024) void k_coarse(
     RtcsmPlan pl, const double* __restrict__ cmap, const int2* __restrict__ idx,
     const int* __restrict__ cbase, const double* __restrict__ zero,
     const int* __restrict__ tedge, int gen, double* __restrict__ cscore,
-    uint8_t* __restrict__ cflag, double* __restrict__ part_c, long long* __restrict__ part_k,
-    const double* __restrict__ sbound, const double* __restrict__ Lp, RtcsmRecord* rec)
+    uint8_t* __restrict__ cflag, double* __restrict__ part_c, long long* __restrict__ part_k)
 {
     __shared__ double sv[16];
     __shared__ long long sk[16];
     const int tt = blockIdx.y;
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    bool active;
-    int jx, jy;
-    bool keep = true;
-    if constexpr (SBMAP) {
-        const int nsb2 = pl.nsbx * pl.nsby;
-        const int sb = p >> 4, m = p & 15;
-        const int a = sb % pl.nsbx, b = sb / pl.nsbx;
-        jx = kSB * a + (m & 3);
-        jy = kSB * b + (m >> 2);
-        active = (sb < nsb2) & (jx < pl.ncx) & (jy < pl.ncy);
-        if (!active) jx = jy = 0;
-        // safe rows only: sbound >= c for every block of the superblock
-        // (k_super); k_select takes a safe block only if c > thr and c >= L
-        if (tedge[tt] != gen && active) {
-            const double bnd = sbound[(size_t)tt * nsb2 + sb];
-            keep = (bnd > pl.thr) && (bnd >= *Lp);
-        }
-    } else {
-        active = p < pl.P;
-        jx = active ? p % pl.ncx : 0;
-        jy = active ? p / pl.ncx : 0;
-    }
+    const bool active = p < pl.P;
+    const int jx = active ? p % pl.ncx : 0;
+    const int jy = active ? p / pl.ncx : 0;
     const int lr = pl.low_res;
     const int W = pl.W, H = pl.H;
     const size_t o = (size_t)tt * pl.Nv;
@@ -433,17 +418,7 @@ __global__ __launch_bounds__(SBMAP ? 256 : 1024) void k_coarse(
     const int* __restrict__ cb = cbase + o;
 
     double sum = 0.0;
-    if constexpr (SBMAP) {
-        const bool kp = active && keep;
-        const unsigned long long live = __ballot(kp);
-        if (live != 0ull) {
-            // dropped lanes of a live wave all read the zero cell
-            const double* __restrict__ lane_base = cmap + (jy * pl.Wqp + jx);
-            sum = seq_sum4<int>(pl.Nv, [&](int v) { return cb[v]; },
-                                [&](const int& c) { return kp ? lane_base + c : zero; });
-            if ((threadIdx.x & 63) == 0) atomicAdd(&rec->coarse_evals, (unsigned long long)__popcll(live));
-        }
-    } else if (PLANES) {
+    if (PLANES) {
         const double* __restrict__ lane_base = cmap + (jy * pl.Wqp + jx);
         sum = seq_sum<int>(pl.Nv, [&](int v) { return cb[v]; }, [&](const int& c) { return lane_base + c; });
     } else {
@@ -471,18 +446,16 @@ __global__ __launch_bounds__(SBMAP ? 256 : 1024) void k_coarse(
     }
     const long long k = (long long)tt * pl.P + (long long)jx * pl.ncy + jy;
     if (active) {
-        cscore[k] = keep ? sum : -INFINITY;
+        cscore[k] = sum;
         cflag[k] = unsafe ? 1 : 0;
     }
-    if constexpr (!SBMAP) {
-        double bv = (active && !unsafe) ? sum : -1.0;
-        long long bk = (active && !unsafe) ? k : LLONG_MAX;
-        block_argmax(bv, bk, sv, sk);
-        if (threadIdx.x == 0) {
-            const int part = blockIdx.y * gridDim.x + blockIdx.x;
-            part_c[part] = bv;
-            part_k[part] = bk;
-        }
+    double bv = (active && !unsafe) ? sum : -1.0;
+    long long bk = (active && !unsafe) ? k : LLONG_MAX;
+    block_argmax(bv, bk, sv, sk);
+    if (threadIdx.x == 0) {
+        const int part = blockIdx.y * gridDim.x + blockIdx.x;
+        part_c[part] = bv;
+        part_k[part] = bk;
     }
 }
 
@@ -544,12 +517,17 @@ __global__ __launch_bounds__(256) void k_super_planes(const double* __restrict__
     if (neg) *negflag = pgen;
 }
 
-// One workgroup (kSupWaves waves) per (64 superblocks, search angle): lane =
-// superblock, wave w sums a quarter of the beams (any order: the bound
-// absorbs the rounding; four batches of gathers in flight), LDS reduction
-// over the waves.  Also the chunk's best superblock for the seed (-inf in
-// rows that may hold unsafe blocks).
+// k_super: one workgroup (kSupWaves waves) per (chunk of superblocks, search
+// angle); lane = superblock, wave w sums a quarter of the beams (any order:
+// the bound absorbs the rounding; four batches of gathers in flight), LDS
+// reduction over the waves.  PAIR (nsb2 <= 32): lanes 32..63 take the odd
+// beams of the wave's range, so one gather instruction serves two beams (the
+// texture-address rate per gather instruction, not bytes, is what this stage
+// spends).  The angle's superblock base row is staged in LDS.  Also the
+// chunk's best superblock for the seed (-inf in rows that may hold unsafe
+// blocks).
 constexpr int kSupWaves = 4;
+template <int PAIR>
 __global__ __launch_bounds__(64 * kSupWaves) void k_super(RtcsmPlan pl, const double* __restrict__ sp,
                                                 const int* __restrict__ cbase, const double* __restrict__ zero,
                                                 const int* __restrict__ tedge, int gen,
@@ -557,31 +535,48 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(RtcsmPlan pl, const do
                                                 double* __restrict__ sbound, double* __restrict__ part_c,
                                                 long long* __restrict__ part_k)
 {
+    extern __shared__ int srow[];   // [Nv]
     __shared__ double red[kSupWaves][64];
+    constexpr int SPW = PAIR ? 32 : 64;   // superblocks per chunk
     const int t = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nsb2 = pl.nsbx * pl.nsby;
-    const int sbi = blockIdx.x * 64 + lane;
+    const int h = PAIR ? (lane >> 5) : 0;
+    const int sbi = blockIdx.x * SPW + (lane & (SPW - 1));
     const bool act = sbi < nsb2;
     const int a = act ? sbi % pl.nsbx : 0, b = act ? sbi / pl.nsbx : 0;
     const double* __restrict__ lb = sp + (b * pl.Wq4 + a);
-    // wave w: a contiguous beam range (wave-uniform index loads, pipelined
-    // gathers); cbase rows are padded for seq_sum's look-ahead
+    LGS_PROBE_DECL;
+    LGS_PROBE_MARK();
+    const int* __restrict__ cbrow = cbase + pl.sb_off + (size_t)t * pl.Nv;
+    for (int v = threadIdx.x; v < pl.Nv; v += blockDim.x) srow[v] = cbrow[v];
+    __syncthreads();
+    LGS_PROBE_MARK();
     const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
     const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
-    const int* __restrict__ cb = cbase + pl.sb_off + (size_t)t * pl.Nv + lo;
-    double s = 0.0;
-    if (cnt > 0)
-        s = seq_sum4<int>(cnt, [&](int v) { return cb[v]; }, [&](const int& c) { return act ? lb + c : zero; });
+    const int* row = srow + lo;
+    double s;
+    if constexpr (PAIR) {
+        const int n2 = (cnt + 1) >> 1;
+        s = seq_sum4<int>(n2, [&](int i) { const int v = 2 * i + h; return (v < cnt) ? row[v] : INT_MIN; },
+                          [&](const int& c) { return (act && c != INT_MIN) ? lb + c : zero; });
+        s += __shfl_xor(s, 32, 64);
+    } else {
+        s = seq_sum4<int>(cnt, [&](int v) { return (v < cnt) ? row[v] : INT_MIN; },
+                          [&](const int& c) { return (act && c != INT_MIN) ? lb + c : zero; });
+    }
     red[w][lane] = s;
+    LGS_PROBE_MARK();
     __syncthreads();
+    LGS_PROBE_MARK();
     if (w != 0) return;
     double tot = 0.0;
     for (int j = 0; j < kSupWaves; ++j) tot += red[j][lane];
     const double bound = (*negflag == pgen) ? INFINITY : tot * pl.sb_mult;
-    if (act) sbound[(size_t)t * nsb2 + sbi] = bound;
+    const bool own = act && h == 0;
+    if (own) sbound[(size_t)t * nsb2 + sbi] = bound;
     // rows that may hold unsafe blocks never seed: -inf (bounds are >= 0)
-    const bool seedable = act && tedge[t] != gen;
+    const bool seedable = own && tedge[t] != gen;
     double bv = seedable ? bound : -INFINITY;
     long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
     for (int off = 32; off > 0; off >>= 1) {
@@ -597,6 +592,178 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(RtcsmPlan pl, const do
         part_c[part] = bv;
         part_k[part] = bk;
     }
+    LGS_PROBE_MARK();
+    LGS_PROBE_PRINT("super(stage, sum w0, barrier, tail)");
+}
+
+// k_coarse_rows (superblock pruning): coarse scores of the blocks k_select
+// could take, kRowSplit workgroups per search angle.  The angle's
+// superblocks are kept when bound > thr and (bound >= L, or the angle may
+// hold unsafe blocks); L = max of the seed candidates' fine lower bounds.
+// The angle's waves take the kept superblocks in turn; a superblock's 16
+// blocks are scored by one wave with gathers and additions transposed:
+// global_load_lds (16 bytes = two neighbouring blocks' cells, no register
+// destination) lands 8 beams x 16 blocks per wave instruction in an LDS
+// ring of kRing slots, kRing instructions ahead of 16 adder lanes that walk
+// the beams in order (the reference's sequential fp64 sum).  The ring is
+// refilled slot by slot behind the adders; counted vmcnt waits keep
+// kRing - 1 gathers in flight.
+constexpr int kRowWaves = 2;   // waves per workgroup
+constexpr int kRowSplit = 2;   // workgroups per angle
+constexpr int kRing = 24;      // 1 KiB glds slots per wave
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14)
+constexpr unsigned waitcnt_imm(unsigned vm, unsigned lgkm)
+{
+    return (vm & 15u) | (7u << 4) | ((lgkm & 15u) << 8) | ((vm >> 4) << 14);
+}
+__global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
+    RtcsmPlan pl, const double* __restrict__ cmap, const int2* __restrict__ idx, const int* __restrict__ cbase,
+    const double* __restrict__ zero, const int* __restrict__ tedge, int gen, const double* __restrict__ sbound,
+    const double* __restrict__ Lc, double* __restrict__ Lp, double* __restrict__ cscore,
+    uint8_t* __restrict__ cflag, RtcsmRecord* rec)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int s_sb[64];
+    __shared__ int s_cnt;
+    const int t = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nsb2 = pl.nsbx * pl.nsby;
+    const int Nv = pl.Nv;
+    LGS_PROBE_DECL;
+    LGS_PROBE_MARK();
+    double L = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < kSeedCands; ++b) L = fmax(L, Lc[b]);
+    if (t == 0 && blockIdx.y == 0 && tid == 0) *Lp = L;
+    const bool te = tedge[t] == gen;
+    // kept superblocks of this angle (nsb2 <= 64 on this path), in key order
+    if (w == 0) {
+        bool kp = false;
+        if (lane < nsb2) {
+            const double bnd = sbound[(size_t)t * nsb2 + lane];
+            kp = (bnd > pl.thr) && (te || bnd >= L);
+        }
+        const unsigned long long bal = __ballot(kp);
+        if (kp) s_sb[__popcll(bal & ((1ull << lane) - 1ull))] = lane;
+        if (lane == 0) {
+            s_cnt = __popcll(bal);
+            unsigned long long nb = 0;
+            for (unsigned long long mm = bal; mm; mm &= mm - 1) {
+                const int sb = __ffsll((long long)mm) - 1;
+                const int a = sb % pl.nsbx, b = sb / pl.nsbx;
+                nb += (unsigned long long)(min(kSB, pl.ncx - kSB * a) * min(kSB, pl.ncy - kSB * b));
+            }
+            if (nb && blockIdx.y == 0) atomicAdd(&rec->coarse_evals, nb);
+        }
+    }
+    __syncthreads();
+    LGS_PROBE_MARK();
+    const int cnt = s_cnt;
+    const int gw = blockIdx.y * kRowWaves + w;   // this wave among the angle's waves
+    if (cnt <= (int)blockIdx.y * kRowWaves) return;   // no superblock for this workgroup
+    int* srow = (int*)smem;                                   // [Nv]
+    const size_t srow_bytes = (sizeof(int) * (size_t)Nv + 15) & ~(size_t)15;
+    double* ring = (double*)(smem + srow_bytes) + (size_t)w * kRing * 128;   // [kRing][64 lanes][2]
+    for (int v = tid; v < Nv; v += blockDim.x) srow[v] = cbase[(size_t)t * Nv + v];
+    __syncthreads();
+    LGS_PROBE_MARK();
+    // gather lanes: beam b of the instruction's 8, block pair p (row p / 2,
+    // columns 2 (p % 2) and + 1); adder lanes m < 16: block (m % 4, m / 4)
+    const int gb = lane >> 3, gp = lane & 7;
+    const int am = lane & 15;
+    const int aslot = ((am >> 2) * 2 + ((am & 3) >> 1)) * 2 + (am & 1);   // (beam 0) offset in doubles
+    const int ninstr = (Nv + 7) / 8;
+    for (int e = gw; e < cnt; e += kRowWaves * kRowSplit) {
+        const int sb = s_sb[e];
+        const int jx0 = kSB * (sb % pl.nsbx), jy0 = kSB * (sb / pl.nsbx);
+        const double* __restrict__ pb = cmap + ((jy0 + (gp >> 1)) * pl.Wqp + jx0 + (gp & 1) * 2);
+        auto offset_of = [&](int i) {   // unconditional LDS read (a branch would cost counted waits)
+            const int v = 8 * i + gb;
+            const int o = srow[min(v, Nv - 1)];
+            return (v < Nv) ? o : -1;
+        };
+        auto issue = [&](int i, int off) {
+            const double* g = (off >= 0) ? pb + off : zero;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(ring + (i % kRing) * 128), 16, 0, 0);
+        };
+        for (int i = 0; i < kRing; ++i) issue(i, offset_of(i));   // past the scan: the zero cells
+        const int jx = jx0 + (am & 3), jy = jy0 + (am >> 2);
+        const bool active = lane < 16 && jx < pl.ncx && jy < pl.ncy;
+        // LDS reads of slot i + 1 are issued before slot i's additions (their
+        // latency hides behind the add chain); slot i is refilled once read
+        double acc = 0.0;
+        double ra[8], rb[8];
+        auto read_slot = [&](int i, double (&x)[8]) {
+            const double* slot = ring + (i % kRing) * 128 + aslot;
+#pragma unroll
+            for (int bb = 0; bb < 8; ++bb) x[bb] = slot[bb * 16];
+        };
+        int off_next = offset_of(kRing);
+        // one step: slot i + 1 -> nxt (LDS), add cur (slot i), refill slot i
+        auto step = [&](int i, double (&cur)[8], double (&nxt)[8]) {
+            __builtin_amdgcn_s_waitcnt(waitcnt_imm(kRing - 2, 15));   // instruction i + 1 has landed
+            read_slot(i + 1, nxt);   // past the scan: zero cells or unused slot contents, never added
+            __builtin_amdgcn_sched_barrier(0);
+            const int off_cur = off_next;
+            off_next = offset_of(i + kRing + 1);
+            const int nb = min(8, Nv - 8 * i);
+            double s = acc;
+#pragma unroll
+            for (int bb = 0; bb < 8; ++bb)
+                if (bb < nb) s += cur[bb];
+            acc = s;
+            __builtin_amdgcn_sched_barrier(0);   // the additions stay ahead of the wait
+            __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));   // slot i + 1 is in registers
+            issue(i + kRing, off_cur);                        // refills slot i (read one step earlier)
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        LGS_PROBE_MARK();
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(kRing - 1, 15));   // instruction 0 has landed
+        read_slot(0, ra);
+        LGS_PROBE_MARK();
+        for (int i = 0; i < ninstr; i += 2) {
+            step(i, ra, rb);
+            if (i + 1 >= ninstr) break;
+            step(i + 1, rb, ra);
+        }
+        LGS_PROBE_MARK();
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15));   // ring drained before its reuse
+        // unsafe test (angles that may hold unsafe blocks only): lane (m, q)
+        // checks beams q, q + 4, ..., OR-reduced over the quarters
+        bool unsafe = false;
+        const int um = lane & 15, uq = lane >> 4;
+        const int ujx = jx0 + (um & 3), ujy = jy0 + (um >> 2);
+        if (te && ujx < pl.ncx && ujy < pl.ncy) {
+            const int2* __restrict__ id = idx + (size_t)t * Nv;
+            const int lr = pl.low_res, lo = -(lr - 1);
+            const int x0 = -pl.win_x + ujx * lr, y0 = -pl.win_y + ujy * lr;
+            for (int v = uq; v < Nv; v += 4) {
+                const int2 c = id[v];
+                if (c.x - pl.win_x < 0 || c.y - pl.win_y < 0) {
+                    const int x = c.x + x0, y = c.y + y0;
+                    unsafe |= (x >= lo) & (x < pl.W) & (y >= lo) & (y < pl.H) & ((x < 0) | (y < 0));
+                }
+            }
+        }
+        unsafe |= __shfl_xor((int)unsafe, 16, 64) != 0;
+        unsafe |= __shfl_xor((int)unsafe, 32, 64) != 0;
+        if (active) {
+            const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
+            cscore[k] = acc;
+            cflag[k] = unsafe ? 1 : 0;
+        }
+        LGS_PROBE_MARK();
+    }
+#ifdef LGS_PROBE
+    if (tid == 0 && cnt >= 1 && blockIdx.y == 0)
+        printf("probe coarse_rows t=%d cnt=%d: select %.2f stage %.2f issue %.2f fill %.2f loop %.2f tail %.2f us\n",
+               t, cnt, 0.01 * (double)(lgs_probe_t[1] - lgs_probe_t[0]),
+               0.01 * (double)(lgs_probe_t[2] - lgs_probe_t[1]), 0.01 * (double)(lgs_probe_t[3] - lgs_probe_t[2]),
+               0.01 * (double)(lgs_probe_t[4] - lgs_probe_t[3]), 0.01 * (double)(lgs_probe_t[5] - lgs_probe_t[4]),
+               0.01 * (double)(lgs_probe_t[6] - lgs_probe_t[5]));
+#endif
 }
 
 // Fine scores of one block by one wave: lane q owns pose (xo = q % lr,
@@ -663,15 +830,6 @@ __device__ void eval_block(const RtcsmPlan& pl, const double* __restrict__ grid,
 constexpr int kMaxChunks = 32;   // transposed evaluator handles Nv <= 2048
 typedef double d2a8 __attribute__((ext_vector_type(2), aligned(8)));
 
-// compile-time loop C = 0, STEP, 2*STEP, ... < MAXC; f returns false to stop
-template <int C, int MAXC, int STEP, class F>
-__device__ __forceinline__ void static_for_step(F&& f)
-{
-    if constexpr (C < MAXC) {
-        if (!f(std::integral_constant<int, C>{})) return;
-        static_for_step<C + STEP, MAXC, STEP>(f);
-    }
-}
 
 template <int LR>
 __device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ grid,
@@ -831,30 +989,28 @@ __global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_seed(
     if (threadIdx.x == 0) *Lout = f;
 }
 
-// k_seed_super (superblock pruning), one 1024-thread workgroup:
-//  1. the kSeedCands best superblocks above thr among k_super's per-chunk
-//     bests (rows that may hold unsafe blocks are excluded there);
-//  2. their members' coarse scores summed in any order (they only choose
+// k_seed_super (superblock pruning): kSeedCands workgroups of 1024 threads.
+//  1. every workgroup picks the same kSeedCands best superblocks above thr
+//     among k_super's per-chunk bests (rows that may hold unsafe blocks are
+//     excluded there); workgroup b takes candidate b;
+//  2. its 16 members' coarse scores summed in any order (they only choose
 //     which block to refine: any safe block's fine max is a valid L);
 //  3. the best member's lr x lr fine scores, also summed in any order, each
 //     lowered by its rounding bound (4 (Nv + 2) eps sum|x| >= the gap to the
-//     reference-order sum), so L <= that block's exact fine max <= the
-//     reference's final score.
-// No candidate: L = -inf (k_coarse still drops superblocks with bound <= thr).
-// Every loop issues its loads in independent batches of 16: one workgroup,
-// so the kernel's duration is its latency chain.
-// Also clears the record's evaluated-block counter for k_coarse.
-// LDS: the candidate rows' cbase (kSeedCands * Nv ints), then the block's
-// index row (Nv int2) in the same space.
-constexpr int kSeedCands = 4;
-constexpr int kSeedMaxNv = 2048;   // LDS: kSeedCands * Nv ints
+//     reference-order sum), so L_b <= that block's exact fine max <= the
+//     reference's final score;
+//  4. L_b goes to Lc[b] (-inf without a candidate); k_coarse_rows and
+//     k_select use L = max_b L_b.
+// Loads are issued in independent batches of 16 (one workgroup per
+// candidate: each one's duration is its latency chain).
+constexpr int kSeedMaxNv = 2048;   // LDS: the candidate row (Nv ints / int2)
 constexpr int kSeedRegParts = 4;   // parts held in registers per thread
 
 __global__ __launch_bounds__(1024) void k_seed_super(
     RtcsmPlan pl, const double* __restrict__ grid, const int2* __restrict__ idx,
     const double* __restrict__ zero, const double* __restrict__ cmap, const int* __restrict__ cbase,
     const double* __restrict__ part_c, const long long* __restrict__ part_k, int nparts,
-    double* __restrict__ Lout, RtcsmRecord* rec)
+    double* __restrict__ Lc, RtcsmRecord* rec)
 {
     extern __shared__ char smem[];
     __shared__ double sv[16];
@@ -864,7 +1020,9 @@ __global__ __launch_bounds__(1024) void k_seed_super(
     __shared__ double reda[1024];
     const int tid = threadIdx.x;
     const int nsb2 = pl.nsbx * pl.nsby;
-    if (tid == 0) rec->coarse_evals = 0ull;
+    const int Nv = pl.Nv;
+    LGS_PROBE_DECL;
+    LGS_PROBE_MARK();
     double pv[kSeedRegParts];
     long long pk[kSeedRegParts];
 #pragma unroll
@@ -874,7 +1032,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(
         pk[j] = (i < nparts) ? part_k[i] : LLONG_MAX;
     }
     int nc = 0;
-    for (; nc < kSeedCands; ++nc) {
+    for (; nc <= (int)blockIdx.x; ++nc) {   // candidates 0..blockIdx.x
         double bv = -INFINITY;
         long long bk = LLONG_MAX;
 #pragma unroll
@@ -899,39 +1057,30 @@ __global__ __launch_bounds__(1024) void k_seed_super(
             if (pk[j] == bk) pv[j] = -INFINITY, pk[j] = LLONG_MAX;
         __syncthreads();
     }
-    if (nc == 0) {
-        if (tid == 0) *Lout = -INFINITY;
-        return;
-    }
-    // 2. member sums: member m = tid % 64 (candidate m / 16), beam group tid / 64
-    const int Nv = pl.Nv;
-    int* srow = (int*)smem;   // [kSeedCands][Nv]
-    for (int i = tid; i < nc * Nv; i += blockDim.x)
-        srow[i] = cbase[(size_t)(cand[i / Nv] / nsb2) * Nv + (i % Nv)];
-    __syncthreads();
-    {
-        const int m = tid & 63, g = tid >> 6;
-        const int ci = m >> 4, mem = m & 15;
-        bool valid = ci < nc;
-        int jx = 0, jy = 0;
-        if (valid) {
-            const int sb = (int)(cand[ci] % nsb2);
-            jx = kSB * (sb % pl.nsbx) + (mem & 3);
-            jy = kSB * (sb / pl.nsbx) + (mem >> 2);
-            valid = jx < pl.ncx && jy < pl.ncy;
-        }
+    double Lmine = -INFINITY;
+    LGS_PROBE_MARK();
+    if (nc > (int)blockIdx.x) {
+        const long long ck = cand[blockIdx.x];
+        const int ct = (int)(ck / nsb2), csb = (int)(ck % nsb2);
+        // 2. member sums: member m = tid % 16, beam group tid / 16 (64 groups)
+        int* srow = (int*)smem;   // [Nv]
+        for (int v = tid; v < Nv; v += blockDim.x) srow[v] = cbase[(size_t)ct * Nv + v];
+        __syncthreads();
+        const int m = tid & 15, g = tid >> 4;
+        const int jx = kSB * (csb % pl.nsbx) + (m & 3);
+        const int jy = kSB * (csb / pl.nsbx) + (m >> 2);
+        const bool valid = jx < pl.ncx && jy < pl.ncy;
         double s = 0.0;
         if (valid) {
             const double* __restrict__ lb = cmap + (jy * pl.Wqp + jx);
-            const int* row = srow + ci * Nv;
-            const int cnt = (g < Nv) ? (Nv - g + 15) / 16 : 0;   // beams g, g + 16, ...
+            const int cnt = (g < Nv) ? (Nv - g + 63) / 64 : 0;   // beams g, g + 64, ...
             double acc[4] = { 0.0, 0.0, 0.0, 0.0 };
             for (int i0 = 0; i0 < cnt; i0 += 16) {
                 double buf[16];
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     const int i = min(i0 + j, cnt - 1);
-                    buf[j] = (i0 + j < cnt) ? lb[row[g + 16 * i]] : 0.0;
+                    buf[j] = (i0 + j < cnt) ? lb[srow[g + 64 * i]] : 0.0;
                 }
 #pragma unroll
                 for (int j = 0; j < 16; ++j) acc[j & 3] += buf[j];
@@ -940,71 +1089,80 @@ __global__ __launch_bounds__(1024) void k_seed_super(
         }
         red[tid] = s;
         __syncthreads();
+        LGS_PROBE_MARK();
         double mv = -1.0;
         long long mk = LLONG_MAX;
-        if (tid < 64) {
+        if (tid < 16) {
             double tot = 0.0;
-            for (int j = 0; j < 16; ++j) tot += red[j * 64 + tid];
+            for (int j = 0; j < 64; ++j) tot += red[j * 16 + tid];
             if (valid) {
                 mv = tot;
-                mk = (cand[ci] / nsb2) * (long long)pl.P + (long long)jx * pl.ncy + jy;
+                mk = (long long)ct * pl.P + (long long)jx * pl.ncy + jy;
             }
         }
         block_argmax(mv, mk, sv, sk);
-        if (tid == 0) cand[0] = mk;
+        // 3. fine scores of block mk, any order, rounding-bounded
+        const int rem = (int)(mk % pl.P);
+        const int bjx = rem / pl.ncy, bjy = rem % pl.ncy;
+        const int lr = pl.low_res, npose = lr * lr;
+        int2* sidx = (int2*)smem;   // [Nv]
         __syncthreads();
-    }
-    // 3. fine scores of block cand[0], any order, rounding-bounded
-    const long long k = cand[0];
-    const int tt = (int)(k / pl.P);
-    const int rem = (int)(k % pl.P);
-    const int bjx = rem / pl.ncy, bjy = rem % pl.ncy;
-    const int lr = pl.low_res, npose = lr * lr;
-    int2* sidx = (int2*)smem;   // [Nv]
-    __syncthreads();
-    for (int v = tid; v < Nv; v += blockDim.x) sidx[v] = idx[(size_t)tt * Nv + v];
-    __syncthreads();
-    int QP = 1;
-    while (QP < npose) QP <<= 1;   // npose <= 1024
-    const int G = (int)blockDim.x / QP;
-    const int q = tid % QP, g = tid / QP;
-    double s = 0.0, a = 0.0;
-    if (q < npose) {
-        const int xo = q % lr, yo = q / lr;
-        const int xf = -pl.win_x + bjx * lr + xo, yf = -pl.win_y + bjy * lr + yo;
-        const int W = pl.W, H = pl.H;
-        const int cnt = (g < Nv) ? (Nv - g + G - 1) / G : 0;   // beams g, g + G, ...
-        for (int i0 = 0; i0 < cnt; i0 += 16) {
-            double buf[16];
+        LGS_PROBE_MARK();
+        for (int v = tid; v < Nv; v += blockDim.x) sidx[v] = idx[(size_t)ct * Nv + v];
+        __syncthreads();
+        LGS_PROBE_MARK();
+        int QP = 1;
+        while (QP < npose) QP <<= 1;   // npose <= 1024
+        const int G = (int)blockDim.x / QP;
+        const int q = tid % QP, gq = tid / QP;
+        double fs = 0.0, fa = 0.0;
+        if (q < npose) {
+            const int xo = q % lr, yo = q / lr;
+            const int xf = -pl.win_x + bjx * lr + xo, yf = -pl.win_y + bjy * lr + yo;
+            const int W = pl.W, H = pl.H;
+            const int cnt = (gq < Nv) ? (Nv - gq + G - 1) / G : 0;   // beams gq, gq + G, ...
+            for (int i0 = 0; i0 < cnt; i0 += 16) {
+                double buf[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int2 c = sidx[g + G * min(i0 + j, cnt - 1)];
-                const int x = c.x + xf, y = c.y + yf;
-                const bool inb = (i0 + j < cnt) & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
-                buf[j] = *(inb ? grid + (unsigned)(y * W + x) : zero);
-            }
+                for (int j = 0; j < 16; ++j) {
+                    const int2 c = sidx[gq + G * min(i0 + j, cnt - 1)];
+                    const int x = c.x + xf, y = c.y + yf;
+                    const bool inb = (i0 + j < cnt) & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
+                    buf[j] = *(inb ? grid + (unsigned)(y * W + x) : zero);
+                }
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                s += buf[j];
-                a += fabs(buf[j]);
+                for (int j = 0; j < 16; ++j) {
+                    fs += buf[j];
+                    fa += fabs(buf[j]);
+                }
             }
         }
-    }
-    red[tid] = s;
-    reda[tid] = a;
-    __syncthreads();
-    double lv = -INFINITY;
-    if (tid < npose) {
-        double ts = 0.0, ta = 0.0;
-        for (int j = 0; j < G; ++j) {
-            ts += red[j * QP + tid];
-            ta += reda[j * QP + tid];
+        __syncthreads();
+        LGS_PROBE_MARK();
+        red[tid] = fs;
+        reda[tid] = fa;
+        __syncthreads();
+        double lv = -INFINITY;
+        if (tid < npose) {
+            double ts = 0.0, ta = 0.0;
+            for (int j = 0; j < G; ++j) {
+                ts += red[j * QP + tid];
+                ta += reda[j * QP + tid];
+            }
+            lv = ts - (4.0 * (double)(Nv + 2) * 0x1p-53) * ta;
         }
-        lv = ts - (4.0 * (double)(Nv + 2) * 0x1p-53) * ta;
+        long long dummy = tid;
+        block_argmax(lv, dummy, sv, sk);
+        Lmine = lv;
+        LGS_PROBE_MARK();
     }
-    long long dummy = tid;
-    block_argmax(lv, dummy, sv, sk);
-    if (tid == 0) *Lout = lv;
+    // 4. publish
+    if (tid == 0) {
+        Lc[blockIdx.x] = Lmine;
+        if (blockIdx.x == 0) rec->coarse_evals = 0ull;   // k_coarse_rows counts
+    }
+    LGS_PROBE_MARK();
+    LGS_PROBE_PRINT("seed(b0: cand, members, argmax, stage, fine, reduce, publish)");
 }
 
 // k_select: one workgroup per segment of kSelSeg consecutive blocks.  The
@@ -1015,18 +1173,31 @@ __global__ __launch_bounds__(1024) void k_seed_super(
 // its position in the reference's block order.
 constexpr int kSelSeg = 1024;
 
+// sbound (superblock pruning, else nullptr): blocks of superblocks
+// k_coarse_rows did not keep were never scored and are never taken (the
+// same keep rule, evaluated again here).
 __global__ __launch_bounds__(kSelSeg) void k_select(RtcsmPlan pl, const double* __restrict__ cscore,
                                                    const uint8_t* __restrict__ cflag,
-                                                   const double* __restrict__ Lp, int* __restrict__ list,
-                                                   int* __restrict__ segcnt)
+                                                   const double* __restrict__ Lp, const double* __restrict__ sbound,
+                                                   const int* __restrict__ tedge, int gen,
+                                                   int* __restrict__ list, int* __restrict__ segcnt)
 {
     __shared__ int s_w[kSelSeg / 64];
     const long long k = (long long)blockIdx.x * kSelSeg + threadIdx.x;
     bool f = false;
     if (k < pl.K) {
+        bool kp = true;
         const double L = *Lp;
-        const double c = cscore[k];
-        f = (c > pl.thr) && (cflag[k] || c >= L);
+        if (sbound) {
+            const int t = (int)(k / pl.P), rem = (int)(k % pl.P);
+            const int jx = rem / pl.ncy, jy = rem % pl.ncy;
+            const double bnd = sbound[(size_t)t * pl.nsbx * pl.nsby + (jy / kSB) * pl.nsbx + jx / kSB];
+            kp = (bnd > pl.thr) && (tedge[t] == gen || bnd >= L);
+        }
+        if (kp) {
+            const double c = cscore[k];
+            f = (c > pl.thr) && (cflag[k] || c >= L);
+        }
     }
     const unsigned long long bal = __ballot(f);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1493,6 +1664,7 @@ struct Workspace {
     double* super;      // superblock planes (same layout)
     double* sbound;     // [T * nsb2]
     int* negflag;
+    double* Lc;         // [kSeedCands] per-candidate seeds
     double* zero;
     int* tedge;
 };
@@ -1546,6 +1718,8 @@ Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
     w.count = (int*)cnt;
     w.Lp = (double*)(cnt + 16);
     w.negflag = (int*)(cnt + 32);
+    static_assert(64 + 8 * kSeedCands <= 128, "S_COUNT layout");
+    w.Lc = (double*)(cnt + 64);   // kSeedCands doubles
     w.zero = ctx->zero;  // zero cell for out-of-map gathers
     w.tedge = (int*)ctx->ensure(S_TEDGE, sizeof(int) * (size_t)pl.T);
     w.poses7 = (double*)ctx->ensure(S_POSES7, sizeof(double) * 21);
@@ -1563,7 +1737,9 @@ void launch_super_planes(lgs_ctx* ctx, const RtcsmPlan& pl, hipStream_t st)
     const int pgen = ctx->planes_gen = ctx->next_stamp();
     dim3 g((pl.Wqp + kSPX - 1) / kSPX, (pl.Hqp + kSPY - 1) / kSPY, pl.low_res * pl.low_res);
     const int tok = ctx->timing_begin(K_SUPER_PLANES, 8.0 * 2.0 * (double)pl.low_res * pl.low_res * pl.pstride);
-    hipLaunchKernelGGL(k_super_planes, g, dim3(256), 0, st, D, S, pl, negflag, pgen);
+        if (!ctx->skipped(K_SUPER_PLANES))
+        hipLaunchKernelGGL(k_super_planes, g, dim3(256), 0, st, D, S, pl, negflag, pgen);
+
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
     ctx->super_fresh = true;
@@ -1597,16 +1773,14 @@ void launch_coarse(lgs_ctx* ctx, const RtcsmPlan& pl, const Workspace& w, const 
     dim3 g((pl.P + cb - 1) / cb, pl.T);
     if (ctx->coarse_planes) {
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1, 0>), g, dim3(cb), 0, st, pl, w.decim, w.idx, w.cbase,
-                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k, nullptr, nullptr,
-                           nullptr);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1>), g, dim3(cb), 0, st, pl, w.decim, w.idx, w.cbase,
+                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
         ctx->timing_end(tok);
     } else {
         LGS_REQUIRE(coarse, "plain coarse map missing");
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<0, 0>), g, dim3(cb), 0, st, pl, coarse, w.idx, w.cbase,
-                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k, nullptr, nullptr,
-                           nullptr);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<0>), g, dim3(cb), 0, st, pl, coarse, w.idx, w.cbase,
+                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
         ctx->timing_end(tok);
     }
     LGS_HIP_CHECK(hipGetLastError());
@@ -1618,32 +1792,41 @@ void launch_coarse_super(lgs_ctx* ctx, const RtcsmPlan& pl, const Workspace& w, 
                          RtcsmRecord* rec, int gen, hipStream_t st)
 {
     const int nsb2 = pl.nsbx * pl.nsby;
-    const int chunks = (nsb2 + 63) / 64;
+    const bool pair = nsb2 <= 32;
+    const int chunks = pair ? 1 : (nsb2 + 63) / 64;
     {
         const int tok = ctx->timing_begin(K_SUPER, 8.0 * (double)pl.T * nsb2 * pl.Nv);
-        hipLaunchKernelGGL(k_super, dim3(chunks, pl.T), dim3(64 * kSupWaves), 0, st, pl, w.super, w.cbase, w.zero, w.tedge,
-                           gen, w.negflag, ctx->planes_gen, w.sbound, w.part_c, w.part_k);
+        const size_t lds = sizeof(int) * (size_t)std::max(pl.Nv, 1);
+        if (ctx->skipped(K_SUPER)) {
+        } else if (pair)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<1>), dim3(chunks, pl.T), dim3(64 * kSupWaves), lds, st, pl,
+                               w.super, w.cbase, w.zero, w.tedge, gen, w.negflag, ctx->planes_gen, w.sbound,
+                               w.part_c, w.part_k);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<0>), dim3(chunks, pl.T), dim3(64 * kSupWaves), lds, st, pl,
+                               w.super, w.cbase, w.zero, w.tedge, gen, w.negflag, ctx->planes_gen, w.sbound,
+                               w.part_c, w.part_k);
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
     }
     {
-        const int tok = ctx->timing_begin(K_SEED, 8.0 * (pl.low_res * pl.low_res + kSeedCands * 16.0) * pl.Nv);
-        const size_t lds = std::max(sizeof(int) * kSeedCands, sizeof(int2)) * (size_t)pl.Nv;
-        hipLaunchKernelGGL(k_seed_super, dim3(1), dim3(1024), lds, st, pl, grid, w.idx, w.zero, w.decim, w.cbase,
-                           w.part_c, w.part_k, chunks * pl.T, w.Lp, rec);
+        const int tok = ctx->timing_begin(K_SEED, 8.0 * kSeedCands * (pl.low_res * pl.low_res + 16.0) * pl.Nv);
+        const size_t lds = sizeof(int2) * (size_t)std::max(pl.Nv, 1);
+        if (!ctx->skipped(K_SEED))
+            hipLaunchKernelGGL(k_seed_super, dim3(kSeedCands), dim3(1024), lds, st, pl, grid, w.idx, w.zero, w.decim,
+                               w.cbase, w.part_c, w.part_k, chunks * pl.T, w.Lc, rec);
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
     }
-    const int lanes = nsb2 * kSB * kSB;
-    const int cb = std::min(256, ((lanes + 63) / 64) * 64);
-    dim3 g((lanes + cb - 1) / cb, pl.T);
     const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
     if (tok >= 0) {
         ctx->pending[tok].dev_rec = rec;
         ctx->pending[tok].bytes_per_eval = 8.0 * pl.Nv;
     }
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1, 1>), g, dim3(cb), 0, st, pl, w.decim, w.idx, w.cbase, w.zero,
-                       w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k, w.sbound, w.Lp, rec);
+    const size_t lds = ((sizeof(int) * (size_t)pl.Nv + 15) & ~(size_t)15) + sizeof(double) * 128 * kRing * kRowWaves;
+    if (!ctx->skipped(K_COARSE))
+        hipLaunchKernelGGL(k_coarse_rows, dim3(pl.T, kRowSplit), dim3(64 * kRowWaves), lds, st, pl, w.decim, w.idx, w.cbase,
+                           w.zero, w.tedge, gen, w.sbound, w.Lc, w.Lp, w.cscore, w.cflag, rec);
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
 }
@@ -1703,8 +1886,9 @@ struct ScanOptions {
 // superblock pruning applies (else k_coarse scores every block)
 inline bool uses_super(const lgs_ctx* ctx, const RtcsmPlan& pl, const ScanOptions& opt)
 {
+    // k_coarse_rows: one ballot over an angle's superblocks, Nv <= 2048
     return !(opt.dense || ctx->force_dense) && ctx->coarse_planes && ctx->super_prune && ctx->super_fresh &&
-           pl.Nv <= kSeedMaxNv;
+           pl.Nv <= kSeedMaxNv && pl.nsbx * pl.nsby <= 64;
 }
 
 // Enqueue the whole device pipeline of one match on ctx->stream; returns the
@@ -1731,7 +1915,8 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
             dim3 g((pl.Nv + 255) / 256, (pl.T + kProjRows - 1) / kProjRows);
             {
                 const int tok_ = ctx->timing_begin(K_PROJECT, 24.0 * (double)pl.T * pl.Nv);
-                hipLaunchKernelGGL(k_project, g, dim3(256), 0, st, pl, scan->d_ranges, scan->d_angles,
+                if (!ctx->skipped(K_PROJECT))
+                    hipLaunchKernelGGL(k_project, g, dim3(256), 0, st, pl, scan->d_ranges, scan->d_angles,
                                    w.idx, w.cbase, w.tedge, gen, d_rec,
                                    ctx->guard_cap, ctx->guard_eps, inject);
                 ctx->timing_end(tok_);
@@ -1749,7 +1934,8 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
         }
     }
     const bool dense = opt.dense || ctx->force_dense;
-    if (uses_super(ctx, pl, opt)) {
+    const bool pruned = uses_super(ctx, pl, opt);
+    if (pruned) {
         launch_coarse_super(ctx, pl, w, grid->d, d_rec, gen, st);
     } else {
         launch_coarse(ctx, pl, w, coarse->d, gen, st);
@@ -1760,20 +1946,22 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
     LGS_HIP_CHECK(hipGetLastError());
     {
         const int tok_ = ctx->timing_begin(K_SELECT, 10.0 * (double)pl.K);
-        hipLaunchKernelGGL(k_select, dim3((unsigned)w.nseg), dim3(kSelSeg), 0, st, pl, w.cscore, w.cflag,
-                           w.Lp, w.list, w.segcnt);
+        if (!ctx->skipped(K_SELECT))
+            hipLaunchKernelGGL(k_select, dim3((unsigned)w.nseg), dim3(kSelSeg), 0, st, pl, w.cscore, w.cflag,
+                           w.Lp, pruned ? w.sbound : nullptr, w.tedge, gen, w.list, w.segcnt);
         ctx->timing_end(tok_);
     }
     LGS_HIP_CHECK(hipGetLastError());
     {
         const int tok_ = ctx->timing_begin(K_FINE, 0.0);
-        launch_fine(pl, grid->d, w, st);
+        if (!ctx->skipped(K_FINE)) launch_fine(pl, grid->d, w, st);
         ctx->timing_end(tok_);
     }
     LGS_HIP_CHECK(hipGetLastError());
     {
         const int tok_ = ctx->timing_begin(K_REPLAY, 0.0);
-        hipLaunchKernelGGL(k_replay, dim3(1), dim3(64), pref_bytes(w), st, pl, w.cscore, w.cflag, w.list,
+        if (!ctx->skipped(K_REPLAY))
+            hipLaunchKernelGGL(k_replay, dim3(1), dim3(64), pref_bytes(w), st, pl, w.cscore, w.cflag, w.list,
                            w.segcnt, w.nseg, w.fval, w.fpos, w.Lp, d_rec, w.poses7);
         ctx->timing_end(tok_);
     }
@@ -1783,9 +1971,10 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
     const double kk = (2.0 * cost->kernel_size + 1) * (2.0 * cost->kernel_size + 1);
     {
         const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * (double)scan->n);
-        hipLaunchKernelGGL(KCOST(cp), dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
-                           scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
-                           ctx->guard_eps, inject, 0, gen);
+        if (!ctx->skipped(K_COST))
+            hipLaunchKernelGGL(KCOST(cp), dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
+                               scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
+                               ctx->guard_eps, inject, 0, gen);
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
     }

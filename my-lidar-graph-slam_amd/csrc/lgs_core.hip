@@ -246,6 +246,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
         return LGS_OK;
     case LGS_OPT_COARSE_PLANES: ctx->coarse_planes = value != 0.0; return LGS_OK;
     case LGS_OPT_SUPER_PRUNE: ctx->super_prune = value != 0.0; return LGS_OK;
+    case LGS_OPT_SKIP_MASK: ctx->skip_mask = (unsigned)value; return LGS_OK;
     case LGS_OPT_GUARD_CAP:
         ctx->guard_cap = (int)value;
         if (ctx->guard_cap < 0) ctx->guard_cap = 0;
@@ -474,7 +475,8 @@ void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, c
     // algorithmic bytes: two separable passes, each reading and
     // writing one fp64 per cell = 32 B/cell
     const int tok = ctx->timing_begin(K_PRECOMPUTE, 32.0 * (double)in->w * (double)in->h);
-    if (win <= kMaxWinTiled) {
+    if (ctx->skipped(K_PRECOMPUTE)) {
+    } else if (win <= kMaxWinTiled) {
         const int fw = kTileX + win - 1, fh = kTileY + win - 1;
         const size_t lds = (size_t)(fh * fw + kTileY * fw) * sizeof(double);
         dim3 grid((in->w + kTileX - 1) / kTileX, (in->h + kTileY - 1) / kTileY);

@@ -142,6 +142,20 @@ struct CostPlan {
 
 }  // namespace lgs
 
+// Phase probes (diagnostics build only, make probe): block 0 / thread 0
+// stamps the 100 MHz wall clock at phase boundaries and prints the deltas.
+#ifdef LGS_PROBE
+#define LGS_PROBE_DECL unsigned long long lgs_probe_t[12]; int lgs_probe_n = 0
+#define LGS_PROBE_MARK() do { if (threadIdx.x == 0) lgs_probe_t[lgs_probe_n < 12 ? lgs_probe_n++ : 11] = wall_clock64(); } while (0)
+#define LGS_PROBE_PRINT(name) do { if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) { \
+    printf("probe %s:", name); for (int i_ = 1; i_ < lgs_probe_n; ++i_) printf(" %.2f", 0.01 * (double)(lgs_probe_t[i_] - lgs_probe_t[i_ - 1])); \
+    printf(" us\n"); } } while (0)
+#else
+#define LGS_PROBE_DECL do { } while (0)
+#define LGS_PROBE_MARK() do { } while (0)
+#define LGS_PROBE_PRINT(name) do { } while (0)
+#endif
+
 namespace lgs {
 enum KernelId { K_PROJECT = 0, K_COARSE, K_SEED, K_SELECT, K_FINE, K_REPLAY, K_COST, K_PRECOMPUTE,
                 K_LINSOLVE, K_RAY_EMIT, K_RAY_APPLY, K_SUPER, K_SUPER_PLANES, K_NUM_KERNELS };
@@ -173,6 +187,11 @@ struct lgs_ctx {
     // memory a destroyed context used, and its stale tags must never match.
     int next_stamp();
     bool super_fresh = false;    // superblock planes match the current phase planes
+    // LGS_OPT_SKIP_MASK (diagnostics only): launches of these kernels are
+    // skipped, leaving stale scratch -- results are meaningless; used to
+    // measure each stage's share of device throughput
+    unsigned skip_mask = 0;
+    bool skipped(int kernel) const { return (skip_mask >> kernel) & 1u; }
     int generation = 0;          // per-enqueue stamp (edge flags need no memset), from next_stamp()
     // arena
     void* buf[lgs::S_NUM_SLOTS] = {};

@@ -45,3 +45,24 @@ def main(path, skip_frac=0.3, take_frac=0.4):
 
 if __name__ == "__main__":
     main(sys.argv[1])
+
+
+def per_queue(path, skip_frac=0.3, take_frac=0.4):
+    """Per hardware queue: kernels, busy fraction and mean gap between
+    consecutive kernels (in-order queue: gaps are host/launch time)."""
+    rows = load(path)
+    ks = [r for r in rows if r[2].startswith("k_")]
+    n = len(ks)
+    sel = ks[int(n * skip_frac): int(n * (skip_frac + take_frac))]
+    t0, t1 = sel[0][0], max(r[1] for r in sel)
+    q = defaultdict(list)
+    for r in sel:
+        q[r[3]].append(r)
+    for qid, rs in sorted(q.items()):
+        rs.sort()
+        busy = sum(e - s for s, e, _, _ in rs)
+        gaps = [rs[i + 1][0] - rs[i][1] for i in range(len(rs) - 1)]
+        big = [g for g in gaps if g > 20000]
+        print(f"queue {qid}: kernels {len(rs)} busy {100.0 * busy / (t1 - t0):.1f}% "
+              f"mean gap {1e-3 * sum(gaps) / max(1, len(gaps)):.2f} us, gaps>20us {len(big)} "
+              f"(mean {1e-3 * sum(big) / max(1, len(big)):.1f} us)")
