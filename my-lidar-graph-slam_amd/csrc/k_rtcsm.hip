@@ -233,6 +233,28 @@ __global__ void k_cost_patch(int4* __restrict__ cidx, const int4* __restrict__ p
 // --------------------------------------------------------------------------
 // wave/block argmax helpers: max value, ties -> smallest key
 // --------------------------------------------------------------------------
+// Copy n elements global -> LDS with the whole workgroup, loads issued in
+// batches of 8 per thread before their stores (a plain strided loop waits one
+// memory latency per element per thread).
+template <class T>
+__device__ __forceinline__ void stage_lds(T* dst, const T* __restrict__ src, int n)
+{
+    const int nt = blockDim.x;
+    for (int v0 = threadIdx.x; v0 < n; v0 += 8 * nt) {
+        T x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int v = v0 + j * nt;
+            if (v < n) x[j] = src[v];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int v = v0 + j * nt;
+            if (v < n) dst[v] = x[j];
+        }
+    }
+}
+
 __device__ __forceinline__ double dmax2(double a, double b) { return (a < b) ? b : a; }
 
 constexpr int kSB = 4;   // superblock = kSB x kSB coarse blocks
@@ -549,7 +571,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(RtcsmPlan pl, const do
     LGS_PROBE_DECL;
     LGS_PROBE_MARK();
     const int* __restrict__ cbrow = cbase + pl.sb_off + (size_t)t * pl.Nv;
-    for (int v = threadIdx.x; v < pl.Nv; v += blockDim.x) srow[v] = cbrow[v];
+    stage_lds(srow, cbrow, pl.Nv);
     __syncthreads();
     LGS_PROBE_MARK();
     const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
@@ -597,20 +619,21 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(RtcsmPlan pl, const do
 }
 
 // k_coarse_rows (superblock pruning): coarse scores of the blocks k_select
-// could take, kRowSplit workgroups per search angle.  The angle's
-// superblocks are kept when bound > thr and (bound >= L, or the angle may
-// hold unsafe blocks); L = max of the seed candidates' fine lower bounds.
-// The angle's waves take the kept superblocks in turn; a superblock's 16
-// blocks are scored by one wave with gathers and additions transposed:
+// could take; workgroup (angle t, patch row pr) of kRowWaves waves.  The
+// angle's superblocks are kept when bound > thr and (bound >= L, or the angle
+// may hold unsafe blocks); L = max of the seed candidates' fine lower bounds.
+// Wave w scores patch row pr (4 blocks) of kept superblocks w, w + kRowWaves,
+// ...: the four rows of a superblock run on four CUs, since a CU's
+// outstanding cache-line misses, not its ALUs, pace a gather whose every beam
+// touches another line.  Gathers and additions are transposed:
 // global_load_lds (16 bytes = two neighbouring blocks' cells, no register
-// destination) lands 8 beams x 16 blocks per wave instruction in an LDS
-// ring of kRing slots, kRing instructions ahead of 16 adder lanes that walk
-// the beams in order (the reference's sequential fp64 sum).  The ring is
-// refilled slot by slot behind the adders; counted vmcnt waits keep
-// kRing - 1 gathers in flight.
-constexpr int kRowWaves = 2;   // waves per workgroup
-constexpr int kRowSplit = 2;   // workgroups per angle
-constexpr int kRing = 24;      // 1 KiB glds slots per wave
+// destination) lands 32 beams x 4 blocks per wave instruction in an LDS ring
+// of kRing slots, kRing instructions ahead of 4 adder lanes that walk the
+// beams in order (the reference's sequential fp64 sum); counted vmcnt waits
+// keep kRing - 1 gathers in flight, and each slot is refilled once read.
+constexpr int kRowWaves = 1;   // waves per workgroup
+constexpr int kRowSplit = 4;   // workgroups per (angle, patch row): kept superblocks e = z, z + 4, ...
+constexpr int kRing = 12;      // 1 KiB glds slots per wave
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14)
@@ -627,7 +650,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int s_sb[64];
     __shared__ int s_cnt;
-    const int t = blockIdx.x;
+    const int t = blockIdx.x, pr = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nsb2 = pl.nsbx * pl.nsby;
     const int Nv = pl.Nv;
@@ -636,7 +659,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
     double L = -INFINITY;
 #pragma unroll
     for (int b = 0; b < kSeedCands; ++b) L = fmax(L, Lc[b]);
-    if (t == 0 && blockIdx.y == 0 && tid == 0) *Lp = L;
+    if (t == 0 && pr == 0 && blockIdx.z == 0 && tid == 0) *Lp = L;
     const bool te = tedge[t] == gen;
     // kept superblocks of this angle (nsb2 <= 64 on this path), in key order
     if (w == 0) {
@@ -655,32 +678,29 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
                 const int a = sb % pl.nsbx, b = sb / pl.nsbx;
                 nb += (unsigned long long)(min(kSB, pl.ncx - kSB * a) * min(kSB, pl.ncy - kSB * b));
             }
-            if (nb && blockIdx.y == 0) atomicAdd(&rec->coarse_evals, nb);
+            if (nb && pr == 0 && blockIdx.z == 0) atomicAdd(&rec->coarse_evals, nb);
         }
     }
     __syncthreads();
     LGS_PROBE_MARK();
     const int cnt = s_cnt;
-    const int gw = blockIdx.y * kRowWaves + w;   // this wave among the angle's waves
-    if (cnt <= (int)blockIdx.y * kRowWaves) return;   // no superblock for this workgroup
+    if (cnt <= (int)blockIdx.z * kRowWaves) return;   // no superblock for this workgroup
     int* srow = (int*)smem;                                   // [Nv]
     const size_t srow_bytes = (sizeof(int) * (size_t)Nv + 15) & ~(size_t)15;
-    double* ring = (double*)(smem + srow_bytes) + (size_t)w * kRing * 128;   // [kRing][64 lanes][2]
-    for (int v = tid; v < Nv; v += blockDim.x) srow[v] = cbase[(size_t)t * Nv + v];
+    double* ring = (double*)(smem + srow_bytes) + (size_t)w * kRing * 128;   // [kRing][32 beams][4 blocks]
+    stage_lds(srow, cbase + (size_t)t * Nv, Nv);
     __syncthreads();
     LGS_PROBE_MARK();
-    // gather lanes: beam b of the instruction's 8, block pair p (row p / 2,
-    // columns 2 (p % 2) and + 1); adder lanes m < 16: block (m % 4, m / 4)
-    const int gb = lane >> 3, gp = lane & 7;
-    const int am = lane & 15;
-    const int aslot = ((am >> 2) * 2 + ((am & 3) >> 1)) * 2 + (am & 1);   // (beam 0) offset in doubles
-    const int ninstr = (Nv + 7) / 8;
-    for (int e = gw; e < cnt; e += kRowWaves * kRowSplit) {
+    // gather lane: beam lane / 2 of the instruction's 32, blocks 2 (lane % 2)
+    // and + 1 of the patch row; adder lane c < 4: block c of the patch row
+    const int gb = lane >> 1, gc = (lane & 1) * 2;
+    const int ninstr = (Nv + 31) / 32;
+    for (int e = blockIdx.z * kRowWaves + w; e < cnt; e += kRowWaves * kRowSplit) {
         const int sb = s_sb[e];
-        const int jx0 = kSB * (sb % pl.nsbx), jy0 = kSB * (sb / pl.nsbx);
-        const double* __restrict__ pb = cmap + ((jy0 + (gp >> 1)) * pl.Wqp + jx0 + (gp & 1) * 2);
+        const int jx0 = kSB * (sb % pl.nsbx), jy = kSB * (sb / pl.nsbx) + pr;
+        const double* __restrict__ pb = cmap + (jy * pl.Wqp + jx0 + gc);
         auto offset_of = [&](int i) {   // unconditional LDS read (a branch would cost counted waits)
-            const int v = 8 * i + gb;
+            const int v = 32 * i + gb;
             const int o = srow[min(v, Nv - 1)];
             return (v < Nv) ? o : -1;
         };
@@ -689,34 +709,33 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
             __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(ring + (i % kRing) * 128), 16, 0, 0);
         };
         for (int i = 0; i < kRing; ++i) issue(i, offset_of(i));   // past the scan: the zero cells
-        const int jx = jx0 + (am & 3), jy = jy0 + (am >> 2);
-        const bool active = lane < 16 && jx < pl.ncx && jy < pl.ncy;
-        // LDS reads of slot i + 1 are issued before slot i's additions (their
-        // latency hides behind the add chain); slot i is refilled once read
+        const int jx = jx0 + (lane & 3);
+        const bool active = lane < 4 && jx < pl.ncx && jy < pl.ncy;
         double acc = 0.0;
-        double ra[8], rb[8];
-        auto read_slot = [&](int i, double (&x)[8]) {
-            const double* slot = ring + (i % kRing) * 128 + aslot;
+        // slot i + 1 -> nxt (LDS reads issued before slot i is added), then
+        // slot i is refilled
+        double ra[32], rb[32];
+        auto read_slot = [&](int i, double (&x)[32]) {
+            const double* slot = ring + (i % kRing) * 128 + (lane & 3);
 #pragma unroll
-            for (int bb = 0; bb < 8; ++bb) x[bb] = slot[bb * 16];
+            for (int bb = 0; bb < 32; ++bb) x[bb] = slot[bb * 4];
         };
-        int off_next = offset_of(kRing);
-        // one step: slot i + 1 -> nxt (LDS), add cur (slot i), refill slot i
-        auto step = [&](int i, double (&cur)[8], double (&nxt)[8]) {
+        int offn = offset_of(kRing);
+        auto step = [&](int i, double (&cur)[32], double (&nxt)[32]) {
             __builtin_amdgcn_s_waitcnt(waitcnt_imm(kRing - 2, 15));   // instruction i + 1 has landed
-            read_slot(i + 1, nxt);   // past the scan: zero cells or unused slot contents, never added
+            read_slot(i + 1, nxt);   // past the scan: zero cells or unused slot contents
+            const int oc = offn;
+            offn = offset_of(i + kRing + 1);
             __builtin_amdgcn_sched_barrier(0);
-            const int off_cur = off_next;
-            off_next = offset_of(i + kRing + 1);
-            const int nb = min(8, Nv - 8 * i);
+            // beams past the scan read the zero cells: adding +0.0 to a sum that
+            // starts at +0.0 is exact (as in seq_sum), so no tail predicate
             double s = acc;
 #pragma unroll
-            for (int bb = 0; bb < 8; ++bb)
-                if (bb < nb) s += cur[bb];
+            for (int bb = 0; bb < 32; ++bb) s += cur[bb];
             acc = s;
-            __builtin_amdgcn_sched_barrier(0);   // the additions stay ahead of the wait
+            __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));   // slot i + 1 is in registers
-            issue(i + kRing, off_cur);                        // refills slot i (read one step earlier)
+            issue(i + kRing, oc);                             // refill slot i
             __builtin_amdgcn_sched_barrier(0);
         };
         LGS_PROBE_MARK();
@@ -730,16 +749,16 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
         }
         LGS_PROBE_MARK();
         __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15));   // ring drained before its reuse
-        // unsafe test (angles that may hold unsafe blocks only): lane (m, q)
-        // checks beams q, q + 4, ..., OR-reduced over the quarters
+        // unsafe test (angles that may hold unsafe blocks only): lane (c, q)
+        // checks beams q, q + 16, ..., OR-reduced over q
         bool unsafe = false;
-        const int um = lane & 15, uq = lane >> 4;
-        const int ujx = jx0 + (um & 3), ujy = jy0 + (um >> 2);
-        if (te && ujx < pl.ncx && ujy < pl.ncy) {
+        const int uc = lane & 3, uq = lane >> 2;
+        const int ujx = jx0 + uc;
+        if (te && ujx < pl.ncx && jy < pl.ncy) {
             const int2* __restrict__ id = idx + (size_t)t * Nv;
             const int lr = pl.low_res, lo = -(lr - 1);
-            const int x0 = -pl.win_x + ujx * lr, y0 = -pl.win_y + ujy * lr;
-            for (int v = uq; v < Nv; v += 4) {
+            const int x0 = -pl.win_x + ujx * lr, y0 = -pl.win_y + jy * lr;
+            for (int v = uq; v < Nv; v += 16) {
                 const int2 c = id[v];
                 if (c.x - pl.win_x < 0 || c.y - pl.win_y < 0) {
                     const int x = c.x + x0, y = c.y + y0;
@@ -747,8 +766,8 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
                 }
             }
         }
-        unsafe |= __shfl_xor((int)unsafe, 16, 64) != 0;
-        unsafe |= __shfl_xor((int)unsafe, 32, 64) != 0;
+#pragma unroll
+        for (int off = 4; off < 64; off <<= 1) unsafe |= __shfl_xor((int)unsafe, off, 64) != 0;
         if (active) {
             const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
             cscore[k] = acc;
@@ -757,7 +776,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
         LGS_PROBE_MARK();
     }
 #ifdef LGS_PROBE
-    if (tid == 0 && cnt >= 1 && blockIdx.y == 0)
+    if (tid == 0 && cnt >= 1 && pr == 0 && blockIdx.z == 0)
         printf("probe coarse_rows t=%d cnt=%d: select %.2f stage %.2f issue %.2f fill %.2f loop %.2f tail %.2f us\n",
                t, cnt, 0.01 * (double)(lgs_probe_t[1] - lgs_probe_t[0]),
                0.01 * (double)(lgs_probe_t[2] - lgs_probe_t[1]), 0.01 * (double)(lgs_probe_t[3] - lgs_probe_t[2]),
@@ -786,8 +805,8 @@ __device__ void eval_block(const RtcsmPlan& pl, const double* __restrict__ grid,
     const int2* __restrict__ id = idx + (size_t)tt * pl.Nv;
     const int lane = threadIdx.x & 63;
     __syncthreads();
-    for (int v = lane; v < pl.Nv + 2 * kPipe; v += 64)
-        sidx[v] = (v < pl.Nv) ? id[v] : make_int2(-(1 << 28), -(1 << 28));
+    stage_lds(sidx, id, pl.Nv);
+    for (int v = pl.Nv + lane; v < pl.Nv + 2 * kPipe; v += 64) sidx[v] = make_int2(-(1 << 28), -(1 << 28));
     __syncthreads();
     double bv = -1.0;
     long long bo = LLONG_MAX;
@@ -831,30 +850,37 @@ constexpr int kMaxChunks = 32;   // transposed evaluator handles Nv <= 2048
 typedef double d2a8 __attribute__((ext_vector_type(2), aligned(8)));
 
 
-template <int LR>
+// row >= 0 (row split): the workgroup is one wave that evaluates block row
+// yo = row only; (f, pos) is then that row's best, and the caller combines the
+// LR rows (k_replay).
+template <int LR, int DEPTH = 2>
 __device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ grid,
                              const int2* __restrict__ idx, const double* __restrict__ zero,
                              long long k, char* smem, double* sv, long long* sk, double& f,
-                             int& pos)
+                             int& pos, int row = -1)
 {
     constexpr int LD = 65;
     const int tt = (int)(k / pl.P);
     const int rem = (int)(k % pl.P);
     const int jx = rem / pl.ncy, jy = rem % pl.ncy;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = row >= 0 ? row : (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int xc = -pl.win_x + jx * LR, yr = -pl.win_y + jy * LR + wave;
     const int W = pl.W, H = pl.H, Nv = pl.Nv;
     const int2* __restrict__ id = idx + (size_t)tt * Nv;
     int2* sidx = (int2*)smem;                                        // [Nv]
-    double* bufs = (double*)(smem + sizeof(int2) * (size_t)((Nv + 1) & ~1)) + wave * 2 * LR * LD;
+    double* bufs = (double*)(smem + sizeof(int2) * (size_t)((Nv + 1) & ~1)) + (row >= 0 ? 0 : wave) * 2 * LR * LD;
     const int nchunk = (Nv + 63) / 64;
 
     __syncthreads();
-    for (int v = threadIdx.x; v < Nv; v += blockDim.x) sidx[v] = id[v];
+    stage_lds(sidx, id, Nv);
     __syncthreads();
 
-    constexpr int kDepth = 2;   // measured: depth 4 made k_fine slower (36 vs 27 us)
-    double ra[LR], rb[LR];
+
+    // chunks of gathers in flight: 2 for the LR-wave block evaluation (depth 4
+    // there made k_fine slower, 36 vs 27 us: register pressure at LR waves per
+    // workgroup); the one-wave row split affords more
+    constexpr int kDepth = DEPTH;
+    double r[DEPTH][LR];
     // A lane's LR cells are consecutive doubles of one row: when the whole
     // run is inside the map (all but the border beams) it is fetched with
     // 16-byte loads (8-byte aligned, which gfx950 global loads accept), i.e.
@@ -866,7 +892,10 @@ __device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ gri
         const bool bv = b < Nv;
         const int x0 = ij.x + xc, y = ij.y + yr;
         bool full = false;
-        if constexpr (LR == 5) full = bv & ((unsigned)y < (unsigned)H) & (x0 >= 0) & (x0 + LR - 1 < W);
+        // 16-byte loads for the inner runs (LR waves, depth 2: fewer memory
+        // instructions per CU); the row split (depth > 2) keeps every lane's
+        // instruction sequence identical, so the waits count exactly
+        if constexpr (LR == 5 && DEPTH == 2) full = bv & ((unsigned)y < (unsigned)H) & (x0 >= 0) & (x0 + LR - 1 < W);
         if (full) {
             const double* p = grid + (unsigned)(y * W + x0);
             const d2a8 a = *(const d2a8*)p;
@@ -915,24 +944,31 @@ __device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ gri
     // gathers contiguous and in program order.  The in-order LDS of a wave
     // makes two row buffers enough (a store never overtakes the previous
     // chunk's reads).
-    gather(0, ra);
-    __builtin_amdgcn_sched_barrier(0);
-    gather(1, rb);
-    __builtin_amdgcn_sched_barrier(0);
-    auto stage = [&](int c, double (&r)[LR], double* buf) {
-        store(r, buf);
+    static_for_step<0, DEPTH, 1>([&](auto dd) {
+        gather(decltype(dd)::value, r[decltype(dd)::value]);
         __builtin_amdgcn_sched_barrier(0);
-        gather(c + kDepth, r);
+        return true;
+    });
+    auto stage = [&](int c, double (&x)[LR], double* buf) {
+        store(x, buf);
+        __builtin_amdgcn_sched_barrier(0);
+        gather(c + kDepth, x);
         __builtin_amdgcn_sched_barrier(0);
         add_chunk(c, buf);
     };
     static_for_step<0, kMaxChunks, kDepth>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
-        if (c >= nchunk) return false;
-        stage(c, ra, bufs);
-        if (c + 1 >= nchunk) return false;
-        stage(c + 1, rb, bufs + LR * LD);
-        return true;
+        bool go = true;
+        static_for_step<0, DEPTH, 1>([&](auto dd) {
+            constexpr int d = decltype(dd)::value;
+            if (c + d >= nchunk) {
+                go = false;
+                return false;
+            }
+            stage(c + d, r[d], bufs + (d & 1) * LR * LD);
+            return true;
+        });
+        return go;
     });
     double bv = -1.0;
     long long bo = LLONG_MAX;
@@ -940,7 +976,18 @@ __device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ gri
         bv = acc;
         bo = (long long)lane * LR + wave;
     }
-    block_argmax(bv, bo, sv, sk);
+    if (row >= 0) {
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ov = __shfl_xor(bv, off, 64);
+            const long long ok = __shfl_xor(bo, off, 64);
+            if (better(ov, ok, bv, bo)) {
+                bv = ov;
+                bo = ok;
+            }
+        }
+    } else {
+        block_argmax(bv, bo, sv, sk);
+    }
     f = bv;
     pos = (int)bo;
 }
@@ -1064,7 +1111,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(
         const int ct = (int)(ck / nsb2), csb = (int)(ck % nsb2);
         // 2. member sums: member m = tid % 16, beam group tid / 16 (64 groups)
         int* srow = (int*)smem;   // [Nv]
-        for (int v = tid; v < Nv; v += blockDim.x) srow[v] = cbase[(size_t)ct * Nv + v];
+        stage_lds(srow, cbase + (size_t)ct * Nv, Nv);
         __syncthreads();
         const int m = tid & 15, g = tid >> 4;
         const int jx = kSB * (csb % pl.nsbx) + (m & 3);
@@ -1108,7 +1155,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(
         int2* sidx = (int2*)smem;   // [Nv]
         __syncthreads();
         LGS_PROBE_MARK();
-        for (int v = tid; v < Nv; v += blockDim.x) sidx[v] = idx[(size_t)ct * Nv + v];
+        stage_lds(sidx, idx + (size_t)ct * Nv, Nv);
         __syncthreads();
         LGS_PROBE_MARK();
         int QP = 1;
@@ -1253,10 +1300,14 @@ __device__ __forceinline__ int seg_of(const int* pref, int nseg, int b)
     return lo;
 }
 
-// k_fine: the listed blocks, dense position b = blockIdx.x, +gridDim.x, ...
-// (LR as in k_seed).  fval/fpos are indexed by dense position.
+// k_fine: the listed blocks, dense position b.  LR > 0: one single-wave
+// workgroup per (block, block row) item b * LR + row = blockIdx.x,
+// +gridDim.x, ... (a block's LR rows on LR CUs: the gathers of one CU's
+// memory pipeline are what a block evaluation waits on); fval/fpos are
+// indexed by item and k_replay combines a block's rows.  LR == 0: one wave
+// per block, indexed by dense position.
 template <int LR>
-__global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_fine(
+__global__ __launch_bounds__(64) void k_fine(
     RtcsmPlan pl, const double* __restrict__ grid, const int2* __restrict__ idx,
     const double* __restrict__ zero, const int* __restrict__ list, const int* __restrict__ segcnt,
     int nseg, unsigned eval_smem, double* __restrict__ fval, int* __restrict__ fpos)
@@ -1266,22 +1317,29 @@ __global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_fine(
     __shared__ long long sk[16];
     __shared__ int ws[16];
     int* pref = (int*)(smem + eval_smem);
+    LGS_PROBE_DECL;
+    LGS_PROBE_MARK();
     seg_prefix(segcnt, nseg, pref, ws);
+    LGS_PROBE_MARK();
     const int n = pref[nseg];
-    for (int b = blockIdx.x; b < n; b += gridDim.x) {
+    constexpr int R = LR > 0 ? LR : 1;
+    for (int it = blockIdx.x; it < n * R; it += gridDim.x) {
+        const int b = it / R;
         const int sg = seg_of(pref, nseg, b);
         const long long k = list[(size_t)sg * kSelSeg + (b - pref[sg])];
         double f;
         int pos;
         if constexpr (LR > 0)
-            eval_block_t<LR>(pl, grid, idx, zero, k, smem, sv, sk, f, pos);
+            eval_block_t<LR, 4>(pl, grid, idx, zero, k, smem, sv, sk, f, pos, it % R);
         else
             eval_block(pl, grid, idx, zero, k, (int2*)smem, f, pos);
         if (threadIdx.x == 0) {
-            fval[b] = f;
-            fpos[b] = pos;
+            fval[it] = f;
+            fpos[it] = pos;
         }
+        LGS_PROBE_MARK();
     }
+    LGS_PROBE_PRINT("fine(seg_prefix, item0[, item1])");
 }
 
 // k_replay (one wave): the reference's sequential acceptance (:98-114 with the
@@ -1293,7 +1351,7 @@ __global__ __launch_bounds__(64) void k_replay(RtcsmPlan pl, const double* __res
                                                const int* __restrict__ list,
                                                const int* __restrict__ segcnt, int nseg,
                                                const double* __restrict__ fval,
-                                               const int* __restrict__ fpos,
+                                               const int* __restrict__ fpos, int frows,
                                                const double* __restrict__ Lp, RtcsmRecord* rec,
                                                double* __restrict__ poses7)
 {
@@ -1316,8 +1374,18 @@ __global__ __launch_bounds__(64) void k_replay(RtcsmPlan pl, const double* __res
             const int sg = seg_of(pref, nseg, b);
             k = list[(size_t)sg * kSelSeg + (b - pref[sg])];
             c = cscore[k];
-            f = fval[b];
-            pos = fpos[b];
+            // k_fine's frows row results of the block: max, ties to the
+            // smallest order index (the reference's x-outer, y-inner walk)
+            f = fval[(size_t)b * frows];
+            pos = fpos[(size_t)b * frows];
+            for (int r = 1; r < frows; ++r) {
+                const double fr = fval[(size_t)b * frows + r];
+                const int pr = fpos[(size_t)b * frows + r];
+                if (fr > f || (fr == f && pr < pos)) {
+                    f = fr;
+                    pos = pr;
+                }
+            }
             if (cflag[k] && c < L && f >= L) dangerous = true;
         }
         const int cnt = min(64, n - b0);
@@ -1650,8 +1718,9 @@ struct Workspace {
     int* list;          // [nseg * kSelSeg] selected blocks, per segment
     int* segcnt;        // [nseg]
     int nseg;
-    double* fval;
+    double* fval;       // [K * frows] k_fine results per (block, row)
     int* fpos;
+    int frows;
     double* part_c;
     long long* part_k;
     int* count;  // [0] = list count
@@ -1668,6 +1737,9 @@ struct Workspace {
     double* zero;
     int* tedge;
 };
+
+// k_fine's items per block: LR rows on the transposed path (LowRes 5), 1 otherwise
+inline int fine_rows(const RtcsmPlan& pl) { return (pl.Nv <= 64 * kMaxChunks && pl.low_res == 5) ? 5 : 1; }
 
 inline size_t sidx_bytes(const RtcsmPlan& pl) { return sizeof(int2) * (size_t)(pl.Nv + 2 * kPipe); }
 
@@ -1710,8 +1782,9 @@ Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
     w.nseg = (int)((K + kSelSeg - 1) / kSelSeg);
     w.segcnt = (int*)ctx->ensure(S_SEL, sizeof(int) * (size_t)w.nseg);
     w.list = (int*)ctx->ensure(S_LIST, sizeof(int) * (size_t)w.nseg * kSelSeg);
-    w.fval = (double*)ctx->ensure(S_FVAL, sizeof(double) * K);
-    w.fpos = (int*)ctx->ensure(S_FPOS, sizeof(int) * K);
+    w.frows = fine_rows(pl);
+    w.fval = (double*)ctx->ensure(S_FVAL, sizeof(double) * K * w.frows);
+    w.fpos = (int*)ctx->ensure(S_FPOS, sizeof(int) * K * w.frows);
     w.part_c = (double*)ctx->ensure(S_PART_C, sizeof(double) * part_alloc);
     w.part_k = (long long*)ctx->ensure(S_PART_K, sizeof(long long) * part_alloc);
     char* cnt = (char*)ctx->ensure(S_COUNT, 128);
@@ -1825,7 +1898,7 @@ void launch_coarse_super(lgs_ctx* ctx, const RtcsmPlan& pl, const Workspace& w, 
     }
     const size_t lds = ((sizeof(int) * (size_t)pl.Nv + 15) & ~(size_t)15) + sizeof(double) * 128 * kRing * kRowWaves;
     if (!ctx->skipped(K_COARSE))
-        hipLaunchKernelGGL(k_coarse_rows, dim3(pl.T, kRowSplit), dim3(64 * kRowWaves), lds, st, pl, w.decim, w.idx, w.cbase,
+        hipLaunchKernelGGL(k_coarse_rows, dim3(pl.T, kSB, kRowSplit), dim3(64 * kRowWaves), lds, st, pl, w.decim, w.idx, w.cbase,
                            w.zero, w.tedge, gen, w.sbound, w.Lc, w.Lp, w.cscore, w.cflag, rec);
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
@@ -1852,15 +1925,16 @@ void launch_seed(const RtcsmPlan& pl, const double* grid, const Workspace& w, in
 }
 // k_fine's grid: one workgroup per CU, looping over the selected blocks (the
 // count is known only on the device; idle workgroups still hold wave slots)
-constexpr int kFineGrid = 256;
+constexpr int kFineGrid = 1024;
 // dynamic LDS: the evaluator's buffers, then the segment prefix (nseg + 1 ints)
 inline size_t pref_bytes(const Workspace& w) { return sizeof(int) * (size_t)(w.nseg + 1); }
 
 template <int LR>
 void launch_fine_t(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
 {
-    const size_t e = (eval_t_smem<LR>(pl.Nv) + 15) & ~size_t(15);
-    hipLaunchKernelGGL(k_fine<LR>, dim3(kFineGrid), dim3(64 * LR), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
+    // one wave's share of the evaluator's LDS (row split)
+    const size_t e = (sizeof(int2) * (size_t)((pl.Nv + 1) & ~1) + sizeof(double) * 2 * LR * 65 + 15) & ~size_t(15);
+    hipLaunchKernelGGL(k_fine<LR>, dim3(kFineGrid), dim3(64), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
                        w.list, w.segcnt, w.nseg, (unsigned)e, w.fval, w.fpos);
 }
 void launch_fine(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
@@ -1962,7 +2036,7 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
         const int tok_ = ctx->timing_begin(K_REPLAY, 0.0);
         if (!ctx->skipped(K_REPLAY))
             hipLaunchKernelGGL(k_replay, dim3(1), dim3(64), pref_bytes(w), st, pl, w.cscore, w.cflag, w.list,
-                           w.segcnt, w.nseg, w.fval, w.fpos, w.Lp, d_rec, w.poses7);
+                           w.segcnt, w.nseg, w.fval, w.fpos, w.frows, w.Lp, d_rec, w.poses7);
         ctx->timing_end(tok_);
     }
     LGS_HIP_CHECK(hipGetLastError());
