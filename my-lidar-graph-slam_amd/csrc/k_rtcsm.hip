@@ -1134,20 +1134,35 @@ __global__ __launch_bounds__(1024) void k_seed_super(
             }
             s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         }
-        red[tid] = s;
+        // member totals: the wave's 4 groups by shuffles, then the 16 waves
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if ((tid & 63) < 16) red[(tid >> 6) * 16 + m] = s;
         __syncthreads();
         LGS_PROBE_MARK();
-        double mv = -1.0;
-        long long mk = LLONG_MAX;
-        if (tid < 16) {
-            double tot = 0.0;
-            for (int j = 0; j < 64; ++j) tot += red[j * 16 + tid];
-            if (valid) {
-                mv = tot;
-                mk = (long long)ct * pl.P + (long long)jx * pl.ncy + jy;
+        if (tid < 64) {
+            double mv = -1.0;
+            long long mk = LLONG_MAX;
+            if (tid < 16) {
+                double tot = 0.0;
+                for (int j = 0; j < (int)(blockDim.x >> 6); ++j) tot += red[j * 16 + tid];
+                if (valid) {
+                    mv = tot;
+                    mk = (long long)ct * pl.P + (long long)jx * pl.ncy + jy;
+                }
             }
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ov = __shfl_xor(mv, off, 64);
+                const long long ok = __shfl_xor(mk, off, 64);
+                if (better(ov, ok, mv, mk)) {
+                    mv = ov;
+                    mk = ok;
+                }
+            }
+            if (tid == 0) sk[0] = mk;
         }
-        block_argmax(mv, mk, sv, sk);
+        __syncthreads();
+        const long long mk = sk[0];
         // 3. fine scores of block mk, any order, rounding-bounded
         const int rem = (int)(mk % pl.P);
         const int bjx = rem / pl.ncy, bjy = rem % pl.ncy;
@@ -1186,21 +1201,42 @@ __global__ __launch_bounds__(1024) void k_seed_super(
         }
         __syncthreads();
         LGS_PROBE_MARK();
-        red[tid] = fs;
-        reda[tid] = fa;
-        __syncthreads();
-        double lv = -INFINITY;
-        if (tid < npose) {
-            double ts = 0.0, ta = 0.0;
-            for (int j = 0; j < G; ++j) {
-                ts += red[j * QP + tid];
-                ta += reda[j * QP + tid];
-            }
-            lv = ts - (4.0 * (double)(Nv + 2) * 0x1p-53) * ta;
+        // pose totals: lanes of a wave with equal q (QP < 64) by shuffles,
+        // then the waves through LDS
+        for (int off = QP; off < 64; off <<= 1) {
+            fs += __shfl_xor(fs, off, 64);
+            fa += __shfl_xor(fa, off, 64);
         }
-        long long dummy = tid;
-        block_argmax(lv, dummy, sv, sk);
-        Lmine = lv;
+        const int wq = min(QP, 64);
+        if ((tid & 63) < wq) {
+            red[(tid >> 6) * wq + (tid & 63)] = fs;
+            reda[(tid >> 6) * wq + (tid & 63)] = fa;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            double lv = -INFINITY;
+            // poses q: this lane's q (QP <= 64) or q = tid + 64 j (QP > 64)
+            for (int q0 = tid; q0 < npose; q0 += 64) {
+                double ts = 0.0, ta = 0.0;
+                if (QP <= 64) {
+                    for (int j = 0; j < (int)(blockDim.x >> 6); ++j) {
+                        ts += red[j * wq + q0];
+                        ta += reda[j * wq + q0];
+                    }
+                } else {   // QP > 64: a wave holds 64 poses of one group
+                    for (int j = 0; j < (int)(blockDim.x >> 6); ++j)
+                        if (((j * 64) % QP) == (q0 / 64) * 64) {
+                            ts += red[j * wq + (q0 & 63)];
+                            ta += reda[j * wq + (q0 & 63)];
+                        }
+                }
+                lv = fmax(lv, ts - (4.0 * (double)(Nv + 2) * 0x1p-53) * ta);
+            }
+            for (int off = 32; off > 0; off >>= 1) lv = fmax(lv, __shfl_xor(lv, off, 64));
+            if (tid == 0) sv[0] = lv;
+        }
+        __syncthreads();
+        Lmine = sv[0];
         LGS_PROBE_MARK();
     }
     // 4. publish
@@ -1559,21 +1595,20 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double
         tm[i] = term;
     }
     __syncthreads();
+    // costValue -= exp(..) (C/mapping/cost_function_greedy_endpoint.cpp): the
+    // cost feeds the normalized cost and the covariance, both held to 1e-5
+    // (north_star), so the terms are summed as a tree (the reference's
+    // beam-order chain differs in the last bits only)
+    __shared__ double wsum[kCostThreads / 64];
+    double part = 0.0;
+    for (int i = threadIdx.x; i < cp.N; i += blockDim.x) part += tm[i];
+    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = part;
+    __syncthreads();
     if (threadIdx.x == 0) {
-        // costValue -= exp(..) in beam order; reads batched so that only the
-        // subtraction chain is serial
-        double cost = 0.0;
-        int i = 0;
-        for (; i + 16 <= cp.N; i += 16) {
-            double t[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) t[j] = tm[i + j];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) cost -= t[j];
-        }
-        for (; i < cp.N; ++i) cost -= tm[i];
-        cost *= cp.scaling_factor;
-        rec->costs[pi] = cost;
+        double tot = 0.0;
+        for (int j = 0; j < (int)(blockDim.x >> 6); ++j) tot += wsum[j];
+        rec->costs[pi] = (0.0 - tot) * cp.scaling_factor;
     }
 }
 
