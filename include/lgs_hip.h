@@ -20,6 +20,9 @@
  *   lgs_rtcsm_optimize_pose_query  ScanMatcherRealTimeCorrelative::OptimizePose(query)
  *                                C/mapping/scan_matcher_real_time_correlative.cpp:31-47
  *                                (the ScanMatcher plugin entry, H/mapping/scan_matcher.hpp:198-199)
+ *   lgs_rtcsm_optimize_pose_query_batch  n independent OptimizePose(query) calls
+ *                                (C/mapping/scan_matcher_real_time_correlative.cpp:31-47 each)
+ *                                as one batched device pipeline
  *   lgs_rtcsm_optimize_pose_batch  LoopDetectorRealTimeCorrelative::Detect's per-node
  *                                loop C/mapping/loop_detector_real_time_correlative.cpp:66-92
  *   lgs_loop_detect_rtcsm        LoopDetectorRealTimeCorrelative::Detect + FindCorrespondingPose
@@ -194,8 +197,20 @@ int  lgs_rtcsm_optimize_pose_query(lgs_ctx* ctx, const lgs_grid* grid,
                                    const lgs_cost_ge_params* cost,
                                    const lgs_scan* scan, lgs_pose2d initial_pose,
                                    lgs_rtcsm_summary* out);
-/* n independent matches against one grid, enqueued back to back with one
- * host synchronisation (loop-closure candidates, C/.../loop_detector_real_time_correlative.cpp:66) */
+/* n independent OptimizePose(query) calls (each query: its map, scan and
+ * initial pose; every query computes its own coarse map, as the reference's
+ * OptimizePose(query) does, even when two queries pass the same map).  One
+ * batched device pipeline: every stage is a single launch over all n queries.
+ * The maps of one call must share size and resolution.  out[j] is
+ * bit-identical to lgs_rtcsm_optimize_pose_query on query j. */
+int  lgs_rtcsm_optimize_pose_query_batch(lgs_ctx* ctx, const lgs_grid* const* grids,
+                                         const lgs_rtcsm_params* params,
+                                         const lgs_cost_ge_params* cost,
+                                         const lgs_scan* const* scans,
+                                         const lgs_pose2d* initial_poses, int n,
+                                         lgs_rtcsm_summary* out);
+/* n independent matches against one grid and its coarse map, as one batched
+ * device pipeline (loop-closure candidates, C/.../loop_detector_real_time_correlative.cpp:66) */
 int  lgs_rtcsm_optimize_pose_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                                    const lgs_rtcsm_params* params,
                                    const lgs_cost_ge_params* cost,

@@ -38,6 +38,7 @@ using namespace lgs;
 
 namespace lgs {
 void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, const PlaneGeom* planes);
+void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, int maxW, int maxH, int win);
 bool precompute_planes_ok(const lgs_grid* in, int win);
 }
 
@@ -46,6 +47,58 @@ namespace {
 
 constexpr int kPipe = 16;   // seq_sum gathers in flight per batch (index arrays padded by 2*kPipe)
 constexpr int kPad = 4 * kPipe;   // cbase padding past the last row (seq_sum4's look-ahead)
+
+// One match of a batched launch (DESIGN.md §3 "batched matching").  A batch's
+// items are uploaded once to device memory; every stage is ONE launch for the
+// whole batch, a grid dimension selecting the item, and each workgroup reads
+// its item through a `const __restrict__` kernel argument with a uniform index
+// (scalar loads).  Items of one batch share the search parameters (P, ncx,
+// ncy, nsb2, low_res); T and Nv differ per scan (grids use the maxima and
+// workgroups past an item's extent exit).  Items matching against the same
+// map share its coarse planes (cmap/super/negflag/pgen).
+struct MatchItem {
+    RtcsmPlan pl;
+    CostPlan cp;
+    const double* grid;      // fine map
+    const double* ranges;
+    const double* angles;
+    const double* cmap;      // coarse map: padded phase planes (or the plain map)
+    const double* super;     // superblock planes of cmap
+    const int* negflag;      // stamped with pgen when the planes hold a negative cell
+    int pgen;                // build stamp of the planes
+    int gen;                 // this match's generation stamp
+    RtcsmRecord* rec;
+    int2* idx;
+    int* cbase;
+    int* tedge;
+    double* cscore;
+    uint8_t* cflag;
+    int* list;
+    int* segcnt;
+    int nseg;
+    int frows;
+    double* fval;
+    int* fpos;
+    double* part_c;
+    long long* part_k;
+    int nparts;
+    double* Lp;
+    double* Lc;
+    double* sbound;
+    double* poses7;
+    int4* cidx;
+    double* terms;
+};
+typedef const MatchItem* __restrict__ Items;
+
+// Per-set superblock-plane job: one coarse map's padded phase planes.
+struct PlaneJob {
+    RtcsmPlan pl;            // layout fields (Wqp, Hqp, pstride, pstride4, sub4, Wq4)
+    const double* planes;
+    double* super;
+    int* negflag;
+    int pgen;
+};
 
 // Generation-tagged counter (gen << 32 | count): a word left by an earlier
 // match counts as zero, so records need no memset.  Returns this caller's slot.
@@ -115,13 +168,18 @@ __device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
 // (fewer, longer waves: the GPU's wave slots, not its ALUs, are what
 // concurrent matches compete for).
 constexpr int kProjRows = 4;
-__global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __restrict__ ranges,
-                                                 const double* __restrict__ angles,
-                                                 int2* __restrict__ idx, int* __restrict__ cbase,
-                                                 int* __restrict__ tedge, int gen,
-                                                 RtcsmRecord* rec, int guard_cap, double guard_eps,
-                                                 int inject)
+__global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, double guard_eps, int inject)
 {
+    const MatchItem& it = items[blockIdx.z];
+    const RtcsmPlan& pl = it.pl;
+    if ((int)blockIdx.y * kProjRows >= pl.T) return;   // past this item's angles (uniform)
+    const double* __restrict__ ranges = it.ranges;
+    const double* __restrict__ angles = it.angles;
+    int2* __restrict__ idx = it.idx;
+    int* __restrict__ cbase = it.cbase;
+    int* __restrict__ tedge = it.tedge;
+    const int gen = it.gen;
+    RtcsmRecord* rec = it.rec;
     __shared__ int s_map[256];
     __shared__ int s_wsum[4];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -193,10 +251,13 @@ __global__ __launch_bounds__(256) void k_project(RtcsmPlan pl, const double* __r
     }
 }
 
-__global__ void k_patch(RtcsmPlan pl, int2* __restrict__ idx, int* __restrict__ cbase,
-                        int* __restrict__ tedge, int gen, const int4* __restrict__ patches,
-                        int n)
+__global__ void k_patch(Items items, const int4* __restrict__ patches, int n)
 {
+    const RtcsmPlan& pl = items[0].pl;
+    int2* __restrict__ idx = items[0].idx;
+    int* __restrict__ cbase = items[0].cbase;
+    int* __restrict__ tedge = items[0].tedge;
+    const int gen = items[0].gen;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const int4 p = patches[k];
@@ -208,9 +269,13 @@ __global__ void k_patch(RtcsmPlan pl, int2* __restrict__ idx, int* __restrict__ 
 }
 
 // full host projection -> coarse info
-__global__ void k_cinfo(RtcsmPlan pl, const int2* __restrict__ idx, int* __restrict__ cbase,
-                        int* __restrict__ tedge, int gen)
+__global__ void k_cinfo(Items items)
 {
+    const RtcsmPlan& pl = items[0].pl;
+    const int2* __restrict__ idx = items[0].idx;
+    int* __restrict__ cbase = items[0].cbase;
+    int* __restrict__ tedge = items[0].tedge;
+    const int gen = items[0].gen;
     const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (o < kPad) {
         cbase[(size_t)pl.T * pl.Nv + o] = 0;
@@ -420,12 +485,20 @@ __device__ __forceinline__ double seq_sum4(int n, Fetch fetch, Addr addr)
 //   PLANES = 0: the coarse map as is (stride lr between lanes).
 // --------------------------------------------------------------------------
 template <int PLANES>
-__global__ __launch_bounds__(1024) void k_coarse(
-    RtcsmPlan pl, const double* __restrict__ cmap, const int2* __restrict__ idx,
-    const int* __restrict__ cbase, const double* __restrict__ zero,
-    const int* __restrict__ tedge, int gen, double* __restrict__ cscore,
-    uint8_t* __restrict__ cflag, double* __restrict__ part_c, long long* __restrict__ part_k)
+__global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __restrict__ zero)
 {
+    const MatchItem& it = items[blockIdx.z];
+    const RtcsmPlan& pl = it.pl;
+    if ((int)blockIdx.y >= pl.T) return;   // past this item's angles (uniform)
+    const double* __restrict__ cmap = it.cmap;
+    const int2* __restrict__ idx = it.idx;
+    const int* __restrict__ cbase = it.cbase;
+    const int* __restrict__ tedge = it.tedge;
+    const int gen = it.gen;
+    double* __restrict__ cscore = it.cscore;
+    uint8_t* __restrict__ cflag = it.cflag;
+    double* __restrict__ part_c = it.part_c;
+    long long* __restrict__ part_k = it.part_k;
     __shared__ double sv[16];
     __shared__ long long sk[16];
     const int tt = blockIdx.y;
@@ -498,17 +571,23 @@ __global__ __launch_bounds__(1024) void k_coarse(
 // NaN fails c > thr and is never selected anyway.
 constexpr int kSPX = 64, kSPY = 32;   // output tile of k_super_planes
 
-__global__ __launch_bounds__(256) void k_super_planes(const double* __restrict__ P, double* __restrict__ S,
-                                                      RtcsmPlan pl, int* __restrict__ negflag, int pgen)
+__global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
 {
+    const PlaneJob& job = jobs[blockIdx.z / nplanes];
+    const int plane = blockIdx.z % nplanes;
+    const RtcsmPlan& pl = job.pl;
+    const double* __restrict__ P = job.planes;
+    double* __restrict__ S = job.super;
+    int* __restrict__ negflag = job.negflag;
+    const int pgen = job.pgen;
     const int Wqp = pl.Wqp, Hqp = pl.Hqp;
     const long long pstride = pl.pstride;
     constexpr int TW = kSPX + kSB - 1, TH = kSPY + kSB - 1;
     __shared__ double tile[TH][TW];
     __shared__ double hm[TH][kSPX];
     const int x0 = blockIdx.x * kSPX, y0 = blockIdx.y * kSPY;
-    const double* __restrict__ base = P + blockIdx.z * pstride;
-    double* __restrict__ out = S + blockIdx.z * pl.pstride4;
+    const double* __restrict__ base = P + plane * pstride;
+    double* __restrict__ out = S + plane * pl.pstride4;
     const int tid = threadIdx.x;
     bool neg = false;
     for (int k = tid; k < TH * TW; k += blockDim.x) {
@@ -550,13 +629,20 @@ __global__ __launch_bounds__(256) void k_super_planes(const double* __restrict__
 // blocks).
 constexpr int kSupWaves = 4;
 template <int PAIR>
-__global__ __launch_bounds__(64 * kSupWaves) void k_super(RtcsmPlan pl, const double* __restrict__ sp,
-                                                const int* __restrict__ cbase, const double* __restrict__ zero,
-                                                const int* __restrict__ tedge, int gen,
-                                                const int* __restrict__ negflag, int pgen,
-                                                double* __restrict__ sbound, double* __restrict__ part_c,
-                                                long long* __restrict__ part_k)
+__global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const double* __restrict__ zero)
 {
+    const MatchItem& it = items[blockIdx.z];
+    const RtcsmPlan& pl = it.pl;
+    if ((int)blockIdx.y >= pl.T) return;   // past this item's angles (uniform)
+    const double* __restrict__ sp = it.super;
+    const int* __restrict__ cbase = it.cbase;
+    const int* __restrict__ tedge = it.tedge;
+    const int gen = it.gen;
+    const int* __restrict__ negflag = it.negflag;
+    const int pgen = it.pgen;
+    double* __restrict__ sbound = it.sbound;
+    double* __restrict__ part_c = it.part_c;
+    long long* __restrict__ part_k = it.part_k;
     extern __shared__ int srow[];   // [Nv]
     __shared__ double red[kSupWaves][64];
     constexpr int SPW = PAIR ? 32 : 64;   // superblocks per chunk
@@ -641,12 +727,23 @@ constexpr unsigned waitcnt_imm(unsigned vm, unsigned lgkm)
 {
     return (vm & 15u) | (7u << 4) | ((lgkm & 15u) << 8) | ((vm >> 4) << 14);
 }
-__global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
-    RtcsmPlan pl, const double* __restrict__ cmap, const int2* __restrict__ idx, const int* __restrict__ cbase,
-    const double* __restrict__ zero, const int* __restrict__ tedge, int gen, const double* __restrict__ sbound,
-    const double* __restrict__ Lc, double* __restrict__ Lp, double* __restrict__ cscore,
-    uint8_t* __restrict__ cflag, RtcsmRecord* rec)
+__global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, const double* __restrict__ zero)
 {
+    const MatchItem& it = items[blockIdx.z / kRowSplit];
+    const int split = blockIdx.z % kRowSplit;   // kept superblocks e = split, split + kRowSplit, ...
+    const RtcsmPlan& pl = it.pl;
+    if ((int)blockIdx.x >= pl.T) return;   // past this item's angles (uniform)
+    const double* __restrict__ cmap = it.cmap;
+    const int2* __restrict__ idx = it.idx;
+    const int* __restrict__ cbase = it.cbase;
+    const int* __restrict__ tedge = it.tedge;
+    const int gen = it.gen;
+    const double* __restrict__ sbound = it.sbound;
+    const double* __restrict__ Lc = it.Lc;
+    double* __restrict__ Lp = it.Lp;
+    double* __restrict__ cscore = it.cscore;
+    uint8_t* __restrict__ cflag = it.cflag;
+    RtcsmRecord* rec = it.rec;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int s_sb[64];
     __shared__ int s_cnt;
@@ -659,7 +756,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
     double L = -INFINITY;
 #pragma unroll
     for (int b = 0; b < kSeedCands; ++b) L = fmax(L, Lc[b]);
-    if (t == 0 && pr == 0 && blockIdx.z == 0 && tid == 0) *Lp = L;
+    if (t == 0 && pr == 0 && split == 0 && tid == 0) *Lp = L;
     const bool te = tedge[t] == gen;
     // kept superblocks of this angle (nsb2 <= 64 on this path), in key order
     if (w == 0) {
@@ -678,13 +775,13 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
                 const int a = sb % pl.nsbx, b = sb / pl.nsbx;
                 nb += (unsigned long long)(min(kSB, pl.ncx - kSB * a) * min(kSB, pl.ncy - kSB * b));
             }
-            if (nb && pr == 0 && blockIdx.z == 0) atomicAdd(&rec->coarse_evals, nb);
+            if (nb && pr == 0 && split == 0) atomicAdd(&rec->coarse_evals, nb);
         }
     }
     __syncthreads();
     LGS_PROBE_MARK();
     const int cnt = s_cnt;
-    if (cnt <= (int)blockIdx.z * kRowWaves) return;   // no superblock for this workgroup
+    if (cnt <= split * kRowWaves) return;   // no superblock for this workgroup
     int* srow = (int*)smem;                                   // [Nv]
     const size_t srow_bytes = (sizeof(int) * (size_t)Nv + 15) & ~(size_t)15;
     double* ring = (double*)(smem + srow_bytes) + (size_t)w * kRing * 128;   // [kRing][32 beams][4 blocks]
@@ -695,7 +792,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
     // and + 1 of the patch row; adder lane c < 4: block c of the patch row
     const int gb = lane >> 1, gc = (lane & 1) * 2;
     const int ninstr = (Nv + 31) / 32;
-    for (int e = blockIdx.z * kRowWaves + w; e < cnt; e += kRowWaves * kRowSplit) {
+    for (int e = split * kRowWaves + w; e < cnt; e += kRowWaves * kRowSplit) {
         const int sb = s_sb[e];
         const int jx0 = kSB * (sb % pl.nsbx), jy = kSB * (sb / pl.nsbx) + pr;
         const double* __restrict__ pb = cmap + (jy * pl.Wqp + jx0 + gc);
@@ -776,7 +873,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(
         LGS_PROBE_MARK();
     }
 #ifdef LGS_PROBE
-    if (tid == 0 && cnt >= 1 && pr == 0 && blockIdx.z == 0)
+    if (tid == 0 && cnt >= 1 && pr == 0 && split == 0)
         printf("probe coarse_rows t=%d cnt=%d: select %.2f stage %.2f issue %.2f fill %.2f loop %.2f tail %.2f us\n",
                t, cnt, 0.01 * (double)(lgs_probe_t[1] - lgs_probe_t[0]),
                0.01 * (double)(lgs_probe_t[2] - lgs_probe_t[1]), 0.01 * (double)(lgs_probe_t[3] - lgs_probe_t[2]),
@@ -1002,11 +1099,17 @@ constexpr size_t eval_t_smem(int Nv)
 // final score (every safe block's fine max is <= the reference's final score).
 // LR > 0: transposed evaluation with LR waves; LR == 0: generic one-wave path.
 template <int LR>
-__global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_seed(
-    RtcsmPlan pl, const double* __restrict__ grid, const int2* __restrict__ idx,
-    const double* __restrict__ zero, const double* __restrict__ part_c,
-    const long long* __restrict__ part_k, int nparts, double* __restrict__ Lout, int force_dense)
+__global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_seed(Items items, const double* __restrict__ zero,
+                                                                 int force_dense)
 {
+    const MatchItem& it = items[blockIdx.y];
+    const RtcsmPlan& pl = it.pl;
+    const double* __restrict__ grid = it.grid;
+    const int2* __restrict__ idx = it.idx;
+    const double* __restrict__ part_c = it.part_c;
+    const long long* __restrict__ part_k = it.part_k;
+    const int nparts = it.nparts;
+    double* __restrict__ Lout = it.Lp;
     extern __shared__ char smem[];
     __shared__ double sv[16];
     __shared__ long long sk[16];
@@ -1053,12 +1156,19 @@ __global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_seed(
 constexpr int kSeedMaxNv = 2048;   // LDS: the candidate row (Nv ints / int2)
 constexpr int kSeedRegParts = 4;   // parts held in registers per thread
 
-__global__ __launch_bounds__(1024) void k_seed_super(
-    RtcsmPlan pl, const double* __restrict__ grid, const int2* __restrict__ idx,
-    const double* __restrict__ zero, const double* __restrict__ cmap, const int* __restrict__ cbase,
-    const double* __restrict__ part_c, const long long* __restrict__ part_k, int nparts,
-    double* __restrict__ Lc, RtcsmRecord* rec)
+__global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* __restrict__ zero)
 {
+    const MatchItem& it = items[blockIdx.y];
+    const RtcsmPlan& pl = it.pl;
+    const double* __restrict__ grid = it.grid;
+    const int2* __restrict__ idx = it.idx;
+    const double* __restrict__ cmap = it.cmap;
+    const int* __restrict__ cbase = it.cbase;
+    const double* __restrict__ part_c = it.part_c;
+    const long long* __restrict__ part_k = it.part_k;
+    const int nparts = it.nparts;
+    double* __restrict__ Lc = it.Lc;
+    RtcsmRecord* rec = it.rec;
     extern __shared__ char smem[];
     __shared__ double sv[16];
     __shared__ long long sk[16];
@@ -1259,12 +1369,19 @@ constexpr int kSelSeg = 1024;
 // sbound (superblock pruning, else nullptr): blocks of superblocks
 // k_coarse_rows did not keep were never scored and are never taken (the
 // same keep rule, evaluated again here).
-__global__ __launch_bounds__(kSelSeg) void k_select(RtcsmPlan pl, const double* __restrict__ cscore,
-                                                   const uint8_t* __restrict__ cflag,
-                                                   const double* __restrict__ Lp, const double* __restrict__ sbound,
-                                                   const int* __restrict__ tedge, int gen,
-                                                   int* __restrict__ list, int* __restrict__ segcnt)
+__global__ __launch_bounds__(kSelSeg) void k_select(Items items, int use_sbound)
 {
+    const MatchItem& it = items[blockIdx.y];
+    if ((int)blockIdx.x >= it.nseg) return;   // past this item's segments (uniform)
+    const RtcsmPlan& pl = it.pl;
+    const double* __restrict__ cscore = it.cscore;
+    const uint8_t* __restrict__ cflag = it.cflag;
+    const double* __restrict__ Lp = it.Lp;
+    const double* __restrict__ sbound = use_sbound ? it.sbound : nullptr;
+    const int* __restrict__ tedge = it.tedge;
+    const int gen = it.gen;
+    int* __restrict__ list = it.list;
+    int* __restrict__ segcnt = it.segcnt;
     __shared__ int s_w[kSelSeg / 64];
     const long long k = (long long)blockIdx.x * kSelSeg + threadIdx.x;
     bool f = false;
@@ -1343,11 +1460,17 @@ __device__ __forceinline__ int seg_of(const int* pref, int nseg, int b)
 // indexed by item and k_replay combines a block's rows.  LR == 0: one wave
 // per block, indexed by dense position.
 template <int LR>
-__global__ __launch_bounds__(64) void k_fine(
-    RtcsmPlan pl, const double* __restrict__ grid, const int2* __restrict__ idx,
-    const double* __restrict__ zero, const int* __restrict__ list, const int* __restrict__ segcnt,
-    int nseg, unsigned eval_smem, double* __restrict__ fval, int* __restrict__ fpos)
+__global__ __launch_bounds__(64) void k_fine(Items items, const double* __restrict__ zero, unsigned eval_smem)
 {
+    const MatchItem& it_ = items[blockIdx.y];
+    const RtcsmPlan& pl = it_.pl;
+    const double* __restrict__ grid = it_.grid;
+    const int2* __restrict__ idx = it_.idx;
+    const int* __restrict__ list = it_.list;
+    const int* __restrict__ segcnt = it_.segcnt;
+    const int nseg = it_.nseg;
+    double* __restrict__ fval = it_.fval;
+    int* __restrict__ fpos = it_.fpos;
     extern __shared__ char smem[];
     __shared__ double sv[16];
     __shared__ long long sk[16];
@@ -1382,15 +1505,21 @@ __global__ __launch_bounds__(64) void k_fine(
 // strict update of :246) over the selected blocks in block order.  Lanes load
 // 64 consecutive entries at once; the acceptance itself walks them in lane
 // order with wave-uniform shuffles.  Then the 7 cost poses.
-__global__ __launch_bounds__(64) void k_replay(RtcsmPlan pl, const double* __restrict__ cscore,
-                                               const uint8_t* __restrict__ cflag,
-                                               const int* __restrict__ list,
-                                               const int* __restrict__ segcnt, int nseg,
-                                               const double* __restrict__ fval,
-                                               const int* __restrict__ fpos, int frows,
-                                               const double* __restrict__ Lp, RtcsmRecord* rec,
-                                               double* __restrict__ poses7)
+__global__ __launch_bounds__(64) void k_replay(Items items)
 {
+    const MatchItem& it = items[blockIdx.x];
+    const RtcsmPlan& pl = it.pl;
+    const double* __restrict__ cscore = it.cscore;
+    const uint8_t* __restrict__ cflag = it.cflag;
+    const int* __restrict__ list = it.list;
+    const int* __restrict__ segcnt = it.segcnt;
+    const int nseg = it.nseg;
+    const double* __restrict__ fval = it.fval;
+    const int* __restrict__ fpos = it.fpos;
+    const int frows = it.frows;
+    const double* __restrict__ Lp = it.Lp;
+    RtcsmRecord* rec = it.rec;
+    double* __restrict__ poses7 = it.poses7;
     extern __shared__ int pref[];   // nseg + 1
     __shared__ int ws[16];
     seg_prefix(segcnt, nseg, pref, ws);
@@ -1537,16 +1666,19 @@ __device__ __forceinline__ double min_sq_dist(const CostPlan& cp, const double* 
 // mode 0: compute cells (+ guard records) and store them in cidx;
 // mode 1: read cells from cidx (after host patches).
 template <int KS>
-__global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double* __restrict__ grid,
-                                                       const double* __restrict__ ranges,
-                                                       const double* __restrict__ angles,
-                                                       const double* __restrict__ poses,
-                                                       int4* __restrict__ cidx,
-                                                       double* __restrict__ gterms,
-                                                       RtcsmRecord* rec, int guard_cap,
-                                                       double guard_eps, int inject, int mode,
-                                                       int gen)
+__global__ __launch_bounds__(kCostThreads) void k_cost(Items items, int guard_cap, double guard_eps, int inject,
+                                                       int mode)
 {
+    const MatchItem& it = items[blockIdx.y];
+    const CostPlan& cp = it.cp;
+    const double* __restrict__ grid = it.grid;
+    const double* __restrict__ ranges = it.ranges;
+    const double* __restrict__ angles = it.angles;
+    const double* __restrict__ poses = it.poses7;
+    int4* __restrict__ cidx = it.cidx;
+    double* __restrict__ gterms = it.terms;
+    RtcsmRecord* rec = it.rec;
+    const int gen = it.gen;
     __shared__ double lterms[kCostLdsTerms];
     const int pi = blockIdx.x;
     const bool in_lds = cp.N <= kCostLdsTerms;
@@ -1613,7 +1745,7 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(CostPlan cp, const double
 }
 
 // kernel size 1 (the launcher JSON's) gets the unrolled instantiation
-#define KCOST(cp) ((cp).kernel_size == 1 ? k_cost<1> : k_cost<0>)
+#define KCOST(ks) ((ks) == 1 ? k_cost<1> : k_cost<0>)
 
 // --------------------------------------------------------------------------
 // dense diagnostics: every fine score of the window (one lane per pose)
@@ -1711,21 +1843,6 @@ RtcsmPlan make_plan(const lgs_grid* grid, const lgs_rtcsm_params* p, const lgs_s
     return pl;
 }
 
-// the plan fields the coarse-map layout depends on (no scan needed)
-RtcsmPlan layout_plan(const lgs_grid* grid, const lgs_rtcsm_params* p)
-{
-    RtcsmPlan pl{};
-    pl.W = grid->w;
-    pl.H = grid->h;
-    pl.low_res = p->low_resolution;
-    pl.win_x = (int)std::ceil(0.5 * p->range_x / grid->res);
-    pl.win_y = (int)std::ceil(0.5 * p->range_y / grid->res);
-    pl.ncx = (2 * pl.win_x) / pl.low_res + 1;
-    pl.ncy = (2 * pl.win_y) / pl.low_res + 1;
-    set_plane_layout(pl);
-    return pl;
-}
-
 CostPlan make_cost_plan(const lgs_grid* grid, const lgs_cost_ge_params* c, const lgs_scan* s)
 {
     CostPlan cp{};
@@ -1745,245 +1862,304 @@ CostPlan make_cost_plan(const lgs_grid* grid, const lgs_cost_ge_params* c, const
     return cp;
 }
 
-struct Workspace {
-    int2* idx;
-    int* cbase;         // [T*Nv + 2*kPipe] padded-plane base offset per (angle, beam)
-    double* cscore;
-    uint8_t* cflag;
-    int* list;          // [nseg * kSelSeg] selected blocks, per segment
-    int* segcnt;        // [nseg]
-    int nseg;
-    double* fval;       // [K * frows] k_fine results per (block, row)
-    int* fpos;
-    int frows;
-    double* part_c;
-    long long* part_k;
-    int* count;  // [0] = list count
-    double* Lp;
-    double* poses7;
-    int4* cidx;
-    double* terms;
-    int nparts;
-    double* decim;      // padded phase planes
-    double* super;      // superblock planes (same layout)
-    double* sbound;     // [T * nsb2]
-    int* negflag;
-    double* Lc;         // [kSeedCands] per-candidate seeds
-    double* zero;
-    int* tedge;
-};
-
 // k_fine's items per block: LR rows on the transposed path (LowRes 5), 1 otherwise
-inline int fine_rows(const RtcsmPlan& pl) { return (pl.Nv <= 64 * kMaxChunks && pl.low_res == 5) ? 5 : 1; }
+inline bool lr5_path(int nv_max, int low_res) { return nv_max <= 64 * kMaxChunks && low_res == 5; }
 
-inline size_t sidx_bytes(const RtcsmPlan& pl) { return sizeof(int2) * (size_t)(pl.Nv + 2 * kPipe); }
+inline size_t sidx_bytes(int nv) { return sizeof(int2) * (size_t)(nv + 2 * kPipe); }
 
 inline int coarse_block(const RtcsmPlan& pl) { return std::min(1024, ((pl.P + 63) / 64) * 64); }
 
-// The padded phase-plane buffer (S_DECIM); its zero margins are written once
-// per (buffer, layout) -- the kernels only ever write the interior.
-double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl)
+inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// Host staging of one batch's descriptors: appended to a pinned buffer, then
+// one host-to-device copy into the S_UPLOAD slot (flush).  Offsets are
+// returned at append time; device addresses are base + offset after flush.
+struct Upload {
+    lgs_ctx* ctx;
+    std::vector<char> host;
+    char* dev = nullptr;
+    explicit Upload(lgs_ctx* c) : ctx(c) {}
+    template <class T>
+    size_t append(const T* p, size_t n)
+    {
+        const size_t off = align256(host.size());
+        host.resize(off + sizeof(T) * n);
+        std::memcpy(host.data() + off, p, sizeof(T) * n);
+        return off;
+    }
+    void flush()
+    {
+        const size_t b = std::max<size_t>(host.size(), 16);
+        char* pin = (char*)ctx->ensure_pinned_up(b);
+        std::memcpy(pin, host.data(), host.size());
+        dev = (char*)ctx->ensure(S_UPLOAD, b);
+        LGS_HIP_CHECK(hipMemcpyAsync(dev, pin, host.size(), hipMemcpyHostToDevice, ctx->stream));
+    }
+    template <class T>
+    const T* at(size_t off) const { return (const T*)(dev + off); }
+};
+
+// Shape of one batched launch sequence: every item shares the search
+// parameters; T and Nv (and K = T * P) differ per scan, so the launch grids
+// and dynamic LDS use the maxima.
+struct BatchShape {
+    int n = 0;
+    int Tmax = 0, NvMax = 0, nsegMax = 0, nparts_max = 0;
+    int P = 0, nsb2 = 0, chunks = 0, low_res = 0, cb = 0;
+    bool pair = false;
+    bool planes = false;    // coarse map in padded phase planes
+    bool pruned = false;    // superblock pruning
+    bool lr5 = false;       // transposed LR = 5 evaluators
+    int frows = 1;
+    int kernel_size = 0;
+};
+
+// per-(chunk|tile, angle) best entries the seed kernel scans: k_super's
+// chunks (pruned) or k_coarse's block tiles
+inline int item_nparts(const BatchShape& B, const RtcsmPlan& pl, bool pruned)
 {
-    const size_t bytes = sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride;
+    return pruned ? B.chunks * pl.T : ((B.P + B.cb - 1) / B.cb) * pl.T;
+}
+
+// superblock pruning applies (else k_coarse scores every block)
+inline bool uses_super(const lgs_ctx* ctx, int nv_max, int nsb2, bool dense)
+{
+    // k_coarse_rows: one ballot over an angle's superblocks, Nv <= 2048
+    return !(dense || ctx->force_dense) && ctx->coarse_planes && ctx->super_prune && nv_max <= kSeedMaxNv &&
+           nsb2 <= 64;
+}
+
+// Per-item workspace: one contiguous region per item carved from S_BATCH_WS
+// (sized for the batch's largest plan), field offsets below.
+struct ItemLayout {
+    size_t idx, cbase, cscore, cflag, list, segcnt, fval, fpos, part_c, part_k, tedge, sbound, poses7, cidx,
+        terms, count, total;
+};
+ItemLayout item_layout(int Tmax, int NvMax, int P, int nsb2, int chunks, int cb, int frows, int Nmax)
+{
+    ItemLayout L{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += align256(std::max<size_t>(bytes, 16));
+        return r;
+    };
+    const size_t K = (size_t)Tmax * P;
+    const size_t nidx = (size_t)Tmax * std::max(NvMax, 1) + kPad;   // seq_sum's look-ahead padding
+    const size_t nseg = (K + kSelSeg - 1) / kSelSeg;
+    const size_t nparts = std::max<size_t>((size_t)((P + cb - 1) / cb) * Tmax, (size_t)chunks * Tmax);
+    L.idx = take(sizeof(int2) * nidx);
+    L.cbase = take(sizeof(int) * 2 * nidx);   // coarse bases, then superblock bases
+    L.cscore = take(sizeof(double) * K);
+    L.cflag = take(K);
+    L.list = take(sizeof(int) * nseg * kSelSeg);
+    L.segcnt = take(sizeof(int) * nseg);
+    L.fval = take(sizeof(double) * K * frows);
+    L.fpos = take(sizeof(int) * K * frows);
+    L.part_c = take(sizeof(double) * nparts);
+    L.part_k = take(sizeof(long long) * nparts);
+    L.tedge = take(sizeof(int) * (size_t)Tmax);
+    L.sbound = take(sizeof(double) * (size_t)Tmax * std::max(nsb2, 1));
+    L.poses7 = take(sizeof(double) * 21);
+    L.cidx = take(sizeof(int4) * 7 * (size_t)Nmax);
+    L.terms = take(sizeof(double) * 7 * (size_t)Nmax);
+    L.count = take(128);   // Lp, Lc[kSeedCands]
+    L.total = o;
+    return L;
+}
+
+void bind_workspace(MatchItem& it, char* base, const ItemLayout& L, int frows)
+{
+    it.idx = (int2*)(base + L.idx);
+    it.cbase = (int*)(base + L.cbase);
+    it.cscore = (double*)(base + L.cscore);
+    it.cflag = (uint8_t*)(base + L.cflag);
+    it.list = (int*)(base + L.list);
+    it.segcnt = (int*)(base + L.segcnt);
+    it.fval = (double*)(base + L.fval);
+    it.fpos = (int*)(base + L.fpos);
+    it.part_c = (double*)(base + L.part_c);
+    it.part_k = (long long*)(base + L.part_k);
+    it.tedge = (int*)(base + L.tedge);
+    it.sbound = (double*)(base + L.sbound);
+    it.poses7 = (double*)(base + L.poses7);
+    it.cidx = (int4*)(base + L.cidx);
+    it.terms = (double*)(base + L.terms);
+    it.Lp = (double*)(base + L.count);
+    it.Lc = (double*)(base + L.count + 64);
+    static_assert(64 + 8 * kSeedCands <= 128, "count block layout");
+    it.frows = frows;
+    it.nseg = (int)((it.pl.K + kSelSeg - 1) / kSelSeg);
+}
+
+// Padded phase-plane buffers of nsets coarse maps (S_DECIM, set s at
+// s * plane_bytes); their zero margins are written once per (buffer, layout,
+// set count) -- the kernels only ever write the interiors.
+inline size_t plane_bytes(const RtcsmPlan& pl)
+{
+    return align256(sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride);
+}
+inline size_t super_bytes(const RtcsmPlan& pl)
+{
+    return align256(sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
+}
+double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets)
+{
+    const size_t bytes = plane_bytes(pl) * (size_t)nsets;
     double* D = (double*)ctx->ensure(S_DECIM, bytes);
     const long long key[4] = { pl.low_res, pl.Wq, pl.Hq, pl.M };
-    if (D != ctx->planes_ptr || std::memcmp(key, ctx->planes_key, sizeof(key)) != 0) {
+    if (D != ctx->planes_ptr || std::memcmp(key, ctx->planes_key, sizeof(key)) != 0 || nsets > ctx->planes_sets) {
         LGS_HIP_CHECK(hipMemsetAsync(D, 0, bytes, ctx->stream));
         ctx->planes_ptr = D;
+        ctx->planes_sets = nsets;
         std::memcpy(ctx->planes_key, key, sizeof(key));
     }
     return D;
 }
 
-Workspace ensure_workspace(lgs_ctx* ctx, const RtcsmPlan& pl, int N)
+// One coarse map of a batch: where its planes live and how they are built.
+struct PlaneSet {
+    const lgs_grid* fine = nullptr;     // precompute from this fine map (OptimizePose(query))
+    const lgs_grid* coarse = nullptr;   // or decimate this caller-supplied coarse map
+    const double* cmap = nullptr;       // what k_coarse / k_seed_super read
+    const double* super = nullptr;
+    const int* negflag = nullptr;
+    int pgen = 0;
+};
+
+// Build the coarse maps of every set: batched precompute straight into the
+// padded phase planes (query path) or a phase-plane copy of a supplied coarse
+// map, then the superblock planes of all sets in one launch.  Without phase
+// planes (LGS_OPT_COARSE_PLANES 0) the sets read plain coarse maps.
+struct SetJobs {
+    size_t jobs_off = 0, njobs = 0, pj_off = 0, npj = 0;
+};
+void launch_decimate(const double* coarse, const RtcsmPlan& pl, double* D, hipStream_t st);
+SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& sets, bool need_super, Upload& up)
 {
-    Workspace w{};
-    const int cb = coarse_block(pl);
-    const int tiles = (pl.P + cb - 1) / cb;
-    w.nparts = tiles * pl.T;
-    w.decim = ctx->coarse_planes ? planes_buffer(ctx, pl) : nullptr;
-    const int nsb2 = pl.nsbx * pl.nsby;
-    // part arrays: k_coarse's per-tile bests (w.nparts) or k_super's per-chunk bests
-    const size_t part_alloc = (size_t)std::max(w.nparts, (nsb2 + 63) / 64 * pl.T);
-    w.super = (double*)ctx->ensure(S_SUPER, sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
-    w.sbound = (double*)ctx->ensure(S_SBOUND, sizeof(double) * (size_t)pl.T * nsb2);
-    const size_t K = (size_t)pl.K;
-    // index arrays padded by 2*kPipe entries: seq_sum's look-ahead loads
-    const size_t nidx = (size_t)pl.T * std::max(pl.Nv, 1) + kPad;
-    w.idx = (int2*)ctx->ensure(S_IDX, sizeof(int2) * nidx);
-    w.cbase = (int*)ctx->ensure(S_CINFO, sizeof(int) * 2 * nidx);   // coarse bases, then superblock bases
-    w.cscore = (double*)ctx->ensure(S_CSCORE, sizeof(double) * K);
-    w.cflag = (uint8_t*)ctx->ensure(S_CFLAG, K);
-    w.nseg = (int)((K + kSelSeg - 1) / kSelSeg);
-    w.segcnt = (int*)ctx->ensure(S_SEL, sizeof(int) * (size_t)w.nseg);
-    w.list = (int*)ctx->ensure(S_LIST, sizeof(int) * (size_t)w.nseg * kSelSeg);
-    w.frows = fine_rows(pl);
-    w.fval = (double*)ctx->ensure(S_FVAL, sizeof(double) * K * w.frows);
-    w.fpos = (int*)ctx->ensure(S_FPOS, sizeof(int) * K * w.frows);
-    w.part_c = (double*)ctx->ensure(S_PART_C, sizeof(double) * part_alloc);
-    w.part_k = (long long*)ctx->ensure(S_PART_K, sizeof(long long) * part_alloc);
-    char* cnt = (char*)ctx->ensure(S_COUNT, 128);
-    w.count = (int*)cnt;
-    w.Lp = (double*)(cnt + 16);
-    w.negflag = (int*)(cnt + 32);
-    static_assert(64 + 8 * kSeedCands <= 128, "S_COUNT layout");
-    w.Lc = (double*)(cnt + 64);   // kSeedCands doubles
-    w.zero = ctx->zero;  // zero cell for out-of-map gathers
-    w.tedge = (int*)ctx->ensure(S_TEDGE, sizeof(int) * (size_t)pl.T);
-    w.poses7 = (double*)ctx->ensure(S_POSES7, sizeof(double) * 21);
-    w.cidx = (int4*)ctx->ensure(S_COST_IDX, sizeof(int4) * 7 * (size_t)N);
-    w.terms = (double*)ctx->ensure(S_COST_TERM, sizeof(double) * 7 * (size_t)N);
-    return w;
+    const int ns = (int)sets.size();
+    hipStream_t st = ctx->stream;
+    const int lr = lp.low_res;
+    if (!ctx->coarse_planes) {
+        // plain layout: precomputed sets get a plain scratch map each
+        int nfine = 0;
+        for (auto& s : sets) nfine += s.fine != nullptr;
+        const size_t cells = (size_t)lp.W * lp.H;
+        double* plain = nfine ? (double*)ctx->ensure(S_COARSE_GRID, sizeof(double) * std::max<size_t>(1, cells) * nfine)
+                              : nullptr;
+        int k = 0;
+        for (auto& s : sets) {
+            if (s.fine) {
+                double* out = plain + cells * (size_t)k++;
+                launch_precompute(ctx, s.fine, lr, out, nullptr);
+                s.cmap = out;
+            } else {
+                s.cmap = s.coarse->d;
+            }
+        }
+        return SetJobs{};
+    }
+    double* D = planes_buffer(ctx, lp, ns);
+    const size_t pb = plane_bytes(lp) / sizeof(double);
+    // precompute: straight into the planes when W, H are multiples of LowRes,
+    // else into a plain scratch that is then decimated
+    std::vector<PrecompJob> jobs;
+    std::vector<int> via_plain;
+    for (int s = 0; s < ns; ++s) {
+        sets[s].cmap = D + pb * (size_t)s;
+        if (!sets[s].fine) continue;
+        if (precompute_planes_ok(sets[s].fine, lr)) {
+            PrecompJob j{};
+            j.in = sets[s].fine->d;
+            j.out = D + pb * (size_t)s;
+            j.W = sets[s].fine->w;
+            j.H = sets[s].fine->h;
+            j.pg = PlaneGeom{ lp.M, lp.Wqp, lp.pstride };
+            jobs.push_back(j);
+        } else {
+            via_plain.push_back(s);
+        }
+    }
+    if (!via_plain.empty()) {
+        const size_t cells = (size_t)lp.W * lp.H;
+        double* plain = (double*)ctx->ensure(S_COARSE_GRID, sizeof(double) * std::max<size_t>(1, cells));
+        for (int s : via_plain) {   // rare (odd map sizes): one set at a time through the shared scratch
+            launch_precompute(ctx, sets[s].fine, lr, plain, nullptr);
+            launch_decimate(plain, lp, D + pb * (size_t)s, st);
+        }
+    }
+    for (int s = 0; s < ns; ++s)
+        if (!sets[s].fine) launch_decimate(sets[s].coarse->d, lp, D + pb * (size_t)s, st);
+    const size_t jobs_off = jobs.empty() ? 0 : up.append(jobs.data(), jobs.size());
+    // superblock planes
+    std::vector<PlaneJob> pj;
+    double* S = nullptr;
+    int* neg = nullptr;
+    if (need_super) {
+        S = (double*)ctx->ensure(S_SUPER, super_bytes(lp) * (size_t)ns);
+        neg = (int*)ctx->ensure(S_NEGFLAG, sizeof(int) * (size_t)ns);
+        for (int s = 0; s < ns; ++s) {
+            PlaneJob j{};
+            j.pl = lp;
+            j.planes = D + pb * (size_t)s;
+            j.super = S + super_bytes(lp) / sizeof(double) * (size_t)s;
+            j.negflag = neg + s;
+            j.pgen = ctx->next_stamp();
+            sets[s].super = j.super;
+            sets[s].negflag = j.negflag;
+            sets[s].pgen = j.pgen;
+            pj.push_back(j);
+        }
+    }
+    const size_t pj_off = pj.empty() ? 0 : up.append(pj.data(), pj.size());
+    // the descriptors of this step go up with the batch's items (one copy):
+    // the caller flushes before calling launch_sets
+    SetJobs sj;
+    sj.jobs_off = jobs_off;
+    sj.njobs = jobs.size();
+    sj.pj_off = pj_off;
+    sj.npj = pj.size();
+    return sj;
 }
 
-// Superblock planes of the current phase planes (after every planes build).
-void launch_super_planes(lgs_ctx* ctx, const RtcsmPlan& pl, hipStream_t st)
+// Launch the set builds staged by build_sets (after the upload's flush).
+void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>& sets, const SetJobs& sj,
+                 const Upload& up)
 {
-    double* D = planes_buffer(ctx, pl);
-    double* S = (double*)ctx->ensure(S_SUPER, sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
-    int* negflag = (int*)((char*)ctx->ensure(S_COUNT, 128) + 32);
-    const int pgen = ctx->planes_gen = ctx->next_stamp();
-    dim3 g((pl.Wqp + kSPX - 1) / kSPX, (pl.Hqp + kSPY - 1) / kSPY, pl.low_res * pl.low_res);
-    const int tok = ctx->timing_begin(K_SUPER_PLANES, 8.0 * 2.0 * (double)pl.low_res * pl.low_res * pl.pstride);
+    if (!ctx->coarse_planes) return;
+    int maxW = 0, maxH = 0;
+    for (auto& s : sets)
+        if (s.fine) {
+            maxW = std::max(maxW, s.fine->w);
+            maxH = std::max(maxH, s.fine->h);
+        }
+    if (sj.njobs) launch_precompute_jobs(ctx, up.at<PrecompJob>(sj.jobs_off), (int)sj.njobs, maxW, maxH, lp.low_res);
+    if (sj.npj) {
+        const int np = lp.low_res * lp.low_res;
+        dim3 g((lp.Wqp + kSPX - 1) / kSPX, (lp.Hqp + kSPY - 1) / kSPY, np * (int)sj.npj);
+        const int tok = ctx->timing_begin(K_SUPER_PLANES, 8.0 * 2.0 * (double)np * lp.pstride * sj.npj);
         if (!ctx->skipped(K_SUPER_PLANES))
-        hipLaunchKernelGGL(k_super_planes, g, dim3(256), 0, st, D, S, pl, negflag, pgen);
-
-    ctx->timing_end(tok);
-    LGS_HIP_CHECK(hipGetLastError());
-    ctx->super_fresh = true;
+            hipLaunchKernelGGL(k_super_planes, g, dim3(256), 0, ctx->stream, up.at<PlaneJob>(sj.pj_off), np);
+        ctx->timing_end(tok);
+        LGS_HIP_CHECK(hipGetLastError());
+    }
 }
 
-// after the planes were (re)written
-void planes_written(lgs_ctx* ctx, const RtcsmPlan& pl, hipStream_t st)
+// Phase-plane copy of a plain coarse map into planes D.
+void launch_decimate(const double* coarse, const RtcsmPlan& pl, double* D, hipStream_t st)
 {
-    if (ctx->super_prune) launch_super_planes(ctx, pl, st);
-    else ctx->super_fresh = false;
-}
-
-// Phase-plane copy of a plain coarse map into the context's S_DECIM slot
-// (once per batch: every match of a batch shares the map).
-void launch_decimate(lgs_ctx* ctx, const double* coarse, const RtcsmPlan& pl, hipStream_t st)
-{
-    double* D = planes_buffer(ctx, pl);
     dim3 gd((pl.Wq + 255) / 256, pl.Hq, pl.low_res * pl.low_res);
     hipLaunchKernelGGL(k_decimate, gd, dim3(256), 0, st, coarse, pl.W, pl.H, pl.low_res, pl.Wq, pl.M, pl.Wqp,
                        pl.pstride, D);
     LGS_HIP_CHECK(hipGetLastError());
-    planes_written(ctx, pl, st);
 }
 
-// Coarse stage: one lane per coarse block; with phase planes the coarse map
-// is already in w.decim (launch_decimate or the planes precompute).
-void launch_coarse(lgs_ctx* ctx, const RtcsmPlan& pl, const Workspace& w, const double* coarse,
-                   int gen, hipStream_t st)
-{
-    const int cb = coarse_block(pl);
-    dim3 g((pl.P + cb - 1) / cb, pl.T);
-    if (ctx->coarse_planes) {
-        const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1>), g, dim3(cb), 0, st, pl, w.decim, w.idx, w.cbase,
-                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
-        ctx->timing_end(tok);
-    } else {
-        LGS_REQUIRE(coarse, "plain coarse map missing");
-        const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<0>), g, dim3(cb), 0, st, pl, coarse, w.idx, w.cbase,
-                           w.zero, w.tedge, gen, w.cscore, w.cflag, w.part_c, w.part_k);
-        ctx->timing_end(tok);
-    }
-    LGS_HIP_CHECK(hipGetLastError());
-}
-
-// Superblock-pruned coarse stage: k_super (bounds) -> k_seed_super (L) ->
-// k_coarse<1, 1> (superblock-major lanes, pruned blocks skipped).
-void launch_coarse_super(lgs_ctx* ctx, const RtcsmPlan& pl, const Workspace& w, const double* grid,
-                         RtcsmRecord* rec, int gen, hipStream_t st)
-{
-    const int nsb2 = pl.nsbx * pl.nsby;
-    const bool pair = nsb2 <= 32;
-    const int chunks = pair ? 1 : (nsb2 + 63) / 64;
-    {
-        const int tok = ctx->timing_begin(K_SUPER, 8.0 * (double)pl.T * nsb2 * pl.Nv);
-        const size_t lds = sizeof(int) * (size_t)std::max(pl.Nv, 1);
-        if (ctx->skipped(K_SUPER)) {
-        } else if (pair)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<1>), dim3(chunks, pl.T), dim3(64 * kSupWaves), lds, st, pl,
-                               w.super, w.cbase, w.zero, w.tedge, gen, w.negflag, ctx->planes_gen, w.sbound,
-                               w.part_c, w.part_k);
-        else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<0>), dim3(chunks, pl.T), dim3(64 * kSupWaves), lds, st, pl,
-                               w.super, w.cbase, w.zero, w.tedge, gen, w.negflag, ctx->planes_gen, w.sbound,
-                               w.part_c, w.part_k);
-        ctx->timing_end(tok);
-        LGS_HIP_CHECK(hipGetLastError());
-    }
-    {
-        const int tok = ctx->timing_begin(K_SEED, 8.0 * kSeedCands * (pl.low_res * pl.low_res + 16.0) * pl.Nv);
-        const size_t lds = sizeof(int2) * (size_t)std::max(pl.Nv, 1);
-        if (!ctx->skipped(K_SEED))
-            hipLaunchKernelGGL(k_seed_super, dim3(kSeedCands), dim3(1024), lds, st, pl, grid, w.idx, w.zero, w.decim,
-                               w.cbase, w.part_c, w.part_k, chunks * pl.T, w.Lc, rec);
-        ctx->timing_end(tok);
-        LGS_HIP_CHECK(hipGetLastError());
-    }
-    const int tok = ctx->timing_begin(K_COARSE, 8.0 * (double)pl.K * pl.Nv);
-    if (tok >= 0) {
-        ctx->pending[tok].dev_rec = rec;
-        ctx->pending[tok].bytes_per_eval = 8.0 * pl.Nv;
-    }
-    const size_t lds = ((sizeof(int) * (size_t)pl.Nv + 15) & ~(size_t)15) + sizeof(double) * 128 * kRing * kRowWaves;
-    if (!ctx->skipped(K_COARSE))
-        hipLaunchKernelGGL(k_coarse_rows, dim3(pl.T, kSB, kRowSplit), dim3(64 * kRowWaves), lds, st, pl, w.decim, w.idx, w.cbase,
-                           w.zero, w.tedge, gen, w.sbound, w.Lc, w.Lp, w.cscore, w.cflag, rec);
-    ctx->timing_end(tok);
-    LGS_HIP_CHECK(hipGetLastError());
-}
-
-// Block evaluation dispatch: transposed multi-wave kernels for the window
-// size the launcher JSON uses (LowRes 5; its LDS need stays < 64 KB), the
-// generic one-wave kernels otherwise.
-template <int LR>
-void launch_seed_t(const RtcsmPlan& pl, const double* grid, const Workspace& w, int dense, hipStream_t st)
-{
-    hipLaunchKernelGGL(k_seed<LR>, dim3(1), dim3(64 * LR), eval_t_smem<LR>(pl.Nv), st, pl, grid, w.idx,
-                       w.zero, w.part_c, w.part_k, w.nparts, w.Lp, dense);
-}
-void launch_seed(const RtcsmPlan& pl, const double* grid, const Workspace& w, int dense, hipStream_t st)
-{
-    switch (pl.Nv <= 64 * kMaxChunks ? pl.low_res : 0) {
-    case 5: launch_seed_t<5>(pl, grid, w, dense, st); break;
-    default:
-        hipLaunchKernelGGL(k_seed<0>, dim3(1), dim3(64), sidx_bytes(pl), st, pl, grid, w.idx, w.zero,
-                           w.part_c, w.part_k, w.nparts, w.Lp, dense);
-    }
-    LGS_HIP_CHECK(hipGetLastError());
-}
-// k_fine's grid: one workgroup per CU, looping over the selected blocks (the
-// count is known only on the device; idle workgroups still hold wave slots)
-constexpr int kFineGrid = 1024;
+// k_fine's grid per item: single-wave workgroups looping over the item's
+// selected (block, row) items (the count is known only on the device; idle
+// workgroups still hold wave slots, so the per-item grid shrinks with the batch)
+inline int fine_grid(int n) { return std::max(64, std::min(1024, 8192 / std::max(n, 1))); }
 // dynamic LDS: the evaluator's buffers, then the segment prefix (nseg + 1 ints)
-inline size_t pref_bytes(const Workspace& w) { return sizeof(int) * (size_t)(w.nseg + 1); }
-
-template <int LR>
-void launch_fine_t(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
-{
-    // one wave's share of the evaluator's LDS (row split)
-    const size_t e = (sizeof(int2) * (size_t)((pl.Nv + 1) & ~1) + sizeof(double) * 2 * LR * 65 + 15) & ~size_t(15);
-    hipLaunchKernelGGL(k_fine<LR>, dim3(kFineGrid), dim3(64), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
-                       w.list, w.segcnt, w.nseg, (unsigned)e, w.fval, w.fpos);
-}
-void launch_fine(const RtcsmPlan& pl, const double* grid, const Workspace& w, hipStream_t st)
-{
-    switch (pl.Nv <= 64 * kMaxChunks ? pl.low_res : 0) {
-    case 5: launch_fine_t<5>(pl, grid, w, st); break;
-    default: {
-        const size_t e = (sidx_bytes(pl) + 15) & ~size_t(15);
-        hipLaunchKernelGGL(k_fine<0>, dim3(kFineGrid), dim3(64), e + pref_bytes(w), st, pl, grid, w.idx, w.zero,
-                           w.list, w.segcnt, w.nseg, (unsigned)e, w.fval, w.fpos);
-    }
-    }
-    LGS_HIP_CHECK(hipGetLastError());
-}
+inline size_t pref_bytes(int nseg) { return sizeof(int) * (size_t)(nseg + 1); }
 
 struct ScanOptions {
     bool dense = false;
@@ -1992,98 +2168,137 @@ struct ScanOptions {
     const std::vector<int4>* cost_patches = nullptr;
 };
 
-// superblock pruning applies (else k_coarse scores every block)
-inline bool uses_super(const lgs_ctx* ctx, const RtcsmPlan& pl, const ScanOptions& opt)
+// Enqueue the whole device pipeline of a batch of matches on ctx->stream: one
+// launch per stage for all items (d_items: the uploaded descriptors).
+// Options (reruns) apply to single-item batches only.
+void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::vector<MatchItem>& items,
+                   const ScanOptions& opt)
 {
-    // k_coarse_rows: one ballot over an angle's superblocks, Nv <= 2048
-    return !(opt.dense || ctx->force_dense) && ctx->coarse_planes && ctx->super_prune && ctx->super_fresh &&
-           pl.Nv <= kSeedMaxNv && pl.nsbx * pl.nsby <= 64;
-}
-
-// Enqueue the whole device pipeline of one match on ctx->stream; returns the
-// generation that tags this match's guard counters in *d_rec.
-int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
-                  const lgs_cost_ge_params* cost, lgs_scan* scan, const RtcsmPlan& pl,
-                  RtcsmRecord* d_rec, const ScanOptions& opt)
-{
-    Workspace w = ensure_workspace(ctx, pl, scan->n);
     hipStream_t st = ctx->stream;
-    const int gen = ctx->generation = ctx->next_stamp();
+    const int n = B.n;
     const int inject = ctx->inject_index ? 1 : 0;
-    if (pl.Nv == 0)   // no beam: the look-ahead padding alone is read
-        LGS_HIP_CHECK(hipMemsetAsync(w.cbase, 0, sizeof(int) * (size_t)(pl.sb_off + kPad), st));
-    if (pl.Nv > 0) {
-        if (opt.host_idx) {
-            LGS_HIP_CHECK(hipMemcpyAsync(w.idx, opt.host_idx->data(), sizeof(int2) * opt.host_idx->size(),
+    const double* zero = ctx->zero;
+    double beams_T = 0.0, beams_K = 0.0;   // sum over items of T*Nv, K*Nv (algorithmic bytes)
+    for (auto& it : items) {
+        beams_T += (double)it.pl.T * it.pl.Nv;
+        beams_K += (double)it.pl.K * it.pl.Nv;
+    }
+    if (opt.host_idx) {
+        // single item: the full host projection replaces k_project
+        const MatchItem& it = items[0];
+        LGS_HIP_CHECK(hipMemcpyAsync(it.idx, opt.host_idx->data(), sizeof(int2) * opt.host_idx->size(),
+                                     hipMemcpyHostToDevice, st));
+        const size_t m = std::max<size_t>((size_t)it.pl.T * it.pl.Nv, kPad);
+        hipLaunchKernelGGL(k_cinfo, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, d_items);
+        LGS_HIP_CHECK(hipGetLastError());
+    } else {
+        dim3 g(std::max(1, (B.NvMax + 255) / 256), (B.Tmax + kProjRows - 1) / kProjRows, n);
+        const int tok_ = ctx->timing_begin(K_PROJECT, 24.0 * beams_T);
+        if (!ctx->skipped(K_PROJECT))
+            hipLaunchKernelGGL(k_project, g, dim3(256), 0, st, d_items, ctx->guard_cap, ctx->guard_eps, inject);
+        ctx->timing_end(tok_);
+        LGS_HIP_CHECK(hipGetLastError());
+        if (opt.patches && !opt.patches->empty()) {
+            int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * opt.patches->size());
+            LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.patches->data(), sizeof(int4) * opt.patches->size(),
                                          hipMemcpyHostToDevice, st));
-            const size_t n = (size_t)pl.T * pl.Nv;
-            hipLaunchKernelGGL(k_cinfo, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pl, w.idx,
-                               w.cbase, w.tedge, gen);
+            const int np = (int)opt.patches->size();
+            hipLaunchKernelGGL(k_patch, dim3((np + 255) / 256), dim3(256), 0, st, d_items, dp, np);
             LGS_HIP_CHECK(hipGetLastError());
-        } else {
-            dim3 g((pl.Nv + 255) / 256, (pl.T + kProjRows - 1) / kProjRows);
-            {
-                const int tok_ = ctx->timing_begin(K_PROJECT, 24.0 * (double)pl.T * pl.Nv);
-                if (!ctx->skipped(K_PROJECT))
-                    hipLaunchKernelGGL(k_project, g, dim3(256), 0, st, pl, scan->d_ranges, scan->d_angles,
-                                   w.idx, w.cbase, w.tedge, gen, d_rec,
-                                   ctx->guard_cap, ctx->guard_eps, inject);
-                ctx->timing_end(tok_);
-            }
-            LGS_HIP_CHECK(hipGetLastError());
-            if (opt.patches && !opt.patches->empty()) {
-                int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * opt.patches->size());
-                LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.patches->data(), sizeof(int4) * opt.patches->size(),
-                                             hipMemcpyHostToDevice, st));
-                const int np = (int)opt.patches->size();
-                hipLaunchKernelGGL(k_patch, dim3((np + 255) / 256), dim3(256), 0, st, pl, w.idx, w.cbase,
-                                   w.tedge, gen, dp, np);
-                LGS_HIP_CHECK(hipGetLastError());
-            }
         }
     }
     const bool dense = opt.dense || ctx->force_dense;
-    const bool pruned = uses_super(ctx, pl, opt);
-    if (pruned) {
-        launch_coarse_super(ctx, pl, w, grid->d, d_rec, gen, st);
+    if (B.pruned) {
+        {
+            const int tok = ctx->timing_begin(K_SUPER, 8.0 * B.nsb2 * beams_T);
+            const size_t lds = sizeof(int) * (size_t)std::max(B.NvMax, 1);
+            dim3 g(B.chunks, B.Tmax, n);
+            if (ctx->skipped(K_SUPER)) {
+            } else if (B.pair)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<1>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<0>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+            ctx->timing_end(tok);
+            LGS_HIP_CHECK(hipGetLastError());
+        }
+        {
+            const int tok = ctx->timing_begin(K_SEED, 8.0 * kSeedCands * (B.low_res * B.low_res + 16.0) * B.NvMax * n);
+            const size_t lds = sizeof(int2) * (size_t)std::max(B.NvMax, 1);
+            if (!ctx->skipped(K_SEED))
+                hipLaunchKernelGGL(k_seed_super, dim3(kSeedCands, n), dim3(1024), lds, st, d_items, zero);
+            ctx->timing_end(tok);
+            LGS_HIP_CHECK(hipGetLastError());
+        }
+        const int tok = ctx->timing_begin(K_COARSE, 8.0 * beams_K);
+        if (tok >= 0) ctx->pending[tok].coarse_evals = true;   // algorithmic bytes from the records
+        const size_t lds = ((sizeof(int) * (size_t)B.NvMax + 15) & ~(size_t)15) +
+                           sizeof(double) * 128 * kRing * kRowWaves;
+        if (!ctx->skipped(K_COARSE))
+            hipLaunchKernelGGL(k_coarse_rows, dim3(B.Tmax, kSB, kRowSplit * n), dim3(64 * kRowWaves), lds, st,
+                               d_items, zero);
+        ctx->timing_end(tok);
+        LGS_HIP_CHECK(hipGetLastError());
     } else {
-        launch_coarse(ctx, pl, w, coarse->d, gen, st);
-        const int tok_ = ctx->timing_begin(K_SEED, 8.0 * pl.low_res * pl.low_res * (double)pl.Nv);
-        launch_seed(pl, grid->d, w, dense ? 1 : 0, st);
-        ctx->timing_end(tok_);
+        {
+            dim3 g((B.P + B.cb - 1) / B.cb, B.Tmax, n);
+            const int tok = ctx->timing_begin(K_COARSE, 8.0 * beams_K);
+            if (B.planes)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1>), g, dim3(B.cb), 0, st, d_items, zero);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<0>), g, dim3(B.cb), 0, st, d_items, zero);
+            ctx->timing_end(tok);
+            LGS_HIP_CHECK(hipGetLastError());
+        }
+        const int tok = ctx->timing_begin(K_SEED, 8.0 * B.low_res * B.low_res * (double)B.NvMax * n);
+        if (B.lr5)
+            hipLaunchKernelGGL(k_seed<5>, dim3(1, n), dim3(64 * 5), eval_t_smem<5>(B.NvMax), st, d_items, zero,
+                               dense ? 1 : 0);
+        else
+            hipLaunchKernelGGL(k_seed<0>, dim3(1, n), dim3(64), sidx_bytes(B.NvMax), st, d_items, zero,
+                               dense ? 1 : 0);
+        ctx->timing_end(tok);
+        LGS_HIP_CHECK(hipGetLastError());
     }
-    LGS_HIP_CHECK(hipGetLastError());
     {
-        const int tok_ = ctx->timing_begin(K_SELECT, 10.0 * (double)pl.K);
+        const int tok_ = ctx->timing_begin(K_SELECT, 10.0 * (double)B.Tmax * B.P * n);
         if (!ctx->skipped(K_SELECT))
-            hipLaunchKernelGGL(k_select, dim3((unsigned)w.nseg), dim3(kSelSeg), 0, st, pl, w.cscore, w.cflag,
-                           w.Lp, pruned ? w.sbound : nullptr, w.tedge, gen, w.list, w.segcnt);
+            hipLaunchKernelGGL(k_select, dim3((unsigned)B.nsegMax, n), dim3(kSelSeg), 0, st, d_items,
+                               B.pruned ? 1 : 0);
         ctx->timing_end(tok_);
+        LGS_HIP_CHECK(hipGetLastError());
     }
-    LGS_HIP_CHECK(hipGetLastError());
     {
         const int tok_ = ctx->timing_begin(K_FINE, 0.0);
-        if (!ctx->skipped(K_FINE)) launch_fine(pl, grid->d, w, st);
+        dim3 g(fine_grid(n), n);
+        if (ctx->skipped(K_FINE)) {
+        } else if (B.lr5) {
+            // one wave's share of the evaluator's LDS (row split)
+            const size_t e = (sizeof(int2) * (size_t)((B.NvMax + 1) & ~1) + sizeof(double) * 2 * 5 * 65 + 15) &
+                             ~size_t(15);
+            hipLaunchKernelGGL(k_fine<5>, g, dim3(64), e + pref_bytes(B.nsegMax), st, d_items, zero, (unsigned)e);
+        } else {
+            const size_t e = (sidx_bytes(B.NvMax) + 15) & ~size_t(15);
+            hipLaunchKernelGGL(k_fine<0>, g, dim3(64), e + pref_bytes(B.nsegMax), st, d_items, zero, (unsigned)e);
+        }
         ctx->timing_end(tok_);
+        LGS_HIP_CHECK(hipGetLastError());
     }
-    LGS_HIP_CHECK(hipGetLastError());
     {
         const int tok_ = ctx->timing_begin(K_REPLAY, 0.0);
         if (!ctx->skipped(K_REPLAY))
-            hipLaunchKernelGGL(k_replay, dim3(1), dim3(64), pref_bytes(w), st, pl, w.cscore, w.cflag, w.list,
-                           w.segcnt, w.nseg, w.fval, w.fpos, w.frows, w.Lp, d_rec, w.poses7);
+            hipLaunchKernelGGL(k_replay, dim3(n), dim3(64), pref_bytes(B.nsegMax), st, d_items);
         ctx->timing_end(tok_);
+        LGS_HIP_CHECK(hipGetLastError());
     }
-    LGS_HIP_CHECK(hipGetLastError());
     // cost + covariance terms at the 7 poses
-    CostPlan cp = make_cost_plan(grid, cost, scan);
-    const double kk = (2.0 * cost->kernel_size + 1) * (2.0 * cost->kernel_size + 1);
+    const double kk = (2.0 * B.kernel_size + 1) * (2.0 * B.kernel_size + 1);
+    double nbeams = 0.0;
+    for (auto& it : items) nbeams += it.cp.N;
     {
-        const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * (double)scan->n);
+        const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * nbeams);
         if (!ctx->skipped(K_COST))
-            hipLaunchKernelGGL(KCOST(cp), dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
-                               scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
-                               ctx->guard_eps, inject, 0, gen);
+            hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, n), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
+                               ctx->guard_eps, inject, 0);
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
     }
@@ -2093,14 +2308,12 @@ int enqueue_match(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
         int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * opt.cost_patches->size());
         LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.cost_patches->data(), sizeof(int4) * opt.cost_patches->size(),
                                      hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, st, w.cidx, dp, np);
+        hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, st, items[0].cidx, dp, np);
         LGS_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(KCOST(cp), dim3(7), dim3(kCostThreads), 0, st, cp, grid->d, scan->d_ranges,
-                           scan->d_angles, w.poses7, w.cidx, w.terms, d_rec, ctx->guard_cap,
-                           ctx->guard_eps, 0, 1, gen);
+        hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, 1), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
+                           ctx->guard_eps, 0, 1);
         LGS_HIP_CHECK(hipGetLastError());
     }
-    return gen;
 }
 
 // Host view of a device record: the generation-tagged guard words decoded.
@@ -2264,13 +2477,9 @@ void finish_summary(const RtcsmPlan& pl, const lgs_scan* scan, lgs_pose2d initia
     out->fine_blocks = rec.n_eval;
 }
 
-void check_args(const lgs_grid* grid, const lgs_grid* coarse, const lgs_rtcsm_params* p,
-                const lgs_cost_ge_params* c, const lgs_scan* s)
+void check_args(const lgs_grid* grid, const lgs_rtcsm_params* p, const lgs_cost_ge_params* c, const lgs_scan* s)
 {
-    LGS_REQUIRE(grid && coarse && p && c && s, "null argument");
-    LGS_REQUIRE(grid->w == coarse->w && grid->h == coarse->h && grid->min_x == coarse->min_x &&
-                    grid->min_y == coarse->min_y && grid->res == coarse->res,
-                "coarse map must have the fine map's geometry (CreateSameSizeMap)");
+    LGS_REQUIRE(grid && p && c && s, "null argument");
     LGS_REQUIRE(p->low_resolution >= 1 && p->low_resolution <= 32, "low_resolution must be in [1, 32]");
     LGS_REQUIRE(p->range_x >= 0 && p->range_y >= 0 && p->range_theta >= 0, "negative search range");
     LGS_REQUIRE(s->n >= 1, "empty scan");
@@ -2278,46 +2487,103 @@ void check_args(const lgs_grid* grid, const lgs_grid* coarse, const lgs_rtcsm_pa
     LGS_REQUIRE(c->kernel_size >= 0, "negative kernel size");
 }
 
-// Run n matches against one grid with one host synchronisation in the common
-// case; guarded projections / dangerous blocks trigger exact per-scan reruns.
-void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
-               const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
-               lgs_scan* const* scans, const lgs_pose2d* init, int n, double nthr,
-               lgs_rtcsm_summary* out, bool coarse_in_planes = false)
+void check_coarse(const lgs_grid* grid, const lgs_grid* coarse)
+{
+    LGS_REQUIRE(coarse, "null coarse map");
+    LGS_REQUIRE(grid->w == coarse->w && grid->h == coarse->h && grid->min_x == coarse->min_x &&
+                    grid->min_y == coarse->min_y && grid->res == coarse->res,
+                "coarse map must have the fine map's geometry (CreateSameSizeMap)");
+}
+
+// Run n matches as one batch: the items share the search parameters and the
+// map geometry; sets are the distinct coarse maps (set_of[j] = item j's).
+// One host synchronisation in the common case; guarded projections and
+// dangerous blocks trigger exact single-item reruns.
+void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
+                 const lgs_grid* const* grids, lgs_scan* const* scans, const lgs_pose2d* init, int n,
+                 double nthr, std::vector<PlaneSet>& sets, const int* set_of, lgs_rtcsm_summary* out)
 {
     LGS_HIP_CHECK(hipSetDevice(ctx->device));
-    std::vector<RtcsmPlan> plans(n);
-    std::vector<int> gens(n);
+    std::vector<MatchItem> items((size_t)n);
+    BatchShape B;
+    B.n = n;
+    int Nmax = 1;
     for (int j = 0; j < n; ++j) {
-        check_args(grid, coarse, params, cost, scans[j]);
+        check_args(grids[j], params, cost, scans[j]);
+        LGS_REQUIRE(grids[j]->w == grids[0]->w && grids[j]->h == grids[0]->h && grids[j]->res == grids[0]->res,
+                    "the maps of one batch must share their size and resolution");
         int nv = 0;
         scan_valid_indices(ctx, scans[j], params->scan_range_max, &nv);
-        plans[j] = make_plan(grid, params, scans[j], init[j], nthr, nv);
+        MatchItem& it = items[j];
+        std::memset(&it, 0, sizeof(it));
+        it.pl = make_plan(grids[j], params, scans[j], init[j], nthr, nv);
         // the segment prefix of the selection lives in LDS next to the evaluator
-        LGS_REQUIRE(plans[j].K <= 7LL * 1024 * 1024, "search window too large (> 7M coarse blocks)");
+        LGS_REQUIRE(it.pl.K <= 7LL * 1024 * 1024, "search window too large (> 7M coarse blocks)");
+        it.cp = make_cost_plan(grids[j], cost, scans[j]);
+        B.Tmax = std::max(B.Tmax, it.pl.T);
+        B.NvMax = std::max(B.NvMax, nv);
+        Nmax = std::max(Nmax, scans[j]->n);
     }
+    for (auto& s : sets)
+        if (s.coarse) check_coarse(grids[0], s.coarse);
+    const RtcsmPlan& p0 = items[0].pl;
+    B.P = p0.P;
+    B.nsb2 = p0.nsbx * p0.nsby;
+    B.low_res = p0.low_res;
+    B.cb = coarse_block(p0);
+    B.pair = B.nsb2 <= 32;
+    B.chunks = B.pair ? 1 : (B.nsb2 + 63) / 64;
+    B.planes = ctx->coarse_planes;
+    B.pruned = uses_super(ctx, B.NvMax, B.nsb2, false);
+    B.lr5 = lr5_path(B.NvMax, B.low_res);
+    B.frows = B.lr5 ? 5 : 1;
+    B.kernel_size = cost->kernel_size;
+    B.nsegMax = (int)(((long long)B.Tmax * B.P + kSelSeg - 1) / kSelSeg);
+    const ItemLayout L = item_layout(B.Tmax, B.NvMax, B.P, B.nsb2, B.chunks, B.cb, B.frows, Nmax);
+    char* ws = (char*)ctx->ensure(S_BATCH_WS, L.total * (size_t)n);
     RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord) * (size_t)n);
     RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned(sizeof(RtcsmRecord) * (size_t)n);
-    if (ctx->coarse_planes && !coarse_in_planes) launch_decimate(ctx, coarse->d, plans[0], ctx->stream);
-    ScanOptions none;
-    for (int j = 0; j < n; ++j) gens[j] = enqueue_match(ctx, grid, coarse, cost, scans[j], plans[j], d_rec + j, none);
-    LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n,
-                                 hipMemcpyDeviceToHost, ctx->stream));
+    Upload up(ctx);
+    const SetJobs sj = build_sets(ctx, p0, sets, B.pruned, up);
+    std::vector<int> gens((size_t)n);
+    for (int j = 0; j < n; ++j) {
+        MatchItem& it = items[j];
+        bind_workspace(it, ws + L.total * (size_t)j, L, B.frows);
+        it.grid = grids[j]->d;
+        it.ranges = scans[j]->d_ranges;
+        it.angles = scans[j]->d_angles;
+        const PlaneSet& s = sets[set_of[j]];
+        it.cmap = s.cmap;
+        it.super = s.super;
+        it.negflag = s.negflag;
+        it.pgen = s.pgen;
+        it.gen = gens[j] = ctx->generation = ctx->next_stamp();
+        it.rec = d_rec + j;
+        it.nparts = item_nparts(B, it.pl, B.pruned);
+    }
+    const size_t items_off = up.append(items.data(), items.size());
+    up.flush();
+    launch_sets(ctx, p0, sets, sj, up);
+    enqueue_items(ctx, B, up.at<MatchItem>(items_off), items, ScanOptions{});
+    LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n, hipMemcpyDeviceToHost,
+                                 ctx->stream));
     ctx->sync();
     if (ctx->profile) {
+        double coarse_bytes = 0.0;   // pruned k_coarse: 8 B x Nv per block it scored
+        for (int j = 0; j < n; ++j) coarse_bytes += 8.0 * items[j].pl.Nv * (double)h_rec[j].coarse_evals;
         for (auto& pt : ctx->pending)
-            if (pt.dev_rec) {
-                const long long j = (const RtcsmRecord*)pt.dev_rec - d_rec;
-                if (j >= 0 && j < n) pt.algo_bytes = pt.bytes_per_eval * (double)h_rec[j].coarse_evals;
-                pt.dev_rec = nullptr;
+            if (pt.coarse_evals) {
+                pt.algo_bytes = coarse_bytes;
+                pt.coarse_evals = false;
             }
         ctx->harvest();
     }
 
     for (int j = 0; j < n; ++j) {
         HostRecord rec(h_rec[j], gens[j]);
-        int guard_hits = rec.guard_count + rec.cost_guard_count;
+        const int guard_hits = rec.guard_count + rec.cost_guard_count;
         int fixups = 0, slow = 0;
+        bool pruned = B.pruned;
         // exactness loop: at most a few reruns
         ScanOptions opt;
         std::vector<int4> patches, cpatch;
@@ -2326,7 +2592,7 @@ void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
             bool use_hidx = false, full_cost = false;
             bool rerun = false;
             if (!opt.host_idx && !opt.patches &&
-                check_projection_guards(ctx, plans[j], scans[j], rec, patches, hidx, use_hidx)) {
+                check_projection_guards(ctx, items[j].pl, scans[j], rec, patches, hidx, use_hidx)) {
                 if (use_hidx) opt.host_idx = &hidx;
                 else opt.patches = &patches;
                 rerun = true;
@@ -2338,12 +2604,12 @@ void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                 slow = 1;
             }
             if (!rerun && !opt.cost_patches) {
-                CostPlan cp = make_cost_plan(grid, cost, scans[j]);
-                if (check_cost_guards(ctx, plans[j], cp, scans[j], rec, cpatch, full_cost)) {
+                const CostPlan& cp = items[j].cp;
+                if (check_cost_guards(ctx, items[j].pl, cp, scans[j], rec, cpatch, full_cost)) {
                     if (full_cost) {
                         // rebuild every cost cell on the host
                         double P7[7][3];
-                        host_poses7(plans[j], rec.best, P7);
+                        host_poses7(items[j].pl, rec.best, P7);
                         cpatch.clear();
                         for (int pi = 0; pi < 7; ++pi)
                             for (int b = 0; b < cp.N; ++b) {
@@ -2361,54 +2627,54 @@ void run_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                 }
             }
             if (!rerun) break;
-            const int g = enqueue_match(ctx, grid, coarse, cost, scans[j], plans[j], d_rec + j, opt);
-            LGS_HIP_CHECK(hipMemcpyAsync(&h_rec[j], d_rec + j, sizeof(RtcsmRecord),
-                                         hipMemcpyDeviceToHost, ctx->stream));
+            // single-item rerun in the item's own workspace and planes
+            BatchShape B1 = B;
+            B1.n = 1;
+            B1.Tmax = items[j].pl.T;
+            B1.nsegMax = items[j].nseg;
+            B1.pruned = pruned = uses_super(ctx, B.NvMax, B.nsb2, opt.dense);
+            std::vector<MatchItem> one(1, items[j]);
+            one[0].nparts = item_nparts(B1, one[0].pl, B1.pruned);
+            const int g = one[0].gen = ctx->generation = ctx->next_stamp();
+            Upload u1(ctx);
+            const size_t off = u1.append(one.data(), 1);
+            u1.flush();
+            enqueue_items(ctx, B1, u1.at<MatchItem>(off), one, opt);
+            LGS_HIP_CHECK(hipMemcpyAsync(&h_rec[j], d_rec + j, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
+                                         ctx->stream));
             ctx->sync();
+            if (ctx->profile) ctx->harvest();
             rec = HostRecord(h_rec[j], g);
             if (opt.patches || opt.host_idx) rec.guard_count = 0;  // already exact
         }
-        finish_summary(plans[j], scans[j], init[j], uses_super(ctx, plans[j], opt), rec, &out[j]);
+        finish_summary(items[j].pl, scans[j], init[j], pruned, rec, &out[j]);
         out[j].guard_hits = guard_hits;
         out[j].fixups = fixups;
         out[j].slow_path = slow;
     }
 }
 
-// ComputeCoarserMap (:148-153) into the context-owned coarse grid.  With the
-// phase-plane layout (and W, H multiples of LowRes) the precompute writes the
-// planes directly into S_DECIM and *in_planes is set: the returned grid then
-// carries the geometry only (d == nullptr).
-const lgs_grid* coarser_map(lgs_ctx* ctx, const lgs_grid* grid, const lgs_rtcsm_params* params,
-                            bool* in_planes)
+// Batches of at most kMaxBatch items (bounded scratch: ~20 MB per config-2
+// item), each with only the coarse maps its items reference.
+constexpr int kMaxBatch = 64;
+void run_chunked(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
+                 const lgs_grid* const* grids, lgs_scan* const* scans, const lgs_pose2d* init, int n,
+                 double nthr, const std::vector<PlaneSet>& sets_all, const int* set_of, lgs_rtcsm_summary* out)
 {
-    const int low_res = params->low_resolution;
-    LGS_HIP_CHECK(hipSetDevice(ctx->device));
-    lgs_grid* cg = ctx->coarse_scratch;
-    if (!cg) {
-        cg = new lgs_grid();
-        cg->ctx = ctx;
-        cg->device = ctx->device;
-        cg->owned = false;
-        ctx->coarse_scratch = cg;
+    for (int j0 = 0; j0 < n; j0 += kMaxBatch) {
+        const int m = std::min(kMaxBatch, n - j0);
+        std::vector<PlaneSet> sets;
+        std::vector<int> so((size_t)m), remap(sets_all.size(), -1);
+        for (int k = 0; k < m; ++k) {
+            const int s = set_of[j0 + k];
+            if (remap[s] < 0) {
+                remap[s] = (int)sets.size();
+                sets.push_back(sets_all[s]);
+            }
+            so[k] = remap[s];
+        }
+        run_matches(ctx, params, cost, grids + j0, scans + j0, init + j0, m, nthr, sets, so.data(), out + j0);
     }
-    cg->d = (double*)ctx->ensure(S_COARSE_GRID, sizeof(double) * std::max<size_t>(1, (size_t)grid->w * grid->h));
-    cg->w = grid->w;
-    cg->h = grid->h;
-    cg->min_x = grid->min_x;
-    cg->min_y = grid->min_y;
-    cg->res = grid->res;
-    *in_planes = ctx->coarse_planes && precompute_planes_ok(grid, low_res);
-    if (*in_planes) {
-        const RtcsmPlan lp = layout_plan(grid, params);
-        const PlaneGeom pg{ lp.M, lp.Wqp, lp.pstride };
-        launch_precompute(ctx, grid, low_res, planes_buffer(ctx, lp), &pg);
-        planes_written(ctx, lp, ctx->stream);
-        cg->d = nullptr;
-    } else {
-        launch_precompute(ctx, grid, low_res, cg->d, nullptr);
-    }
-    return cg;
 }
 
 }  // namespace
@@ -2418,10 +2684,13 @@ extern "C" int lgs_rtcsm_optimize_pose(lgs_ctx* ctx, const lgs_grid* grid, const
                                        const lgs_cost_ge_params* cost, const lgs_scan* scan,
                                        lgs_pose2d initial, double nthr, lgs_rtcsm_summary* out)
 {
-    if (!ctx || !out) return LGS_ERR_INVALID_ARG;
+    if (!ctx || !out || !grid || !coarse || !scan) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
+        std::vector<PlaneSet> sets(1);
+        sets[0].coarse = coarse;
+        const int set0 = 0;
         lgs_scan* s = const_cast<lgs_scan*>(scan);
-        run_batch(ctx, grid, coarse, params, cost, &s, &initial, 1, nthr, out);
+        run_matches(ctx, params, cost, &grid, &s, &initial, 1, nthr, sets, &set0, out);
     });
 }
 
@@ -2432,11 +2701,15 @@ extern "C" int lgs_rtcsm_optimize_pose_batch(lgs_ctx* ctx, const lgs_grid* grid,
                                              const lgs_pose2d* initial, int n, double nthr,
                                              lgs_rtcsm_summary* out)
 {
-    if (!ctx || !out || !scans || !initial || n < 0) return LGS_ERR_INVALID_ARG;
+    if (!ctx || !out || !scans || !initial || n < 0 || !grid || !coarse) return LGS_ERR_INVALID_ARG;
     if (n == 0) return LGS_OK;
     return guarded(ctx, [&] {
-        run_batch(ctx, grid, coarse, params, cost, const_cast<lgs_scan* const*>(scans), initial, n,
-                  nthr, out);
+        std::vector<PlaneSet> sets(1);
+        sets[0].coarse = coarse;
+        const std::vector<int> set_of((size_t)n, 0);
+        const std::vector<const lgs_grid*> grids((size_t)n, grid);
+        run_chunked(ctx, params, cost, grids.data(), const_cast<lgs_scan* const*>(scans), initial, n, nthr, sets,
+                    set_of.data(), out);
     });
 }
 
@@ -2446,13 +2719,37 @@ extern "C" int lgs_rtcsm_optimize_pose_query(lgs_ctx* ctx, const lgs_grid* grid,
                                              const lgs_scan* scan, lgs_pose2d initial,
                                              lgs_rtcsm_summary* out)
 {
-    if (!ctx || !grid || !params || !out) return LGS_ERR_INVALID_ARG;
+    if (!ctx || !grid || !params || !out || !scan) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
-        LGS_REQUIRE(params->low_resolution >= 1, "low_resolution must be >= 1");
-        bool planes = false;
-        const lgs_grid* cg = coarser_map(ctx, grid, params, &planes);
+        std::vector<PlaneSet> sets(1);
+        sets[0].fine = grid;   // ComputeCoarserMap (:148-153) of the query's own map
+        const int set0 = 0;
         lgs_scan* s = const_cast<lgs_scan*>(scan);
-        run_batch(ctx, grid, cg, params, cost, &s, &initial, 1, DBL_MIN, out, planes);
+        run_matches(ctx, params, cost, &grid, &s, &initial, 1, DBL_MIN, sets, &set0, out);
+    });
+}
+
+extern "C" int lgs_rtcsm_optimize_pose_query_batch(lgs_ctx* ctx, const lgs_grid* const* grids,
+                                                   const lgs_rtcsm_params* params,
+                                                   const lgs_cost_ge_params* cost,
+                                                   const lgs_scan* const* scans,
+                                                   const lgs_pose2d* initial, int n,
+                                                   lgs_rtcsm_summary* out)
+{
+    if (!ctx || !grids || !params || !cost || !scans || !initial || !out || n < 0) return LGS_ERR_INVALID_ARG;
+    if (n == 0) return LGS_OK;
+    return guarded(ctx, [&] {
+        // every query precomputes its own coarse map, as OptimizePose(query)
+        // does (:31-47) -- also when two queries pass the same map
+        std::vector<PlaneSet> sets((size_t)n);
+        std::vector<int> set_of((size_t)n);
+        for (int j = 0; j < n; ++j) {
+            LGS_REQUIRE(grids[j] && scans[j], "null query");
+            sets[j].fine = grids[j];
+            set_of[j] = j;
+        }
+        run_chunked(ctx, params, cost, grids, const_cast<lgs_scan* const*>(scans), initial, n, DBL_MIN, sets,
+                    set_of.data(), out);
     });
 }
 
@@ -2474,27 +2771,48 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
             dims[3] = pl.ncx; dims[4] = pl.ncy; dims[5] = nfx; dims[6] = nfy;
         }
         if (!coarse_scores && !fine_scores) return;
-        Workspace w = ensure_workspace(ctx, pl, s->n);
-        const int gen = ctx->generation = ctx->next_stamp();
+        check_coarse(grid, coarse);
+        const int cb = coarse_block(pl);
+        const ItemLayout L = item_layout(pl.T, nv, pl.P, pl.nsbx * pl.nsby, 1, cb, 1, s->n);
+        char* ws = (char*)ctx->ensure(S_BATCH_WS, L.total);
         RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord));
         LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0, sizeof(RtcsmRecord), ctx->stream));
-        if (nv > 0) {
-            dim3 g((nv + 255) / 256, (pl.T + kProjRows - 1) / kProjRows);
-            hipLaunchKernelGGL(k_project, g, dim3(256), 0, ctx->stream, pl, s->d_ranges, s->d_angles,
-                               w.idx, w.cbase, w.tedge, gen, d_rec, 0, -1.0, 0);
-            LGS_HIP_CHECK(hipGetLastError());
-        }
+        std::vector<PlaneSet> sets(1);
+        sets[0].coarse = coarse;
+        Upload up(ctx);
+        const SetJobs sj = build_sets(ctx, pl, sets, false, up);
+        MatchItem it;
+        std::memset(&it, 0, sizeof(it));
+        it.pl = pl;
+        bind_workspace(it, ws, L, 1);
+        it.grid = grid->d;
+        it.ranges = s->d_ranges;
+        it.angles = s->d_angles;
+        it.cmap = sets[0].cmap;
+        it.gen = ctx->generation = ctx->next_stamp();
+        it.rec = d_rec;
+        const size_t off = up.append(&it, 1);
+        up.flush();
+        launch_sets(ctx, pl, sets, sj, up);
+        Items d_items = up.at<MatchItem>(off);
+        dim3 g(std::max(1, (nv + 255) / 256), (pl.T + kProjRows - 1) / kProjRows, 1);
+        hipLaunchKernelGGL(k_project, g, dim3(256), 0, ctx->stream, d_items, 0, -1.0, 0);
+        LGS_HIP_CHECK(hipGetLastError());
         if (coarse_scores) {
-            if (ctx->coarse_planes) launch_decimate(ctx, coarse->d, pl, ctx->stream);
-            launch_coarse(ctx, pl, w, coarse->d, gen, ctx->stream);
-            LGS_HIP_CHECK(hipMemcpyAsync(coarse_scores, w.cscore, sizeof(double) * (size_t)pl.K,
+            dim3 gc((pl.P + cb - 1) / cb, pl.T, 1);
+            if (ctx->coarse_planes)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1>), gc, dim3(cb), 0, ctx->stream, d_items, ctx->zero);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<0>), gc, dim3(cb), 0, ctx->stream, d_items, ctx->zero);
+            LGS_HIP_CHECK(hipGetLastError());
+            LGS_HIP_CHECK(hipMemcpyAsync(coarse_scores, it.cscore, sizeof(double) * (size_t)pl.K,
                                          hipMemcpyDeviceToHost, ctx->stream));
         }
         if (fine_scores) {
             const size_t nf = (size_t)pl.T * nfx * nfy;
             double* d = (double*)ctx->ensure(S_DENSE_FINE, sizeof(double) * nf);
-            dim3 g((nfx * nfy + 255) / 256, pl.T);
-            hipLaunchKernelGGL(k_fine_dense, g, dim3(256), 0, ctx->stream, pl, grid->d, w.idx, nfx,
+            dim3 gf((nfx * nfy + 255) / 256, pl.T);
+            hipLaunchKernelGGL(k_fine_dense, gf, dim3(256), 0, ctx->stream, pl, grid->d, it.idx, nfx,
                                nfy, d);
             LGS_HIP_CHECK(hipGetLastError());
             LGS_HIP_CHECK(hipMemcpyAsync(fine_scores, d, sizeof(double) * nf, hipMemcpyDeviceToHost,
@@ -2511,18 +2829,28 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
     if (!ctx || !grid || !cost || !scan || !out_cost) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
-        CostPlan cp = make_cost_plan(grid, cost, scan);
-        double* poses = (double*)ctx->ensure(S_POSES7, sizeof(double) * 21);
-        int4* cidx = (int4*)ctx->ensure(S_COST_IDX, sizeof(int4) * 7 * (size_t)scan->n);
-        double* terms = (double*)ctx->ensure(S_COST_TERM, sizeof(double) * 7 * (size_t)scan->n);
+        const CostPlan cp = make_cost_plan(grid, cost, scan);
+        const ItemLayout L = item_layout(1, 1, 1, 1, 1, 64, 1, scan->n);
+        char* ws = (char*)ctx->ensure(S_BATCH_WS, L.total);
         RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord));
         RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned(sizeof(RtcsmRecord));
+        MatchItem it;
+        std::memset(&it, 0, sizeof(it));
+        bind_workspace(it, ws, L, 1);
+        it.cp = cp;
+        it.grid = grid->d;
+        it.ranges = scan->d_ranges;
+        it.angles = scan->d_angles;
+        it.rec = d_rec;
+        const int gen = it.gen = ctx->generation = ctx->next_stamp();
         double hp[3] = { pose.x, pose.y, pose.theta };
-        const int gen = ctx->generation = ctx->next_stamp();
-        LGS_HIP_CHECK(hipMemcpyAsync(poses, hp, sizeof(hp), hipMemcpyHostToDevice, ctx->stream));
-        hipLaunchKernelGGL(KCOST(cp), dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
-                           scan->d_ranges, scan->d_angles, poses, cidx, terms, d_rec, ctx->guard_cap,
-                           ctx->guard_eps, 0, 0, gen);
+        LGS_HIP_CHECK(hipMemcpyAsync(it.poses7, hp, sizeof(hp), hipMemcpyHostToDevice, ctx->stream));
+        Upload up(ctx);
+        const size_t off = up.append(&it, 1);
+        up.flush();
+        Items d_items = up.at<MatchItem>(off);
+        hipLaunchKernelGGL(KCOST(cp.kernel_size), dim3(1, 1), dim3(kCostThreads), 0, ctx->stream, d_items,
+                           ctx->guard_cap, ctx->guard_eps, 0, 0);
         LGS_HIP_CHECK(hipGetLastError());
         LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                      ctx->stream));
@@ -2537,11 +2865,10 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
                 host_cost_cells(cp, scan, hp, b, cells);
                 row[b] = make_int4(cells[0], cells[1], cells[2], cells[3]);
             }
-            LGS_HIP_CHECK(hipMemcpyAsync(cidx, row.data(), sizeof(int4) * row.size(),
+            LGS_HIP_CHECK(hipMemcpyAsync(it.cidx, row.data(), sizeof(int4) * row.size(),
                                          hipMemcpyHostToDevice, ctx->stream));
-            hipLaunchKernelGGL(KCOST(cp), dim3(1), dim3(kCostThreads), 0, ctx->stream, cp, grid->d,
-                               scan->d_ranges, scan->d_angles, poses, cidx, terms, d_rec,
-                               ctx->guard_cap, ctx->guard_eps, 0, 1, gen);
+            hipLaunchKernelGGL(KCOST(cp.kernel_size), dim3(1, 1), dim3(kCostThreads), 0, ctx->stream, d_items,
+                               ctx->guard_cap, ctx->guard_eps, 0, 1);
             LGS_HIP_CHECK(hipGetLastError());
             LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                          ctx->stream));
@@ -2557,6 +2884,8 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
 // with OptimizePose(.., ScoreThreshold) and, when found, the loop edge
 // InverseCompound(localMapNode.Pose(), estimatedPose).  One result per
 // candidate, in candidate order (found == 0 where the reference appends none).
+// Candidates are independent, so the queries whose local maps share a size
+// are matched together in batches (each query's coarse map built once per batch).
 extern "C" int lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* params,
                                      const lgs_cost_ge_params* cost, double score_threshold,
                                      const lgs_loop_query* queries, int num_queries,
@@ -2569,9 +2898,6 @@ extern "C" int lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* param
     return guarded(ctx, [&] {
         LGS_REQUIRE(score_threshold > 0.0 && score_threshold <= 1.0,
                     "score threshold must be in (0, 1] (:21-22)");
-        std::vector<lgs_rtcsm_summary> sums;
-        std::vector<lgs_scan*> scans;
-        std::vector<lgs_pose2d> poses;
         int covered = 0;
         for (int q = 0; q < num_queries; ++q) {
             const lgs_loop_query& Q = queries[q];
@@ -2580,28 +2906,55 @@ extern "C" int lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* param
                             Q.first_candidate + Q.num_candidates <= num_candidates,
                         "loop queries must cover the candidates contiguously and in order");
             covered += Q.num_candidates;
-            if (Q.num_candidates == 0) continue;
-            bool planes = false;
-            const lgs_grid* coarse = Q.coarse ? Q.coarse : coarser_map(ctx, Q.map, params, &planes);
-            const int n = Q.num_candidates;
-            scans.resize(n);
-            poses.resize(n);
-            sums.resize(n);
-            for (int j = 0; j < n; ++j) {
-                const lgs_loop_candidate& c = candidates[Q.first_candidate + j];
-                LGS_REQUIRE(c.scan, "loop candidate without a scan");
-                scans[j] = const_cast<lgs_scan*>(c.scan);
-                poses[j] = c.node_pose;
+            for (int j = 0; j < Q.num_candidates; ++j)
+                LGS_REQUIRE(candidates[Q.first_candidate + j].scan, "loop candidate without a scan");
+        }
+        LGS_REQUIRE(covered == num_candidates, "loop queries must cover every candidate");
+        // group the queries by map geometry (one batch shape per group)
+        std::vector<bool> done((size_t)num_queries, false);
+        for (int q0 = 0; q0 < num_queries; ++q0) {
+            if (done[q0]) continue;
+            const lgs_grid* m0 = queries[q0].map;
+            std::vector<PlaneSet> sets;
+            std::vector<int> set_of, cand;
+            std::vector<const lgs_grid*> grids;
+            std::vector<lgs_scan*> scans;
+            std::vector<lgs_pose2d> poses;
+            for (int q = q0; q < num_queries; ++q) {
+                const lgs_loop_query& Q = queries[q];
+                if (done[q] || Q.map->w != m0->w || Q.map->h != m0->h || Q.map->res != m0->res) continue;
+                done[q] = true;
+                if (Q.num_candidates == 0) continue;
+                PlaneSet ps;
+                if (Q.coarse) ps.coarse = Q.coarse;
+                else ps.fine = Q.map;
+                sets.push_back(ps);
+                for (int j = 0; j < Q.num_candidates; ++j) {
+                    const lgs_loop_candidate& c = candidates[Q.first_candidate + j];
+                    set_of.push_back((int)sets.size() - 1);
+                    cand.push_back(Q.first_candidate + j);
+                    grids.push_back(Q.map);
+                    scans.push_back(const_cast<lgs_scan*>(c.scan));
+                    poses.push_back(c.node_pose);
+                }
             }
-            run_batch(ctx, Q.map, coarse, params, cost, scans.data(), poses.data(), n, score_threshold,
-                      sums.data(), planes);
-            for (int j = 0; j < n; ++j) {
-                lgs_loop_result& r = results[Q.first_candidate + j];
+            if (cand.empty()) continue;
+            std::vector<lgs_rtcsm_summary> sums(cand.size());
+            run_chunked(ctx, params, cost, grids.data(), scans.data(), poses.data(), (int)cand.size(),
+                        score_threshold, sets, set_of.data(), sums.data());
+            for (size_t k = 0; k < cand.size(); ++k) {
+                const int ci = cand[k];
+                int qi = 0;
+                while (!(ci >= queries[qi].first_candidate &&
+                         ci < queries[qi].first_candidate + queries[qi].num_candidates))
+                    ++qi;
+                const lgs_loop_query& Q = queries[qi];
+                lgs_loop_result& r = results[ci];
                 std::memset(&r, 0, sizeof(r));
-                const lgs_rtcsm_summary& s = sums[j];
+                const lgs_rtcsm_summary& s = sums[k];
                 r.found = s.pose_found;
                 r.start_node_index = Q.local_map_node_index;
-                r.end_node_index = candidates[Q.first_candidate + j].node_index;
+                r.end_node_index = candidates[ci].node_index;
                 r.start_node_pose = Q.local_map_node_pose;
                 r.estimated_pose = s.estimated_pose;
                 r.score = s.score_max;
@@ -2610,6 +2963,5 @@ extern "C" int lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* param
                 std::memcpy(r.covariance, s.covariance, sizeof(r.covariance));
             }
         }
-        LGS_REQUIRE(covered == num_candidates, "loop queries must cover every candidate");
     });
 }

@@ -51,6 +51,21 @@ void* lgs_ctx::ensure_pinned(size_t bytes)
     return pinned;
 }
 
+void* lgs_ctx::ensure_pinned_up(size_t bytes)
+{
+    if (pinned_up_bytes >= bytes) return pinned_up;
+    if (pinned_up) {
+        LGS_HIP_CHECK(hipStreamSynchronize(stream));
+        LGS_HIP_CHECK(hipHostFree(pinned_up));
+        pinned_up = nullptr;
+        pinned_up_bytes = 0;
+    }
+    size_t want = bytes + bytes / 4;
+    LGS_HIP_CHECK(hipHostMalloc(&pinned_up, want, hipHostMallocDefault));
+    pinned_up_bytes = want;
+    return pinned_up;
+}
+
 namespace lgs {
 const char* const kKernelNames[K_NUM_KERNELS] = { "k_project", "k_coarse", "k_seed", "k_select",
                                                   "k_fine", "k_replay", "k_cost", "k_precompute",
@@ -139,11 +154,8 @@ void lgs_ctx::release()
     pending.clear();
     for (auto e : event_pool) hipEventDestroy(e);
     event_pool.clear();
-    if (coarse_scratch) {
-        if (coarse_scratch->owned && coarse_scratch->d) hipFree(coarse_scratch->d);
-        delete coarse_scratch;
-        coarse_scratch = nullptr;
-    }
+    if (pinned_up) hipHostFree(pinned_up);
+    pinned_up = nullptr;
     if (stream) hipStreamDestroy(stream);
     stream = nullptr;
 }
@@ -397,9 +409,8 @@ __device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b 
 // pg.Wqp > 0: the output is written directly into the interior of the padded
 // phase-plane layout of k_rtcsm.hip (plane ry*w + rx, row y/w + M, column
 // x/w + M; requires W, H multiples of w).
-__global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restrict__ in,
-                                                          double* __restrict__ out, int W,
-                                                          int H, int w, PlaneGeom pg)
+__device__ __forceinline__ void precompute_tile(const double* __restrict__ in, double* __restrict__ out, int W,
+                                                int H, int w, const PlaneGeom& pg)
 {
     extern __shared__ double lds[];
     const int x0 = blockIdx.x * kTileX, y0 = blockIdx.y * kTileY;
@@ -438,6 +449,22 @@ __global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restri
             out[(size_t)y * W + x] = m;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restrict__ in,
+                                                          double* __restrict__ out, int W,
+                                                          int H, int w, PlaneGeom pg)
+{
+    precompute_tile(in, out, W, H, w, pg);
+}
+
+// Batched: job blockIdx.z (maps of a batch may differ in size; the grid
+// covers the largest, tiles past a job's map exit).
+__global__ __launch_bounds__(256) void k_precompute_jobs(const PrecompJob* __restrict__ jobs, int w)
+{
+    const PrecompJob& j = jobs[blockIdx.z];
+    if ((int)blockIdx.x * kTileX >= j.W || (int)blockIdx.y * kTileY >= j.H) return;
+    precompute_tile(j.in, j.out, j.W, j.H, w, j.pg);
 }
 
 // Fallback for large windows: direct 2-D window per output.
@@ -486,6 +513,20 @@ void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, c
         dim3 grid((in->w + 255) / 256, in->h);
         hipLaunchKernelGGL(k_precompute_direct, grid, dim3(256), 0, ctx->stream, in->d, out,
                            in->w, in->h, win);
+    }
+    ctx->timing_end(tok);
+    LGS_HIP_CHECK(hipGetLastError());
+}
+void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, int maxW, int maxH, int win)
+{
+    LGS_REQUIRE(win >= 1 && win <= kMaxWinTiled, "batched precompute: window must be in [1, 32]");
+    if (njobs == 0 || maxW == 0 || maxH == 0) return;
+    const int tok = ctx->timing_begin(K_PRECOMPUTE, 32.0 * (double)maxW * (double)maxH * njobs);
+    if (!ctx->skipped(K_PRECOMPUTE)) {
+        const int fw = kTileX + win - 1, fh = kTileY + win - 1;
+        const size_t lds = (size_t)(fh * fw + kTileY * fw) * sizeof(double);
+        dim3 grid((maxW + kTileX - 1) / kTileX, (maxH + kTileY - 1) / kTileY, njobs);
+        hipLaunchKernelGGL(k_precompute_jobs, grid, dim3(256), lds, ctx->stream, d_jobs, win);
     }
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());

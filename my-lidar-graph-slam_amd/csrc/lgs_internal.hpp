@@ -65,6 +65,9 @@ enum Slot {
     S_LIN0, S_LIN1,   // K4 staging
     S_SUPER,        // double: superblock planes (forward kSB x kSB max of S_DECIM)
     S_SBOUND,       // double [T * nsb2] superblock bounds
+    S_UPLOAD,       // per-batch descriptors (MatchItem, PlaneJob, PrecompJob), one H2D copy
+    S_BATCH_WS,     // per-item match workspaces of a batch (k_rtcsm.hip ItemLayout)
+    S_NEGFLAG,      // int per coarse-map set: negative-cell stamp of its planes
     S_NUM_SLOTS
 };
 
@@ -132,6 +135,14 @@ struct PlaneGeom {
     long long pstride;
 };
 
+// One coarse-map precompute of a batched launch (k_precompute_jobs).
+struct PrecompJob {
+    const double* in;
+    double* out;
+    int W, H;
+    PlaneGeom pg;   // pg.Wqp > 0: write the padded phase planes
+};
+
 struct CostPlan {
     double min_range, max_range;   // filter (open interval)
     double hit_and_missed_dist, occupancy_threshold;
@@ -164,10 +175,9 @@ struct PendingTiming {
     int kernel;
     hipEvent_t a, b;
     double algo_bytes;
-    // pruned k_coarse: device record whose coarse_evals (x bytes_per_eval)
-    // replaces algo_bytes once the host copy of the record is known
-    const void* dev_rec = nullptr;
-    double bytes_per_eval = 0.0;
+    // pruned k_coarse: algo_bytes is set from the batch's records (blocks
+    // actually scored x 8 B x Nv) once their host copy is known
+    bool coarse_evals = false;
 };
 }  // namespace lgs
 
@@ -182,11 +192,9 @@ struct lgs_ctx {
     int guard_cap = lgs::kGuardInline;
     bool coarse_planes = true;   // phase-plane coarse layout (LGS_OPT_COARSE_PLANES)
     bool super_prune = true;     // superblock pruning of k_coarse (LGS_OPT_SUPER_PRUNE)
-    int planes_gen = 0;          // stamp of the last superblock-plane build (negative-value flag)
     // Stamps come from one process-wide counter: a context's scratch may be
     // memory a destroyed context used, and its stale tags must never match.
     int next_stamp();
-    bool super_fresh = false;    // superblock planes match the current phase planes
     // LGS_OPT_SKIP_MASK (diagnostics only): launches of these kernels are
     // skipped, leaving stale scratch -- results are meaningless; used to
     // measure each stage's share of device throughput
@@ -198,9 +206,11 @@ struct lgs_ctx {
     size_t buf_bytes[lgs::S_NUM_SLOTS] = {};
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
-    lgs_grid* coarse_scratch = nullptr;
-    // padded phase-plane buffer: margins zeroed once per (buffer, layout)
+    void* pinned_up = nullptr;   // staging of the per-batch descriptor upload
+    size_t pinned_up_bytes = 0;
+    // padded phase-plane buffer: margins zeroed once per (buffer, layout, set count)
     void* planes_ptr = nullptr;
+    int planes_sets = 0;
     long long planes_key[4] = { -1, -1, -1, -1 };
     double* zero = nullptr;      // 32 zero doubles: target of out-of-map gathers
     // profiling (LGS_OPT_PROFILE)
@@ -226,6 +236,7 @@ struct lgs_ctx {
 
     void* ensure(int slot, size_t bytes);
     void* ensure_pinned(size_t bytes);
+    void* ensure_pinned_up(size_t bytes);
     void release();
 };
 

@@ -174,6 +174,9 @@ _PROTOS = [
                                           Pose2D, C.c_double, C.POINTER(RtcsmSummary)]),
     ("lgs_rtcsm_optimize_pose_query", C.c_int, [_P, _P, C.POINTER(RtcsmParams), C.POINTER(CostGEParams), _P,
                                                 Pose2D, C.POINTER(RtcsmSummary)]),
+    ("lgs_rtcsm_optimize_pose_query_batch", C.c_int, [_P, C.POINTER(_P), C.POINTER(RtcsmParams),
+                                                      C.POINTER(CostGEParams), C.POINTER(_P), C.POINTER(Pose2D),
+                                                      C.c_int, C.POINTER(RtcsmSummary)]),
     ("lgs_rtcsm_optimize_pose_batch", C.c_int, [_P, _P, _P, C.POINTER(RtcsmParams), C.POINTER(CostGEParams),
                                                 C.POINTER(_P), C.POINTER(Pose2D), C.c_int, C.c_double,
                                                 C.POINTER(RtcsmSummary)]),
@@ -325,6 +328,21 @@ class Context:
                                                     Pose2D(*init), C.byref(out))
         self.check(rc, "rtcsm_optimize_pose_query")
         return out
+
+    def optimize_pose_query_batch(self, grids, params: RtcsmParams, cost: CostGEParams, scans, inits):
+        """n independent OptimizePose(query) calls as one batched pipeline;
+        grids: one map per query (or a single map for all)."""
+        n = len(scans)
+        if not isinstance(grids, (list, tuple)):
+            grids = [grids] * n
+        garr = (_P * n)(*[g.h for g in grids])
+        sarr = (_P * n)(*[s.h for s in scans])
+        poses = (Pose2D * n)(*[Pose2D(*p) for p in inits])
+        out = (RtcsmSummary * n)()
+        rc = self.lib.lgs_rtcsm_optimize_pose_query_batch(self.h, garr, C.byref(params), C.byref(cost), sarr,
+                                                          poses, n, out)
+        self.check(rc, "rtcsm_optimize_pose_query_batch")
+        return list(out)
 
     def optimize_pose_batch(self, grid, coarse, params, cost, scans: Sequence["Scan"], inits, thr: float):
         n = len(scans)

@@ -1,0 +1,149 @@
+"""GPU parity tests for the batched matcher (lgs_rtcsm_optimize_pose_query_batch
+and the batched lgs_rtcsm_optimize_pose_batch / loop paths).
+
+One launch per pipeline stage serves every query of a batch; each query must
+still give exactly what a lone OptimizePose(query) gives (and the oracle):
+bit-exact argmax window, score and pose, cost/covariance within 1e-5.  The
+batches mix scans whose search-angle counts T and valid-beam counts Nv differ
+(the kernels size their grids for the largest and per-item workgroups exit),
+scans with no valid beam at all, different maps per query, and more queries
+than one device batch holds (chunking).
+"""
+import numpy as np
+import pytest
+
+from conftest import launcher_cost
+from lgs_amd import abi, scene
+from test_gpu_rtcsm import assert_same, build_map, oracle_match
+
+pytestmark = pytest.mark.gpu
+
+
+def _queries(world, rng, n, n_beams, jitter=(0.3, 0.3, 0.2)):
+    ang = scene.beam_angles(n_beams)
+    out = []
+    for _ in range(n):
+        true = (rng.uniform(-1, 1), rng.uniform(-1, 1), rng.uniform(-np.pi, np.pi))
+        r = scene.ray_cast(world, true, ang)
+        init = (true[0] + rng.uniform(-jitter[0], jitter[0]), true[1] + rng.uniform(-jitter[1], jitter[1]),
+                true[2] + rng.uniform(-jitter[2], jitter[2]))
+        out.append((r, init))
+    return ang, out
+
+
+@pytest.fixture(scope="module")
+def small_map(world):
+    return build_map(world, 400, 0.05, 100, scene.arc_poses(5), n_beams=541)
+
+
+def test_query_batch_matches_single_and_oracle(ctx, world, small_map):
+    cells, mx, my = small_map
+    rng = np.random.default_rng(7)
+    ang, qs = _queries(world, rng, 10, 541)
+    # vary T (max range -> angular step) and Nv (beams >= ScanRangeMax are dropped)
+    qs[2] = (np.minimum(qs[2][0], 6.0), qs[2][1])
+    qs[5] = (np.where(np.arange(541) % 3 == 0, 25.0, qs[5][0]), qs[5][1])
+    qs[7] = (np.full(541, 25.0), qs[7][1])          # no valid beam at all
+    params = (5, 1.0, 1.0, 0.6, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    scans = [ctx.scan(r, ang) for r, _ in qs]
+    inits = [i for _, i in qs]
+    batch = ctx.optimize_pose_query_batch(g, P, cost, scans, inits)
+    for j, ((r, init), b) in enumerate(zip(qs, batch)):
+        one = ctx.optimize_pose_query(g, P, cost, scans[j], init)
+        assert list(b.best_win) == list(one.best_win), j
+        assert b.score_max == one.score_max, j
+        assert b.estimated_pose.tuple() == one.estimated_pose.tuple(), j
+        assert b.normalized_cost == one.normalized_cost, j
+        assert list(b.covariance) == list(one.covariance), j
+        assert_same(b, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"q{j}")
+
+
+def test_query_batch_distinct_maps(ctx, world):
+    """Each query carries its own map (same size): its own coarse map."""
+    rng = np.random.default_rng(11)
+    maps = [build_map(world, 300, 0.05, 100, scene.arc_poses(k + 2), n_beams=361) for k in range(3)]
+    ang, qs = _queries(world, rng, 6, 361)
+    params = (5, 0.8, 0.8, 0.5, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    grids = [ctx.grid_from_array(c, mx, my, 0.05) for c, mx, my in maps]
+    which = [j % 3 for j in range(6)]
+    scans = [ctx.scan(r, ang) for r, _ in qs]
+    batch = ctx.optimize_pose_query_batch([grids[w] for w in which], P, cost, scans, [i for _, i in qs])
+    for j, ((r, init), b) in enumerate(zip(qs, batch)):
+        c, mx, my = maps[which[j]]
+        assert_same(b, oracle_match(c, mx, my, 0.05, params, r, ang, init), f"q{j}")
+
+
+def test_query_batch_chunked(ctx, world):
+    """More queries than one device batch (kMaxBatch = 64): chunked, same results."""
+    cells, mx, my = build_map(world, 200, 0.05, 100, scene.arc_poses(3), n_beams=181)
+    rng = np.random.default_rng(3)
+    ang, qs = _queries(world, rng, 70, 181, jitter=(0.1, 0.1, 0.1))
+    params = (5, 0.4, 0.4, 0.3, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    scans = [ctx.scan(r, ang) for r, _ in qs]
+    batch = ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])
+    for j in (0, 1, 63, 64, 69):
+        r, init = qs[j]
+        assert_same(batch[j], oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"q{j}")
+
+
+def test_query_batch_fixups_and_dense(ctx, world, small_map):
+    """Guard fix-ups (injected index corruption) and the dense mode inside a batch."""
+    cells, mx, my = small_map
+    rng = np.random.default_rng(5)
+    ang, qs = _queries(world, rng, 4, 541)
+    params = (5, 1.0, 1.0, 0.6, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    scans = [ctx.scan(r, ang) for r, _ in qs]
+    ora = [oracle_match(cells, mx, my, 0.05, params, r, ang, init) for r, init in qs]
+    try:
+        ctx.set_option(abi.LGS_OPT_GUARD_EPS, 0.02)
+        ctx.set_option(abi.LGS_OPT_INJECT_INDEX, 1)
+        for j, b in enumerate(ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])):
+            assert b.fixups == 1, j
+            assert_same(b, ora[j], f"inject q{j}")
+        ctx.set_option(abi.LGS_OPT_INJECT_INDEX, 0)
+        ctx.set_option(abi.LGS_OPT_GUARD_EPS, 1e-9)
+        ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 1)
+        for j, b in enumerate(ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])):
+            assert_same(b, ora[j], f"dense q{j}")
+    finally:
+        ctx.set_option(abi.LGS_OPT_INJECT_INDEX, 0)
+        ctx.set_option(abi.LGS_OPT_GUARD_EPS, 1e-9)
+        ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 0)
+
+
+@pytest.mark.parametrize("planes,prune", [(1, 1), (1, 0), (0, 0)])
+def test_query_batch_layouts(ctx, world, small_map, planes, prune):
+    """Superblock pruning on/off and the plain coarse layout give the same batch."""
+    cells, mx, my = small_map
+    rng = np.random.default_rng(9)
+    ang, qs = _queries(world, rng, 5, 541)
+    params = (5, 1.0, 1.0, 0.6, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    scans = [ctx.scan(r, ang) for r, _ in qs]
+    try:
+        ctx.set_option(abi.LGS_OPT_COARSE_PLANES, planes)
+        ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, prune)
+        batch = ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])
+    finally:
+        ctx.set_option(abi.LGS_OPT_COARSE_PLANES, 1)
+        ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 1)
+    for j, ((r, init), b) in enumerate(zip(qs, batch)):
+        assert_same(b, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"q{j}")
+
+
+def test_query_batch_rejects_mixed_sizes(ctx, world):
+    a = ctx.grid_from_array(np.zeros((100, 100)), -2.5, -2.5, 0.05)
+    b = ctx.grid_from_array(np.zeros((120, 100)), -2.5, -2.5, 0.05)
+    ang = scene.beam_angles(91)
+    sc = ctx.scan(np.full(91, 2.0), ang)
+    with pytest.raises(abi.LgsError):
+        ctx.optimize_pose_query_batch([a, b], abi.RtcsmParams(5, 0.4, 0.4, 0.3, 20.0), launcher_cost(),
+                                      [sc, sc], [(0, 0, 0), (0, 0, 0)])

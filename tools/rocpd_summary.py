@@ -8,6 +8,8 @@ import sys
 
 
 def short(name: str) -> str:
+    if name.startswith("void "):
+        name = name[len("void "):]
     if name.startswith("(anonymous namespace)::"):
         name = name[len("(anonymous namespace)::"):]
     if "rocprim" in name:
