@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--batch", type=int, default=64,
                     help="match workload: queries per call (lgs_rtcsm_optimize_pose_query_batch; 1 = one "
                          "lgs_rtcsm_optimize_pose_query call per scan)")
+    ap.add_argument("--lanes-min-batch", type=int, default=None,
+                    help="A/B: LGS_OPT_LANES_MIN_BATCH (pruned coarse stage kernel choice by batch size)")
+    ap.add_argument("--latency-calls", type=int, default=100,
+                    help="match workload: lone OptimizePose(query) calls timed for p50/p90 (0 = skip, e.g. under "
+                         "rocprofv3 so that the trace holds the batched launches only)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
     ap.add_argument("--timed-events", default="dominant", choices=["dominant", "all", "none"],
                     help="HIP-event timing inside the timed region: the roofline kernel only (default), "
@@ -242,6 +247,8 @@ def run_match(args, D, ctx):
         c.set_option(abi.LGS_OPT_COARSE_PLANES, args.coarse_planes)
         c.set_option(abi.LGS_OPT_SUPER_PRUNE, args.super_prune)
         c.set_option(abi.LGS_OPT_SPIN_SYNC, args.spin_sync)
+        if args.lanes_min_batch is not None:
+            c.set_option(abi.LGS_OPT_LANES_MIN_BATCH, args.lanes_min_batch)
         state.append((c, c.grid_from_array(cells, mx, my, 0.05), [c.scan(r, ang) for r in scans]))
     P, cost = abi.RtcsmParams(*PARAMS), abi.CostGEParams(*COST)
     n = len(scans)
@@ -298,7 +305,7 @@ def run_match(args, D, ctx):
     c0, g0, ds0 = state[0]
     c0.set_option(abi.LGS_OPT_PROFILE_MASK, 0)
     lat1 = []
-    for k in range(min(100, args.steps)):
+    for k in range(args.latency_calls):
         j = (args.warmup + k) % n
         ts = time.perf_counter()
         c0.optimize_pose_query(g0, P, cost, ds0[j], inits[j])
@@ -349,8 +356,8 @@ def run_match(args, D, ctx):
                                 f"per GPU, each issuing batches of {B} OptimizePose(query) matches "
                                 f"(one launch per stage per batch) + RCCL all-gather of poses"),
         # latency of one lone OptimizePose(query) call (what the frontend waits for)
-        p50_scan_match_ms=round(1e3 * float(np.median(lat1)), 4),
-        p90_scan_match_ms=round(1e3 * float(np.percentile(lat1, 90)), 4),
+        p50_scan_match_ms=round(1e3 * float(np.median(lat1)), 4) if lat1 else None,
+        p90_scan_match_ms=round(1e3 * float(np.percentile(lat1, 90)), 4) if lat1 else None,
         # latency of one batched call under the timed load
         p50_batch_call_ms=round(float(np.percentile(lat_ms, 50)), 4),
         roofline=roofline_from(stats, "k_coarse", args.pmc), cpu_baseline=cpu,

@@ -63,7 +63,7 @@ struct MatchItem {
     const double* ranges;
     const double* angles;
     const double* cmap;      // coarse map: padded phase planes (or the plain map)
-    const double* super;     // superblock planes of cmap
+    const float* super;      // superblock planes of cmap (fp32, rounded up)
     const int* negflag;      // stamped with pgen when the planes hold a negative cell
     int pgen;                // build stamp of the planes
     int gen;                 // this match's generation stamp
@@ -91,11 +91,36 @@ struct MatchItem {
 };
 typedef const MatchItem* __restrict__ Items;
 
+// XCD-aware workgroup order (speed only, never correctness).  Blocks b and
+// b + 8 are observed to share an XCD (round-robin dispatch, MI355X_MICROARCH.md
+// §Workgroup dispatch); the bijective remap gives each XCD a contiguous range
+// of logical workgroups, x fastest, then y, then z.  Grids order their
+// dimensions so that an item's (one map's) workgroups are contiguous: they
+// then meet in one XCD's L2 instead of all eight.  Only for kernels whose
+// workgroups carry even work (k_super, k_super_planes, k_project, the
+// precompute): where the work concentrates on few workgroups of an item
+// (k_coarse_rows, k_fine) the remap loads one XCD and idles the rest.
+struct Blk {
+    int x, y, z;
+};
+__device__ __forceinline__ Blk xcd_block()
+{
+#ifdef LGS_NO_XCD
+    return { (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z };
+#endif
+    const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+    const int nwg = gx * gy * gz;
+    const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    return { l % gx, (l / gx) % gy, l / (gx * gy) };
+}
+
 // Per-set superblock-plane job: one coarse map's padded phase planes.
 struct PlaneJob {
     RtcsmPlan pl;            // layout fields (Wqp, Hqp, pstride, pstride4, sub4, Wq4)
     const double* planes;
-    double* super;
+    float* super;
     int* negflag;
     int pgen;
 };
@@ -167,12 +192,20 @@ __device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
 // upload of the compaction), then projects them for kProjRows search angles
 // (fewer, longer waves: the GPU's wave slots, not its ALUs, are what
 // concurrent matches compete for).
-constexpr int kProjRows = 4;
+// cos/sin(th_t + a_i) by rotation: one sincos per beam and one per search
+// angle (shared through LDS) instead of one per (angle, beam).  The rotation
+// differs from glibc's cos/sin of the rounded sum th_t + a_i by a few ulps
+// plus the rounding of that sum (<= 2^-53 |th + a|): with ranges <= 100 m and
+// cells >= 1 mm that is < 1e-11 cells, far inside the 1e-9-cell guard, so
+// every projection whose glibc floor could differ is still guarded and
+// re-checked on the host.
+constexpr int kProjRows = 8;
 __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, double guard_eps, int inject)
 {
-    const MatchItem& it = items[blockIdx.z];
+    const Blk wg = xcd_block();
+    const MatchItem& it = items[wg.z];
     const RtcsmPlan& pl = it.pl;
-    if ((int)blockIdx.y * kProjRows >= pl.T) return;   // past this item's angles (uniform)
+    if (wg.y * kProjRows >= pl.T) return;   // past this item's angles (uniform)
     const double* __restrict__ ranges = it.ranges;
     const double* __restrict__ angles = it.angles;
     int2* __restrict__ idx = it.idx;
@@ -182,8 +215,18 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     RtcsmRecord* rec = it.rec;
     __shared__ int s_map[256];
     __shared__ int s_wsum[4];
+    __shared__ double s_ct[kProjRows], s_st[kProjRows];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int v0 = blockIdx.x * 256;
+    if (tid < kProjRows) {
+        // currentSensorPose.mTheta = sensorPose.mTheta + stepTheta * t (:90-91)
+        const int t = wg.y * kProjRows + tid - pl.win_t;
+        const double th = pl.st + pl.step_t * (double)t;
+        double sn, cs;
+        sincos(th, &sn, &cs);
+        s_ct[tid] = cs;
+        s_st[tid] = sn;
+    }
+    const int v0 = wg.x * 256;
     const int chunk = (pl.N + 255) / 256;
     const int lo = min(tid * chunk, pl.N), hi = min(lo + chunk, pl.N);
     int nvalid = 0;
@@ -207,7 +250,7 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     const int v = v0 + tid;
     // seq_sum's look-ahead reads up to kPad entries past the last row:
     // keep them at the zero margin (base 0)
-    if (blockIdx.x == 0 && blockIdx.y == 0 && tid < kPad) {
+    if (wg.x == 0 && wg.y == 0 && tid < kPad) {
         cbase[(size_t)pl.T * pl.Nv + tid] = 0;
         cbase[pl.sb_off + (size_t)pl.T * pl.Nv + tid] = 0;
     }
@@ -215,14 +258,15 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     const int i = s_map[tid];
     const double r = ranges[i];
     const double a = angles[i];
-    const int tt1 = min(pl.T, (int)(blockIdx.y + 1) * kProjRows);
-    for (int tt = blockIdx.y * kProjRows; tt < tt1; ++tt) {
-    const int t = tt - pl.win_t;
-    // currentSensorPose.mTheta = sensorPose.mTheta + stepTheta * t (:90-91)
-    const double th = pl.st + pl.step_t * (double)t;
-    // HitPoint: cos(sensorPose.mTheta + scanAngle) (H/sensor/sensor_data.hpp:168-172)
-    const double c = cos(th + a);
-    const double s = sin(th + a);
+    double sa, ca;
+    sincos(a, &sa, &ca);
+    const int tt1 = min(pl.T, (wg.y + 1) * kProjRows);
+    for (int tt = wg.y * kProjRows; tt < tt1; ++tt) {
+    // HitPoint: cos(sensorPose.mTheta + scanAngle) (H/sensor/sensor_data.hpp:168-172),
+    // by rotation (see kProjRows)
+    const int kr = tt - wg.y * kProjRows;
+    const double c = s_ct[kr] * ca - s_st[kr] * sa;
+    const double s = s_st[kr] * ca + s_ct[kr] * sa;
     const double hx = pl.sx + r * c;
     const double hy = pl.sy + r * s;
     const double qx = (hx - pl.min_x) / pl.res;
@@ -573,11 +617,12 @@ constexpr int kSPX = 64, kSPY = 32;   // output tile of k_super_planes
 
 __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
 {
-    const PlaneJob& job = jobs[blockIdx.z / nplanes];
-    const int plane = blockIdx.z % nplanes;
+    const Blk wg = xcd_block();
+    const PlaneJob& job = jobs[wg.z / nplanes];
+    const int plane = wg.z % nplanes;
     const RtcsmPlan& pl = job.pl;
     const double* __restrict__ P = job.planes;
-    double* __restrict__ S = job.super;
+    float* __restrict__ S = job.super;
     int* __restrict__ negflag = job.negflag;
     const int pgen = job.pgen;
     const int Wqp = pl.Wqp, Hqp = pl.Hqp;
@@ -585,9 +630,9 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
     constexpr int TW = kSPX + kSB - 1, TH = kSPY + kSB - 1;
     __shared__ double tile[TH][TW];
     __shared__ double hm[TH][kSPX];
-    const int x0 = blockIdx.x * kSPX, y0 = blockIdx.y * kSPY;
+    const int x0 = wg.x * kSPX, y0 = wg.y * kSPY;
     const double* __restrict__ base = P + plane * pstride;
-    double* __restrict__ out = S + plane * pl.pstride4;
+    float* __restrict__ out = S + plane * pl.pstride4;
     const int tid = threadIdx.x;
     bool neg = false;
     for (int k = tid; k < TH * TW; k += blockDim.x) {
@@ -613,7 +658,9 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
         double m = hm[yy][xx];
 #pragma unroll
         for (int j = 1; j < kSB; ++j) m = dmax2(m, hm[yy + j][xx]);
-        out[((y & 3) * 4 + (x & 3)) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + (x >> 2)] = m;
+        // fp32 rounded toward +inf: still >= every member's coarse value, half
+        // the bytes for k_super's gathers
+        out[((y & 3) * 4 + (x & 3)) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + (x >> 2)] = __double2float_ru(m);
     }
     if (neg) *negflag = pgen;
 }
@@ -631,10 +678,12 @@ constexpr int kSupWaves = 4;
 template <int PAIR>
 __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const double* __restrict__ zero)
 {
-    const MatchItem& it = items[blockIdx.z];
+    const Blk wg = xcd_block();
+    const MatchItem& it = items[wg.z];
     const RtcsmPlan& pl = it.pl;
-    if ((int)blockIdx.y >= pl.T) return;   // past this item's angles (uniform)
-    const double* __restrict__ sp = it.super;
+    if (wg.y >= pl.T) return;   // past this item's angles (uniform)
+    const float* __restrict__ sp = it.super;
+    const float* __restrict__ zf = (const float*)zero;
     const int* __restrict__ cbase = it.cbase;
     const int* __restrict__ tedge = it.tedge;
     const int gen = it.gen;
@@ -646,14 +695,14 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
     extern __shared__ int srow[];   // [Nv]
     __shared__ double red[kSupWaves][64];
     constexpr int SPW = PAIR ? 32 : 64;   // superblocks per chunk
-    const int t = blockIdx.y;
+    const int t = wg.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nsb2 = pl.nsbx * pl.nsby;
     const int h = PAIR ? (lane >> 5) : 0;
-    const int sbi = blockIdx.x * SPW + (lane & (SPW - 1));
+    const int sbi = wg.x * SPW + (lane & (SPW - 1));
     const bool act = sbi < nsb2;
     const int a = act ? sbi % pl.nsbx : 0, b = act ? sbi / pl.nsbx : 0;
-    const double* __restrict__ lb = sp + (b * pl.Wq4 + a);
+    const float* __restrict__ lb = sp + (b * pl.Wq4 + a);
     LGS_PROBE_DECL;
     LGS_PROBE_MARK();
     const int* __restrict__ cbrow = cbase + pl.sb_off + (size_t)t * pl.Nv;
@@ -667,11 +716,11 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
     if constexpr (PAIR) {
         const int n2 = (cnt + 1) >> 1;
         s = seq_sum4<int>(n2, [&](int i) { const int v = 2 * i + h; return (v < cnt) ? row[v] : INT_MIN; },
-                          [&](const int& c) { return (act && c != INT_MIN) ? lb + c : zero; });
+                          [&](const int& c) { return (act && c != INT_MIN) ? lb + c : zf; });
         s += __shfl_xor(s, 32, 64);
     } else {
         s = seq_sum4<int>(cnt, [&](int v) { return (v < cnt) ? row[v] : INT_MIN; },
-                          [&](const int& c) { return (act && c != INT_MIN) ? lb + c : zero; });
+                          [&](const int& c) { return (act && c != INT_MIN) ? lb + c : zf; });
     }
     red[w][lane] = s;
     LGS_PROBE_MARK();
@@ -696,7 +745,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
         }
     }
     if (lane == 0) {
-        const int part = t * gridDim.x + blockIdx.x;
+        const int part = t * gridDim.x + wg.x;
         part_c[part] = bv;
         part_k[part] = bk;
     }
@@ -729,10 +778,14 @@ constexpr unsigned waitcnt_imm(unsigned vm, unsigned lgkm)
 }
 __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, const double* __restrict__ zero)
 {
-    const MatchItem& it = items[blockIdx.z / kRowSplit];
-    const int split = blockIdx.z % kRowSplit;   // kept superblocks e = split, split + kRowSplit, ...
+    // plain block order: the kept superblocks concentrate on few angles of
+    // each item, and the XCD remap would put one item's busy workgroups on
+    // one XCD (measured 0.59 -> 0.89 ms for 64 config-2 scans)
+    const Blk wg = { (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z };
+    const MatchItem& it = items[wg.z / kRowSplit];
+    const int split = wg.z % kRowSplit;   // kept superblocks e = split, split + kRowSplit, ...
     const RtcsmPlan& pl = it.pl;
-    if ((int)blockIdx.x >= pl.T) return;   // past this item's angles (uniform)
+    if (wg.x >= pl.T) return;   // past this item's angles (uniform)
     const double* __restrict__ cmap = it.cmap;
     const int2* __restrict__ idx = it.idx;
     const int* __restrict__ cbase = it.cbase;
@@ -747,7 +800,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, con
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int s_sb[64];
     __shared__ int s_cnt;
-    const int t = blockIdx.x, pr = blockIdx.y;
+    const int t = wg.x, pr = wg.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nsb2 = pl.nsbx * pl.nsby;
     const int Nv = pl.Nv;
@@ -880,6 +933,89 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, con
                0.01 * (double)(lgs_probe_t[4] - lgs_probe_t[3]), 0.01 * (double)(lgs_probe_t[5] - lgs_probe_t[4]),
                0.01 * (double)(lgs_probe_t[6] - lgs_probe_t[5]));
 #endif
+}
+
+// k_coarse_lanes (superblock pruning, batched launches): the same scores as
+// k_coarse_rows with one LANE per coarse block: workgroup (angle t, item) of
+// 4 waves, wave w takes kept superblocks 4w .. 4w + 3 (+16, ...), lane =
+// (superblock, member block), and every lane walks the beams in order with
+// pipelined gathers (seq_sum: the reference's sequential fp64 sum, no LDS).
+// A wave then carries 64 blocks' add chains at once instead of k_coarse_rows'
+// 4 adder lanes, which is what a batch of many scans needs (k_coarse_rows
+// keeps the lower latency for a lone scan).
+constexpr int kLaneWaves = 4;
+__global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, const double* __restrict__ zero)
+{
+    const MatchItem& it = items[blockIdx.y];
+    const RtcsmPlan& pl = it.pl;
+    const int t = blockIdx.x;
+    if (t >= pl.T) return;   // past this item's angles (uniform)
+    const double* __restrict__ cmap = it.cmap;
+    const int2* __restrict__ idx = it.idx;
+    const int* __restrict__ cb = it.cbase + (size_t)t * pl.Nv;
+    const int gen = it.gen;
+    __shared__ int s_sb[64];
+    __shared__ int s_cnt;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nsb2 = pl.nsbx * pl.nsby;
+    double L = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < kSeedCands; ++b) L = fmax(L, it.Lc[b]);
+    if (t == 0 && tid == 0) *it.Lp = L;
+    const bool te = it.tedge[t] == gen;
+    // kept superblocks of this angle (nsb2 <= 64 on this path), in key order
+    if (w == 0) {
+        bool kp = false;
+        if (lane < nsb2) {
+            const double bnd = it.sbound[(size_t)t * nsb2 + lane];
+            kp = (bnd > pl.thr) && (te || bnd >= L);
+        }
+        const unsigned long long bal = __ballot(kp);
+        if (kp) s_sb[__popcll(bal & ((1ull << lane) - 1ull))] = lane;
+        if (lane == 0) {
+            s_cnt = __popcll(bal);
+            unsigned long long nb = 0;
+            for (unsigned long long mm = bal; mm; mm &= mm - 1) {
+                const int sb = __ffsll((long long)mm) - 1;
+                const int a = sb % pl.nsbx, b = sb / pl.nsbx;
+                nb += (unsigned long long)(min(kSB, pl.ncx - kSB * a) * min(kSB, pl.ncy - kSB * b));
+            }
+            if (nb) atomicAdd(&it.rec->coarse_evals, nb);
+        }
+    }
+    __syncthreads();
+    const int cnt = s_cnt;
+    for (int e0 = 4 * w; e0 < cnt; e0 += 4 * kLaneWaves) {   // wave-uniform
+        const int e = e0 + (lane >> 4), m = lane & 15;
+        const bool has = e < cnt;
+        const int sb = has ? s_sb[e] : 0;
+        const int jx = kSB * (sb % pl.nsbx) + (m & 3), jy = kSB * (sb / pl.nsbx) + (m >> 2);
+        const bool active = has && jx < pl.ncx && jy < pl.ncy;
+        const double* __restrict__ lane_base = cmap + (active ? jy * pl.Wqp + jx : 0);
+        // inactive lanes (partial superblocks, the wave's tail) read the zero cell
+        const double sum = seq_sum<int>(pl.Nv, [&](int v) { return cb[v]; },
+                                        [&](const int& c) { return active ? lane_base + c : zero; });
+        // unsafe: some coarse read left of / below the map while the block's
+        // fine reads can land inside (x, y >= -(lr-1)); rare, so a separate pass
+        bool unsafe = false;
+        if (te && active) {
+            const int2* __restrict__ id = idx + (size_t)t * pl.Nv;
+            const int lr = pl.low_res, lo = -(lr - 1);
+            const int x0 = -pl.win_x + jx * lr, y0 = -pl.win_y + jy * lr;
+            for (int v = 0; v < pl.Nv; ++v) {
+                const int2 q = id[v];
+                if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0) {
+                    const int x = q.x + x0, y = q.y + y0;
+                    unsafe |= (x >= lo) & (x < pl.W) & (y >= lo) & (y < pl.H) & ((x < 0) | (y < 0));
+                }
+            }
+        }
+        if (active) {
+            const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
+            it.cscore[k] = sum;
+            it.cflag[k] = unsafe ? 1 : 0;
+        }
+    }
 }
 
 // Fine scores of one block by one wave: lane q owns pose (xo = q % lr,
@@ -1462,7 +1598,8 @@ __device__ __forceinline__ int seg_of(const int* pref, int nseg, int b)
 template <int LR>
 __global__ __launch_bounds__(64) void k_fine(Items items, const double* __restrict__ zero, unsigned eval_smem)
 {
-    const MatchItem& it_ = items[blockIdx.y];
+    const Blk wg = { (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z };   // (as k_coarse_rows: uneven work)
+    const MatchItem& it_ = items[wg.y];
     const RtcsmPlan& pl = it_.pl;
     const double* __restrict__ grid = it_.grid;
     const int2* __restrict__ idx = it_.idx;
@@ -1482,7 +1619,7 @@ __global__ __launch_bounds__(64) void k_fine(Items items, const double* __restri
     LGS_PROBE_MARK();
     const int n = pref[nseg];
     constexpr int R = LR > 0 ? LR : 1;
-    for (int it = blockIdx.x; it < n * R; it += gridDim.x) {
+    for (int it = wg.x; it < n * R; it += gridDim.x) {
         const int b = it / R;
         const int sg = seg_of(pref, nseg, b);
         const long long k = list[(size_t)sg * kSelSeg + (b - pref[sg])];
@@ -2001,18 +2138,30 @@ inline size_t plane_bytes(const RtcsmPlan& pl)
 }
 inline size_t super_bytes(const RtcsmPlan& pl)
 {
-    return align256(sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
+    return align256(sizeof(float) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
 }
-double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets)
+double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_super)
 {
     const size_t bytes = plane_bytes(pl) * (size_t)nsets;
     double* D = (double*)ctx->ensure(S_DECIM, bytes);
+    // (k_super_planes writes every superblock-plane value; they are zeroed
+    // with the planes only so that no stale value is ever read)
+    const size_t sbytes = super_bytes(pl) * (size_t)nsets;
+    float* S = with_super ? (float*)ctx->ensure(S_SUPER, sbytes) : nullptr;
     const long long key[4] = { pl.low_res, pl.Wq, pl.Hq, pl.M };
-    if (D != ctx->planes_ptr || std::memcmp(key, ctx->planes_key, sizeof(key)) != 0 || nsets > ctx->planes_sets) {
+    if (D != ctx->planes_ptr || std::memcmp(key, ctx->planes_key, sizeof(key)) != 0 || nsets > ctx->planes_sets ||
+        (with_super && (S != ctx->super_ptr || nsets > ctx->super_sets))) {
         LGS_HIP_CHECK(hipMemsetAsync(D, 0, bytes, ctx->stream));
         ctx->planes_ptr = D;
         ctx->planes_sets = nsets;
         std::memcpy(ctx->planes_key, key, sizeof(key));
+        ctx->super_ptr = nullptr;
+        ctx->super_sets = 0;
+        if (with_super) {
+            LGS_HIP_CHECK(hipMemsetAsync(S, 0, sbytes, ctx->stream));
+            ctx->super_ptr = S;
+            ctx->super_sets = nsets;
+        }
     }
     return D;
 }
@@ -2022,7 +2171,7 @@ struct PlaneSet {
     const lgs_grid* fine = nullptr;     // precompute from this fine map (OptimizePose(query))
     const lgs_grid* coarse = nullptr;   // or decimate this caller-supplied coarse map
     const double* cmap = nullptr;       // what k_coarse / k_seed_super read
-    const double* super = nullptr;
+    const float* super = nullptr;
     const int* negflag = nullptr;
     int pgen = 0;
 };
@@ -2034,6 +2183,7 @@ struct PlaneSet {
 struct SetJobs {
     size_t jobs_off = 0, njobs = 0, pj_off = 0, npj = 0;
 };
+
 void launch_decimate(const double* coarse, const RtcsmPlan& pl, double* D, hipStream_t st);
 SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& sets, bool need_super, Upload& up)
 {
@@ -2059,66 +2209,58 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
         }
         return SetJobs{};
     }
-    double* D = planes_buffer(ctx, lp, ns);
-    const size_t pb = plane_bytes(lp) / sizeof(double);
-    // precompute: straight into the planes when W, H are multiples of LowRes,
-    // else into a plain scratch that is then decimated
+    double* D = planes_buffer(ctx, lp, ns, need_super);
+    float* S = need_super ? (float*)ctx->ensure(S_SUPER, super_bytes(lp) * (size_t)ns) : nullptr;
+    int* neg = need_super ? (int*)ctx->ensure(S_NEGFLAG, sizeof(int) * (size_t)ns) : nullptr;
+    const size_t pb = plane_bytes(lp) / sizeof(double), sbb = super_bytes(lp) / sizeof(float);
+    // fine maps with W, H multiples of LowRes: the precompute writes the
+    // planes directly (one batched launch); other maps go through a plain
+    // scratch map and the phase-plane copy, and supplied coarse maps through
+    // the copy; then the superblock planes of every set (one batched launch).
+    // (A fused planes + superblock-planes pass from the fine map was measured
+    // slower: 1.08-1.19 ms vs 0.40 + 0.56 ms for 64 config-2 maps.)
     std::vector<PrecompJob> jobs;
-    std::vector<int> via_plain;
-    for (int s = 0; s < ns; ++s) {
-        sets[s].cmap = D + pb * (size_t)s;
-        if (!sets[s].fine) continue;
-        if (precompute_planes_ok(sets[s].fine, lr)) {
-            PrecompJob j{};
-            j.in = sets[s].fine->d;
-            j.out = D + pb * (size_t)s;
-            j.W = sets[s].fine->w;
-            j.H = sets[s].fine->h;
-            j.pg = PlaneGeom{ lp.M, lp.Wqp, lp.pstride };
-            jobs.push_back(j);
-        } else {
-            via_plain.push_back(s);
-        }
-    }
-    if (!via_plain.empty()) {
-        const size_t cells = (size_t)lp.W * lp.H;
-        double* plain = (double*)ctx->ensure(S_COARSE_GRID, sizeof(double) * std::max<size_t>(1, cells));
-        for (int s : via_plain) {   // rare (odd map sizes): one set at a time through the shared scratch
-            launch_precompute(ctx, sets[s].fine, lr, plain, nullptr);
-            launch_decimate(plain, lp, D + pb * (size_t)s, st);
-        }
-    }
-    for (int s = 0; s < ns; ++s)
-        if (!sets[s].fine) launch_decimate(sets[s].coarse->d, lp, D + pb * (size_t)s, st);
-    const size_t jobs_off = jobs.empty() ? 0 : up.append(jobs.data(), jobs.size());
-    // superblock planes
     std::vector<PlaneJob> pj;
-    double* S = nullptr;
-    int* neg = nullptr;
-    if (need_super) {
-        S = (double*)ctx->ensure(S_SUPER, super_bytes(lp) * (size_t)ns);
-        neg = (int*)ctx->ensure(S_NEGFLAG, sizeof(int) * (size_t)ns);
-        for (int s = 0; s < ns; ++s) {
-            PlaneJob j{};
-            j.pl = lp;
-            j.planes = D + pb * (size_t)s;
-            j.super = S + super_bytes(lp) / sizeof(double) * (size_t)s;
+    for (int s = 0; s < ns; ++s) {
+        PlaneSet& ps = sets[s];
+        ps.cmap = D + pb * (size_t)s;
+        PlaneJob j{};
+        j.pl = lp;
+        j.planes = D + pb * (size_t)s;
+        if (need_super) {
+            j.super = S + sbb * (size_t)s;
             j.negflag = neg + s;
             j.pgen = ctx->next_stamp();
-            sets[s].super = j.super;
-            sets[s].negflag = j.negflag;
-            sets[s].pgen = j.pgen;
-            pj.push_back(j);
+            ps.super = j.super;
+            ps.negflag = j.negflag;
+            ps.pgen = j.pgen;
         }
+        if (ps.fine && precompute_planes_ok(ps.fine, lr)) {
+            PrecompJob q{};
+            q.in = ps.fine->d;
+            q.out = D + pb * (size_t)s;
+            q.W = ps.fine->w;
+            q.H = ps.fine->h;
+            q.pg = PlaneGeom{ lp.M, lp.Wqp, lp.pstride };
+            jobs.push_back(q);
+        } else if (ps.fine) {
+            // rare (odd map sizes): one set at a time through the shared scratch
+            const size_t cells = (size_t)lp.W * lp.H;
+            double* plain = (double*)ctx->ensure(S_COARSE_GRID, sizeof(double) * std::max<size_t>(1, cells));
+            launch_precompute(ctx, ps.fine, lr, plain, nullptr);
+            launch_decimate(plain, lp, D + pb * (size_t)s, st);
+        } else {
+            launch_decimate(ps.coarse->d, lp, D + pb * (size_t)s, st);
+        }
+        if (need_super) pj.push_back(j);
     }
-    const size_t pj_off = pj.empty() ? 0 : up.append(pj.data(), pj.size());
     // the descriptors of this step go up with the batch's items (one copy):
     // the caller flushes before calling launch_sets
     SetJobs sj;
-    sj.jobs_off = jobs_off;
     sj.njobs = jobs.size();
-    sj.pj_off = pj_off;
+    sj.jobs_off = jobs.empty() ? 0 : up.append(jobs.data(), jobs.size());
     sj.npj = pj.size();
+    sj.pj_off = pj.empty() ? 0 : up.append(pj.data(), pj.size());
     return sj;
 }
 
@@ -2231,11 +2373,15 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         }
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * beams_K);
         if (tok >= 0) ctx->pending[tok].coarse_evals = true;   // algorithmic bytes from the records
-        const size_t lds = ((sizeof(int) * (size_t)B.NvMax + 15) & ~(size_t)15) +
-                           sizeof(double) * 128 * kRing * kRowWaves;
-        if (!ctx->skipped(K_COARSE))
+        if (ctx->skipped(K_COARSE)) {
+        } else if (n >= ctx->lanes_min_batch) {
+            hipLaunchKernelGGL(k_coarse_lanes, dim3(B.Tmax, n), dim3(64 * kLaneWaves), 0, st, d_items, zero);
+        } else {
+            const size_t lds = ((sizeof(int) * (size_t)B.NvMax + 15) & ~(size_t)15) +
+                               sizeof(double) * 128 * kRing * kRowWaves;
             hipLaunchKernelGGL(k_coarse_rows, dim3(B.Tmax, kSB, kRowSplit * n), dim3(64 * kRowWaves), lds, st,
                                d_items, zero);
+        }
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
     } else {

@@ -258,6 +258,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
         return LGS_OK;
     case LGS_OPT_COARSE_PLANES: ctx->coarse_planes = value != 0.0; return LGS_OK;
     case LGS_OPT_SUPER_PRUNE: ctx->super_prune = value != 0.0; return LGS_OK;
+    case LGS_OPT_LANES_MIN_BATCH: ctx->lanes_min_batch = (int)value; return LGS_OK;
     case LGS_OPT_SKIP_MASK: ctx->skip_mask = (unsigned)value; return LGS_OK;
     case LGS_OPT_GUARD_CAP:
         ctx->guard_cap = (int)value;
@@ -410,10 +411,10 @@ __device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b 
 // phase-plane layout of k_rtcsm.hip (plane ry*w + rx, row y/w + M, column
 // x/w + M; requires W, H multiples of w).
 __device__ __forceinline__ void precompute_tile(const double* __restrict__ in, double* __restrict__ out, int W,
-                                                int H, int w, const PlaneGeom& pg)
+                                                int H, int w, const PlaneGeom& pg, int bx, int by)
 {
     extern __shared__ double lds[];
-    const int x0 = blockIdx.x * kTileX, y0 = blockIdx.y * kTileY;
+    const int x0 = bx * kTileX, y0 = by * kTileY;
     const int x1 = min(x0 + kTileX, W), y1 = min(y0 + kTileY, H);
     const int sx0 = win_start(x0, W, w), sy0 = win_start(y0, H, w);
     const int sx1 = win_start(x1 - 1, W, w) + w, sy1 = win_start(y1 - 1, H, w) + w;
@@ -455,16 +456,27 @@ __global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restri
                                                           double* __restrict__ out, int W,
                                                           int H, int w, PlaneGeom pg)
 {
-    precompute_tile(in, out, W, H, w, pg);
+    precompute_tile(in, out, W, H, w, pg, blockIdx.x, blockIdx.y);
 }
 
 // Batched: job blockIdx.z (maps of a batch may differ in size; the grid
 // covers the largest, tiles past a job's map exit).
+// XCD-aware order (speed only): one map's tiles on one XCD (see k_rtcsm.hip xcd_block)
 __global__ __launch_bounds__(256) void k_precompute_jobs(const PrecompJob* __restrict__ jobs, int w)
 {
-    const PrecompJob& j = jobs[blockIdx.z];
-    if ((int)blockIdx.x * kTileX >= j.W || (int)blockIdx.y * kTileY >= j.H) return;
-    precompute_tile(j.in, j.out, j.W, j.H, w, j.pg);
+    const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
+    const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+#ifdef LGS_NO_XCD
+    const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    (void)l;
+#else
+    const int bx = l % gx, by = (l / gx) % gy, bz = l / (gx * gy);
+#endif
+    const PrecompJob& j = jobs[bz];
+    if (bx * kTileX >= j.W || by * kTileY >= j.H) return;
+    precompute_tile(j.in, j.out, j.W, j.H, w, j.pg, bx, by);
 }
 
 // Fallback for large windows: direct 2-D window per output.

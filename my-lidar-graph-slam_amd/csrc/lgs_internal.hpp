@@ -192,6 +192,7 @@ struct lgs_ctx {
     int guard_cap = lgs::kGuardInline;
     bool coarse_planes = true;   // phase-plane coarse layout (LGS_OPT_COARSE_PLANES)
     bool super_prune = true;     // superblock pruning of k_coarse (LGS_OPT_SUPER_PRUNE)
+    int lanes_min_batch = 2;     // pruned coarse stage: k_coarse_lanes from this batch size on (LGS_OPT_LANES_MIN_BATCH)
     // Stamps come from one process-wide counter: a context's scratch may be
     // memory a destroyed context used, and its stale tags must never match.
     int next_stamp();
@@ -211,6 +212,8 @@ struct lgs_ctx {
     // padded phase-plane buffer: margins zeroed once per (buffer, layout, set count)
     void* planes_ptr = nullptr;
     int planes_sets = 0;
+    void* super_ptr = nullptr;   // superblock planes zeroed with them (k_planes_fused leaves far margins)
+    int super_sets = 0;
     long long planes_key[4] = { -1, -1, -1, -1 };
     double* zero = nullptr;      // 32 zero doubles: target of out-of-map gathers
     // profiling (LGS_OPT_PROFILE)

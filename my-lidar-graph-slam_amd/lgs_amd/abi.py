@@ -25,6 +25,7 @@ LGS_OPT_COARSE_PLANES = 6
 LGS_OPT_PROFILE_MASK = 7
 LGS_OPT_SPIN_SYNC = 8
 LGS_OPT_SUPER_PRUNE = 9
+LGS_OPT_LANES_MIN_BATCH = 11
 LGS_OPT_SKIP_MASK = 10   # diagnostics only
 KERNEL_IDS = ["k_project", "k_coarse", "k_seed", "k_select", "k_fine", "k_replay", "k_cost", "k_precompute",
               "k_linsolve", "k_ray_emit", "k_ray_apply", "k_super", "k_super_planes"]   # lgs_ctx_kernel_stats order
@@ -210,11 +211,13 @@ SYMBOLS = [p[0] for p in _PROTOS]
 _lib: Optional[C.CDLL] = None
 
 
-def load(path: str = LIB_PATH) -> C.CDLL:
-    """Load liblgs_hip.so and bind prototypes.  Raises if missing (no fallback)."""
+def load(path: str = None) -> C.CDLL:
+    """Load liblgs_hip.so and bind prototypes.  Raises if missing (no fallback).
+    LGS_LIB overrides the path (A/B builds of the same library, tools/ab_build.sh)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("LGS_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"HIP extension missing: {path} (run __graft_entry__.build())")
     lib = C.CDLL(path)

@@ -147,3 +147,25 @@ def test_query_batch_rejects_mixed_sizes(ctx, world):
     with pytest.raises(abi.LgsError):
         ctx.optimize_pose_query_batch([a, b], abi.RtcsmParams(5, 0.4, 0.4, 0.3, 20.0), launcher_cost(),
                                       [sc, sc], [(0, 0, 0), (0, 0, 0)])
+
+
+@pytest.mark.parametrize("low_res,n_cells", [(5, 400), (4, 400), (2, 300), (8, 400)])
+def test_query_planes_equal_supplied_coarse_planes(ctx, world, low_res, n_cells):
+    """The query path writes the coarse planes straight from the batched
+    precompute; OptimizePose with a caller coarse map builds them by the
+    phase-plane copy.  Equal planes keep the same superblocks: identical
+    results AND identical counts of scored coarse blocks."""
+    cells, mx, my = build_map(world, n_cells, 0.05, 100, scene.arc_poses(5), n_beams=541)
+    rng = np.random.default_rng(low_res)
+    ang, qs = _queries(world, rng, 4, 541)
+    params = (low_res, 1.0, 1.0, 0.5, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    cg = ctx.precompute_max(g, low_res)
+    for j, (r, init) in enumerate(qs):
+        sc = ctx.scan(r, ang)
+        fused = ctx.optimize_pose_query(g, P, cost, sc, init)
+        two = ctx.optimize_pose(g, cg, P, cost, sc, init, 2.2250738585072014e-308)
+        assert fused.coarse_blocks == two.coarse_blocks, (j, fused.coarse_blocks, two.coarse_blocks)
+        assert list(fused.best_win) == list(two.best_win) and fused.score_max == two.score_max, j
+        assert_same(fused, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"lr{low_res} q{j}")
