@@ -613,7 +613,9 @@ __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __re
 // cell stamps *negflag with this build's generation and k_super then keeps
 // every superblock.  NaN cells are skipped by the max: a block whose sum is
 // NaN fails c > thr and is never selected anyway.
-constexpr int kSPX = 64, kSPY = 32;   // output tile of k_super_planes
+// output tile of k_super_planes: 128 padded columns = 32 consecutive values of
+// each column sub-phase, so every output row segment is one 128-byte store run
+constexpr int kSPX = 128, kSPY = 16;
 
 __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
 {
@@ -651,8 +653,10 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
         hm[yy][xx] = m;
     }
     __syncthreads();
+    // destination order: (row, column sub-phase, column / 4), the last fastest
     for (int k = tid; k < kSPY * kSPX; k += blockDim.x) {
-        const int yy = k / kSPX, xx = k % kSPX;
+        const int yy = k / kSPX, r = k % kSPX;
+        const int xx = 4 * (r % (kSPX / 4)) + r / (kSPX / 4);
         const int x = x0 + xx, y = y0 + yy;
         if (x >= Wqp || y >= Hqp) continue;
         double m = hm[yy][xx];

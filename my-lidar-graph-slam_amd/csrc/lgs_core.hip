@@ -459,6 +459,70 @@ __global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restri
     precompute_tile(in, out, W, H, w, pg, blockIdx.x, blockIdx.y);
 }
 
+// Batched precompute straight into the padded phase planes (W, H multiples of
+// the window LR <= 8).  A tile is kPQX coarse columns x kPTY fine rows: its
+// output row segment of one plane is kPQX consecutive doubles, and the store
+// loop walks (row, plane column, qx) with qx fastest, so the plane writes are
+// contiguous runs (the generic tile above scatters consecutive lanes over
+// the LR planes).  Same passes, same values (max is exact).
+constexpr int kPQX = 32, kPTY = 16;
+template <int LR>
+__global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __restrict__ jobs)
+{
+    const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
+    const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+#ifdef LGS_NO_XCD
+    const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    (void)l;
+#else
+    const int bx = l % gx, by = (l / gx) % gy, bz = l / (gx * gy);
+#endif
+    const PrecompJob& j = jobs[bz];
+    const int W = j.W, H = j.H;
+    const int x0 = bx * kPQX * LR, y0 = by * kPTY;
+    if (x0 >= W || y0 >= H) return;   // past this job's map (uniform)
+    const int x1 = min(x0 + kPQX * LR, W), y1 = min(y0 + kPTY, H);
+    const int sx0 = win_start(x0, W, LR), sy0 = win_start(y0, H, LR);
+    const int sx1 = win_start(x1 - 1, W, LR) + LR, sy1 = win_start(y1 - 1, H, LR) + LR;
+    const int fw = sx1 - sx0, fh = sy1 - sy0;
+    extern __shared__ double lds[];
+    double* tile = lds;              // [fh][fw]
+    double* m1 = lds + fh * fw;      // [kPTY][fw]
+    const double* __restrict__ in = j.in;
+    const int tid = threadIdx.x;
+    for (int k = tid; k < fh * fw; k += blockDim.x) {
+        const int yy = sy0 + k / fw, xx = sx0 + k % fw;
+        tile[k] = (xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;
+    }
+    __syncthreads();
+    const int oh = y1 - y0;
+    for (int k = tid; k < oh * fw; k += blockDim.x) {   // SlidingWindowMaxRow (y pass)
+        const int oy = k / fw, cx = k % fw;
+        const double* c = tile + (win_start(y0 + oy, H, LR) - sy0) * fw + cx;
+        double m = c[0];
+#pragma unroll
+        for (int i = 1; i < LR; ++i) m = dmax(m, c[i * fw]);
+        m1[oy * fw + cx] = m;
+    }
+    __syncthreads();
+    const PlaneGeom& pg = j.pg;
+    const int nq = (x1 - x0) / LR;   // coarse columns of this tile (W is a multiple of LR)
+    for (int k = tid; k < oh * LR * kPQX; k += blockDim.x) {   // SlidingWindowMaxCol (x pass)
+        const int oy = k / (LR * kPQX), rem = k % (LR * kPQX);
+        const int rx = rem / kPQX, qxl = rem % kPQX;
+        if (qxl >= nq) continue;
+        const int x = x0 + qxl * LR + rx, y = y0 + oy;
+        const double* c = m1 + oy * fw + (win_start(x, W, LR) - sx0);
+        double m = c[0];
+#pragma unroll
+        for (int i = 1; i < LR; ++i) m = dmax(m, c[i]);
+        const int qy = y / LR, ry = y - qy * LR;
+        j.out[(ry * LR + rx) * pg.pstride + (long long)(qy + pg.M) * pg.Wqp + (x0 / LR + qxl) + pg.M] = m;
+    }
+}
+
 // Batched: job blockIdx.z (maps of a batch may differ in size; the grid
 // covers the largest, tiles past a job's map exit).
 // XCD-aware order (speed only): one map's tiles on one XCD (see k_rtcsm.hip xcd_block)
@@ -534,7 +598,19 @@ void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, i
     LGS_REQUIRE(win >= 1 && win <= kMaxWinTiled, "batched precompute: window must be in [1, 32]");
     if (njobs == 0 || maxW == 0 || maxH == 0) return;
     const int tok = ctx->timing_begin(K_PRECOMPUTE, 32.0 * (double)maxW * (double)maxH * njobs);
-    if (!ctx->skipped(K_PRECOMPUTE)) {
+    if (ctx->skipped(K_PRECOMPUTE)) {
+    } else if (win <= 8) {
+        // plane-ordered tiles (every job of this path writes planes)
+        const int fw = kPQX * win + win - 1, fh = kPTY + win - 1;
+        const size_t lds = (size_t)(fh * fw + kPTY * fw) * sizeof(double);
+        dim3 grid((maxW + kPQX * win - 1) / (kPQX * win), (maxH + kPTY - 1) / kPTY, njobs);
+        switch (win) {
+#define LGS_PP_CASE(L) case L: hipLaunchKernelGGL(k_precompute_planes<L>, grid, dim3(256), lds, ctx->stream, d_jobs); break;
+        LGS_PP_CASE(1) LGS_PP_CASE(2) LGS_PP_CASE(3) LGS_PP_CASE(4) LGS_PP_CASE(5) LGS_PP_CASE(6)
+        LGS_PP_CASE(7) LGS_PP_CASE(8)
+#undef LGS_PP_CASE
+        }
+    } else {
         const int fw = kTileX + win - 1, fh = kTileY + win - 1;
         const size_t lds = (size_t)(fh * fw + kTileY * fw) * sizeof(double);
         dim3 grid((maxW + kTileX - 1) / kTileX, (maxH + kTileY - 1) / kTileY, njobs);
