@@ -38,6 +38,12 @@
  *                                C/mapping/scan_matcher_linear_solver.cpp:38-148
  *   lgs_cost_square_error        CostSquareError::Cost / ComputeCovariance
  *                                C/mapping/cost_function_square_error.cpp:21-58, :112-135
+ *   lgs_grid_precompute_pyramid  PrecomputeGridMaps C/mapping/grid_map_builder.cpp:471-495
+ *   lgs_bb_optimize_pose_batch   ScanMatcherBranchBound::OptimizePose(map, pyramid, scan, pose, thr)
+ *                                C/mapping/scan_matcher_branch_bound.cpp:47-154
+ *   lgs_bb_optimize_pose_query   ScanMatcherBranchBound::OptimizePose(query) :29-44
+ *   lgs_loop_detect_bb           LoopDetectorBranchBound::Detect + FindCorrespondingPose
+ *                                C/mapping/loop_detector_branch_bound.cpp:26-117
  *
  * Threading: one lgs_ctx per matcher instance (the reference's frontend and
  * loop detector own distinct matchers, C/slam_launcher.cpp:774-775, :835).  A
@@ -317,6 +323,51 @@ int  lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* params, const l
                            double score_threshold, const lgs_loop_query* queries, int num_queries,
                            const lgs_loop_candidate* candidates, int num_candidates,
                            lgs_loop_result* results);
+
+/* ---- branch-and-bound matcher ----
+ * ScanMatcherBranchBound (C/mapping/scan_matcher_branch_bound.cpp:8-200,
+ * H/mapping/scan_matcher_branch_bound.hpp) with ScorePixelAccurate
+ * (C/mapping/score_function_pixel_accurate.cpp:19-77) and the grid-map
+ * pyramid PrecomputeGridMaps (C/mapping/grid_map_builder.cpp:471-495).
+ * The device scores every node the reference's depth-first search can visit
+ * (level by level, a superset bounded by the threshold argument of
+ * DESIGN.md §4.6); the host then replays the reference's LIFO search over
+ * those scores, so the result is the reference's own (best node, score,
+ * nodes visited).  Field order follows the constructor (nodeHeightMax,
+ * rangeX, rangeY, rangeTheta, scanRangeMax) then ScorePixelAccurate
+ * (usableRangeMin, usableRangeMax). */
+typedef struct {
+    int    node_height_max;
+    double range_x, range_y, range_theta;
+    double scan_range_max;
+    double score_usable_range_min, score_usable_range_max;
+} lgs_bb_params;
+
+/* PrecomputeGridMaps: pyramid[h] = window-max map with window 2^h,
+ * h = 0..node_height_max (node_height_max + 1 grids of the input's geometry,
+ * created by the caller). */
+int  lgs_grid_precompute_pyramid(lgs_ctx* ctx, const lgs_grid* in, int node_height_max,
+                                 lgs_grid* const* pyramid);
+/* OptimizePose(gridMap, precompMaps, scan, pose, thr) (:47-154) for n scans
+ * against one pyramid (loop-closure candidates); summaries as the RTCSM
+ * ones, with best_win = the best node's (x, y, theta), coarse_blocks = nodes
+ * scored on the device, fine_blocks = nodes the reference's search visits. */
+int  lgs_bb_optimize_pose_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* const* pyramid,
+                                const lgs_bb_params* params, const lgs_cost_ge_params* cost,
+                                const lgs_scan* const* scans, const lgs_pose2d* initial_poses, int n,
+                                double normalized_score_threshold, lgs_rtcsm_summary* out);
+/* OptimizePose(query) (:29-44): pyramid of the query's map, threshold DBL_MIN */
+int  lgs_bb_optimize_pose_query(lgs_ctx* ctx, const lgs_grid* grid, const lgs_bb_params* params,
+                                const lgs_cost_ge_params* cost, const lgs_scan* scan,
+                                lgs_pose2d initial_pose, lgs_rtcsm_summary* out);
+/* LoopDetectorBranchBound::Detect + FindCorrespondingPose
+ * (C/mapping/loop_detector_branch_bound.cpp:26-117): per query the pyramid of
+ * its local map (computed here; lgs_loop_query.coarse is ignored), then every
+ * candidate matched with the score threshold.  One result per candidate. */
+int  lgs_loop_detect_bb(lgs_ctx* ctx, const lgs_bb_params* params, const lgs_cost_ge_params* cost,
+                        double score_threshold, const lgs_loop_query* queries, int num_queries,
+                        const lgs_loop_candidate* candidates, int num_candidates,
+                        lgs_loop_result* results);
 
 /* ---- K4: Gauss-Newton refine (ScanMatcherLinearSolver + CostSquareError) ----
  * Replaces ScanMatcherLinearSolver::OptimizePose (C/mapping/scan_matcher_linear_solver.cpp:38-85,

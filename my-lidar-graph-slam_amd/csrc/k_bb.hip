@@ -1,0 +1,820 @@
+// k_bb.hip -- branch-and-bound matcher on MI355X.
+//
+// Restates ScanMatcherBranchBound::OptimizePose
+// (C/mapping/scan_matcher_branch_bound.cpp:47-154) with ScorePixelAccurate
+// (C/mapping/score_function_pixel_accurate.cpp:19-77) over the window-max
+// pyramid of PrecomputeGridMaps (C/mapping/grid_map_builder.cpp:471-495).
+//
+// The reference walks a LIFO depth-first search whose pruning depends on the
+// best score found so far, and its node scores recompute every hit point at
+// the node's own pose, so parent scores do not bound child scores exactly
+// (rounding): the visit order decides the result.  The device therefore does
+// not search; it scores, level by level, every node the reference's search
+// can visit:
+//   * a node is visited only if each ancestor was expanded, i.e. scored above
+//     the running best at its turn, which is >= the threshold thr0;
+//   * before the first leaf is accepted the search only walks the first
+//     descent (the last-pushed top node, then always the last-pushed child);
+//     if that whole path scores above thr0 its leaf L1 is accepted and every
+//     later expansion needs a score > s(L1).
+// So expanding every node scored above thr_exp = (path valid ? s(L1) : thr0),
+// plus the path nodes, covers the visited set.  The host then replays the
+// reference's search over these scores, exactly, and the greedy-endpoint
+// cost/covariance of the best pose come from k_cost (k_rtcsm.hip).
+//
+//   k_bb_trig    r cos(theta_t + a), r sin(theta_t + a) per (angle, valid beam)
+//   k_bb_score   one lane per node: hit cells at the node pose (the
+//                reference's own arithmetic), sequential fp64 beam-order sum
+//                of the level's map values; cells within guard_eps of a cell
+//                boundary are recorded and re-checked on the host with glibc
+//   k_bb_expand  the four children of every node scored above thr_exp (or on
+//                the first descent), wave-aggregated appends
+//   k_bb_rescore exact re-score of a node from host (glibc) cells
+#include "lgs_internal.hpp"
+
+#include <algorithm>
+#include <cfloat>
+#include <cstring>
+#include <unordered_map>
+
+using namespace lgs;
+
+namespace lgs {
+void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, const PlaneGeom* planes);
+void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params* cost, lgs_scan* const* scans,
+                    const lgs_pose2d* best, int n, lgs_rtcsm_summary* out);
+}  // namespace lgs
+
+namespace {
+
+constexpr int kBBMaxH = 12;   // NodeHeightMax limit (window 4096 cells)
+
+// One match of a batched branch-and-bound launch (device memory).
+struct BBItem {
+    double sx, sy, st;            // sensor pose (Compound(initialPose, relPose))
+    double step_x, step_y, step_t;
+    double min_x, min_y, res;     // map geometry
+    double thr_exp;               // expansion threshold (see header)
+    int W, H;
+    int T, Nv, win_t;
+    int px, py, pt, hmax;         // first descent's top node; path forced when path_ok
+    int path_ok;
+    const double* ranges;
+    const double* angles;
+    const int* vidx;              // valid beams (ScorePixelAccurate filter), beam order
+    double* rc;                   // [T][Nv]
+    double* rs;
+    const double* maps[kBBMaxH + 1];
+};
+
+// node: x = item << 4 | level, y = x index, z = y index, w = theta index
+__device__ __forceinline__ int node_item(int4 n) { return n.x >> 4; }
+__device__ __forceinline__ int node_level(int4 n) { return n.x & 15; }
+
+struct BBGuard {
+    int level, node, v, pad;      // node index within its level's list
+    int ix, iy, pad2, pad3;       // device cell
+};
+
+__device__ __forceinline__ bool near_cell_boundary(double q, double eps)
+{
+    const double f = q - floor(q);
+    const double e = eps + fabs(q) * 1e-13;
+    return f < e || f > 1.0 - e;
+}
+
+__global__ __launch_bounds__(256) void k_bb_trig(const BBItem* __restrict__ items)
+{
+    const BBItem& it = items[blockIdx.z];
+    const int t = blockIdx.y;
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= it.T || v >= it.Nv) return;
+    const int i = it.vidx[v];
+    // nodePose.mTheta = sensorPose.mTheta + currentNode.mTheta * stepTheta (:96-99)
+    const double th = it.st + (double)(t - it.win_t) * it.step_t;
+    // ScanData::HitPoint (H/sensor/sensor_data.hpp:162-173)
+    double sn, cs;
+    sincos(th + it.angles[i], &sn, &cs);
+    const double r = it.ranges[i];
+    it.rc[(size_t)t * it.Nv + v] = r * cs;
+    it.rs[(size_t)t * it.Nv + v] = r * sn;
+}
+
+constexpr int kBBPipe = 8;
+__global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ items, const int4* __restrict__ nodes,
+                                                  int n, int level_id, double* __restrict__ scores,
+                                                  BBGuard* __restrict__ guards, int* __restrict__ nguard,
+                                                  int guard_cap, double guard_eps, int inject)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int4 nd = nodes[i];
+    const BBItem& it = items[node_item(nd)];
+    const int h = node_level(nd);
+    // nodePose (:96-99)
+    const double nx = it.sx + (double)nd.y * it.step_x;
+    const double ny = it.sy + (double)nd.z * it.step_y;
+    const int Nv = it.Nv, W = it.W, H = it.H;
+    const double* __restrict__ rc = it.rc + (size_t)(nd.w + it.win_t) * Nv;
+    const double* __restrict__ rs = it.rs + (size_t)(nd.w + it.win_t) * Nv;
+    const double* __restrict__ map = it.maps[h];
+    const double minx = it.min_x, miny = it.min_y, res = it.res;
+    double sum = 0.0;
+    for (int v0 = 0; v0 < Nv; v0 += kBBPipe) {
+        double val[kBBPipe];
+#pragma unroll
+        for (int j = 0; j < kBBPipe; ++j) {
+            const int v = v0 + j;
+            val[j] = 0.0;
+            if (v < Nv) {
+                // WorldCoordinateToGridCellIndex of HitPoint (H/grid_map/grid_map.hpp:779-790)
+                const double qx = (nx + rc[v] - minx) / res;
+                const double qy = (ny + rs[v] - miny) / res;
+                int ix = (int)floor(qx), iy = (int)floor(qy);
+                if (near_cell_boundary(qx, guard_eps) || near_cell_boundary(qy, guard_eps)) {
+                    ix += inject;
+                    const int slot = atomicAdd(nguard, 1);
+                    if (slot < guard_cap) {
+                        BBGuard g;
+                        g.level = level_id;
+                        g.node = i;
+                        g.v = v;
+                        g.ix = ix;
+                        g.iy = iy;
+                        g.pad = g.pad2 = g.pad3 = 0;
+                        guards[slot] = g;
+                    }
+                }
+                // GridMap::Value(idx, unknown): 0.0 outside; unknown cells
+                // (0.0) are skipped by the reference (:55-56), adding 0.0 is the same
+                if (((unsigned)ix < (unsigned)W) & ((unsigned)iy < (unsigned)H)) val[j] = map[(size_t)iy * W + ix];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kBBPipe; ++j) sum += val[j];
+    }
+    scores[i] = sum;
+}
+
+__global__ __launch_bounds__(256) void k_bb_expand(const BBItem* __restrict__ items, const int4* __restrict__ nodes,
+                                                   const double* __restrict__ scores, int n,
+                                                   int4* __restrict__ next, int* __restrict__ count, int cap,
+                                                   int* __restrict__ overflow)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool ex = false;
+    int4 nd = make_int4(0, 0, 0, 0);
+    if (i < n) {
+        nd = nodes[i];
+        const int h = node_level(nd);
+        if (h > 0) {
+            const BBItem& it = items[node_item(nd)];
+            const int off = (1 << it.hmax) - (1 << h);
+            const bool path = it.path_ok && nd.w == it.pt && nd.y == it.px + off && nd.z == it.py + off;
+            ex = scores[i] > it.thr_exp || path;
+        }
+    }
+    const unsigned long long bal = __ballot(ex);
+    if (bal == 0ull) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)bal) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(count, 4 * __popcll(bal));
+    base = __shfl(base, leader, 64);
+    if (!ex) return;
+    const int pos = base + 4 * __popcll(bal & ((1ull << lane) - 1ull));
+    if (pos + 4 > cap) {
+        *overflow = 1;
+        return;
+    }
+    // :123-135: children (x, y), (x + ws, y), (x, y + ws), (x + ws, y + ws)
+    const int h = node_level(nd) - 1, ws = 1 << h;
+    const int head = (node_item(nd) << 4) | h;
+    next[pos + 0] = make_int4(head, nd.y, nd.z, nd.w);
+    next[pos + 1] = make_int4(head, nd.y + ws, nd.z, nd.w);
+    next[pos + 2] = make_int4(head, nd.y, nd.z + ws, nd.w);
+    next[pos + 3] = make_int4(head, nd.y + ws, nd.z + ws, nd.w);
+}
+
+// Exact re-score of listed nodes (one workgroup each) from host cells:
+// cells[k * Nmax + v] for valid beam v; lanes load, lane 0 adds in beam order.
+__global__ __launch_bounds__(64) void k_bb_rescore(const double* const* __restrict__ maps, const int* __restrict__ dims,
+                                                   const int2* __restrict__ cells, const int* __restrict__ nv,
+                                                   int Nmax, double* __restrict__ out)
+{
+    __shared__ double buf[64];
+    const int k = blockIdx.x;
+    const double* __restrict__ map = maps[k];
+    const int W = dims[2 * k], H = dims[2 * k + 1];
+    const int n = nv[k];
+    double sum = 0.0;
+    for (int v0 = 0; v0 < n; v0 += 64) {
+        const int v = v0 + threadIdx.x;
+        double val = 0.0;
+        if (v < n) {
+            const int2 c = cells[(size_t)k * Nmax + v];
+            if (((unsigned)c.x < (unsigned)W) & ((unsigned)c.y < (unsigned)H)) val = map[(size_t)c.y * W + c.x];
+        }
+        buf[threadIdx.x] = val;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int m = min(64, n - v0);
+            for (int j = 0; j < m; ++j) sum += buf[j];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[k] = sum;
+}
+
+// ------------------------------------------------------------------ host
+inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// Per-batch device arena carved from one slot (sizes known before the launch).
+struct Carver {
+    char* base;
+    size_t off = 0;
+    explicit Carver(char* b) : base(b) {}
+    template <class T>
+    T* take(size_t n)
+    {
+        T* p = (T*)(base + off);
+        off += align256(sizeof(T) * std::max<size_t>(n, 1));
+        return p;
+    }
+};
+
+struct BBHost {   // host plan of one match
+    lgs_pose2d sensor;
+    double step_x, step_y, step_t;
+    int win_x, win_y, win_t, T, Nv, N;
+    double thr0;
+    std::vector<int> vidx;
+    std::vector<int> top_x, top_y;
+};
+
+inline uint64_t node_key(int h, int x, int y, int t)
+{
+    return ((uint64_t)(unsigned)h << 60) | ((uint64_t)((unsigned)(x + (1 << 19)) & 0xFFFFFu) << 40) |
+           ((uint64_t)((unsigned)(y + (1 << 19)) & 0xFFFFFu) << 20) | (uint64_t)((unsigned)(t + (1 << 19)) & 0xFFFFFu);
+}
+
+BBHost make_bb_plan(const lgs_grid* grid, const lgs_bb_params* p, const lgs_scan* scan, lgs_pose2d init,
+                    double nthr)
+{
+    BBHost b;
+    b.sensor = compound(init, scan->rel);   // :54-56
+    // ComputeSearchStep (:178-198)
+    const double maxRange = std::min(scan->max_elem, p->scan_range_max);
+    const double theta = grid->res / maxRange;
+    b.step_x = grid->res;
+    b.step_y = grid->res;
+    b.step_t = std::acos(1.0 - 0.5 * theta * theta);
+    // :65-70
+    b.win_x = (int)std::ceil(0.5 * p->range_x / b.step_x);
+    b.win_y = (int)std::ceil(0.5 * p->range_y / b.step_y);
+    b.win_t = (int)std::ceil(0.5 * p->range_theta / b.step_t);
+    b.T = 2 * b.win_t + 1;
+    b.N = scan->n;
+    b.thr0 = nthr * (double)scan->n;   // :73-75
+    // ScorePixelAccurate's beam filter (:27-41)
+    const double minRange = std::max(p->score_usable_range_min, scan->min_range);
+    const double maxR = std::min(p->score_usable_range_max, scan->max_range);
+    for (int i = 0; i < scan->n; ++i) {
+        const double r = scan->h_ranges[i];
+        if (r >= maxR || r <= minRange) continue;
+        b.vidx.push_back(i);
+    }
+    b.Nv = (int)b.vidx.size();
+    const int wmax = 1 << p->node_height_max;   // :81-88
+    for (int x = -b.win_x; x <= b.win_x; x += wmax) b.top_x.push_back(x);
+    for (int y = -b.win_y; y <= b.win_y; y += wmax) b.top_y.push_back(y);
+    return b;
+}
+
+// exact hit cell of valid beam v at a node pose (glibc sincos, the reference's arithmetic)
+void host_bb_cell(const BBHost& b, const lgs_grid* g, const lgs_scan* scan, int x, int y, int t, int v, int& ix,
+                  int& iy)
+{
+    const double nx = b.sensor.x + (double)x * b.step_x;
+    const double ny = b.sensor.y + (double)y * b.step_y;
+    const double th = b.sensor.theta + (double)t * b.step_t;
+    const int i = b.vidx[v];
+    double s, c;
+    ref_sincos(th + scan->h_angles[i], s, c);
+    const double r = scan->h_ranges[i];
+    ix = (int)std::floor((nx + r * c - g->min_x) / g->res);
+    iy = (int)std::floor((ny + r * s - g->min_y) / g->res);
+}
+
+struct BBLevel {
+    int4* d_nodes = nullptr;
+    double* d_scores = nullptr;
+    int n = 0;
+    std::vector<int4> nodes;
+    std::vector<double> scores;
+};
+
+// Run n branch-and-bound matches: grids[j] (fine map, its geometry) and
+// pyr[j][0..H] (the map pyramid, device pointers).
+// no_path: expand with thr0 everywhere (the fallback when a guard-corrected
+// first descent changed the threshold the superset was built with).
+void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost, const lgs_grid* const* grids,
+            const double* const* const* pyr, lgs_scan* const* scans, const lgs_pose2d* init, int n, double nthr,
+            lgs_rtcsm_summary* out, bool no_path = false)
+{
+    LGS_HIP_CHECK(hipSetDevice(ctx->device));
+    std::memset(out, 0, sizeof(lgs_rtcsm_summary) * (size_t)n);
+    const int Hm = p->node_height_max;
+    std::vector<BBHost> plans;
+    plans.reserve((size_t)n);
+    int Tmax = 1, NvMax = 1;
+    size_t trig_doubles = 0;
+    for (int j = 0; j < n; ++j) {
+        plans.push_back(make_bb_plan(grids[j], p, scans[j], init[j], nthr));
+        Tmax = std::max(Tmax, plans[j].T);
+        NvMax = std::max(NvMax, plans[j].Nv);
+        trig_doubles += 2 * (size_t)plans[j].T * std::max(plans[j].Nv, 1);
+    }
+    // device scratch: trig tables + valid-beam lists
+    size_t vtot = 0;
+    for (auto& b : plans) vtot += std::max<size_t>(b.vidx.size(), 1);
+    const size_t bytes = align256(sizeof(double) * trig_doubles) + 256 * (size_t)n * 2 + align256(sizeof(int) * vtot) +
+                         256 * (size_t)n;
+    Carver cv((char*)ctx->ensure(S_BB0, bytes));
+    std::vector<BBItem> items((size_t)n);
+    std::vector<int*> d_vidx((size_t)n);
+    for (int j = 0; j < n; ++j) {
+        const BBHost& b = plans[j];
+        BBItem& it = items[j];
+        std::memset(&it, 0, sizeof(it));
+        it.sx = b.sensor.x;
+        it.sy = b.sensor.y;
+        it.st = b.sensor.theta;
+        it.step_x = b.step_x;
+        it.step_y = b.step_y;
+        it.step_t = b.step_t;
+        it.min_x = grids[j]->min_x;
+        it.min_y = grids[j]->min_y;
+        it.res = grids[j]->res;
+        it.W = grids[j]->w;
+        it.H = grids[j]->h;
+        it.T = b.T;
+        it.Nv = b.Nv;
+        it.win_t = b.win_t;
+        it.px = b.top_x.back();
+        it.py = b.top_y.back();
+        it.pt = b.win_t;
+        it.hmax = Hm;
+        it.thr_exp = b.thr0;
+        it.ranges = scans[j]->d_ranges;
+        it.angles = scans[j]->d_angles;
+        it.rc = cv.take<double>((size_t)b.T * std::max(b.Nv, 1));
+        it.rs = cv.take<double>((size_t)b.T * std::max(b.Nv, 1));
+        d_vidx[j] = cv.take<int>(std::max<size_t>(b.vidx.size(), 1));
+        it.vidx = d_vidx[j];
+        for (int h = 0; h <= Hm; ++h) it.maps[h] = pyr[j][h];
+    }
+    for (int j = 0; j < n; ++j)
+        if (!plans[j].vidx.empty())
+            LGS_HIP_CHECK(hipMemcpyAsync(d_vidx[j], plans[j].vidx.data(), sizeof(int) * plans[j].vidx.size(),
+                                         hipMemcpyHostToDevice, ctx->stream));
+    // guards (shared by every level of the batch)
+    int* d_counts = (int*)ctx->ensure(S_BB3, 256);   // [0] guards, [1] children, [2] overflow
+    BBGuard* d_guards = (BBGuard*)ctx->ensure(S_BB4, sizeof(BBGuard) * (size_t)ctx->guard_cap);
+    LGS_HIP_CHECK(hipMemsetAsync(d_counts, 0, 256, ctx->stream));
+
+    // pass 1: trig tables and the first descent of every match
+    std::vector<int4> path((size_t)n * (Hm + 1));
+    for (int j = 0; j < n; ++j)
+        for (int h = Hm; h >= 0; --h) {
+            const int off = (1 << Hm) - (1 << h);
+            path[(size_t)j * (Hm + 1) + (Hm - h)] = make_int4((j << 4) | h, items[j].px + off, items[j].py + off,
+                                                              items[j].pt);
+        }
+    double* d_pscores = (double*)ctx->ensure(S_BB5, sizeof(double) * path.size());
+    std::vector<double> pscores(path.size());
+    {
+        Upload up(ctx);
+        const size_t ioff = up.append(items.data(), items.size());
+        const size_t poff = up.append(path.data(), path.size());
+        up.flush();
+        const BBItem* d_items = up.at<BBItem>(ioff);
+        dim3 g((NvMax + 255) / 256, Tmax, n);
+        hipLaunchKernelGGL(k_bb_trig, g, dim3(256), 0, ctx->stream, d_items);
+        LGS_HIP_CHECK(hipGetLastError());
+        const int np = (int)path.size();
+        hipLaunchKernelGGL(k_bb_score, dim3((np + 255) / 256), dim3(256), 0, ctx->stream, d_items,
+                           up.at<int4>(poff), np, -1, d_pscores, d_guards, d_counts, ctx->guard_cap, ctx->guard_eps,
+                           ctx->inject_index ? 1 : 0);
+        LGS_HIP_CHECK(hipGetLastError());
+        LGS_HIP_CHECK(hipMemcpyAsync(pscores.data(), d_pscores, sizeof(double) * np, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+        ctx->sync();
+    }
+    // the path scores may carry unchecked guards: they only choose thr_exp,
+    // and a wrong choice is caught below (a node missing from the table)
+    for (int j = 0; j < n; ++j) {
+        bool ok = !no_path;
+        for (int k = 0; k <= Hm; ++k) ok &= pscores[(size_t)j * (Hm + 1) + k] > plans[j].thr0;
+        items[j].path_ok = ok ? 1 : 0;
+        if (ok) items[j].thr_exp = std::max(plans[j].thr0, pscores[(size_t)j * (Hm + 1) + Hm]);
+    }
+    LGS_HIP_CHECK(hipMemsetAsync(d_counts, 0, 256, ctx->stream));
+
+    // pass 2: level by level, every node the search can visit
+    std::vector<BBLevel> levels((size_t)Hm + 1);   // index = Hm - h
+    {
+        std::vector<int4> top;
+        for (int j = 0; j < n; ++j)
+            for (int x : plans[j].top_x)
+                for (int y : plans[j].top_y)
+                    for (int t = -plans[j].win_t; t <= plans[j].win_t; ++t)
+                        top.push_back(make_int4((j << 4) | Hm, x, y, t));
+        Upload up(ctx);
+        const size_t ioff = up.append(items.data(), items.size());
+        const size_t toff = up.append(top.data(), top.size());
+        up.flush();
+        const BBItem* d_items = up.at<BBItem>(ioff);
+        // node/score buffers per level: grown by the host between levels
+        int cur_n = (int)top.size();
+        int4* cur_nodes = (int4*)ctx->ensure(S_BB1, sizeof(int4) * (size_t)cur_n);
+        LGS_HIP_CHECK(hipMemcpyAsync(cur_nodes, up.at<int4>(toff), sizeof(int4) * (size_t)cur_n,
+                                     hipMemcpyDeviceToDevice, ctx->stream));
+        std::vector<void*> keep;   // per-level device buffers (freed at the end)
+        for (int h = Hm; h >= 0; --h) {
+            BBLevel& L = levels[(size_t)(Hm - h)];
+            L.n = cur_n;
+            L.d_nodes = cur_nodes;
+            LGS_HIP_CHECK(hipMalloc(&L.d_scores, sizeof(double) * std::max(cur_n, 1)));
+            keep.push_back(L.d_scores);
+            if (cur_n > 0) {
+                hipLaunchKernelGGL(k_bb_score, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items,
+                                   cur_nodes, cur_n, Hm - h, L.d_scores, d_guards, d_counts, ctx->guard_cap,
+                                   ctx->guard_eps, ctx->inject_index ? 1 : 0);
+                LGS_HIP_CHECK(hipGetLastError());
+            }
+            if (h == 0 || cur_n == 0) break;
+            const int cap = 4 * cur_n;
+            int4* next = nullptr;
+            LGS_HIP_CHECK(hipMalloc(&next, sizeof(int4) * (size_t)cap));
+            keep.push_back(next);
+            LGS_HIP_CHECK(hipMemsetAsync(d_counts + 1, 0, 2 * sizeof(int), ctx->stream));
+            hipLaunchKernelGGL(k_bb_expand, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items, cur_nodes,
+                               L.d_scores, cur_n, next, d_counts + 1, cap, d_counts + 2);
+            LGS_HIP_CHECK(hipGetLastError());
+            int cnt[2] = { 0, 0 };
+            LGS_HIP_CHECK(hipMemcpyAsync(cnt, d_counts + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+            ctx->sync();
+            LGS_REQUIRE(cnt[1] == 0, "branch-and-bound: child list overflow");
+            cur_n = cnt[0];
+            cur_nodes = next;
+        }
+        // host copies of every level
+        for (auto& L : levels) {
+            L.nodes.resize((size_t)L.n);
+            L.scores.resize((size_t)L.n);
+            if (L.n == 0) continue;
+            LGS_HIP_CHECK(hipMemcpyAsync(L.nodes.data(), L.d_nodes, sizeof(int4) * (size_t)L.n, hipMemcpyDeviceToHost,
+                                         ctx->stream));
+            LGS_HIP_CHECK(hipMemcpyAsync(L.scores.data(), L.d_scores, sizeof(double) * (size_t)L.n,
+                                         hipMemcpyDeviceToHost, ctx->stream));
+        }
+        int ng = 0;
+        LGS_HIP_CHECK(hipMemcpyAsync(&ng, d_counts, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        ctx->sync();
+        std::vector<BBGuard> guards((size_t)std::min(ng, ctx->guard_cap));
+        if (!guards.empty())
+            LGS_HIP_CHECK(hipMemcpy(guards.data(), d_guards, sizeof(BBGuard) * guards.size(), hipMemcpyDeviceToHost));
+        for (void* q : keep) LGS_HIP_CHECK(hipFree(q));
+        for (auto& L : levels) L.d_nodes = nullptr, L.d_scores = nullptr;
+
+        // guarded cells: exact glibc cells; nodes with any differing cell are
+        // re-scored from host cells (or, past guard_cap records, every node
+        // of the batch is re-checked on the host)
+        std::vector<std::pair<int, int>> dirty;   // (level id, node index)
+        if (ng > ctx->guard_cap) {
+            for (int l = 0; l <= Hm; ++l)
+                for (int i = 0; i < levels[(size_t)l].n; ++i) dirty.push_back({ l, i });
+        } else {
+            for (const BBGuard& g : guards) {
+                const int4 nd = levels[(size_t)g.level].nodes[(size_t)g.node];
+                const int j = nd.x >> 4;
+                int ix, iy;
+                host_bb_cell(plans[j], grids[j], scans[j], nd.y, nd.z, nd.w, g.v, ix, iy);
+                if (ix != g.ix || iy != g.iy) dirty.push_back({ g.level, g.node });
+            }
+            std::sort(dirty.begin(), dirty.end());
+            dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+        }
+        for (int j = 0; j < n; ++j) out[j].guard_hits = 0;
+        for (const BBGuard& g : guards) {
+            const int4 nd = levels[(size_t)g.level].nodes[(size_t)g.node];
+            out[nd.x >> 4].guard_hits += 1;
+        }
+        if (!dirty.empty()) {
+            const int nd_n = (int)dirty.size();
+            std::vector<int2> cells((size_t)nd_n * NvMax);
+            std::vector<int> nvs((size_t)nd_n), dims((size_t)2 * nd_n);
+            std::vector<const double*> maps((size_t)nd_n);
+            for (int k = 0; k < nd_n; ++k) {
+                const int4 nd = levels[(size_t)dirty[k].first].nodes[(size_t)dirty[k].second];
+                const int j = nd.x >> 4, h = nd.x & 15;
+                nvs[k] = plans[j].Nv;
+                dims[2 * k] = grids[j]->w;
+                dims[2 * k + 1] = grids[j]->h;
+                maps[k] = pyr[j][h];
+                for (int v = 0; v < plans[j].Nv; ++v) {
+                    int ix, iy;
+                    host_bb_cell(plans[j], grids[j], scans[j], nd.y, nd.z, nd.w, v, ix, iy);
+                    cells[(size_t)k * NvMax + v] = make_int2(ix, iy);
+                }
+                out[j].fixups = 1;
+            }
+            Upload u2(ctx);
+            const size_t co = u2.append(cells.data(), cells.size());
+            const size_t no = u2.append(nvs.data(), nvs.size());
+            const size_t dof = u2.append(dims.data(), dims.size());
+            const size_t mo = u2.append(maps.data(), maps.size());
+            u2.flush();
+            double* d_out = (double*)ctx->ensure(S_BB5, sizeof(double) * (size_t)nd_n);
+            hipLaunchKernelGGL(k_bb_rescore, dim3(nd_n), dim3(64), 0, ctx->stream, u2.at<const double*>(mo),
+                               u2.at<int>(dof), u2.at<int2>(co), u2.at<int>(no), NvMax, d_out);
+            LGS_HIP_CHECK(hipGetLastError());
+            std::vector<double> rs((size_t)nd_n);
+            LGS_HIP_CHECK(hipMemcpyAsync(rs.data(), d_out, sizeof(double) * (size_t)nd_n, hipMemcpyDeviceToHost,
+                                         ctx->stream));
+            ctx->sync();
+            for (int k = 0; k < nd_n; ++k) levels[(size_t)dirty[k].first].scores[(size_t)dirty[k].second] = rs[k];
+        }
+    }
+
+    // host replay of the reference's search (:81-140) over the scored nodes
+    std::vector<std::unordered_map<uint64_t, double>> table((size_t)n);
+    std::vector<int64_t> scored((size_t)n, 0);
+    for (auto& L : levels)
+        for (int i = 0; i < L.n; ++i) ++scored[(size_t)(L.nodes[(size_t)i].x >> 4)];
+    for (int j = 0; j < n; ++j) table[j].reserve((size_t)scored[j] * 2 + 16);
+    for (auto& L : levels)
+        for (int i = 0; i < L.n; ++i) {
+            const int4 nd = L.nodes[(size_t)i];
+            table[(size_t)(nd.x >> 4)].emplace(node_key(nd.x & 15, nd.y, nd.z, nd.w), L.scores[(size_t)i]);
+        }
+    std::vector<lgs_pose2d> best((size_t)n);
+    std::vector<char> failed((size_t)n, 0);
+    struct SNode { int x, y, t, h; };
+    std::vector<SNode> st;
+    for (int j = 0; j < n; ++j) {
+        const BBHost& b = plans[j];
+        double scoreMax = b.thr0;
+        lgs_pose2d bestPose = b.sensor;
+        int bx = 0, by = 0, bt = 0;
+        int64_t visited = 0;
+        st.clear();
+        for (int x : b.top_x)
+            for (int y : b.top_y)
+                for (int t = -b.win_t; t <= b.win_t; ++t) st.push_back({ x, y, t, Hm });
+        const auto& tab = table[(size_t)j];
+        while (!st.empty()) {
+            const SNode cur = st.back();
+            st.pop_back();
+            const auto f = tab.find(node_key(cur.h, cur.x, cur.y, cur.t));
+            if (f == tab.end()) {
+                LGS_REQUIRE(!no_path, "branch-and-bound: the search reached a node the device did not score");
+                failed[(size_t)j] = 1;   // rerun with the thr0 superset
+                break;
+            }
+            const double score = f->second;
+            ++visited;
+            if (score <= scoreMax) continue;   // :105-109
+            if (cur.h == 0) {                  // :112-119
+                bestPose = { b.sensor.x + (double)cur.x * b.step_x, b.sensor.y + (double)cur.y * b.step_y,
+                             b.sensor.theta + (double)cur.t * b.step_t };
+                scoreMax = score;
+                bx = cur.x;
+                by = cur.y;
+                bt = cur.t;
+                continue;
+            }
+            const int h = cur.h - 1, ws = 1 << h;   // :120-137
+            st.push_back({ cur.x, cur.y, cur.t, h });
+            st.push_back({ cur.x + ws, cur.y, cur.t, h });
+            st.push_back({ cur.x, cur.y + ws, cur.t, h });
+            st.push_back({ cur.x + ws, cur.y + ws, cur.t, h });
+        }
+        lgs_rtcsm_summary& o = out[j];
+        const int gh = o.guard_hits, fx = o.fixups;
+        std::memset(&o, 0, sizeof(o));
+        o.guard_hits = gh;
+        o.fixups = fx;
+        o.pose_found = scoreMax > b.thr0;   // :142-144
+        o.initial_pose = init[j];
+        o.score_max = scoreMax;
+        o.score_threshold = b.thr0;
+        o.best_win[0] = bx;
+        o.best_win[1] = by;
+        o.best_win[2] = bt;
+        o.win[0] = b.win_x;
+        o.win[1] = b.win_y;
+        o.win[2] = b.win_t;
+        o.steps[0] = b.step_x;
+        o.steps[1] = b.step_y;
+        o.steps[2] = b.step_t;
+        o.best_sensor_pose = bestPose;
+        o.coarse_blocks = scored[(size_t)j];
+        o.fine_blocks = visited;
+        best[j] = bestPose;
+    }
+    // cost and covariance at the best poses (:146-153), grouped by map
+    std::vector<int> order, redo;
+    for (int j = 0; j < n; ++j) (failed[(size_t)j] ? redo : order).push_back(j);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return grids[a] < grids[b]; });
+    for (size_t k0 = 0; k0 < order.size();) {
+        size_t k1 = k0;
+        while (k1 < order.size() && grids[order[k1]] == grids[order[k0]]) ++k1;
+        std::vector<lgs_scan*> sc;
+        std::vector<lgs_pose2d> bp;
+        std::vector<lgs_rtcsm_summary> tmp;
+        for (size_t k = k0; k < k1; ++k) {
+            sc.push_back(scans[order[k]]);
+            bp.push_back(best[order[k]]);
+            tmp.push_back(out[order[k]]);
+        }
+        cost_summaries(ctx, grids[order[k0]], cost, sc.data(), bp.data(), (int)sc.size(), tmp.data());
+        for (size_t k = k0; k < k1; ++k) out[order[k]] = tmp[k - k0];
+        k0 = k1;
+    }
+    if (!redo.empty()) {
+        std::vector<const lgs_grid*> g2;
+        std::vector<const double* const*> p2;
+        std::vector<lgs_scan*> s2;
+        std::vector<lgs_pose2d> i2;
+        for (int j : redo) {
+            g2.push_back(grids[j]);
+            p2.push_back(pyr[j]);
+            s2.push_back(scans[j]);
+            i2.push_back(init[j]);
+        }
+        std::vector<lgs_rtcsm_summary> o2(redo.size());
+        run_bb(ctx, p, cost, g2.data(), p2.data(), s2.data(), i2.data(), (int)redo.size(), nthr, o2.data(), true);
+        for (size_t k = 0; k < redo.size(); ++k) out[redo[k]] = o2[k];
+    }
+}
+
+void check_bb(const lgs_bb_params* p, const lgs_cost_ge_params* c)
+{
+    LGS_REQUIRE(p && c, "null argument");
+    LGS_REQUIRE(p->node_height_max >= 0 && p->node_height_max <= kBBMaxH, "node_height_max must be in [0, 12]");
+    LGS_REQUIRE(p->range_x >= 0 && p->range_y >= 0 && p->range_theta >= 0, "negative search range");
+    LGS_REQUIRE(c->kernel_size >= 0, "negative kernel size");
+}
+
+// PrecomputeGridMaps into n_maps x (H+1) scratch maps of S_BB2; returns the pointers
+std::vector<std::vector<const double*>> pyramids(lgs_ctx* ctx, const lgs_grid* const* maps, int n_maps, int Hm)
+{
+    size_t total = 0;
+    for (int m = 0; m < n_maps; ++m) total += (size_t)(Hm + 1) * align256(sizeof(double) * (size_t)maps[m]->w * maps[m]->h);
+    char* base = (char*)ctx->ensure(S_BB2, std::max<size_t>(total, 16));
+    std::vector<std::vector<const double*>> out((size_t)n_maps);
+    size_t off = 0;
+    for (int m = 0; m < n_maps; ++m) {
+        for (int h = 0; h <= Hm; ++h) {
+            double* d = (double*)(base + off);
+            off += align256(sizeof(double) * (size_t)maps[m]->w * maps[m]->h);
+            launch_precompute(ctx, maps[m], 1 << h, d, nullptr);
+            out[m].push_back(d);
+        }
+    }
+    return out;
+}
+
+}  // namespace
+
+extern "C" int lgs_grid_precompute_pyramid(lgs_ctx* ctx, const lgs_grid* in, int node_height_max,
+                                           lgs_grid* const* pyramid)
+{
+    if (!ctx || !in || !pyramid || node_height_max < 0 || node_height_max > kBBMaxH) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        for (int h = 0; h <= node_height_max; ++h) {
+            LGS_REQUIRE(pyramid[h] && pyramid[h]->w == in->w && pyramid[h]->h == in->h,
+                        "pyramid grids must have the input's size");
+            launch_precompute(ctx, in, 1 << h, pyramid[h]->d, nullptr);
+        }
+        ctx->sync();
+    });
+}
+
+extern "C" int lgs_bb_optimize_pose_batch(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* const* pyramid,
+                                          const lgs_bb_params* params, const lgs_cost_ge_params* cost,
+                                          const lgs_scan* const* scans, const lgs_pose2d* initial, int n,
+                                          double nthr, lgs_rtcsm_summary* out)
+{
+    if (!ctx || !grid || !pyramid || !scans || !initial || !out || n < 0) return LGS_ERR_INVALID_ARG;
+    if (n == 0) return LGS_OK;
+    return guarded(ctx, [&] {
+        check_bb(params, cost);
+        std::vector<const double*> pyr;
+        for (int h = 0; h <= params->node_height_max; ++h) {
+            LGS_REQUIRE(pyramid[h] && pyramid[h]->w == grid->w && pyramid[h]->h == grid->h,
+                        "pyramid grids must have the map's size");
+            pyr.push_back(pyramid[h]->d);
+        }
+        std::vector<const double* const*> pp((size_t)n, pyr.data());
+        std::vector<const lgs_grid*> grids((size_t)n, grid);
+        std::vector<lgs_scan*> sc((size_t)n);
+        for (int j = 0; j < n; ++j) {
+            LGS_REQUIRE(scans[j] && scans[j]->n >= 1, "empty scan");
+            sc[j] = const_cast<lgs_scan*>(scans[j]);
+        }
+        for (int j0 = 0; j0 < n; j0 += 64) {
+            const int m = std::min(64, n - j0);
+            run_bb(ctx, params, cost, grids.data() + j0, pp.data() + j0, sc.data() + j0, initial + j0, m, nthr,
+                   out + j0);
+        }
+    });
+}
+
+extern "C" int lgs_bb_optimize_pose_query(lgs_ctx* ctx, const lgs_grid* grid, const lgs_bb_params* params,
+                                          const lgs_cost_ge_params* cost, const lgs_scan* scan,
+                                          lgs_pose2d initial, lgs_rtcsm_summary* out)
+{
+    if (!ctx || !grid || !scan || !out) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        check_bb(params, cost);
+        LGS_REQUIRE(scan->n >= 1, "empty scan");
+        auto pyr = pyramids(ctx, &grid, 1, params->node_height_max);   // ComputeCoarserMaps (:157-165)
+        const double* const* pp = pyr[0].data();
+        lgs_scan* s = const_cast<lgs_scan*>(scan);
+        run_bb(ctx, params, cost, &grid, &pp, &s, &initial, 1, DBL_MIN, out);
+    });
+}
+
+extern "C" int lgs_loop_detect_bb(lgs_ctx* ctx, const lgs_bb_params* params, const lgs_cost_ge_params* cost,
+                                  double score_threshold, const lgs_loop_query* queries, int num_queries,
+                                  const lgs_loop_candidate* candidates, int num_candidates,
+                                  lgs_loop_result* results)
+{
+    if (!ctx || !params || !cost || (num_queries > 0 && !queries) || num_queries < 0 || num_candidates < 0 ||
+        (num_candidates > 0 && (!candidates || !results)))
+        return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        check_bb(params, cost);
+        LGS_REQUIRE(score_threshold > 0.0 && score_threshold <= 1.0, "score threshold must be in (0, 1] (:18-19)");
+        int covered = 0;
+        for (int q = 0; q < num_queries; ++q) {
+            const lgs_loop_query& Q = queries[q];
+            LGS_REQUIRE(Q.map, "loop query without a local map");
+            LGS_REQUIRE(Q.first_candidate == covered && Q.num_candidates >= 0 &&
+                            Q.first_candidate + Q.num_candidates <= num_candidates,
+                        "loop queries must cover the candidates contiguously and in order");
+            covered += Q.num_candidates;
+            for (int j = 0; j < Q.num_candidates; ++j)
+                LGS_REQUIRE(candidates[Q.first_candidate + j].scan, "loop candidate without a scan");
+        }
+        LGS_REQUIRE(covered == num_candidates, "loop queries must cover every candidate");
+        // batches of whole queries, at most ~64 candidates: each query's
+        // pyramid once per batch (LocalMapInfo caches it, :45-55)
+        for (int q0 = 0; q0 < num_queries;) {
+            int q1 = q0, m = 0;
+            while (q1 < num_queries && (m == 0 || m + queries[q1].num_candidates <= 64)) m += queries[q1++].num_candidates;
+            std::vector<const lgs_grid*> qmaps;
+            for (int q = q0; q < q1; ++q) qmaps.push_back(queries[q].map);
+            auto pyr = pyramids(ctx, qmaps.data(), (int)qmaps.size(), params->node_height_max);
+            std::vector<const lgs_grid*> grids;
+            std::vector<const double* const*> pp;
+            std::vector<lgs_scan*> sc;
+            std::vector<lgs_pose2d> poses;
+            std::vector<int> cand, qof;
+            for (int q = q0; q < q1; ++q)
+                for (int j = 0; j < queries[q].num_candidates; ++j) {
+                    const lgs_loop_candidate& c = candidates[queries[q].first_candidate + j];
+                    grids.push_back(queries[q].map);
+                    pp.push_back(pyr[(size_t)(q - q0)].data());
+                    sc.push_back(const_cast<lgs_scan*>(c.scan));
+                    poses.push_back(c.node_pose);
+                    cand.push_back(queries[q].first_candidate + j);
+                    qof.push_back(q);
+                }
+            std::vector<lgs_rtcsm_summary> sums(cand.size());
+            if (!cand.empty())
+                run_bb(ctx, params, cost, grids.data(), pp.data(), sc.data(), poses.data(), (int)cand.size(),
+                       score_threshold, sums.data());
+            for (size_t k = 0; k < cand.size(); ++k) {
+                const lgs_loop_query& Q = queries[qof[k]];
+                lgs_loop_result& r = results[cand[k]];
+                std::memset(&r, 0, sizeof(r));
+                const lgs_rtcsm_summary& s = sums[k];
+                r.found = s.pose_found;   // FindCorrespondingPose (:99-117)
+                r.start_node_index = Q.local_map_node_index;
+                r.end_node_index = candidates[cand[k]].node_index;
+                r.start_node_pose = Q.local_map_node_pose;
+                r.estimated_pose = s.estimated_pose;
+                r.score = s.score_max;
+                r.normalized_cost = s.normalized_cost;
+                if (s.pose_found) r.relative_pose = inverse_compound(Q.local_map_node_pose, s.estimated_pose);
+                std::memcpy(r.covariance, s.covariance, sizeof(r.covariance));
+            }
+            q0 = q1;
+        }
+    });
+}

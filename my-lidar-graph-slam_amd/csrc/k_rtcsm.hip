@@ -2012,34 +2012,6 @@ inline int coarse_block(const RtcsmPlan& pl) { return std::min(1024, ((pl.P + 63
 
 inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// Host staging of one batch's descriptors: appended to a pinned buffer, then
-// one host-to-device copy into the S_UPLOAD slot (flush).  Offsets are
-// returned at append time; device addresses are base + offset after flush.
-struct Upload {
-    lgs_ctx* ctx;
-    std::vector<char> host;
-    char* dev = nullptr;
-    explicit Upload(lgs_ctx* c) : ctx(c) {}
-    template <class T>
-    size_t append(const T* p, size_t n)
-    {
-        const size_t off = align256(host.size());
-        host.resize(off + sizeof(T) * n);
-        std::memcpy(host.data() + off, p, sizeof(T) * n);
-        return off;
-    }
-    void flush()
-    {
-        const size_t b = std::max<size_t>(host.size(), 16);
-        char* pin = (char*)ctx->ensure_pinned_up(b);
-        std::memcpy(pin, host.data(), host.size());
-        dev = (char*)ctx->ensure(S_UPLOAD, b);
-        LGS_HIP_CHECK(hipMemcpyAsync(dev, pin, host.size(), hipMemcpyHostToDevice, ctx->stream));
-    }
-    template <class T>
-    const T* at(size_t off) const { return (const T*)(dev + off); }
-};
-
 // Shape of one batched launch sequence: every item shares the search
 // parameters; T and Nv (and K = T * P) differ per scan, so the launch grids
 // and dynamic LDS use the maxima.
@@ -2556,15 +2528,26 @@ bool check_projection_guards(lgs_ctx* ctx, const RtcsmPlan& pl, const lgs_scan* 
     return !patches.empty();
 }
 
+bool check_cost_guards_p7(lgs_ctx* ctx, const double P7[7][3], const CostPlan& cp, const lgs_scan* scan,
+                          const HostRecord& rec, std::vector<int4>& cpatch, bool& full);
+
 bool check_cost_guards(lgs_ctx* ctx, const RtcsmPlan& pl, const CostPlan& cp,
                        const lgs_scan* scan, const HostRecord& rec, std::vector<int4>& cpatch,
                        bool& full)
 {
+    double P7[7][3];
+    host_poses7(pl, rec.best, P7);
+    return check_cost_guards_p7(ctx, P7, cp, scan, rec, cpatch, full);
+}
+
+// Verify the guarded cost cells of the 7 poses P7 against glibc; true if the
+// costs must be re-evaluated (cpatch: (key, cells) pairs, or full = every row).
+bool check_cost_guards_p7(lgs_ctx* ctx, const double P7[7][3], const CostPlan& cp, const lgs_scan* scan,
+                          const HostRecord& rec, std::vector<int4>& cpatch, bool& full)
+{
     cpatch.clear();
     full = false;
     if (rec.cost_guard_count == 0) return false;
-    double P7[7][3];
-    host_poses7(pl, rec.best, P7);
     if (rec.cost_guard_count > ctx->guard_cap) {
         full = true;
         return true;
@@ -2828,6 +2811,107 @@ void run_chunked(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
 }
 
 }  // namespace
+
+namespace lgs {
+// CostGreedyEndpoint::Cost at the seven poses of ComputeGradient /
+// ComputeCovariance around each item's best sensor pose
+// (C/mapping/cost_function_greedy_endpoint.cpp:32-171), one k_cost launch for
+// all n items; then the summary fields every matcher derives from them
+// (:128-138 of the RTCSM matcher, :142-153 of the branch-and-bound one):
+// normalized cost, estimated pose, covariance.  Guarded cells are re-checked
+// with glibc and mismatching items re-evaluated with host cells.
+void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params* cost, lgs_scan* const* scans,
+                    const lgs_pose2d* best, int n, lgs_rtcsm_summary* out)
+{
+    if (n <= 0) return;
+    int Nmax = 1;
+    for (int j = 0; j < n; ++j) Nmax = std::max(Nmax, scans[j]->n);
+    const ItemLayout L = item_layout(1, 1, 1, 1, 1, 64, 1, Nmax);
+    char* ws = (char*)ctx->ensure(S_BATCH_WS, L.total * (size_t)n);
+    RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord) * (size_t)n);
+    RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned(sizeof(RtcsmRecord) * (size_t)n);
+    std::vector<MatchItem> items((size_t)n);
+    std::vector<double> P7((size_t)n * 21);
+    std::vector<int> gens((size_t)n);
+    for (int j = 0; j < n; ++j) {
+        MatchItem& it = items[j];
+        std::memset(&it, 0, sizeof(it));
+        bind_workspace(it, ws + L.total * (size_t)j, L, 1);
+        it.cp = make_cost_plan(grid, cost, scans[j]);
+        it.grid = grid->d;
+        it.ranges = scans[j]->d_ranges;
+        it.angles = scans[j]->d_angles;
+        it.rec = d_rec + j;
+        it.gen = gens[j] = ctx->generation = ctx->next_stamp();
+        // the poses of ComputeGradient (:119-136), as k_replay forms them
+        const double x = best[j].x, y = best[j].y, th = best[j].theta, dl = grid->res, da = 1e-2;
+        const double v[21] = { x, y, th, x + dl, y + 0.0, th + 0.0, x - dl, y - 0.0, th - 0.0,
+                               x + 0.0, y + dl, th + 0.0, x - 0.0, y - dl, th - 0.0,
+                               x + 0.0, y + 0.0, th + da, x - 0.0, y - 0.0, th - da };
+        std::memcpy(&P7[(size_t)j * 21], v, sizeof(v));
+    }
+    Upload up(ctx);
+    const size_t poff = up.append(P7.data(), P7.size());
+    const size_t ioff = up.append(items.data(), items.size());
+    char* dev = up.prepare();
+    for (int j = 0; j < n; ++j) up.host_at<MatchItem>(ioff)[j].poses7 = (double*)(dev + poff) + 21 * (size_t)j;
+    up.copy();
+    Items d_items = up.at<MatchItem>(ioff);
+    const int ks = cost->kernel_size;
+    hipLaunchKernelGGL(KCOST(ks), dim3(7, n), dim3(kCostThreads), 0, ctx->stream, d_items, ctx->guard_cap,
+                       ctx->guard_eps, ctx->inject_index ? 1 : 0, 0);
+    LGS_HIP_CHECK(hipGetLastError());
+    LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    for (int j = 0; j < n; ++j) {
+        HostRecord rec(h_rec[j], gens[j]);
+        double p7[7][3];
+        std::memcpy(p7, &P7[(size_t)j * 21], sizeof(p7));
+        std::vector<int4> cpatch;
+        bool full = false;
+        out[j].guard_hits += rec.cost_guard_count;
+        if (check_cost_guards_p7(ctx, p7, items[j].cp, scans[j], rec, cpatch, full)) {
+            const CostPlan& cp = items[j].cp;
+            if (full) {
+                cpatch.clear();
+                for (int pi = 0; pi < 7; ++pi)
+                    for (int b = 0; b < cp.N; ++b) {
+                        const double r = scans[j]->h_ranges[b];
+                        if (r >= cp.max_range || r <= cp.min_range) continue;
+                        int cells[4];
+                        host_cost_cells(cp, scans[j], p7[pi], b, cells);
+                        cpatch.push_back(make_int4(pi * cp.N + b, 0, 0, 0));
+                        cpatch.push_back(make_int4(cells[0], cells[1], cells[2], cells[3]));
+                    }
+            }
+            // single-item rerun reading the patched cells (mode 1)
+            const int np = (int)(cpatch.size() / 2);
+            int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * std::max<size_t>(cpatch.size(), 1));
+            LGS_HIP_CHECK(hipMemcpyAsync(dp, cpatch.data(), sizeof(int4) * cpatch.size(), hipMemcpyHostToDevice,
+                                         ctx->stream));
+            if (np) hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, ctx->stream,
+                                       items[j].cidx, dp, np);
+            hipLaunchKernelGGL(KCOST(ks), dim3(7, 1), dim3(kCostThreads), 0, ctx->stream, d_items + j,
+                               ctx->guard_cap, ctx->guard_eps, 0, 1);
+            LGS_HIP_CHECK(hipGetLastError());
+            LGS_HIP_CHECK(hipMemcpyAsync(&h_rec[j], d_rec + j, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
+                                         ctx->stream));
+            ctx->sync();
+            out[j].fixups = 1;
+        }
+        const double* c = h_rec[j].costs;
+        out[j].normalized_cost = c[0] / (double)scans[j]->n;
+        out[j].estimated_pose = move_backward(best[j], scans[j]->rel);
+        const double dl = grid->res, da = 1e-2;
+        const double g[3] = { 0.5 * (c[1] - c[2]) / dl, 0.5 * (c[3] - c[4]) / dl, 0.5 * (c[5] - c[6]) / da };
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) out[j].covariance[3 * a + b] = g[a] * g[b];
+        out[j].covariance[0] += 0.01;
+        out[j].covariance[4] += 0.01;
+        out[j].covariance[8] += 0.01;
+    }
+}
+}  // namespace lgs
 
 extern "C" int lgs_rtcsm_optimize_pose(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,
                                        const lgs_rtcsm_params* params,

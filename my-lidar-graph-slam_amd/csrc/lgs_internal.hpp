@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -68,6 +69,7 @@ enum Slot {
     S_UPLOAD,       // per-batch descriptors (MatchItem, PlaneJob, PrecompJob), one H2D copy
     S_BATCH_WS,     // per-item match workspaces of a batch (k_rtcsm.hip ItemLayout)
     S_NEGFLAG,      // int per coarse-map set: negative-cell stamp of its planes
+    S_BB0, S_BB1, S_BB2, S_BB3, S_BB4, S_BB5,   // branch-and-bound (k_bb.hip)
     S_NUM_SLOTS
 };
 
@@ -303,6 +305,48 @@ inline lgs_pose2d inverse_compound(lgs_pose2d s, lgs_pose2d e)
 }
 
 const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* scan, double scan_range_max, int* nv);
+
+// Host staging of one batch's descriptors: appended to a pinned buffer, then
+// one host-to-device copy into the S_UPLOAD slot (flush).  Offsets are
+// returned at append time; device addresses are base + offset after flush.
+struct Upload {
+    lgs_ctx* ctx;
+    std::vector<char> host;
+    char* dev = nullptr;
+    explicit Upload(lgs_ctx* c) : ctx(c) {}
+    template <class T>
+    size_t append(const T* p, size_t n)
+    {
+        const size_t off = (host.size() + 255) & ~(size_t)255;
+        host.resize(off + sizeof(T) * n);
+        std::memcpy(host.data() + off, p, sizeof(T) * n);
+        return off;
+    }
+    // prepare(): the device address of the staged bytes (so that staged
+    // descriptors can be patched to point into the upload itself), copy():
+    // the host-to-device copy; flush() = both.
+    char* prepare()
+    {
+        dev = (char*)ctx->ensure(S_UPLOAD, std::max<size_t>(host.size(), 16));
+        return dev;
+    }
+    void copy()
+    {
+        const size_t b = std::max<size_t>(host.size(), 16);
+        char* pin = (char*)ctx->ensure_pinned_up(b);
+        std::memcpy(pin, host.data(), host.size());
+        LGS_HIP_CHECK(hipMemcpyAsync(dev, pin, host.size(), hipMemcpyHostToDevice, ctx->stream));
+    }
+    void flush()
+    {
+        prepare();
+        copy();
+    }
+    template <class T>
+    T* host_at(size_t off) { return (T*)(host.data() + off); }
+    template <class T>
+    const T* at(size_t off) const { return (const T*)(dev + off); }
+};
 
 // C-ABI guard: run f, map exceptions to status codes + ctx->last_error.
 template <class F>

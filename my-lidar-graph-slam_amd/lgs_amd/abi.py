@@ -92,6 +92,14 @@ class RtcsmSummary(C.Structure):
     ]
 
 
+class BBParams(C.Structure):
+    """lgs_bb_params: ScanMatcherBranchBound ctor (nodeHeightMax, rangeX/Y/Theta,
+    scanRangeMax) + ScorePixelAccurate (usableRangeMin/Max)."""
+    _fields_ = [("node_height_max", C.c_int), ("range_x", C.c_double), ("range_y", C.c_double),
+                ("range_theta", C.c_double), ("scan_range_max", C.c_double),
+                ("score_usable_range_min", C.c_double), ("score_usable_range_max", C.c_double)]
+
+
 class BuilderParams(C.Structure):
     _fields_ = [("usable_range_min", C.c_double), ("usable_range_max", C.c_double),
                 ("prob_hit", C.c_double), ("prob_miss", C.c_double)]
@@ -195,6 +203,15 @@ _PROTOS = [
                                                C.POINTER(BuilderParams)]),
     ("lgs_map_download", C.c_int, [_P, _P, C.POINTER(C.c_double), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32)]),
+    ("lgs_grid_precompute_pyramid", C.c_int, [_P, _P, C.c_int, C.POINTER(_P)]),
+    ("lgs_bb_optimize_pose_batch", C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(BBParams), C.POINTER(CostGEParams),
+                                             C.POINTER(_P), C.POINTER(Pose2D), C.c_int, C.c_double,
+                                             C.POINTER(RtcsmSummary)]),
+    ("lgs_bb_optimize_pose_query", C.c_int, [_P, _P, C.POINTER(BBParams), C.POINTER(CostGEParams), _P, Pose2D,
+                                             C.POINTER(RtcsmSummary)]),
+    ("lgs_loop_detect_bb", C.c_int, [_P, C.POINTER(BBParams), C.POINTER(CostGEParams), C.c_double,
+                                     C.POINTER(LoopQuery), C.c_int, C.POINTER(LoopCandidate), C.c_int,
+                                     C.POINTER(LoopResult)]),
     ("lgs_loop_detect_rtcsm", C.c_int, [_P, C.POINTER(RtcsmParams), C.POINTER(CostGEParams), C.c_double,
                                         C.POINTER(LoopQuery), C.c_int, C.POINTER(LoopCandidate), C.c_int,
                                         C.POINTER(LoopResult)]),
@@ -382,6 +399,45 @@ class Context:
         out = (LoopResult * max(1, len(candidates)))()
         self.check(self.lib.lgs_loop_detect_rtcsm(self.h, C.byref(params), C.byref(cost), float(thr), qs,
                                                   len(queries), cs, len(candidates), out), "loop_detect_rtcsm")
+        return out
+
+    # ---- branch-and-bound matcher ----
+    def precompute_pyramid(self, src: "Grid", node_height_max: int):
+        """PrecomputeGridMaps: [window-max grid with window 2^h for h = 0..H]"""
+        out = [self.grid(src.w, src.hgt, src.min_x, src.min_y, src.res) for _ in range(node_height_max + 1)]
+        arr = (_P * len(out))(*[g.h for g in out])
+        self.check(self.lib.lgs_grid_precompute_pyramid(self.h, src.h, int(node_height_max), arr),
+                   "grid_precompute_pyramid")
+        return out
+
+    def bb_optimize_pose_batch(self, grid, pyramid, params: "BBParams", cost: CostGEParams, scans, inits,
+                               thr: float):
+        n = len(scans)
+        parr = (_P * len(pyramid))(*[g.h for g in pyramid])
+        sarr = (_P * n)(*[s.h for s in scans])
+        poses = (Pose2D * n)(*[Pose2D(*p) for p in inits])
+        out = (RtcsmSummary * max(1, n))()
+        self.check(self.lib.lgs_bb_optimize_pose_batch(self.h, grid.h, parr, C.byref(params), C.byref(cost), sarr,
+                                                       poses, n, float(thr), out), "bb_optimize_pose_batch")
+        return list(out)[:n]
+
+    def bb_optimize_pose_query(self, grid, params: "BBParams", cost: CostGEParams, scan, init) -> RtcsmSummary:
+        out = RtcsmSummary()
+        self.check(self.lib.lgs_bb_optimize_pose_query(self.h, grid.h, C.byref(params), C.byref(cost), scan.h,
+                                                       Pose2D(*init), C.byref(out)), "bb_optimize_pose_query")
+        return out
+
+    def loop_detect_bb(self, params: "BBParams", cost: CostGEParams, thr: float, queries, candidates):
+        """as loop_detect, with LoopDetectorBranchBound (the coarse entry of a query is ignored)"""
+        qs = (LoopQuery * max(1, len(queries)))()
+        for i, (m, c, pose, idx, first, cnt) in enumerate(queries):
+            qs[i] = LoopQuery(m.h, None, Pose2D(*pose), idx, first, cnt)
+        cs = (LoopCandidate * max(1, len(candidates)))()
+        for i, (s, pose, idx) in enumerate(candidates):
+            cs[i] = LoopCandidate(s.h, Pose2D(*pose), idx, 0)
+        out = (LoopResult * max(1, len(candidates)))()
+        self.check(self.lib.lgs_loop_detect_bb(self.h, C.byref(params), C.byref(cost), float(thr), qs,
+                                               len(queries), cs, len(candidates), out), "loop_detect_bb")
         return out
 
     # ---- Gauss-Newton refine (K4) ----

@@ -358,6 +358,165 @@ int orc_rtcsm_optimize_pose_query(const orc_grid* grid, const orc_rtcsm_params* 
     return rc;
 }
 
+/* ------------------------------------------------------------------ */
+/* branch-and-bound matcher                                             */
+/* ------------------------------------------------------------------ */
+double orc_pixel_accurate_score(const orc_grid* g, const orc_bb_params* p, const orc_scan* scan,
+                                orc_pose sp)
+{
+    /* C/mapping/score_function_pixel_accurate.cpp:19-77 */
+    double sumScore = 0.0;
+    const double minRange = std_max(p->score_usable_range_min, scan->min_range);
+    const double maxRange = std_min(p->score_usable_range_max, scan->max_range);
+    for (int i = 0; i < scan->n; ++i) {
+        const double scanRange = scan->ranges[i];
+        if (scanRange >= maxRange || scanRange <= minRange)
+            continue;
+        /* ScanData::HitPoint (H/sensor/sensor_data.hpp:162-173), cos/sin fused */
+        double sinT, cosT;
+        sincos(sp.theta + scan->angles[i], &sinT, &cosT);
+        const double hx = sp.x + scanRange * cosT;
+        const double hy = sp.y + scanRange * sinT;
+        int ix, iy;
+        world_to_cell(g->min_x, g->min_y, g->res, hx, hy, &ix, &iy);
+        const double v = grid_value(g, ix, iy);
+        if (v == 0.0)     /* unknown: skipped (:55-56) */
+            continue;
+        sumScore += v;
+    }
+    return sumScore;
+}
+
+void orc_precompute_grid_maps(const double* in, int w, int h, int node_height_max, double** maps)
+{
+    /* C/mapping/grid_map_builder.cpp:471-495: window 1, 2, 4, ..., 2^H */
+    for (int nodeHeight = 0, winSize = 1; nodeHeight <= node_height_max; ++nodeHeight, winSize <<= 1)
+        orc_precompute_grid_map(in, w, h, winSize, maps[nodeHeight]);
+}
+
+typedef struct { int x, y, t, h; } bb_node;
+
+int orc_bb_optimize_pose(const orc_grid* grid, const orc_grid* maps, const orc_bb_params* p,
+                         const orc_cost_ge* cost, const orc_scan* scan, orc_pose initial_pose,
+                         double normalized_score_threshold, orc_summary* out)
+{
+    memset(out, 0, sizeof(*out));
+    if (scan->n <= 0)
+        return 1;
+    /* :54-56 */
+    const orc_pose sensorPose = orc_compound(initial_pose, scan->rel_sensor_pose);
+    /* :59-62 ComputeSearchStep (:178-198), identical to the RTCSM one */
+    double stepX, stepY, stepTheta;
+    orc_rtcsm_search_step(grid->res, scan, p->scan_range_max, &stepX, &stepY, &stepTheta);
+    /* :65-70 */
+    const int winX = (int)ceil(0.5 * p->range_x / stepX);
+    const int winY = (int)ceil(0.5 * p->range_y / stepY);
+    const int winTheta = (int)ceil(0.5 * p->range_theta / stepTheta);
+    /* :73-78 */
+    const double scoreThreshold = normalized_score_threshold * (double)scan->n;
+    double scoreMax = scoreThreshold;
+    orc_pose bestSensorPose = sensorPose;
+    int best[3] = { 0, 0, 0 };
+    /* :81-88 stack of nodes covering the window (x outer, y, t inner) */
+    const int winSizeMax = 1 << p->node_height_max;
+    size_t cap = 1024, top = 0;
+    bb_node* st = (bb_node*)malloc(sizeof(bb_node) * cap);
+    for (int x = -winX; x <= winX; x += winSizeMax)
+        for (int y = -winY; y <= winY; y += winSizeMax)
+            for (int t = -winTheta; t <= winTheta; ++t) {
+                if (top == cap) {
+                    cap *= 2;
+                    st = (bb_node*)realloc(st, sizeof(bb_node) * cap);
+                }
+                st[top].x = x;
+                st[top].y = y;
+                st[top].t = t;
+                st[top].h = p->node_height_max;
+                ++top;
+            }
+    int64_t nodes = 0, accepted = 0;
+    /* :92-140 */
+    while (top > 0) {
+        const bb_node cur = st[top - 1];
+        orc_pose nodePose;
+        nodePose.x = sensorPose.x + cur.x * stepX;
+        nodePose.y = sensorPose.y + cur.y * stepY;
+        nodePose.theta = sensorPose.theta + cur.t * stepTheta;
+        const double score = orc_pixel_accurate_score(&maps[cur.h], p, scan, nodePose);
+        ++nodes;
+        if (score <= scoreMax) {   /* :105-109 */
+            --top;
+            continue;
+        }
+        if (cur.h == 0) {          /* :112-119 leaf */
+            --top;
+            bestSensorPose = nodePose;
+            scoreMax = score;
+            best[0] = cur.x;
+            best[1] = cur.y;
+            best[2] = cur.t;
+            ++accepted;
+        } else {                   /* :120-137 four children, pushed in this order */
+            const int h = cur.h - 1, ws = 1 << h;
+            --top;
+            if (top + 4 > cap) {
+                cap *= 2;
+                st = (bb_node*)realloc(st, sizeof(bb_node) * cap);
+            }
+            const bb_node c[4] = { { cur.x, cur.y, cur.t, h }, { cur.x + ws, cur.y, cur.t, h },
+                                   { cur.x, cur.y + ws, cur.t, h }, { cur.x + ws, cur.y + ws, cur.t, h } };
+            for (int k = 0; k < 4; ++k)
+                st[top++] = c[k];
+        }
+    }
+    free(st);
+    /* :142-153 */
+    const int poseFound = scoreMax > scoreThreshold;
+    const double costVal = orc_cost_ge_cost(grid, cost, scan, bestSensorPose);
+    out->normalized_cost = costVal / (double)scan->n;
+    out->estimated_pose = orc_move_backward(bestSensorPose, scan->rel_sensor_pose);
+    orc_cost_ge_covariance(grid, cost, scan, bestSensorPose, out->covariance);
+    out->pose_found = poseFound;
+    out->initial_pose = initial_pose;
+    out->score_max = scoreMax;
+    out->score_threshold = scoreThreshold;
+    out->best_win[0] = best[0];
+    out->best_win[1] = best[1];
+    out->best_win[2] = best[2];
+    out->win[0] = winX;
+    out->win[1] = winY;
+    out->win[2] = winTheta;
+    out->steps[0] = stepX;
+    out->steps[1] = stepY;
+    out->steps[2] = stepTheta;
+    out->sensor_pose = sensorPose;
+    out->best_sensor_pose = bestSensorPose;
+    out->coarse_evals = nodes;
+    out->fine_blocks = accepted;
+    return 0;
+}
+
+int orc_bb_optimize_pose_query(const orc_grid* grid, const orc_bb_params* p, const orc_cost_ge* cost,
+                               const orc_scan* scan, orc_pose initial_pose, orc_summary* out)
+{
+    /* :29-44: ComputeCoarserMaps (:157-165) then DBL_MIN */
+    const int H = p->node_height_max;
+    double** bufs = (double**)malloc(sizeof(double*) * (size_t)(H + 1));
+    orc_grid* maps = (orc_grid*)malloc(sizeof(orc_grid) * (size_t)(H + 1));
+    for (int h = 0; h <= H; ++h) {
+        bufs[h] = (double*)calloc((size_t)grid->w * (size_t)grid->h + 1, sizeof(double));
+        maps[h] = *grid;
+        maps[h].cells = bufs[h];
+    }
+    orc_precompute_grid_maps(grid->cells, grid->w, grid->h, H, bufs);
+    const int rc = orc_bb_optimize_pose(grid, maps, p, cost, scan, initial_pose, DBL_MIN, out);
+    for (int h = 0; h <= H; ++h)
+        free(bufs[h]);
+    free(bufs);
+    free(maps);
+    return rc;
+}
+
 int orc_rtcsm_dense_scores(const orc_grid* grid, const orc_grid* coarse,
                            const orc_rtcsm_params* p, const orc_scan* scan,
                            orc_pose initial_pose, double* coarse_scores,

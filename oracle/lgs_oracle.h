@@ -173,6 +173,34 @@ int orc_construct_map_from_scans(orc_map* m, const orc_node* nodes, int n_nodes,
 int orc_integrate_scan(orc_map* m, orc_pose robot_pose, const orc_scan* scan,
                        const orc_builder_params* bp);
 
+/* ---- branch-and-bound matcher (C/mapping/scan_matcher_branch_bound.cpp,
+ *      C/mapping/score_function_pixel_accurate.cpp, pyramid
+ *      C/mapping/grid_map_builder.cpp:471-495) ---- */
+typedef struct {
+    int node_height_max;
+    double range_x, range_y, range_theta;
+    double scan_range_max;
+    double score_usable_range_min, score_usable_range_max;   /* ScorePixelAccurate */
+} orc_bb_params;
+
+/* ScorePixelAccurate::Score (:19-77): sum of the map values at the hit cells
+ * of the beams with range in (max(umin, scan.min), min(umax, scan.max)) */
+double orc_pixel_accurate_score(const orc_grid* g, const orc_bb_params* p, const orc_scan* scan,
+                                orc_pose sensor_pose);
+/* PrecomputeGridMaps (:471-495): maps[h] = window-max map with window 2^h,
+ * h = 0..node_height_max; maps must hold node_height_max+1 buffers of w*h */
+void orc_precompute_grid_maps(const double* in, int w, int h, int node_height_max, double** maps);
+/* ScanMatcherBranchBound::OptimizePose(gridMap, precompMaps, scan, pose, thr)
+ * (:47-154): LIFO depth-first branch and bound.  maps[h] (h = 0..H) share the
+ * grid's geometry.  out->coarse_evals = nodes scored, out->fine_blocks =
+ * leaves accepted; best_win = the best node's (x, y, t). */
+int orc_bb_optimize_pose(const orc_grid* grid, const orc_grid* maps, const orc_bb_params* p,
+                         const orc_cost_ge* cost, const orc_scan* scan, orc_pose initial_pose,
+                         double normalized_score_threshold, orc_summary* out);
+/* OptimizePose(query) (:29-44): pyramid, then DBL_MIN threshold */
+int orc_bb_optimize_pose_query(const orc_grid* grid, const orc_bb_params* p, const orc_cost_ge* cost,
+                               const orc_scan* scan, orc_pose initial_pose, orc_summary* out);
+
 /* ---- Gauss-Newton refine (C/mapping/scan_matcher_linear_solver.cpp, cost_function_square_error.cpp) ---- */
 typedef struct {
     int num_iterations_max;

@@ -195,6 +195,64 @@ def rtcsm_search(grid, coarse, min_x, min_y, res, ranges, angles, sensor, low_re
     return dict(found=smax > thr, score=smax, best=best, win=[wx, wy, wt], step_t=step_t)
 
 
+def pixel_accurate_score(grid, min_x, min_y, res, ranges, angles, pose, umin, umax, smin, smax):
+    """C/mapping/score_function_pixel_accurate.cpp:19-77"""
+    min_range = umin if smin < umin else smin      # std::max
+    max_range = smax if smax < umax else umax      # std::min
+    s = 0.0
+    for r, a in zip(ranges, angles):
+        if r >= max_range or r <= min_range:
+            continue
+        sn, cs = sincos(pose[2] + a)
+        hx = pose[0] + r * cs
+        hy = pose[1] + r * sn
+        v = gval(grid, int(math.floor((hx - min_x) / res)), int(math.floor((hy - min_y) / res)))
+        if v == 0.0:
+            continue
+        s += v
+    return s
+
+
+def bb_search(grid, min_x, min_y, res, ranges, angles, sensor, H, rx, ry, rt, rmax, nthr, umin, umax):
+    """C/mapping/scan_matcher_branch_bound.cpp:47-140 (search part) with the
+    PrecomputeGridMaps pyramid (C/mapping/grid_map_builder.cpp:471-495)."""
+    pyr = [precompute(grid, 1 << h) for h in range(H + 1)]
+    mr = ranges[0]
+    for r in ranges[1:]:
+        if mr < r:
+            mr = r
+    max_range = rmax if rmax < mr else mr
+    theta = res / max_range
+    step_t = math.acos(1.0 - 0.5 * theta * theta)
+    wx = int(math.ceil(0.5 * rx / res))
+    wy = int(math.ceil(0.5 * ry / res))
+    wt = int(math.ceil(0.5 * rt / step_t))
+    thr = nthr * len(ranges)
+    smax = thr
+    best = [0, 0, 0]
+    stack = []
+    ws_max = 1 << H
+    for x in range(-wx, wx + 1, ws_max):
+        for y in range(-wy, wy + 1, ws_max):
+            for t in range(-wt, wt + 1):
+                stack.append((x, y, t, H))
+    visited = 0
+    while stack:
+        x, y, t, h = stack.pop()
+        pose = (sensor[0] + x * res, sensor[1] + y * res, sensor[2] + t * step_t)
+        sc = pixel_accurate_score(pyr[h], min_x, min_y, res, ranges, angles, pose, umin, umax, 0.0, 30.0)
+        visited += 1
+        if sc <= smax:
+            continue
+        if h == 0:
+            smax = sc
+            best = [x, y, t]
+            continue
+        w = 1 << (h - 1)
+        stack += [(x, y, t, h - 1), (x + w, y, t, h - 1), (x, y + w, t, h - 1), (x + w, y + w, t, h - 1)]
+    return dict(found=smax > thr, score=smax, best=best, win=[wx, wy, wt], step_t=step_t, visited=visited)
+
+
 def main():
     rnd = random.Random(1234)
     kat = {"_note": __doc__.strip().splitlines()[0]}
@@ -289,6 +347,29 @@ def main():
                    "res": res, "range": [0.3, 0.2, 0.4], "scan_range_max": 20.0,
                    "nthr": 2.2250738585072014e-308 if case != 2 else 0.3, **out})
     kat["rtcsm_py"] = rs
+
+    # tiny branch-and-bound searches (pure-Python LIFO search)
+    bb = []
+    for case in range(5):
+        w = h = 20
+        grid = [[0.0] * w for _ in range(h)]
+        for _ in range(60):
+            grid[rnd.randrange(h)][rnd.randrange(w)] = rnd.choice([0.6, 0.8, 0.999, 0.45, 0.01])
+        if case == 3:
+            grid = [[0.5] * w for _ in range(h)]        # ties everywhere
+        n = 16
+        ranges = [rnd.uniform(0.1, 0.45) for _ in range(n)]
+        if case == 4:
+            ranges[2] = 0.005                            # below the usable range: skipped
+        angles = [-math.pi + i * (2 * math.pi / n) for i in range(n)]
+        sensor = (0.52, 0.49, 0.2 * case)
+        H = 2 if case != 1 else 3
+        nthr = 2.2250738585072014e-308 if case != 2 else 0.4
+        out = bb_search(grid, 0.0, 0.0, 0.05, ranges, angles, sensor, H, 0.3, 0.2, 0.3, 20.0, nthr, 0.01, 20.0)
+        bb.append({"grid": grid, "node_height_max": H, "ranges": ranges, "angles": angles, "sensor": sensor,
+                   "res": 0.05, "range": [0.3, 0.2, 0.3], "scan_range_max": 20.0, "nthr": nthr,
+                   "usable": [0.01, 20.0], **out})
+    kat["bb_py"] = bb
 
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump(kat, f, indent=None, separators=(",", ":"))

@@ -71,6 +71,12 @@ class LinsolveParams(C.Structure):
                 ("cost_usable_range_min", C.c_double), ("cost_usable_range_max", C.c_double)]
 
 
+class BBParams(C.Structure):
+    _fields_ = [("node_height_max", C.c_int), ("range_x", C.c_double), ("range_y", C.c_double),
+                ("range_theta", C.c_double), ("scan_range_max", C.c_double),
+                ("score_usable_range_min", C.c_double), ("score_usable_range_max", C.c_double)]
+
+
 _D = C.POINTER(C.c_double)
 _lib = None
 
@@ -134,6 +140,16 @@ def lib():
         L.orc_linsolve_optimize_pose.argtypes = [C.POINTER(Grid), C.POINTER(LinsolveParams), C.POINTER(Scan),
                                                  Pose, C.POINTER(Summary), C.POINTER(Pose)]
         L.orc_solve3_colpiv_qr.argtypes = [_D, _D, _D]
+        L.orc_pixel_accurate_score.restype = C.c_double
+        L.orc_pixel_accurate_score.argtypes = [C.POINTER(Grid), C.POINTER(BBParams), C.POINTER(Scan), Pose]
+        L.orc_precompute_grid_maps.argtypes = [_D, C.c_int, C.c_int, C.c_int, C.POINTER(_D)]
+        L.orc_bb_optimize_pose.restype = C.c_int
+        L.orc_bb_optimize_pose.argtypes = [C.POINTER(Grid), C.POINTER(Grid), C.POINTER(BBParams),
+                                           C.POINTER(CostGE), C.POINTER(Scan), Pose, C.c_double,
+                                           C.POINTER(Summary)]
+        L.orc_bb_optimize_pose_query.restype = C.c_int
+        L.orc_bb_optimize_pose_query.argtypes = [C.POINTER(Grid), C.POINTER(BBParams), C.POINTER(CostGE),
+                                                 C.POINTER(Scan), Pose, C.POINTER(Summary)]
         _lib = L
     return _lib
 
@@ -164,6 +180,16 @@ def precompute(cells, win):
     out = np.zeros_like(c)
     lib().orc_precompute_grid_map(dp(c), w, h, int(win), dp(out))
     return out
+
+
+def precompute_pyramid(cells, node_height_max):
+    """PrecomputeGridMaps: [window-max map with window 2^h for h = 0..H]"""
+    c = np.ascontiguousarray(cells, dtype=np.float64)
+    h, w = c.shape
+    outs = [np.zeros_like(c) for _ in range(node_height_max + 1)]
+    ptrs = (_D * len(outs))(*[dp(o) for o in outs])
+    lib().orc_precompute_grid_maps(dp(c), w, h, int(node_height_max), ptrs)
+    return outs
 
 
 def bresenham(x0, y0, x1, y1):

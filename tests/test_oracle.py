@@ -76,6 +76,39 @@ def test_rtcsm_search_kat(i):
     assert out.steps[2] == c["step_t"]
 
 
+@pytest.mark.parametrize("i", range(len(KAT["bb_py"])))
+def test_bb_search_kat(i):
+    """ScanMatcherBranchBound: best node, score and the number of nodes the
+    LIFO search visits, against the pure-Python restatement."""
+    c = KAT["bb_py"][i]
+    grid = np.array(c["grid"])
+    H = c["node_height_max"]
+    pyr = ob.precompute_pyramid(grid, H)
+    keep = [ob.OGrid(m, 0.0, 0.0, c["res"]) for m in pyr]
+    maps = (ob.Grid * (H + 1))(*[k.g for k in keep])
+    g = ob.OGrid(grid, 0.0, 0.0, c["res"])
+    sc = ob.OScan(c["ranges"], c["angles"])
+    prm = ob.BBParams(H, *c["range"], c["scan_range_max"], *c["usable"])
+    out = ob.Summary()
+    cost = ob.CostGE(0.01, 20.0, 0.075, 0.1, 1, 0.05, 1.0)
+    ob.lib().orc_bb_optimize_pose(C.byref(g.g), maps, C.byref(prm), C.byref(cost), C.byref(sc.s),
+                                  ob.Pose(*c["sensor"]), c["nthr"], C.byref(out))
+    assert bool(out.pose_found) == c["found"]
+    assert out.score_max == c["score"]
+    assert list(out.best_win) == c["best"]
+    assert list(out.win) == c["win"]
+    assert out.steps[2] == c["step_t"]
+    assert out.coarse_evals == c["visited"]
+
+
+def test_pyramid_is_precompute_per_height():
+    rng = np.random.default_rng(3)
+    grid = rng.choice([0.0, 0.0, 0.3, 0.8], size=(37, 50)) * rng.uniform(0.5, 1.0, size=(37, 50))
+    pyr = ob.precompute_pyramid(grid, 5)
+    for h, m in enumerate(pyr):
+        assert np.array_equal(m, ob.precompute(grid, 1 << h))
+
+
 def _small_scene(seed, n=64, w=80):
     rng = np.random.default_rng(seed)
     grid = np.zeros((w, w))
