@@ -41,6 +41,7 @@ from lgs_amd import abi, scene  # noqa: E402
 METRIC = "scans/sec + p50 scan-match ms, 1081-beam vs 1000×1000@5cm grid, 1/2/4/8 GPU"
 PARAMS = (5, 4.0, 4.0, 1.0471976, 20.0)          # LowRes, rangeX, rangeY, rangeTheta, ScanRangeMax
 LOOP_PARAMS = (5, 5.0, 5.0, 1.0, 20.0)           # launcher_settings_default.json:107-113
+BB_PARAMS = (6, 2.0, 2.0, 1.0, 20.0, 0.01, 20.0)  # LoopDetectorBranchBound (launcher_settings_default.json:128-146)
 COST = (0.01, 20.0, 0.075, 0.1, 1, 0.05, 1.0)    # launcher-built CostGreedyEndpoint members
 LINSOLVE = (50, 0.0, 0.01, 20.0, 1e-3, 1e-3, 0.01, 20.0)   # config 3
 BUILDER = (0.01, 20.0, 0.6, 0.45)                # GridMapBuilder usable range, pHit, pMiss
@@ -52,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default: 200 (match/refine), 4 (loop), 500 (stream)")
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--workload", default="match", choices=["match", "refine", "loop", "stream"])
+    ap.add_argument("--workload", default="match", choices=["match", "refine", "loop", "loop_bb", "stream"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--coarse-planes", type=int, default=1, help="A/B: 1 phase-plane coarse layout, 0 plain")
@@ -76,8 +77,8 @@ def parse():
                     help="HIP-event timing inside the timed region: the roofline kernel only (default), "
                          "every kernel, or none (A/B of the event overhead)")
     a = ap.parse_args()
-    d_steps = dict(match=200, refine=200, loop=4, stream=500)[a.workload]
-    d_warm = dict(match=10, refine=5, loop=1, stream=10)[a.workload]
+    d_steps = dict(match=200, refine=200, loop=4, loop_bb=2, stream=500)[a.workload]
+    d_warm = dict(match=10, refine=5, loop=1, loop_bb=1, stream=10)[a.workload]
     a.steps = d_steps if a.steps is None else a.steps
     a.warmup = d_warm if a.warmup is None else a.warmup
     return a
@@ -433,7 +434,10 @@ def run_refine(args, D, ctx):
 
 # ---------------------------------------------------------------------- loop
 def run_loop(args, D, ctx):
+    """config 5; --workload loop_bb: the same batch through the reference's
+    default loop detector, LoopDetectorBranchBound."""
     from lgs_amd import loopbatch
+    bb = args.workload == "loop_bb"
     world = scene.make_world()
     bp = abi.BuilderParams(*BUILDER)
 
@@ -445,12 +449,16 @@ def run_loop(args, D, ctx):
         return cells, g["min_x"], g["min_y"], 0.05
 
     maps, cands = scene.loop_problem(world, build, n_maps=32, nodes_per_map=16, n_beams=1081, seed=5,
-                                     perturb=(2.0, 0.4), arc_scans=10)
-    P, cost = abi.RtcsmParams(*LOOP_PARAMS), abi.CostGEParams(*COST)
-    fn = loopbatch.hip_detect_fn(ctx, maps, cands, P, cost, 0.6)
+                                     perturb=(0.8, 0.3) if bb else (2.0, 0.4), arc_scans=10)
+    cost = abi.CostGEParams(*COST)
+    if bb:
+        fn = loopbatch.hip_detect_fn_bb(ctx, maps, cands, abi.BBParams(*BB_PARAMS), cost, 0.6)
+    else:
+        fn = loopbatch.hip_detect_fn(ctx, maps, cands, abi.RtcsmParams(*LOOP_PARAMS), cost, 0.6)
     for _ in range(args.warmup):
         loopbatch.run_sharded(cands, fn, D.rank, D.world, D.d, D.device())
-    set_timed_events(ctx, args, "k_coarse")
+    dominant = "k_bb_score" if bb else "k_coarse"
+    set_timed_events(ctx, args, dominant)
     D.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -464,8 +472,24 @@ def run_loop(args, D, ctx):
         ob = oracle_lib()
         grids = {}
         prm, oc = ob.RtcsmParams(*LOOP_PARAMS), ob.CostGE(*COST)
+        bprm = ob.BBParams(*BB_PARAMS)
+
+        def one_bb(i):
+            c = cands[i]
+            if c.query not in grids:   # the pyramid once per map (LocalMapInfo caches it)
+                m = maps[c.query]
+                keep = [ob.OGrid(x, m.min_x, m.min_y, 0.05) for x in ob.precompute_pyramid(m.cells, BB_PARAMS[0])]
+                grids[c.query] = (ob.OGrid(m.cells, m.min_x, m.min_y, 0.05), keep,
+                                  (ob.Grid * len(keep))(*[k.g for k in keep]))
+            g, _, arr = grids[c.query]
+            s = ob.Summary()
+            ob.lib().orc_bb_optimize_pose(C.byref(g.g), arr, C.byref(bprm), C.byref(oc),
+                                          C.byref(ob.OScan(c.ranges, c.angles).s), ob.Pose(*c.pose), 0.6,
+                                          C.byref(s))
 
         def one(i):
+            if bb:
+                return one_bb(i)
             c = cands[i]
             if c.query not in grids:
                 m = maps[c.query]
@@ -478,19 +502,23 @@ def run_loop(args, D, ctx):
                                              C.byref(s))
         rate, times = timed(args.cpu_seconds, range(0, len(cands), 37), one)
         cpu = dict(value=round(rate, 4), unit="candidates/s", cores=1, kind="port",
-                   sample=f"{len(times)} config-5 candidates through the oracle's OptimizePose "
-                          f"(coarse map precomputed per map, as LocalMapInfo caches it; 1 thread), "
-                          f"p50 {1e3 * np.median(times):.1f} ms")
+                   sample=f"{len(times)} config-5 candidates through the oracle's "
+                          f"{'ScanMatcherBranchBound' if bb else 'RTCSM'} OptimizePose "
+                          f"({'pyramid' if bb else 'coarse map'} precomputed per map, as LocalMapInfo caches it; "
+                          f"1 thread), p50 {1e3 * np.median(times):.1f} ms")
     value = args.steps * len(cands) / elapsed
     line = dict(
-        metric="loop-closure candidates/sec, 512 candidates (32 maps x 16 nodes), 1081 beams, +-2.5 m/+-0.5 rad",
+        metric=("loop-closure candidates/sec, LoopDetectorBranchBound, 512 candidates (32 maps x 16 nodes), "
+                "1081 beams, +-1 m/+-0.5 rad, NodeHeightMax 6" if bb else
+                "loop-closure candidates/sec, 512 candidates (32 maps x 16 nodes), 1081 beams, +-2.5 m/+-0.5 rad"),
         value=round(value, 2), unit="candidates/s", n_gpus=D.world, steps=args.steps, warmup=args.warmup,
         ms_per_step=round(1e3 * elapsed / args.steps, 4), higher_is_better=True, scaling="strong",
         vs_baseline=None, dtype="f64", data="synthetic: 32 device-built local maps (600x600 @ 5 cm), 512 scans",
-        config=dict(workload="config5: LoopDetectorRealTimeCorrelative::Detect batch", candidates=len(cands),
+        config=dict(workload=("config5 (f1): LoopDetectorBranchBound::Detect batch" if bb else
+                              "config5: LoopDetectorRealTimeCorrelative::Detect batch"), candidates=len(cands),
                     found=found, parallelism=f"candidates sharded in contiguous blocks over {D.world} ranks + "
                                              "RCCL all-gather of 176-B result records"),
-        roofline=roofline_from(stats, "k_coarse", args.pmc), cpu_baseline=cpu)
+        roofline=roofline_from(stats, dominant, args.pmc), cpu_baseline=cpu)
     return line, stats, value
 
 
@@ -553,7 +581,8 @@ def main():
     args = parse()
     D = Dist()
     ctx = abi.Context(D.local)
-    line, stats, _ = dict(match=run_match, refine=run_refine, loop=run_loop, stream=run_stream)[args.workload](
+    line, stats, _ = dict(match=run_match, refine=run_refine, loop=run_loop, loop_bb=run_loop,
+                          stream=run_stream)[args.workload](
         args, D, ctx)
     line["kernels"] = {k: dict(launches=v["launches"], avg_ms=round(v["total_ms"] / max(1, v["launches"]), 5))
                        for k, v in stats.items()}

@@ -35,6 +35,10 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstring>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
 #include <unordered_map>
 
 using namespace lgs;
@@ -76,13 +80,6 @@ struct BBGuard {
     int ix, iy, pad2, pad3;       // device cell
 };
 
-__device__ __forceinline__ bool near_cell_boundary(double q, double eps)
-{
-    const double f = q - floor(q);
-    const double e = eps + fabs(q) * 1e-13;
-    return f < e || f > 1.0 - e;
-}
-
 __global__ __launch_bounds__(256) void k_bb_trig(const BBItem* __restrict__ items)
 {
     const BBItem& it = items[blockIdx.z];
@@ -100,7 +97,11 @@ __global__ __launch_bounds__(256) void k_bb_trig(const BBItem* __restrict__ item
     it.rs[(size_t)t * it.Nv + v] = r * sn;
 }
 
-constexpr int kBBPipe = 8;
+constexpr int kBBPipe = 16;
+// The cell index uses (hit - min) * (1 / res) instead of the reference's
+// division: the product is within 1 ulp of the quotient (~1e-13 cells at
+// map sizes here), far inside guard_eps, so every cell whose floor could
+// differ from the reference's is guarded and re-checked on the host.
 __global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ items, const int4* __restrict__ nodes,
                                                   int n, int level_id, double* __restrict__ scores,
                                                   BBGuard* __restrict__ guards, int* __restrict__ nguard,
@@ -118,37 +119,44 @@ __global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ ite
     const double* __restrict__ rc = it.rc + (size_t)(nd.w + it.win_t) * Nv;
     const double* __restrict__ rs = it.rs + (size_t)(nd.w + it.win_t) * Nv;
     const double* __restrict__ map = it.maps[h];
-    const double minx = it.min_x, miny = it.min_y, res = it.res;
+    const double minx = it.min_x, miny = it.min_y, inv = 1.0 / it.res;
     double sum = 0.0;
     for (int v0 = 0; v0 < Nv; v0 += kBBPipe) {
-        double val[kBBPipe];
+        double cx[kBBPipe], cy[kBBPipe], val[kBBPipe];
+#pragma unroll
+        for (int j = 0; j < kBBPipe; ++j) {   // independent loads first
+            const int v = min(v0 + j, Nv - 1);
+            cx[j] = rc[v];
+            cy[j] = rs[v];
+        }
 #pragma unroll
         for (int j = 0; j < kBBPipe; ++j) {
             const int v = v0 + j;
-            val[j] = 0.0;
-            if (v < Nv) {
-                // WorldCoordinateToGridCellIndex of HitPoint (H/grid_map/grid_map.hpp:779-790)
-                const double qx = (nx + rc[v] - minx) / res;
-                const double qy = (ny + rs[v] - miny) / res;
-                int ix = (int)floor(qx), iy = (int)floor(qy);
-                if (near_cell_boundary(qx, guard_eps) || near_cell_boundary(qy, guard_eps)) {
-                    ix += inject;
-                    const int slot = atomicAdd(nguard, 1);
-                    if (slot < guard_cap) {
-                        BBGuard g;
-                        g.level = level_id;
-                        g.node = i;
-                        g.v = v;
-                        g.ix = ix;
-                        g.iy = iy;
-                        g.pad = g.pad2 = g.pad3 = 0;
-                        guards[slot] = g;
-                    }
+            // WorldCoordinateToGridCellIndex of HitPoint (H/grid_map/grid_map.hpp:779-790)
+            const double qx = (nx + cx[j] - minx) * inv;
+            const double qy = (ny + cy[j] - miny) * inv;
+            const double fx = floor(qx), fy = floor(qy);
+            int ix = (int)fx, iy = (int)fy;
+            const double ex = guard_eps + fabs(qx) * 1e-13, ey = guard_eps + fabs(qy) * 1e-13;
+            const double rx = qx - fx, ry = qy - fy;
+            if (v < Nv && (rx < ex || rx > 1.0 - ex || ry < ey || ry > 1.0 - ey)) {
+                ix += inject;
+                const int slot = atomicAdd(nguard, 1);
+                if (slot < guard_cap) {
+                    BBGuard g;
+                    g.level = level_id;
+                    g.node = i;
+                    g.v = v;
+                    g.ix = ix;
+                    g.iy = iy;
+                    g.pad = g.pad2 = g.pad3 = 0;
+                    guards[slot] = g;
                 }
-                // GridMap::Value(idx, unknown): 0.0 outside; unknown cells
-                // (0.0) are skipped by the reference (:55-56), adding 0.0 is the same
-                if (((unsigned)ix < (unsigned)W) & ((unsigned)iy < (unsigned)H)) val[j] = map[(size_t)iy * W + ix];
             }
+            // GridMap::Value(idx, unknown): 0.0 outside; unknown cells (0.0)
+            // are skipped by the reference (:55-56), adding 0.0 is the same
+            const bool inb = (v < Nv) & ((unsigned)ix < (unsigned)W) & ((unsigned)iy < (unsigned)H);
+            val[j] = inb ? map[(size_t)iy * W + ix] : 0.0;
         }
 #pragma unroll
         for (int j = 0; j < kBBPipe; ++j) sum += val[j];
@@ -324,6 +332,16 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
 {
     LGS_HIP_CHECK(hipSetDevice(ctx->device));
     std::memset(out, 0, sizeof(lgs_rtcsm_summary) * (size_t)n);
+    // LGS_BB_TIMING=1: per-phase host wall times on stderr (diagnostics)
+    static const bool timing = std::getenv("LGS_BB_TIMING") != nullptr;
+    auto t_prev = std::chrono::steady_clock::now();
+    double t_ms[6] = {};
+    auto lap = [&](int k) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        t_ms[k] += std::chrono::duration<double, std::milli>(now - t_prev).count();
+        t_prev = now;
+    };
     const int Hm = p->node_height_max;
     std::vector<BBHost> plans;
     plans.reserve((size_t)n);
@@ -420,6 +438,7 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         if (ok) items[j].thr_exp = std::max(plans[j].thr0, pscores[(size_t)j * (Hm + 1) + Hm]);
     }
     LGS_HIP_CHECK(hipMemsetAsync(d_counts, 0, 256, ctx->stream));
+    lap(0);
 
     // pass 2: level by level, every node the search can visit
     std::vector<BBLevel> levels((size_t)Hm + 1);   // index = Hm - h
@@ -440,28 +459,34 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         int4* cur_nodes = (int4*)ctx->ensure(S_BB1, sizeof(int4) * (size_t)cur_n);
         LGS_HIP_CHECK(hipMemcpyAsync(cur_nodes, up.at<int4>(toff), sizeof(int4) * (size_t)cur_n,
                                      hipMemcpyDeviceToDevice, ctx->stream));
-        std::vector<void*> keep;   // per-level device buffers (freed at the end)
         for (int h = Hm; h >= 0; --h) {
             BBLevel& L = levels[(size_t)(Hm - h)];
             L.n = cur_n;
             L.d_nodes = cur_nodes;
-            LGS_HIP_CHECK(hipMalloc(&L.d_scores, sizeof(double) * std::max(cur_n, 1)));
-            keep.push_back(L.d_scores);
+            // per-level buffers: aux 2l = scores, 2l + 1 = the next level's nodes
+            L.d_scores = (double*)ctx->ensure_aux(2 * (Hm - h), sizeof(double) * (size_t)std::max(cur_n, 1));
             if (cur_n > 0) {
+                // algorithmic bytes: 8 B per (node, valid beam) map lookup
+                double lookups = 0.0;
+                for (int j = 0; j < n; ++j) lookups += (double)plans[j].Nv;
+                const int tok = ctx->timing_begin(K_BB_SCORE, 8.0 * lookups / n * cur_n);
                 hipLaunchKernelGGL(k_bb_score, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items,
                                    cur_nodes, cur_n, Hm - h, L.d_scores, d_guards, d_counts, ctx->guard_cap,
                                    ctx->guard_eps, ctx->inject_index ? 1 : 0);
+                ctx->timing_end(tok);
                 LGS_HIP_CHECK(hipGetLastError());
             }
             if (h == 0 || cur_n == 0) break;
             const int cap = 4 * cur_n;
-            int4* next = nullptr;
-            LGS_HIP_CHECK(hipMalloc(&next, sizeof(int4) * (size_t)cap));
-            keep.push_back(next);
+            int4* next = (int4*)ctx->ensure_aux(2 * (Hm - h) + 1, sizeof(int4) * (size_t)cap);
             LGS_HIP_CHECK(hipMemsetAsync(d_counts + 1, 0, 2 * sizeof(int), ctx->stream));
-            hipLaunchKernelGGL(k_bb_expand, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items, cur_nodes,
-                               L.d_scores, cur_n, next, d_counts + 1, cap, d_counts + 2);
-            LGS_HIP_CHECK(hipGetLastError());
+            {
+                const int tok = ctx->timing_begin(K_BB_EXPAND, 0.0);
+                hipLaunchKernelGGL(k_bb_expand, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items,
+                                   cur_nodes, L.d_scores, cur_n, next, d_counts + 1, cap, d_counts + 2);
+                ctx->timing_end(tok);
+                LGS_HIP_CHECK(hipGetLastError());
+            }
             int cnt[2] = { 0, 0 };
             LGS_HIP_CHECK(hipMemcpyAsync(cnt, d_counts + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
             ctx->sync();
@@ -485,8 +510,8 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         std::vector<BBGuard> guards((size_t)std::min(ng, ctx->guard_cap));
         if (!guards.empty())
             LGS_HIP_CHECK(hipMemcpy(guards.data(), d_guards, sizeof(BBGuard) * guards.size(), hipMemcpyDeviceToHost));
-        for (void* q : keep) LGS_HIP_CHECK(hipFree(q));
         for (auto& L : levels) L.d_nodes = nullptr, L.d_scores = nullptr;
+        if (ctx->profile) ctx->harvest();
 
         // guarded cells: exact glibc cells; nodes with any differing cell are
         // re-scored from host cells (or, past guard_cap records, every node
@@ -548,22 +573,28 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         }
     }
 
+    lap(1);
     // host replay of the reference's search (:81-140) over the scored nodes
-    std::vector<std::unordered_map<uint64_t, double>> table((size_t)n);
+    // (candidates are independent: their tables and searches run on a few
+    // host threads; each thread owns whole candidates)
+    std::vector<std::vector<std::pair<int, int>>> bucket((size_t)n);   // (level id, node index)
+    for (int l = 0; l <= Hm; ++l) {
+        const BBLevel& L = levels[(size_t)l];
+        for (int i = 0; i < L.n; ++i) bucket[(size_t)(L.nodes[(size_t)i].x >> 4)].push_back({ l, i });
+    }
     std::vector<int64_t> scored((size_t)n, 0);
-    for (auto& L : levels)
-        for (int i = 0; i < L.n; ++i) ++scored[(size_t)(L.nodes[(size_t)i].x >> 4)];
-    for (int j = 0; j < n; ++j) table[j].reserve((size_t)scored[j] * 2 + 16);
-    for (auto& L : levels)
-        for (int i = 0; i < L.n; ++i) {
-            const int4 nd = L.nodes[(size_t)i];
-            table[(size_t)(nd.x >> 4)].emplace(node_key(nd.x & 15, nd.y, nd.z, nd.w), L.scores[(size_t)i]);
-        }
+    for (int j = 0; j < n; ++j) scored[(size_t)j] = (int64_t)bucket[(size_t)j].size();
     std::vector<lgs_pose2d> best((size_t)n);
     std::vector<char> failed((size_t)n, 0);
     struct SNode { int x, y, t, h; };
-    std::vector<SNode> st;
-    for (int j = 0; j < n; ++j) {
+    auto replay = [&](int j) {
+        std::unordered_map<uint64_t, double> tab;
+        tab.reserve(bucket[(size_t)j].size() * 2 + 16);
+        for (const auto& li : bucket[(size_t)j]) {
+            const int4 nd = levels[(size_t)li.first].nodes[(size_t)li.second];
+            tab.emplace(node_key(nd.x & 15, nd.y, nd.z, nd.w), levels[(size_t)li.first].scores[(size_t)li.second]);
+        }
+        std::vector<SNode> st;
         const BBHost& b = plans[j];
         double scoreMax = b.thr0;
         lgs_pose2d bestPose = b.sensor;
@@ -573,14 +604,12 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         for (int x : b.top_x)
             for (int y : b.top_y)
                 for (int t = -b.win_t; t <= b.win_t; ++t) st.push_back({ x, y, t, Hm });
-        const auto& tab = table[(size_t)j];
         while (!st.empty()) {
             const SNode cur = st.back();
             st.pop_back();
             const auto f = tab.find(node_key(cur.h, cur.x, cur.y, cur.t));
             if (f == tab.end()) {
-                LGS_REQUIRE(!no_path, "branch-and-bound: the search reached a node the device did not score");
-                failed[(size_t)j] = 1;   // rerun with the thr0 superset
+                failed[(size_t)j] = no_path ? 2 : 1;   // 1: rerun with the thr0 superset
                 break;
             }
             const double score = f->second;
@@ -623,7 +652,20 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         o.coarse_blocks = scored[(size_t)j];
         o.fine_blocks = visited;
         best[j] = bestPose;
+    };
+    {
+        const int nt = std::max(1, std::min(n, std::min(16, (int)std::thread::hardware_concurrency())));
+        std::vector<std::thread> th;
+        for (int w = 1; w < nt; ++w)
+            th.emplace_back([&, w] {
+                for (int j = w; j < n; j += nt) replay(j);
+            });
+        for (int j = 0; j < n; j += nt) replay(j);
+        for (auto& t : th) t.join();
     }
+    for (int j = 0; j < n; ++j)
+        LGS_REQUIRE(failed[(size_t)j] != 2, "branch-and-bound: the search reached a node the device did not score");
+    lap(2);
     // cost and covariance at the best poses (:146-153), grouped by map
     std::vector<int> order, redo;
     for (int j = 0; j < n; ++j) (failed[(size_t)j] ? redo : order).push_back(j);
@@ -642,6 +684,13 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         cost_summaries(ctx, grids[order[k0]], cost, sc.data(), bp.data(), (int)sc.size(), tmp.data());
         for (size_t k = k0; k < k1; ++k) out[order[k]] = tmp[k - k0];
         k0 = k1;
+    }
+    lap(3);
+    if (timing) {
+        int64_t nodes = 0;
+        for (int j = 0; j < n; ++j) nodes += out[j].coarse_blocks;
+        std::fprintf(stderr, "bb n=%d nodes=%lld: trig+path %.2f ms, levels %.2f ms, replay %.2f ms, cost %.2f ms\n",
+                     n, (long long)nodes, t_ms[0], t_ms[1], t_ms[2], t_ms[3]);
     }
     if (!redo.empty()) {
         std::vector<const lgs_grid*> g2;

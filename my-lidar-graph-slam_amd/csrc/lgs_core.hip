@@ -36,6 +36,26 @@ void* lgs_ctx::ensure(int slot, size_t bytes)
     return p;
 }
 
+void* lgs_ctx::ensure_aux(int i, size_t bytes)
+{
+    if ((int)aux.size() <= i) {
+        aux.resize((size_t)i + 1, nullptr);
+        aux_bytes.resize((size_t)i + 1, 0);
+    }
+    if (bytes == 0) bytes = 16;
+    if (aux_bytes[i] >= bytes) return aux[i];
+    if (aux[i]) {
+        LGS_HIP_CHECK(hipStreamSynchronize(stream));
+        LGS_HIP_CHECK(hipFree(aux[i]));
+        aux[i] = nullptr;
+        aux_bytes[i] = 0;
+    }
+    const size_t want = bytes + bytes / 2;
+    if (hipMalloc(&aux[i], want) != hipSuccess) throw Error(LGS_ERR_OOM, "hipMalloc failed for an auxiliary buffer");
+    aux_bytes[i] = want;
+    return aux[i];
+}
+
 void* lgs_ctx::ensure_pinned(size_t bytes)
 {
     if (pinned_bytes >= bytes) return pinned;
@@ -70,7 +90,7 @@ namespace lgs {
 const char* const kKernelNames[K_NUM_KERNELS] = { "k_project", "k_coarse", "k_seed", "k_select",
                                                   "k_fine", "k_replay", "k_cost", "k_precompute",
                                                   "k_linsolve", "k_ray_emit", "k_ray_apply",
-                                                  "k_super", "k_super_planes" };
+                                                  "k_super", "k_super_planes", "k_bb_score", "k_bb_expand" };
 }
 
 int lgs_ctx::next_stamp()
@@ -145,6 +165,10 @@ void lgs_ctx::release()
     }
     if (pinned) hipHostFree(pinned);
     pinned = nullptr;
+    for (void* q : aux)
+        if (q) hipFree(q);
+    aux.clear();
+    aux_bytes.clear();
     if (zero) hipFree(zero);
     zero = nullptr;
     for (auto& p : pending) {
@@ -543,22 +567,36 @@ __global__ __launch_bounds__(256) void k_precompute_jobs(const PrecompJob* __res
     precompute_tile(j.in, j.out, j.W, j.H, w, j.pg, bx, by);
 }
 
-// Fallback for large windows: direct 2-D window per output.
-__global__ void k_precompute_direct(const double* __restrict__ in, double* __restrict__ out,
-                                    int W, int H, int w)
+// Large windows (> 32, e.g. the branch-and-bound pyramid's 64): the two
+// separable passes as their own launches through a scratch map, each output
+// the max of its w window (SlidingWindowMaxRow, then SlidingWindowMaxCol;
+// win_start gives the tail rule, reads past the end are 0).
+__global__ void k_precompute_sep_y(const double* __restrict__ in, double* __restrict__ out, int W, int H, int w)
 {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= W) return;
-    const int sx = win_start(x, W, w), sy = win_start(y, H, w);
+    const int s = win_start(y, H, w);
     double m = 0.0;
-    bool first = true;
-    for (int yy = sy; yy < sy + w; ++yy)
-        for (int xx = sx; xx < sx + w; ++xx) {
-            const double v = (xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;
-            m = first ? v : dmax(m, v);
-            first = false;
-        }
+    for (int j = 0; j < w; ++j) {
+        const double v = (s + j < H) ? in[(size_t)(s + j) * W + x] : 0.0;
+        m = (j == 0) ? v : dmax(m, v);
+    }
+    out[(size_t)y * W + x] = m;
+}
+
+__global__ void k_precompute_sep_x(const double* __restrict__ in, double* __restrict__ out, int W, int H, int w)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    const int s = win_start(x, W, w);
+    const double* row = in + (size_t)y * W;
+    double m = 0.0;
+    for (int j = 0; j < w; ++j) {
+        const double v = (s + j < W) ? row[s + j] : 0.0;
+        m = (j == 0) ? v : dmax(m, v);
+    }
     out[(size_t)y * W + x] = m;
 }
 
@@ -586,9 +624,11 @@ void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, c
         hipLaunchKernelGGL(k_precompute_tiled, grid, dim3(256), lds, ctx->stream, in->d, out,
                            in->w, in->h, win, pg);
     } else {
+        LGS_REQUIRE(!planes, "phase-plane precompute: window must be <= 32");
+        double* tmp = (double*)ctx->ensure(S_PRECOMP_TMP, sizeof(double) * (size_t)in->w * in->h);
         dim3 grid((in->w + 255) / 256, in->h);
-        hipLaunchKernelGGL(k_precompute_direct, grid, dim3(256), 0, ctx->stream, in->d, out,
-                           in->w, in->h, win);
+        hipLaunchKernelGGL(k_precompute_sep_y, grid, dim3(256), 0, ctx->stream, in->d, tmp, in->w, in->h, win);
+        hipLaunchKernelGGL(k_precompute_sep_x, grid, dim3(256), 0, ctx->stream, tmp, out, in->w, in->h, win);
     }
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());

@@ -70,6 +70,7 @@ enum Slot {
     S_BATCH_WS,     // per-item match workspaces of a batch (k_rtcsm.hip ItemLayout)
     S_NEGFLAG,      // int per coarse-map set: negative-cell stamp of its planes
     S_BB0, S_BB1, S_BB2, S_BB3, S_BB4, S_BB5,   // branch-and-bound (k_bb.hip)
+    S_PRECOMP_TMP,  // double [W*H]: pass-1 result of the large-window precompute
     S_NUM_SLOTS
 };
 
@@ -171,7 +172,8 @@ struct CostPlan {
 
 namespace lgs {
 enum KernelId { K_PROJECT = 0, K_COARSE, K_SEED, K_SELECT, K_FINE, K_REPLAY, K_COST, K_PRECOMPUTE,
-                K_LINSOLVE, K_RAY_EMIT, K_RAY_APPLY, K_SUPER, K_SUPER_PLANES, K_NUM_KERNELS };
+                K_LINSOLVE, K_RAY_EMIT, K_RAY_APPLY, K_SUPER, K_SUPER_PLANES, K_BB_SCORE, K_BB_EXPAND,
+                K_NUM_KERNELS };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 struct PendingTiming {
     int kernel;
@@ -240,6 +242,11 @@ struct lgs_ctx {
     void sync();
 
     void* ensure(int slot, size_t bytes);
+    // grow-only auxiliary device buffers indexed by number (per-level
+    // branch-and-bound lists; freed in release())
+    std::vector<void*> aux;
+    std::vector<size_t> aux_bytes;
+    void* ensure_aux(int i, size_t bytes);
     void* ensure_pinned(size_t bytes);
     void* ensure_pinned_up(size_t bytes);
     void release();

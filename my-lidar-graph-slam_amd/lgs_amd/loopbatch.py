@@ -100,6 +100,32 @@ def hip_detect_fn(ctx: "abi.Context", maps: Sequence[LocalMap], cands: Sequence[
     return fn
 
 
+def hip_detect_fn_bb(ctx: "abi.Context", maps: Sequence[LocalMap], cands: Sequence[Candidate],
+                     params: "abi.BBParams", cost: "abi.CostGEParams", threshold: float
+                     ) -> Callable[[List[Tuple[int, int, int]], int, int], np.ndarray]:
+    """As hip_detect_fn with LoopDetectorBranchBound (C/mapping/loop_detector_branch_bound.cpp:26-117):
+    lgs_loop_detect_bb builds each query's map pyramid itself."""
+    grids = {}
+    scans = {}
+
+    def fn(subq, lo, hi):
+        queries, cl = [], []
+        for q, first, count in subq:
+            if q not in grids:
+                m = maps[q]
+                grids[q] = ctx.grid_from_array(m.cells, m.min_x, m.min_y, m.res)
+            queries.append((grids[q], None, maps[q].node_pose, maps[q].node_index, first, count))
+        for i in range(lo, hi):
+            c = cands[i]
+            if i not in scans:
+                scans[i] = ctx.scan(c.ranges, c.angles)
+            cl.append((scans[i], c.pose, c.node_index))
+        out = ctx.loop_detect_bb(params, cost, threshold, queries, cl)
+        return np.frombuffer(bytes(out), dtype=np.uint8)[: (hi - lo) * RECORD_BYTES].reshape(hi - lo, RECORD_BYTES)
+
+    return fn
+
+
 def run_sharded(cands: Sequence[Candidate], detect_fn, rank: int = 0, world: int = 1, dist=None,
                 device=None) -> np.ndarray:
     """All candidates' records (uint8 [n, 176]) in candidate order, on every rank."""
