@@ -176,6 +176,57 @@ DeviceGrid ScanMatcherRealTimeCorrelativeHip::ComputeCoarserMap(const DeviceGrid
     return out;
 }
 
+// ------------------------------------------------ ScanMatcherBranchBoundHip
+ScanMatcherBranchBoundHip::ScanMatcherBranchBoundHip(DevicePtr dev, const ScorePixelAccurateParams& sf,
+                                                     const CostGreedyEndpointParams& c, int nodeHeightMax,
+                                                     double rangeX, double rangeY, double rangeTheta,
+                                                     double scanRangeMax)
+    : mDev(std::move(dev))
+{
+    mParams = { nodeHeightMax, rangeX, rangeY, rangeTheta, scanRangeMax, sf.mUsableRangeMin, sf.mUsableRangeMax };
+    mCost = { c.mUsableRangeMin, c.mUsableRangeMax, c.mHitAndMissedDist, c.mOccupancyThreshold,
+              c.mKernelSize, c.mScalingFactor, c.mStandardDeviation };
+}
+
+ScanMatchingSummary ScanMatcherBranchBoundHip::OptimizePose(const ScanMatchingQuery& q)
+{
+    mDev->Check(lgs_bb_optimize_pose_query(mDev->Handle(), q.mGridMap->Handle(), &mParams, &mCost,
+                                           q.mScanData->Handle(), to_c(q.mInitialPose), &mLast),
+                "lgs_bb_optimize_pose_query");
+    return summary_of(mLast);
+}
+
+ScanMatchingSummary ScanMatcherBranchBoundHip::OptimizePose(const DeviceGrid& gridMap,
+                                                            const std::vector<DeviceGridPtr>& precompMaps,
+                                                            const ScanDataPtr& scanData,
+                                                            const RobotPose2D<double>& initialPose, double thr) const
+{
+    std::vector<const lgs_grid*> pyr;
+    for (const auto& m : precompMaps) pyr.push_back(m->Handle());
+    if ((int)pyr.size() != mParams.node_height_max + 1)
+        throw Error(LGS_ERR_INVALID_ARG, "ScanMatcherBranchBoundHip: one precomputed map per node height needed");
+    const lgs_scan* s = scanData->Handle();
+    const lgs_pose2d p = to_c(initialPose);
+    mDev->Check(lgs_bb_optimize_pose_batch(mDev->Handle(), gridMap.Handle(), pyr.data(), &mParams, &mCost, &s, &p,
+                                           1, thr, &mLast),
+                "lgs_bb_optimize_pose_batch");
+    return summary_of(mLast);
+}
+
+std::vector<DeviceGridPtr> ScanMatcherBranchBoundHip::ComputeCoarserMaps(const DeviceGrid& g) const
+{
+    std::vector<DeviceGridPtr> out;
+    std::vector<lgs_grid*> hs;
+    for (int h = 0; h <= mParams.node_height_max; ++h) {
+        out.push_back(std::make_shared<DeviceGrid>(mDev, g.NumCellsX(), g.NumCellsY(), g.MinX(), g.MinY(),
+                                                   g.Resolution()));
+        hs.push_back(const_cast<lgs_grid*>(out.back()->Handle()));
+    }
+    mDev->Check(lgs_grid_precompute_pyramid(mDev->Handle(), g.Handle(), mParams.node_height_max, hs.data()),
+                "lgs_grid_precompute_pyramid");
+    return out;
+}
+
 // ------------------------------------------------ ScanMatcherLinearSolverHip
 ScanMatcherLinearSolverHip::ScanMatcherLinearSolverHip(DevicePtr dev, int numOfIterationsMax,
                                                        double convergenceThreshold, double usableRangeMin,
@@ -310,6 +361,49 @@ void LoopDetectorRealTimeCorrelativeHip::Detect(std::vector<LoopDetectionQuery>&
                "lgs_loop_detect_rtcsm");
     for (const auto& r : out) {
         if (!r.found) continue;   // the reference appends only detected loops, in order (:77-88)
+        LoopDetectionResult o;
+        o.mRelativePose = from_c(r.relative_pose);
+        o.mStartNodePose = from_c(r.start_node_pose);
+        o.mStartNodeIdx = r.start_node_index;
+        o.mEndNodeIdx = r.end_node_index;
+        o.mEstimatedCovMat = cov_of(r.covariance);
+        results.push_back(o);
+    }
+}
+
+// ------------------------------------------------ LoopDetectorBranchBoundHip
+LoopDetectorBranchBoundHip::LoopDetectorBranchBoundHip(std::shared_ptr<ScanMatcherBranchBoundHip> m, double thr)
+    : mScanMatcher(std::move(m)), mScoreThreshold(thr)
+{
+    if (!(thr > 0.0 && thr <= 1.0))   // the reference asserts this (:18-19)
+        throw Error(LGS_ERR_INVALID_ARG, "LoopDetectorBranchBoundHip: score threshold must be in (0, 1]");
+}
+
+void LoopDetectorBranchBoundHip::Detect(std::vector<LoopDetectionQuery>& queries,
+                                        std::vector<LoopDetectionResult>& results)
+{
+    results.clear();
+    if (queries.empty()) return;
+    const DevicePtr& dev = mScanMatcher->Dev();
+    std::vector<lgs_loop_query> qs;
+    std::vector<lgs_loop_candidate> cs;
+    for (auto& q : queries) {
+        lgs_loop_query c{};
+        c.map = q.mLocalMap->Handle();   // lgs_loop_detect_bb builds the pyramid (:45-55)
+        c.local_map_node_pose = to_c(q.mLocalMapNodePose);
+        c.local_map_node_index = q.mLocalMapNodeIndex;
+        c.first_candidate = (int)cs.size();
+        c.num_candidates = (int)q.mPoseGraphNodes.size();
+        qs.push_back(c);
+        for (const auto& n : q.mPoseGraphNodes)
+            cs.push_back(lgs_loop_candidate{ n.mScanData->Handle(), to_c(n.mPose), n.mIndex, 0 });
+    }
+    std::vector<lgs_loop_result> out(cs.size());
+    dev->Check(lgs_loop_detect_bb(dev->Handle(), &mScanMatcher->Params(), &mScanMatcher->Cost(), mScoreThreshold,
+                                  qs.data(), (int)qs.size(), cs.data(), (int)cs.size(), out.data()),
+               "lgs_loop_detect_bb");
+    for (const auto& r : out) {
+        if (!r.found) continue;   // only detected loops, in query -> node order (:61-84)
         LoopDetectionResult o;
         o.mRelativePose = from_c(r.relative_pose);
         o.mStartNodePose = from_c(r.start_node_pose);

@@ -197,6 +197,39 @@ private:
     mutable lgs_rtcsm_summary mLast{};
 };
 
+// ScorePixelAccurate (C/mapping/score_function_pixel_accurate.cpp:9-17)
+struct ScorePixelAccurateParams {
+    double mUsableRangeMin = 0.01, mUsableRangeMax = 20.0;
+};
+
+// ScanMatcherBranchBound (C/mapping/scan_matcher_branch_bound.cpp:8-200): the
+// device scores every node the reference's search can visit, the host
+// replays the search.
+class ScanMatcherBranchBoundHip final : public ScanMatcher {
+public:
+    ScanMatcherBranchBoundHip(DevicePtr dev, const ScorePixelAccurateParams& scoreFunc,
+                              const CostGreedyEndpointParams& costFunc, int nodeHeightMax, double rangeX,
+                              double rangeY, double rangeTheta, double scanRangeMax);
+    // OptimizePose(query): pyramid + search with threshold DBL_MIN (:29-44)
+    ScanMatchingSummary OptimizePose(const ScanMatchingQuery& queryInfo) override;
+    // the const overload used by the loop detector (:47-154)
+    ScanMatchingSummary OptimizePose(const DeviceGrid& gridMap, const std::vector<DeviceGridPtr>& precompMaps,
+                                     const ScanDataPtr& scanData, const RobotPose2D<double>& initialPose,
+                                     double normalizedScoreThreshold) const;
+    // ComputeCoarserMaps (:157-165): heights 0..NodeHeightMax
+    std::vector<DeviceGridPtr> ComputeCoarserMaps(const DeviceGrid& gridMap) const;
+    const lgs_rtcsm_summary& LastSummary() const { return mLast; }
+    const lgs_bb_params& Params() const { return mParams; }
+    const lgs_cost_ge_params& Cost() const { return mCost; }
+    const DevicePtr& Dev() const { return mDev; }
+
+private:
+    DevicePtr mDev;
+    lgs_bb_params mParams{};
+    lgs_cost_ge_params mCost{};
+    mutable lgs_rtcsm_summary mLast{};
+};
+
 // ScanMatcherLinearSolver (C/mapping/scan_matcher_linear_solver.cpp:38-148)
 // with CostSquareError(usableRangeMin, usableRangeMax).
 class ScanMatcherLinearSolverHip final : public ScanMatcher {
@@ -275,6 +308,19 @@ public:
 
 private:
     std::shared_ptr<ScanMatcherRealTimeCorrelativeHip> mScanMatcher;
+    double mScoreThreshold;
+};
+
+// LoopDetectorBranchBound (C/mapping/loop_detector_branch_bound.cpp:10-117):
+// pyramids computed per query (LocalMapInfo caches them, :45-55), every node
+// matched, found ones appended in query -> node order.
+class LoopDetectorBranchBoundHip {
+public:
+    LoopDetectorBranchBoundHip(std::shared_ptr<ScanMatcherBranchBoundHip> scanMatcher, double scoreThreshold);
+    void Detect(std::vector<LoopDetectionQuery>& queries, std::vector<LoopDetectionResult>& results);
+
+private:
+    std::shared_ptr<ScanMatcherBranchBoundHip> mScanMatcher;
     double mScoreThreshold;
 };
 

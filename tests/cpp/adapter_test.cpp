@@ -265,6 +265,67 @@ int main()
                                       " of 8 found)");
     }
 
+    // ---- ScanMatcherBranchBoundHip (query + the loop overload) and LoopDetectorBranchBoundHip
+    {
+        const ScorePixelAccurateParams sp;   // 0.01 / 20.0
+        auto bbm = std::make_shared<ScanMatcherBranchBoundHip>(dev, sp, cost, 3, 0.6, 0.6, 0.3, 20.0);
+        const orc_bb_params obb = { 3, 0.6, 0.6, 0.3, 20.0, sp.mUsableRangeMin, sp.mUsableRangeMax };
+        const RobotPose2D<double> truth(0.1, -0.05, 0.4);
+        auto sc = std::make_shared<ScanData>(dev, ang, ray_cast(world, truth.mX, truth.mY, truth.mTheta, ang));
+        const RobotPose2D<double> init(0.15, -0.02, 0.43);
+        const ScanMatchingQuery q(lgrid, sc, init);
+        const ScanMatchingSummary s = bbm->OptimizePose(q);
+        const orc_scan os = oscan(*sc);
+        orc_summary o{};
+        orc_bb_optimize_pose_query(&og, &obb, &oc, &os, { init.mX, init.mY, init.mTheta }, &o);
+        check(s.mPoseFound == (o.pose_found != 0) && same_pose(s.mEstimatedPose, o.estimated_pose) &&
+                  bbm->LastSummary().score_max == o.score_max && bbm->LastSummary().fine_blocks == o.coarse_evals,
+              "ScanMatcherBranchBound::OptimizePose(query) == oracle (pose, score, nodes visited)");
+        // the loop overload with the matcher's own pyramid, threshold 0.35
+        const auto pyr = bbm->ComputeCoarserMaps(*lgrid);
+        const ScanMatchingSummary s2 = bbm->OptimizePose(*lgrid, pyr, sc, init, 0.35);
+        std::vector<std::vector<double>> bufs(4, std::vector<double>((std::size_t)ol.w * ol.h));
+        std::vector<orc_grid> maps;
+        for (int h = 0; h <= 3; ++h) {
+            orc_precompute_grid_map(ol.cells, ol.w, ol.h, 1 << h, bufs[h].data());
+            maps.push_back({ bufs[h].data(), ol.w, ol.h, ol.min_x, ol.min_y, ol.res });
+        }
+        orc_summary o2{};
+        orc_bb_optimize_pose(&og, maps.data(), &obb, &oc, &os, { init.mX, init.mY, init.mTheta }, 0.35, &o2);
+        check(s2.mPoseFound == (o2.pose_found != 0) && same_pose(s2.mEstimatedPose, o2.estimated_pose) &&
+                  bbm->LastSummary().fine_blocks == o2.coarse_evals,
+              "ScanMatcherBranchBound::OptimizePose(map, pyramid, .., 0.35) == oracle");
+        LoopDetectorBranchBoundHip det(bbm, 0.35);
+        std::vector<LoopDetectionQuery> qs(1);
+        qs[0].mLocalMap = lgrid;
+        qs[0].mLocalMapNodePose = { 0.05, 0.0, 0.1 };
+        qs[0].mLocalMapNodeIndex = 3;
+        for (int j = 0; j < 3; ++j) {
+            LoopCandidateNode nd;
+            const RobotPose2D<double> tr(0.1 * j - 0.1, 0.05 * j, 0.2 * j);
+            nd.mScanData = std::make_shared<ScanData>(dev, ang, ray_cast(world, tr.mX, tr.mY, tr.mTheta, ang));
+            nd.mPose = { tr.mX + jit(rng), tr.mY + jit(rng), tr.mTheta + jit(rng) };
+            nd.mIndex = 200 + j;
+            qs[0].mPoseGraphNodes.push_back(nd);
+        }
+        std::vector<LoopDetectionResult> res;
+        det.Detect(qs, res);
+        std::vector<std::pair<int, orc_pose>> expect;
+        for (const auto& n : qs[0].mPoseGraphNodes) {
+            const orc_scan ns = oscan(*n.mScanData);
+            orc_summary o3{};
+            orc_bb_optimize_pose(&og, maps.data(), &obb, &oc, &ns, { n.mPose.mX, n.mPose.mY, n.mPose.mTheta }, 0.35,
+                                 &o3);
+            if (!o3.pose_found) continue;
+            expect.push_back({ n.mIndex, orc_inverse_compound({ 0.05, 0.0, 0.1 }, o3.estimated_pose) });
+        }
+        bool ok = res.size() == expect.size();
+        for (std::size_t i = 0; ok && i < res.size(); ++i)
+            ok = res[i].mEndNodeIdx == expect[i].first && same_pose(res[i].mRelativePose, expect[i].second);
+        check(ok && !res.empty(), "LoopDetectorBranchBound::Detect == oracle (" + std::to_string(res.size()) +
+                                      " of 3 found)");
+    }
+
     // ---- error behaviour: status -> exception
     {
         bool threw = false;
