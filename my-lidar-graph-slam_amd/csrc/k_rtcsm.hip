@@ -637,12 +637,22 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
     float* __restrict__ out = S + plane * pl.pstride4;
     const int tid = threadIdx.x;
     bool neg = false;
-    for (int k = tid; k < TH * TW; k += blockDim.x) {
+    // all of a thread's loads issued before its LDS stores (a load-store loop
+    // would wait one memory latency per element)
+    constexpr int kTileLoads = (TH * TW + 255) / 256;
+    double cv[kTileLoads];
+#pragma unroll
+    for (int j = 0; j < kTileLoads; ++j) {
+        const int k = tid + j * 256;
         const int yy = k / TW, xx = k % TW;
         const int x = x0 + xx, y = y0 + yy;
-        const double c = (x < Wqp && y < Hqp) ? base[(long long)y * Wqp + x] : 0.0;   // 0 past the plane
-        neg |= c < 0.0;
-        tile[yy][xx] = c;
+        cv[j] = (k < TH * TW && x < Wqp && y < Hqp) ? base[(long long)y * Wqp + x] : 0.0;   // 0 past the plane
+    }
+#pragma unroll
+    for (int j = 0; j < kTileLoads; ++j) {
+        const int k = tid + j * 256;
+        neg |= cv[j] < 0.0;
+        if (k < TH * TW) tile[k / TW][k % TW] = cv[j];
     }
     __syncthreads();
     for (int k = tid; k < TH * kSPX; k += blockDim.x) {

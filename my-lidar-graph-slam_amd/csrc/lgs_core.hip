@@ -446,9 +446,19 @@ __device__ __forceinline__ void precompute_tile(const double* __restrict__ in, d
     double* tile = lds;                          // [fh][fw]
     double* m1 = lds + fh * fw;                  // [y1-y0][fw]
     const int tid = threadIdx.x;
-    for (int k = tid; k < fh * fw; k += blockDim.x) {
-        const int yy = sy0 + k / fw, xx = sx0 + k % fw;
-        tile[k] = (xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;
+    for (int k0 = tid; k0 < fh * fw; k0 += 8 * (int)blockDim.x) {   // 8 loads in flight per thread
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = k0 + j * (int)blockDim.x;
+            const int yy = sy0 + k / fw, xx = sx0 + k % fw;
+            v[j] = (k < fh * fw && xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = k0 + j * (int)blockDim.x;
+            if (k < fh * fw) tile[k] = v[j];
+        }
     }
     __syncthreads();
     const int oh = y1 - y0;
@@ -516,9 +526,19 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
     double* m1 = lds + fh * fw;      // [kPTY][fw]
     const double* __restrict__ in = j.in;
     const int tid = threadIdx.x;
-    for (int k = tid; k < fh * fw; k += blockDim.x) {
-        const int yy = sy0 + k / fw, xx = sx0 + k % fw;
-        tile[k] = (xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;
+    for (int k0 = tid; k0 < fh * fw; k0 += 8 * (int)blockDim.x) {   // 8 loads in flight per thread
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = k0 + j * (int)blockDim.x;
+            const int yy = sy0 + k / fw, xx = sx0 + k % fw;
+            v[j] = (k < fh * fw && xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = k0 + j * (int)blockDim.x;
+            if (k < fh * fw) tile[k] = v[j];
+        }
     }
     __syncthreads();
     const int oh = y1 - y0;
