@@ -767,6 +767,96 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
     LGS_PROBE_PRINT("super(stage, sum w0, barrier, tail)");
 }
 
+// k_super_quad: k_super's bounds with 8-byte gathers.  A beam's superblocks
+// are nsby rows of nsbx consecutive floats (sub-phase layout), so a lane
+// fetches TWO neighbouring superblocks (a, a + 1) of one row with one 8-byte
+// load: 15 lanes cover a beam's 5 x 5 superblocks and one wave instruction
+// serves 4 beams (k_super<1>: 2 beams).  Used when nsby * ceil(nsbx / 2) <= 16.
+// Same outputs as k_super (sbound, one part per angle); loads are 4-byte
+// aligned, which gfx950 global loads accept.  The odd tail superblock's pair
+// reads one float past its row: inside the padded planes (the allocation has
+// >= 256 B of slack) and never added.
+typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
+constexpr int kQuadPipe = 8;
+__global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, const double* __restrict__ zero)
+{
+    const Blk wg = xcd_block();
+    const MatchItem& it = items[wg.z];
+    const RtcsmPlan& pl = it.pl;
+    if (wg.y >= pl.T) return;   // past this item's angles (uniform)
+    const float* __restrict__ sp = it.super;
+    const f2a4* __restrict__ z2 = (const f2a4*)zero;
+    extern __shared__ int srow[];   // [Nv]
+    __shared__ double red[kSupWaves][32];
+    const int t = wg.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nsbx = pl.nsbx, nsb2 = nsbx * pl.nsby;
+    const int np = (nsbx + 1) >> 1;
+    const int q = lane >> 4, idx = lane & 15;
+    const bool act = idx < pl.nsby * np;
+    const int b = act ? idx / np : 0, a0 = act ? 2 * (idx % np) : 0;
+    const float* __restrict__ lb = sp + (b * pl.Wq4 + a0);
+    const int* __restrict__ cbrow = it.cbase + pl.sb_off + (size_t)t * pl.Nv;
+    stage_lds(srow, cbrow, pl.Nv);
+    __syncthreads();
+    const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
+    const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
+    const int* row = srow + lo;
+    const int n4 = (cnt + 3) >> 2;   // beam slot q takes beams 4 i + q
+    double s0 = 0.0, s1 = 0.0;
+    for (int i0 = 0; i0 < n4; i0 += kQuadPipe) {
+        f2a4 x[kQuadPipe];
+#pragma unroll
+        for (int j = 0; j < kQuadPipe; ++j) {
+            const int v = 4 * (i0 + j) + q;
+            const int c = (v < cnt) ? row[min(v, cnt - 1)] : 0;
+            x[j] = *((act && v < cnt) ? (const f2a4*)(lb + c) : z2);
+        }
+#pragma unroll
+        for (int j = 0; j < kQuadPipe; ++j) {
+            s0 += (double)x[j].x;
+            s1 += (double)x[j].y;
+        }
+    }
+    // the 4 beam slots, then the waves
+    s0 += __shfl_xor(s0, 16, 64);
+    s1 += __shfl_xor(s1, 16, 64);
+    s0 += __shfl_xor(s0, 32, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    if (q == 0) {
+        red[w][2 * idx] = s0;
+        red[w][2 * idx + 1] = s1;
+    }
+    __syncthreads();
+    if (w != 0) return;
+    const int sbi = lane;
+    const bool own = sbi < nsb2;
+    double tot = 0.0;
+    if (own) {
+        const int a = sbi % nsbx, bb = sbi / nsbx;
+        const int k = 2 * (bb * np + (a >> 1)) + (a & 1);
+        for (int j = 0; j < kSupWaves; ++j) tot += red[j][k];
+    }
+    const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult;
+    if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
+    // rows that may hold unsafe blocks never seed: -inf (bounds are >= 0)
+    const bool seedable = own && it.tedge[t] != it.gen;
+    double bv = seedable ? bound : -INFINITY;
+    long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(bv, off, 64);
+        const long long ok = __shfl_xor(bk, off, 64);
+        if (better(ov, ok, bv, bk)) {
+            bv = ov;
+            bk = ok;
+        }
+    }
+    if (lane == 0) {
+        it.part_c[t] = bv;
+        it.part_k[t] = bk;
+    }
+}
+
 // k_coarse_rows (superblock pruning): coarse scores of the blocks k_select
 // could take; workgroup (angle t, patch row pr) of kRowWaves waves.  The
 // angle's superblocks are kept when bound > thr and (bound >= L, or the angle
@@ -2030,6 +2120,7 @@ struct BatchShape {
     int Tmax = 0, NvMax = 0, nsegMax = 0, nparts_max = 0;
     int P = 0, nsb2 = 0, chunks = 0, low_res = 0, cb = 0;
     bool pair = false;
+    bool quad = false;      // k_super_quad (nsby * ceil(nsbx / 2) <= 16; chunks == 1)
     bool planes = false;    // coarse map in padded phase planes
     bool pruned = false;    // superblock pruning
     bool lr5 = false;       // transposed LR = 5 evaluators
@@ -2124,7 +2215,7 @@ inline size_t plane_bytes(const RtcsmPlan& pl)
 }
 inline size_t super_bytes(const RtcsmPlan& pl)
 {
-    return align256(sizeof(float) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
+    return align256(sizeof(float) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4 + 64);   // + slack: k_super_quad reads one float past a row
 }
 double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_super)
 {
@@ -2342,7 +2433,9 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             const size_t lds = sizeof(int) * (size_t)std::max(B.NvMax, 1);
             dim3 g(B.chunks, B.Tmax, n);
             if (ctx->skipped(K_SUPER)) {
-            } else if (B.pair)
+            } else if (B.quad)
+                hipLaunchKernelGGL(k_super_quad, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+            else if (B.pair)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<1>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<0>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
@@ -2676,6 +2769,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     B.cb = coarse_block(p0);
     B.pair = B.nsb2 <= 32;
     B.chunks = B.pair ? 1 : (B.nsb2 + 63) / 64;
+    B.quad = ctx->super_quad && p0.nsby * ((p0.nsbx + 1) / 2) <= 16;
     B.planes = ctx->coarse_planes;
     B.pruned = uses_super(ctx, B.NvMax, B.nsb2, false);
     B.lr5 = lr5_path(B.NvMax, B.low_res);

@@ -283,6 +283,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_COARSE_PLANES: ctx->coarse_planes = value != 0.0; return LGS_OK;
     case LGS_OPT_SUPER_PRUNE: ctx->super_prune = value != 0.0; return LGS_OK;
     case LGS_OPT_LANES_MIN_BATCH: ctx->lanes_min_batch = (int)value; return LGS_OK;
+    case LGS_OPT_SUPER_QUAD: ctx->super_quad = value != 0.0; return LGS_OK;
     case LGS_OPT_SKIP_MASK: ctx->skip_mask = (unsigned)value; return LGS_OK;
     case LGS_OPT_GUARD_CAP:
         ctx->guard_cap = (int)value;

@@ -196,6 +196,7 @@ struct lgs_ctx {
     int guard_cap = lgs::kGuardInline;
     bool coarse_planes = true;   // phase-plane coarse layout (LGS_OPT_COARSE_PLANES)
     bool super_prune = true;     // superblock pruning of k_coarse (LGS_OPT_SUPER_PRUNE)
+    bool super_quad = true;      // k_super_quad (8-byte superblock gathers) where it applies (LGS_OPT_SUPER_QUAD)
     int lanes_min_batch = 2;     // pruned coarse stage: k_coarse_lanes from this batch size on (LGS_OPT_LANES_MIN_BATCH)
     // Stamps come from one process-wide counter: a context's scratch may be
     // memory a destroyed context used, and its stale tags must never match.
