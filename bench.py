@@ -86,22 +86,33 @@ def parse():
 
 
 class Dist:
-    """torch.distributed (RCCL) when launched by torchrun with WORLD_SIZE > 1."""
+    """torch.distributed (RCCL) when launched by torchrun with WORLD_SIZE > 1.
+
+    LGS_BENCH_REHEARSE=1 (rehearsal of the multi-rank path on a one-GPU box):
+    every rank uses GPU 0 and the collectives run over gloo on host tensors."""
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.rehearse = os.environ.get("LGS_BENCH_REHEARSE") == "1"
         self.d = None
+        if self.rehearse:
+            self.local = 0
         if self.world > 1:
             import torch
             import torch.distributed as tdist
-            torch.cuda.set_device(self.local)
-            tdist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            if self.rehearse:
+                tdist.init_process_group("gloo")
+            else:
+                torch.cuda.set_device(self.local)
+                tdist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
             self.d = tdist
 
     def device(self):
-        return f"cuda:{self.local}" if self.d else None
+        if not self.d:
+            return None
+        return "cpu" if self.rehearse else f"cuda:{self.local}"
 
     def barrier(self):
         if self.d:
@@ -121,6 +132,10 @@ class Dist:
         import torch
         local = torch.from_numpy(np.ascontiguousarray(a)).to(self.device())
         out = torch.empty((self.world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        if self.rehearse:
+            parts = [torch.empty_like(local) for _ in range(self.world)]
+            self.d.all_gather(parts, local)
+            return torch.stack(parts).numpy()
         self.d.all_gather_into_tensor(out, local)
         torch.cuda.synchronize()
         return out.cpu().numpy()
