@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default: 200 (match/refine), 4 (loop), 500 (stream)")
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--workload", default="match", choices=["match", "refine", "loop", "loop_bb", "stream"])
+    ap.add_argument("--workload", default="match", choices=["match", "refine", "loop", "loop_bb", "stream", "rebuild"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--coarse-planes", type=int, default=1, help="A/B: 1 phase-plane coarse layout, 0 plain")
@@ -78,8 +78,8 @@ def parse():
                     help="HIP-event timing inside the timed region: the roofline kernel only (default), "
                          "every kernel, or none (A/B of the event overhead)")
     a = ap.parse_args()
-    d_steps = dict(match=200, refine=200, loop=4, loop_bb=2, stream=500)[a.workload]
-    d_warm = dict(match=10, refine=5, loop=1, loop_bb=1, stream=10)[a.workload]
+    d_steps = dict(match=200, refine=200, loop=4, loop_bb=2, stream=500, rebuild=20)[a.workload]
+    d_warm = dict(match=10, refine=5, loop=1, loop_bb=1, stream=10, rebuild=2)[a.workload]
     a.steps = d_steps if a.steps is None else a.steps
     a.warmup = d_warm if a.warmup is None else a.warmup
     return a
@@ -96,10 +96,13 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.rehearse = os.environ.get("LGS_BENCH_REHEARSE") == "1"
+        # LGS_BENCH_DIST=1: the RCCL process group even at world size 1 (checks,
+        # on a one-GPU box, the torch-first HIP runtime sharing of the N>1 path)
+        force = os.environ.get("LGS_BENCH_DIST") == "1"
         self.d = None
         if self.rehearse:
             self.local = 0
-        if self.world > 1:
+        if self.world > 1 or force:
             import torch
             import torch.distributed as tdist
             if self.rehearse:
@@ -595,12 +598,75 @@ def run_stream(args, D, ctx):
     return line, stats, value
 
 
+# ------------------------------------------------------------------- rebuild
+def run_rebuild(args, D, ctx):
+    """SURVEY f2: GridMapBuilder::AfterLoopClosure -- every local map rebuilt
+    from its nodes after the pose graph moved them (one
+    lgs_maps_construct_from_scans call per step), then one ConstructGlobalMap
+    outside the timed region.  400 nodes on a 5 m circle (0.1 m apart), 10
+    local maps of 40 nodes, 1081 beams, 5 cm, PatchSize 64."""
+    world = scene.make_world()
+    ang = scene.beam_angles(1081)
+    n_nodes, per_map = 400, 40
+    truths = [(5.0 * np.cos(0.02 * k), 5.0 * np.sin(0.02 * k), 0.02 * k + np.pi / 2) for k in range(n_nodes)]
+    ranges_ = [scene.ray_cast(world, t, ang) for t in truths]
+    dscans = [ctx.scan(r, ang) for r in ranges_]
+    rng = np.random.default_rng(11 + D.rank)
+    # pose-graph corrections: a few variants, applied in turn
+    variants = [[(x + rng.normal(0, 0.03), y + rng.normal(0, 0.03), t + rng.normal(0, 0.01)) for x, y, t in truths]
+                for _ in range(4)]
+    ranges = [(lo, lo + per_map - 1) for lo in range(0, n_nodes, per_map)]
+    bp = abi.BuilderParams(*BUILDER)
+    maps = [ctx.map(0.05, 64, 0, 0, center=truths[lo][:2]) for lo, _ in ranges]
+    ctx.construct_maps(maps, ranges, dscans, truths, bp)
+    for k in range(args.warmup):
+        ctx.construct_maps(maps, ranges, dscans, variants[k % 4], bp)
+    set_timed_events(ctx, args, "k_ray_apply")
+    D.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ctx.construct_maps(maps, ranges, dscans, variants[k % 4], bp)
+    elapsed = D.max(time.perf_counter() - t0)
+    stats = ctx.kernel_stats()
+    ctx.set_option(abi.LGS_OPT_PROFILE, 0)
+    t1 = time.perf_counter()
+    gm = ctx.construct_global_map(0.05, 64, dscans, variants[0], bp)
+    global_ms = 1e3 * (time.perf_counter() - t1)
+    gg = gm.geometry()
+    cpu = None
+    if D.rank == 0 and not args.no_cpu and D.world == 1:
+        ob = oracle_lib()
+        oscans = [ob.OScan(r, ang) for r in ranges_]
+        obp = ob.BuilderParams(*BUILDER)
+
+        def one(i):
+            lo, hi = ranges[i]
+            om = ob.OMap(0.05, 64, 0, 0, center=truths[lo][:2])
+            om.construct(variants[0][lo:hi + 1], oscans[lo:hi + 1], obp)
+
+        rate, times = timed(args.cpu_seconds, range(len(ranges)), one)
+        cpu = dict(value=round(rate * per_map, 2), unit="nodes/s", cores=1, kind="port",
+                   sample=f"{len(times)} local maps x {per_map} nodes through the oracle's ConstructMapFromScans "
+                          f"(1 thread, as AfterLoopClosure runs), p50 {1e3 * np.median(times):.1f} ms per map")
+    value = args.steps * n_nodes * D.world / elapsed
+    line = dict(
+        metric="AfterLoopClosure rebuild: pose-graph nodes re-ray-cast/sec, 10 local maps x 40 nodes, 1081 beams",
+        value=round(value, 2), unit="nodes/s", n_gpus=D.world, steps=args.steps, warmup=args.warmup,
+        ms_per_step=round(1e3 * elapsed / args.steps, 4), higher_is_better=True, scaling="weak",
+        vs_baseline=None, dtype="f64", data="synthetic 400-node circular trajectory, pose corrections N(0, 3 cm)",
+        config=dict(workload="f2: GridMapBuilder::AfterLoopClosure (all local maps, one fused ray-cast pass)",
+                    nodes=n_nodes, local_maps=len(maps), beams=1081, parallelism=f"replicas x{D.world}"),
+        global_map=dict(ms=round(global_ms, 3), cells=[gg["w"], gg["h"]], nodes=n_nodes),
+        roofline=roofline_from(stats, "k_ray_apply", args.pmc), cpu_baseline=cpu)
+    return line, stats, value
+
+
 def main():
     args = parse()
     D = Dist()
     ctx = abi.Context(D.local)
     line, stats, _ = dict(match=run_match, refine=run_refine, loop=run_loop, loop_bb=run_loop,
-                          stream=run_stream)[args.workload](
+                          stream=run_stream, rebuild=run_rebuild)[args.workload](
         args, D, ctx)
     line["kernels"] = {k: dict(launches=v["launches"], avg_ms=round(v["total_ms"] / max(1, v["launches"]), 5))
                        for k, v in stats.items()}

@@ -34,6 +34,10 @@
  *                                C/mapping/grid_map_builder.cpp:149-186
  *   lgs_map_construct_from_scans GridMapBuilder::ConstructMapFromScans
  *                                C/mapping/grid_map_builder.cpp:227-332 (UpdateLatestMap :196-207)
+ *   lgs_maps_construct_from_scans GridMapBuilder::AfterLoopClosure's rebuild of every
+ *                                local map C/mapping/grid_map_builder.cpp:62-80
+ *   lgs_map_construct_global     GridMapBuilder::ConstructGlobalMap
+ *                                C/mapping/grid_map_builder.cpp:83-95
  *   lgs_linsolve_optimize_pose   ScanMatcherLinearSolver::OptimizePose(query)
  *                                C/mapping/scan_matcher_linear_solver.cpp:38-148
  *   lgs_cost_square_error        CostSquareError::Cost / ComputeCovariance
@@ -156,6 +160,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_SKIP_MASK     10  /* diagnostics only: bitmask of kernels (lgs_ctx_kernel_stats order) not launched -- results are invalid */
 #define LGS_OPT_SUPER_PRUNE   9   /* 1 (default) = skip coarse blocks whose 4x4-superblock bound is below the seed score, 0 = evaluate every coarse block */
 #define LGS_OPT_SUPER_QUAD    12  /* 1 (default) = superblock bounds with 8-byte gathers where the window allows, 0 = 4-byte (A/B) */
+#define LGS_OPT_RAY_CHUNK_KEYS 13  /* ray-cast keys per emit/sort/apply pass (default 2^28, max 2^30); more keys are cast in scan order over several passes */
 #define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: lane-per-block kernel for batches of at least this many matches (default 2; 1 = always), else the row kernel */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 
@@ -276,6 +281,24 @@ int  lgs_map_update_scan(lgs_ctx* ctx, lgs_map* map, const lgs_scan* scan, lgs_p
 int  lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* map, const lgs_scan* const* scans,
                                   const lgs_pose2d* robot_poses, int n,
                                   const lgs_builder_params* params);
+/* GridMapBuilder::AfterLoopClosure's map loop (C/mapping/grid_map_builder.cpp:62-80):
+ * ConstructMapFromScans(maps[i], poseGraph, idx_min[i], idx_max[i]) for every
+ * i, where node k of the pose graph is (scans[k], robot_poses[k]) and
+ * idx_min[i] <= idx_max[i] < n_nodes (inclusive ranges; they may overlap).
+ * The maps must be distinct.  Each map is resized and reset as
+ * lgs_map_construct_from_scans does; all maps then share one ray-cast pass,
+ * which gives the same cells as constructing them one after another. */
+int  lgs_maps_construct_from_scans(lgs_ctx* ctx, lgs_map* const* maps, const int* idx_min,
+                                   const int* idx_max, int n_maps, const lgs_scan* const* scans,
+                                   const lgs_pose2d* robot_poses, int n_nodes,
+                                   const lgs_builder_params* params);
+/* GridMapBuilder::ConstructGlobalMap (C/mapping/grid_map_builder.cpp:83-95): a
+ * new map of (resolution, patch_size) with 0 x 0 cells centred at (0, 0),
+ * then ConstructMapFromScans over all n nodes.  Any number of scans: the
+ * ray-cast runs in passes of at most LGS_OPT_RAY_CHUNK_KEYS keys. */
+int  lgs_map_construct_global(lgs_ctx* ctx, double resolution, int patch_size,
+                              const lgs_scan* const* scans, const lgs_pose2d* robot_poses, int n,
+                              const lgs_builder_params* params, lgs_map** out);
 /* Copy cells and per-cell hit/miss update counts (since create/construct) to
  * the host; any pointer may be NULL.  Sizes: num_cells_x * num_cells_y. */
 int  lgs_map_download(lgs_ctx* ctx, const lgs_map* map, double* cells, uint32_t* hit_count,

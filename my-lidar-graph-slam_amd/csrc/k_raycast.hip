@@ -11,10 +11,12 @@
 //   host       hit points with glibc sin/cos (bit-exact), bounding box, map
 //              geometry (Expand/Resize), sensor/hit cells, ray lengths + offsets
 //   k_emit     one thread per ray walks Bresenham (H/util.hpp:256-303) and emits
-//              a 64-bit key (cell << 32 | ray << 1 | is_hit) per visited cell;
-//              a ray visits a cell at most once, so (cell, ray) is unique
-//   sort       hipcub radix sort on the key: each cell's updates become a
-//              contiguous run ordered by ray = the reference's update order
+//              a 32-bit key (cell << 1 | is_hit) per visited cell at the ray's
+//              offset, so the key array is in ray order
+//   sort       stable hipcub radix sort on the cell bits only: each cell's
+//              updates become a contiguous run that keeps ray order = the
+//              reference's update order (a ray visits a cell at most once)
+//   k_runmask  hit and run-end bitmaps of the sorted keys (one ballot per 64)
 //   k_apply    one thread per run applies the Bayes updates sequentially and
 //              counts hits/misses
 #include "lgs_internal.hpp"
@@ -22,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <array>
 #include <cfloat>
 #include <cstring>
 
@@ -38,6 +41,7 @@ struct lgs_map {
     double* d_cells = nullptr;
     uint32_t* d_hit = nullptr;
     uint32_t* d_miss = nullptr;
+    size_t cap = 0;  // cells allocated (>= w*h; construct reuses a large enough allocation)
     lgs_grid view;
 };
 
@@ -46,13 +50,13 @@ namespace {
 constexpr double kPMin = 1e-3;
 constexpr double kPMax = 1.0 - kPMin;
 
-__device__ __forceinline__ double clampv(double v, double lo, double hi)
+__host__ __device__ __forceinline__ double clampv(double v, double lo, double hi)
 {
     return (v < lo) ? lo : (hi < v) ? hi : v;  // std::clamp
 }
 
 // BinaryBayesGridCell::Update (H/grid_map/binary_bayes_grid_cell.hpp:75-119)
-__device__ __forceinline__ double bayes_update(double v, double p)
+__host__ __device__ __forceinline__ double bayes_update(double v, double p)
 {
     if (v == 0.0) return clampv(p, kPMin, kPMax);
     const double co = clampv(v, kPMin, kPMax);
@@ -61,21 +65,46 @@ __device__ __forceinline__ double bayes_update(double v, double p)
     return clampv(clampv(o / (1.0 + o), kPMin, kPMax), kPMin, kPMax);
 }
 
-struct Ray {
-    int sx, sy, hx, hy;
+// The same operations with clamp(p) and odds(clamp(p)) evaluated once by the
+// caller (identical values: the reference recomputes the same constant).
+__device__ __forceinline__ double bayes_update_k(double v, double cp, double op)
+{
+#ifdef LGS_AB_APPLY_NOMATH  // diagnostics only: results invalid
+    return (v == 0.0) ? cp : clampv(v * op, kPMin, kPMax);
+#endif
+    if (v == 0.0) return cp;
+    const double co = clampv(v, kPMin, kPMax);
+    const double o = (co / (1.0 - co)) * op;
+    return clampv(clampv(o / (1.0 + o), kPMin, kPMax), kPMin, kPMax);
+}
+
+// One map of a ray-cast pass.  Several maps (AfterLoopClosure's local maps)
+// share one emit/sort/apply pass: map j owns the global cell range
+// [base, base + w*h) of the 31-bit cell space of the keys.
+struct RayMap {
+    unsigned long long base;
+    int w, h;
+    double* cells;
+    uint32_t* hit;
+    uint32_t* miss;
 };
 
 // One thread per ray: Bresenham walk (H/util.hpp:256-303), start cell
-// inclusive, end (hit) cell last.
+// inclusive, end (hit) cell last.  rmap[r] names the ray's map (null: map 0).
 __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
-                                             const long long* __restrict__ offs, int nrays,
-                                             int W, int H, unsigned long long* __restrict__ keys,
+                                             const long long* __restrict__ offs,
+                                             const int* __restrict__ rmap, int nrays,
+                                             const RayMap* __restrict__ maps,
+                                             unsigned* __restrict__ keys,
                                              int* __restrict__ outside)
 {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrays) return;
     const int4 ry = rays[r];
-    unsigned long long* out = keys + offs[r];
+    const RayMap mp = maps[rmap ? rmap[r] : 0];
+    const int W = mp.w, H = mp.h;
+    const unsigned base = (unsigned)mp.base;
+    unsigned* out = keys + offs[r];
     int deltaX = ry.z - ry.x;
     int deltaY = ry.w - ry.y;
     const int stepX = (deltaX < 0) ? -1 : 1;
@@ -83,18 +112,17 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
     int nx = ry.x, ny = ry.y;
     deltaX = abs(deltaX * 2);
     deltaY = abs(deltaY * 2);
-    const unsigned long long tag = (unsigned long long)r << 1;
     int bad = 0;
-    auto emit = [&](int x, int y, unsigned long long hit) {
+    auto emit = [&](int x, int y, unsigned hit) {
         const bool in = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
         bad |= !in;
-        const unsigned long long cell = in ? (unsigned long long)y * W + x : 0ull;
-        *out++ = (cell << 32) | tag | hit;
+        const unsigned cell = base + (in ? (unsigned)y * (unsigned)W + (unsigned)x : 0u);
+        *out++ = (cell << 1) | hit;
     };
     if (deltaX > deltaY) {
         int err = deltaY - deltaX / 2;
         while (nx != ry.z) {
-            emit(nx, ny, 0ull);
+            emit(nx, ny, 0u);
             if (err >= 0) {
                 ny += stepY;
                 err -= deltaX;
@@ -105,7 +133,7 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
     } else {
         int err = deltaX - deltaY / 2;
         while (ny != ry.w) {
-            emit(nx, ny, 0ull);
+            emit(nx, ny, 0u);
             if (err >= 0) {
                 nx += stepX;
                 err -= deltaY;
@@ -114,63 +142,221 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
             err += deltaX;
         }
     }
-    emit(nx, ny, 1ull);  // == (hx, hy): the hit cell, updated last
+    emit(nx, ny, 1u);  // == (hx, hy): the hit cell, updated last
     if (bad) atomicAdd(outside, 1);
 }
 
-// One thread per run of equal cells in the sorted keys.  The run is walked in
-// batches of 8 keys loaded together (one memory latency per batch instead of
-// per key).  BinaryBayesGridCell::Update is applied in order; odds(p) is the
-// same constant the reference recomputes every time, and an update that maps
-// a saturated value onto itself (v == 1e-3 under a miss with odds(pMiss) <= 1,
-// v == 1 - 1e-3 under a hit) is skipped after the kernel has checked on the
-// device that it is an exact fixed point -- long runs (cells next to the
-// sensor) are mostly such updates.
-constexpr int kApplyBatch = 8;
+// k_runmask: one thread per sorted key; each wavefront covers 64 consecutive
+// keys (64-aligned) and writes two 64-bit words with ballots -- bit j of
+// hitw = key j is a hit, bit j of endw = key j is the last of its cell's run.
+__global__ __launch_bounds__(256) void k_runmask(const unsigned* __restrict__ keys, long long n,
+                                                 unsigned long long* __restrict__ hitw,
+                                                 unsigned long long* __restrict__ endw)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < n;
+    const unsigned k = in ? keys[i] : 0u;
+    const bool last = in && (i + 1 >= n || (keys[i + 1] >> 1) != (k >> 1));
+    const unsigned long long hb = __ballot(in && (k & 1u));
+    const unsigned long long eb = __ballot(last);
+    if ((threadIdx.x & 63) == 0 && in) {
+        hitw[i >> 6] = hb;
+        endw[i >> 6] = eb;
+    }
+}
 
-__global__ __launch_bounds__(256) void k_apply(const unsigned long long* __restrict__ keys,
-                                               long long n, double* __restrict__ cells,
-                                               uint32_t* __restrict__ hits,
-                                               uint32_t* __restrict__ misses, double p_hit,
-                                               double p_miss)
+// Summaries of the words, one bit per word (64 words = 4096 keys per
+// summary word): the word holds a hit (hit2), a miss (miss2), a run end
+// (end2).  k_apply jumps over whole words of identity updates with them.
+__global__ __launch_bounds__(256) void k_runsummary(const unsigned long long* __restrict__ hitw,
+                                                    const unsigned long long* __restrict__ endw, long long nw,
+                                                    unsigned long long* __restrict__ hit2,
+                                                    unsigned long long* __restrict__ miss2,
+                                                    unsigned long long* __restrict__ end2)
+{
+    const long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = w < nw;
+    const unsigned long long hw = in ? hitw[w] : 0ull, ew = in ? endw[w] : 0ull;
+    const unsigned long long h2 = __ballot(in && hw != 0ull);
+    const unsigned long long m2 = __ballot(in && ~hw != 0ull);
+    const unsigned long long e2 = __ballot(in && ew != 0ull);
+    if ((threadIdx.x & 63) == 0 && in) {
+        hit2[w >> 6] = h2;
+        miss2[w >> 6] = m2;
+        end2[w >> 6] = e2;
+    }
+}
+
+// Number of runs (set bits of endw) -- for the algorithmic bytes of a timed
+// pass only, launched outside the timed span.
+__global__ __launch_bounds__(256) void k_count_runs(const unsigned long long* __restrict__ endw, long long nw,
+                                                    unsigned long long* __restrict__ runs)
+{
+    __shared__ unsigned long long part[4];
+    unsigned long long c = 0;
+    for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (long long)gridDim.x * blockDim.x)
+        c += __popcll(endw[w]);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(runs, part[0] + part[1] + part[2] + part[3]);
+}
+
+__device__ __forceinline__ int find_map(const RayMap* __restrict__ maps, int nmaps, unsigned cell)
+{
+    int lo = 0, hi = nmaps - 1;  // last j with base <= cell
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (maps[mid].base <= cell) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Update chains (memoised Bayes updates).  Chain c starts at anchor a[c] and
+// applies one update type (type[c]: 0 miss, 1 hit) repeatedly: t[c][j] is the
+// value after j such updates, up to a fixed point (fixed[c]) or kChain
+// entries.  The anchors are the values where long same-type stretches start:
+// clamp(pMiss) and clamp(pHit) (first update of a fresh cell), Update(1e-3,
+// pHit) and Update(1 - 1e-3, pMiss) (leaving a saturated value).  Built on the
+// host with the same IEEE operations as bayes_update (the parity tests compare
+// every cell bit for bit with the CPU restatement).
+constexpr int kChain = 64;
+struct BayesChains {
+    double a[4];
+    double t[4][kChain];
+    int len[4];
+    int fixed[4];
+};
+
+BayesChains make_chains(double p_hit, double p_miss)
+{
+    BayesChains c{};
+    const double anchor[4] = { clampv(p_miss, kPMin, kPMax), clampv(p_hit, kPMin, kPMax),
+                               bayes_update(kPMin, p_hit), bayes_update(kPMax, p_miss) };
+    const double p[4] = { p_miss, p_hit, p_miss, p_hit };  // chain types: miss, hit, miss, hit
+    for (int k = 0; k < 4; ++k) {
+        c.a[k] = anchor[k];
+        double v = anchor[k];
+        c.t[k][0] = v;
+        int j = 1;
+        c.fixed[k] = 0;
+        for (; j < kChain; ++j) {
+            const double nv = bayes_update(v, p[k]);
+            if (nv == v) {
+                c.fixed[k] = 1;
+                break;
+            }
+            c.t[k][j] = v = nv;
+        }
+        c.len[k] = j;
+    }
+    return c;
+}
+
+// k_apply: one thread per run of equal cells (the thread at the run's first
+// key) applies BinaryBayesGridCell::Update in key order = the reference's
+// order.  The run is read 64 keys at a time from the hit/end words, not key by
+// key, and the updates that are exact fixed points -- a miss at v == 1e-3
+// with odds(pMiss) <= 1, a hit at v == 1 - 1e-3 -- are jumped over with the
+// masks after the kernel has checked on the device that they are identities
+// (cells next to the sensor see thousands of such misses).
+__global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys, long long n,
+                                               const unsigned long long* __restrict__ hitw,
+                                               const unsigned long long* __restrict__ endw,
+                                               const unsigned long long* __restrict__ hit2,
+                                               const unsigned long long* __restrict__ miss2,
+                                               const unsigned long long* __restrict__ end2,
+                                               const RayMap* __restrict__ maps, int nmaps,
+                                               const BayesChains* __restrict__ ch,
+                                               double p_hit, double p_miss)
 {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const unsigned long long k = keys[i];
-    const unsigned cell = (unsigned)(k >> 32);
-    if (i > 0 && (unsigned)(keys[i - 1] >> 32) == cell) return;
+    if (i > 0 && !((endw[(i - 1) >> 6] >> ((i - 1) & 63)) & 1ull)) return;  // not a run start
+    const unsigned cell = keys[i] >> 1;
     const bool miss_fixed = bayes_update(kPMin, p_miss) == kPMin;
     const bool hit_fixed = bayes_update(kPMax, p_hit) == kPMax;
-    double v = cells[cell];
+    const double cph = clampv(p_hit, kPMin, kPMax), cpm = clampv(p_miss, kPMin, kPMax);
+    const double oph = cph / (1.0 - cph), opm = cpm / (1.0 - cpm);
+    const RayMap mp = maps[find_map(maps, nmaps, cell)];
+    const unsigned long long local = cell - mp.base;
+    double v = mp.cells[local];
     uint32_t nh = 0, nm = 0;
-    for (long long j = i;; j += kApplyBatch) {
-        unsigned long long kb[kApplyBatch];
-        if (j + kApplyBatch <= n) {
-#pragma unroll
-            for (int t = 0; t < kApplyBatch; ++t) kb[t] = keys[j + t];
-        } else {
-#pragma unroll
-            for (int t = 0; t < kApplyBatch; ++t) kb[t] = (j + t < n) ? keys[j + t] : ~0ull;
-        }
-        bool end = false;
-#pragma unroll
-        for (int t = 0; t < kApplyBatch; ++t) {
-            if (!end && (unsigned)(kb[t] >> 32) != cell) end = true;
-            if (!end) {
-                if (kb[t] & 1ull) {
-                    if (!(hit_fixed && v == kPMax)) v = bayes_update(v, p_hit);
-                    ++nh;
-                } else {
-                    if (!(miss_fixed && v == kPMin)) v = bayes_update(v, p_miss);
-                    ++nm;
-                }
+    const double a0 = ch->a[0], a1 = ch->a[1], a2 = ch->a[2], a3 = ch->a[3];
+    // the miss chain and the hit chain v is on (-1: none) and the index in it
+    int cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, ck = (v == a1) ? 1 : (v == a3) ? 3 : -1;
+    int jm = 0, jk = 0;
+    for (long long p = i;;) {
+        const int sh = (int)(p & 63);
+        const bool id_miss = miss_fixed && v == kPMin, id_hit = hit_fixed && v == kPMax;
+        if (sh == 0 && (id_miss || id_hit)) {
+            // whole words inside the run whose updates are all identities:
+            // no run end and no hit (resp. miss) in them
+            const long long w = p >> 6;
+            const int b = (int)(w & 63);
+            const unsigned long long stop = (end2[w >> 6] | (id_miss ? hit2[w >> 6] : miss2[w >> 6])) >> b;
+            const int k = stop ? __ffsll((long long)stop) - 1 : 64 - b;
+            if (k > 0) {
+                if (id_miss) nm += 64u * (unsigned)k; else nh += 64u * (unsigned)k;
+                p += 64LL * k;
+                continue;
             }
         }
-        if (end) break;
+        const unsigned long long hm = hitw[p >> 6] >> sh;
+        const unsigned long long em = endw[p >> 6] >> sh;
+        const int cnt = em ? __ffsll((long long)em) : 64 - sh;  // keys of the run in this word
+        const unsigned long long inm = (cnt == 64) ? ~0ull : ((1ull << cnt) - 1ull);
+        const unsigned long long h = hm & inm, m = inm & ~hm;
+        nh += __popcll(h);
+        nm += cnt - __popcll(h);
+        int pos = 0;
+        while (pos < cnt) {
+            if (miss_fixed && v == kPMin) {        // misses are identities: next hit
+                const unsigned long long rest = h >> pos;
+                if (!rest) break;
+                pos += __ffsll((long long)rest) - 1;
+            } else if (hit_fixed && v == kPMax) {  // hits are identities: next miss
+                const unsigned long long rest = m >> pos;
+                if (!rest) break;
+                pos += __ffsll((long long)rest) - 1;
+            }
+            const bool is_hit = (h >> pos) & 1ull;
+            const int c = is_hit ? ck : cm;
+            if (c >= 0) {
+                // k same-type updates from pos: jump along the chain
+                const unsigned long long other = (is_hit ? m : h) >> pos;
+                const int k = other ? __ffsll((long long)other) - 1 : cnt - pos;
+                const int last = ch->len[c] - 1;
+                const int j0 = is_hit ? jk : jm;
+                int j = j0 + k, used = k;
+                if (j > last) {
+                    if (!ch->fixed[c]) used = last - j0;  // table ends: the rest normally
+                    j = last;
+                }
+                v = ch->t[c][j];
+                pos += used;
+                if (is_hit) {
+                    jk = j;
+                    if (used < k) ck = -1;
+                    cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, jm = 0;
+                } else {
+                    jm = j;
+                    if (used < k) cm = -1;
+                    ck = (v == a1) ? 1 : (v == a3) ? 3 : -1, jk = 0;
+                }
+                continue;
+            }
+            v = bayes_update_k(v, is_hit ? cph : cpm, is_hit ? oph : opm);
+            ++pos;
+            cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, jm = 0;
+            ck = (v == a1) ? 1 : (v == a3) ? 3 : -1, jk = 0;
+        }
+        if (em) break;
+        p += cnt;
     }
-    cells[cell] = v;
-    hits[cell] += nh;
-    misses[cell] += nm;
+    mp.cells[local] = v;
+    mp.hit[local] += nh;
+    mp.miss[local] += nm;
 }
 
 // ---------------------------------------------------------------------------
@@ -218,22 +404,47 @@ void map_sync_view(lgs_map* m)
 }
 
 // Resize (:652-711): patches overlapping the new range keep their cells.
-void map_resize(lgs_map* m, double minX, double minY, double maxX, double maxY)
+struct ResizeGeom {
+    int pminx, pminy, npx, npy, w, h;
+};
+
+ResizeGeom resize_geom(const lgs_map* m, double minX, double minY, double maxX, double maxY)
 {
     int cminx, cminy, cmaxx, cmaxy;
     world_to_cell(m, minX, minY, cminx, cminy);
     world_to_cell(m, maxX, maxY, cmaxx, cmaxy);
     const int ps = m->ps;
-    const int pminx = cell_to_patch(cminx, ps), pminy = cell_to_patch(cminy, ps);
+    ResizeGeom g;
+    g.pminx = cell_to_patch(cminx, ps);
+    g.pminy = cell_to_patch(cminy, ps);
     const int pmaxx = cell_to_patch(cmaxx, ps), pmaxy = cell_to_patch(cmaxy, ps);
-    const int npx = std::max(0, pmaxx - pminx + 1);
-    const int npy = std::max(0, pmaxy - pminy + 1);
-    const int nw = npx * ps, nh = npy * ps;
+    g.npx = std::max(0, pmaxx - g.pminx + 1);
+    g.npy = std::max(0, pmaxy - g.pminy + 1);
+    g.w = g.npx * ps;
+    g.h = g.npy * ps;
+    return g;
+}
+
+void map_set_geom(lgs_map* m, const ResizeGeom& g)
+{
+    m->npx = g.npx;
+    m->npy = g.npy;
+    m->w = g.w;
+    m->h = g.h;
+    m->min_x += (g.pminx * m->ps) * m->res;
+    m->min_y += (g.pminy * m->ps) * m->res;
+    map_sync_view(m);
+}
+
+void map_resize(lgs_map* m, double minX, double minY, double maxX, double maxY)
+{
+    const ResizeGeom g = resize_geom(m, minX, minY, maxX, maxY);
+    const int ps = m->ps, nw = g.w, nh = g.h, pminx = g.pminx, pminy = g.pminy;
     double* cells;
     uint32_t *hit, *miss;
     map_alloc(m, nw, nh, &cells, &hit, &miss);
     const int x0 = std::max(0, pminx), y0 = std::max(0, pminy);
-    const int x1 = std::min(m->npx, pmaxx + 1), y1 = std::min(m->npy, pmaxy + 1);
+    const int x1 = std::min(m->npx, pminx + g.npx), y1 = std::min(m->npy, pminy + g.npy);
     if (x1 > x0 && y1 > y0) {
         const size_t cw = (size_t)(x1 - x0) * ps, ch = (size_t)(y1 - y0) * ps;
         const size_t ox = (size_t)x0 * ps, oy = (size_t)y0 * ps;
@@ -256,13 +467,36 @@ void map_resize(lgs_map* m, double minX, double minY, double maxX, double maxY)
     m->d_cells = cells;
     m->d_hit = hit;
     m->d_miss = miss;
-    m->npx = npx;
-    m->npy = npy;
-    m->w = nw;
-    m->h = nh;
-    m->min_x += (pminx * ps) * m->res;
-    m->min_y += (pminy * ps) * m->res;
-    map_sync_view(m);
+    m->cap = std::max<size_t>(1, (size_t)nw * nh);
+    map_set_geom(m, g);
+}
+
+// Resize followed by Reset (ConstructMapFromScans :288-290): every cell ends
+// up zero, so nothing is copied and an allocation that is large enough is
+// reused.
+void map_resize_reset(lgs_map* m, double minX, double minY, double maxX, double maxY)
+{
+    const ResizeGeom g = resize_geom(m, minX, minY, maxX, maxY);
+    const size_t need = std::max<size_t>(1, (size_t)g.w * g.h);
+    hipStream_t st = m->ctx->stream;
+    if (need > m->cap) {
+        double* cells;
+        uint32_t *hit, *miss;
+        map_alloc(m, g.w, g.h, &cells, &hit, &miss);  // zeroed
+        LGS_HIP_CHECK(hipStreamSynchronize(st));
+        hipFree(m->d_cells);
+        hipFree(m->d_hit);
+        hipFree(m->d_miss);
+        m->d_cells = cells;
+        m->d_hit = hit;
+        m->d_miss = miss;
+        m->cap = need;
+    } else {
+        LGS_HIP_CHECK(hipMemsetAsync(m->d_cells, 0, need * sizeof(double), st));
+        LGS_HIP_CHECK(hipMemsetAsync(m->d_hit, 0, need * sizeof(uint32_t), st));
+        LGS_HIP_CHECK(hipMemsetAsync(m->d_miss, 0, need * sizeof(uint32_t), st));
+    }
+    map_set_geom(m, g);
 }
 
 bool map_inside(const lgs_map* m, double x, double y)
@@ -285,21 +519,14 @@ void map_expand(lgs_map* m, double minX, double minY, double maxX, double maxY, 
     map_resize(m, minPX, minPY, maxPX, maxPY);
 }
 
-void map_reset(lgs_map* m)
-{
-    const size_t n = std::max<size_t>(1, (size_t)m->w * (size_t)m->h);
-    hipStream_t st = m->ctx->stream;
-    LGS_HIP_CHECK(hipMemsetAsync(m->d_cells, 0, n * sizeof(double), st));
-    LGS_HIP_CHECK(hipMemsetAsync(m->d_hit, 0, n * sizeof(uint32_t), st));
-    LGS_HIP_CHECK(hipMemsetAsync(m->d_miss, 0, n * sizeof(uint32_t), st));
-}
-
 inline double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
 inline double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
 
 struct ScanHits {
     lgs_pose2d sensor;
     std::vector<double> xy;  // hit points (x, y) of the usable beams, beam order
+    // min x, min y, max x, max y of the sensor and the hit points
+    double box[4];
 };
 
 // ComputeBoundingBoxAndScanPoints hit points (:335-380), glibc sin/cos
@@ -318,70 +545,264 @@ ScanHits scan_hits(const lgs_scan* s, lgs_pose2d robot, const lgs_builder_params
         h.xy.push_back(h.sensor.x + r * c);
         h.xy.push_back(h.sensor.y + r * sn);
     }
+    double b0 = h.sensor.x, b1 = h.sensor.y, b2 = h.sensor.x, b3 = h.sensor.y;
+    for (size_t q = 0; q + 1 < h.xy.size(); q += 2) {
+        b0 = smin(b0, h.xy[q]);
+        b1 = smin(b1, h.xy[q + 1]);
+        b2 = smax(b2, h.xy[q]);
+        b3 = smax(b3, h.xy[q + 1]);
+    }
+    h.box[0] = b0, h.box[1] = b1, h.box[2] = b2, h.box[3] = b3;
     return h;
 }
 
-// Ray-cast the given scans (already in the map's geometry) in order.
-void raycast(lgs_map* m, const std::vector<ScanHits>& scans, const lgs_builder_params* bp)
+// One map of a ray-cast pass and its scans (hit points in world coordinates).
+struct MapJob {
+    lgs_map* m;
+    std::vector<ScanHits> hs;
+};
+
+// Hit points of every job's scans (one parallel region over all of them) and
+// each job's bounding box as ConstructMapFromScans accumulates it (:234-285)
+// -- note topRight starts at numeric_limits<double>::min().  min/max of the
+// per-scan boxes equals the reference's running min/max (no NaN reaches here).
+void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, const std::vector<int>& count,
+                    const lgs_scan* const* scans, const lgs_pose2d* poses, const lgs_builder_params* bp,
+                    std::vector<std::array<double, 4>>& boxes)
 {
-    lgs_ctx* ctx = m->ctx;
+    std::vector<std::pair<int, int>> work;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        jobs[j].hs.resize(count[j]);
+        for (int k = 0; k < count[j]; ++k) work.emplace_back((int)j, k);
+    }
+    host_parallel_for((int)work.size(), 2, [&](int w) {
+        const int j = work[w].first, k = work[w].second;
+        jobs[j].hs[k] = scan_hits(scans[first[j] + k], poses[first[j] + k], bp);
+    });
+    boxes.assign(jobs.size(), std::array<double, 4>{DBL_MAX, DBL_MAX, DBL_MIN, DBL_MIN});
+    for (size_t j = 0; j < jobs.size(); ++j)
+        for (const ScanHits& h : jobs[j].hs) {
+            auto& b = boxes[j];
+            b[0] = smin(b[0], h.box[0]);
+            b[1] = smin(b[1], h.box[1]);
+            b[2] = smax(b[2], h.box[2]);
+            b[3] = smax(b[3], h.box[3]);
+        }
+}
+
+// Ray-cast every job's scans (already in its map's geometry), jobs in order,
+// each job's scans in order.  The rays of all jobs share emit/sort/apply
+// passes; a pass holds at most ctx->ray_chunk_keys keys and 2^32 cells of
+// maps, and passes run in ray order, so each cell still sees its updates in
+// the reference's order.
+void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_params* bp)
+{
     hipStream_t st = ctx->stream;
-    std::vector<int4> rays;
-    std::vector<long long> offs;
-    long long total = 0;
-    for (const ScanHits& h : scans) {
+    struct Unit {
+        int job;
+        const ScanHits* h;
+        std::vector<int4> rays;
+        std::vector<int> len;
+        long long keys;
+    };
+    std::vector<Unit> units;
+    for (int j = 0; j < (int)jobs.size(); ++j)
+        for (const ScanHits& h : jobs[j].hs)
+            if (h.xy.size() >= 2) units.push_back(Unit{j, &h, {}, {}, 0});
+    if (units.empty()) return;
+    for (const MapJob& J : jobs)
+        LGS_REQUIRE((size_t)J.m->w * J.m->h < (1ull << 31), "map too large for 31-bit cell keys");
+    // sensor/hit cells and ray lengths (parallel over scans)
+    host_parallel_for((int)units.size(), 2, [&](int u) {
+        Unit& U = units[u];
+        const lgs_map* m = jobs[U.job].m;
+        const ScanHits& h = *U.h;
         int sx, sy;
         world_to_cell(m, h.sensor.x, h.sensor.y, sx, sy);
-        for (size_t k = 0; k + 1 < h.xy.size(); k += 2) {
+        const size_t nr = h.xy.size() / 2;
+        U.rays.resize(nr);
+        U.len.resize(nr);
+        long long keys = 0;
+        for (size_t k = 0; k < nr; ++k) {
             int hx, hy;
-            world_to_cell(m, h.xy[k], h.xy[k + 1], hx, hy);
-            rays.push_back(make_int4(sx, sy, hx, hy));
-            offs.push_back(total);
-            total += std::max(std::abs(hx - sx), std::abs(hy - sy)) + 1;
+            world_to_cell(m, h.xy[2 * k], h.xy[2 * k + 1], hx, hy);
+            U.rays[k] = make_int4(sx, sy, hx, hy);
+            U.len[k] = std::max(std::abs(hx - sx), std::abs(hy - sy)) + 1;
+            keys += U.len[k];
         }
+        U.keys = keys;
+    });
+    long long total_keys = 0, total_rays = 0;
+    unsigned long long total_cells = 0;
+    for (size_t q = 0; q < units.size(); ++q) {
+        total_keys += units[q].keys;
+        total_rays += (long long)units[q].len.size();
+        if (q == 0 || units[q].job != units[q - 1].job)
+            total_cells += (unsigned long long)jobs[units[q].job].m->w * jobs[units[q].job].m->h;
     }
-    const int nrays = (int)rays.size();
-    if (nrays == 0) return;
-    LGS_REQUIRE((size_t)m->w * m->h < (1ull << 32), "map too large for 32-bit cell keys");
-    int4* d_rays = (int4*)ctx->ensure(S_RAY0, sizeof(int4) * nrays);
-    long long* d_offs = (long long*)ctx->ensure(S_RAY1, sizeof(long long) * nrays);
-    unsigned long long* d_keys = (unsigned long long*)ctx->ensure(S_RAY2, sizeof(unsigned long long) * total);
-    unsigned long long* d_sorted = (unsigned long long*)ctx->ensure(S_RAY3, sizeof(unsigned long long) * total);
+    const long long budget = std::max(1LL, std::min(ctx->ray_chunk_keys, 1LL << 30));
+    // [0] rays leaving the map (int), [2..3] runs of equal cells applied (u64)
     int* d_bad = (int*)ctx->ensure(S_RAY4, 16);
-    // stage rays + offsets through pinned memory (async copy)
-    const size_t rb = sizeof(int4) * nrays, ob = sizeof(long long) * nrays;
-    char* pin = (char*)ctx->ensure_pinned(rb + ob + 64);
-    std::memcpy(pin, rays.data(), rb);
-    std::memcpy(pin + rb, offs.data(), ob);
-    LGS_HIP_CHECK(hipMemcpyAsync(d_rays, pin, rb, hipMemcpyHostToDevice, st));
-    LGS_HIP_CHECK(hipMemcpyAsync(d_offs, pin + rb, ob, hipMemcpyHostToDevice, st));
-    LGS_HIP_CHECK(hipMemsetAsync(d_bad, 0, sizeof(int), st));
-    // algorithmic bytes: 8 B per emitted key (emit), 8 B key +
-    // 16 B cell read/write per update (apply)
-    int tok = ctx->timing_begin(K_RAY_EMIT, 8.0 * (double)total);
-    hipLaunchKernelGGL(k_emit, dim3((nrays + 63) / 64), dim3(64), 0, st, d_rays, d_offs, nrays, m->w,
-                       m->h, d_keys, d_bad);
-    ctx->timing_end(tok);
-    LGS_HIP_CHECK(hipGetLastError());
-    int cell_bits = 1;
-    while (cell_bits < 32 && (1ull << cell_bits) < (unsigned long long)m->w * m->h) ++cell_bits;
-    size_t tbytes = 0;
-    LGS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tbytes, d_keys, d_sorted, (int)total, 0,
-                                                    32 + cell_bits, st));
-    void* temp = ctx->ensure(S_RAY5, tbytes);
-    LGS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp, tbytes, d_keys, d_sorted, (int)total, 0,
-                                                    32 + cell_bits, st));
-    tok = ctx->timing_begin(K_RAY_APPLY, 24.0 * (double)total);
-    hipLaunchKernelGGL(k_apply, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d_sorted, total,
-                       m->d_cells, m->d_hit, m->d_miss, bp->prob_hit, bp->prob_miss);
-    ctx->timing_end(tok);
-    LGS_HIP_CHECK(hipGetLastError());
-    int bad = 0;
-    LGS_HIP_CHECK(hipMemcpyAsync(pin, d_bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    unsigned long long* d_runs = (unsigned long long*)(d_bad + 2);
+    LGS_HIP_CHECK(hipMemsetAsync(d_bad, 0, 16, st));
+    int apply_tok = -1;
+    const BayesChains chains = make_chains(bp->prob_hit, bp->prob_miss);
+    size_t u = 0, r = 0;
+    int pass = 0;
+    char* pin = nullptr;
+    while (u < units.size()) {
+        // plan one pass: rays [(u, r), (eu, er)) and the maps they touch
+        std::vector<RayMap> maps;
+        unsigned long long cells = 0;
+        long long keys = 0, nr = 0;
+        int cur = -1;
+        size_t eu = u, er = r;
+        if (pass == 0 && total_keys <= budget && total_rays < (1LL << 30) && total_cells <= (1ull << 31)) {
+            // everything in one pass (the usual case): whole units
+            for (size_t q = 0; q < units.size(); ++q)
+                if (q == 0 || units[q].job != units[q - 1].job) {
+                    const lgs_map* m = jobs[units[q].job].m;
+                    maps.push_back(RayMap{cells, m->w, m->h, m->d_cells, m->d_hit, m->d_miss});
+                    cells += (unsigned long long)m->w * m->h;
+                }
+            keys = total_keys, nr = total_rays, eu = units.size(), er = 0;
+        }
+        while (eu < units.size()) {
+            const Unit& U = units[eu];
+            if (er >= U.len.size()) {
+                ++eu, er = 0;
+                continue;
+            }
+            const long long L = U.len[er];
+            if (nr > 0 && (keys + L > budget || nr >= (1LL << 30))) break;
+            if (U.job != cur) {
+                const lgs_map* m = jobs[U.job].m;
+                const unsigned long long mc = (unsigned long long)m->w * m->h;
+                if (nr > 0 && cells + mc > (1ull << 31)) break;
+                maps.push_back(RayMap{cells, m->w, m->h, m->d_cells, m->d_hit, m->d_miss});
+                cells += mc;
+                cur = U.job;
+            }
+            keys += L, ++nr, ++er;
+        }
+        const int nmaps = (int)maps.size();
+        const bool multi = nmaps > 1;
+        // stage the map table, rays, key offsets and ray->map indices
+        auto al = [](size_t b) { return (b + 63) & ~(size_t)63; };
+        const size_t cb = al(sizeof(BayesChains));
+        const size_t mb = cb + al(sizeof(RayMap) * nmaps), rb = al(sizeof(int4) * nr),
+                     ob = al(sizeof(long long) * nr), ib = multi ? al(sizeof(int) * nr) : 0;
+        if (pass > 0) ctx->sync();  // the previous pass's uploads have left the staging buffer
+        pin = (char*)ctx->ensure_pinned(mb + rb + ob + ib + 64);
+        std::memcpy(pin, &chains, sizeof(BayesChains));
+        std::memcpy(pin + cb, maps.data(), sizeof(RayMap) * nmaps);
+        int4* prays = (int4*)(pin + mb);
+        long long* poffs = (long long*)(pin + mb + rb);
+        int* pmap = (int*)(pin + mb + rb + ob);
+        {
+            // segments = the pass's part of each unit; their ray and key
+            // offsets by a prefix over segments, then a parallel fill
+            struct Seg {
+                size_t unit, r0, r1;
+                long long ray0, key0;
+                int map;
+            };
+            std::vector<Seg> segs;
+            long long ray0 = 0, key0 = 0;
+            int mi = -1, cj = -1;
+            for (size_t cu = u; cu < units.size() && ray0 < nr; ++cu) {
+                const Unit& U = units[cu];
+                const size_t r0 = (cu == u) ? r : 0;
+                const size_t r1 = std::min(U.len.size(), r0 + (size_t)(nr - ray0));
+                if (r1 <= r0) continue;
+                if (U.job != cj) cj = U.job, ++mi;
+                segs.push_back(Seg{cu, r0, r1, ray0, key0, mi});
+                long long kk = 0;
+                if (r0 == 0 && r1 == U.len.size()) kk = U.keys;
+                else
+                    for (size_t q = r0; q < r1; ++q) kk += U.len[q];
+                ray0 += (long long)(r1 - r0);
+                key0 += kk;
+            }
+            host_parallel_for((int)segs.size(), 4, [&](int g) {
+                const Seg& S = segs[g];
+                const Unit& U = units[S.unit];
+                long long k = S.ray0, off = S.key0;
+                for (size_t q = S.r0; q < S.r1; ++q, ++k) {
+                    prays[k] = U.rays[q];
+                    poffs[k] = off;
+                    if (multi) pmap[k] = S.map;
+                    off += U.len[q];
+                }
+            });
+        }
+        char* d_stage = (char*)ctx->ensure(S_RAY6, mb + rb + ob + ib);
+        LGS_HIP_CHECK(hipMemcpyAsync(d_stage, pin, mb + rb + ob + ib, hipMemcpyHostToDevice, st));
+        const BayesChains* d_chains = (const BayesChains*)d_stage;
+        const RayMap* d_maps = (const RayMap*)(d_stage + cb);
+        const int4* d_rays = (const int4*)(d_stage + mb);
+        const long long* d_offs = (const long long*)(d_stage + mb + rb);
+        const int* d_rmap = multi ? (const int*)(d_stage + mb + rb + ob) : nullptr;
+        unsigned* d_keys = (unsigned*)ctx->ensure(S_RAY2, sizeof(unsigned) * keys);
+        unsigned* d_sorted = (unsigned*)ctx->ensure(S_RAY3, sizeof(unsigned) * keys);
+        // algorithmic bytes: 4 B per emitted key (emit); 4 B per
+        // key + 32 B per run of equal cells (cell, hit and miss counters read
+        // and written once; the run count is added after the last pass)
+        int tok = ctx->timing_begin(K_RAY_EMIT, 4.0 * (double)keys);
+        hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, st, d_rays, d_offs,
+                           d_rmap, (int)nr, d_maps, d_keys, d_bad);
+        ctx->timing_end(tok);
+        LGS_HIP_CHECK(hipGetLastError());
+        int cell_bits = 1;
+        while (cell_bits < 32 && (1ull << cell_bits) < cells) ++cell_bits;
+        size_t tbytes = 0;
+        LGS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tbytes, d_keys, d_sorted, (int)keys, 1,
+                                                        1 + cell_bits, st));
+        void* temp = ctx->ensure(S_RAY5, tbytes);
+        LGS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp, tbytes, d_keys, d_sorted, (int)keys, 1,
+                                                        1 + cell_bits, st));
+        tok = ctx->timing_begin(K_RAY_APPLY, 4.0 * (double)keys);
+        if (tok >= 0) apply_tok = tok;
+        const long long nw = (keys + 63) / 64;
+        const long long nw2 = (nw + 63) / 64;
+        unsigned long long* d_hitw =
+            (unsigned long long*)ctx->ensure(S_RAY7, sizeof(unsigned long long) * (2 * nw + 3 * nw2));
+        unsigned long long* d_endw = d_hitw + nw;
+        unsigned long long* d_hit2 = d_endw + nw;
+        unsigned long long* d_miss2 = d_hit2 + nw2;
+        unsigned long long* d_end2 = d_miss2 + nw2;
+        const unsigned blocks = (unsigned)((keys + 255) / 256);
+        hipLaunchKernelGGL(k_runmask, dim3(blocks), dim3(256), 0, st, d_sorted, keys, d_hitw, d_endw);
+        hipLaunchKernelGGL(k_runsummary, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, d_hitw, d_endw, nw,
+                           d_hit2, d_miss2, d_end2);
+        hipLaunchKernelGGL(k_apply, dim3(blocks), dim3(256), 0, st, d_sorted, keys, d_hitw, d_endw, d_hit2,
+                           d_miss2, d_end2, d_maps, nmaps, d_chains, bp->prob_hit, bp->prob_miss);
+        ctx->timing_end(tok);
+        if (tok >= 0)
+            hipLaunchKernelGGL(k_count_runs, dim3((unsigned)std::min<long long>((nw + 255) / 256, 512)), dim3(256), 0,
+                               st, d_endw, nw, d_runs);
+        LGS_HIP_CHECK(hipGetLastError());
+        u = eu, r = er;
+        ++pass;
+    }
     ctx->sync();
-    if (ctx->profile) ctx->harvest();
+    LGS_HIP_CHECK(hipMemcpyAsync(pin, d_bad, 16, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    int bad = 0;
+    unsigned long long runs = 0;
     std::memcpy(&bad, pin, sizeof(int));
+    std::memcpy(&runs, pin + 8, sizeof(runs));
+    if (apply_tok >= 0) ctx->pending[apply_tok].algo_bytes += 32.0 * (double)runs;
+    if (ctx->profile) ctx->harvest();
     if (bad) throw Error(LGS_ERR_INTERNAL, "ray cell outside the map geometry");
+}
+
+void raycast(lgs_map* m, std::vector<ScanHits>&& scans, const lgs_builder_params* bp)
+{
+    std::vector<MapJob> jobs(1);
+    jobs[0].m = m;
+    jobs[0].hs = std::move(scans);
+    raycast_maps(m->ctx, jobs, bp);
 }
 
 }  // namespace
@@ -412,6 +833,7 @@ extern "C" int lgs_map_create(lgs_ctx* ctx, double res, int ps, int ncx, int ncy
         m->min_y = cy - offY * res;
         try {
             map_alloc(m, m->w, m->h, &m->d_cells, &m->d_hit, &m->d_miss);
+            m->cap = std::max<size_t>(1, (size_t)m->w * m->h);
         } catch (...) {
             delete m;
             throw;
@@ -461,15 +883,9 @@ extern "C" int lgs_map_update_scan(lgs_ctx* ctx, lgs_map* m, const lgs_scan* sca
         m->ctx = ctx;
         std::vector<ScanHits> hs(1, scan_hits(scan, robot, bp));
         // bounding box starts at the sensor position (:346-352)
-        double blx = hs[0].sensor.x, bly = hs[0].sensor.y, trx = blx, try_ = bly;
-        for (size_t k = 0; k + 1 < hs[0].xy.size(); k += 2) {
-            blx = smin(blx, hs[0].xy[k]);
-            bly = smin(bly, hs[0].xy[k + 1]);
-            trx = smax(trx, hs[0].xy[k]);
-            try_ = smax(try_, hs[0].xy[k + 1]);
-        }
-        map_expand(m, blx, bly, trx, try_, 5.0);  // :157-158 (default enlargeStep)
-        raycast(m, hs, bp);
+        const double* bx = hs[0].box;
+        map_expand(m, bx[0], bx[1], bx[2], bx[3], 5.0);  // :157-158 (default enlargeStep)
+        raycast(m, std::move(hs), bp);
     });
 }
 
@@ -481,28 +897,65 @@ extern "C" int lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* m, const lgs_
     return guarded(ctx, [&] {
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         m->ctx = ctx;
-        // :234-285 -- note topRight starts at numeric_limits<double>::min()
-        double blx = DBL_MAX, bly = DBL_MAX, trx = DBL_MIN, try_ = DBL_MIN;
-        std::vector<ScanHits> hs;
-        hs.reserve(n);
-        for (int k = 0; k < n; ++k) {
-            hs.push_back(scan_hits(scans[k], poses[k], bp));
-            const ScanHits& h = hs.back();
-            blx = smin(blx, h.sensor.x);
-            bly = smin(bly, h.sensor.y);
-            trx = smax(trx, h.sensor.x);
-            try_ = smax(try_, h.sensor.y);
-            for (size_t q = 0; q + 1 < h.xy.size(); q += 2) {
-                blx = smin(blx, h.xy[q]);
-                bly = smin(bly, h.xy[q + 1]);
-                trx = smax(trx, h.xy[q]);
-                try_ = smax(try_, h.xy[q + 1]);
-            }
-        }
-        map_resize(m, blx, bly, trx, try_);  // :288-289
-        map_reset(m);                        // :290
-        raycast(m, hs, bp);                  // :293-329
+        std::vector<MapJob> jobs(1);
+        jobs[0].m = m;
+        std::vector<std::array<double, 4>> box;
+        hits_and_boxes(jobs, {0}, {n}, scans, poses, bp, box);       // :234-285
+        map_resize_reset(m, box[0][0], box[0][1], box[0][2], box[0][3]);  // :288-290
+        raycast_maps(ctx, jobs, bp);                                     // :293-329
     });
+}
+
+extern "C" int lgs_maps_construct_from_scans(lgs_ctx* ctx, lgs_map* const* maps, const int* idx_min,
+                                             const int* idx_max, int n_maps, const lgs_scan* const* scans,
+                                             const lgs_pose2d* poses, int n_nodes,
+                                             const lgs_builder_params* bp)
+{
+    if (!ctx || !bp || n_maps < 0 || n_nodes < 0) return LGS_ERR_INVALID_ARG;
+    if (n_maps > 0 && (!maps || !idx_min || !idx_max || !scans || !poses)) return LGS_ERR_INVALID_ARG;
+    for (int i = 0; i < n_maps; ++i) {
+        if (!maps[i] || idx_min[i] < 0 || idx_min[i] > idx_max[i] || idx_max[i] >= n_nodes)
+            return LGS_ERR_INVALID_ARG;
+        for (int j = 0; j < i; ++j)
+            if (maps[j] == maps[i]) return LGS_ERR_INVALID_ARG;
+    }
+    return guarded(ctx, [&] {
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        // AfterLoopClosure (:66-74): ConstructMapFromScans per local map; the
+        // geometry of each is fixed before any ray is cast, so the ray-casts
+        // of all maps run as one pass over the maps in order
+        std::vector<MapJob> jobs(n_maps);
+        std::vector<int> first(n_maps), count(n_maps);
+        for (int i = 0; i < n_maps; ++i) {
+            maps[i]->ctx = ctx;
+            jobs[i].m = maps[i];
+            first[i] = idx_min[i];
+            count[i] = idx_max[i] - idx_min[i] + 1;
+        }
+        std::vector<std::array<double, 4>> box;
+        hits_and_boxes(jobs, first, count, scans, poses, bp, box);
+        for (int i = 0; i < n_maps; ++i) map_resize_reset(maps[i], box[i][0], box[i][1], box[i][2], box[i][3]);
+        raycast_maps(ctx, jobs, bp);
+    });
+}
+
+extern "C" int lgs_map_construct_global(lgs_ctx* ctx, double res, int ps, const lgs_scan* const* scans,
+                                        const lgs_pose2d* poses, int n, const lgs_builder_params* bp,
+                                        lgs_map** out)
+{
+    if (!ctx || !bp || !out || n < 0 || (n > 0 && (!scans || !poses))) return LGS_ERR_INVALID_ARG;
+    *out = nullptr;
+    lgs_map* m = nullptr;
+    // GridMapType gridMap { res, patchSize, 0, 0, Point2D(0, 0) } (:89-90)
+    int rc = lgs_map_create(ctx, res, ps, 0, 0, 0.0, 0.0, &m);
+    if (rc != LGS_OK) return rc;
+    rc = lgs_map_construct_from_scans(ctx, m, scans, poses, n, bp);  // :91
+    if (rc != LGS_OK) {
+        lgs_map_destroy(m);
+        return rc;
+    }
+    *out = m;
+    return LGS_OK;
 }
 
 extern "C" int lgs_map_download(lgs_ctx* ctx, const lgs_map* m, double* cells, uint32_t* hit,

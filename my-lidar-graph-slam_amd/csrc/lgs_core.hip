@@ -10,7 +10,12 @@
 #include "lgs_internal.hpp"
 
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
+#include <thread>
+
+#include <pthread.h>
 
 using namespace lgs;
 
@@ -284,6 +289,10 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_SUPER_PRUNE: ctx->super_prune = value != 0.0; return LGS_OK;
     case LGS_OPT_LANES_MIN_BATCH: ctx->lanes_min_batch = (int)value; return LGS_OK;
     case LGS_OPT_SUPER_QUAD: ctx->super_quad = value != 0.0; return LGS_OK;
+    case LGS_OPT_RAY_CHUNK_KEYS:
+        if (!(value >= 1.0)) return LGS_ERR_INVALID_ARG;
+        ctx->ray_chunk_keys = (long long)std::min(value, (double)(1LL << 30));
+        return LGS_OK;
     case LGS_OPT_SKIP_MASK: ctx->skip_mask = (unsigned)value; return LGS_OK;
     case LGS_OPT_GUARD_CAP:
         ctx->guard_cap = (int)value;
@@ -758,5 +767,89 @@ const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* s, double rmax, int* nv)
     (void)ctx;
     *nv = s->nv;   // the device compacts the same beams itself (k_project)
     return s->h_vidx.data();
+}
+
+namespace {
+// Host worker pool behind host_parallel_for: workers sleep on a condition
+// variable between regions (a region costs a wake-up, not thread creation).
+class HostPool {
+public:
+    static HostPool* get()
+    {
+        static std::once_flag once;
+        std::call_once(once, [] { pthread_atfork(nullptr, nullptr, [] { pool = nullptr; }); });
+        std::lock_guard<std::mutex> lk(create_mu);
+        if (!pool) pool = new HostPool();  // never destroyed: workers live for the process
+        return pool;
+    }
+    int size() const { return nworkers + 1; }
+    // false (nothing run) if another region holds the pool: the caller runs inline
+    bool run(int n, int nt, const std::function<void(int)>& f)
+    {
+        std::unique_lock<std::mutex> call(call_mu, std::try_to_lock);
+        if (!call.owns_lock()) return false;
+        const int helpers = std::min(nt - 1, nworkers);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            fn = &f;
+            count = n;
+            next.store(0);
+            slots = helpers;
+            busy = helpers;
+            ++gen;
+        }
+        if (helpers > 0) cv.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return busy == 0; });
+        return true;
+    }
+    static inline thread_local bool inside = false;  // running a region's f (nested calls go inline)
+
+private:
+    HostPool()
+    {
+        const int hw = std::max(1, (int)std::thread::hardware_concurrency());
+        nworkers = std::min(15, hw - 1);
+        for (int i = 0; i < nworkers; ++i) std::thread([this] { loop(); }).detach();
+    }
+    void work()
+    {
+        inside = true;
+        for (int i; (i = next.fetch_add(1)) < count;) (*fn)(i);
+        inside = false;
+    }
+    void loop()
+    {
+        unsigned long long seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return gen != seen; });
+            seen = gen;
+            if (slots == 0) continue;
+            --slots;
+            lk.unlock();
+            work();
+            lk.lock();
+            if (--busy == 0) done.notify_all();
+        }
+    }
+    static inline HostPool* pool = nullptr;
+    static inline std::mutex create_mu;
+    std::mutex call_mu, mu;
+    std::condition_variable cv, done;
+    const std::function<void(int)>* fn = nullptr;
+    int count = 0, nworkers = 0, slots = 0, busy = 0;
+    std::atomic<int> next{0};
+    unsigned long long gen = 0;
+};
+}  // namespace
+
+void host_parallel_for(int n, int grain, const std::function<void(int)>& f)
+{
+    HostPool* p = (n > 1) ? HostPool::get() : nullptr;
+    const int nt = p ? std::min(p->size(), (n + std::max(1, grain) - 1) / std::max(1, grain)) : 1;
+    if (nt <= 1 || HostPool::inside || !p->run(n, nt, f))
+        for (int i = 0; i < n; ++i) f(i);
 }
 }  // namespace lgs

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -198,6 +199,7 @@ struct lgs_ctx {
     bool super_prune = true;     // superblock pruning of k_coarse (LGS_OPT_SUPER_PRUNE)
     bool super_quad = true;      // k_super_quad (8-byte superblock gathers) where it applies (LGS_OPT_SUPER_QUAD)
     int lanes_min_batch = 2;     // pruned coarse stage: k_coarse_lanes from this batch size on (LGS_OPT_LANES_MIN_BATCH)
+    long long ray_chunk_keys = 1LL << 28;  // ray-cast keys per emit/sort/apply pass (LGS_OPT_RAY_CHUNK_KEYS)
     // Stamps come from one process-wide counter: a context's scratch may be
     // memory a destroyed context used, and its stale tags must never match.
     int next_stamp();
@@ -374,5 +376,10 @@ int guarded(lgs_ctx* ctx, F&& f)
         return LGS_ERR_INTERNAL;
     }
 }
+
+// f(i) for i in [0, n) on a persistent pool of host threads (at most 16
+// including the caller; at most ceil(n / grain) of them).  f must not throw.
+// One parallel region runs at a time; nested calls run inline.
+void host_parallel_for(int n, int grain, const std::function<void(int)>& f);
 
 }  // namespace lgs

@@ -294,6 +294,56 @@ void GridMapHip::ConstructMapFromScans(const std::vector<ScanDataPtr>& scans,
                 "lgs_map_construct_from_scans");
 }
 
+static void scan_arrays(const std::vector<ScanDataPtr>& scans, const std::vector<RobotPose2D<double>>& poses,
+                        std::vector<const lgs_scan*>& hs, std::vector<lgs_pose2d>& ps, const char* what)
+{
+    if (scans.size() != poses.size()) throw Error(LGS_ERR_INVALID_ARG, std::string(what) + ": size mismatch");
+    for (std::size_t i = 0; i < scans.size(); ++i) {
+        hs.push_back(scans[i]->Handle());
+        ps.push_back(to_c(poses[i]));
+    }
+}
+
+void GridMapHip::ConstructMapsFromScans(const std::vector<GridMapHip*>& maps, const std::vector<int>& nodeIdxMin,
+                                        const std::vector<int>& nodeIdxMax, const std::vector<ScanDataPtr>& scans,
+                                        const std::vector<RobotPose2D<double>>& poses,
+                                        const GridMapBuilderParams& p)
+{
+    if (maps.empty()) return;
+    if (nodeIdxMin.size() != maps.size() || nodeIdxMax.size() != maps.size())
+        throw Error(LGS_ERR_INVALID_ARG, "ConstructMapsFromScans: size mismatch");
+    std::vector<const lgs_scan*> hs;
+    std::vector<lgs_pose2d> ps;
+    scan_arrays(scans, poses, hs, ps, "ConstructMapsFromScans");
+    std::vector<lgs_map*> ms;
+    for (GridMapHip* m : maps) {
+        if (!m || m->mDev != maps[0]->mDev)
+            throw Error(LGS_ERR_INVALID_ARG, "ConstructMapsFromScans: maps of one device");
+        ms.push_back(m->mMap);
+    }
+    const lgs_builder_params bp = bp_of(p);
+    const DevicePtr& dev = maps[0]->mDev;
+    dev->Check(lgs_maps_construct_from_scans(dev->Handle(), ms.data(), nodeIdxMin.data(), nodeIdxMax.data(),
+                                             (int)ms.size(), hs.data(), ps.data(), (int)hs.size(), &bp),
+               "lgs_maps_construct_from_scans");
+}
+
+std::unique_ptr<GridMapHip> GridMapHip::ConstructGlobalMap(DevicePtr dev, double resolution, int patchSize,
+                                                           const std::vector<ScanDataPtr>& scans,
+                                                           const std::vector<RobotPose2D<double>>& poses,
+                                                           const GridMapBuilderParams& p)
+{
+    std::vector<const lgs_scan*> hs;
+    std::vector<lgs_pose2d> ps;
+    scan_arrays(scans, poses, hs, ps, "ConstructGlobalMap");
+    const lgs_builder_params bp = bp_of(p);
+    lgs_map* m = nullptr;
+    dev->Check(lgs_map_construct_global(dev->Handle(), resolution, patchSize, hs.data(), ps.data(), (int)hs.size(),
+                                        &bp, &m),
+               "lgs_map_construct_global");
+    return std::unique_ptr<GridMapHip>(new GridMapHip(std::move(dev), m));
+}
+
 lgs_map_geometry GridMapHip::Geometry() const
 {
     lgs_map_geometry g{};

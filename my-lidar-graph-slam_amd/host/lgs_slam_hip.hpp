@@ -267,12 +267,26 @@ public:
     void ConstructMapFromScans(const std::vector<ScanDataPtr>& scans,
                                const std::vector<RobotPose2D<double>>& robotPoses,
                                const GridMapBuilderParams& p);
+    // GridMapBuilder::AfterLoopClosure's rebuild of every local map
+    // (C/mapping/grid_map_builder.cpp:62-80): maps[i] from the pose-graph
+    // nodes nodeIdxMin[i]..nodeIdxMax[i] of (scans, robotPoses), one fused
+    // device pass for all maps.
+    static void ConstructMapsFromScans(const std::vector<GridMapHip*>& maps, const std::vector<int>& nodeIdxMin,
+                                       const std::vector<int>& nodeIdxMax, const std::vector<ScanDataPtr>& scans,
+                                       const std::vector<RobotPose2D<double>>& robotPoses,
+                                       const GridMapBuilderParams& p);
+    // GridMapBuilder::ConstructGlobalMap (C/mapping/grid_map_builder.cpp:83-95)
+    static std::unique_ptr<GridMapHip> ConstructGlobalMap(DevicePtr dev, double resolution, int patchSize,
+                                                          const std::vector<ScanDataPtr>& scans,
+                                                          const std::vector<RobotPose2D<double>>& robotPoses,
+                                                          const GridMapBuilderParams& p);
     lgs_map_geometry Geometry() const;
     // non-owning view of the current cells (valid until the next geometry change)
     DeviceGridPtr Grid() const;
     void Download(std::vector<double>* cells, std::vector<uint32_t>* hits, std::vector<uint32_t>* misses) const;
 
 private:
+    GridMapHip(DevicePtr dev, lgs_map* map) : mDev(std::move(dev)), mMap(map) {}
     DevicePtr mDev;
     lgs_map* mMap = nullptr;
 };

@@ -27,6 +27,7 @@ LGS_OPT_SPIN_SYNC = 8
 LGS_OPT_SUPER_PRUNE = 9
 LGS_OPT_LANES_MIN_BATCH = 11
 LGS_OPT_SUPER_QUAD = 12
+LGS_OPT_RAY_CHUNK_KEYS = 13
 LGS_OPT_SKIP_MASK = 10   # diagnostics only
 KERNEL_IDS = ["k_project", "k_coarse", "k_seed", "k_select", "k_fine", "k_replay", "k_cost", "k_precompute",
               "k_linsolve", "k_ray_emit", "k_ray_apply", "k_super", "k_super_planes", "k_bb_score",
@@ -203,6 +204,11 @@ _PROTOS = [
     ("lgs_map_update_scan", C.c_int, [_P, _P, _P, Pose2D, C.POINTER(BuilderParams)]),
     ("lgs_map_construct_from_scans", C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(Pose2D), C.c_int,
                                                C.POINTER(BuilderParams)]),
+    ("lgs_maps_construct_from_scans", C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                                C.c_int, C.POINTER(_P), C.POINTER(Pose2D), C.c_int,
+                                                C.POINTER(BuilderParams)]),
+    ("lgs_map_construct_global", C.c_int, [_P, C.c_double, C.c_int, C.POINTER(_P), C.POINTER(Pose2D), C.c_int,
+                                           C.POINTER(BuilderParams), C.POINTER(_P)]),
     ("lgs_map_download", C.c_int, [_P, _P, C.POINTER(C.c_double), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32)]),
     ("lgs_grid_precompute_pyramid", C.c_int, [_P, _P, C.c_int, C.POINTER(_P)]),
@@ -476,6 +482,28 @@ class Context:
         h = _P()
         self.check(self.lib.lgs_map_create(self.h, res, patch_size, ncx, ncy, center[0], center[1],
                                            C.byref(h)), "map_create")
+        return Map(self, h)
+
+    def construct_maps(self, maps, ranges, scans, poses, bp: "BuilderParams"):
+        """GridMapBuilder::AfterLoopClosure's rebuild: maps[i] from pose-graph
+        nodes ranges[i] = (idx_min, idx_max) inclusive; node k = (scans[k], poses[k])."""
+        nm, n = len(maps), len(scans)
+        mh = (_P * nm)(*[m.h for m in maps])
+        lo = (C.c_int * nm)(*[int(a) for a, _ in ranges])
+        hi = (C.c_int * nm)(*[int(b) for _, b in ranges])
+        arr = (_P * n)(*[s.h for s in scans])
+        ps = (Pose2D * n)(*[Pose2D(*p) for p in poses])
+        self.check(self.lib.lgs_maps_construct_from_scans(self.h, mh, lo, hi, nm, arr, ps, n, C.byref(bp)),
+                   "maps_construct_from_scans")
+
+    def construct_global_map(self, res: float, patch_size: int, scans, poses, bp: "BuilderParams") -> "Map":
+        """GridMapBuilder::ConstructGlobalMap: a new map from all nodes."""
+        n = len(scans)
+        arr = (_P * n)(*[s.h for s in scans])
+        ps = (Pose2D * n)(*[Pose2D(*p) for p in poses])
+        h = _P()
+        self.check(self.lib.lgs_map_construct_global(self.h, res, patch_size, arr, ps, n, C.byref(bp), C.byref(h)),
+                   "map_construct_global")
         return Map(self, h)
 
     def cost_greedy_endpoint(self, grid, cost: CostGEParams, scan, pose) -> float:

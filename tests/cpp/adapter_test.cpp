@@ -165,6 +165,41 @@ int main()
               "GridMapHip::ConstructMapFromScans == oracle");
     }
 
+    // ---- AfterLoopClosure (two local maps, overlapping node ranges) and ConstructGlobalMap
+    {
+        std::vector<orc_scan> oss;
+        for (std::size_t k = 0; k < scans.size(); ++k) oss.push_back(oscan(*scans[k]));
+        auto oracle_construct = [&](orc_map* o, int lo, int hi) {
+            std::vector<orc_node> nodes;
+            for (int k = lo; k <= hi; ++k) nodes.push_back({ { poses[k].mX, poses[k].mY, poses[k].mTheta }, oss[k] });
+            orc_construct_map_from_scans(o, nodes.data(), (int)nodes.size(), &obp);
+        };
+        auto same = [](const GridMapHip& g, const orc_map& o) {
+            std::vector<double> c;
+            std::vector<uint32_t> h, m;
+            g.Download(&c, &h, &m);
+            const lgs_map_geometry geo = g.Geometry();
+            const std::size_t n = (std::size_t)o.w * o.h;
+            return geo.num_cells_x == o.w && geo.num_cells_y == o.h && geo.min_x == o.min_x &&
+                   geo.min_y == o.min_y && c.size() == n && std::memcmp(c.data(), o.cells, n * sizeof(double)) == 0 &&
+                   std::memcmp(h.data(), o.hit_count, n * 4) == 0 && std::memcmp(m.data(), o.miss_count, n * 4) == 0;
+        };
+        GridMapHip second(dev, 0.05, 64, 0, 0, poses[2]);
+        orc_map o2{};
+        orc_map_init(&o2, 0.05, 64, 0, 0, poses[2].mX, poses[2].mY);
+        GridMapHip::ConstructMapsFromScans({ &local, &second }, { 0, 2 }, { 5, 3 }, scans, poses, bp);
+        oracle_construct(&om, 0, 5);
+        oracle_construct(&o2, 2, 3);
+        check(same(local, om) && same(second, o2), "GridMapHip::ConstructMapsFromScans (AfterLoopClosure) == oracle");
+        auto global = GridMapHip::ConstructGlobalMap(dev, 0.05, 64, scans, poses, bp);
+        orc_map og{};
+        orc_map_init(&og, 0.05, 64, 0, 0, 0.0, 0.0);
+        oracle_construct(&og, 0, 5);
+        check(same(*global, og), "GridMapHip::ConstructGlobalMap == oracle");
+        orc_map_free(&o2);
+        orc_map_free(&og);
+    }
+
     // ---- ScanMatcherRealTimeCorrelativeHip::OptimizePose(query) on the latest map
     const auto cost = CostGreedyEndpointParams::FromLauncherJson(0.01, 20.0, 0.075, 0.1, 1, 0.05, 1.0);
     auto rtc = std::make_shared<ScanMatcherRealTimeCorrelativeHip>(dev, cost, 5, 0.6, 0.6, 0.4, 20.0);

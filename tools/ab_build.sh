@@ -7,7 +7,7 @@ name=$1; shift
 OUT=../../tools/exp/ab_$name
 mkdir -p $OUT
 FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -fno-fast-math -fno-gpu-rdc -I../../include -I. $*"
-for f in lgs_core k_rtcsm k_raycast k_linsolve; do
+for f in lgs_core k_rtcsm k_raycast k_linsolve k_bb; do
   /opt/rocm/bin/hipcc $FLAGS -c -o $OUT/$f.o $f.hip &
 done
 wait
