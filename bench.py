@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--latency-calls", type=int, default=100,
                     help="match workload: lone OptimizePose(query) calls timed for p50/p90 (0 = skip, e.g. under "
                          "rocprofv3 so that the trace holds the batched launches only)")
+    ap.add_argument("--interp", type=int, default=1,
+                    help="stream workload: 1 (default, the launcher's UseScanInterpolator) interpolates every "
+                         "scan (lgs_scan_interpolate, DistScans 0.05 / DistThresholdEmpty 0.25), 0 raw scans")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
     ap.add_argument("--timed-events", default="dominant", choices=["dominant", "all", "none"],
                     help="HIP-event timing inside the timed region: the roofline kernel only (default), "
@@ -557,15 +560,25 @@ def run_stream(args, D, ctx):
     P, cost = abi.RtcsmParams(5, 0.2, 0.2, 0.5, 20.0), abi.CostGEParams(*COST)   # JSON frontend window
     local = ctx.map(0.05, 100, 200, 200, center=truths[0][:2])
     latest = ctx.map(0.05, 100, 200, 200, center=truths[0][:2])
-    dscans = [ctx.scan(r, ang) for r in ranges]
+    raw = [ctx.scan(r, ang) for r in ranges]
+    dscans = [None] * n
+
+    def frontend_scan(k):   # ScanInterpolator::Interpolate (launcher default on)
+        dscans[k] = ctx.interpolate(raw[k], 0.05, 0.25) if args.interp else raw[k]
+
+    frontend_scan(0)
     est = [truths[0]]
     local.update_scan(dscans[0], est[0], bp)
 
+    def odometry(rng_, last):
+        # the true relative motion + noise, composed onto the last estimate
+        d = (0.1 + rng_.normal(0, 0.01), rng_.normal(0, 0.01), 0.02 + rng_.normal(0, 0.005))
+        c, s = np.cos(last[2]), np.sin(last[2])
+        return (last[0] + c * d[0] - s * d[1], last[1] + s * d[0] + c * d[1], last[2] + d[2])
+
     def step(k):
-        # odometry: the true relative motion + noise, composed onto the last estimate
-        d = (0.1 + rng.normal(0, 0.01), rng.normal(0, 0.01), 0.02 + rng.normal(0, 0.005))
-        c, s = np.cos(est[-1][2]), np.sin(est[-1][2])
-        guess = (est[-1][0] + c * d[0] - s * d[1], est[-1][1] + s * d[0] + c * d[1], est[-1][2] + d[2])
+        guess = odometry(rng, est[-1])
+        frontend_scan(k)
         lo = max(0, k - 10)
         latest.construct(dscans[lo:k], est[lo:k], bp)                       # UpdateLatestMap (10 scans)
         out = ctx.optimize_pose_query(latest.grid(), P, cost, dscans[k], guess)
@@ -586,15 +599,57 @@ def run_stream(args, D, ctx):
     steps = n - args.warmup - 1
     drift = max(abs(est[-1][0] - truths[len(est) - 1][0]), abs(est[-1][1] - truths[len(est) - 1][1]))
     value = steps * D.world / elapsed
+    cpu = None
+    if D.rank == 0 and not args.no_cpu and D.world == 1:
+        # the same frontend through the oracle from step 1 (same odometry draws):
+        # its poses must equal the GPU run's, step for step
+        ob = oracle_lib()
+        orng = np.random.default_rng(7)
+        obp = ob.BuilderParams(*BUILDER)
+        oprm, ocost = ob.RtcsmParams(5, 0.2, 0.2, 0.5, 20.0), ob.CostGE(*COST)
+        olocal = ob.OMap(0.05, 100, 200, 200, center=truths[0][:2])
+        olatest = ob.OMap(0.05, 100, 200, 200, center=truths[0][:2])
+
+        def oscan(k):
+            r, a = ob.scan_interpolate(ranges[k], ang, 0.05, 0.25) if args.interp else (ranges[k], ang)
+            return ob.OScan(r, a)
+
+        oscans = [oscan(0)]
+        oest = [truths[0]]
+        olocal.integrate(oest[0], oscans[0], obp)
+        times = []
+        t_start = time.perf_counter()
+        for k in range(1, n):
+            t1 = time.perf_counter()
+            guess = odometry(orng, oest[-1])
+            oscans.append(oscan(k))
+            lo = max(0, k - 10)
+            olatest.construct(oest[lo:k], oscans[lo:k], obp)
+            g = olatest.geometry()
+            og = ob.OGrid(olatest.cells(), g["min_x"], g["min_y"], 0.05)
+            out = ob.Summary()
+            ob.lib().orc_rtcsm_optimize_pose_query(C.byref(og.g), C.byref(oprm), C.byref(ocost),
+                                                   C.byref(oscans[k].s), ob.Pose(*guess), C.byref(out))
+            e = out.estimated_pose
+            oest.append((e.x, e.y, e.theta))
+            olocal.integrate(oest[-1], oscans[k], obp)
+            times.append(time.perf_counter() - t1)
+            if time.perf_counter() - t_start > args.cpu_seconds and len(times) >= 3:
+                break
+        same = all(tuple(a) == tuple(b) for a, b in zip(oest, est))
+        cpu = dict(value=round(len(times) / sum(times), 3), unit="scans/s", cores=1, kind="port",
+                   sample=f"the first {len(times)} frontend steps through the oracle (interpolate, 10-scan "
+                          f"ConstructMapFromScans, OptimizePose(query), insert; 1 thread); poses identical to "
+                          f"the GPU run's for all of them: {same}")
     line = dict(
         metric="frontend scans/sec: match vs latest map + local-map insert + latest-map rebuild, 1081 beams",
         value=round(value, 2), unit="scans/s", n_gpus=D.world, steps=steps, warmup=args.warmup,
         ms_per_step=round(1e3 * elapsed / steps, 4), higher_is_better=True, scaling="weak", vs_baseline=None,
         dtype="f64", data="synthetic circular trajectory, odometry noise (0.01 m, 0.005 rad)",
         config=dict(workload="config4: streaming frontend (JSON window 0.2/0.2/0.5)", beams=1081,
-                    latest_map_scans=10, parallelism=f"replicas x{D.world}"),
+                    scan_interpolator=bool(args.interp), latest_map_scans=10, parallelism=f"replicas x{D.world}"),
         final_drift_m=round(float(drift), 4),
-        roofline=roofline_from(stats, "k_ray_apply", args.pmc), cpu_baseline=None)
+        roofline=roofline_from(stats, "k_ray_apply", args.pmc), cpu_baseline=cpu)
     return line, stats, value
 
 

@@ -34,6 +34,8 @@
  *                                C/mapping/grid_map_builder.cpp:149-186
  *   lgs_map_construct_from_scans GridMapBuilder::ConstructMapFromScans
  *                                C/mapping/grid_map_builder.cpp:227-332 (UpdateLatestMap :196-207)
+ *   lgs_scan_interpolate         ScanInterpolator::Interpolate
+ *                                C/mapping/scan_interpolator.cpp:9-98
  *   lgs_maps_construct_from_scans GridMapBuilder::AfterLoopClosure's rebuild of every
  *                                local map C/mapping/grid_map_builder.cpp:62-80
  *   lgs_map_construct_global     GridMapBuilder::ConstructGlobalMap
@@ -196,6 +198,18 @@ int  lgs_grid_precompute_max(lgs_ctx* ctx, const lgs_grid* in, int win, lgs_grid
 /* ---- scans: uploaded once, resident in HBM ---- */
 int  lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* host, lgs_scan** out);
 void lgs_scan_destroy(lgs_scan* scan);
+/* Number of beams, and (if the pointers are non-null) a copy of the ranges and
+ * angles of `scan` into caller arrays of at least that many doubles. */
+int  lgs_scan_get(const lgs_scan* scan, int* n, double* ranges, double* angles);
+/* ScanInterpolator::Interpolate (C/mapping/scan_interpolator.cpp:9-98): a new
+ * device-resident scan whose points are spaced dist_scans apart along the
+ * polyline of `in`'s points, except across gaps of >= dist_threshold_empty
+ * (launcher JSON "ScanInterpolator": DistScans 0.05, DistThresholdEmpty 0.25).
+ * The relative sensor pose and min/max range are copied.  The recurrence is
+ * sequential and uses glibc sincos/atan2/sqrt, so it runs on the host; the
+ * result is uploaded once, like lgs_scan_create. */
+int  lgs_scan_interpolate(lgs_ctx* ctx, const lgs_scan* in, double dist_scans, double dist_threshold_empty,
+                          lgs_scan** out);
 
 /* ---- correlative scan matcher ---- */
 int  lgs_rtcsm_optimize_pose(lgs_ctx* ctx, const lgs_grid* grid, const lgs_grid* coarse,

@@ -742,6 +742,72 @@ extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan**
     });
 }
 
+extern "C" int lgs_scan_get(const lgs_scan* s, int* n, double* ranges, double* angles)
+{
+    if (!s || !n) return LGS_ERR_INVALID_ARG;
+    *n = s->n;
+    if (ranges) std::memcpy(ranges, s->h_ranges.data(), sizeof(double) * (size_t)s->n);
+    if (angles) std::memcpy(angles, s->h_angles.data(), sizeof(double) * (size_t)s->n);
+    return LGS_OK;
+}
+
+// ScanInterpolator::Interpolate (C/mapping/scan_interpolator.cpp:9-98).  The
+// walk along the polyline carries (previous point, accumulated distance) from
+// point to point and revisits a point after each inserted one, so it is a
+// sequential recurrence; it stays on the host with glibc's sincos (the
+// reference's ToCartesianCoordinate sin/cos pair, H/util.hpp:148-152, fused by
+// GCC), sqrt and atan2 (ToPolarCoordinate :156-161) for bit-exact points.
+extern "C" int lgs_scan_interpolate(lgs_ctx* ctx, const lgs_scan* in, double dist_scans,
+                                    double dist_threshold_empty, lgs_scan** out)
+{
+    if (!ctx || !in || !out) return LGS_ERR_INVALID_ARG;
+    *out = nullptr;
+    std::vector<double> rr, aa;
+    int rc = guarded(ctx, [&] {
+        LGS_REQUIRE(in->n >= 1, "scan must have >= 1 beam");
+        const int n = in->n;
+        std::vector<double> px(n), py(n);
+        for (int i = 0; i < n; ++i) {
+            double sn, cs;
+            ref_sincos(in->h_angles[i], sn, cs);
+            px[i] = in->h_ranges[i] * cs;
+            py[i] = in->h_ranges[i] * sn;
+        }
+        rr.reserve(2 * (size_t)n);
+        aa.reserve(2 * (size_t)n);
+        auto polar = [&](double x, double y) {
+            rr.push_back(std::sqrt(x * x + y * y));
+            aa.push_back(std::atan2(y, x));
+        };
+        polar(px[0], py[0]);
+        double qx = px[0], qy = py[0], acc = 0.0;  // previous point, distance walked since it
+        int i = 1;
+        while (i < n) {
+            const double dx = qx - px[i], dy = qy - py[i];
+            const double d = std::sqrt(dx * dx + dy * dy);  // Distance (H/point.hpp:113-117)
+            if (acc + d < dist_scans) {           // too close: walk on
+                acc += d;
+                qx = px[i], qy = py[i];
+                ++i;
+            } else if (acc + d >= dist_threshold_empty) {  // gap: keep the point as is
+                polar(px[i], py[i]);
+                qx = px[i], qy = py[i];
+                acc = 0.0;
+                ++i;
+            } else {                              // insert a point dist_scans along the segment
+                const double t = (dist_scans - acc) / d;
+                const double nx = (px[i] - qx) * t + qx, ny = (py[i] - qy) * t + qy;
+                polar(nx, ny);
+                qx = nx, qy = ny;
+                acc = 0.0;                        // and look at point i again
+            }
+        }
+    });
+    if (rc != LGS_OK) return rc;
+    const lgs_scan_host hs{ rr.data(), aa.data(), (int)rr.size(), in->rel, in->min_range, in->max_range };
+    return lgs_scan_create(ctx, &hs, out);
+}
+
 extern "C" void lgs_scan_destroy(lgs_scan* s)
 {
     if (!s) return;

@@ -107,9 +107,28 @@ ScanData::ScanData(DevicePtr dev, const std::vector<double>& angles, const std::
     mDev->Check(lgs_scan_create(mDev->Handle(), &h, &mScan), "lgs_scan_create");
 }
 
+ScanData::ScanData(DevicePtr dev, lgs_scan* adopted, const RobotPose2D<double>& relPose)
+    : mDev(std::move(dev)), mRelPose(relPose), mScan(adopted)
+{
+    int n = 0;
+    mDev->Check(lgs_scan_get(mScan, &n, nullptr, nullptr), "lgs_scan_get");
+    mRanges.resize(n);
+    mAngles.resize(n);
+    mDev->Check(lgs_scan_get(mScan, &n, mRanges.data(), mAngles.data()), "lgs_scan_get");
+}
+
 ScanData::~ScanData()
 {
     if (mScan) lgs_scan_destroy(mScan);
+}
+
+ScanDataPtr ScanInterpolatorHip::Interpolate(const ScanDataPtr& scanData) const
+{
+    if (!scanData) throw Error(LGS_ERR_INVALID_ARG, "Interpolate: null scan");
+    lgs_scan* out = nullptr;
+    mDev->Check(lgs_scan_interpolate(mDev->Handle(), scanData->Handle(), mDistScans, mDistThresholdEmpty, &out),
+                "lgs_scan_interpolate");
+    return ScanDataPtr(new ScanData(mDev, out, scanData->RelativeSensorPose()));
 }
 
 // ------------------------------------------------------ cost parameters

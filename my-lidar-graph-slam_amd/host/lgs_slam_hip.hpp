@@ -122,12 +122,28 @@ public:
     const lgs_scan* Handle() const { return mScan; }
 
 private:
+    friend class ScanInterpolatorHip;
+    ScanData(DevicePtr dev, lgs_scan* adopted, const RobotPose2D<double>& relPose);  // takes ownership
     DevicePtr mDev;
     std::vector<double> mAngles, mRanges;
     RobotPose2D<double> mRelPose;
     lgs_scan* mScan = nullptr;
 };
 using ScanDataPtr = std::shared_ptr<const ScanData>;
+
+// Mapping::ScanInterpolator (H/mapping/scan_interpolator.hpp,
+// C/mapping/scan_interpolator.cpp:9-98): the interpolated scan is created
+// device-resident directly.
+class ScanInterpolatorHip {
+public:
+    ScanInterpolatorHip(DevicePtr dev, double distScans = 0.05, double distThresholdEmpty = 0.25)
+        : mDev(std::move(dev)), mDistScans(distScans), mDistThresholdEmpty(distThresholdEmpty) {}
+    ScanDataPtr Interpolate(const ScanDataPtr& scanData) const;
+
+private:
+    DevicePtr mDev;
+    double mDistScans, mDistThresholdEmpty;
+};
 
 // H/mapping/scan_matcher.hpp:20-77
 struct ScanMatchingQuery {

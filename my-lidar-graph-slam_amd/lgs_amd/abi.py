@@ -196,6 +196,8 @@ _PROTOS = [
                                          C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     ("lgs_cost_greedy_endpoint", C.c_int, [_P, _P, C.POINTER(CostGEParams), _P, Pose2D,
                                            C.POINTER(C.c_double)]),
+    ("lgs_scan_get", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    ("lgs_scan_interpolate", C.c_int, [_P, _P, C.c_double, C.c_double, C.POINTER(_P)]),
     ("lgs_map_create", C.c_int, [_P, C.c_double, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
                                  C.POINTER(_P)]),
     ("lgs_map_destroy", None, [_P]),
@@ -340,6 +342,17 @@ class Context:
         s = _P()
         self.check(self.lib.lgs_scan_create(self.h, C.byref(hs), C.byref(s)), "scan_create")
         return Scan(self, s, r, a, rel_pose, min_range, max_range)
+
+    def interpolate(self, scan: "Scan", dist_scans: float = 0.05, dist_threshold_empty: float = 0.25) -> "Scan":
+        """ScanInterpolator::Interpolate: a new device scan (launcher defaults 0.05 / 0.25)."""
+        s = _P()
+        self.check(self.lib.lgs_scan_interpolate(self.h, scan.h, dist_scans, dist_threshold_empty, C.byref(s)),
+                   "scan_interpolate")
+        n = C.c_int()
+        self.check(self.lib.lgs_scan_get(s, C.byref(n), None, None), "scan_get")
+        r, a = np.zeros(n.value), np.zeros(n.value)
+        self.check(self.lib.lgs_scan_get(s, C.byref(n), dptr(r), dptr(a)), "scan_get")
+        return Scan(self, s, r, a, scan.rel_pose, scan.min_range, scan.max_range)
 
     # ---- matcher ----
     def optimize_pose(self, grid, coarse, params: RtcsmParams, cost: CostGEParams, scan, init,

@@ -1243,3 +1243,56 @@ int orc_linsolve_optimize_pose(const orc_grid* g, const orc_linsolve_params* p,
     orc_sq_covariance(g, p->cost_usable_range_min, p->cost_usable_range_max, scan, best, out->covariance);
     return 0;
 }
+
+/* ScanInterpolator::Interpolate, C/mapping/scan_interpolator.cpp:9-98.
+ * ToCartesianCoordinate H/util.hpp:148-152 (GCC fuses the sin/cos pair into
+ * sincos), Distance H/point.hpp:113-117, ToPolarCoordinate H/util.hpp:156-161. */
+int orc_scan_interpolate(const double* ranges, const double* angles, int n, double dist_scans,
+                         double dist_threshold_empty, double* out_ranges, double* out_angles, int cap)
+{
+    if (n < 1) return 0;
+    double* px = (double*)malloc(sizeof(double) * (size_t)n);
+    double* py = (double*)malloc(sizeof(double) * (size_t)n);
+    for (int i = 0; i < n; ++i) { /* :22-27 */
+        double s, c;
+        sincos(angles[i], &s, &c);
+        px[i] = ranges[i] * c;
+        py[i] = ranges[i] * s;
+    }
+    int m = 0;
+#define EMIT(X, Y)                                                     \
+    do {                                                               \
+        const double ex_ = (X), ey_ = (Y);                             \
+        if (m < cap) {                                                 \
+            out_ranges[m] = sqrt(ex_ * ex_ + ey_ * ey_);               \
+            out_angles[m] = atan2(ey_, ex_);                           \
+        }                                                              \
+        ++m;                                                           \
+    } while (0)
+    EMIT(px[0], py[0]); /* :30-31 */
+    double prevx = px[0], prevy = py[0], acc = 0.0;
+    for (int i = 1; i < n; ++i) { /* :37-68 */
+        const double x = px[i], y = py[i];
+        const double d = sqrt((prevx - x) * (prevx - x) + (prevy - y) * (prevy - y));
+        if (acc + d < dist_scans) {
+            acc += d;
+            prevx = x, prevy = y;
+        } else if (acc + d >= dist_threshold_empty) {
+            EMIT(x, y);
+            prevx = x, prevy = y;
+            acc = 0.0;
+        } else {
+            const double ratio = (dist_scans - acc) / d;
+            const double qx = (x - prevx) * ratio + prevx;
+            const double qy = (y - prevy) * ratio + prevy;
+            EMIT(qx, qy);
+            prevx = qx, prevy = qy;
+            acc = 0.0;
+            --i; /* process the current point again */
+        }
+    }
+#undef EMIT
+    free(px);
+    free(py);
+    return m;
+}

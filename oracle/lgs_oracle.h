@@ -225,6 +225,12 @@ void orc_sq_covariance(const orc_grid* g, double umin, double umax, const orc_sc
 /* colPivHouseholderQr().solve() restated for 3x3 (Eigen, not vendored) */
 void orc_solve3_colpiv_qr(const double H[9], const double b[3], double x[3]);
 
+/* ---- ScanInterpolator::Interpolate (C/mapping/scan_interpolator.cpp:9-98) ----
+ * n >= 1 input beams; writes at most cap output beams (range, angle) and
+ * returns the number the reference produces (may exceed cap: call again). */
+int orc_scan_interpolate(const double* ranges, const double* angles, int n, double dist_scans,
+                         double dist_threshold_empty, double* out_ranges, double* out_angles, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -165,6 +165,24 @@ int main()
               "GridMapHip::ConstructMapFromScans == oracle");
     }
 
+    // ---- ScanInterpolatorHip vs the oracle (launcher defaults 0.05 / 0.25)
+    {
+        const ScanInterpolatorHip interp(dev);
+        bool ok = true;
+        std::size_t total = 0;
+        for (const auto& sc : scans) {
+            const ScanDataPtr out = interp.Interpolate(sc);
+            std::vector<double> orr(4 * sc->NumOfScans() + 16), oa(orr.size());
+            const int m = orc_scan_interpolate(sc->Ranges().data(), sc->Angles().data(), (int)sc->NumOfScans(), 0.05,
+                                               0.25, orr.data(), oa.data(), (int)orr.size());
+            ok = ok && m == (int)out->NumOfScans() &&
+                 std::memcmp(orr.data(), out->Ranges().data(), sizeof(double) * m) == 0 &&
+                 std::memcmp(oa.data(), out->Angles().data(), sizeof(double) * m) == 0;
+            total += out->NumOfScans();
+        }
+        check(ok, "ScanInterpolatorHip::Interpolate == oracle", std::to_string(total) + " points from 6 scans");
+    }
+
     // ---- AfterLoopClosure (two local maps, overlapping node ranges) and ConstructGlobalMap
     {
         std::vector<orc_scan> oss;

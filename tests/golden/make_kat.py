@@ -253,6 +253,39 @@ def bb_search(grid, min_x, min_y, res, ranges, angles, sensor, H, rx, ry, rt, rm
     return dict(found=smax > thr, score=smax, best=best, win=[wx, wy, wt], step_t=step_t, visited=visited)
 
 
+def scan_interpolate(ranges, angles, dist_scans, dist_empty):
+    """ScanInterpolator::Interpolate (C/mapping/scan_interpolator.cpp:9-98):
+    ToCartesianCoordinate (H/util.hpp:148-152, a sin/cos pair -> sincos),
+    Distance (H/point.hpp:113-117), ToPolarCoordinate (H/util.hpp:156-161)."""
+    pts = []
+    for r, a in zip(ranges, angles):
+        sn, cs = sincos(a)
+        pts.append((r * cs, r * sn))
+    out = [pts[0]]
+    prev = pts[0]
+    acc = 0.0
+    i = 1
+    while i < len(ranges):
+        p = pts[i]
+        d = math.sqrt((prev[0] - p[0]) * (prev[0] - p[0]) + (prev[1] - p[1]) * (prev[1] - p[1]))
+        if acc + d < dist_scans:
+            acc += d
+            prev = p
+        elif acc + d >= dist_empty:
+            out.append(p)
+            prev = p
+            acc = 0.0
+        else:
+            ratio = (dist_scans - acc) / d
+            q = ((p[0] - prev[0]) * ratio + prev[0], (p[1] - prev[1]) * ratio + prev[1])
+            out.append(q)
+            prev = q
+            acc = 0.0
+            continue            # process point i again
+        i += 1
+    return ([math.sqrt(x * x + y * y) for x, y in out], [math.atan2(y, x) for x, y in out])
+
+
 def main():
     rnd = random.Random(1234)
     kat = {"_note": __doc__.strip().splitlines()[0]}
@@ -370,6 +403,25 @@ def main():
                    "res": 0.05, "range": [0.3, 0.2, 0.3], "scan_range_max": 20.0, "nthr": nthr,
                    "usable": [0.01, 20.0], **out})
     kat["bb_py"] = bb
+
+    # ScanInterpolator (DistScans / DistThresholdEmpty of the launcher JSON and others)
+    si = []
+    for case in range(8):
+        n = [1, 2, 37, 181, 361, 90, 50, 120][case]
+        a0, a1 = -math.pi / 2 * (1 + 0.5 * (case % 2)), math.pi / 2 * (1 + 0.5 * (case % 2))
+        angles = [a0 + (a1 - a0) * k / max(1, n - 1) for k in range(n)]
+        ranges = []
+        for k in range(n):
+            base = 1.0 + 0.8 * math.sin(0.05 * k * (case + 1))
+            ranges.append(base if rnd.random() > 0.1 else base * rnd.uniform(1.5, 4.0))   # gaps
+        if case == 6:
+            ranges = [0.5] * n                           # equal-range arc: spacing below DistScans
+        ds, de = [(0.05, 0.25), (0.05, 0.25), (0.05, 0.25), (0.05, 0.25), (0.1, 0.3), (0.02, 0.5),
+                  (0.05, 0.25), (0.03, 0.06)][case]
+        rr, aa = scan_interpolate(ranges, angles, ds, de)
+        si.append({"ranges": ranges, "angles": angles, "dist_scans": ds, "dist_empty": de,
+                   "out_ranges": rr, "out_angles": aa})
+    kat["interp_py"] = si
 
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump(kat, f, indent=None, separators=(",", ":"))

@@ -98,6 +98,8 @@ def lib():
         L.orc_bresenham.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_int), C.c_int]
         L.orc_precompute_grid_map.argtypes = [_D, C.c_int, C.c_int, C.c_int, _D]
         L.orc_bayes_update.restype = C.c_double
+        L.orc_scan_interpolate.restype = C.c_int
+        L.orc_scan_interpolate.argtypes = [_D, _D, C.c_int, C.c_double, C.c_double, _D, _D, C.c_int]
         L.orc_bayes_update.argtypes = [C.c_double, C.c_double]
         L.orc_rtcsm_search_step.argtypes = [C.c_double, C.POINTER(Scan), C.c_double, _D, _D, _D]
         L.orc_rtcsm_scan_indices.restype = C.c_int
@@ -180,6 +182,19 @@ def precompute(cells, win):
     out = np.zeros_like(c)
     lib().orc_precompute_grid_map(dp(c), w, h, int(win), dp(out))
     return out
+
+
+def scan_interpolate(ranges, angles, dist_scans, dist_empty):
+    """ScanInterpolator::Interpolate -> (ranges, angles) arrays."""
+    r = np.ascontiguousarray(ranges, dtype=np.float64)
+    a = np.ascontiguousarray(angles, dtype=np.float64)
+    cap = 4 * len(r) + 16
+    while True:
+        orr, oa = np.zeros(cap), np.zeros(cap)
+        m = lib().orc_scan_interpolate(dp(r), dp(a), len(r), dist_scans, dist_empty, dp(orr), dp(oa), cap)
+        if m <= cap:
+            return orr[:m], oa[:m]
+        cap = m
 
 
 def precompute_pyramid(cells, node_height_max):

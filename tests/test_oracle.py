@@ -101,6 +101,15 @@ def test_bb_search_kat(i):
     assert out.coarse_evals == c["visited"]
 
 
+@pytest.mark.parametrize("i", range(len(KAT["interp_py"])))
+def test_scan_interpolate_kat(i):
+    """ScanInterpolator::Interpolate against the pure-Python restatement (bit-exact)."""
+    c = KAT["interp_py"][i]
+    r, a = ob.scan_interpolate(c["ranges"], c["angles"], c["dist_scans"], c["dist_empty"])
+    assert r.tolist() == c["out_ranges"]
+    assert a.tolist() == c["out_angles"]
+
+
 def test_pyramid_is_precompute_per_height():
     rng = np.random.default_rng(3)
     grid = rng.choice([0.0, 0.0, 0.3, 0.8], size=(37, 50)) * rng.uniform(0.5, 1.0, size=(37, 50))
