@@ -45,6 +45,29 @@ bool precompute_planes_ok(const lgs_grid* in, int win);
 namespace {
 
 
+// Superblock plane element: fp16 (default) or fp32 (-DLGS_SUPER_F16=0), both
+// rounded toward +inf from the fp64 maxima, so every stored value is >= the
+// coarse values it bounds (the bound's sum is taken in fp64 either way).
+#ifndef LGS_SUPER_F16
+#define LGS_SUPER_F16 1
+#endif
+#if LGS_SUPER_F16
+typedef _Float16 SuperT;
+__device__ __forceinline__ SuperT super_round_up(double m)
+{
+    const float f = __double2float_ru(m);
+    SuperT h = (SuperT)f;  // nearest
+    if ((float)h < f) {    // one ulp up (f > 0 here: a negative cell disables the bounds)
+        unsigned short b = __builtin_bit_cast(unsigned short, h);
+        h = __builtin_bit_cast(SuperT, (unsigned short)(b + 1));
+    }
+    return h;
+}
+#else
+typedef float SuperT;
+__device__ __forceinline__ SuperT super_round_up(double m) { return __double2float_ru(m); }
+#endif
+
 constexpr int kPipe = 16;   // seq_sum gathers in flight per batch (index arrays padded by 2*kPipe)
 constexpr int kPad = 4 * kPipe;   // cbase padding past the last row (seq_sum4's look-ahead)
 
@@ -63,7 +86,7 @@ struct MatchItem {
     const double* ranges;
     const double* angles;
     const double* cmap;      // coarse map: padded phase planes (or the plain map)
-    const float* super;      // superblock planes of cmap (fp32, rounded up)
+    const SuperT* super;     // superblock planes of cmap (SuperT, rounded up)
     const int* negflag;      // stamped with pgen when the planes hold a negative cell
     int pgen;                // build stamp of the planes
     int gen;                 // this match's generation stamp
@@ -120,7 +143,7 @@ __device__ __forceinline__ Blk xcd_block()
 struct PlaneJob {
     RtcsmPlan pl;            // layout fields (Wqp, Hqp, pstride, pstride4, sub4, Wq4)
     const double* planes;
-    float* super;
+    SuperT* super;
     int* negflag;
     int pgen;
 };
@@ -624,7 +647,7 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
     const int plane = wg.z % nplanes;
     const RtcsmPlan& pl = job.pl;
     const double* __restrict__ P = job.planes;
-    float* __restrict__ S = job.super;
+    SuperT* __restrict__ S = job.super;
     int* __restrict__ negflag = job.negflag;
     const int pgen = job.pgen;
     const int Wqp = pl.Wqp, Hqp = pl.Hqp;
@@ -634,7 +657,7 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
     __shared__ double hm[TH][kSPX];
     const int x0 = wg.x * kSPX, y0 = wg.y * kSPY;
     const double* __restrict__ base = P + plane * pstride;
-    float* __restrict__ out = S + plane * pl.pstride4;
+    SuperT* __restrict__ out = S + plane * pl.pstride4;
     const int tid = threadIdx.x;
     bool neg = false;
     // all of a thread's loads issued before its LDS stores (a load-store loop
@@ -672,9 +695,9 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
         double m = hm[yy][xx];
 #pragma unroll
         for (int j = 1; j < kSB; ++j) m = dmax2(m, hm[yy + j][xx]);
-        // fp32 rounded toward +inf: still >= every member's coarse value, half
-        // the bytes for k_super's gathers
-        out[((y & 3) * 4 + (x & 3)) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + (x >> 2)] = __double2float_ru(m);
+        // rounded toward +inf: still >= every member's coarse value, a
+        // quarter (fp16) or half (fp32) of the bytes for k_super's gathers
+        out[((y & 3) * 4 + (x & 3)) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + (x >> 2)] = super_round_up(m);
     }
     if (neg) *negflag = pgen;
 }
@@ -696,8 +719,8 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
     const MatchItem& it = items[wg.z];
     const RtcsmPlan& pl = it.pl;
     if (wg.y >= pl.T) return;   // past this item's angles (uniform)
-    const float* __restrict__ sp = it.super;
-    const float* __restrict__ zf = (const float*)zero;
+    const SuperT* __restrict__ sp = it.super;
+    const SuperT* __restrict__ zf = (const SuperT*)zero;
     const int* __restrict__ cbase = it.cbase;
     const int* __restrict__ tedge = it.tedge;
     const int gen = it.gen;
@@ -716,7 +739,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
     const int sbi = wg.x * SPW + (lane & (SPW - 1));
     const bool act = sbi < nsb2;
     const int a = act ? sbi % pl.nsbx : 0, b = act ? sbi / pl.nsbx : 0;
-    const float* __restrict__ lb = sp + (b * pl.Wq4 + a);
+    const SuperT* __restrict__ lb = sp + (b * pl.Wq4 + a);
     LGS_PROBE_DECL;
     LGS_PROBE_MARK();
     const int* __restrict__ cbrow = cbase + pl.sb_off + (size_t)t * pl.Nv;
@@ -776,7 +799,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
 // aligned, which gfx950 global loads accept.  The odd tail superblock's pair
 // reads one float past its row: inside the padded planes (the allocation has
 // >= 256 B of slack) and never added.
-typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef SuperT f2a4 __attribute__((ext_vector_type(2), aligned(sizeof(SuperT))));
 constexpr int kQuadPipe = 8;
 __global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, const double* __restrict__ zero)
 {
@@ -784,7 +807,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, cons
     const MatchItem& it = items[wg.z];
     const RtcsmPlan& pl = it.pl;
     if (wg.y >= pl.T) return;   // past this item's angles (uniform)
-    const float* __restrict__ sp = it.super;
+    const SuperT* __restrict__ sp = it.super;
     const f2a4* __restrict__ z2 = (const f2a4*)zero;
     extern __shared__ int srow[];   // [Nv]
     __shared__ double red[kSupWaves][32];
@@ -795,7 +818,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, cons
     const int q = lane >> 4, idx = lane & 15;
     const bool act = idx < pl.nsby * np;
     const int b = act ? idx / np : 0, a0 = act ? 2 * (idx % np) : 0;
-    const float* __restrict__ lb = sp + (b * pl.Wq4 + a0);
+    const SuperT* __restrict__ lb = sp + (b * pl.Wq4 + a0);
     const int* __restrict__ cbrow = it.cbase + pl.sb_off + (size_t)t * pl.Nv;
     stage_lds(srow, cbrow, pl.Nv);
     __syncthreads();
@@ -2215,7 +2238,7 @@ inline size_t plane_bytes(const RtcsmPlan& pl)
 }
 inline size_t super_bytes(const RtcsmPlan& pl)
 {
-    return align256(sizeof(float) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4 + 64);   // + slack: k_super_quad reads one float past a row
+    return align256(sizeof(SuperT) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4 + 64);   // + slack: k_super_quad reads one float past a row
 }
 double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_super)
 {
@@ -2224,7 +2247,7 @@ double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_su
     // (k_super_planes writes every superblock-plane value; they are zeroed
     // with the planes only so that no stale value is ever read)
     const size_t sbytes = super_bytes(pl) * (size_t)nsets;
-    float* S = with_super ? (float*)ctx->ensure(S_SUPER, sbytes) : nullptr;
+    SuperT* S = with_super ? (SuperT*)ctx->ensure(S_SUPER, sbytes) : nullptr;
     const long long key[4] = { pl.low_res, pl.Wq, pl.Hq, pl.M };
     if (D != ctx->planes_ptr || std::memcmp(key, ctx->planes_key, sizeof(key)) != 0 || nsets > ctx->planes_sets ||
         (with_super && (S != ctx->super_ptr || nsets > ctx->super_sets))) {
@@ -2248,7 +2271,7 @@ struct PlaneSet {
     const lgs_grid* fine = nullptr;     // precompute from this fine map (OptimizePose(query))
     const lgs_grid* coarse = nullptr;   // or decimate this caller-supplied coarse map
     const double* cmap = nullptr;       // what k_coarse / k_seed_super read
-    const float* super = nullptr;
+    const SuperT* super = nullptr;
     const int* negflag = nullptr;
     int pgen = 0;
 };
@@ -2287,9 +2310,9 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
         return SetJobs{};
     }
     double* D = planes_buffer(ctx, lp, ns, need_super);
-    float* S = need_super ? (float*)ctx->ensure(S_SUPER, super_bytes(lp) * (size_t)ns) : nullptr;
+    SuperT* S = need_super ? (SuperT*)ctx->ensure(S_SUPER, super_bytes(lp) * (size_t)ns) : nullptr;
     int* neg = need_super ? (int*)ctx->ensure(S_NEGFLAG, sizeof(int) * (size_t)ns) : nullptr;
-    const size_t pb = plane_bytes(lp) / sizeof(double), sbb = super_bytes(lp) / sizeof(float);
+    const size_t pb = plane_bytes(lp) / sizeof(double), sbb = super_bytes(lp) / sizeof(SuperT);
     // fine maps with W, H multiples of LowRes: the precompute writes the
     // planes directly (one batched launch); other maps go through a plain
     // scratch map and the phase-plane copy, and supplied coarse maps through
