@@ -162,6 +162,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_SKIP_MASK     10  /* diagnostics only: bitmask of kernels (lgs_ctx_kernel_stats order) not launched -- results are invalid */
 #define LGS_OPT_SUPER_PRUNE   9   /* 1 (default) = skip coarse blocks whose 4x4-superblock bound is below the seed score, 0 = evaluate every coarse block */
 #define LGS_OPT_SUPER_QUAD    12  /* 1 (default) = superblock bounds with 8-byte gathers where the window allows, 0 = 4-byte (A/B) */
+#define LGS_OPT_SUPER_HEX     14  /* 1 (default) = superblock bounds with 4 fp16 superblocks per 8-byte gather where the window allows, 0 = k_super_quad (A/B) */
 #define LGS_OPT_RAY_CHUNK_KEYS 13  /* ray-cast keys per emit/sort/apply pass (default 2^28, max 2^30); more keys are cast in scan order over several passes */
 #define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: lane-per-block kernel for batches of at least this many matches (default 2; 1 = always), else the row kernel */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);

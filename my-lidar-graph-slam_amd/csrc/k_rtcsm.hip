@@ -880,6 +880,103 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, cons
     }
 }
 
+#if LGS_SUPER_F16
+// k_super_hex: k_super_quad with 8-byte gathers of FOUR fp16 superblocks
+// (a .. a + 3) of one row: a beam's 5 x 5 superblocks take 10 lanes, so one
+// wave instruction serves 6 beams (lanes 60..63 idle) instead of 4.  Used when
+// nsby * ceil(nsbx / 4) <= 10.  The beam slots are summed with shuffles
+// (slot q holds lanes 10 q .. 10 q + 9).  Tail elements past the row are read
+// from the padded planes (+ slack) and never added.
+typedef SuperT f4a2 __attribute__((ext_vector_type(4), aligned(sizeof(SuperT))));
+constexpr int kHexPipe = 8;
+__global__ __launch_bounds__(64 * kSupWaves) void k_super_hex(Items items, const double* __restrict__ zero)
+{
+    const Blk wg = xcd_block();
+    const MatchItem& it = items[wg.z];
+    const RtcsmPlan& pl = it.pl;
+    if (wg.y >= pl.T) return;   // past this item's angles (uniform)
+    const SuperT* __restrict__ sp = it.super;
+    const f4a2* __restrict__ z4 = (const f4a2*)zero;
+    extern __shared__ int srow[];   // [Nv]
+    __shared__ double red[kSupWaves][40];
+    const int t = wg.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nsbx = pl.nsbx, nsb2 = nsbx * pl.nsby;
+    const int np = (nsbx + 3) >> 2;
+    const int q = lane / 10, idx = lane - 10 * q;
+    const bool act = q < 6 && idx < pl.nsby * np;
+    const int b = act ? idx / np : 0, a0 = act ? 4 * (idx % np) : 0;
+    const SuperT* __restrict__ lb = sp + (b * pl.Wq4 + a0);
+    const int* __restrict__ cbrow = it.cbase + pl.sb_off + (size_t)t * pl.Nv;
+    stage_lds(srow, cbrow, pl.Nv);
+    __syncthreads();
+    const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
+    const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
+    const int* row = srow + lo;
+    const int n6 = (cnt + 5) / 6;   // beam slot q takes beams 6 i + q
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    for (int i0 = 0; i0 < n6; i0 += kHexPipe) {
+        f4a2 x[kHexPipe];
+#pragma unroll
+        for (int j = 0; j < kHexPipe; ++j) {
+            const int v = 6 * (i0 + j) + q;
+            const int c = (v < cnt) ? row[min(v, cnt - 1)] : 0;
+            x[j] = *((act && v < cnt) ? (const f4a2*)(lb + c) : z4);
+        }
+#pragma unroll
+        for (int j = 0; j < kHexPipe; ++j) {
+            s0 += (double)x[j].x;
+            s1 += (double)x[j].y;
+            s2 += (double)x[j].z;
+            s3 += (double)x[j].w;
+        }
+    }
+    // the 6 beam slots: lanes idx, idx + 10, ..., idx + 50 into slot 0
+    double r0 = s0, r1 = s1, r2 = s2, r3 = s3;
+#pragma unroll
+    for (int k = 1; k < 6; ++k) {
+        const int src = min(idx + 10 * k, 63);
+        r0 += __shfl(s0, src, 64);
+        r1 += __shfl(s1, src, 64);
+        r2 += __shfl(s2, src, 64);
+        r3 += __shfl(s3, src, 64);
+    }
+    if (q == 0) {
+        red[w][4 * idx] = r0;
+        red[w][4 * idx + 1] = r1;
+        red[w][4 * idx + 2] = r2;
+        red[w][4 * idx + 3] = r3;
+    }
+    __syncthreads();
+    if (w != 0) return;
+    const int sbi = lane;
+    const bool own = sbi < nsb2;
+    double tot = 0.0;
+    if (own) {
+        const int a = sbi % nsbx, bb = sbi / nsbx;
+        const int k = 4 * (bb * np + (a >> 2)) + (a & 3);
+        for (int j = 0; j < kSupWaves; ++j) tot += red[j][k];
+    }
+    const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult;
+    if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
+    const bool seedable = own && it.tedge[t] != it.gen;
+    double bv = seedable ? bound : -INFINITY;
+    long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(bv, off, 64);
+        const long long ok = __shfl_xor(bk, off, 64);
+        if (better(ov, ok, bv, bk)) {
+            bv = ov;
+            bk = ok;
+        }
+    }
+    if (lane == 0) {
+        it.part_c[t] = bv;
+        it.part_k[t] = bk;
+    }
+}
+#endif
+
 // k_coarse_rows (superblock pruning): coarse scores of the blocks k_select
 // could take; workgroup (angle t, patch row pr) of kRowWaves waves.  The
 // angle's superblocks are kept when bound > thr and (bound >= L, or the angle
@@ -2144,6 +2241,7 @@ struct BatchShape {
     int P = 0, nsb2 = 0, chunks = 0, low_res = 0, cb = 0;
     bool pair = false;
     bool quad = false;      // k_super_quad (nsby * ceil(nsbx / 2) <= 16; chunks == 1)
+    bool hex = false;       // k_super_hex (fp16 planes, nsby * ceil(nsbx / 4) <= 10; chunks == 1)
     bool planes = false;    // coarse map in padded phase planes
     bool pruned = false;    // superblock pruning
     bool lr5 = false;       // transposed LR = 5 evaluators
@@ -2456,7 +2554,9 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             const size_t lds = sizeof(int) * (size_t)std::max(B.NvMax, 1);
             dim3 g(B.chunks, B.Tmax, n);
             if (ctx->skipped(K_SUPER)) {
-            } else if (B.quad)
+            } else if (B.hex)
+                hipLaunchKernelGGL(k_super_hex, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+            else if (B.quad)
                 hipLaunchKernelGGL(k_super_quad, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else if (B.pair)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<1>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
@@ -2793,6 +2893,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     B.pair = B.nsb2 <= 32;
     B.chunks = B.pair ? 1 : (B.nsb2 + 63) / 64;
     B.quad = ctx->super_quad && p0.nsby * ((p0.nsbx + 1) / 2) <= 16;
+    B.hex = LGS_SUPER_F16 && ctx->super_hex && B.quad && p0.nsby * ((p0.nsbx + 3) / 4) <= 10;
     B.planes = ctx->coarse_planes;
     B.pruned = uses_super(ctx, B.NvMax, B.nsb2, false);
     B.lr5 = lr5_path(B.NvMax, B.low_res);

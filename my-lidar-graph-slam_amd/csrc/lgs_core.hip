@@ -289,6 +289,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_SUPER_PRUNE: ctx->super_prune = value != 0.0; return LGS_OK;
     case LGS_OPT_LANES_MIN_BATCH: ctx->lanes_min_batch = (int)value; return LGS_OK;
     case LGS_OPT_SUPER_QUAD: ctx->super_quad = value != 0.0; return LGS_OK;
+    case LGS_OPT_SUPER_HEX: ctx->super_hex = value != 0.0; return LGS_OK;
     case LGS_OPT_RAY_CHUNK_KEYS:
         if (!(value >= 1.0)) return LGS_ERR_INVALID_ARG;
         ctx->ray_chunk_keys = (long long)std::min(value, (double)(1LL << 30));
