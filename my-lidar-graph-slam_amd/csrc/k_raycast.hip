@@ -592,7 +592,7 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
 
 // Ray-cast every job's scans (already in its map's geometry), jobs in order,
 // each job's scans in order.  The rays of all jobs share emit/sort/apply
-// passes; a pass holds at most ctx->ray_chunk_keys keys and 2^32 cells of
+// passes; a pass holds at most ctx->ray_chunk_keys keys and 2^31 cells of
 // maps, and passes run in ray order, so each cell still sees its updates in
 // the reference's order.
 void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_params* bp)
