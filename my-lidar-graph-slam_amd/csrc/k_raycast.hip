@@ -91,59 +91,78 @@ struct RayMap {
 
 // One thread per ray: Bresenham walk (H/util.hpp:256-303), start cell
 // inclusive, end (hit) cell last.  rmap[r] names the ray's map (null: map 0).
+// The 64 rays of a workgroup (one wave) own one contiguous key range (their
+// offsets are consecutive), so when that range fits kEmitLds keys the walk
+// writes into LDS and the wave then copies the range out with coalesced
+// stores (one thread per ray writing its own run would touch 64 lines per
+// store instruction); longer ranges are written directly.
+#ifndef LGS_EMIT_LDS
+#define LGS_EMIT_LDS 8192
+#endif
+constexpr int kEmitLds = LGS_EMIT_LDS;
 __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
                                              const long long* __restrict__ offs,
                                              const int* __restrict__ rmap, int nrays,
-                                             const RayMap* __restrict__ maps,
+                                             long long nkeys, const RayMap* __restrict__ maps,
                                              unsigned* __restrict__ keys,
                                              int* __restrict__ outside)
 {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrays) return;
-    const int4 ry = rays[r];
-    const RayMap mp = maps[rmap ? rmap[r] : 0];
-    const int W = mp.w, H = mp.h;
-    const unsigned base = (unsigned)mp.base;
-    unsigned* out = keys + offs[r];
-    int deltaX = ry.z - ry.x;
-    int deltaY = ry.w - ry.y;
-    const int stepX = (deltaX < 0) ? -1 : 1;
-    const int stepY = (deltaY < 0) ? -1 : 1;
-    int nx = ry.x, ny = ry.y;
-    deltaX = abs(deltaX * 2);
-    deltaY = abs(deltaY * 2);
-    int bad = 0;
-    auto emit = [&](int x, int y, unsigned hit) {
-        const bool in = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
-        bad |= !in;
-        const unsigned cell = base + (in ? (unsigned)y * (unsigned)W + (unsigned)x : 0u);
-        *out++ = (cell << 1) | hit;
-    };
-    if (deltaX > deltaY) {
-        int err = deltaY - deltaX / 2;
-        while (nx != ry.z) {
-            emit(nx, ny, 0u);
-            if (err >= 0) {
-                ny += stepY;
-                err -= deltaX;
-            }
-            nx += stepX;
-            err += deltaY;
-        }
-    } else {
-        int err = deltaX - deltaY / 2;
-        while (ny != ry.w) {
-            emit(nx, ny, 0u);
-            if (err >= 0) {
+    __shared__ unsigned buf[kEmitLds > 0 ? kEmitLds : 1];
+    const int r0 = blockIdx.x * 64;
+    const int r = r0 + threadIdx.x;
+    const long long base = offs[r0];
+    const long long end = (r0 + 64 < nrays) ? offs[r0 + 64] : nkeys;
+    const bool staged = kEmitLds > 0 && end - base <= kEmitLds;   // uniform
+    if (r < nrays) {
+        const int4 ry = rays[r];
+        const RayMap mp = maps[rmap ? rmap[r] : 0];
+        const int W = mp.w, H = mp.h;
+        const unsigned cbase = (unsigned)mp.base;
+        unsigned* out = staged ? buf + (offs[r] - base) : keys + offs[r];
+        int deltaX = ry.z - ry.x;
+        int deltaY = ry.w - ry.y;
+        const int stepX = (deltaX < 0) ? -1 : 1;
+        const int stepY = (deltaY < 0) ? -1 : 1;
+        int nx = ry.x, ny = ry.y;
+        deltaX = abs(deltaX * 2);
+        deltaY = abs(deltaY * 2);
+        int bad = 0;
+        auto emit = [&](int x, int y, unsigned hit) {
+            const bool in = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
+            bad |= !in;
+            const unsigned cell = cbase + (in ? (unsigned)y * (unsigned)W + (unsigned)x : 0u);
+            *out++ = (cell << 1) | hit;
+        };
+        if (deltaX > deltaY) {
+            int err = deltaY - deltaX / 2;
+            while (nx != ry.z) {
+                emit(nx, ny, 0u);
+                if (err >= 0) {
+                    ny += stepY;
+                    err -= deltaX;
+                }
                 nx += stepX;
-                err -= deltaY;
+                err += deltaY;
             }
-            ny += stepY;
-            err += deltaX;
+        } else {
+            int err = deltaX - deltaY / 2;
+            while (ny != ry.w) {
+                emit(nx, ny, 0u);
+                if (err >= 0) {
+                    nx += stepX;
+                    err -= deltaY;
+                }
+                ny += stepY;
+                err += deltaX;
+            }
         }
+        emit(nx, ny, 1u);  // == (hx, hy): the hit cell, updated last
+        if (bad) atomicAdd(outside, 1);
     }
-    emit(nx, ny, 1u);  // == (hx, hy): the hit cell, updated last
-    if (bad) atomicAdd(outside, 1);
+    if (!staged) return;
+    __syncthreads();
+    const int n = (int)(end - base);
+    for (int j = threadIdx.x; j < n; j += 64) keys[base + j] = buf[j];
 }
 
 // k_runmask: one thread per sorted key; each wavefront covers 64 consecutive
@@ -750,7 +769,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
         // and written once; the run count is added after the last pass)
         int tok = ctx->timing_begin(K_RAY_EMIT, 4.0 * (double)keys);
         hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, st, d_rays, d_offs,
-                           d_rmap, (int)nr, d_maps, d_keys, d_bad);
+                           d_rmap, (int)nr, keys, d_maps, d_keys, d_bad);
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
         int cell_bits = 1;
