@@ -22,6 +22,7 @@
 #include "lgs_internal.hpp"
 
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <array>
@@ -609,6 +610,26 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
         }
 }
 
+// Stable sort of the 32-bit keys on the cell bits [1, 1 + cell_bits): hipcub's
+// default onesweep (8-bit digits), or rocprim onesweep with
+// LGS_RAY_RADIX_BITS-bit digits (A/B: fewer passes over ~22 cell bits).
+#ifndef LGS_RAY_RADIX_BITS
+#define LGS_RAY_RADIX_BITS 8
+#endif
+hipError_t ray_sort(void* temp, size_t& bytes, const unsigned* in, unsigned* out, long long n, int cell_bits,
+                    hipStream_t st)
+{
+#if LGS_RAY_RADIX_BITS == 8
+    return hipcub::DeviceRadixSort::SortKeys(temp, bytes, in, out, (int)n, 1, 1 + cell_bits, st);
+#else
+    using cfg = rocprim::radix_sort_config<
+        rocprim::default_config, rocprim::default_config,
+        rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<512, 12>,
+                                            LGS_RAY_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+    return rocprim::radix_sort_keys<cfg>(temp, bytes, in, out, (int)n, 1u, (unsigned)(1 + cell_bits), st);
+#endif
+}
+
 // Ray-cast every job's scans (already in its map's geometry), jobs in order,
 // each job's scans in order.  The rays of all jobs share emit/sort/apply
 // passes; a pass holds at most ctx->ray_chunk_keys keys and 2^31 cells of
@@ -775,11 +796,9 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
         int cell_bits = 1;
         while (cell_bits < 32 && (1ull << cell_bits) < cells) ++cell_bits;
         size_t tbytes = 0;
-        LGS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tbytes, d_keys, d_sorted, (int)keys, 1,
-                                                        1 + cell_bits, st));
+        LGS_HIP_CHECK(ray_sort(nullptr, tbytes, d_keys, d_sorted, keys, cell_bits, st));
         void* temp = ctx->ensure(S_RAY5, tbytes);
-        LGS_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp, tbytes, d_keys, d_sorted, (int)keys, 1,
-                                                        1 + cell_bits, st));
+        LGS_HIP_CHECK(ray_sort(temp, tbytes, d_keys, d_sorted, keys, cell_bits, st));
         tok = ctx->timing_begin(K_RAY_APPLY, 4.0 * (double)keys);
         if (tok >= 0) apply_tok = tok;
         const long long nw = (keys + 63) / 64;
