@@ -34,6 +34,7 @@
  *                                C/mapping/grid_map_builder.cpp:149-186
  *   lgs_map_construct_from_scans GridMapBuilder::ConstructMapFromScans
  *                                C/mapping/grid_map_builder.cpp:227-332 (UpdateLatestMap :196-207)
+ *   lgs_map_render_gray          MapSaver::DrawMap C/io/map_saver.cpp:276-313
  *   lgs_scan_interpolate         ScanInterpolator::Interpolate
  *                                C/mapping/scan_interpolator.cpp:9-98
  *   lgs_maps_construct_from_scans GridMapBuilder::AfterLoopClosure's rebuild of every
@@ -314,6 +315,13 @@ int  lgs_maps_construct_from_scans(lgs_ctx* ctx, lgs_map* const* maps, const int
 int  lgs_map_construct_global(lgs_ctx* ctx, double resolution, int patch_size,
                               const lgs_scan* const* scans, const lgs_pose2d* robot_poses, int n,
                               const lgs_builder_params* params, lgs_map** out);
+/* MapSaver::DrawMap (C/io/map_saver.cpp:276-313) over the whole map: one gray
+ * byte per cell, (uint8)((1 - p) * 255) for 0 < p <= 1 and 192 otherwise, rows
+ * flipped up-down as the reference writes its PNG (:455-456); image holds
+ * num_cells_x * num_cells_y bytes.  The reference crops the image to the
+ * allocated patches (GridMap::ComputeActualMapSize); the caller crops with
+ * the hit/miss counts if it needs that extent. */
+int  lgs_map_render_gray(lgs_ctx* ctx, const lgs_map* map, uint8_t* image);
 /* Copy cells and per-cell hit/miss update counts (since create/construct) to
  * the host; any pointer may be NULL.  Sizes: num_cells_x * num_cells_y. */
 int  lgs_map_download(lgs_ctx* ctx, const lgs_map* map, double* cells, uint32_t* hit_count,

@@ -379,6 +379,27 @@ __global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys
     mp.miss[local] += nm;
 }
 
+// MapSaver::DrawMap (C/io/map_saver.cpp:276-313) for every cell of the map:
+// gray = (uint8)((1 - p) * 255) for 0 < p <= 1, else the background 192;
+// rows flipped up-down as the PNG is written (:455-456).  One thread per
+// 4 consecutive cells of a row (4-byte stores).
+__global__ __launch_bounds__(256) void k_render_gray(const double* __restrict__ cells, int W, int H,
+                                                     uint8_t* __restrict__ img)
+{
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int qw = (W + 3) / 4;
+    if (q >= (long long)qw * H) return;
+    const int y = (int)(q / qw), x0 = (int)(q % qw) * 4;
+    uint8_t* row = img + (size_t)(H - 1 - y) * W;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int x = x0 + i;
+        if (x >= W) break;
+        const double v = cells[(size_t)y * W + x];
+        row[x] = (v <= 0.0 || v > 1.0) ? (uint8_t)192 : (uint8_t)((1.0 - v) * 255.0);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host: geometry restated from H/grid_map/grid_map.hpp
 // ---------------------------------------------------------------------------
@@ -994,6 +1015,24 @@ extern "C" int lgs_map_construct_global(lgs_ctx* ctx, double res, int ps, const 
     }
     *out = m;
     return LGS_OK;
+}
+
+extern "C" int lgs_map_render_gray(lgs_ctx* ctx, const lgs_map* m, uint8_t* image)
+{
+    if (!ctx || !m || !image) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        const size_t n = (size_t)m->w * m->h;
+        if (!n) return;
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        hipStream_t st = ctx->stream;
+        uint8_t* d_img = (uint8_t*)ctx->ensure(S_RAY2, n);
+        const long long threads = (long long)((m->w + 3) / 4) * m->h;
+        hipLaunchKernelGGL(k_render_gray, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, m->d_cells,
+                           m->w, m->h, d_img);
+        LGS_HIP_CHECK(hipGetLastError());
+        LGS_HIP_CHECK(hipMemcpyAsync(image, d_img, n, hipMemcpyDeviceToHost, st));
+        LGS_HIP_CHECK(hipStreamSynchronize(st));
+    });
 }
 
 extern "C" int lgs_map_download(lgs_ctx* ctx, const lgs_map* m, double* cells, uint32_t* hit,

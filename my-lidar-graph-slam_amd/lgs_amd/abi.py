@@ -212,6 +212,7 @@ _PROTOS = [
                                                 C.POINTER(BuilderParams)]),
     ("lgs_map_construct_global", C.c_int, [_P, C.c_double, C.c_int, C.POINTER(_P), C.POINTER(Pose2D), C.c_int,
                                            C.POINTER(BuilderParams), C.POINTER(_P)]),
+    ("lgs_map_render_gray", C.c_int, [_P, _P, C.POINTER(C.c_uint8)]),
     ("lgs_map_download", C.c_int, [_P, _P, C.POINTER(C.c_double), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32)]),
     ("lgs_grid_precompute_pyramid", C.c_int, [_P, _P, C.c_int, C.POINTER(_P)]),
@@ -591,6 +592,16 @@ class Map:
         ps = (Pose2D * n)(*[Pose2D(*p) for p in poses])
         self.ctx.check(self.ctx.lib.lgs_map_construct_from_scans(self.ctx.h, self.h, arr, ps, n, C.byref(bp)),
                        "map_construct_from_scans")
+
+    def render_gray(self) -> np.ndarray:
+        """MapSaver::DrawMap gray image (rows flipped up-down), uint8 [h, w]."""
+        g = self.geometry()
+        img = np.zeros((g["h"], g["w"]), dtype=np.uint8)
+        if img.size:
+            self.ctx.check(self.ctx.lib.lgs_map_render_gray(self.ctx.h, self.h,
+                                                            img.ctypes.data_as(C.POINTER(C.c_uint8))),
+                           "map_render_gray")
+        return img
 
     def download(self):
         g = self.geometry()

@@ -155,3 +155,17 @@ def test_long_runs(ctx, world, p_hit, p_miss):
     om.construct(poses, oscans, ob.BuilderParams(0.01, 20.0, p_hit, p_miss))
     same_map(gm, om, f"{p_hit}/{p_miss}")
     assert om.hits().max() >= 100 and om.misses().max() >= 1000
+
+
+def test_render_gray_matches_drawmap(ctx, world):
+    """f4: MapSaver::DrawMap's gray levels (C/io/map_saver.cpp:276-313) for every
+    cell, rows flipped up-down (:455-456); restated with numpy on the same
+    downloaded cells (truncating uint8 cast of (1 - p) * 255, 192 for p <= 0)."""
+    poses = _trajectory(20, seed=8)
+    dscans, _ = _nodes(ctx, world, poses, 361)
+    gm = ctx.construct_global_map(0.05, 64, dscans, poses, abi.BuilderParams(*BP))
+    cells, _, _ = gm.download()
+    img = gm.render_gray()
+    want = np.where((cells <= 0.0) | (cells > 1.0), 192, ((1.0 - cells) * 255.0).astype(np.uint8)).astype(np.uint8)
+    assert np.array_equal(img, want[::-1])
+    assert (img == 192).any() and (img < 192).any()
