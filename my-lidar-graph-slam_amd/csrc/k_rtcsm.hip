@@ -888,7 +888,10 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, cons
 // (slot q holds lanes 10 q .. 10 q + 9).  Tail elements past the row are read
 // from the padded planes (+ slack) and never added.
 typedef SuperT f4a2 __attribute__((ext_vector_type(4), aligned(sizeof(SuperT))));
-constexpr int kHexPipe = 8;
+#ifndef LGS_HEX_PIPE
+#define LGS_HEX_PIPE 16
+#endif
+constexpr int kHexPipe = LGS_HEX_PIPE;   // gathers in flight per lane
 __global__ __launch_bounds__(64 * kSupWaves) void k_super_hex(Items items, const double* __restrict__ zero)
 {
     const Blk wg = xcd_block();
