@@ -77,7 +77,12 @@ def parse():
     ap.add_argument("--interp", type=int, default=1,
                     help="stream workload: 1 (default, the launcher's UseScanInterpolator) interpolates every "
                          "scan (lgs_scan_interpolate, DistScans 0.05 / DistThresholdEmpty 0.25), 0 raw scans")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_pmc_summary.json"),
+                    help="rocprofv3 PMC summary (tools/pmc_summary.py) of THIS library build: roofline.traffic "
+                         "is taken from it only when its lib_sha256 matches liblgs_hip.so, else null")
+    ap.add_argument("--loop-line", type=int, default=1,
+                    help="match workload: also run config 5 (512 loop candidates sharded over the ranks, strong "
+                         "scaling) after the timed region and report it as 'config5_strong_scaling'")
     ap.add_argument("--timed-events", default="dominant", choices=["dominant", "all", "none"],
                     help="HIP-event timing inside the timed region: the roofline kernel only (default), "
                          "every kernel, or none (A/B of the event overhead)")
@@ -95,8 +100,11 @@ class Dist:
     LGS_BENCH_REHEARSE=1 (rehearsal of the multi-rank path on a one-GPU box):
     every rank uses GPU 0 and the collectives run over gloo on host tensors."""
 
-    def __init__(self):
+    def __init__(self, gpus: int = 1):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        if self.world != gpus:
+            sys.stderr.write(f"bench.py: --gpus {gpus} but WORLD_SIZE={self.world}\n")
+            sys.exit(2)
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.rehearse = os.environ.get("LGS_BENCH_REHEARSE") == "1"
@@ -152,24 +160,52 @@ class Dist:
             self.d.destroy_process_group()
 
 
-def roofline_from(stats, kernel, pmc_path):
+def lib_sha256() -> str:
+    import hashlib
+    with open(abi.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_for(pmc_path, trace_kernel):
+    """Counter bytes per launch of `trace_kernel` from a PMC summary of THIS
+    build (tools/pmc_summary.py records the library's sha256), else None.
+    gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads
+    (MI355X_MICROARCH.md §HBM): 'traffic' doubles it; the raw sum is kept too."""
+    try:
+        pmc = json.load(open(pmc_path))
+    except (OSError, ValueError):
+        return None
+    if pmc.get("lib_sha256") != lib_sha256():
+        return None
+    e = pmc.get("kernels", {}).get(trace_kernel)
+    if not e or "fetch_bytes_per_launch" not in e or "write_bytes_per_launch" not in e:
+        return None
+    return dict(traffic=2.0 * e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"],
+                raw=e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"], avg_us=e.get("avg_us"),
+                l2_hit_rate=e.get("l2_hit_rate"), profile=os.path.relpath(pmc_path, ROOT))
+
+
+def roofline_from(stats, kernel, pmc_path, trace_kernel, bound):
+    """Roofline of the dominant kernel: achieved = ALGORITHMIC bytes per launch
+     / event-timed average launch duration; frac against the
+    8 TB/s HBM peak.  frac_hbm_counters = the PMC-counted HBM bytes of the same
+    kernel (from this build's profile) over the same time; null without one."""
     k = stats.get(kernel)
     if not k or not k["launches"] or not k["algo_bytes"]:
         return None
     per_launch = k["algo_bytes"] / k["launches"]
     avg_ms = k["total_ms"] / k["launches"]
     achieved = per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            key = next((n for n in pmc if n.startswith(kernel)), None)
-            traffic = pmc[key].get("hbm_bytes_per_launch") if key else None
-        except Exception:
-            traffic = None
-    return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel=kernel,
-                avg_launch_ms=round(avg_ms, 5), algo_bytes_per_launch=per_launch)
+    p = pmc_for(pmc_path, trace_kernel)
+    traffic = round(p["traffic"]) if p else None
+    frac_hbm = round(traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if p else None
+    return dict(bound=bound, achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                frac_algorithmic=round(achieved / HBM_PEAK_GBS, 4), frac_hbm_counters=frac_hbm,
+                traffic_raw_fetch_plus_write=round(p["raw"]) if p else None,
+                l2_hit_rate=p["l2_hit_rate"] if p else None, pmc_profile=p["profile"] if p else None,
+                pmc_avg_launch_us=p["avg_us"] if p else None,
+                kernel=trace_kernel, avg_launch_ms=round(avg_ms, 5), algo_bytes_per_launch=per_launch)
 
 
 def set_timed_events(ctx, args, dominant):
@@ -263,7 +299,9 @@ def run_match(args, D, ctx):
     ang = scene.beam_angles(1081)
     cells, mx, my = bench_map(world, ang)
     rng = np.random.default_rng(1000 + D.rank)
-    scans, inits, truths = random_scans(world, ang, rng, min(args.warmup + args.steps, 256))
+    # a fixed set of 256 scans: the workload (and coarse_blocks_scored_mean) does
+    # not depend on --steps / --warmup
+    scans, inits, truths = random_scans(world, ang, rng, 256)
     S = max(1, args.streams)
     ctxs = [ctx] + [abi.Context(D.local) for _ in range(S - 1)]
     state = []
@@ -364,7 +402,7 @@ def run_match(args, D, ctx):
         rate, times = cpu_throughput(args.cpu_seconds, range(4 * T), one, T)
         cpu = dict(value=round(rate, 4), unit="scans/s", cores=T, kind="port",
                    sample=f"{len(times)} config-2 scans through the oracle's OptimizePose(query) (C restatement, "
-                          f"-O2 -ffp-contract=off) on {T} threads, one independent scan per thread; "
+                          f"-O3 -ffp-contract=off, the reference's -O3) on {T} threads, one independent scan per thread; "
                           f"single-scan p50 {1e3 * np.median(times):.1f} ms",
                    speedup=round(value / rate, 1),
                    single_core_scans_per_s=round(1.0 / float(np.median(times)), 4),
@@ -388,7 +426,7 @@ def run_match(args, D, ctx):
         p90_scan_match_ms=round(1e3 * float(np.percentile(lat1, 90)), 4) if lat1 else None,
         # latency of one batched call under the timed load
         p50_batch_call_ms=round(float(np.percentile(lat_ms, 50)), 4),
-        roofline=roofline_from(stats, "k_coarse", args.pmc), cpu_baseline=cpu,
+        roofline=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_lanes", "l2-gather"), cpu_baseline=cpu,
         pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events,
         super_prune=bool(args.super_prune),
         coarse_blocks_scored_mean=round(float(results[:, 4].mean()), 1),
@@ -545,7 +583,8 @@ def run_loop(args, D, ctx):
                               "config5: LoopDetectorRealTimeCorrelative::Detect batch"), candidates=len(cands),
                     found=found, parallelism=f"candidates sharded in contiguous blocks over {D.world} ranks + "
                                              "RCCL all-gather of 176-B result records"),
-        roofline=roofline_from(stats, dominant, args.pmc), cpu_baseline=cpu)
+        roofline=roofline_from(stats, dominant, args.pmc, "k_bb_score" if bb else "k_coarse_lanes", "l2-gather"),
+        cpu_baseline=cpu)
     return line, stats, value
 
 
@@ -652,7 +691,7 @@ def run_stream(args, D, ctx):
         config=dict(workload="config4: streaming frontend (JSON window 0.2/0.2/0.5)", beams=1081,
                     scan_interpolator=bool(args.interp), latest_map_scans=10, parallelism=f"replicas x{D.world}"),
         final_drift_m=round(float(drift), 4),
-        roofline=roofline_from(stats, "k_ray_apply", args.pmc), cpu_baseline=cpu)
+        roofline=roofline_from(stats, "k_ray_apply", args.pmc, "k_apply", "hbm"), cpu_baseline=cpu)
     return line, stats, value
 
 
@@ -715,19 +754,44 @@ def run_rebuild(args, D, ctx):
         config=dict(workload="f2: GridMapBuilder::AfterLoopClosure (all local maps, one fused ray-cast pass)",
                     nodes=n_nodes, local_maps=len(maps), beams=1081, parallelism=f"replicas x{D.world}"),
         global_map=dict(ms=round(global_ms, 3), cells=[gg["w"], gg["h"]], nodes=n_nodes),
-        roofline=roofline_from(stats, "k_ray_apply", args.pmc), cpu_baseline=cpu)
+        roofline=roofline_from(stats, "k_ray_apply", args.pmc, "k_apply", "hbm"), cpu_baseline=cpu)
     return line, stats, value
+
+
+def spawn_ranks(args) -> None:
+    """--gpus N without a launcher: start N ranks (one process per GPU) with
+    torch.distributed.run as a CHILD process, before anything here touches the
+    GPU, and exit with its status."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
 
 
 def main():
     args = parse()
-    D = Dist()
+    spawn_ranks(args)
+    D = Dist(args.gpus)
     ctx = abi.Context(D.local)
     line, stats, _ = dict(match=run_match, refine=run_refine, loop=run_loop, loop_bb=run_loop,
                           stream=run_stream, rebuild=run_rebuild)[args.workload](
         args, D, ctx)
     line["kernels"] = {k: dict(launches=v["launches"], avg_ms=round(v["total_ms"] / max(1, v["launches"]), 5))
                        for k, v in stats.items()}
+    if args.workload == "match" and args.loop_line:
+        # config 5 next to the config-2 replicas line: the 512 loop candidates
+        # split over the ranks (strong scaling), measured after the main timed region
+        la = argparse.Namespace(**vars(args))
+        la.workload, la.steps, la.warmup, la.no_cpu = "loop", 4, 1, True
+        ll, _, _ = run_loop(la, D, ctx)
+        line["config5_strong_scaling"] = {k: ll[k] for k in ("metric", "value", "unit", "n_gpus", "steps",
+                                                              "ms_per_step", "scaling", "config", "roofline")}
     if D.rank == 0:
         print(json.dumps(line), flush=True)
     D.close()

@@ -166,7 +166,16 @@ int  lgs_abi_version(void);
 #define LGS_OPT_SUPER_HEX     14  /* 1 (default) = superblock bounds with 4 fp16 superblocks per 8-byte gather where the window allows, 0 = k_super_quad (A/B) */
 #define LGS_OPT_RAY_CHUNK_KEYS 13  /* ray-cast keys per emit/sort/apply pass (default 2^28, max 2^30); more keys are cast in scan order over several passes */
 #define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: lane-per-block kernel for batches of at least this many matches (default 2; 1 = always), else the row kernel */
+#define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
+
+/* Diagnostics: copy one intermediate buffer of item 0 of the context's last
+ * correlative batch to `out` (at most cap bytes; *bytes = its full size).
+ * which: 0 sbound [T*nsb2 f64], 1 part_c [nparts f64], 2 part_k [nparts i64],
+ * 3 Lp at byte 0, Lc[4] f64 at byte 64, 4 tedge [T i32] (1 = flagged by
+ * the last enqueue of item 0, else 0), 5 cbase [2*(T*Nv+pad) i32],
+ * 6 idx [T*Nv int2], 7 cscore [K f64]. */
+int  lgs_debug_item_buffer(lgs_ctx* ctx, int which, void* out, size_t cap, size_t* bytes);
 
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is
  * the algorithmic byte count of DESIGN.md §Roofline (e.g. 8 B per coarse-score

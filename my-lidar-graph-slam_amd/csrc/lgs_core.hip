@@ -203,7 +203,8 @@ extern "C" int lgs_ctx_create(int device, lgs_ctx** out)
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&ctx->zero, 32 * sizeof(double)) != hipSuccess ||
-        hipMemset(ctx->zero, 0, 32 * sizeof(double)) != hipSuccess) {
+        hipMemsetAsync(ctx->zero, 0, 32 * sizeof(double), ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
         delete ctx;
         return LGS_ERR_HIP;
     }
@@ -295,6 +296,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
         ctx->ray_chunk_keys = (long long)std::min(value, (double)(1LL << 30));
         return LGS_OK;
     case LGS_OPT_SKIP_MASK: ctx->skip_mask = (unsigned)value; return LGS_OK;
+    case LGS_OPT_POISON_WS: ctx->poison_ws = value != 0.0; return LGS_OK;
     case LGS_OPT_GUARD_CAP:
         ctx->guard_cap = (int)value;
         if (ctx->guard_cap < 0) ctx->guard_cap = 0;

@@ -29,6 +29,7 @@ LGS_OPT_LANES_MIN_BATCH = 11
 LGS_OPT_SUPER_QUAD = 12
 LGS_OPT_RAY_CHUNK_KEYS = 13
 LGS_OPT_SUPER_HEX = 14
+LGS_OPT_POISON_WS = 15   # diagnostics only
 LGS_OPT_SKIP_MASK = 10   # diagnostics only
 KERNEL_IDS = ["k_project", "k_coarse", "k_seed", "k_select", "k_fine", "k_replay", "k_cost", "k_precompute",
               "k_linsolve", "k_ray_emit", "k_ray_apply", "k_super", "k_super_planes", "k_bb_score",
@@ -233,6 +234,7 @@ _PROTOS = [
                                                    C.POINTER(Pose2D), C.c_int, C.POINTER(LinsolveSummary)]),
     ("lgs_cost_square_error", C.c_int, [_P, _P, C.c_double, C.c_double, _P, Pose2D, C.POINTER(C.c_double),
                                         C.POINTER(C.c_double)]),
+    ("lgs_debug_item_buffer", C.c_int, [_P, C.c_int, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
 ]
 
 SYMBOLS = [p[0] for p in _PROTOS]
@@ -520,6 +522,21 @@ class Context:
         self.check(self.lib.lgs_map_construct_global(self.h, res, patch_size, arr, ps, n, C.byref(bp), C.byref(h)),
                    "map_construct_global")
         return Map(self, h)
+
+    DEBUG_BUFFERS = {"sbound": (0, np.float64), "part_c": (1, np.float64), "part_k": (2, np.int64),
+                     "L": (3, np.float64), "tedge": (4, np.int32), "cbase": (5, np.int32), "idx": (6, np.int32),
+                     "cscore": (7, np.float64)}
+
+    def debug_buffer(self, name: str) -> np.ndarray:
+        """Diagnostics: an intermediate buffer of item 0 of the last correlative
+        batch (lgs_debug_item_buffer); "L" = [Lp, pad x7, Lc0..Lc3]."""
+        which, dt = self.DEBUG_BUFFERS[name]
+        n = C.c_size_t()
+        self.check(self.lib.lgs_debug_item_buffer(self.h, which, None, 0, C.byref(n)), "debug_item_buffer")
+        out = np.zeros(n.value // np.dtype(dt).itemsize, dtype=dt)
+        self.check(self.lib.lgs_debug_item_buffer(self.h, which, out.ctypes.data_as(_P), out.nbytes, C.byref(n)),
+                   "debug_item_buffer")
+        return out
 
     def cost_greedy_endpoint(self, grid, cost: CostGEParams, scan, pose) -> float:
         v = C.c_double()

@@ -153,9 +153,9 @@ def test_query_batch_rejects_mixed_sizes(ctx, world):
 def test_query_planes_equal_supplied_coarse_planes(ctx, world, low_res, n_cells):
     """The query path writes the coarse planes straight from the batched
     precompute; OptimizePose with a caller coarse map builds them by the
-    phase-plane copy: identical results.  (The number of coarse blocks scored
-    is not compared: it varies between identical calls after some call
-    histories, in both superblock-plane precisions -- see DESIGN.md §4.1b.)"""
+    phase-plane copy: identical results, including the number of coarse
+    blocks the superblock pruning scored (the pruning is a function of the
+    call's inputs only)."""
     cells, mx, my = build_map(world, n_cells, 0.05, 100, scene.arc_poses(5), n_beams=541)
     rng = np.random.default_rng(low_res)
     ang, qs = _queries(world, rng, 4, 541)
@@ -168,4 +168,51 @@ def test_query_planes_equal_supplied_coarse_planes(ctx, world, low_res, n_cells)
         fused = ctx.optimize_pose_query(g, P, cost, sc, init)
         two = ctx.optimize_pose(g, cg, P, cost, sc, init, 2.2250738585072014e-308)
         assert list(fused.best_win) == list(two.best_win) and fused.score_max == two.score_max, j
+        assert fused.coarse_blocks == two.coarse_blocks, (j, fused.coarse_blocks, two.coarse_blocks)
         assert_same(fused, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"lr{low_res} q{j}")
+
+
+def _record(out):
+    return (out.pose_found, list(out.best_win), out.score_max, out.estimated_pose.tuple(), out.normalized_cost,
+            list(out.covariance), out.coarse_blocks, out.fine_blocks, out.guard_hits, out.fixups, out.slow_path)
+
+
+@pytest.mark.parametrize("poison", [0, 1])
+def test_pruning_is_history_independent(ctx, world, small_map, poison):
+    """Every record field -- including coarse_blocks, the superblock pruning's
+    work and the roofline's algorithmic bytes -- is a function of the call's
+    inputs only: call A, then calls that leave other contents in the
+    workspace (another T and Nv, a batch, the dense path, the plain layout),
+    then A again.  With LGS_OPT_POISON_WS every workspace byte is 0xFF before
+    each batch, so a read-before-write would change the result."""
+    cells, mx, my = small_map
+    rng = np.random.default_rng(21)
+    ang, qs = _queries(world, rng, 4, 541)
+    params = (5, 1.0, 1.0, 0.6, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    scans = [ctx.scan(r, ang) for r, _ in qs]
+    short = ctx.scan(np.where(np.arange(541) % 3 == 0, 25.0, np.minimum(qs[0][0], 5.0)), ang)
+    ctx.set_option(abi.LGS_OPT_POISON_WS, poison)
+    try:
+        first = [_record(ctx.optimize_pose_query(g, P, cost, sc, i)) for sc, (_, i) in zip(scans, qs)]
+        batch1 = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])]
+        for k in range(3):
+            ctx.optimize_pose_query(g, abi.RtcsmParams(5, 0.6, 0.6, 1.0, 20.0), cost, short, (0.1, 0.0, 0.3))
+            ctx.optimize_pose_query_batch(g, P, cost, [short] + scans[:k + 1], [(0.0, 0.0, 0.0)] + [i for _, i in qs][:k + 1])
+            if k == 1:
+                ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 1)
+                ctx.optimize_pose_query(g, P, cost, scans[2], qs[2][1])
+                ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 0)
+            if k == 2:
+                ctx.set_option(abi.LGS_OPT_COARSE_PLANES, 0)
+                ctx.optimize_pose_query(g, P, cost, scans[1], qs[1][1])
+                ctx.set_option(abi.LGS_OPT_COARSE_PLANES, 1)
+            again = [_record(ctx.optimize_pose_query(g, P, cost, sc, i)) for sc, (_, i) in zip(scans, qs)]
+            assert again == first, k
+            batch = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])]
+            assert batch == batch1, k
+    finally:
+        ctx.set_option(abi.LGS_OPT_POISON_WS, 0)
+        ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 0)
+        ctx.set_option(abi.LGS_OPT_COARSE_PLANES, 1)
