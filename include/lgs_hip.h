@@ -169,13 +169,13 @@ int  lgs_abi_version(void);
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 
-/* Diagnostics: copy one intermediate buffer of item 0 of the context's last
- * correlative batch to `out` (at most cap bytes; *bytes = its full size).
+/* Diagnostics: copy one intermediate buffer of item `item` of the context's
+ * last correlative batch to `out` (at most cap bytes; *bytes = its full size).
  * which: 0 sbound [T*nsb2 f64], 1 part_c [nparts f64], 2 part_k [nparts i64],
  * 3 Lp at byte 0, Lc[4] f64 at byte 64, 4 tedge [T i32] (1 = flagged by
  * the last enqueue of item 0, else 0), 5 cbase [2*(T*Nv+pad) i32],
  * 6 idx [T*Nv int2], 7 cscore [K f64]. */
-int  lgs_debug_item_buffer(lgs_ctx* ctx, int which, void* out, size_t cap, size_t* bytes);
+int  lgs_debug_item_buffer(lgs_ctx* ctx, int item, int which, void* out, size_t cap, size_t* bytes);
 
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is
  * the algorithmic byte count of DESIGN.md §Roofline (e.g. 8 B per coarse-score

@@ -2907,10 +2907,15 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     char* ws = (char*)ctx->ensure(S_BATCH_WS, L.total * (size_t)n);
     RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord) * (size_t)n);
     RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned(sizeof(RtcsmRecord) * (size_t)n);
+    // The angle flags are only ever SET (k_project stamps an angle whose lattice
+    // leaves the map low): clear every item's flags first.  (A generation stamp
+    // alone is not enough -- the workspace also holds ints of other layouts,
+    // e.g. a cost cell index equal to this match's stamp.)
     if (ctx->poison_ws) {   // diagnostics: any read-before-write of this batch sees 0xFF bytes
         LGS_HIP_CHECK(hipMemsetAsync(ws, 0xFF, L.total * (size_t)n, ctx->stream));
         LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0xFF, sizeof(RtcsmRecord) * (size_t)n, ctx->stream));
     }
+    LGS_HIP_CHECK(hipMemset2DAsync(ws + L.tedge, L.total, 0, sizeof(int) * (size_t)B.Tmax, (size_t)n, ctx->stream));
     Upload up(ctx);
     const SetJobs sj = build_sets(ctx, p0, sets, B.pruned, up);
     std::vector<int> gens((size_t)n);
@@ -2929,21 +2934,23 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
         it.rec = d_rec + j;
         it.nparts = item_nparts(B, it.pl, B.pruned);
     }
-    {
-        // item 0's intermediates for lgs_debug_item_buffer
-        const MatchItem& i0 = items[0];
-        const RtcsmPlan& q = i0.pl;
+    ctx->dbg.assign((size_t)n, lgs_ctx::DbgItem{});
+    for (int j = 0; j < n; ++j) {
+        // every item's intermediates for lgs_debug_item_buffer (diagnostics)
+        const MatchItem& ij = items[j];
+        const RtcsmPlan& q = ij.pl;
         const size_t nidx = (size_t)q.T * std::max(q.Nv, 1) + kPad;
-        const void* b[8] = { i0.sbound, i0.part_c, i0.part_k, i0.Lp, i0.tedge, i0.cbase, i0.idx, i0.cscore };
-        const size_t s[8] = { sizeof(double) * (size_t)q.T * B.nsb2, sizeof(double) * (size_t)i0.nparts,
-                              sizeof(long long) * (size_t)i0.nparts, 64 + sizeof(double) * kSeedCands,
-                              sizeof(int) * (size_t)q.T, sizeof(int) * 2 * nidx,
-                              sizeof(int2) * (size_t)q.T * q.Nv, sizeof(double) * (size_t)q.K };
+        const void* b[8] = { ij.sbound, ij.part_c, ij.part_k, ij.Lp, ij.tedge, ij.cbase, ij.idx, ij.cscore };
+        const size_t sz[8] = { sizeof(double) * (size_t)q.T * B.nsb2, sizeof(double) * (size_t)ij.nparts,
+                               sizeof(long long) * (size_t)ij.nparts, 64 + sizeof(double) * kSeedCands,
+                               sizeof(int) * (size_t)q.T, sizeof(int) * 2 * nidx,
+                               sizeof(int2) * (size_t)q.T * q.Nv, sizeof(double) * (size_t)q.K };
+        lgs_ctx::DbgItem& d = ctx->dbg[j];
         for (int k = 0; k < 8; ++k) {
-            ctx->dbg_buf[k] = b[k];
-            ctx->dbg_bytes[k] = s[k];
+            d.buf[k] = b[k];
+            d.bytes[k] = sz[k];
         }
-        ctx->dbg_gen = i0.gen;
+        d.gen = ij.gen;
     }
     const size_t items_off = up.append(items.data(), items.size());
     up.flush();
@@ -3020,7 +3027,8 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
             std::vector<MatchItem> one(1, items[j]);
             one[0].nparts = item_nparts(B1, one[0].pl, B1.pruned);
             const int g = one[0].gen = ctx->generation = ctx->next_stamp();
-            if (j == 0) ctx->dbg_gen = g;
+            LGS_HIP_CHECK(hipMemsetAsync(one[0].tedge, 0, sizeof(int) * (size_t)one[0].pl.T, ctx->stream));
+            if ((size_t)j < ctx->dbg.size()) ctx->dbg[j].gen = g;
             Upload u1(ctx);
             const size_t off = u1.append(one.data(), 1);
             u1.flush();
@@ -3165,21 +3173,22 @@ void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params
 }
 }  // namespace lgs
 
-extern "C" int lgs_debug_item_buffer(lgs_ctx* ctx, int which, void* out, size_t cap, size_t* bytes)
+extern "C" int lgs_debug_item_buffer(lgs_ctx* ctx, int item, int which, void* out, size_t cap, size_t* bytes)
 {
-    if (!ctx || which < 0 || which >= 8) return LGS_ERR_INVALID_ARG;
+    if (!ctx || which < 0 || which >= 8 || item < 0) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
-        LGS_REQUIRE(ctx->dbg_buf[which], "no correlative batch has run on this context");
-        const size_t n = ctx->dbg_bytes[which];
+        LGS_REQUIRE((size_t)item < ctx->dbg.size(), "no such item in the last correlative batch");
+        const lgs_ctx::DbgItem& d = ctx->dbg[(size_t)item];
+        const size_t n = d.bytes[which];
         if (bytes) *bytes = n;
         if (!out || cap == 0) return;
         const size_t k = std::min(cap, n);
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         ctx->sync();
-        LGS_HIP_CHECK(hipMemcpy(out, ctx->dbg_buf[which], k, hipMemcpyDeviceToHost));
-        if (which == 4) {   // generation stamps -> flags of item 0's last enqueue
+        LGS_HIP_CHECK(hipMemcpy(out, d.buf[which], k, hipMemcpyDeviceToHost));
+        if (which == 4) {   // generation stamps -> flags of the item's last enqueue
             int* f = (int*)out;
-            for (size_t i = 0; i < k / sizeof(int); ++i) f[i] = f[i] == ctx->dbg_gen ? 1 : 0;
+            for (size_t i = 0; i < k / sizeof(int); ++i) f[i] = f[i] == d.gen ? 1 : 0;
         }
     });
 }
@@ -3296,6 +3305,7 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
         it.cmap = sets[0].cmap;
         it.gen = ctx->generation = ctx->next_stamp();
         it.rec = d_rec;
+        LGS_HIP_CHECK(hipMemsetAsync(it.tedge, 0, sizeof(int) * (size_t)pl.T, ctx->stream));
         const size_t off = up.append(&it, 1);
         up.flush();
         launch_sets(ctx, pl, sets, sj, up);

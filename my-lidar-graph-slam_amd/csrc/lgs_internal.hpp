@@ -211,10 +211,13 @@ struct lgs_ctx {
     bool skipped(int kernel) const { return (skip_mask >> kernel) & 1u; }
     // LGS_OPT_POISON_WS (diagnostics): 0xFF-fill match workspaces before a batch
     bool poison_ws = false;
-    // item 0 of the last correlative batch (lgs_debug_item_buffer)
-    const void* dbg_buf[8] = {};
-    size_t dbg_bytes[8] = {};
-    int dbg_gen = 0;
+    // intermediates of every item of the last correlative batch (lgs_debug_item_buffer)
+    struct DbgItem {
+        const void* buf[8];
+        size_t bytes[8];
+        int gen;
+    };
+    std::vector<DbgItem> dbg;
     int generation = 0;          // per-enqueue stamp (edge flags need no memset), from next_stamp()
     // arena
     void* buf[lgs::S_NUM_SLOTS] = {};

@@ -234,7 +234,7 @@ _PROTOS = [
                                                    C.POINTER(Pose2D), C.c_int, C.POINTER(LinsolveSummary)]),
     ("lgs_cost_square_error", C.c_int, [_P, _P, C.c_double, C.c_double, _P, Pose2D, C.POINTER(C.c_double),
                                         C.POINTER(C.c_double)]),
-    ("lgs_debug_item_buffer", C.c_int, [_P, C.c_int, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("lgs_debug_item_buffer", C.c_int, [_P, C.c_int, C.c_int, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
 ]
 
 SYMBOLS = [p[0] for p in _PROTOS]
@@ -527,14 +527,15 @@ class Context:
                      "L": (3, np.float64), "tedge": (4, np.int32), "cbase": (5, np.int32), "idx": (6, np.int32),
                      "cscore": (7, np.float64)}
 
-    def debug_buffer(self, name: str) -> np.ndarray:
-        """Diagnostics: an intermediate buffer of item 0 of the last correlative
-        batch (lgs_debug_item_buffer); "L" = [Lp, pad x7, Lc0..Lc3]."""
+    def debug_buffer(self, name: str, item: int = 0) -> np.ndarray:
+        """Diagnostics: an intermediate buffer of one item of the last
+        correlative batch (lgs_debug_item_buffer); "L" = [Lp, pad x7, Lc0..Lc3]."""
         which, dt = self.DEBUG_BUFFERS[name]
         n = C.c_size_t()
-        self.check(self.lib.lgs_debug_item_buffer(self.h, which, None, 0, C.byref(n)), "debug_item_buffer")
+        self.check(self.lib.lgs_debug_item_buffer(self.h, item, which, None, 0, C.byref(n)), "debug_item_buffer")
         out = np.zeros(n.value // np.dtype(dt).itemsize, dtype=dt)
-        self.check(self.lib.lgs_debug_item_buffer(self.h, which, out.ctypes.data_as(_P), out.nbytes, C.byref(n)),
+        self.check(self.lib.lgs_debug_item_buffer(self.h, item, which, out.ctypes.data_as(_P), out.nbytes,
+                                                  C.byref(n)),
                    "debug_item_buffer")
         return out
 

@@ -172,6 +172,49 @@ def test_query_planes_equal_supplied_coarse_planes(ctx, world, low_res, n_cells)
         assert_same(fused, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"lr{low_res} q{j}")
 
 
+_FIELDS = ("found", "best_win", "score", "pose", "ncost", "cov", "coarse_blocks", "fine_blocks", "guard_hits",
+           "fixups", "slow_path")
+
+
+def _diff(a, b):
+    return [(j, f, x, y) for j, (ra, rb) in enumerate(zip(a, b)) for f, x, y in zip(_FIELDS, ra, rb) if x != y]
+
+
+def _buffers(ctx, n):
+    out = [{b: ctx.debug_buffer(b, j) for b in ("sbound", "part_c", "part_k", "L", "tedge", "cbase", "idx")}
+           for j in range(n)]
+    for d in out:
+        d["L"] = np.concatenate([d["L"][:1], d["L"][8:12]])   # Lp, Lc[0..3] (not the padding between)
+    return out
+
+
+def _buffer_diff(a, b):
+    """first differing intermediate buffer of every item (diagnostics)"""
+    out = []
+    for j, (x, y) in enumerate(zip(a, b)):
+        for name in x:
+            u, v = x[name], y[name]
+            if u.shape != v.shape or not np.array_equal(u.view(np.uint8), v.view(np.uint8)):
+                k = int(np.argmax(u.view(np.uint8) != v.view(np.uint8))) // u.itemsize if u.shape == v.shape else -1
+                out.append((j, name, k, u[k] if k >= 0 else u.shape, v[k] if k >= 0 else v.shape))
+    return out
+
+
+def _expected_blocks(bufs, ncx, ncy, thr):
+    """coarse blocks the keep rule selects, recomputed on the host from an
+    item's sbound / Lc / tedge (diagnostics)"""
+    nsbx, nsby = (ncx + 3) // 4, (ncy + 3) // 4
+    sb = bufs["sbound"].reshape(-1, nsbx * nsby)
+    L = bufs["L"][1:5].max()
+    tot = 0
+    for t in range(sb.shape[0]):
+        for i in range(nsbx * nsby):
+            a, b = i % nsbx, i // nsbx
+            if sb[t, i] > thr and (bufs["tedge"][t] or sb[t, i] >= L):
+                tot += min(4, ncx - 4 * a) * min(4, ncy - 4 * b)
+    return tot
+
+
 def _record(out):
     return (out.pose_found, list(out.best_win), out.score_max, out.estimated_pose.tuple(), out.normalized_cost,
             list(out.covariance), out.coarse_blocks, out.fine_blocks, out.guard_hits, out.fixups, out.slow_path)
@@ -197,6 +240,7 @@ def test_pruning_is_history_independent(ctx, world, small_map, poison):
     try:
         first = [_record(ctx.optimize_pose_query(g, P, cost, sc, i)) for sc, (_, i) in zip(scans, qs)]
         batch1 = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])]
+        snap1 = _buffers(ctx, len(scans))
         for k in range(3):
             ctx.optimize_pose_query(g, abi.RtcsmParams(5, 0.6, 0.6, 1.0, 20.0), cost, short, (0.1, 0.0, 0.3))
             ctx.optimize_pose_query_batch(g, P, cost, [short] + scans[:k + 1], [(0.0, 0.0, 0.0)] + [i for _, i in qs][:k + 1])
@@ -209,9 +253,15 @@ def test_pruning_is_history_independent(ctx, world, small_map, poison):
                 ctx.optimize_pose_query(g, P, cost, scans[1], qs[1][1])
                 ctx.set_option(abi.LGS_OPT_COARSE_PLANES, 1)
             again = [_record(ctx.optimize_pose_query(g, P, cost, sc, i)) for sc, (_, i) in zip(scans, qs)]
-            assert again == first, k
+            assert again == first, (k, _diff(again, first))
             batch = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])]
-            assert batch == batch1, k
+            if batch != batch1:
+                snap = _buffers(ctx, len(scans))
+                exp1 = [_expected_blocks(b, 5, 5, 0.0) for b in snap1]
+                exp = [_expected_blocks(b, 5, 5, 0.0) for b in snap]
+                for row in [k, _diff(batch, batch1), exp1, exp] + _buffer_diff(snap1, snap):
+                    print("HISTORY-DIAG", row)
+                assert batch == batch1, (k, _diff(batch, batch1), _buffer_diff(snap1, snap), exp1, exp)
     finally:
         ctx.set_option(abi.LGS_OPT_POISON_WS, 0)
         ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 0)

@@ -3,11 +3,12 @@
 
     python tools/pmc_summary.py <trace_dir> <pmc_fetch_dir> <pmc_write_dir> <pmc_l2_dir> <out_prefix>
 
+    [<liblgs_hip.so profiled>]
+
 Writes <out_prefix>_kernel_stats.md (kernel-trace durations) and
-<out_prefix>_pmc.json / profiles/<...>_pmc_summary.json-style dict with, per
-kernel: dispatches, avg duration, FETCH_SIZE/WRITE_SIZE per dispatch (KB as
-rocprofv3 reports them) and the HBM bytes per launch used as bench.py's
-roofline.traffic.  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE
+<out_prefix>_pmc.json = {"lib_sha256": the profiled library's hash, "kernels":
+{name: dispatches, avg duration, FETCH_SIZE / WRITE_SIZE per dispatch}};
+bench.py takes roofline.traffic from it only for the same library build.  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE
 counts 64 B per 128-B request of wide coalesced reads, so the reported value is
 doubled for those; our gathers are 8-B per lane, an access width the guide
 lists as uncalibrated, so both the raw and the x2 figure are recorded and the
@@ -48,6 +49,8 @@ def counters(d):
 
 def main():
     trace, fetch, write, l2, prefix = sys.argv[1:6]
+    lib = sys.argv[6] if len(sys.argv) > 6 else os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "my-lidar-graph-slam_amd", "lgs_amd", "liblgs_hip.so")
     rows = list(csv.DictReader(open(one(trace, "*kernel_trace.csv"))))
     dur = defaultdict(list)
     for r in rows:
@@ -73,12 +76,17 @@ def main():
             h, m = sum(cl[k]["TCC_HIT_sum"]), sum(cl[k].get("TCC_MISS_sum", [0]))
             e["l2_hit_rate"] = round(h / max(1.0, h + m), 4)
         if "fetch_kb_per_dispatch" in e:
-            raw = 1024.0 * (e["fetch_kb_per_dispatch"] + e.get("write_kb_per_dispatch", 0.0))
-            e["hbm_bytes_per_launch"] = round(raw)
-            e["hbm_bytes_per_launch_x2_fetch"] = round(raw + 1024.0 * e["fetch_kb_per_dispatch"])
+            e["fetch_bytes_per_launch"] = round(1024.0 * e["fetch_kb_per_dispatch"])
+        if "write_kb_per_dispatch" in e:
+            e["write_bytes_per_launch"] = round(1024.0 * e["write_kb_per_dispatch"])
         out[k] = e
-    json.dump(out, open(prefix + "_pmc.json", "w"), indent=1)
-    print(json.dumps(out.get("k_coarse<1>", {}), indent=1))
+    import hashlib
+    doc = {"lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+           "note": "rocprofv3 FETCH_SIZE / WRITE_SIZE (separate --pmc passes) per dispatch; gfx950 FETCH_SIZE counts "
+                   "half the bytes of wide coalesced reads (MI355X_MICROARCH.md HBM section): bench.py doubles it",
+           "kernels": out}
+    json.dump(doc, open(prefix + "_pmc.json", "w"), indent=1)
+    print(json.dumps(out.get("k_coarse_lanes", {}), indent=1))
 
 
 if __name__ == "__main__":
