@@ -71,6 +71,7 @@ def parse():
                     help="A/B: LGS_OPT_LANES_MIN_BATCH (pruned coarse stage kernel choice by batch size)")
     ap.add_argument("--super-quad", type=int, default=None, help="A/B: LGS_OPT_SUPER_QUAD")
     ap.add_argument("--super-hex", type=int, default=None, help="A/B: LGS_OPT_SUPER_HEX")
+    ap.add_argument("--fine-lanes", type=int, default=None, help="A/B: LGS_OPT_FINE_LANES")
     ap.add_argument("--latency-calls", type=int, default=100,
                     help="match workload: lone OptimizePose(query) calls timed for p50/p90 (0 = skip, e.g. under "
                          "rocprofv3 so that the trace holds the batched launches only)")
@@ -315,6 +316,8 @@ def run_match(args, D, ctx):
             c.set_option(abi.LGS_OPT_SUPER_QUAD, args.super_quad)
         if args.super_hex is not None:
             c.set_option(abi.LGS_OPT_SUPER_HEX, args.super_hex)
+        if args.fine_lanes is not None:
+            c.set_option(abi.LGS_OPT_FINE_LANES, args.fine_lanes)
         state.append((c, c.grid_from_array(cells, mx, my, 0.05), [c.scan(r, ang) for r in scans]))
     P, cost = abi.RtcsmParams(*PARAMS), abi.CostGEParams(*COST)
     n = len(scans)

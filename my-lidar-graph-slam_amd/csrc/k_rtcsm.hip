@@ -68,6 +68,7 @@ typedef float SuperT;
 __device__ __forceinline__ SuperT super_round_up(double m) { return __double2float_ru(m); }
 #endif
 
+constexpr int kMaxBatchItems = 64;   // matches per batched launch chain (run_chunked)
 constexpr int kPipe = 16;   // seq_sum gathers in flight per batch (index arrays padded by 2*kPipe)
 constexpr int kPad = 4 * kPipe;   // cbase padding past the last row (seq_sum4's look-ahead)
 
@@ -99,6 +100,8 @@ struct MatchItem {
     int* list;
     int* segcnt;
     int nseg;
+    int* dlist;              // selected blocks, dense in block order (k_compact)
+    int* nsel;               // their number
     int frows;
     double* fval;
     int* fpos;
@@ -1865,6 +1868,110 @@ __global__ __launch_bounds__(64) void k_fine(Items items, const double* __restri
     LGS_PROBE_PRINT("fine(seg_prefix, item0[, item1])");
 }
 
+// k_compact: one workgroup per item writes the item's selected blocks (the
+// per-segment lists of k_select) dense in block order, dlist[0..n), and n.
+// Wave w copies segments w, w + 4, ...
+__global__ __launch_bounds__(256) void k_compact(Items items)
+{
+    const MatchItem& it = items[blockIdx.x];
+    extern __shared__ int pref[];   // nseg + 1
+    __shared__ int ws[16];
+    seg_prefix(it.segcnt, it.nseg, pref, ws);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int sg = w; sg < it.nseg; sg += 4) {
+        const int c = pref[sg + 1] - pref[sg];
+        const int* __restrict__ src = it.list + (size_t)sg * kSelSeg;
+        int* __restrict__ dst = it.dlist + pref[sg];
+        for (int i = lane; i < c; i += 64) dst[i] = src[i];
+    }
+    if (threadIdx.x == 0) *it.nsel = pref[it.nseg];
+}
+
+// k_fine_lanes: EvaluateHighResolutionMap (:227-256) for every selected block
+// of the batch, one wave per block and one LANE per fine pose (lr * lr <= 64
+// lanes): each lane walks the beams in order with pipelined gathers (seq_sum:
+// the reference's sequential fp64 sum), so the add chains of all poses run
+// side by side -- the transposed evaluator (eval_block_t) ran one block row
+// per wave with LR adding lanes.  The batch's blocks form one global index
+// space (items' counts prefix-summed in LDS), so a scan with thousands of
+// selected blocks (tie-heavy maps) spreads over the whole GPU instead of
+// loading its own workgroups.  Block max and its first position in the
+// reference's (x outer, y inner) order: lane q = xo * lr + yo, ties to the
+// smallest q.  Writes fval[b], fpos[b] (frows = 1).
+constexpr int kFineLanesWaves = 1;   // one wave per workgroup: its LDS holds the block's index row
+constexpr int kFineLanesMaxNv = 2048;
+__global__ __launch_bounds__(64 * kFineLanesWaves) void k_fine_lanes(Items items, int n,
+                                                                    const double* __restrict__ zero)
+{
+    __shared__ int ipref[kMaxBatchItems + 1];
+    extern __shared__ int2 sidx[];   // [Nv + 4 * kPipe] the block's angle row
+    if (threadIdx.x < 64) {   // inclusive scan of the items' counts (n <= 64)
+        const int j = threadIdx.x;
+        const int c = (j < n) ? *items[j].nsel : 0;
+        int incl = c;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off, 64);
+            if (j >= off) incl += t;
+        }
+        if (j < n) ipref[j + 1] = incl;
+        if (j == 0) ipref[0] = 0;
+    }
+    __syncthreads();
+    const int total = ipref[n];
+    const int lane = threadIdx.x & 63;
+    for (int g = blockIdx.x; g < total; g += gridDim.x) {   // workgroup-uniform
+        int lo = 0, hi = n - 1;   // item of block g: last j with ipref[j] <= g
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (ipref[mid] <= g) lo = mid;
+            else hi = mid - 1;
+        }
+        // the item and block are uniform: SGPRs, so the descriptor fields are
+        // scalar loads
+        const int j = __builtin_amdgcn_readfirstlane(lo);
+        const MatchItem& it = items[j];
+        const RtcsmPlan& pl = it.pl;
+        const int b = __builtin_amdgcn_readfirstlane(g - ipref[j]);
+        const int k = it.dlist[b];
+        const int tt = k / pl.P, rem = k % pl.P;
+        const int jx = rem / pl.ncy, jy = rem % pl.ncy;
+        const int lr = pl.low_res, npose = lr * lr;
+        const bool act = lane < npose;
+        const int xo = lane / lr, yo = lane - (lane / lr) * lr;
+        const int xf = -pl.win_x + jx * lr + xo, yf = -pl.win_y + jy * lr + yo;
+        const int W = pl.W, H = pl.H, Nv = pl.Nv;
+        const double* __restrict__ grid = it.grid;
+        // the angle row of beam cells staged in LDS (8 loads in flight per
+        // lane), then read back as broadcasts: the gathers of a batch then wait
+        // on LDS, not on a global index load
+        __syncthreads();
+        stage_lds(sidx, it.idx + (size_t)tt * Nv, Nv);
+        for (int v = Nv + lane; v < Nv + 4 * kPipe; v += 64) sidx[v] = make_int2(-(1 << 28), -(1 << 28));
+        __syncthreads();
+        // four batches of gathers in flight (seq_sum4): the kernel's duration
+        // is one wave's latency chain over the beams
+        const double s = seq_sum4<int2>(Nv, [&](int v) { return sidx[v]; }, [&](const int2& c) {
+            const int x = c.x + xf, y = c.y + yf;
+            const bool inb = act & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
+            return inb ? grid + (unsigned)(y * W + x) : zero;
+        });
+        double bv = act ? s : -INFINITY;
+        long long bo = act ? (long long)lane : LLONG_MAX;
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ov = __shfl_xor(bv, off, 64);
+            const long long ok = __shfl_xor(bo, off, 64);
+            if (better(ov, ok, bv, bo)) {
+                bv = ov;
+                bo = ok;
+            }
+        }
+        if (lane == 0) {
+            it.fval[b] = bv;
+            it.fpos[b] = (int)bo;
+        }
+    }
+}
+
 // k_replay (one wave): the reference's sequential acceptance (:98-114 with the
 // strict update of :246) over the selected blocks in block order.  Lanes load
 // 64 consecutive entries at once; the acceptance itself walks them in lane
@@ -2248,6 +2355,7 @@ struct BatchShape {
     bool planes = false;    // coarse map in padded phase planes
     bool pruned = false;    // superblock pruning
     bool lr5 = false;       // transposed LR = 5 evaluators
+    bool fine_lanes = false;   // k_compact + k_fine_lanes (lr * lr <= 64)
     int frows = 1;
     int kernel_size = 0;
 };
@@ -2270,7 +2378,7 @@ inline bool uses_super(const lgs_ctx* ctx, int nv_max, int nsb2, bool dense)
 // Per-item workspace: one contiguous region per item carved from S_BATCH_WS
 // (sized for the batch's largest plan), field offsets below.
 struct ItemLayout {
-    size_t idx, cbase, cscore, cflag, list, segcnt, fval, fpos, part_c, part_k, tedge, sbound, poses7, cidx,
+    size_t idx, cbase, cscore, cflag, list, segcnt, dlist, fval, fpos, part_c, part_k, tedge, sbound, poses7, cidx,
         terms, count, total;
 };
 ItemLayout item_layout(int Tmax, int NvMax, int P, int nsb2, int chunks, int cb, int frows, int Nmax)
@@ -2292,6 +2400,7 @@ ItemLayout item_layout(int Tmax, int NvMax, int P, int nsb2, int chunks, int cb,
     L.cflag = take(K);
     L.list = take(sizeof(int) * nseg * kSelSeg);
     L.segcnt = take(sizeof(int) * nseg);
+    L.dlist = take(sizeof(int) * K);
     L.fval = take(sizeof(double) * K * frows);
     L.fpos = take(sizeof(int) * K * frows);
     L.part_c = take(sizeof(double) * nparts);
@@ -2301,7 +2410,7 @@ ItemLayout item_layout(int Tmax, int NvMax, int P, int nsb2, int chunks, int cb,
     L.poses7 = take(sizeof(double) * 21);
     L.cidx = take(sizeof(int4) * 7 * (size_t)Nmax);
     L.terms = take(sizeof(double) * 7 * (size_t)Nmax);
-    L.count = take(128);   // Lp, Lc[kSeedCands]
+    L.count = take(128);   // Lp, Lc[kSeedCands], nsel
     L.total = o;
     return L;
 }
@@ -2325,7 +2434,9 @@ void bind_workspace(MatchItem& it, char* base, const ItemLayout& L, int frows)
     it.terms = (double*)(base + L.terms);
     it.Lp = (double*)(base + L.count);
     it.Lc = (double*)(base + L.count + 64);
-    static_assert(64 + 8 * kSeedCands <= 128, "count block layout");
+    it.nsel = (int*)(base + L.count + 64 + 8 * kSeedCands);
+    it.dlist = (int*)(base + L.dlist);
+    static_assert(64 + 8 * kSeedCands + 4 <= 128, "count block layout");
     it.frows = frows;
     it.nseg = (int)((it.pl.K + kSelSeg - 1) / kSelSeg);
 }
@@ -2618,7 +2729,16 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
     }
-    {
+    if (B.fine_lanes) {
+        hipLaunchKernelGGL(k_compact, dim3(n), dim3(256), pref_bytes(B.nsegMax), st, d_items);
+        LGS_HIP_CHECK(hipGetLastError());
+        const int tok_ = ctx->timing_begin(K_FINE, 0.0);
+        if (!ctx->skipped(K_FINE))
+            hipLaunchKernelGGL(k_fine_lanes, dim3(4096), dim3(64 * kFineLanesWaves),
+                               sizeof(int2) * (size_t)(B.NvMax + 4 * kPipe), st, d_items, n, zero);
+        ctx->timing_end(tok_);
+        LGS_HIP_CHECK(hipGetLastError());
+    } else {
         const int tok_ = ctx->timing_begin(K_FINE, 0.0);
         dim3 g(fine_grid(n), n);
         if (ctx->skipped(K_FINE)) {
@@ -2866,6 +2986,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
                  double nthr, std::vector<PlaneSet>& sets, const int* set_of, lgs_rtcsm_summary* out)
 {
     LGS_HIP_CHECK(hipSetDevice(ctx->device));
+    LGS_REQUIRE(n >= 1 && n <= kMaxBatchItems, "batch of 1..64 matches (run_chunked splits larger ones)");
     std::vector<MatchItem> items((size_t)n);
     BatchShape B;
     B.n = n;
@@ -2900,7 +3021,11 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     B.planes = ctx->coarse_planes;
     B.pruned = uses_super(ctx, B.NvMax, B.nsb2, false);
     B.lr5 = lr5_path(B.NvMax, B.low_res);
-    B.frows = B.lr5 ? 5 : 1;
+    // lone matches keep the transposed row evaluator (LR waves per block: lower
+    // latency for a handful of blocks); batches spread their blocks lane-per-pose
+    B.fine_lanes = ctx->fine_lanes && n >= ctx->lanes_min_batch && B.low_res * B.low_res <= 64 &&
+                   B.NvMax <= kFineLanesMaxNv;
+    B.frows = (B.lr5 && !B.fine_lanes) ? 5 : 1;
     B.kernel_size = cost->kernel_size;
     B.nsegMax = (int)(((long long)B.Tmax * B.P + kSelSeg - 1) / kSelSeg);
     const ItemLayout L = item_layout(B.Tmax, B.NvMax, B.P, B.nsb2, B.chunks, B.cb, B.frows, Nmax);
@@ -3049,7 +3174,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
 
 // Batches of at most kMaxBatch items (bounded scratch: ~20 MB per config-2
 // item), each with only the coarse maps its items reference.
-constexpr int kMaxBatch = 64;
+constexpr int kMaxBatch = kMaxBatchItems;
 void run_chunked(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
                  const lgs_grid* const* grids, lgs_scan* const* scans, const lgs_pose2d* init, int n,
                  double nthr, const std::vector<PlaneSet>& sets_all, const int* set_of, lgs_rtcsm_summary* out)
