@@ -175,7 +175,8 @@ int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
  * which: 0 sbound [T*nsb2 f64], 1 part_c [nparts f64], 2 part_k [nparts i64],
  * 3 Lp at byte 0, Lc[4] f64 at byte 64, 4 tedge [T i32] (1 = flagged by
  * the last enqueue of item 0, else 0), 5 cbase [2*(T*Nv+pad) i32],
- * 6 idx [T*Nv int2], 7 cscore [K f64]. */
+ * 6 idx [T*Nv int2], 7 cscore [K f64], 8 coarse phase planes [lr*lr planes
+ * of Hqp x Wqp f64, DESIGN.md §2], 9 superblock planes [fp16]. */
 int  lgs_debug_item_buffer(lgs_ctx* ctx, int item, int which, void* out, size_t cap, size_t* bytes);
 
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is

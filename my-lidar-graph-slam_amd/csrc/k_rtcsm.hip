@@ -2262,7 +2262,7 @@ void set_plane_layout(RtcsmPlan& pl)
     pl.nsbx = (pl.ncx + kSB - 1) / kSB;
     pl.nsby = (pl.ncy + kSB - 1) / kSB;
     pl.M = std::max(kSB * pl.nsbx, kSB * pl.nsby);
-    pl.Wqp = pl.Wq + 2 * pl.M;
+    pl.Wqp = (pl.Wq + 2 * pl.M + 1) & ~1;   // even: 16-byte aligned plane rows (k_precompute_planes' paired stores)
     pl.Hqp = pl.Hq + 2 * pl.M;
     pl.pstride = (long long)pl.Wqp * pl.Hqp;
     pl.Wq4 = (pl.Wqp + 3) / 4;
@@ -3075,6 +3075,10 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
             d.buf[k] = b[k];
             d.bytes[k] = sz[k];
         }
+        d.buf[8] = ij.cmap;   // the item's coarse phase planes and superblock planes
+        d.bytes[8] = B.planes ? plane_bytes(q) : sizeof(double) * (size_t)q.W * q.H;
+        d.buf[9] = ij.super;
+        d.bytes[9] = ij.super ? super_bytes(q) : 0;
         d.gen = ij.gen;
     }
     const size_t items_off = up.append(items.data(), items.size());
@@ -3300,7 +3304,7 @@ void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params
 
 extern "C" int lgs_debug_item_buffer(lgs_ctx* ctx, int item, int which, void* out, size_t cap, size_t* bytes)
 {
-    if (!ctx || which < 0 || which >= 8 || item < 0) return LGS_ERR_INVALID_ARG;
+    if (!ctx || which < 0 || which >= 10 || item < 0) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
         LGS_REQUIRE((size_t)item < ctx->dbg.size(), "no such item in the last correlative batch");
         const lgs_ctx::DbgItem& d = ctx->dbg[(size_t)item];

@@ -508,12 +508,21 @@ __global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restri
 }
 
 // Batched precompute straight into the padded phase planes (W, H multiples of
-// the window LR <= 8).  A tile is kPQX coarse columns x kPTY fine rows: its
-// output row segment of one plane is kPQX consecutive doubles, and the store
-// loop walks (row, plane column, qx) with qx fastest, so the plane writes are
-// contiguous runs (the generic tile above scatters consecutive lanes over
-// the LR planes).  Same passes, same values (max is exact).
-constexpr int kPQX = 32, kPTY = 16;
+// the window LR <= 8).  A tile is kPQX coarse columns x kPTY fine rows.
+//  1. y pass (SlidingWindowMaxRow) in registers: a thread owns footprint
+//     columns, loads its column's kPTY + LR - 1 values once (all loads issued
+//     before any max) and writes the kPTY window maxima to LDS;
+//  2. x pass (SlidingWindowMaxCol) from LDS, each thread producing TWO
+//     consecutive coarse columns of one plane row and writing them with one
+//     16-byte store (padded plane rows are even, so the pair is aligned); the
+//     lanes of a wave walk a plane row, so a wave writes 512-byte runs.
+// Same values as the reference's passes (max is exact).
+constexpr int kPTY = 16;
+// coarse columns per tile: the footprint (kPQX * LR + LR - 1 fine columns) fits
+// the 256 threads of the y pass, and kPQX is even (column pairs)
+template <int LR>
+constexpr int pqx() { return ((257 - LR) / LR) & ~1; }
+typedef double d2a16 __attribute__((ext_vector_type(2)));
 template <int LR>
 __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __restrict__ jobs)
 {
@@ -529,55 +538,85 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
 #endif
     const PrecompJob& j = jobs[bz];
     const int W = j.W, H = j.H;
+    constexpr int kPQX = pqx<LR>();
     const int x0 = bx * kPQX * LR, y0 = by * kPTY;
     if (x0 >= W || y0 >= H) return;   // past this job's map (uniform)
     const int x1 = min(x0 + kPQX * LR, W), y1 = min(y0 + kPTY, H);
     const int sx0 = win_start(x0, W, LR), sy0 = win_start(y0, H, LR);
-    const int sx1 = win_start(x1 - 1, W, LR) + LR, sy1 = win_start(y1 - 1, H, LR) + LR;
-    const int fw = sx1 - sx0, fh = sy1 - sy0;
-    extern __shared__ double lds[];
-    double* tile = lds;              // [fh][fw]
-    double* m1 = lds + fh * fw;      // [kPTY][fw]
+    const int sx1 = win_start(x1 - 1, W, LR) + LR;
+    const int fw = sx1 - sx0;
+    const int oh = y1 - y0;
+    constexpr int FW = kPQX * LR + LR - 1;
+    static_assert(FW <= 256, "one footprint column per thread");
+    constexpr int FH = kPTY + LR - 1;
+    __shared__ double m1[kPTY][FW];
     const double* __restrict__ in = j.in;
     const int tid = threadIdx.x;
-    for (int k0 = tid; k0 < fh * fw; k0 += 8 * (int)blockDim.x) {   // 8 loads in flight per thread
-        double v[8];
+    for (int c = tid; c < fw; c += 256) {   // one column per thread (FW <= 256)
+        const int xx = sx0 + c;
+        double v[FH];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int k = k0 + j * (int)blockDim.x;
-            const int yy = sy0 + k / fw, xx = sx0 + k % fw;
-            v[j] = (k < fh * fw && xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;
+        for (int k = 0; k < FH; ++k) {
+            const int yy = sy0 + k;
+            v[k] = (xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;   // reads past the end are 0
         }
+        // window maxima of every start row (static register indices), then row
+        // oy takes the window starting at win_start(y0 + oy) - sy0 =
+        // min(oy + d, st) (the tail repeats the last full window)
+        double wm[kPTY];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int k = k0 + j * (int)blockDim.x;
-            if (k < fh * fw) tile[k] = v[j];
+        for (int k = 0; k < kPTY; ++k) {
+            double m = v[k];
+#pragma unroll
+            for (int i = 1; i < LR; ++i) m = dmax(m, v[k + i]);
+            wm[k] = m;
         }
-    }
-    __syncthreads();
-    const int oh = y1 - y0;
-    for (int k = tid; k < oh * fw; k += blockDim.x) {   // SlidingWindowMaxRow (y pass)
-        const int oy = k / fw, cx = k % fw;
-        const double* c = tile + (win_start(y0 + oy, H, LR) - sy0) * fw + cx;
-        double m = c[0];
+        const int d = y0 - sy0, st = max(0, H - LR - sy0);
+        if (d == 0 && st >= kPTY - 1) {   // interior tiles (uniform): row oy's window starts at oy
 #pragma unroll
-        for (int i = 1; i < LR; ++i) m = dmax(m, c[i * fw]);
-        m1[oy * fw + cx] = m;
+            for (int oy = 0; oy < kPTY; ++oy)
+                if (oy < oh) m1[oy][c] = wm[oy];
+        } else {
+#pragma unroll
+            for (int oy = 0; oy < kPTY; ++oy) {
+                const int s = min(oy + d, st);
+                double m = wm[0];
+#pragma unroll
+                for (int k = 1; k < kPTY; ++k) m = (k == s) ? wm[k] : m;
+                if (oy < oh) m1[oy][c] = m;
+            }
+        }
     }
     __syncthreads();
     const PlaneGeom& pg = j.pg;
-    const int nq = (x1 - x0) / LR;   // coarse columns of this tile (W is a multiple of LR)
-    for (int k = tid; k < oh * LR * kPQX; k += blockDim.x) {   // SlidingWindowMaxCol (x pass)
-        const int oy = k / (LR * kPQX), rem = k % (LR * kPQX);
-        const int rx = rem / kPQX, qxl = rem % kPQX;
-        if (qxl >= nq) continue;
-        const int x = x0 + qxl * LR + rx, y = y0 + oy;
-        const double* c = m1 + oy * fw + (win_start(x, W, LR) - sx0);
-        double m = c[0];
+    const int nq = (x1 - x0) / LR;        // coarse columns of this tile (W is a multiple of LR)
+    const int np = (nq + 1) >> 1;         // column pairs
+    double* __restrict__ out = j.out;
+    for (int k = tid; k < oh * LR * (kPQX / 2); k += 256) {   // (row, plane column, pair), pair fastest
+        const int oy = k / (LR * (kPQX / 2)), rem = k % (LR * (kPQX / 2));
+        const int rx = rem / (kPQX / 2), p = rem % (kPQX / 2);
+        if (p >= np) continue;
+        const int qxl = 2 * p;
+        const int xa = x0 + qxl * LR + rx;
+        const double* ca = &m1[oy][win_start(xa, W, LR) - sx0];
+        double ma = ca[0];
 #pragma unroll
-        for (int i = 1; i < LR; ++i) m = dmax(m, c[i]);
-        const int qy = y / LR, ry = y - qy * LR;
-        j.out[(ry * LR + rx) * pg.pstride + (long long)(qy + pg.M) * pg.Wqp + (x0 / LR + qxl) + pg.M] = m;
+        for (int i = 1; i < LR; ++i) ma = dmax(ma, ca[i]);
+        const int y = y0 + oy, qy = y / LR, ry = y - qy * LR;
+        double* dst = out + (ry * LR + rx) * pg.pstride + (long long)(qy + pg.M) * pg.Wqp + (x0 / LR + qxl) + pg.M;
+        if (qxl + 1 < nq) {
+            const int xb = xa + LR;
+            const double* cb = &m1[oy][win_start(xb, W, LR) - sx0];
+            double mb = cb[0];
+#pragma unroll
+            for (int i = 1; i < LR; ++i) mb = dmax(mb, cb[i]);
+            d2a16 v;
+            v.x = ma;
+            v.y = mb;
+            *(d2a16*)dst = v;
+        } else {
+            *dst = ma;
+        }
     }
 }
 
@@ -675,11 +714,9 @@ void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, i
     if (ctx->skipped(K_PRECOMPUTE)) {
     } else if (win <= 8) {
         // plane-ordered tiles (every job of this path writes planes)
-        const int fw = kPQX * win + win - 1, fh = kPTY + win - 1;
-        const size_t lds = (size_t)(fh * fw + kPTY * fw) * sizeof(double);
-        dim3 grid((maxW + kPQX * win - 1) / (kPQX * win), (maxH + kPTY - 1) / kPTY, njobs);
         switch (win) {
-#define LGS_PP_CASE(L) case L: hipLaunchKernelGGL(k_precompute_planes<L>, grid, dim3(256), lds, ctx->stream, d_jobs); break;
+#define LGS_PP_CASE(L) case L: hipLaunchKernelGGL(k_precompute_planes<L>, \
+            dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + kPTY - 1) / kPTY, njobs), dim3(256), 0, ctx->stream, d_jobs); break;
         LGS_PP_CASE(1) LGS_PP_CASE(2) LGS_PP_CASE(3) LGS_PP_CASE(4) LGS_PP_CASE(5) LGS_PP_CASE(6)
         LGS_PP_CASE(7) LGS_PP_CASE(8)
 #undef LGS_PP_CASE

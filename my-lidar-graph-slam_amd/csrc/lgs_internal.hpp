@@ -214,8 +214,8 @@ struct lgs_ctx {
     bool poison_ws = false;
     // intermediates of every item of the last correlative batch (lgs_debug_item_buffer)
     struct DbgItem {
-        const void* buf[8];
-        size_t bytes[8];
+        const void* buf[10];
+        size_t bytes[10];
         int gen;
     };
     std::vector<DbgItem> dbg;

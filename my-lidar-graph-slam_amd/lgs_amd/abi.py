@@ -526,7 +526,7 @@ class Context:
 
     DEBUG_BUFFERS = {"sbound": (0, np.float64), "part_c": (1, np.float64), "part_k": (2, np.int64),
                      "L": (3, np.float64), "tedge": (4, np.int32), "cbase": (5, np.int32), "idx": (6, np.int32),
-                     "cscore": (7, np.float64)}
+                     "cscore": (7, np.float64), "planes": (8, np.float64), "super": (9, np.float16)}
 
     def debug_buffer(self, name: str, item: int = 0) -> np.ndarray:
         """Diagnostics: an intermediate buffer of one item of the last

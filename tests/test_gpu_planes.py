@@ -1,0 +1,102 @@
+"""The coarse map as the matcher holds it on the device: the
+padded phase planes written straight by the batched precompute
+(k_precompute_planes) or by the phase-plane copy of a supplied coarse map
+(k_decimate), and the fp16 superblock planes (k_super_planes), checked
+element by element against the oracle's PrecomputeGridMap
+(C/mapping/grid_map_builder.cpp:518-536, H/util.hpp:198-253)."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+from conftest import launcher_cost
+from lgs_amd import abi, scene
+
+pytestmark = pytest.mark.gpu
+
+
+def layout(W, H, res, lr, rx, ry):
+    wx, wy = math.ceil(0.5 * rx / res), math.ceil(0.5 * ry / res)
+    ncx, ncy = 2 * wx // lr + 1, 2 * wy // lr + 1
+    nsbx, nsby = (ncx + 3) // 4, (ncy + 3) // 4
+    M = 4 * max(nsbx, nsby)
+    Wq, Hq = -(-W // lr), -(-H // lr)
+    Wqp = (Wq + 2 * M + 1) & ~1
+    Hqp = Hq + 2 * M
+    Wq4, Hq4 = -(-Wqp // 4), -(-Hqp // 4)
+    return dict(M=M, Wq=Wq, Hq=Hq, Wqp=Wqp, Hqp=Hqp, Wq4=Wq4, Hq4=Hq4, sub4=Wq4 * Hq4)
+
+
+def expected_planes(cells, lr, L):
+    C = ob.precompute(cells, lr)
+    H, W = C.shape
+    P = np.zeros((lr * lr, L["Hqp"], L["Wqp"]))
+    for ry in range(lr):
+        for rx in range(lr):
+            sub = C[ry::lr, rx::lr]
+            P[ry * lr + rx, L["M"]:L["M"] + sub.shape[0], L["M"]:L["M"] + sub.shape[1]] = sub
+    return P
+
+
+def check_super(P, S, lr, L):
+    """S (fp16, sub-phase layout) >= the forward 4x4 max of every plane, by at most one fp16 ulp"""
+    Hqp, Wqp = L["Hqp"], L["Wqp"]
+    pad = np.zeros((lr * lr, Hqp + 3, Wqp + 3))
+    pad[:, :Hqp, :Wqp] = P
+    m = np.max([pad[:, j:j + Hqp, i:i + Wqp] for j in range(4) for i in range(4)], axis=0)
+    pstride4 = 16 * L["sub4"]
+    for p in range(lr * lr):
+        got = np.zeros((Hqp, Wqp))
+        for sy in range(4):
+            for sx in range(4):
+                blk = S[p * pstride4 + (sy * 4 + sx) * L["sub4"]:][:L["sub4"]].reshape(L["Hq4"], L["Wq4"])
+                ys, xs = np.arange(sy, Hqp, 4), np.arange(sx, Wqp, 4)
+                got[np.ix_(ys, xs)] = blk[:len(ys), :len(xs)].astype(np.float64)
+        assert np.all(got >= m[p]), p
+        ulp = np.spacing(got.astype(np.float16)).astype(np.float64)
+        assert np.all(got - m[p] <= ulp), p
+
+
+@pytest.mark.parametrize("lr,n,batch", [(5, 400, 1), (5, 400, 3), (4, 200, 2), (2, 150, 2), (8, 240, 1), (3, 100, 2)])
+def test_device_coarse_planes(ctx, world, lr, n, batch):
+    rng = np.random.default_rng(lr * 100 + n)
+    cells = np.where(rng.random((n, n)) < 0.3, rng.choice([0.001, 0.3, 0.45, 0.6, 0.999], (n, n)), 0.0)
+    mx = my = -0.05 * n / 2
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    ang = scene.beam_angles(361)
+    scans = [ctx.scan(rng.uniform(0.5, 4.0, 361), ang) for _ in range(batch)]
+    P = abi.RtcsmParams(lr, 1.0, 1.2, 0.3, 20.0)
+    inits = [(rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5), rng.uniform(-3, 3)) for _ in range(batch)]
+    if batch == 1:
+        ctx.optimize_pose_query(g, P, launcher_cost(), scans[0], inits[0])
+    else:
+        ctx.optimize_pose_query_batch(g, P, launcher_cost(), scans, inits)
+    L = layout(n, n, 0.05, lr, 1.0, 1.2)
+    want = expected_planes(cells, lr, L)
+    for j in range(batch):
+        got = ctx.debug_buffer("planes", j)[:want.size].reshape(want.shape)
+        assert np.array_equal(got, want), j
+        check_super(want, ctx.debug_buffer("super", j), lr, L)
+
+
+def test_device_coarse_planes_supplied_map(ctx):
+    """OptimizePose with a caller's coarse map: the phase-plane copy, incl. a map
+    whose size is not a multiple of LowRes (the plain-scratch route)"""
+    rng = np.random.default_rng(3)
+    for n, lr in [(203, 5), (160, 4)]:
+        cells = np.where(rng.random((n, n)) < 0.3, rng.random((n, n)), 0.0)
+        g = ctx.grid_from_array(cells, -5.0, -5.0, 0.05)
+        cg = ctx.precompute_max(g, lr)
+        ang = scene.beam_angles(181)
+        sc = ctx.scan(rng.uniform(0.5, 4.0, 181), ang)
+        P = abi.RtcsmParams(lr, 1.0, 1.2, 0.3, 20.0)
+        ctx.optimize_pose(g, cg, P, launcher_cost(), sc, (0.1, 0.2, 0.3), 0.1)
+        L = layout(n, n, 0.05, lr, 1.0, 1.2)
+        want = expected_planes(cells, lr, L)
+        got = ctx.debug_buffer("planes", 0)[:want.size].reshape(want.shape)
+        assert np.array_equal(got, want), (n, lr)
+        out = ctx.optimize_pose_query(g, P, launcher_cost(), sc, (0.1, 0.2, 0.3))
+        got = ctx.debug_buffer("planes", 0)[:want.size].reshape(want.shape)
+        assert np.array_equal(got, want), (n, lr, "query")
+        assert out.pose_found in (0, 1)
