@@ -22,7 +22,6 @@
 #include "lgs_internal.hpp"
 
 #include <hipcub/hipcub.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <array>
@@ -70,9 +69,6 @@ __host__ __device__ __forceinline__ double bayes_update(double v, double p)
 // caller (identical values: the reference recomputes the same constant).
 __device__ __forceinline__ double bayes_update_k(double v, double cp, double op)
 {
-#ifdef LGS_AB_APPLY_NOMATH  // diagnostics only: results invalid
-    return (v == 0.0) ? cp : clampv(v * op, kPMin, kPMax);
-#endif
     if (v == 0.0) return cp;
     const double co = clampv(v, kPMin, kPMax);
     const double o = (co / (1.0 - co)) * op;
@@ -97,10 +93,7 @@ struct RayMap {
 // writes into LDS and the wave then copies the range out with coalesced
 // stores (one thread per ray writing its own run would touch 64 lines per
 // store instruction); longer ranges are written directly.
-#ifndef LGS_EMIT_LDS
-#define LGS_EMIT_LDS 8192
-#endif
-constexpr int kEmitLds = LGS_EMIT_LDS;
+constexpr int kEmitLds = 8192;   // keys staged per 64-ray wave (0 = direct stores: 268 vs 213 us per rebuild)
 __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
                                              const long long* __restrict__ offs,
                                              const int* __restrict__ rmap, int nrays,
@@ -632,23 +625,12 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
 }
 
 // Stable sort of the 32-bit keys on the cell bits [1, 1 + cell_bits): hipcub's
-// default onesweep (8-bit digits), or rocprim onesweep with
-// LGS_RAY_RADIX_BITS-bit digits (A/B: fewer passes over ~22 cell bits).
-#ifndef LGS_RAY_RADIX_BITS
-#define LGS_RAY_RADIX_BITS 8
-#endif
+// onesweep radix sort (8-bit digits; rocprim onesweep with 11-bit digits was
+// measured slower, 3.2 -> 4.8 ms per rebuild step).
 hipError_t ray_sort(void* temp, size_t& bytes, const unsigned* in, unsigned* out, long long n, int cell_bits,
                     hipStream_t st)
 {
-#if LGS_RAY_RADIX_BITS == 8
     return hipcub::DeviceRadixSort::SortKeys(temp, bytes, in, out, (int)n, 1, 1 + cell_bits, st);
-#else
-    using cfg = rocprim::radix_sort_config<
-        rocprim::default_config, rocprim::default_config,
-        rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<512, 12>,
-                                            LGS_RAY_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
-    return rocprim::radix_sort_keys<cfg>(temp, bytes, in, out, (int)n, 1u, (unsigned)(1 + cell_bits), st);
-#endif
 }
 
 // Ray-cast every job's scans (already in its map's geometry), jobs in order,

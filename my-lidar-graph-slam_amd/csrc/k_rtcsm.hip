@@ -45,13 +45,9 @@ bool precompute_planes_ok(const lgs_grid* in, int win);
 namespace {
 
 
-// Superblock plane element: fp16 (default) or fp32 (-DLGS_SUPER_F16=0), both
-// rounded toward +inf from the fp64 maxima, so every stored value is >= the
-// coarse values it bounds (the bound's sum is taken in fp64 either way).
-#ifndef LGS_SUPER_F16
-#define LGS_SUPER_F16 1
-#endif
-#if LGS_SUPER_F16
+// Superblock plane element: fp16 rounded toward +inf from the fp64 maxima, so
+// every stored value is >= the coarse values it bounds (the bound's sum is
+// taken in fp64).
 typedef _Float16 SuperT;
 __device__ __forceinline__ SuperT super_round_up(double m)
 {
@@ -63,10 +59,6 @@ __device__ __forceinline__ SuperT super_round_up(double m)
     }
     return h;
 }
-#else
-typedef float SuperT;
-__device__ __forceinline__ SuperT super_round_up(double m) { return __double2float_ru(m); }
-#endif
 
 constexpr int kMaxBatchItems = 64;   // matches per batched launch chain (run_chunked)
 constexpr int kPipe = 16;   // seq_sum gathers in flight per batch (index arrays padded by 2*kPipe)
@@ -639,9 +631,16 @@ __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __re
 // cell stamps *negflag with this build's generation and k_super then keeps
 // every superblock.  NaN cells are skipped by the max: a block whose sum is
 // NaN fails c > thr and is never selected anyway.
-// output tile of k_super_planes: 128 padded columns = 32 consecutive values of
-// each column sub-phase, so every output row segment is one 128-byte store run
-constexpr int kSPX = 128, kSPY = 16;
+// k_super_planes: one workgroup per (tile of kSPX padded columns x kSPY
+// padded rows, plane, set).
+//  1. vertical 4-max in registers: a thread owns one footprint column
+//     (kSPX + 3 <= 256), loads its kSPY + 3 values (0 past the plane) at once
+//     and writes kSPY window maxima to LDS;
+//  2. horizontal 4-max from LDS, rounded toward +inf to fp16 (round-up is
+//     monotone, so rounding the max = max of the rounded), 8 consecutive
+//     superblocks of one sub-phase row per thread, one 16-byte store (Wq4 is a
+//     multiple of 8, so sub-phase rows are 16-byte aligned).
+constexpr int kSPX = 224, kSPY = 16;   // kSPX = 4 sub-phases x 56 (7 stores of 8)
 
 __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
 {
@@ -654,53 +653,58 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
     int* __restrict__ negflag = job.negflag;
     const int pgen = job.pgen;
     const int Wqp = pl.Wqp, Hqp = pl.Hqp;
-    const long long pstride = pl.pstride;
     constexpr int TW = kSPX + kSB - 1, TH = kSPY + kSB - 1;
-    __shared__ double tile[TH][TW];
-    __shared__ double hm[TH][kSPX];
+    __shared__ double vm[kSPY][TW];
     const int x0 = wg.x * kSPX, y0 = wg.y * kSPY;
-    const double* __restrict__ base = P + plane * pstride;
+    const double* __restrict__ base = P + plane * pl.pstride;
     SuperT* __restrict__ out = S + plane * pl.pstride4;
     const int tid = threadIdx.x;
     bool neg = false;
-    // all of a thread's loads issued before its LDS stores (a load-store loop
-    // would wait one memory latency per element)
-    constexpr int kTileLoads = (TH * TW + 255) / 256;
-    double cv[kTileLoads];
+    if (tid < TW) {
+        const int x = x0 + tid;
+        double v[TH];
 #pragma unroll
-    for (int j = 0; j < kTileLoads; ++j) {
-        const int k = tid + j * 256;
-        const int yy = k / TW, xx = k % TW;
-        const int x = x0 + xx, y = y0 + yy;
-        cv[j] = (k < TH * TW && x < Wqp && y < Hqp) ? base[(long long)y * Wqp + x] : 0.0;   // 0 past the plane
-    }
+        for (int k = 0; k < TH; ++k) {
+            const int y = y0 + k;
+            v[k] = (x < Wqp && y < Hqp) ? base[(long long)y * Wqp + x] : 0.0;   // 0 past the plane
+        }
 #pragma unroll
-    for (int j = 0; j < kTileLoads; ++j) {
-        const int k = tid + j * 256;
-        neg |= cv[j] < 0.0;
-        if (k < TH * TW) tile[k / TW][k % TW] = cv[j];
-    }
-    __syncthreads();
-    for (int k = tid; k < TH * kSPX; k += blockDim.x) {
-        const int yy = k / kSPX, xx = k % kSPX;
-        double m = tile[yy][xx];
+        for (int k = 0; k < TH; ++k) neg |= v[k] < 0.0;
 #pragma unroll
-        for (int i = 1; i < kSB; ++i) m = dmax2(m, tile[yy][xx + i]);
-        hm[yy][xx] = m;
+        for (int r = 0; r < kSPY; ++r) {
+            double m = v[r];
+#pragma unroll
+            for (int i = 1; i < kSB; ++i) m = dmax2(m, v[r + i]);
+            vm[r][tid] = m;
+        }
     }
     __syncthreads();
-    // destination order: (row, column sub-phase, column / 4), the last fastest
-    for (int k = tid; k < kSPY * kSPX; k += blockDim.x) {
-        const int yy = k / kSPX, r = k % kSPX;
-        const int xx = 4 * (r % (kSPX / 4)) + r / (kSPX / 4);
-        const int x = x0 + xx, y = y0 + yy;
-        if (x >= Wqp || y >= Hqp) continue;
-        double m = hm[yy][xx];
+    // horizontal 4-max, lane = padded column (conflict-free LDS reads), rounded
+    // up to fp16 and stored sub-phase-major: hs[r][sx][X4] = S at column 4 X4 + sx
+    constexpr int kQ = kSPX / 4;
+    __shared__ __attribute__((aligned(16))) SuperT hs[kSPY][4][kQ];
+    if (tid < kSPX) {
 #pragma unroll
-        for (int j = 1; j < kSB; ++j) m = dmax2(m, hm[yy + j][xx]);
-        // rounded toward +inf: still >= every member's coarse value, a
-        // quarter (fp16) or half (fp32) of the bytes for k_super's gathers
-        out[((y & 3) * 4 + (x & 3)) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + (x >> 2)] = super_round_up(m);
+        for (int r = 0; r < kSPY; ++r) {
+            double m = vm[r][tid];
+#pragma unroll
+            for (int j = 1; j < kSB; ++j) m = dmax2(m, vm[r][tid + j]);
+            hs[r][tid & 3][tid >> 2] = super_round_up(m);
+        }
+    }
+    __syncthreads();
+    // one 16-byte store of 8 consecutive superblocks of a sub-phase row per
+    // task (row, sub-phase, chunk), chunk fastest
+    constexpr int kChunks = kQ / 8;
+    typedef SuperT s8 __attribute__((ext_vector_type(8)));
+    const int q0 = x0 >> 2;   // the tile's first superblock column (x0 is a multiple of 4)
+    for (int k = tid; k < kSPY * 4 * kChunks; k += blockDim.x) {
+        const int r = k / (4 * kChunks), rem = k % (4 * kChunks);
+        const int sx = rem / kChunks, ch = rem % kChunks;
+        const int y = y0 + r;
+        const int xq = q0 + 8 * ch;
+        if (y >= Hqp || xq >= pl.Wq4) continue;
+        *(s8*)(out + ((y & 3) * 4 + sx) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + xq) = *(const s8*)&hs[r][sx][8 * ch];
     }
     if (neg) *negflag = pgen;
 }
@@ -883,7 +887,6 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, cons
     }
 }
 
-#if LGS_SUPER_F16
 // k_super_hex: k_super_quad with 8-byte gathers of FOUR fp16 superblocks
 // (a .. a + 3) of one row: a beam's 5 x 5 superblocks take 10 lanes, so one
 // wave instruction serves 6 beams (lanes 60..63 idle) instead of 4.  Used when
@@ -891,10 +894,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, cons
 // (slot q holds lanes 10 q .. 10 q + 9).  Tail elements past the row are read
 // from the padded planes (+ slack) and never added.
 typedef SuperT f4a2 __attribute__((ext_vector_type(4), aligned(sizeof(SuperT))));
-#ifndef LGS_HEX_PIPE
-#define LGS_HEX_PIPE 16
-#endif
-constexpr int kHexPipe = LGS_HEX_PIPE;   // gathers in flight per lane
+constexpr int kHexPipe = 16;   // gathers in flight per lane (4: 0.463, 8: 0.458, 16: 0.449 ms per 64 scans)
 __global__ __launch_bounds__(64 * kSupWaves) void k_super_hex(Items items, const double* __restrict__ zero)
 {
     const Blk wg = xcd_block();
@@ -981,7 +981,6 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_hex(Items items, const
         it.part_k[t] = bk;
     }
 }
-#endif
 
 // k_coarse_rows (superblock pruning): coarse scores of the blocks k_select
 // could take; workgroup (angle t, patch row pr) of kRowWaves waves.  The
@@ -2265,7 +2264,7 @@ void set_plane_layout(RtcsmPlan& pl)
     pl.Wqp = (pl.Wq + 2 * pl.M + 1) & ~1;   // even: 16-byte aligned plane rows (k_precompute_planes' paired stores)
     pl.Hqp = pl.Hq + 2 * pl.M;
     pl.pstride = (long long)pl.Wqp * pl.Hqp;
-    pl.Wq4 = (pl.Wqp + 3) / 4;
+    pl.Wq4 = (((pl.Wqp + 3) / 4) + 7) & ~7;   // 16-byte aligned fp16 sub-phase rows (k_super_planes' stores)
     pl.Hq4 = (pl.Hqp + 3) / 4;
     pl.sub4 = (long long)pl.Wq4 * pl.Hq4;
     pl.pstride4 = 16 * pl.sub4;
@@ -3017,7 +3016,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     B.pair = B.nsb2 <= 32;
     B.chunks = B.pair ? 1 : (B.nsb2 + 63) / 64;
     B.quad = ctx->super_quad && p0.nsby * ((p0.nsbx + 1) / 2) <= 16;
-    B.hex = LGS_SUPER_F16 && ctx->super_hex && B.quad && p0.nsby * ((p0.nsbx + 3) / 4) <= 10;
+    B.hex = ctx->super_hex && B.quad && p0.nsby * ((p0.nsbx + 3) / 4) <= 10;
     B.planes = ctx->coarse_planes;
     B.pruned = uses_super(ctx, B.NvMax, B.nsb2, false);
     B.lr5 = lr5_path(B.NvMax, B.low_res);

@@ -24,7 +24,7 @@ def layout(W, H, res, lr, rx, ry):
     Wq, Hq = -(-W // lr), -(-H // lr)
     Wqp = (Wq + 2 * M + 1) & ~1
     Hqp = Hq + 2 * M
-    Wq4, Hq4 = -(-Wqp // 4), -(-Hqp // 4)
+    Wq4, Hq4 = ((-(-Wqp // 4)) + 7) & ~7, -(-Hqp // 4)
     return dict(M=M, Wq=Wq, Hq=Hq, Wqp=Wqp, Hqp=Hqp, Wq4=Wq4, Hq4=Hq4, sub4=Wq4 * Hq4)
 
 
