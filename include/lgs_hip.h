@@ -190,6 +190,11 @@ typedef struct {
 } lgs_kernel_stat;
 int  lgs_ctx_kernel_stats(lgs_ctx* ctx, lgs_kernel_stat* out, int cap);  /* returns count (>=0) or -status */
 int  lgs_ctx_reset_stats(lgs_ctx* ctx);
+/* Correlative-match counters since the last lgs_ctx_reset_stats, over every
+ * OptimizePose / loop-detect match on the context (always collected):
+ * out4 = {matches, coarse blocks scored, coarse blocks a dense search scores
+ * (sum of the plans' K), matches that used superblock pruning}. */
+int  lgs_ctx_match_counters(lgs_ctx* ctx, int64_t* out4);
 
 /* ---- grids: dense row-major fp64, cell (x,y) at y*w+x, 0.0 = unknown ---- */
 int  lgs_grid_create(lgs_ctx* ctx, int w, int h, double min_x, double min_y,
@@ -381,6 +386,21 @@ int  lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* params, const l
                            double score_threshold, const lgs_loop_query* queries, int num_queries,
                            const lgs_loop_candidate* candidates, int num_candidates,
                            lgs_loop_result* results);
+
+/* Multi-GPU Detect for a caller that owns several GPUs in one
+ * process (the reference's backend calls Detect once,
+ * C/mapping/lidar_graph_slam_backend.cpp:39-40): the same contract and the
+ * same results, byte for byte, as lgs_loop_detect_rtcsm on ctxs[0].  The
+ * candidates are split into num_ctx contiguous shards, shard k =
+ * [k*n/N, (k+1)*n/N) runs on ctxs[k] on its own host thread; maps, coarse maps
+ * and scans owned by another context are copied to ctxs[k] first (peer copy
+ * over xGMI; scans re-uploaded from their host copy).  Errors of any shard are
+ * reported on ctxs[0]. */
+int  lgs_loop_detect_rtcsm_multi(lgs_ctx* const* ctxs, int num_ctx, const lgs_rtcsm_params* params,
+                                 const lgs_cost_ge_params* cost, double score_threshold,
+                                 const lgs_loop_query* queries, int num_queries,
+                                 const lgs_loop_candidate* candidates, int num_candidates,
+                                 lgs_loop_result* results);
 
 /* ---- branch-and-bound matcher ----
  * ScanMatcherBranchBound (C/mapping/scan_matcher_branch_bound.cpp:8-200,

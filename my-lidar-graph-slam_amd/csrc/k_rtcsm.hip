@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstring>
+#include <thread>
 #include <type_traits>
 
 using namespace lgs;
@@ -3172,6 +3173,10 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
         out[j].guard_hits = guard_hits;
         out[j].fixups = fixups;
         out[j].slow_path = slow;
+        ctx->count_matches += 1;
+        ctx->count_coarse_blocks += out[j].coarse_blocks;
+        ctx->count_coarse_blocks_dense += items[j].pl.K;
+        ctx->count_pruned += pruned ? 1 : 0;
     }
 }
 
@@ -3606,5 +3611,164 @@ extern "C" int lgs_loop_detect_rtcsm(lgs_ctx* ctx, const lgs_rtcsm_params* param
                 std::memcpy(r.covariance, s.covariance, sizeof(r.covariance));
             }
         }
+    });
+}
+
+namespace {
+
+// A copy of `src` (any device) owned by ctx: peer copy over xGMI, or a plain
+// device copy when both live on the same GPU.
+lgs_grid* clone_grid(lgs_ctx* ctx, const lgs_grid* src)
+{
+    lgs_grid* g = nullptr;
+    const int rc = lgs_grid_create(ctx, src->w, src->h, src->min_x, src->min_y, src->res, &g);
+    if (rc != LGS_OK) throw Error(rc, ctx->last_error);
+    const size_t bytes = sizeof(double) * (size_t)src->w * (size_t)src->h;
+    if (bytes) {
+        const hipError_t e = hipMemcpyPeerAsync(g->d, ctx->device, src->d, src->device, bytes, ctx->stream);
+        if (e == hipSuccess) ctx->sync();
+        if (e != hipSuccess) {
+            lgs_grid_destroy(g);
+            throw Error(LGS_ERR_HIP, std::string("hipMemcpyPeerAsync: ") + hipGetErrorString(e));
+        }
+    }
+    return g;
+}
+
+lgs_scan* clone_scan(lgs_ctx* ctx, const lgs_scan* src)
+{
+    lgs_scan_host h{};
+    h.n = src->n;
+    h.ranges = src->h_ranges.data();
+    h.angles = src->h_angles.data();
+    h.rel_sensor_pose = src->rel;
+    h.min_range = src->min_range;
+    h.max_range = src->max_range;
+    lgs_scan* s = nullptr;
+    const int rc = lgs_scan_create(ctx, &h, &s);
+    if (rc != LGS_OK) throw Error(rc, ctx->last_error);
+    return s;
+}
+
+// One shard of a multi-device loop batch: candidates [lo, hi) on ctx, the
+// queries clipped to that range; maps and scans are cloned onto ctx unless
+// they are its own.
+struct LoopShard {
+    lgs_ctx* ctx = nullptr;
+    int lo = 0, hi = 0;
+    std::vector<lgs_loop_query> qs;
+    std::vector<lgs_loop_candidate> cs;
+    std::vector<lgs_grid*> grids;   // owned clones
+    std::vector<lgs_scan*> scans;   // owned clones
+    int status = LGS_OK;
+    std::string error;
+
+    ~LoopShard()
+    {
+        for (lgs_grid* g : grids) lgs_grid_destroy(g);
+        for (lgs_scan* s : scans) lgs_scan_destroy(s);
+    }
+    const lgs_grid* own(const lgs_grid* g, std::vector<std::pair<const lgs_grid*, lgs_grid*>>& memo)
+    {
+        if (!g || g->ctx == ctx) return g;
+        for (auto& m : memo)
+            if (m.first == g) return m.second;
+        grids.push_back(clone_grid(ctx, g));
+        memo.push_back({ g, grids.back() });
+        return grids.back();
+    }
+    void prepare(const lgs_loop_query* queries, int num_queries, const lgs_loop_candidate* candidates)
+    {
+        std::vector<std::pair<const lgs_grid*, lgs_grid*>> memo;
+        for (int q = 0; q < num_queries; ++q) {
+            const lgs_loop_query& Q = queries[q];
+            const int a = std::max(Q.first_candidate, lo), b = std::min(Q.first_candidate + Q.num_candidates, hi);
+            if (a >= b) continue;
+            lgs_loop_query c = Q;
+            c.map = own(Q.map, memo);
+            c.coarse = own(Q.coarse, memo);
+            c.first_candidate = (int)cs.size();
+            c.num_candidates = b - a;
+            qs.push_back(c);
+            for (int i = a; i < b; ++i) {
+                lgs_loop_candidate k = candidates[i];
+                if (k.scan->ctx != ctx) {
+                    scans.push_back(clone_scan(ctx, k.scan));
+                    k.scan = scans.back();
+                }
+                cs.push_back(k);
+            }
+        }
+    }
+};
+
+}  // namespace
+
+extern "C" int lgs_loop_detect_rtcsm_multi(lgs_ctx* const* ctxs, int num_ctx, const lgs_rtcsm_params* params,
+                                           const lgs_cost_ge_params* cost, double score_threshold,
+                                           const lgs_loop_query* queries, int num_queries,
+                                           const lgs_loop_candidate* candidates, int num_candidates,
+                                           lgs_loop_result* results)
+{
+    if (!ctxs || num_ctx < 1 || !ctxs[0]) return LGS_ERR_INVALID_ARG;
+    for (int k = 1; k < num_ctx; ++k)
+        if (!ctxs[k]) return LGS_ERR_INVALID_ARG;
+    lgs_ctx* const c0 = ctxs[0];
+    if (num_ctx == 1 || num_candidates <= 1)
+        return lgs_loop_detect_rtcsm(c0, params, cost, score_threshold, queries, num_queries, candidates,
+                                     num_candidates, results);
+    if (!params || !cost || (num_queries > 0 && !queries) || num_queries < 0 || num_candidates < 0 ||
+        (num_candidates > 0 && (!candidates || !results)))
+        return LGS_ERR_INVALID_ARG;
+    return guarded(c0, [&] {
+        // the single-context contract first, so a bad batch fails the same way
+        // whatever the shard boundaries (:21-22, queries covering the candidates)
+        LGS_REQUIRE(score_threshold > 0.0 && score_threshold <= 1.0, "score threshold must be in (0, 1] (:21-22)");
+        int covered = 0;
+        for (int q = 0; q < num_queries; ++q) {
+            const lgs_loop_query& Q = queries[q];
+            LGS_REQUIRE(Q.map, "loop query without a local map");
+            LGS_REQUIRE(Q.first_candidate == covered && Q.num_candidates >= 0 &&
+                            Q.first_candidate + Q.num_candidates <= num_candidates,
+                        "loop queries must cover the candidates contiguously and in order");
+            covered += Q.num_candidates;
+            for (int j = 0; j < Q.num_candidates; ++j)
+                LGS_REQUIRE(candidates[Q.first_candidate + j].scan, "loop candidate without a scan");
+        }
+        LGS_REQUIRE(covered == num_candidates, "loop queries must cover every candidate");
+        const int N = std::min(num_ctx, num_candidates);
+        std::vector<LoopShard> shards((size_t)N);
+        for (int k = 0; k < N; ++k) {   // contiguous shards, as the gloo/RCCL path
+            shards[k].ctx = ctxs[k];
+            shards[k].lo = (int)((long long)num_candidates * k / N);
+            shards[k].hi = (int)((long long)num_candidates * (k + 1) / N);
+        }
+        auto work = [&](LoopShard& sh) {
+            try {
+                if (hipSetDevice(sh.ctx->device) != hipSuccess) throw Error(LGS_ERR_HIP, "hipSetDevice failed");
+                sh.prepare(queries, num_queries, candidates);
+                sh.status = lgs_loop_detect_rtcsm(sh.ctx, params, cost, score_threshold, sh.qs.data(),
+                                                  (int)sh.qs.size(), sh.cs.data(), (int)sh.cs.size(),
+                                                  results + sh.lo);
+                if (sh.status != LGS_OK) sh.error = sh.ctx->last_error;
+            } catch (const Error& e) {
+                sh.status = e.code;
+                sh.error = e.what();
+            } catch (const std::exception& e) {
+                sh.status = LGS_ERR_INTERNAL;
+                sh.error = e.what();
+            }
+        };
+        std::vector<std::thread> threads;
+        for (int k = 1; k < N; ++k) threads.emplace_back(work, std::ref(shards[k]));
+        work(shards[0]);
+        for (auto& t : threads) t.join();
+        LGS_HIP_CHECK(hipSetDevice(c0->device));
+        for (int k = 0; k < N; ++k)
+            if (shards[k].status != LGS_OK)
+                throw Error(shards[k].status, "shard " + std::to_string(k) + " (device " +
+                                                  std::to_string(shards[k].ctx->device) + "): " + shards[k].error);
+        // a result's start_node_index etc. come from its query, which each
+        // shard saw clipped but unchanged: nothing to remap
     });
 }

@@ -265,7 +265,18 @@ extern "C" int lgs_ctx_reset_stats(lgs_ctx* ctx)
             ctx->stat_ms[k] = 0;
             ctx->stat_bytes[k] = 0;
         }
+        ctx->count_matches = ctx->count_coarse_blocks = ctx->count_coarse_blocks_dense = ctx->count_pruned = 0;
     });
+}
+
+extern "C" int lgs_ctx_match_counters(lgs_ctx* ctx, int64_t* out4)
+{
+    if (!ctx || !out4) return LGS_ERR_INVALID_ARG;
+    out4[0] = ctx->count_matches;
+    out4[1] = ctx->count_coarse_blocks;
+    out4[2] = ctx->count_coarse_blocks_dense;
+    out4[3] = ctx->count_pruned;
+    return LGS_OK;
 }
 
 extern "C" void* lgs_ctx_stream(lgs_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
@@ -755,6 +766,7 @@ extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan**
     *out = nullptr;
     return guarded(ctx, [&] {
         LGS_REQUIRE(hs->n >= 1 && hs->ranges && hs->angles, "scan must have >= 1 beam");
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
         lgs_scan* s = new lgs_scan();
         s->ctx = ctx;
         s->device = ctx->device;

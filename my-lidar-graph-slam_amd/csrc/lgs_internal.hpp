@@ -242,6 +242,8 @@ struct lgs_ctx {
     int64_t stat_launches[lgs::K_NUM_KERNELS] = {};
     double stat_ms[lgs::K_NUM_KERNELS] = {};
     double stat_bytes[lgs::K_NUM_KERNELS] = {};
+    // correlative matches since the last lgs_ctx_reset_stats (lgs_ctx_match_counters)
+    int64_t count_matches = 0, count_coarse_blocks = 0, count_coarse_blocks_dense = 0, count_pruned = 0;
 
     // profiling helpers: begin() before a launch, end() after it, harvest()
     // after a stream synchronisation.

@@ -394,9 +394,11 @@ void GridMapHip::Download(std::vector<double>* cells, std::vector<uint32_t>* hit
 
 // ------------------------------------------ LoopDetectorRealTimeCorrelativeHip
 LoopDetectorRealTimeCorrelativeHip::LoopDetectorRealTimeCorrelativeHip(
-    std::shared_ptr<ScanMatcherRealTimeCorrelativeHip> m, double thr)
-    : mScanMatcher(std::move(m)), mScoreThreshold(thr)
+    std::shared_ptr<ScanMatcherRealTimeCorrelativeHip> m, double thr, std::vector<DevicePtr> extra)
+    : mScanMatcher(std::move(m)), mScoreThreshold(thr), mExtraDevices(std::move(extra))
 {
+    for (const auto& d : mExtraDevices)
+        if (!d) throw Error(LGS_ERR_INVALID_ARG, "LoopDetectorRealTimeCorrelativeHip: null device");
     if (!(thr > 0.0 && thr <= 1.0))   // the reference asserts this (:21-22)
         throw Error(LGS_ERR_INVALID_ARG, "LoopDetectorRealTimeCorrelativeHip: score threshold must be in (0, 1]");
 }
@@ -424,10 +426,12 @@ void LoopDetectorRealTimeCorrelativeHip::Detect(std::vector<LoopDetectionQuery>&
             cs.push_back(lgs_loop_candidate{ n.mScanData->Handle(), to_c(n.mPose), n.mIndex, 0 });
     }
     std::vector<lgs_loop_result> out(cs.size());
-    dev->Check(lgs_loop_detect_rtcsm(dev->Handle(), &mScanMatcher->Params(), &mScanMatcher->Cost(),
-                                     mScoreThreshold, qs.data(), (int)qs.size(), cs.data(), (int)cs.size(),
-                                     out.data()),
-               "lgs_loop_detect_rtcsm");
+    std::vector<lgs_ctx*> ctxs{ dev->Handle() };
+    for (const auto& d : mExtraDevices) ctxs.push_back(d->Handle());
+    dev->Check(lgs_loop_detect_rtcsm_multi(ctxs.data(), (int)ctxs.size(), &mScanMatcher->Params(),
+                                           &mScanMatcher->Cost(), mScoreThreshold, qs.data(), (int)qs.size(),
+                                           cs.data(), (int)cs.size(), out.data()),
+               "lgs_loop_detect_rtcsm_multi");
     for (const auto& r : out) {
         if (!r.found) continue;   // the reference appends only detected loops, in order (:77-88)
         LoopDetectionResult o;

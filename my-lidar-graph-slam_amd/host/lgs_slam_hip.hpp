@@ -330,15 +330,20 @@ struct LoopDetectionResult {
 
 class LoopDetectorRealTimeCorrelativeHip {
 public:
+    // extraDevices: more GPUs of this process to shard the candidates over
+    // (lgs_loop_detect_rtcsm_multi); the matcher's own device is shard 0 and
+    // holds the queries' maps and scans.  Results are the same with or without.
     LoopDetectorRealTimeCorrelativeHip(std::shared_ptr<ScanMatcherRealTimeCorrelativeHip> scanMatcher,
-                                       double scoreThreshold);
+                                       double scoreThreshold, std::vector<DevicePtr> extraDevices = {});
     // Detect (:26-92): coarse maps computed once per query, every node matched,
     // found ones appended in query -> node order.
     void Detect(std::vector<LoopDetectionQuery>& queries, std::vector<LoopDetectionResult>& results);
+    int NumDevices() const { return 1 + (int)mExtraDevices.size(); }
 
 private:
     std::shared_ptr<ScanMatcherRealTimeCorrelativeHip> mScanMatcher;
     double mScoreThreshold;
+    std::vector<DevicePtr> mExtraDevices;
 };
 
 // LoopDetectorBranchBound (C/mapping/loop_detector_branch_bound.cpp:10-117):

@@ -173,6 +173,7 @@ _PROTOS = [
     ("lgs_ctx_set_option", C.c_int, [_P, C.c_int, C.c_double]),
     ("lgs_ctx_kernel_stats", C.c_int, [_P, C.POINTER(KernelStat), C.c_int]),
     ("lgs_ctx_reset_stats", C.c_int, [_P]),
+    ("lgs_ctx_match_counters", C.c_int, [_P, C.POINTER(C.c_int64)]),
     ("lgs_grid_create", C.c_int, [_P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.POINTER(_P)]),
     ("lgs_grid_wrap", C.c_int, [_P, _P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.POINTER(_P)]),
     ("lgs_grid_destroy", None, [_P]),
@@ -229,6 +230,9 @@ _PROTOS = [
     ("lgs_loop_detect_rtcsm", C.c_int, [_P, C.POINTER(RtcsmParams), C.POINTER(CostGEParams), C.c_double,
                                         C.POINTER(LoopQuery), C.c_int, C.POINTER(LoopCandidate), C.c_int,
                                         C.POINTER(LoopResult)]),
+    ("lgs_loop_detect_rtcsm_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(RtcsmParams),
+                                              C.POINTER(CostGEParams), C.c_double, C.POINTER(LoopQuery), C.c_int,
+                                              C.POINTER(LoopCandidate), C.c_int, C.POINTER(LoopResult)]),
     ("lgs_linsolve_optimize_pose", C.c_int, [_P, _P, C.POINTER(LinsolveParams), _P, Pose2D,
                                              C.POINTER(LinsolveSummary), C.POINTER(C.c_double)]),
     ("lgs_linsolve_optimize_pose_batch", C.c_int, [_P, _P, C.POINTER(LinsolveParams), C.POINTER(_P),
@@ -300,6 +304,13 @@ class Context:
 
     def reset_stats(self):
         self.check(self.lib.lgs_ctx_reset_stats(self.h), "reset_stats")
+
+    def match_counters(self) -> dict:
+        """matches / coarse blocks scored / dense coarse blocks / pruned matches
+        since the last reset_stats (lgs_ctx_match_counters)"""
+        buf = (C.c_int64 * 4)()
+        self.check(self.lib.lgs_ctx_match_counters(self.h, buf), "match_counters")
+        return dict(matches=buf[0], coarse_blocks=buf[1], coarse_blocks_dense=buf[2], pruned=buf[3])
 
     def synchronize(self):
         self.check(self.lib.lgs_ctx_synchronize(self.h), "synchronize")
@@ -413,9 +424,12 @@ class Context:
         return list(dims), cs, fs
 
     # ---- loop-closure batch ----
-    def loop_detect(self, params: RtcsmParams, cost: CostGEParams, thr: float, queries, candidates):
+    def loop_detect(self, params: RtcsmParams, cost: CostGEParams, thr: float, queries, candidates,
+                    shards: Sequence["Context"] = ()):
         """queries: [(map Grid, coarse Grid|None, node_pose, node_index, first, count)];
-        candidates: [(Scan, node_pose, node_index)] -> ctypes LoopResult array (one per candidate)."""
+        candidates: [(Scan, node_pose, node_index)] -> ctypes LoopResult array (one per candidate).
+        shards: further contexts (GPUs) to split the candidates over
+        (lgs_loop_detect_rtcsm_multi; this context is shard 0)."""
         qs = (LoopQuery * max(1, len(queries)))()
         for i, (m, c, pose, idx, first, cnt) in enumerate(queries):
             qs[i] = LoopQuery(m.h, c.h if c is not None else None, Pose2D(*pose), idx, first, cnt)
@@ -423,6 +437,12 @@ class Context:
         for i, (s, pose, idx) in enumerate(candidates):
             cs[i] = LoopCandidate(s.h, Pose2D(*pose), idx, 0)
         out = (LoopResult * max(1, len(candidates)))()
+        if shards:
+            hs = (_P * (1 + len(shards)))(self.h, *[c.h for c in shards])
+            self.check(self.lib.lgs_loop_detect_rtcsm_multi(hs, len(hs), C.byref(params), C.byref(cost), float(thr),
+                                                            qs, len(queries), cs, len(candidates), out),
+                       "loop_detect_rtcsm_multi")
+            return out
         self.check(self.lib.lgs_loop_detect_rtcsm(self.h, C.byref(params), C.byref(cost), float(thr), qs,
                                                   len(queries), cs, len(candidates), out), "loop_detect_rtcsm")
         return out

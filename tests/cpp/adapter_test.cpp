@@ -92,6 +92,11 @@ bool same_pose(const RobotPose2D<double>& a, const orc_pose& b)
     return a.mX == b.x && a.mY == b.y && a.mTheta == b.theta;
 }
 
+bool same_pose(const RobotPose2D<double>& a, const RobotPose2D<double>& b)
+{
+    return a.mX == b.mX && a.mY == b.mY && a.mTheta == b.mTheta;
+}
+
 std::string fmt_pose(const RobotPose2D<double>& a, const orc_pose& b)
 {
     char buf[256];
@@ -316,6 +321,20 @@ int main()
             ok = res[i].mEndNodeIdx == expect[i].first && same_pose(res[i].mRelativePose, expect[i].second);
         check(ok && !res.empty(), "LoopDetectorRealTimeCorrelative::Detect == oracle (" + std::to_string(res.size()) +
                                       " of 8 found)");
+        // the same Detect sharded over two more contexts on this GPU (one host
+        // thread each, maps peer-copied): identical results
+        auto d2 = std::make_shared<Device>(0), d3 = std::make_shared<Device>(0);
+        LoopDetectorRealTimeCorrelativeHip multi(rtc, 0.35, { d2, d3 });
+        std::vector<LoopDetectionResult> mres;
+        multi.Detect(qs, mres);
+        bool same_all = mres.size() == res.size() && multi.NumDevices() == 3;
+        for (std::size_t i = 0; same_all && i < res.size(); ++i) {
+            const auto &a = res[i], &b = mres[i];
+            same_all = a.mStartNodeIdx == b.mStartNodeIdx && a.mEndNodeIdx == b.mEndNodeIdx &&
+                       same_pose(a.mRelativePose, b.mRelativePose) && same_pose(a.mStartNodePose, b.mStartNodePose) &&
+                       a.mEstimatedCovMat.m == b.mEstimatedCovMat.m;
+        }
+        check(same_all, "LoopDetectorRealTimeCorrelativeHip over 3 devices == one device");
     }
 
     // ---- ScanMatcherBranchBoundHip (query + the loop overload) and LoopDetectorBranchBoundHip

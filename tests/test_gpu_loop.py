@@ -79,6 +79,55 @@ def test_loop_detect_config5_json_window(ctx, world):
     maps, cands = scene.loop_problem(world, build, n_maps=2, nodes_per_map=2, n_beams=1081, seed=21,
                                      perturb=(1.0, 0.3), arc_scans=8)
     p, c = abi.RtcsmParams(*LOOP_JSON), abi.CostGEParams(*small.COST)
+    ctx.reset_stats()
     dev = loopbatch.run_sharded(cands, loopbatch.hip_detect_fn(ctx, maps, cands, p, c, 0.6))
     orc = loopbatch.run_sharded(cands, oracle_detect_fn(maps, cands, LOOP_JSON, small.COST, 0.6))
     compare(loopbatch.decode(dev), loopbatch.decode(orc))
+    # the JSON window has 6 x 6 = 36 superblocks per angle (21 x 21 coarse
+    # blocks at LowRes 5): superblock pruning runs, and scores fewer blocks
+    # than the dense search (loop_detector_real_time_correlative.cpp:100-125)
+    cnt = ctx.match_counters()
+    assert cnt["matches"] == len(cands) and cnt["pruned"] == len(cands), cnt
+    assert cnt["coarse_blocks"] < cnt["coarse_blocks_dense"], cnt
+    ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 1)
+    try:
+        ctx.reset_stats()
+        dense = loopbatch.run_sharded(cands, loopbatch.hip_detect_fn(ctx, maps, cands, p, c, 0.6))
+        cd = ctx.match_counters()
+    finally:
+        ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 0)
+    assert cd["pruned"] == 0 and cd["coarse_blocks"] == cd["coarse_blocks_dense"] == cnt["coarse_blocks_dense"], cd
+    assert dense.tobytes() == dev.tobytes()
+
+
+@pytest.mark.parametrize("n_shards", [2, 3])
+def test_loop_detect_multi_context_identical(ctx, n_shards):
+    """lgs_loop_detect_rtcsm_multi: the candidates split over more contexts
+    (here all on GPU 0, one host thread each, maps and scans copied over) give
+    byte-identical records to the one-context call (the
+    multi-GPU form of the backend's single Detect call,
+    lidar_graph_slam_backend.cpp:39-40)."""
+    maps, cands = small.make_problem()
+    p, c = abi.RtcsmParams(*small.PARAMS), abi.CostGEParams(*small.COST)
+    grids = [ctx.grid_from_array(m.cells, m.min_x, m.min_y, m.res) for m in maps]
+    coarse = [ctx.precompute_max(g, small.PARAMS[0]) if i % 2 == 0 else None for i, g in enumerate(grids)]
+    scans = [ctx.scan(x.ranges, x.angles) for x in cands]
+    qs, first = [], 0
+    for qi, m in enumerate(maps):
+        n = sum(1 for x in cands if x.query == qi)
+        qs.append((grids[qi], coarse[qi], m.node_pose, m.node_index, first, n))
+        first += n
+    cl = [(s, x.pose, x.node_index) for s, x in zip(scans, cands)]
+    one = bytes(ctx.loop_detect(p, c, small.THR, qs, cl))
+    others = [abi.Context(0) for _ in range(n_shards - 1)]
+    try:
+        multi = bytes(ctx.loop_detect(p, c, small.THR, qs, cl, shards=others))
+        again = bytes(ctx.loop_detect(p, c, small.THR, qs, cl, shards=others))
+        with pytest.raises(abi.LgsError):   # the single-context contract holds (:21-22)
+            ctx.loop_detect(p, c, 1.5, qs, cl, shards=others)
+    finally:
+        for o in others:
+            o.close()
+    assert multi == one
+    assert again == one
+    assert len(cands) >= n_shards
