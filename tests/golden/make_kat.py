@@ -27,8 +27,11 @@ import json
 import math
 import os
 import random
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
 
 _libm = ctypes.CDLL(ctypes.util.find_library("m"))
 _libm.sincos.restype = None
@@ -422,6 +425,9 @@ def main():
         si.append({"ranges": ranges, "angles": angles, "dist_scans": ds, "dist_empty": de,
                    "out_ranges": rr, "out_angles": aa})
     kat["interp_py"] = si
+
+    import kat_ext                  # round-2 restatements (cost, refine, geometry)
+    kat_ext.extend(kat, rnd)
 
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump(kat, f, indent=None, separators=(",", ":"))

@@ -248,3 +248,96 @@ def test_colpiv_qr_solves():
         x = np.zeros(3)
         ob.lib().orc_solve3_colpiv_qr(ob.dp(np.ascontiguousarray(H)), ob.dp(b), ob.dp(x))
         assert np.allclose(H @ x, b, rtol=1e-9, atol=1e-9)
+
+
+# ---- round-2 known answers (tests/golden/kat_ext.py) ----
+
+def _ogrid(c):
+    return ob.OGrid(np.array(c["grid"], dtype=np.float64), c["min"][0], c["min"][1], c["res"])
+
+
+def _oscan(c, rel=(0.0, 0.0, 0.0)):
+    return ob.OScan(c["ranges"], c["angles"], rel, c["scan_range"][0], c["scan_range"][1])
+
+
+@pytest.mark.parametrize("i", range(len(KAT["cost_ge_py"])))
+def test_cost_greedy_endpoint_kat(i):
+    """CostGreedyEndpoint Cost / ComputeCovariance (cost_function_greedy_endpoint.cpp:32-171)
+    in both constructor argument orders (the launcher's swap, slam_launcher.cpp:68-71):
+    bit-exact (same glibc exp, same summation order)."""
+    c = KAT["cost_ge_py"][i]
+    g, s = _ogrid(c), _oscan(c)
+    cp = ob.CostGE(*c["params"])
+    assert ob.lib().orc_cost_ge_cost(C.byref(g.g), C.byref(cp), C.byref(s.s), ob.Pose(*c["pose"])) == c["cost"]
+    cov = np.zeros(9)
+    ob.lib().orc_cost_ge_covariance(C.byref(g.g), C.byref(cp), C.byref(s.s), ob.Pose(*c["pose"]), ob.dp(cov))
+    assert cov.tolist() == c["cov"]
+
+
+def test_cost_greedy_endpoint_orders_differ():
+    """the swapped order really is a different cost (scale 0.05, sigma 1.0)"""
+    pairs = [KAT["cost_ge_py"][k:k + 2] for k in range(0, len(KAT["cost_ge_py"]), 2)]
+    assert all(a["order"] == "json" and b["order"] == "launcher" for a, b in pairs)
+    assert any(a["cost"] != b["cost"] for a, b in pairs)
+
+
+@pytest.mark.parametrize("i", range(len(KAT["sq_py"])))
+def test_square_error_and_step_kat(i):
+    """CostSquareError bicubic value / cost / covariance and one LinearSolver
+    OptimizeStep with the column-pivoting QR (cost_function_square_error.cpp:20-346,
+    scan_matcher_linear_solver.cpp:88-148).  Eigen's inner summation order is not
+    restated, so the bar is a relative 1e-12."""
+    c = KAT["sq_py"][i]
+    g, s = _ogrid(c), _oscan(c)
+    L = ob.lib()
+    for (x, y), want in zip(c["points"], c["smoothed"]):
+        assert L.orc_sq_smoothed_value(C.byref(g.g), x, y) == pytest.approx(want, rel=1e-12, abs=1e-15)
+    um, uM = c["usable"]
+    pose = ob.Pose(*c["pose"])
+    assert L.orc_sq_cost(C.byref(g.g), um, uM, C.byref(s.s), pose) == pytest.approx(c["cost"], rel=1e-12)
+    cov = np.zeros(9)
+    L.orc_sq_covariance(C.byref(g.g), um, uM, C.byref(s.s), pose, ob.dp(cov))
+    assert np.allclose(cov, c["cov"], rtol=1e-12, atol=1e-14)
+    lp = ob.LinsolveParams(1, 0.0, um, uM, c["reg"][0], c["reg"][1], um, uM)
+    st = L.orc_linsolve_step(C.byref(g.g), C.byref(lp), C.byref(s.s), pose)
+    assert np.allclose([st.x, st.y, st.theta], c["step"], rtol=1e-12, atol=1e-14)
+
+
+def test_colpiv_qr_kat():
+    for c in KAT["colpiv_qr_py"]:
+        x = np.zeros(3)
+        ob.lib().orc_solve3_colpiv_qr(ob.dp(np.array(c["H"])), ob.dp(np.array(c["b"])), ob.dp(x))
+        assert np.allclose(x, c["x"], rtol=1e-12, atol=1e-14)
+
+
+def _geo(m):
+    g = m.geometry()
+    return dict(w=g["w"], h=g["h"], min_x=g["min_x"], min_y=g["min_y"], npx=g["npx"], npy=g["npy"])
+
+
+@pytest.mark.parametrize("i", range(len(KAT["geometry_py"])))
+def test_grid_geometry_kat(i):
+    """GridMap constructor / Resize / Expand / patch index (grid_map.hpp:337-391,
+    652-736, 905-915): every state bit-exact."""
+    c = KAT["geometry_py"][i]
+    res, ps, ncx, ncy, cx, cy = c["init"]
+    m = ob.OMap(res, ps, ncx, ncy, (cx, cy))
+    assert _geo(m) == c["init_state"]
+    for op, want in zip(c["ops"], c["states"]):
+        if op[0] == "resize":
+            ob.lib().orc_map_resize(C.byref(m.m), *op[1:5])
+        else:
+            ob.lib().orc_map_expand(C.byref(m.m), *op[1:6])
+        assert _geo(m) == want, op
+
+
+@pytest.mark.parametrize("i", range(len(KAT["construct_geometry_py"])))
+def test_construct_map_geometry_kat(i):
+    """ConstructMapFromScans' bounding box and Resize (grid_map_builder.cpp:227-290),
+    incl. the DBL_MIN topRight start: the resulting geometry bit-exact."""
+    c = KAT["construct_geometry_py"][i]
+    res, ps, nc = c["init"]
+    m = ob.OMap(res, ps, nc, nc)
+    scans = [ob.OScan(n["ranges"], n["angles"], tuple(n["rel"]), *n["scan_range"]) for n in c["nodes"]]
+    m.construct([tuple(n["pose"]) for n in c["nodes"]], scans, ob.BuilderParams(*c["usable"], 0.6, 0.45))
+    assert _geo(m) == c["state"]
