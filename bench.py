@@ -44,6 +44,7 @@ LOOP_PARAMS = (5, 5.0, 5.0, 1.0, 20.0)           # launcher_settings_default.jso
 BB_PARAMS = (6, 2.0, 2.0, 1.0, 20.0, 0.01, 20.0)  # LoopDetectorBranchBound (launcher_settings_default.json:128-146)
 COST = (0.01, 20.0, 0.075, 0.1, 1, 0.05, 1.0)    # launcher-built CostGreedyEndpoint members
 LINSOLVE = (50, 0.0, 0.01, 20.0, 1e-3, 1e-3, 0.01, 20.0)   # config 3
+STREAM_WINDOWS = {"json": (0.2, 0.2, 0.5), "config2": (4.0, 4.0, 1.0471976)}   # search range x, y, theta
 BUILDER = (0.01, 20.0, 0.6, 0.45)                # GridMapBuilder usable range, pHit, pMiss
 HBM_PEAK_GBS = 8000.0                            # MI355X_MICROARCH.md: 8.0 TB/s spec
 
@@ -78,6 +79,9 @@ def parse():
     ap.add_argument("--interp", type=int, default=1,
                     help="stream workload: 1 (default, the launcher's UseScanInterpolator) interpolates every "
                          "scan (lgs_scan_interpolate, DistScans 0.05 / DistThresholdEmpty 0.25), 0 raw scans")
+    ap.add_argument("--window", default="json", choices=sorted(STREAM_WINDOWS),
+                    help="stream workload: search window (json = the launcher's frontend 0.2 m/0.2 m/0.5 rad, "
+                         "config2 = +-2 m/+-30 deg)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_pmc_summary.json"),
                     help="rocprofv3 PMC summary (tools/pmc_summary.py) of THIS library build: roofline.traffic "
                          "is taken from it only when its lib_sha256 matches liblgs_hip.so, else null")
@@ -602,7 +606,8 @@ def run_stream(args, D, ctx):
     truths = [(5.0 * np.cos(0.02 * k), 5.0 * np.sin(0.02 * k), 0.02 * k + np.pi / 2) for k in range(n)]
     ranges = [scene.ray_cast(world, t, ang) for t in truths]
     bp = abi.BuilderParams(*BUILDER)
-    P, cost = abi.RtcsmParams(5, 0.2, 0.2, 0.5, 20.0), abi.CostGEParams(*COST)   # JSON frontend window
+    win = STREAM_WINDOWS[args.window]
+    P, cost = abi.RtcsmParams(5, *win, 20.0), abi.CostGEParams(*COST)
     local = ctx.map(0.05, 100, 200, 200, center=truths[0][:2])
     latest = ctx.map(0.05, 100, 200, 200, center=truths[0][:2])
     raw = [ctx.scan(r, ang) for r in ranges]
@@ -621,27 +626,39 @@ def run_stream(args, D, ctx):
         c, s = np.cos(last[2]), np.sin(last[2])
         return (last[0] + c * d[0] - s * d[1], last[1] + s * d[0] + c * d[1], last[2] + d[2])
 
+    phase = dict(interpolate=0.0, latest_map=0.0, match=0.0, insert=0.0)
+
     def step(k):
+        t = [time.perf_counter()]
         guess = odometry(rng, est[-1])
         frontend_scan(k)
+        t.append(time.perf_counter())
         lo = max(0, k - 10)
         latest.construct(dscans[lo:k], est[lo:k], bp)                       # UpdateLatestMap (10 scans)
+        t.append(time.perf_counter())
         out = ctx.optimize_pose_query(latest.grid(), P, cost, dscans[k], guess)
         e = out.estimated_pose
         est.append((e.x, e.y, e.theta))
+        t.append(time.perf_counter())
         local.update_scan(dscans[k], est[-1], bp)                           # UpdateGridMap insert
+        t.append(time.perf_counter())
+        for i, name in enumerate(phase):
+            phase[name] += t[i + 1] - t[i]
 
     for k in range(1, args.warmup + 1):
         step(k)
     set_timed_events(ctx, args, "k_ray_apply")
     D.barrier()
     t0 = time.perf_counter()
+    for name in phase:
+        phase[name] = 0.0
     for k in range(args.warmup + 1, n):
         step(k)
     elapsed = D.max(time.perf_counter() - t0)
     stats = ctx.kernel_stats()
     ctx.set_option(abi.LGS_OPT_PROFILE, 0)
     steps = n - args.warmup - 1
+    breakdown = {f"{name}_ms": round(1e3 * v / steps, 4) for name, v in phase.items()}
     drift = max(abs(est[-1][0] - truths[len(est) - 1][0]), abs(est[-1][1] - truths[len(est) - 1][1]))
     value = steps * D.world / elapsed
     cpu = None
@@ -651,7 +668,7 @@ def run_stream(args, D, ctx):
         ob = oracle_lib()
         orng = np.random.default_rng(7)
         obp = ob.BuilderParams(*BUILDER)
-        oprm, ocost = ob.RtcsmParams(5, 0.2, 0.2, 0.5, 20.0), ob.CostGE(*COST)
+        oprm, ocost = ob.RtcsmParams(5, *win, 20.0), ob.CostGE(*COST)
         olocal = ob.OMap(0.05, 100, 200, 200, center=truths[0][:2])
         olatest = ob.OMap(0.05, 100, 200, 200, center=truths[0][:2])
 
@@ -691,9 +708,10 @@ def run_stream(args, D, ctx):
         value=round(value, 2), unit="scans/s", n_gpus=D.world, steps=steps, warmup=args.warmup,
         ms_per_step=round(1e3 * elapsed / steps, 4), higher_is_better=True, scaling="weak", vs_baseline=None,
         dtype="f64", data="synthetic circular trajectory, odometry noise (0.01 m, 0.005 rad)",
-        config=dict(workload="config4: streaming frontend (JSON window 0.2/0.2/0.5)", beams=1081,
+        config=dict(workload=f"config4: streaming frontend ({args.window} window "
+                             f"{'/'.join(str(v) for v in win)})", beams=1081,
                     scan_interpolator=bool(args.interp), latest_map_scans=10, parallelism=f"replicas x{D.world}"),
-        final_drift_m=round(float(drift), 4),
+        final_drift_m=round(float(drift), 4), breakdown_per_step=breakdown,
         roofline=roofline_from(stats, "k_ray_apply", args.pmc, "k_apply", "hbm"), cpu_baseline=cpu)
     return line, stats, value
 

@@ -146,16 +146,33 @@ struct PlaneJob {
 
 // Generation-tagged counter (gen << 32 | count): a word left by an earlier
 // match counts as zero, so records need no memset.  Returns this caller's slot.
-__device__ __forceinline__ int tagged_slot(unsigned long long* w, unsigned gen)
+__device__ __forceinline__ int tagged_add(unsigned long long* w, unsigned gen, unsigned k)
 {
     unsigned long long cur = *(volatile unsigned long long*)w, assumed;
     unsigned cnt;
     do {
         assumed = cur;
         cnt = ((unsigned)(assumed >> 32) == gen) ? (unsigned)assumed : 0u;
-        cur = atomicCAS(w, assumed, ((unsigned long long)gen << 32) | (unsigned long long)(cnt + 1u));
+        cur = atomicCAS(w, assumed, ((unsigned long long)gen << 32) | (unsigned long long)(cnt + k));
     } while (cur != assumed);
     return (int)cnt;
+}
+
+// Slot of a guard record: the active lanes with want = true take consecutive
+// slots with ONE compare-and-swap loop per wave (a loop per lane on one
+// address serialises thousands of retries when many hit points sit on cell
+// boundaries: axis-aligned walls, measured 7 ms per k_cost launch).  Every
+// active lane must call it; lanes without a record get -1.
+__device__ __forceinline__ int tagged_slot_wave(unsigned long long* w, unsigned gen, bool want)
+{
+    const unsigned long long m = __ballot(want);
+    if (m == 0ull) return -1;
+    const int lane = (int)__lane_id();
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = tagged_add(w, gen, (unsigned)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return want ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
 }
 
 __device__ __forceinline__ bool near_boundary(double q, double eps)
@@ -188,7 +205,10 @@ __device__ __forceinline__ int super_base(int ix, int iy, const RtcsmPlan& pl)
     const int bx = ix - pl.win_x, by = iy - pl.win_y;
     const int qx0 = floor_div(bx, lr), qy0 = floor_div(by, lr);
     const int rx = bx - lr * qx0, ry = by - lr * qy0;
-    const bool touches = (qx0 < pl.Wq) & (qx0 + pl.ncx > 0) & (qy0 < pl.Hq) & (qy0 + pl.ncy > 0);
+    // the strip qx = -1 (rx > 0) / qy = -1 (ry > 0) holds the clamped values
+    // of k_super_planes: a window that reaches only the strip still counts
+    const bool touches = (qx0 < pl.Wq) & (qx0 + pl.ncx > (rx > 0 ? -1 : 0)) & (qy0 < pl.Hq) &
+                         (qy0 + pl.ncy > (ry > 0 ? -1 : 0));
     const int Qx = qx0 + pl.M, Qy = qy0 + pl.M;
     return touches ? (int)((ry * lr + rx) * pl.pstride4 + ((Qy & 3) * 4 + (Qx & 3)) * pl.sub4 +
                            (long long)(Qy >> 2) * pl.Wq4 + (Qx >> 2))
@@ -292,8 +312,9 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     const double qy = (hy - pl.min_y) / pl.res;
     int ix = (int)floor(qx);
     int iy = (int)floor(qy);
-    if (near_boundary(qx, guard_eps) || near_boundary(qy, guard_eps)) {
-        const int slot = tagged_slot(&rec->guard_word, (unsigned)gen);
+    const bool guarded = near_boundary(qx, guard_eps) || near_boundary(qy, guard_eps);
+    const int slot = tagged_slot_wave(&rec->guard_word, (unsigned)gen, guarded);
+    if (guarded) {
         if (slot < guard_cap) {
             GuardRec g;
             g.t = tt;
@@ -657,17 +678,30 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
     constexpr int TW = kSPX + kSB - 1, TH = kSPY + kSB - 1;
     __shared__ double vm[kSPY][TW];
     const int x0 = wg.x * kSPX, y0 = wg.y * kSPY;
-    const double* __restrict__ base = P + plane * pl.pstride;
     SuperT* __restrict__ out = S + plane * pl.pstride4;
     const int tid = threadIdx.x;
+    // the strip left of / below the map (padded column / row M - 1 of the
+    // planes rx >= 1 / ry >= 1: coarse x, y in [-(lr - 1), -1], whose fine
+    // windows overlap the map) reads the map's first coarse column / row
+    // C(0, y) / C(x, 0) >= every fine value of the overlap, so superblock
+    // bounds also bound the FINE scores of unsafe blocks;
+    // the coarse planes themselves keep the reference's zeros there
+    const int lr = pl.low_res, M = pl.M;
+    const int rx = plane % lr, ry = plane / lr;
     bool neg = false;
     if (tid < TW) {
         const int x = x0 + tid;
+        const bool cx = (x == M - 1) && rx > 0;
+        const int sx = cx ? M : x;
+        const double* __restrict__ colp = P + (long long)(cx ? ry * lr : plane) * pl.pstride;   // plane (ry, 0)
+        const double* __restrict__ rowp = P + (long long)(cx ? 0 : rx) * pl.pstride;           // plane (0, rx)
         double v[TH];
 #pragma unroll
         for (int k = 0; k < TH; ++k) {
             const int y = y0 + k;
-            v[k] = (x < Wqp && y < Hqp) ? base[(long long)y * Wqp + x] : 0.0;   // 0 past the plane
+            const bool cy = (y == M - 1) && ry > 0;
+            const double* __restrict__ src = cy ? rowp + (long long)M * Wqp : colp + (long long)y * Wqp;
+            v[k] = (x < Wqp && y < Hqp) ? src[sx] : 0.0;   // 0 past the plane
         }
 #pragma unroll
         for (int k = 0; k < TH; ++k) neg |= v[k] < 0.0;
@@ -730,8 +764,6 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
     const SuperT* __restrict__ sp = it.super;
     const SuperT* __restrict__ zf = (const SuperT*)zero;
     const int* __restrict__ cbase = it.cbase;
-    const int* __restrict__ tedge = it.tedge;
-    const int gen = it.gen;
     const int* __restrict__ negflag = it.negflag;
     const int pgen = it.pgen;
     double* __restrict__ sbound = it.sbound;
@@ -777,8 +809,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
     const double bound = (*negflag == pgen) ? INFINITY : tot * pl.sb_mult;
     const bool own = act && h == 0;
     if (own) sbound[(size_t)t * nsb2 + sbi] = bound;
-    // rows that may hold unsafe blocks never seed: -inf (bounds are >= 0)
-    const bool seedable = own && tedge[t] != gen;
+    const bool seedable = own;   // k_seed_super skips unsafe members
     double bv = seedable ? bound : -INFINITY;
     long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
     for (int off = 32; off > 0; off >>= 1) {
@@ -870,8 +901,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, cons
     }
     const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult;
     if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
-    // rows that may hold unsafe blocks never seed: -inf (bounds are >= 0)
-    const bool seedable = own && it.tedge[t] != it.gen;
+    const bool seedable = own;   // k_seed_super skips unsafe members
     double bv = seedable ? bound : -INFINITY;
     long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
     for (int off = 32; off > 0; off >>= 1) {
@@ -966,7 +996,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_hex(Items items, const
     }
     const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult;
     if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
-    const bool seedable = own && it.tedge[t] != it.gen;
+    const bool seedable = own;   // k_seed_super skips unsafe members
     double bv = seedable ? bound : -INFINITY;
     long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
     for (int off = 32; off > 0; off >>= 1) {
@@ -1046,7 +1076,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, con
         bool kp = false;
         if (lane < nsb2) {
             const double bnd = sbound[(size_t)t * nsb2 + lane];
-            kp = (bnd > pl.thr) && (te || bnd >= L);
+            kp = (bnd > pl.thr) && bnd >= L;
         }
         const unsigned long long bal = __ballot(kp);
         if (kp) s_sb[__popcll(bal & ((1ull << lane) - 1ull))] = lane;
@@ -1198,7 +1228,7 @@ __global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, c
         bool kp = false;
         if (lane < nsb2) {
             const double bnd = it.sbound[(size_t)t * nsb2 + lane];
-            kp = (bnd > pl.thr) && (te || bnd >= L);
+            kp = (bnd > pl.thr) && bnd >= L;
         }
         const unsigned long long bal = __ballot(kp);
         if (kp) s_sb[__popcll(bal & ((1ull << lane) - 1ull))] = lane;
@@ -1610,6 +1640,25 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             }
             s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         }
+        // unsafe members (some coarse read in the strip left of / below the
+        // map while the block's fine reads overlap it) cannot seed: their
+        // fine scores may exceed their coarse score, so L would not be a
+        // lower bound of the reference's result
+        __shared__ int s_unsafe[16];
+        if (tid < 16) s_unsafe[tid] = 0;
+        __syncthreads();
+        if (valid && it.tedge[ct] == it.gen) {
+            const int lr = pl.low_res, lo = -(lr - 1);
+            const int x0 = -pl.win_x + jx * lr, y0 = -pl.win_y + jy * lr;
+            const int2* __restrict__ id = idx + (size_t)ct * Nv;
+            bool uns = false;
+            for (int v = g; v < Nv; v += 64) {
+                const int2 c = id[v];
+                const int x = c.x + x0, y = c.y + y0;
+                uns |= (x >= lo) & (x < pl.W) & (y >= lo) & (y < pl.H) & ((x < 0) | (y < 0));
+            }
+            if (uns) s_unsafe[m] = 1;
+        }
         // member totals: the wave's 4 groups by shuffles, then the 16 waves
         s += __shfl_xor(s, 16, 64);
         s += __shfl_xor(s, 32, 64);
@@ -1622,7 +1671,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             if (tid < 16) {
                 double tot = 0.0;
                 for (int j = 0; j < (int)(blockDim.x >> 6); ++j) tot += red[j * 16 + tid];
-                if (valid) {
+                if (valid && !s_unsafe[tid]) {
                     mv = tot;
                     mk = (long long)ct * pl.P + (long long)jx * pl.ncy + jy;
                 }
@@ -1639,6 +1688,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
         }
         __syncthreads();
         const long long mk = sk[0];
+    if (mk != LLONG_MAX) {   // (uniform) every member unsafe: no seed from this candidate
         // 3. fine scores of block mk, any order, rounding-bounded
         const int rem = (int)(mk % pl.P);
         const int bjx = rem / pl.ncy, bjy = rem % pl.ncy;
@@ -1715,6 +1765,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
         Lmine = sv[0];
         LGS_PROBE_MARK();
     }
+    }
     // 4. publish
     if (tid == 0) {
         Lc[blockIdx.x] = Lmine;
@@ -1744,8 +1795,6 @@ __global__ __launch_bounds__(kSelSeg) void k_select(Items items, int use_sbound)
     const uint8_t* __restrict__ cflag = it.cflag;
     const double* __restrict__ Lp = it.Lp;
     const double* __restrict__ sbound = use_sbound ? it.sbound : nullptr;
-    const int* __restrict__ tedge = it.tedge;
-    const int gen = it.gen;
     int* __restrict__ list = it.list;
     int* __restrict__ segcnt = it.segcnt;
     __shared__ int s_w[kSelSeg / 64];
@@ -1758,7 +1807,7 @@ __global__ __launch_bounds__(kSelSeg) void k_select(Items items, int use_sbound)
             const int t = (int)(k / pl.P), rem = (int)(k % pl.P);
             const int jx = rem / pl.ncy, jy = rem % pl.ncy;
             const double bnd = sbound[(size_t)t * pl.nsbx * pl.nsby + (jy / kSB) * pl.nsbx + jx / kSB];
-            kp = (bnd > pl.thr) && (tedge[t] == gen || bnd >= L);
+            kp = (bnd > pl.thr) && bnd >= L;
         }
         if (kp) {
             const double c = cscore[k];
@@ -2160,35 +2209,35 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(Items items, int guard_ca
     for (int i = threadIdx.x; i < cp.N; i += blockDim.x) {
         int4 c;
         if (mode == 0) {
-            c = make_int4(INT_MIN, 0, 0, 0);
             const double r = ranges[i];
-            if (!(r >= cp.max_range || r <= cp.min_range)) {
+            const bool valid = !(r >= cp.max_range || r <= cp.min_range);
+            double q[4] = { 0.0, 0.0, 0.0, 0.0 };
+            if (valid) {
                 const double cs = cos(pt + angles[i]);
                 const double sn = sin(pt + angles[i]);
-                const double q[4] = {
-                    (px + r * cs - cp.min_x) / cp.res,
-                    (py + r * sn - cp.min_y) / cp.res,
-                    (px + (r - cp.hit_and_missed_dist) * cs - cp.min_x) / cp.res,
-                    (py + (r - cp.hit_and_missed_dist) * sn - cp.min_y) / cp.res,
-                };
-                int cell[4];
-                for (int j = 0; j < 4; ++j) {
-                    cell[j] = (int)floor(q[j]);
-                    if (near_boundary(q[j], guard_eps)) {
-                        cell[j] += inject;
-                        const int slot = tagged_slot(&rec->cost_guard_word, (unsigned)gen);
-                        if (slot < guard_cap) {
-                            CostGuardRec g;
-                            g.pose_which = pi * 4 + j;
-                            g.beam = i;
-                            g.ix = cell[j];
-                            g.iy = 0;
-                            rec->cost_guard[slot] = g;
-                        }
+                q[0] = (px + r * cs - cp.min_x) / cp.res;
+                q[1] = (py + r * sn - cp.min_y) / cp.res;
+                q[2] = (px + (r - cp.hit_and_missed_dist) * cs - cp.min_x) / cp.res;
+                q[3] = (py + (r - cp.hit_and_missed_dist) * sn - cp.min_y) / cp.res;
+            }
+            int cell[4];
+            for (int j = 0; j < 4; ++j) {
+                cell[j] = (int)floor(q[j]);
+                const bool guarded = valid && near_boundary(q[j], guard_eps);
+                const int slot = tagged_slot_wave(&rec->cost_guard_word, (unsigned)gen, guarded);
+                if (guarded) {
+                    cell[j] += inject;
+                    if (slot < guard_cap) {
+                        CostGuardRec g;
+                        g.pose_which = pi * 4 + j;
+                        g.beam = i;
+                        g.ix = cell[j];
+                        g.iy = 0;
+                        rec->cost_guard[slot] = g;
                     }
                 }
-                c = make_int4(cell[0], cell[1], cell[2], cell[3]);
             }
+            c = valid ? make_int4(cell[0], cell[1], cell[2], cell[3]) : make_int4(INT_MIN, 0, 0, 0);
             cidx[(size_t)pi * cp.N + i] = c;
         } else {
             c = cidx[(size_t)pi * cp.N + i];
@@ -2620,7 +2669,27 @@ struct ScanOptions {
     const std::vector<int4>* patches = nullptr;    // projection patches (t, v, ix, iy)
     const std::vector<int2>* host_idx = nullptr;   // full host projection [T*Nv]
     const std::vector<int4>* cost_patches = nullptr;
+    // the search result is already exact: only the cost terms are redone from
+    // the previous run's cells with cost_patches applied
+    bool cost_only = false;
 };
+
+// Host-patched cost cells (cidx[key.x] = cells, computed on the host with
+// glibc) and the cost terms recomputed from them (k_cost mode 1).
+void enqueue_cost_patches(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::vector<MatchItem>& items,
+                          const std::vector<int4>& cost_patches)
+{
+    hipStream_t st = ctx->stream;
+    const int np = (int)(cost_patches.size() / 2);
+    int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * cost_patches.size());
+    LGS_HIP_CHECK(hipMemcpyAsync(dp, cost_patches.data(), sizeof(int4) * cost_patches.size(),
+                                 hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, st, items[0].cidx, dp, np);
+    LGS_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, 1), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
+                       ctx->guard_eps, 0, 1);
+    LGS_HIP_CHECK(hipGetLastError());
+}
 
 // Enqueue the whole device pipeline of a batch of matches on ctx->stream: one
 // launch per stage for all items (d_items: the uploaded descriptors).
@@ -2628,6 +2697,11 @@ struct ScanOptions {
 void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::vector<MatchItem>& items,
                    const ScanOptions& opt)
 {
+    if (opt.cost_only) {
+        if (opt.cost_patches && !opt.cost_patches->empty())
+            enqueue_cost_patches(ctx, B, d_items, items, *opt.cost_patches);
+        return;
+    }
     hipStream_t st = ctx->stream;
     const int n = B.n;
     const int inject = ctx->inject_index ? 1 : 0;
@@ -2773,18 +2847,8 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
     }
-    if (opt.cost_patches && !opt.cost_patches->empty()) {
-        // (key, cells) pairs: cidx[key.x] = cells, computed on the host with glibc
-        const int np = (int)(opt.cost_patches->size() / 2);
-        int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * opt.cost_patches->size());
-        LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.cost_patches->data(), sizeof(int4) * opt.cost_patches->size(),
-                                     hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, st, items[0].cidx, dp, np);
-        LGS_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, 1), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
-                           ctx->guard_eps, 0, 1);
-        LGS_HIP_CHECK(hipGetLastError());
-    }
+    if (opt.cost_patches && !opt.cost_patches->empty())
+        enqueue_cost_patches(ctx, B, d_items, items, *opt.cost_patches);
 }
 
 // Host view of a device record: the generation-tagged guard words decoded.
@@ -3142,6 +3206,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
                             }
                     }
                     opt.cost_patches = &cpatch;
+                    opt.cost_only = true;   // the search result stands: redo the cost terms only
                     rerun = true;
                     fixups = 1;
                 }

@@ -65,3 +65,79 @@ def test_interpolated_scan_matches_like_the_oracle(ctx, world):
         orr, oa = ob.scan_interpolate(r, ang, 0.05, 0.25)
         got = ctx.optimize_pose_query(g, P, cost, isc, init)
         assert_same(got, oracle_match(cells, mx, my, 0.05, (5, 0.3, 0.3, 0.4, 20.0), orr, oa, init), f"k{k}")
+
+
+# ------------------------------------------------------------------ chained frontend
+def _odometry(rng, last):
+    # the true relative motion + noise, composed onto the last estimate (bench.py run_stream)
+    d = (0.1 + rng.normal(0, 0.01), rng.normal(0, 0.01), 0.02 + rng.normal(0, 0.005))
+    c, s = np.cos(last[2]), np.sin(last[2])
+    return (last[0] + c * d[0] - s * d[1], last[1] + s * d[0] + c * d[1], last[2] + d[2])
+
+
+def _chain(ctx, world, steps, window, n_beams, check_maps_every=10):
+    """LidarGraphSlamFrontEnd::ProcessScan's per-scan loop
+    (C/mapping/lidar_graph_slam_frontend.cpp:78-127) on the device, step for step
+    against the same loop through the oracle: ScanInterpolator::Interpolate, the
+    latest map rebuilt from the last 10 scans (ConstructMapFromScans), OptimizePose
+    (query) from the odometry guess, and the local-map insert (UpdateGridMap).
+    Every step's scan, match summary and (every few steps) both maps must agree."""
+    from test_gpu_raycast import same_map
+    ang = scene.beam_angles(n_beams)
+    n = steps + 1
+    truths = [(5.0 * np.cos(0.02 * k), 5.0 * np.sin(0.02 * k), 0.02 * k + np.pi / 2) for k in range(n)]
+    ranges = [scene.ray_cast(world, t, ang) for t in truths]
+    BP = (0.01, 20.0, 0.6, 0.45)
+    bp, obp = abi.BuilderParams(*BP), ob.BuilderParams(*BP)
+    params = (5, *window, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    local = ctx.map(0.05, 100, 200, 200, center=truths[0][:2])
+    latest = ctx.map(0.05, 100, 200, 200, center=truths[0][:2])
+    olocal = ob.OMap(0.05, 100, 200, 200, center=truths[0][:2])
+    olatest = ob.OMap(0.05, 100, 200, 200, center=truths[0][:2])
+    dscans, oscans = [], []
+    for k in range(n):
+        dscans.append(ctx.interpolate(ctx.scan(ranges[k], ang), 0.05, 0.25))
+        orr, oa = ob.scan_interpolate(ranges[k], ang, 0.05, 0.25)
+        assert dscans[-1].ranges.tolist() == orr.tolist(), k
+        oscans.append(ob.OScan(orr, oa))
+    est = [truths[0]]
+    local.update_scan(dscans[0], est[0], bp)
+    olocal.integrate(est[0], oscans[0], obp)
+    rng = np.random.default_rng(7)
+    ctx.reset_stats()
+    for k in range(1, n):
+        guess = _odometry(rng, est[-1])
+        lo = max(0, k - 10)
+        latest.construct(dscans[lo:k], est[lo:k], bp)
+        olatest.construct(est[lo:k], oscans[lo:k], obp)
+        if k % check_maps_every == 1:
+            same_map(latest, olatest, f"latest k{k}")
+        got = ctx.optimize_pose_query(latest.grid(), P, cost, dscans[k], guess)
+        g = olatest.geometry()
+        ora = oracle_match(olatest.cells(), g["min_x"], g["min_y"], 0.05, params,
+                           oscans[k].r, oscans[k].a, guess)
+        assert_same(got, ora, f"step {k}")
+        e = got.estimated_pose
+        est.append((e.x, e.y, e.theta))
+        local.update_scan(dscans[k], est[-1], bp)
+        olocal.integrate(est[-1], oscans[k], obp)
+    same_map(local, olocal, "local map")
+    return est, truths, ctx.match_counters()
+
+
+def test_frontend_chain_json_window(ctx, world):
+    """60 chained frontend steps with the launcher's frontend window (0.2 m / 0.2 m / 0.5 rad)."""
+    est, truths, _ = _chain(ctx, world, 60, (0.2, 0.2, 0.5), 1081)
+    assert abs(est[-1][0] - truths[-1][0]) < 0.2 and abs(est[-1][1] - truths[-1][1]) < 0.2
+
+
+def test_frontend_chain_config2_window(ctx, world):
+    """Chained steps with the config-2 window (+-2 m / +-30 deg) against the
+    10-scan latest map: the scan's hits sit at the map's low edges, so many
+    blocks are 'unsafe' (coarse reads left of / below the map).  The superblock
+    bounds also bound their fine scores (clamped strip): the
+    pruned search must stay exact AND skip most blocks."""
+    _, _, cnt = _chain(ctx, world, 12, (4.0, 4.0, 1.0471976), 541, check_maps_every=4)
+    assert cnt["matches"] == 12 and cnt["pruned"] == 12, cnt
+    assert cnt["coarse_blocks"] < 0.5 * cnt["coarse_blocks_dense"], cnt

@@ -39,11 +39,29 @@ def expected_planes(cells, lr, L):
     return P
 
 
+def clamp_strip(P, lr, M):
+    """The superblock planes' input: the phase planes with the strip left of /
+    below the map (padded column / row M - 1 of the planes rx > 0 / ry > 0)
+    holding the map's first coarse column / row"""
+    Q = P.copy()
+    for ry in range(lr):
+        for rx in range(lr):
+            p = ry * lr + rx
+            if rx > 0:
+                Q[p, :, M - 1] = P[ry * lr, :, M]
+            if ry > 0:
+                Q[p, M - 1, :] = P[rx, M, :]
+            if rx > 0 and ry > 0:
+                Q[p, M - 1, M - 1] = P[0, M, M]
+    return Q
+
+
 def check_super(P, S, lr, L):
-    """S (fp16, sub-phase layout) >= the forward 4x4 max of every plane, by at most one fp16 ulp"""
+    """S (fp16, sub-phase layout) >= the forward 4x4 max of every (strip-clamped)
+    plane, by at most one fp16 ulp"""
     Hqp, Wqp = L["Hqp"], L["Wqp"]
     pad = np.zeros((lr * lr, Hqp + 3, Wqp + 3))
-    pad[:, :Hqp, :Wqp] = P
+    pad[:, :Hqp, :Wqp] = clamp_strip(P, lr, L["M"])
     m = np.max([pad[:, j:j + Hqp, i:i + Wqp] for j in range(4) for i in range(4)], axis=0)
     pstride4 = 16 * L["sub4"]
     for p in range(lr * lr):

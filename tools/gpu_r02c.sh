@@ -1,0 +1,8 @@
+#!/bin/bash
+# r02 pass c: -m gpu suite, smoke, default bench line.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r02c_gpu_tests.log 2>&1 &&
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r02c_smoke.log 2>&1 &&
+timeout -k 10 600 python -u bench.py > gpurun_out/r02c_bench.json 2> gpurun_out/r02c_bench.err
