@@ -215,6 +215,27 @@ __device__ __forceinline__ int super_base(int ix, int iy, const RtcsmPlan& pl)
                    : 0;
 }
 
+// Coarse value C(x, y) of an in-map coarse cell in the padded phase planes.
+__device__ __forceinline__ double coarse_at(const double* __restrict__ cmap, int x, int y, const RtcsmPlan& pl)
+{
+    const int lr = pl.low_res;
+    return cmap[(long long)((y % lr) * lr + x % lr) * pl.pstride + (long long)(y / lr + pl.M) * pl.Wqp +
+                (x / lr + pl.M)];
+}
+
+// One beam of the unsafe test of block (x0, y0) (its coarse read at x, y):
+// true if the read lies in the strip left of / below the map while the
+// block's fine reads of the beam overlap the map.  Then C(max(x, 0),
+// max(y, 0)) bounds those fine reads and is added to ext.
+__device__ __forceinline__ bool strip_read(const double* __restrict__ cmap, int x, int y, const RtcsmPlan& pl,
+                                           double& ext)
+{
+    const int lo = -(pl.low_res - 1);
+    const bool s = (x >= lo) & (x < pl.W) & (y >= lo) & (y < pl.H) & ((x < 0) | (y < 0));
+    if (s) ext += coarse_at(cmap, max(x, 0), max(y, 0), pl);
+    return s;
+}
+
 __device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
 {
     const int lr = pl.low_res;
@@ -1161,27 +1182,31 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, con
         __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15));   // ring drained before its reuse
         // unsafe test (angles that may hold unsafe blocks only): lane (c, q)
         // checks beams q, q + 16, ..., OR-reduced over q
+        // (+ ext: the strip reads' bound of the fine values, see strip_read)
         bool unsafe = false;
+        double ext = 0.0;
         const int uc = lane & 3, uq = lane >> 2;
         const int ujx = jx0 + uc;
         if (te && ujx < pl.ncx && jy < pl.ncy) {
             const int2* __restrict__ id = idx + (size_t)t * Nv;
-            const int lr = pl.low_res, lo = -(lr - 1);
+            const int lr = pl.low_res;
             const int x0 = -pl.win_x + ujx * lr, y0 = -pl.win_y + jy * lr;
             for (int v = uq; v < Nv; v += 16) {
                 const int2 c = id[v];
-                if (c.x - pl.win_x < 0 || c.y - pl.win_y < 0) {
-                    const int x = c.x + x0, y = c.y + y0;
-                    unsafe |= (x >= lo) & (x < pl.W) & (y >= lo) & (y < pl.H) & ((x < 0) | (y < 0));
-                }
+                if (c.x - pl.win_x < 0 || c.y - pl.win_y < 0) unsafe |= strip_read(cmap, c.x + x0, c.y + y0, pl, ext);
             }
         }
 #pragma unroll
-        for (int off = 4; off < 64; off <<= 1) unsafe |= __shfl_xor((int)unsafe, off, 64) != 0;
+        for (int off = 4; off < 64; off <<= 1) {
+            unsafe |= __shfl_xor((int)unsafe, off, 64) != 0;
+            ext += __shfl_xor(ext, off, 64);
+        }
         if (active) {
             const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
             cscore[k] = acc;
-            cflag[k] = unsafe ? 1 : 0;
+            // an unsafe block whose fine scores all stay below L can change
+            // nothing: it is treated as safe (c <= bound < L)
+            cflag[k] = (unsafe && (acc + ext) * pl.sb_mult >= L) ? 1 : 0;
         }
         LGS_PROBE_MARK();
     }
@@ -1257,23 +1282,24 @@ __global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, c
                                         [&](const int& c) { return active ? lane_base + c : zero; });
         // unsafe: some coarse read left of / below the map while the block's
         // fine reads can land inside (x, y >= -(lr-1)); rare, so a separate pass
+        // (+ ext: the strip reads' bound of the fine values, see strip_read)
         bool unsafe = false;
+        double ext = 0.0;
         if (te && active) {
             const int2* __restrict__ id = idx + (size_t)t * pl.Nv;
-            const int lr = pl.low_res, lo = -(lr - 1);
+            const int lr = pl.low_res;
             const int x0 = -pl.win_x + jx * lr, y0 = -pl.win_y + jy * lr;
             for (int v = 0; v < pl.Nv; ++v) {
                 const int2 q = id[v];
-                if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0) {
-                    const int x = q.x + x0, y = q.y + y0;
-                    unsafe |= (x >= lo) & (x < pl.W) & (y >= lo) & (y < pl.H) & ((x < 0) | (y < 0));
-                }
+                if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0) unsafe |= strip_read(cmap, q.x + x0, q.y + y0, pl, ext);
             }
         }
         if (active) {
             const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
             it.cscore[k] = sum;
-            it.cflag[k] = unsafe ? 1 : 0;
+            // an unsafe block whose fine scores all stay below L can change
+            // nothing: it is treated as safe (c <= bound < L)
+            it.cflag[k] = (unsafe && (sum + ext) * pl.sb_mult >= L) ? 1 : 0;
         }
     }
 }
@@ -1623,7 +1649,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
         const int jx = kSB * (csb % pl.nsbx) + (m & 3);
         const int jy = kSB * (csb / pl.nsbx) + (m >> 2);
         const bool valid = jx < pl.ncx && jy < pl.ncy;
-        double s = 0.0;
+        double s = 0.0, sa = 0.0;   // member sum and its sum of magnitudes
         if (valid) {
             const double* __restrict__ lb = cmap + (jy * pl.Wqp + jx);
             const int cnt = (g < Nv) ? (Nv - g + 63) / 64 : 0;   // beams g, g + 64, ...
@@ -1636,59 +1662,58 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
                     buf[j] = (i0 + j < cnt) ? lb[srow[g + 64 * i]] : 0.0;
                 }
 #pragma unroll
-                for (int j = 0; j < 16; ++j) acc[j & 3] += buf[j];
+                for (int j = 0; j < 16; ++j) {
+                    acc[j & 3] += buf[j];
+                    sa += fabs(buf[j]);
+                }
             }
             s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-        }
-        // unsafe members (some coarse read in the strip left of / below the
-        // map while the block's fine reads overlap it) cannot seed: their
-        // fine scores may exceed their coarse score, so L would not be a
-        // lower bound of the reference's result
-        __shared__ int s_unsafe[16];
-        if (tid < 16) s_unsafe[tid] = 0;
-        __syncthreads();
-        if (valid && it.tedge[ct] == it.gen) {
-            const int lr = pl.low_res, lo = -(lr - 1);
-            const int x0 = -pl.win_x + jx * lr, y0 = -pl.win_y + jy * lr;
-            const int2* __restrict__ id = idx + (size_t)ct * Nv;
-            bool uns = false;
-            for (int v = g; v < Nv; v += 64) {
-                const int2 c = id[v];
-                const int x = c.x + x0, y = c.y + y0;
-                uns |= (x >= lo) & (x < pl.W) & (y >= lo) & (y < pl.H) & ((x < 0) | (y < 0));
-            }
-            if (uns) s_unsafe[m] = 1;
         }
         // member totals: the wave's 4 groups by shuffles, then the 16 waves
         s += __shfl_xor(s, 16, 64);
         s += __shfl_xor(s, 32, 64);
-        if ((tid & 63) < 16) red[(tid >> 6) * 16 + m] = s;
+        sa += __shfl_xor(sa, 16, 64);
+        sa += __shfl_xor(sa, 32, 64);
+        if ((tid & 63) < 16) {
+            red[(tid >> 6) * 16 + m] = s;
+            reda[(tid >> 6) * 16 + m] = sa;
+        }
         __syncthreads();
         LGS_PROBE_MARK();
         if (tid < 64) {
-            double mv = -1.0;
+            double mv = -1.0, ma = 0.0;
             long long mk = LLONG_MAX;
             if (tid < 16) {
-                double tot = 0.0;
-                for (int j = 0; j < (int)(blockDim.x >> 6); ++j) tot += red[j * 16 + tid];
-                if (valid && !s_unsafe[tid]) {
+                double tot = 0.0, tota = 0.0;
+                for (int j = 0; j < (int)(blockDim.x >> 6); ++j) {
+                    tot += red[j * 16 + tid];
+                    tota += reda[j * 16 + tid];
+                }
+                if (valid) {
                     mv = tot;
+                    ma = tota;
                     mk = (long long)ct * pl.P + (long long)jx * pl.ncy + jy;
                 }
             }
             for (int off = 32; off > 0; off >>= 1) {
                 const double ov = __shfl_xor(mv, off, 64);
+                const double oa = __shfl_xor(ma, off, 64);
                 const long long ok = __shfl_xor(mk, off, 64);
                 if (better(ov, ok, mv, mk)) {
                     mv = ov;
+                    ma = oa;
                     mk = ok;
                 }
             }
-            if (tid == 0) sk[0] = mk;
+            if (tid == 0) {
+                sk[0] = mk;
+                sv[1] = mv;
+                sv[2] = ma;
+            }
         }
         __syncthreads();
         const long long mk = sk[0];
-    if (mk != LLONG_MAX) {   // (uniform) every member unsafe: no seed from this candidate
+        const double cmk = sv[1], cma = sv[2];   // block mk's coarse score (any order), sum of |terms|
         // 3. fine scores of block mk, any order, rounding-bounded
         const int rem = (int)(mk % pl.P);
         const int bjx = rem / pl.ncy, bjy = rem % pl.ncy;
@@ -1762,9 +1787,12 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             if (tid == 0) sv[0] = lv;
         }
         __syncthreads();
-        Lmine = sv[0];
+        // s_final >= f_mk if the reference refines block mk, else >= c_mk
+        // (it skips the block only when c_mk <= scoreMax), so min(f, c) is a
+        // lower bound of the result for ANY block, unsafe ones included
+        // (their f may exceed c); both terms rounding-bounded from below
+        Lmine = fmin(sv[0], cmk - (4.0 * (double)(Nv + 2) * 0x1p-53) * cma);
         LGS_PROBE_MARK();
-    }
     }
     // 4. publish
     if (tid == 0) {
