@@ -79,6 +79,11 @@ def parse():
     ap.add_argument("--interp", type=int, default=1,
                     help="stream workload: 1 (default, the launcher's UseScanInterpolator) interpolates every "
                          "scan (lgs_scan_interpolate, DistScans 0.05 / DistThresholdEmpty 0.25), 0 raw scans")
+    ap.add_argument("--dropin-line", type=int, default=1,
+                    help="match workload: also time INTEGRATION.md's drop-in query path (Flatten of a patch map + "
+                         "upload + match, C++) and report it as 'dropin'")
+    ap.add_argument("--driver", default="cpp", choices=["cpp", "py"],
+                    help="stream workload: the frontend loop in C++ over the adapter (default) or in Python")
     ap.add_argument("--window", default="json", choices=sorted(STREAM_WINDOWS),
                     help="stream workload: search window (json = the launcher's frontend 0.2 m/0.2 m/0.5 rad, "
                          "config2 = +-2 m/+-30 deg)")
@@ -92,7 +97,8 @@ def parse():
                     help="HIP-event timing inside the timed region: the roofline kernel only (default), "
                          "every kernel, or none (A/B of the event overhead)")
     a = ap.parse_args()
-    d_steps = dict(match=200, refine=200, loop=4, loop_bb=2, stream=500, rebuild=20)[a.workload]
+    d_steps = dict(match=200, refine=200, loop=4, loop_bb=2, stream=10000 if a.driver == "cpp" else 500,
+                   rebuild=20)[a.workload]
     d_warm = dict(match=10, refine=5, loop=1, loop_bb=1, stream=10, rebuild=2)[a.workload]
     a.steps = d_steps if a.steps is None else a.steps
     a.warmup = d_warm if a.warmup is None else a.warmup
@@ -242,6 +248,75 @@ def oracle_lib():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind as ob
     return ob
+
+
+class FbIn(C.Structure):
+    _fields_ = [("device", C.c_int), ("n_scans", C.c_int), ("warmup", C.c_int), ("n_beams", C.c_int),
+                ("n_segs", C.c_int), ("interp", C.c_int), ("latest_scans", C.c_int), ("low_res", C.c_int),
+                ("range_x", C.c_double), ("range_y", C.c_double), ("range_theta", C.c_double),
+                ("scan_range_max", C.c_double), ("segs", C.POINTER(C.c_double)), ("angles", C.POINTER(C.c_double)),
+                ("truths", C.POINTER(C.c_double)), ("odo", C.POINTER(C.c_double)), ("n_dump", C.c_int)]
+
+
+class FbOut(C.Structure):
+    _fields_ = [("est", C.POINTER(C.c_double)), ("guess", C.POINTER(C.c_double)),
+                ("dump_ranges", C.POINTER(C.c_double)), ("total_s", C.c_double), ("phase_s", C.c_double * 5),
+                ("steps_timed", C.c_int), ("not_found", C.c_int)]
+
+
+class DropinIn(C.Structure):
+    _fields_ = [("device", C.c_int), ("w", C.c_int), ("h", C.c_int), ("patch_size", C.c_int),
+                ("min_x", C.c_double), ("min_y", C.c_double), ("res", C.c_double),
+                ("cells", C.POINTER(C.c_double)), ("n_beams", C.c_int), ("n_queries", C.c_int),
+                ("ranges", C.POINTER(C.c_double)), ("angles", C.POINTER(C.c_double)),
+                ("inits", C.POINTER(C.c_double)), ("low_res", C.c_int), ("range_x", C.c_double),
+                ("range_y", C.c_double), ("range_theta", C.c_double), ("scan_range_max", C.c_double)]
+
+
+class DropinOut(C.Structure):
+    _fields_ = [("flatten_s", C.c_double), ("upload_s", C.c_double), ("match_uploaded_s", C.c_double),
+                ("match_resident_s", C.c_double), ("same", C.c_int)]
+
+
+def bench_drivers():
+    """liblgs_frontend_bench.so: C++ loops over the adapter (host/frontend_bench.cpp)."""
+    lib = C.CDLL(os.path.join(ROOT, "my-lidar-graph-slam_amd", "lgs_amd", "liblgs_frontend_bench.so"))
+    lib.lgs_frontend_bench.argtypes = [C.POINTER(FbIn), C.POINTER(FbOut)]
+    lib.lgs_dropin_bench.argtypes = [C.POINTER(DropinIn), C.POINTER(DropinOut)]
+    return lib
+
+
+def dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def dropin_line(args, D, n_queries=32):
+    """INTEGRATION.md §2's drop-in query path for the unchanged reference
+    frontend: Flatten of a patch-based GridMapType (1000x1000, PatchSize 100,
+    virtual Value() per cell) + upload per query, beside the match on the
+    resident map (C++ driver, lgs_dropin_bench)."""
+    world = scene.make_world()
+    ang = scene.beam_angles(1081)
+    cells, mx, my = bench_map(world, ang)
+    rng = np.random.default_rng(5 + D.rank)
+    scans, inits, _ = random_scans(world, ang, rng, n_queries)
+    r = np.ascontiguousarray(np.stack(scans), dtype=np.float64)
+    ini = np.ascontiguousarray(np.array(inits, dtype=np.float64))
+    c = np.ascontiguousarray(cells, dtype=np.float64)
+    a = np.ascontiguousarray(ang)
+    h, w = c.shape
+    din = DropinIn(D.local, w, h, 100, mx, my, 0.05, dptr(c), len(ang), n_queries, dptr(r), dptr(a), dptr(ini),
+                   *PARAMS)
+    dout = DropinOut()
+    rc = bench_drivers().lgs_dropin_bench(C.byref(din), C.byref(dout))
+    if rc != 0:
+        raise RuntimeError(f"lgs_dropin_bench failed with status {rc}")
+    ms = lambda v: round(1e3 * v / n_queries, 4)   # noqa: E731
+    return dict(queries=n_queries, flatten_ms=ms(dout.flatten_s), upload_ms=ms(dout.upload_s),
+                match_uploaded_ms=ms(dout.match_uploaded_s), match_resident_ms=ms(dout.match_resident_s),
+                per_query_ms=ms(dout.flatten_s + dout.upload_s + dout.match_uploaded_s), same_poses=bool(dout.same),
+                note="unchanged reference frontend: Flatten(GridMapType) + 8 MB upload per OptimizePose; "
+                     "GridMapHip keeps the latest map resident instead (INTEGRATION.md §4)")
 
 
 def timed(budget_s, items, fn):
@@ -716,6 +791,94 @@ def run_stream(args, D, ctx):
     return line, stats, value
 
 
+def run_stream_cpp(args, D, ctx):
+    """Config 4 driven from C++ (host/frontend_bench.cpp lgs_frontend_bench):
+    the same frontend as run_stream -- scan upload, ScanInterpolator, latest map
+    from the last 10 scans, OptimizePose(query) from the odometry guess,
+    local-map insert -- through the reference-shaped adapter classes with no
+    Python between calls.  Trajectory: 0.1 m / 0.02 rad per scan on a 5 m
+    circle, odometry noise sigma (0.01 m, 0.005 rad), seed 7 + rank.  The CPU
+    baseline replays the first steps through the oracle with the driver's own
+    guesses and raw ranges; its poses must equal the driver's bit for bit."""
+    world = scene.make_world()
+    ang = np.ascontiguousarray(scene.beam_angles(1081))
+    n = args.warmup + args.steps + 1
+    k = np.arange(n, dtype=np.float64)
+    truths = np.ascontiguousarray(np.stack([5.0 * np.cos(0.02 * k), 5.0 * np.sin(0.02 * k), 0.02 * k + np.pi / 2], 1))
+    rng = np.random.default_rng(7 + D.rank)
+    odo = np.zeros((n, 3))
+    for i in range(1, n):
+        odo[i] = (0.1 + rng.normal(0, 0.01), rng.normal(0, 0.01), 0.02 + rng.normal(0, 0.005))
+    win = STREAM_WINDOWS[args.window]
+    segs = np.ascontiguousarray(world, dtype=np.float64)
+    n_dump = min(n, 400)
+    est, guess = np.zeros((n, 3)), np.zeros((n, 3))
+    dump = np.zeros((n_dump, len(ang)))
+    fin = FbIn(D.local, n, args.warmup, len(ang), len(segs), int(args.interp), 10, 5, *win, 20.0, dptr(segs), dptr(ang),
+               dptr(truths), dptr(odo), n_dump)
+    fout = FbOut(dptr(est), dptr(guess), dptr(dump))
+    D.barrier()
+    rc = bench_drivers().lgs_frontend_bench(C.byref(fin), C.byref(fout))
+    if rc != 0:
+        raise RuntimeError(f"lgs_frontend_bench failed with status {rc}")
+    steps = fout.steps_timed
+    elapsed = D.max(fout.total_s)
+    value = steps * D.world / elapsed
+    names = ("scan_upload", "interpolate", "latest_map", "match", "insert")
+    breakdown = {f"{nm}_ms": round(1e3 * fout.phase_s[i] / steps, 4) for i, nm in enumerate(names)}
+    drift = float(np.max(np.abs(est[-1, :2] - truths[-1, :2])))
+    cpu = None
+    if D.rank == 0 and not args.no_cpu and D.world == 1:
+        ob = oracle_lib()
+        obp = ob.BuilderParams(*BUILDER)
+        oprm, ocost = ob.RtcsmParams(5, *win, 20.0), ob.CostGE(*COST)
+        olocal = ob.OMap(0.05, 100, 200, 200, center=tuple(truths[0][:2]))
+        olatest = ob.OMap(0.05, 100, 200, 200, center=tuple(truths[0][:2]))
+
+        def oscan(j):
+            r, a = ob.scan_interpolate(dump[j], ang, 0.05, 0.25) if args.interp else (dump[j], ang)
+            return ob.OScan(r, a)
+
+        oscans = [oscan(0)]
+        oest = [tuple(truths[0])]
+        olocal.integrate(oest[0], oscans[0], obp)
+        times = []
+        t_start = time.perf_counter()
+        for j in range(1, n_dump):
+            t1 = time.perf_counter()
+            oscans.append(oscan(j))
+            lo = max(0, j - 10)
+            olatest.construct(oest[lo:j], oscans[lo:j], obp)
+            g = olatest.geometry()
+            og = ob.OGrid(olatest.cells(), g["min_x"], g["min_y"], 0.05)
+            out = ob.Summary()
+            ob.lib().orc_rtcsm_optimize_pose_query(C.byref(og.g), C.byref(oprm), C.byref(ocost),
+                                                   C.byref(oscans[j].s), ob.Pose(*guess[j]), C.byref(out))
+            e = out.estimated_pose
+            oest.append((e.x, e.y, e.theta))
+            olocal.integrate(oest[-1], oscans[j], obp)
+            times.append(time.perf_counter() - t1)
+            if time.perf_counter() - t_start > args.cpu_seconds and len(times) >= 3:
+                break
+        same = all(tuple(est[j]) == oest[j] for j in range(len(oest)))
+        cpu = dict(value=round(len(times) / sum(times), 3), unit="scans/s", cores=1, kind="port",
+                   sample=f"the first {len(times)} frontend steps through the oracle (interpolate, 10-scan "
+                          f"ConstructMapFromScans, OptimizePose(query) from the C++ run's guesses, insert; "
+                          f"1 thread); poses identical to the GPU run's for all of them: {same}")
+    line = dict(
+        metric="frontend scans/sec: match vs latest map + local-map insert + latest-map rebuild, 1081 beams",
+        value=round(value, 2), unit="scans/s", n_gpus=D.world, steps=steps, warmup=args.warmup,
+        ms_per_step=round(1e3 * elapsed / steps, 4), higher_is_better=True, scaling="weak", vs_baseline=None,
+        dtype="f64", data="synthetic circular trajectory, odometry noise (0.01 m, 0.005 rad)",
+        config=dict(workload=f"config4: streaming frontend, {n - 1}-scan trajectory ({args.window} window "
+                             f"{'/'.join(str(v) for v in win)})", beams=1081,
+                    scan_interpolator=bool(args.interp), latest_map_scans=10, driver="C++ adapter loop",
+                    parallelism=f"replicas x{D.world}"),
+        final_drift_m=round(drift, 4), not_found=fout.not_found, breakdown_per_step=breakdown,
+        roofline=None, cpu_baseline=cpu)
+    return line, {}, value
+
+
 # ------------------------------------------------------------------- rebuild
 def run_rebuild(args, D, ctx):
     """SURVEY f2: GridMapBuilder::AfterLoopClosure -- every local map rebuilt
@@ -801,7 +964,8 @@ def main():
     D = Dist(args.gpus)
     ctx = abi.Context(D.local)
     line, stats, _ = dict(match=run_match, refine=run_refine, loop=run_loop, loop_bb=run_loop,
-                          stream=run_stream, rebuild=run_rebuild)[args.workload](
+                          stream=run_stream_cpp if args.driver == "cpp" else run_stream,
+                          rebuild=run_rebuild)[args.workload](
         args, D, ctx)
     line["kernels"] = {k: dict(launches=v["launches"], avg_ms=round(v["total_ms"] / max(1, v["launches"]), 5))
                        for k, v in stats.items()}
@@ -813,6 +977,8 @@ def main():
         ll, _, _ = run_loop(la, D, ctx)
         line["config5_strong_scaling"] = {k: ll[k] for k in ("metric", "value", "unit", "n_gpus", "steps",
                                                               "ms_per_step", "scaling", "config", "roofline")}
+    if args.workload == "match" and args.dropin_line:
+        line["dropin"] = dropin_line(args, D)
     if D.rank == 0:
         print(json.dumps(line), flush=True)
     D.close()

@@ -225,7 +225,9 @@ int  lgs_scan_get(const lgs_scan* scan, int* n, double* ranges, double* angles);
  * (launcher JSON "ScanInterpolator": DistScans 0.05, DistThresholdEmpty 0.25).
  * The relative sensor pose and min/max range are copied.  The recurrence is
  * sequential and uses glibc sincos/atan2/sqrt, so it runs on the host; the
- * result is uploaded once, like lgs_scan_create. */
+ * result is uploaded once, like lgs_scan_create.  LGS_ERR_INVALID_ARG unless
+ * 0 < dist_scans <= dist_threshold_empty (both finite) and every point of
+ * `in` is finite: the reference's loop would never end otherwise. */
 int  lgs_scan_interpolate(lgs_ctx* ctx, const lgs_scan* in, double dist_scans, double dist_threshold_empty,
                           lgs_scan** out);
 

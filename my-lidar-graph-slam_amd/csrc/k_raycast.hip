@@ -405,22 +405,24 @@ inline void world_to_cell(const lgs_map* m, double x, double y, int& ix, int& iy
 
 inline int cell_to_patch(int idx, int ps) { return (idx < 0) ? (idx / ps - 1) : (idx / ps); }  // :905-915
 
+// Cells, hit and miss counters of a map live in ONE allocation (cells at 0,
+// hits at 8 n, misses at 12 n bytes), zeroed with one memset; d_cells owns it.
 void map_alloc(lgs_map* m, int w, int h, double** cells, uint32_t** hit, uint32_t** miss)
 {
     const size_t n = std::max<size_t>(1, (size_t)w * (size_t)h);
-    *cells = nullptr;
-    *hit = *miss = nullptr;
-    if (hipMalloc(cells, n * sizeof(double)) != hipSuccess ||
-        hipMalloc(hit, n * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(miss, n * sizeof(uint32_t)) != hipSuccess) {
-        hipFree(*cells);
-        hipFree(*hit);
-        throw Error(LGS_ERR_OOM, "hipMalloc failed for map");
-    }
-    hipStream_t st = m->ctx->stream;
-    LGS_HIP_CHECK(hipMemsetAsync(*cells, 0, n * sizeof(double), st));
-    LGS_HIP_CHECK(hipMemsetAsync(*hit, 0, n * sizeof(uint32_t), st));
-    LGS_HIP_CHECK(hipMemsetAsync(*miss, 0, n * sizeof(uint32_t), st));
+    void* p = nullptr;
+    if (hipMalloc(&p, n * 16) != hipSuccess) throw Error(LGS_ERR_OOM, "hipMalloc failed for map");
+    *cells = (double*)p;
+    *hit = (uint32_t*)((char*)p + 8 * n);
+    *miss = (uint32_t*)((char*)p + 12 * n);
+    LGS_HIP_CHECK(hipMemsetAsync(p, 0, n * 16, m->ctx->stream));
+}
+
+void map_free(lgs_map* m)
+{
+    hipFree(m->d_cells);
+    m->d_cells = nullptr;
+    m->d_hit = m->d_miss = nullptr;
 }
 
 void map_sync_view(lgs_map* m)
@@ -495,9 +497,7 @@ void map_resize(lgs_map* m, double minX, double minY, double maxX, double maxY)
                                        cw * sizeof(uint32_t), ch, hipMemcpyDeviceToDevice, st));
     }
     LGS_HIP_CHECK(hipStreamSynchronize(m->ctx->stream));
-    hipFree(m->d_cells);
-    hipFree(m->d_hit);
-    hipFree(m->d_miss);
+    map_free(m);
     m->d_cells = cells;
     m->d_hit = hit;
     m->d_miss = miss;
@@ -518,17 +518,17 @@ void map_resize_reset(lgs_map* m, double minX, double minY, double maxX, double 
         uint32_t *hit, *miss;
         map_alloc(m, g.w, g.h, &cells, &hit, &miss);  // zeroed
         LGS_HIP_CHECK(hipStreamSynchronize(st));
-        hipFree(m->d_cells);
-        hipFree(m->d_hit);
-        hipFree(m->d_miss);
+        map_free(m);
         m->d_cells = cells;
         m->d_hit = hit;
         m->d_miss = miss;
         m->cap = need;
     } else {
-        LGS_HIP_CHECK(hipMemsetAsync(m->d_cells, 0, need * sizeof(double), st));
-        LGS_HIP_CHECK(hipMemsetAsync(m->d_hit, 0, need * sizeof(uint32_t), st));
-        LGS_HIP_CHECK(hipMemsetAsync(m->d_miss, 0, need * sizeof(uint32_t), st));
+        // the counters move to the offsets of the new cell count (one memset
+        // zeroes cells, hits and misses)
+        m->d_hit = (uint32_t*)((char*)m->d_cells + 8 * need);
+        m->d_miss = (uint32_t*)((char*)m->d_cells + 12 * need);
+        LGS_HIP_CHECK(hipMemsetAsync(m->d_cells, 0, need * 16, st));
     }
     map_set_geom(m, g);
 }
@@ -590,10 +590,27 @@ ScanHits scan_hits(const lgs_scan* s, lgs_pose2d robot, const lgs_builder_params
     return h;
 }
 
+// scan_hits through the scan's one-entry cache (lgs_scan::hits_cache), keyed
+// bitwise on the robot pose and the usable range.  Callers that may run in
+// parallel over the same scan pass store = false and store afterwards.
+typedef std::shared_ptr<const ScanHits> HitsPtr;
+HitsPtr cached_hits(const lgs_scan* s, lgs_pose2d robot, const lgs_builder_params* bp, bool store)
+{
+    const double key[5] = { robot.x, robot.y, robot.theta, bp->usable_range_min, bp->usable_range_max };
+    if (s->hits_cache && std::memcmp(key, s->hits_key, sizeof(key)) == 0)
+        return std::static_pointer_cast<const ScanHits>(s->hits_cache);
+    HitsPtr h = std::make_shared<const ScanHits>(scan_hits(s, robot, bp));
+    if (store) {
+        s->hits_cache = h;
+        std::memcpy(s->hits_key, key, sizeof(key));
+    }
+    return h;
+}
+
 // One map of a ray-cast pass and its scans (hit points in world coordinates).
 struct MapJob {
     lgs_map* m;
-    std::vector<ScanHits> hs;
+    std::vector<HitsPtr> hs;
 };
 
 // Hit points of every job's scans (one parallel region over all of them) and
@@ -611,11 +628,17 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
     }
     host_parallel_for((int)work.size(), 2, [&](int w) {
         const int j = work[w].first, k = work[w].second;
-        jobs[j].hs[k] = scan_hits(scans[first[j] + k], poses[first[j] + k], bp);
+        jobs[j].hs[k] = cached_hits(scans[first[j] + k], poses[first[j] + k], bp, false);
     });
     boxes.assign(jobs.size(), std::array<double, 4>{DBL_MAX, DBL_MAX, DBL_MIN, DBL_MIN});
     for (size_t j = 0; j < jobs.size(); ++j)
-        for (const ScanHits& h : jobs[j].hs) {
+        for (int k = 0; k < count[j]; ++k) {
+            const ScanHits& h = *jobs[j].hs[k];
+            const lgs_scan* s = scans[first[j] + k];
+            const lgs_pose2d p = poses[first[j] + k];
+            const double key[5] = { p.x, p.y, p.theta, bp->usable_range_min, bp->usable_range_max };
+            s->hits_cache = jobs[j].hs[k];   // (serial: a scan may appear twice)
+            std::memcpy(s->hits_key, key, sizeof(key));
             auto& b = boxes[j];
             b[0] = smin(b[0], h.box[0]);
             b[1] = smin(b[1], h.box[1]);
@@ -650,8 +673,8 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
     };
     std::vector<Unit> units;
     for (int j = 0; j < (int)jobs.size(); ++j)
-        for (const ScanHits& h : jobs[j].hs)
-            if (h.xy.size() >= 2) units.push_back(Unit{j, &h, {}, {}, 0});
+        for (const HitsPtr& h : jobs[j].hs)
+            if (h->xy.size() >= 2) units.push_back(Unit{j, h.get(), {}, {}, 0});
     if (units.empty()) return;
     for (const MapJob& J : jobs)
         LGS_REQUIRE((size_t)J.m->w * J.m->h < (1ull << 31), "map too large for 31-bit cell keys");
@@ -826,7 +849,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
         u = eu, r = er;
         ++pass;
     }
-    ctx->sync();
+    // (stream order: the copy into the staging buffer follows the uploads from it)
     LGS_HIP_CHECK(hipMemcpyAsync(pin, d_bad, 16, hipMemcpyDeviceToHost, st));
     ctx->sync();
     int bad = 0;
@@ -838,7 +861,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
     if (bad) throw Error(LGS_ERR_INTERNAL, "ray cell outside the map geometry");
 }
 
-void raycast(lgs_map* m, std::vector<ScanHits>&& scans, const lgs_builder_params* bp)
+void raycast(lgs_map* m, std::vector<HitsPtr>&& scans, const lgs_builder_params* bp)
 {
     std::vector<MapJob> jobs(1);
     jobs[0].m = m;
@@ -888,9 +911,7 @@ extern "C" void lgs_map_destroy(lgs_map* m)
 {
     if (!m) return;
     hipSetDevice(m->device);
-    hipFree(m->d_cells);
-    hipFree(m->d_hit);
-    hipFree(m->d_miss);
+    map_free(m);
     delete m;
 }
 
@@ -922,9 +943,9 @@ extern "C" int lgs_map_update_scan(lgs_ctx* ctx, lgs_map* m, const lgs_scan* sca
     return guarded(ctx, [&] {
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         m->ctx = ctx;
-        std::vector<ScanHits> hs(1, scan_hits(scan, robot, bp));
+        std::vector<HitsPtr> hs(1, cached_hits(scan, robot, bp, true));
         // bounding box starts at the sensor position (:346-352)
-        const double* bx = hs[0].box;
+        const double* bx = hs[0]->box;
         map_expand(m, bx[0], bx[1], bx[2], bx[3], 5.0);  // :157-158 (default enlargeStep)
         raycast(m, std::move(hs), bp);
     });

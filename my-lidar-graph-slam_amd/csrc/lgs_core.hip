@@ -818,6 +818,13 @@ extern "C" int lgs_scan_interpolate(lgs_ctx* ctx, const lgs_scan* in, double dis
     std::vector<double> rr, aa;
     int rc = guarded(ctx, [&] {
         LGS_REQUIRE(in->n >= 1, "scan must have >= 1 beam");
+        // the walk below advances only if every distance is a number and a
+        // point is inserted at most dist_scans along a segment: reject what
+        // would make the reference's loop run forever (NaN/inf points,
+        // dist_scans <= 0)
+        LGS_REQUIRE(std::isfinite(dist_scans) && std::isfinite(dist_threshold_empty) && dist_scans > 0.0 &&
+                        dist_scans <= dist_threshold_empty,
+                    "need 0 < dist_scans <= dist_threshold_empty, both finite");
         const int n = in->n;
         std::vector<double> px(n), py(n);
         for (int i = 0; i < n; ++i) {
@@ -825,6 +832,7 @@ extern "C" int lgs_scan_interpolate(lgs_ctx* ctx, const lgs_scan* in, double dis
             ref_sincos(in->h_angles[i], sn, cs);
             px[i] = in->h_ranges[i] * cs;
             py[i] = in->h_ranges[i] * sn;
+            LGS_REQUIRE(std::isfinite(px[i]) && std::isfinite(py[i]), "non-finite range or angle");
         }
         rr.reserve(2 * (size_t)n);
         aa.reserve(2 * (size_t)n);

@@ -15,6 +15,7 @@
 #include <functional>
 #include <stdexcept>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "lgs_hip.h"
@@ -292,6 +293,11 @@ struct lgs_scan {
     double cached_rmax = NAN;
     int nv = 0;
     std::vector<int> h_vidx;      // host copy (guard re-projection); the device compacts itself
+    // hit points of the last (robot pose, usable range) they were computed for
+    // (k_raycast.hip scan_hits): the frontend inserts a scan at its estimated
+    // pose and then rebuilds the latest map from it at that same pose 10 times
+    mutable std::shared_ptr<const void> hits_cache;
+    mutable double hits_key[5] = { NAN, NAN, NAN, NAN, NAN };
 };
 
 extern "C" void sincos(double x, double* s, double* c);  // glibc

@@ -49,6 +49,23 @@ def test_interpolate_parameters_and_edges(ctx, ds, de):
     _check(ctx, np.array([1.0, 1.0]), np.array([0.0, 1e-9]), ds, de)
 
 
+def test_interpolate_rejects_endless_inputs(ctx):
+    """Arguments that would make the reference's walk loop forever are
+    LGS_ERR_INVALID_ARG: dist_scans <= 0 or > dist_threshold_empty, non-finite
+    distances, NaN/inf points."""
+    a = np.linspace(-1.0, 1.0, 20)
+    sc = ctx.scan(np.full(20, 2.0), a)
+    for ds, de in [(0.0, 0.25), (-0.05, 0.25), (0.3, 0.25), (np.nan, 0.25), (0.05, np.inf)]:
+        with pytest.raises(abi.LgsError):
+            ctx.interpolate(sc, ds, de)
+    for bad in (np.nan, np.inf):
+        r = np.full(20, 2.0)
+        r[7] = bad
+        with pytest.raises(abi.LgsError):
+            ctx.interpolate(ctx.scan(r, a), 0.05, 0.25)
+    assert len(ctx.interpolate(sc, 0.05, 0.25).ranges) > 20
+
+
 def test_interpolated_scan_matches_like_the_oracle(ctx, world):
     """Interpolate, then OptimizePose(query) on the device scan == the oracle on
     the oracle's interpolated ranges/angles (the frontend's order)."""
