@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--dropin-line", type=int, default=1,
                     help="match workload: also time INTEGRATION.md's drop-in query path (Flatten of a patch map + "
                          "upload + match, C++) and report it as 'dropin'")
+    ap.add_argument("--fused", type=int, default=1,
+                    help="stream workload (C++ driver): GridMapBuilder::AppendScan as one fused call (1) or as "
+                         "the insert + the latest-map rebuild (0)")
     ap.add_argument("--driver", default="cpp", choices=["cpp", "py"],
                     help="stream workload: the frontend loop in C++ over the adapter (default) or in Python")
     ap.add_argument("--window", default="json", choices=sorted(STREAM_WINDOWS),
@@ -252,7 +255,8 @@ def oracle_lib():
 
 class FbIn(C.Structure):
     _fields_ = [("device", C.c_int), ("n_scans", C.c_int), ("warmup", C.c_int), ("n_beams", C.c_int),
-                ("n_segs", C.c_int), ("interp", C.c_int), ("latest_scans", C.c_int), ("low_res", C.c_int),
+                ("n_segs", C.c_int), ("interp", C.c_int), ("latest_scans", C.c_int), ("fused", C.c_int),
+                ("low_res", C.c_int),
                 ("range_x", C.c_double), ("range_y", C.c_double), ("range_theta", C.c_double),
                 ("scan_range_max", C.c_double), ("segs", C.POINTER(C.c_double)), ("angles", C.POINTER(C.c_double)),
                 ("truths", C.POINTER(C.c_double)), ("odo", C.POINTER(C.c_double)), ("n_dump", C.c_int)]
@@ -260,7 +264,7 @@ class FbIn(C.Structure):
 
 class FbOut(C.Structure):
     _fields_ = [("est", C.POINTER(C.c_double)), ("guess", C.POINTER(C.c_double)),
-                ("dump_ranges", C.POINTER(C.c_double)), ("total_s", C.c_double), ("phase_s", C.c_double * 5),
+                ("dump_ranges", C.POINTER(C.c_double)), ("total_s", C.c_double), ("phase_s", C.c_double * 4),
                 ("steps_timed", C.c_int), ("not_found", C.c_int)]
 
 
@@ -814,7 +818,8 @@ def run_stream_cpp(args, D, ctx):
     n_dump = min(n, 400)
     est, guess = np.zeros((n, 3)), np.zeros((n, 3))
     dump = np.zeros((n_dump, len(ang)))
-    fin = FbIn(D.local, n, args.warmup, len(ang), len(segs), int(args.interp), 10, 5, *win, 20.0, dptr(segs), dptr(ang),
+    fin = FbIn(D.local, n, args.warmup, len(ang), len(segs), int(args.interp), 10, int(args.fused), 5, *win, 20.0,
+               dptr(segs), dptr(ang),
                dptr(truths), dptr(odo), n_dump)
     fout = FbOut(dptr(est), dptr(guess), dptr(dump))
     D.barrier()
@@ -824,7 +829,7 @@ def run_stream_cpp(args, D, ctx):
     steps = fout.steps_timed
     elapsed = D.max(fout.total_s)
     value = steps * D.world / elapsed
-    names = ("scan_upload", "interpolate", "latest_map", "match", "insert")
+    names = ("scan_upload", "interpolate", "match", "append_scan")
     breakdown = {f"{nm}_ms": round(1e3 * fout.phase_s[i] / steps, 4) for i, nm in enumerate(names)}
     drift = float(np.max(np.abs(est[-1, :2] - truths[-1, :2])))
     cpu = None
@@ -873,6 +878,7 @@ def run_stream_cpp(args, D, ctx):
         config=dict(workload=f"config4: streaming frontend, {n - 1}-scan trajectory ({args.window} window "
                              f"{'/'.join(str(v) for v in win)})", beams=1081,
                     scan_interpolator=bool(args.interp), latest_map_scans=10, driver="C++ adapter loop",
+                    append_scan="fused (lgs_map_append_scan)" if args.fused else "UpdateScan + ConstructMapFromScans",
                     parallelism=f"replicas x{D.world}"),
         final_drift_m=round(drift, 4), not_found=fout.not_found, breakdown_per_step=breakdown,
         roofline=None, cpu_baseline=cpu)

@@ -315,6 +315,14 @@ int  lgs_map_update_scan(lgs_ctx* ctx, lgs_map* map, const lgs_scan* scan, lgs_p
 int  lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* map, const lgs_scan* const* scans,
                                   const lgs_pose2d* robot_poses, int n,
                                   const lgs_builder_params* params);
+/* GridMapBuilder::AppendScan (C/mapping/grid_map_builder.cpp:48-59): the
+ * newest scan scans[n-1] at robot_poses[n-1] inserted into `local` exactly as
+ * lgs_map_update_scan does (UpdateGridMap :98-193), and `latest` rebuilt from
+ * all n scans exactly as lgs_map_construct_from_scans does (UpdateLatestMap
+ * :196-207; n = min(node count, NumOfScansForLatestMap)).  Same results as the
+ * two calls; both ray-casts share one device pass.  local != latest. */
+int  lgs_map_append_scan(lgs_ctx* ctx, lgs_map* local, lgs_map* latest, const lgs_scan* const* scans,
+                         const lgs_pose2d* robot_poses, int n, const lgs_builder_params* params);
 /* GridMapBuilder::AfterLoopClosure's map loop (C/mapping/grid_map_builder.cpp:62-80):
  * ConstructMapFromScans(maps[i], poseGraph, idx_min[i], idx_max[i]) for every
  * i, where node k of the pose graph is (scans[k], robot_poses[k]) and

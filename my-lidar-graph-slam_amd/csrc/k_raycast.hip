@@ -968,6 +968,32 @@ extern "C" int lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* m, const lgs_
     });
 }
 
+extern "C" int lgs_map_append_scan(lgs_ctx* ctx, lgs_map* local, lgs_map* latest, const lgs_scan* const* scans,
+                                   const lgs_pose2d* poses, int n, const lgs_builder_params* bp)
+{
+    if (!ctx || !local || !latest || local == latest || !scans || !poses || !bp || n < 1)
+        return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        // GridMapBuilder::AppendScan (:48-59) = UpdateGridMap's insert of the
+        // newest scan into the local map (:149-186) + UpdateLatestMap's
+        // ConstructMapFromScans over the last n scans (:196-207).  The two maps
+        // are independent, so both ray-casts share one device pass.
+        local->ctx = latest->ctx = ctx;
+        std::vector<MapJob> jobs(2);
+        jobs[0].m = local;
+        jobs[1].m = latest;
+        std::vector<std::array<double, 4>> box;
+        hits_and_boxes(jobs, { n - 1, 0 }, { 1, n }, scans, poses, bp, box);
+        // the insert's box is the scan's own (sensor included, :346-352), not
+        // ConstructMapFromScans' running box with its DBL_MIN start
+        const double* bx = jobs[0].hs[0]->box;
+        map_expand(local, bx[0], bx[1], bx[2], bx[3], 5.0);                     // :157-158
+        map_resize_reset(latest, box[1][0], box[1][1], box[1][2], box[1][3]);   // :288-290
+        raycast_maps(ctx, jobs, bp);
+    });
+}
+
 extern "C" int lgs_maps_construct_from_scans(lgs_ctx* ctx, lgs_map* const* maps, const int* idx_min,
                                              const int* idx_max, int n_maps, const lgs_scan* const* scans,
                                              const lgs_pose2d* poses, int n_nodes,

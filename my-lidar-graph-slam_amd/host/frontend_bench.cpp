@@ -6,9 +6,9 @@
 // trajectory, every step through the reference-shaped classes:
 //   sensor scan arrives (host ranges)     -> ScanData (upload)
 //   ScanInterpolator::Interpolate          -> ScanInterpolatorHip
-//   UpdateLatestMap (last N scans)         -> GridMapHip::ConstructMapFromScans
 //   OptimizePose(query) from the odometry  -> ScanMatcherRealTimeCorrelativeHip
-//   UpdateGridMap's insert                 -> GridMapHip::UpdateScan
+//   GridMapBuilder::AppendScan             -> GridMapHip::AppendScan (fused) or
+//     (UpdateGridMap insert + UpdateLatestMap)  UpdateScan + ConstructMapFromScans
 // The synthetic sensor (exact segment ray cast) is outside every timer.
 //
 // lgs_dropin_bench: the cost of the unchanged reference frontend's query path
@@ -39,6 +39,7 @@ struct lgs_fb_in {
     int n_segs;
     int interp;           // 1: ScanInterpolator on (launcher default)
     int latest_scans;     // scans of the latest map (launcher JSON: 10)
+    int fused;            // 1: GridMapBuilder::AppendScan as one call (lgs_map_append_scan)
     int low_res;
     double range_x, range_y, range_theta, scan_range_max;
     const double* segs;     // [n_segs][4] world segments
@@ -53,7 +54,7 @@ struct lgs_fb_out {
     double* guess;          // [n_scans][3] odometry guesses (scan 0: the truth)
     double* dump_ranges;    // [n_dump][n_beams]
     double total_s;         // timed steps, wall clock
-    double phase_s[5];      // upload, interpolate, latest map, match, insert
+    double phase_s[4];      // upload, interpolate, match, AppendScan (insert + latest map)
     int steps_timed;
     int not_found;          // matches with mPoseFound == false
 };
@@ -204,7 +205,7 @@ extern "C" int lgs_frontend_bench(const lgs_fb_in* in, lgs_fb_out* out)
         std::vector<ScanDataPtr> scans;
         std::vector<RobotPose2D<double>> est;
         std::vector<double> r((size_t)nb);
-        double ph[5] = { 0, 0, 0, 0, 0 };
+        double ph[4] = { 0, 0, 0, 0 };
         out->not_found = 0;
         for (int k = 0; k < n; ++k) {
             if (k == in->warmup + 1) {   // timed steps from here
@@ -221,7 +222,6 @@ extern "C" int lgs_frontend_bench(const lgs_fb_in* in, lgs_fb_out* out)
             const Clock::time_point c = Clock::now();
             scans.push_back(scan);
             RobotPose2D<double> pose, guess;
-            Clock::time_point d = c, e = c;
             if (k == 0) {
                 pose = guess = RobotPose2D<double>(t0[0], t0[1], t0[2]);
             } else {
@@ -231,27 +231,33 @@ extern "C" int lgs_frontend_bench(const lgs_fb_in* in, lgs_fb_out* out)
                 const double cs = std::cos(l.mTheta), sn = std::sin(l.mTheta);
                 guess = RobotPose2D<double>(l.mX + cs * o[0] - sn * o[1], l.mY + sn * o[0] + cs * o[1],
                                             l.mTheta + o[2]);
-                const int lo = std::max(0, k - in->latest_scans);
-                const std::vector<ScanDataPtr> ls(scans.begin() + lo, scans.begin() + k);
-                const std::vector<RobotPose2D<double>> lp(est.begin() + lo, est.begin() + k);
-                latest.ConstructMapFromScans(ls, lp, bp);   // UpdateLatestMap
-                d = Clock::now();
+                // against the latest map of the previous AppendScan
                 const ScanMatchingSummary s = matcher.OptimizePose(ScanMatchingQuery(latest.Grid(), scan, guess));
                 out->not_found += s.mPoseFound ? 0 : 1;
                 pose = s.mEstimatedPose;
-                e = Clock::now();
             }
-            local.UpdateScan(*scan, pose, bp);   // UpdateGridMap's insert
-            const Clock::time_point f = Clock::now();
+            const Clock::time_point d = Clock::now();
             est.push_back(pose);
+            // GridMapBuilder::AppendScan: local-map insert + latest map from the
+            // last latest_scans scans, one call (lgs_map_append_scan)
+            const int lo = std::max(0, k + 1 - in->latest_scans);
+            const std::vector<ScanDataPtr> ls(scans.begin() + lo, scans.begin() + k + 1);
+            const std::vector<RobotPose2D<double>> lp(est.begin() + lo, est.begin() + k + 1);
+            if (in->fused) {
+                GridMapHip::AppendScan(local, latest, ls, lp, bp);
+            } else {
+                local.UpdateScan(*scan, pose, bp);        // UpdateGridMap's insert
+                latest.ConstructMapFromScans(ls, lp, bp);   // UpdateLatestMap
+            }
+            const Clock::time_point f = Clock::now();
             out->est[3 * k] = pose.mX, out->est[3 * k + 1] = pose.mY, out->est[3 * k + 2] = pose.mTheta;
             out->guess[3 * k] = guess.mX, out->guess[3 * k + 1] = guess.mY, out->guess[3 * k + 2] = guess.mTheta;
-            ph[0] += secs(a, b), ph[1] += secs(b, c), ph[2] += secs(c, d), ph[3] += secs(d, e), ph[4] += secs(e, f);
+            ph[0] += secs(a, b), ph[1] += secs(b, c), ph[2] += secs(c, d), ph[3] += secs(d, f);
         }
         dev->Synchronize();
-        // the sensor's ray cast is excluded: total = the five phases
-        out->total_s = ph[0] + ph[1] + ph[2] + ph[3] + ph[4];
-        for (int i = 0; i < 5; ++i) out->phase_s[i] = ph[i];
+        // the sensor's ray cast is excluded: total = the four phases
+        out->total_s = ph[0] + ph[1] + ph[2] + ph[3];
+        for (int i = 0; i < 4; ++i) out->phase_s[i] = ph[i];
         out->steps_timed = n - 1 - in->warmup;
     });
 }

@@ -323,6 +323,19 @@ static void scan_arrays(const std::vector<ScanDataPtr>& scans, const std::vector
     }
 }
 
+void GridMapHip::AppendScan(GridMapHip& localMap, GridMapHip& latestMap, const std::vector<ScanDataPtr>& scans,
+                            const std::vector<RobotPose2D<double>>& poses, const GridMapBuilderParams& p)
+{
+    if (localMap.mDev != latestMap.mDev) throw Error(LGS_ERR_INVALID_ARG, "AppendScan: maps of one device");
+    std::vector<const lgs_scan*> hs;
+    std::vector<lgs_pose2d> ps;
+    scan_arrays(scans, poses, hs, ps, "AppendScan");
+    const lgs_builder_params bp = bp_of(p);
+    localMap.mDev->Check(lgs_map_append_scan(localMap.mDev->Handle(), localMap.mMap, latestMap.mMap, hs.data(),
+                                             ps.data(), (int)hs.size(), &bp),
+                         "lgs_map_append_scan");
+}
+
 void GridMapHip::ConstructMapsFromScans(const std::vector<GridMapHip*>& maps, const std::vector<int>& nodeIdxMin,
                                         const std::vector<int>& nodeIdxMax, const std::vector<ScanDataPtr>& scans,
                                         const std::vector<RobotPose2D<double>>& poses,

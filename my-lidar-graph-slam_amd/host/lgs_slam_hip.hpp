@@ -283,6 +283,12 @@ public:
     void ConstructMapFromScans(const std::vector<ScanDataPtr>& scans,
                                const std::vector<RobotPose2D<double>>& robotPoses,
                                const GridMapBuilderParams& p);
+    // GridMapBuilder::AppendScan (C/mapping/grid_map_builder.cpp:48-59): the
+    // newest scan (scans.back() at robotPoses.back()) into `localMap` as
+    // UpdateScan does, and `latestMap` rebuilt from all of `scans` as
+    // ConstructMapFromScans does -- one fused device pass for both maps.
+    static void AppendScan(GridMapHip& localMap, GridMapHip& latestMap, const std::vector<ScanDataPtr>& scans,
+                           const std::vector<RobotPose2D<double>>& robotPoses, const GridMapBuilderParams& p);
     // GridMapBuilder::AfterLoopClosure's rebuild of every local map
     // (C/mapping/grid_map_builder.cpp:62-80): maps[i] from the pose-graph
     // nodes nodeIdxMin[i]..nodeIdxMax[i] of (scans, robotPoses), one fused

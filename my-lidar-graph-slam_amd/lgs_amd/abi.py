@@ -210,6 +210,8 @@ _PROTOS = [
     ("lgs_map_update_scan", C.c_int, [_P, _P, _P, Pose2D, C.POINTER(BuilderParams)]),
     ("lgs_map_construct_from_scans", C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(Pose2D), C.c_int,
                                                C.POINTER(BuilderParams)]),
+    ("lgs_map_append_scan", C.c_int, [_P, _P, _P, C.POINTER(_P), C.POINTER(Pose2D), C.c_int,
+                                      C.POINTER(BuilderParams)]),
     ("lgs_maps_construct_from_scans", C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                                 C.c_int, C.POINTER(_P), C.POINTER(Pose2D), C.c_int,
                                                 C.POINTER(BuilderParams)]),
@@ -631,6 +633,15 @@ class Map:
         ps = (Pose2D * n)(*[Pose2D(*p) for p in poses])
         self.ctx.check(self.ctx.lib.lgs_map_construct_from_scans(self.ctx.h, self.h, arr, ps, n, C.byref(bp)),
                        "map_construct_from_scans")
+
+    def append_scan(self, latest: "Map", scans, poses, bp: BuilderParams):
+        """GridMapBuilder::AppendScan: scans[-1] inserted into this (local) map,
+        `latest` rebuilt from all of `scans` (lgs_map_append_scan)."""
+        n = len(scans)
+        arr = (_P * n)(*[s.h for s in scans])
+        ps = (Pose2D * n)(*[Pose2D(*p) for p in poses])
+        self.ctx.check(self.ctx.lib.lgs_map_append_scan(self.ctx.h, self.h, latest.h, arr, ps, n, C.byref(bp)),
+                       "map_append_scan")
 
     def render_gray(self) -> np.ndarray:
         """MapSaver::DrawMap gray image (rows flipped up-down), uint8 [h, w]."""

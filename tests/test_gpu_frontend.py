@@ -92,7 +92,7 @@ def _odometry(rng, last):
     return (last[0] + c * d[0] - s * d[1], last[1] + s * d[0] + c * d[1], last[2] + d[2])
 
 
-def _chain(ctx, world, steps, window, n_beams, check_maps_every=10):
+def _chain(ctx, world, steps, window, n_beams, check_maps_every=10, fused=False):
     """LidarGraphSlamFrontEnd::ProcessScan's per-scan loop
     (C/mapping/lidar_graph_slam_frontend.cpp:78-127) on the device, step for step
     against the same loop through the oracle: ScanInterpolator::Interpolate, the
@@ -119,14 +119,18 @@ def _chain(ctx, world, steps, window, n_beams, check_maps_every=10):
         assert dscans[-1].ranges.tolist() == orr.tolist(), k
         oscans.append(ob.OScan(orr, oa))
     est = [truths[0]]
-    local.update_scan(dscans[0], est[0], bp)
+    if fused:   # GridMapBuilder::AppendScan: insert + latest map in one call
+        local.append_scan(latest, dscans[:1], est[:1], bp)
+    else:
+        local.update_scan(dscans[0], est[0], bp)
     olocal.integrate(est[0], oscans[0], obp)
     rng = np.random.default_rng(7)
     ctx.reset_stats()
     for k in range(1, n):
         guess = _odometry(rng, est[-1])
         lo = max(0, k - 10)
-        latest.construct(dscans[lo:k], est[lo:k], bp)
+        if not fused:
+            latest.construct(dscans[lo:k], est[lo:k], bp)
         olatest.construct(est[lo:k], oscans[lo:k], obp)
         if k % check_maps_every == 1:
             same_map(latest, olatest, f"latest k{k}")
@@ -137,7 +141,10 @@ def _chain(ctx, world, steps, window, n_beams, check_maps_every=10):
         assert_same(got, ora, f"step {k}")
         e = got.estimated_pose
         est.append((e.x, e.y, e.theta))
-        local.update_scan(dscans[k], est[-1], bp)
+        if fused:
+            local.append_scan(latest, dscans[max(0, k - 9):k + 1], est[max(0, k - 9):k + 1], bp)
+        else:
+            local.update_scan(dscans[k], est[-1], bp)
         olocal.integrate(est[-1], oscans[k], obp)
     same_map(local, olocal, "local map")
     return est, truths, ctx.match_counters()
@@ -146,6 +153,13 @@ def _chain(ctx, world, steps, window, n_beams, check_maps_every=10):
 def test_frontend_chain_json_window(ctx, world):
     """60 chained frontend steps with the launcher's frontend window (0.2 m / 0.2 m / 0.5 rad)."""
     est, truths, _ = _chain(ctx, world, 60, (0.2, 0.2, 0.5), 1081)
+    assert abs(est[-1][0] - truths[-1][0]) < 0.2 and abs(est[-1][1] - truths[-1][1]) < 0.2
+
+
+def test_frontend_chain_append_scan(ctx, world):
+    """The same loop with GridMapBuilder::AppendScan as one call
+    (lgs_map_append_scan: local insert + latest rebuild in one device pass)."""
+    est, truths, _ = _chain(ctx, world, 30, (0.2, 0.2, 0.5), 1081, check_maps_every=3, fused=True)
     assert abs(est[-1][0] - truths[-1][0]) < 0.2 and abs(est[-1][1] - truths[-1][1]) < 0.2
 
 
