@@ -167,6 +167,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_RAY_CHUNK_KEYS 13  /* ray-cast keys per emit/sort/apply pass (default 2^28, max 2^30); more keys are cast in scan order over several passes */
 #define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: lane-per-block kernel for batches of at least this many matches (default 2; 1 = always), else the row kernel */
 #define LGS_OPT_FINE_LANES    16  /* 1 (default) = fine stage with one lane per pose over the batch's block list, 0 = transposed row evaluator (A/B) */
+#define LGS_OPT_LINSOLVE_SPLIT 17 /* 1 (default) = a lone ScanMatcherLinearSolver refine spreads its beams over up to 32 one-wave workgroups (in-launch hand-off per pass), 0 = one workgroup (A/B) */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

@@ -467,6 +467,174 @@ __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double*
     }
 }
 
+// --------------------------------------------------------------------------
+// Split refine (a lone OptimizePose): k_linsolve's 8 waves become 8 one-wave
+// workgroups on 8 CUs (the single workgroup is bound by one CU's gather
+// issue: ~80 gathers per beam).  Workgroup j takes exactly wave j's beams
+// (j * 64 + lane + k * 512), accumulates them in the same per-lane order and
+// reduces them with the same butterfly, and the 8 partials are added in wave
+// order like wg_sum: a split refine is bit-identical to the same refine in
+// one workgroup or in a batch (a chunk-per-workgroup order measured 0.54 ms
+// but moves the 50-iteration config-3 end points, which jitter on the
+// reference's truncation edges, past 1e-5 on 2 of 24 seeds).
+// Per pass every workgroup publishes its 13 partials as 26 write-through
+// 8-byte granules {tag = pass + 1, 32 bits of a double}
+// (cdna_hip_programming.md, publish/consume recipe R2: the data is the flag,
+// agent-scope relaxed atomics, no fence); every workgroup sweeps all 8 x 26
+// granules until every tag matches, adds the partials and runs the 3x3 solve
+// itself, so every workgroup holds the identical pose and takes the identical
+// stopping decision -- no broadcast, no second hand-off per pass.  Granules
+// are double-buffered by pass parity: a workgroup writes pass p + 2 only
+// after every workgroup has published p + 1, i.e. finished reading pass p.
+// Spins are bounded (~0.2 s of s_memrealtime): on time-out the timeout word
+// is set, every workgroup leaves, and the host reports an error.
+// --------------------------------------------------------------------------
+constexpr int kSplitWG = kLsThreads / 64;
+constexpr int kGran = 2 * kAcc;   // granules per workgroup and pass
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ bool split_exchange(gu64* __restrict__ gran, gu32* __restrict__ tmo, int pass_idx,
+                                               double (&acc)[kAcc], unsigned* __restrict__ lds)
+{
+    const int lane = threadIdx.x;
+    const unsigned epoch = (unsigned)pass_idx + 1u;
+    gu64* slot = gran + (size_t)(pass_idx & 1) * kSplitWG * kGran;
+    // wave totals (every lane: wg_sum's butterfly), then lane g < 26
+    // publishes half g & 1 of sum g >> 1
+#pragma unroll
+    for (int k = 0; k < kAcc; ++k)
+        for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off, 64);
+    double mine = acc[0];
+#pragma unroll
+    for (int k = 1; k < kAcc; ++k) mine = ((lane >> 1) == k) ? acc[k] : mine;
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(mine);
+    const unsigned half = (lane & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
+    if (lane < kGran)
+        __hip_atomic_store(slot + (size_t)blockIdx.x * kGran + lane, ((unsigned long long)epoch << 32) | half,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // sweep every workgroup's granules of this pass until all tags match
+    constexpr int total = kSplitWG * kGran;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        bool ok = true;
+        for (int g = lane; g < total; g += 64) {
+            const unsigned long long x = __hip_atomic_load(slot + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lds[g] = (unsigned)x;
+            ok &= (unsigned)(x >> 32) == epoch;
+        }
+        if (__all(ok)) break;
+        if (__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // 100 MHz clock: 0.2 s
+            if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();   // (one wave) the granule values in LDS
+    // lane k < 13: partial k of the workgroups in wave order (wg_sum's), then broadcast
+    double sk = 0.0;
+    if (lane < kAcc)
+        for (int j = 0; j < kSplitWG; ++j) {
+            const unsigned lo = lds[j * kGran + 2 * lane], hi = lds[j * kGran + 2 * lane + 1];
+            const double v = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+            sk = (j == 0) ? v : sk + v;
+        }
+#pragma unroll
+    for (int k = 0; k < kAcc; ++k) acc[k] = __shfl(sk, k, 64);
+    __syncthreads();   // LDS free for the next pass
+    return true;
+}
+
+// pass() of one wave: beams blockIdx.x * 64 + lane, + kLsThreads, ...
+// (computing two of a lane's beams together measured slower: 0.91 -> 1.18 ms,
+// 256 VGPRs at one wave per SIMD)
+__device__ __forceinline__ void wave_pass(const LsPlan& p, const double* __restrict__ grid, const LsScanRef& sc,
+                                          const double pose[3], double smin, double smax, double cmin, double cmax,
+                                          double (&acc)[kAcc])
+{
+#pragma unroll
+    for (int k = 0; k < kAcc; ++k) acc[k] = 0.0;
+    for (int i = blockIdx.x * 64 + threadIdx.x; i < sc.n; i += kLsThreads) {
+        const double r = sc.ranges[i];
+        const bool in_step = !(r >= smax || r <= smin);
+        const bool in_cost = !(r >= cmax || r <= cmin);
+        if (!in_step && !in_cost) continue;
+        double e, gv[3];
+        beam_terms(p, grid, pose, r, sc.angles[i], e, gv);
+        if (in_step) {
+            acc[0] += e * gv[0];
+            acc[1] += e * gv[1];
+            acc[2] += e * gv[2];
+            acc[3] += gv[0] * gv[0];
+            acc[4] += gv[0] * gv[1];
+            acc[5] += gv[0] * gv[2];
+            acc[6] += gv[1] * gv[1];
+            acc[7] += gv[1] * gv[2];
+            acc[8] += gv[2] * gv[2];
+        }
+        if (in_cost) {
+            acc[9] += e * e;
+            acc[10] += 2.0 * e * (-gv[0]);
+            acc[11] += 2.0 * e * (-gv[1]);
+            acc[12] += 2.0 * e * (-gv[2]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_linsolve_split(LsPlan p, const double* __restrict__ grid, LsScanRef sc,
+                                                       LsRecord* __restrict__ out, double* __restrict__ traj,
+                                                       gu64* __restrict__ gran, gu32* __restrict__ tmo)
+{
+    __shared__ unsigned lds[kSplitWG * kGran];
+    const double smin = fmax(p.step_min, sc.min_range), smax = fmin(p.step_max, sc.max_range);
+    const double cmin = fmax(p.cost_min, sc.min_range), cmax = fmin(p.cost_max, sc.max_range);
+    double pose[3] = { sc.pose0[0], sc.pose0[1], sc.pose0[2] };
+    double acc[kAcc];
+    int pass_idx = 0;
+    wave_pass(p, grid, sc, pose, smin, smax, cmin, cmax, acc);
+    if (!split_exchange(gran, tmo, pass_idx++, acc, lds)) return;
+    double prevCost = DBL_MAX, cost = DBL_MAX;
+    int it = 0;
+    for (;;) {
+        // OptimizeStep (:88-148), solved by every lane of every workgroup
+        const double H[9] = { acc[3] + p.reg_t, acc[4], acc[5],
+                              acc[4], acc[6] + p.reg_t, acc[7],
+                              acc[5], acc[7], acc[8] + p.reg_r };
+        const double b[3] = { acc[0], acc[1], acc[2] };
+        double d[3];
+        solve3_colpiv_qr(H, b, d);
+        pose[0] = pose[0] + d[0];
+        pose[1] = pose[1] + d[1];
+        pose[2] = pose[2] + d[2];
+        wave_pass(p, grid, sc, pose, smin, smax, cmin, cmax, acc);
+        if (!split_exchange(gran, tmo, pass_idx++, acc, lds)) return;
+        cost = acc[9];
+        if (traj && blockIdx.x == 0 && threadIdx.x == 0) {
+            double* t = traj + (size_t)it * 4;
+            t[0] = pose[0];
+            t[1] = pose[1];
+            t[2] = pose[2];
+            t[3] = cost;
+        }
+        if (++it >= p.max_iter || fabs(prevCost - cost) < p.conv) break;
+        prevCost = cost;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        LsRecord rec;
+        rec.pose[0] = pose[0];
+        rec.pose[1] = pose[1];
+        rec.pose[2] = pose[2];
+        rec.cost = cost;
+        rec.grad[0] = acc[10];
+        rec.grad[1] = acc[11];
+        rec.grad[2] = acc[12];
+        rec.iterations = it;
+        rec.pad = 0;
+        out[0] = rec;
+    }
+}
+
 // CostSquareError::Cost and ComputeGradient sums at one pose (diagnostics):
 // out[0] = cost, out[1..3] = sum 2 e (-grad)
 __global__ __launch_bounds__(kLsThreads) void k_sq_cost(LsPlan p, const double* __restrict__ grid,
@@ -542,20 +710,33 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     // pinned staging: [refs | records | trajectory]
     const size_t b_refs = sizeof(LsScanRef) * n, b_rec = sizeof(LsRecord) * n;
     const size_t b_traj = traj ? sizeof(double) * 4 * (size_t)iters * n : 0;
-    char* h = (char*)ctx->ensure_pinned(b_refs + b_rec + b_traj);
+    char* h = (char*)ctx->ensure_pinned(b_refs + b_rec + b_traj + 16);   // + the split refine's timeout word
     std::memcpy(h, refs.data(), b_refs);
     char* d = (char*)ctx->ensure(S_LIN0, b_refs + b_rec + b_traj);
     LGS_HIP_CHECK(hipMemcpyAsync(d, h, b_refs, hipMemcpyHostToDevice, ctx->stream));
+    const bool split = n == 1 && ctx->linsolve_split;
+    constexpr size_t b_gran = sizeof(unsigned long long) * 2 * kSplitWG * kGran;   // multiple of 16
+    char* hs = split ? (char*)ctx->ensure(S_LIN2, b_gran + 16) : nullptr;
+    if (split)   // granule tags and the timeout word zeroed every call (one block from the start)
+        LGS_HIP_CHECK(hipMemsetAsync(hs, 0, b_gran + 16, ctx->stream));
     const int tok = ctx->timing_begin(K_LINSOLVE, 0.0);
-    hipLaunchKernelGGL(k_linsolve, dim3(n), dim3(kLsThreads), 0, ctx->stream, p, grid->d,
-                       (const LsScanRef*)d, (LsRecord*)(d + b_refs),
-                       traj ? (double*)(d + b_refs + b_rec) : nullptr);
+    if (split)
+        hipLaunchKernelGGL(k_linsolve_split, dim3(kSplitWG), dim3(64), 0, ctx->stream, p, grid->d, refs[0],
+                           (LsRecord*)(d + b_refs), traj ? (double*)(d + b_refs + b_rec) : nullptr, (gu64*)hs,
+                           (gu32*)(hs + b_gran));
+    else
+        hipLaunchKernelGGL(k_linsolve, dim3(n), dim3(kLsThreads), 0, ctx->stream, p, grid->d,
+                           (const LsScanRef*)d, (LsRecord*)(d + b_refs),
+                           traj ? (double*)(d + b_refs + b_rec) : nullptr);
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
     LGS_HIP_CHECK(hipMemcpyAsync(h + b_refs, d + b_refs, b_rec + b_traj, hipMemcpyDeviceToHost,
                                  ctx->stream));
+    unsigned* htmo = (unsigned*)(h + b_refs + b_rec + b_traj);
+    if (split) LGS_HIP_CHECK(hipMemcpyAsync(htmo, hs + b_gran, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
     ctx->sync();
     if (ctx->profile) ctx->harvest();
+    if (split && *htmo != 0u) throw Error(LGS_ERR_INTERNAL, "split refine: in-launch hand-off timed out");
     const LsRecord* rec = (const LsRecord*)(h + b_refs);
     for (int j = 0; j < n; ++j) {
         lgs_linsolve_summary& o = out[j];

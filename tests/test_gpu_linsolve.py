@@ -199,11 +199,32 @@ def test_linsolve_batch_equals_single(ctx, world, small_map):
         inits.append((true[0] + 0.02, true[1] - 0.03, true[2] + 0.01))
     lp = abi.LinsolveParams(*CONFIG3)
     batch = ctx.linsolve_batch(g, lp, scans, inits)
-    for s, i, b in zip(scans, inits, batch):
-        one = ctx.linsolve(g, lp, s, i)
-        assert (one.estimated_pose.x, one.estimated_pose.y, one.estimated_pose.theta) == \
-            (b.estimated_pose.x, b.estimated_pose.y, b.estimated_pose.theta)
-        assert one.normalized_cost == b.normalized_cost and list(one.covariance) == list(b.covariance)
+    # a lone refine runs split over 8 workgroups (LGS_OPT_LINSOLVE_SPLIT, the
+    # default) or in one workgroup; both sum exactly like the batch kernel
+    for split in (1, 0):
+        ctx.set_option(abi.LGS_OPT_LINSOLVE_SPLIT, split)
+        try:
+            for s, i, b in zip(scans, inits, batch):
+                one = ctx.linsolve(g, lp, s, i)
+                assert (one.estimated_pose.x, one.estimated_pose.y, one.estimated_pose.theta) == \
+                    (b.estimated_pose.x, b.estimated_pose.y, b.estimated_pose.theta), split
+                assert one.normalized_cost == b.normalized_cost and list(one.covariance) == list(b.covariance)
+                assert one.iterations == b.iterations
+        finally:
+            ctx.set_option(abi.LGS_OPT_LINSOLVE_SPLIT, 1)
+
+
+@pytest.mark.parametrize("n_beams", [1, 63, 65, 2049, 3000])
+def test_linsolve_split_shapes(ctx, world, small_map, n_beams):
+    """The split refine at workgroup-count edges (1 beam = one workgroup, one
+    lane; > 32 x 64 beams = several beams per lane), checked step by step
+    against the oracle like every lone refine."""
+    cells, mx, my = small_map
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    og = ob.OGrid(cells, mx, my, 0.05)
+    ang = scene.beam_angles(n_beams) if n_beams > 1 else np.array([0.3])
+    r = scene.ray_cast(world, (0.2, -0.1, 0.4), ang)
+    check_solve(ctx, g, og, (20, 0.0, 0.01, 20.0, 1e-3, 1e-3, 0.01, 20.0), r, ang, (0.23, -0.12, 0.41))
 
 
 @pytest.mark.parametrize("seed", range(3))
