@@ -35,6 +35,10 @@
  *   lgs_map_construct_from_scans GridMapBuilder::ConstructMapFromScans
  *                                C/mapping/grid_map_builder.cpp:227-332 (UpdateLatestMap :196-207)
  *   lgs_map_render_gray          MapSaver::DrawMap C/io/map_saver.cpp:276-313
+ *   lgs_map_render_gray_region   MapSaver::SaveMapCore's DrawMap of the actual map size
+ *                                C/io/map_saver.cpp:413-437
+ *   lgs_map_actual_size          GridMap::ComputeActualMapSize H/grid_map/grid_map.hpp:969-1015
+ *   lgs_map_download_patches     Patch::IsAllocated H/grid_map/grid_map_patch.hpp:40
  *   lgs_scan_interpolate         ScanInterpolator::Interpolate
  *                                C/mapping/scan_interpolator.cpp:9-98
  *   lgs_maps_construct_from_scans GridMapBuilder::AfterLoopClosure's rebuild of every
@@ -349,6 +353,24 @@ int  lgs_map_construct_global(lgs_ctx* ctx, double resolution, int patch_size,
  * allocated patches (GridMap::ComputeActualMapSize); the caller crops with
  * the hit/miss counts if it needs that extent. */
 int  lgs_map_render_gray(lgs_ctx* ctx, const lgs_map* map, uint8_t* image);
+/* MapSaver::DrawMap for the w x h cells starting at cell (x0, y0) -- the
+ * region SaveMapCore draws (C/io/map_saver.cpp:413-437): gray bytes as
+ * lgs_map_render_gray, rows flipped up-down if flip_rows.  The region must lie
+ * inside the map. */
+int  lgs_map_render_gray_region(lgs_ctx* ctx, const lgs_map* map, int x0, int y0, int w, int h,
+                                int flip_rows, uint8_t* image);
+/* Patch::IsAllocated per patch (H/grid_map/grid_map_patch.hpp:40), row-major
+ * num_patches_x * num_patches_y bytes: a patch is allocated by the first
+ * update of one of its cells (GridMap::GridCellAt, H/grid_map/grid_map.hpp:807-823),
+ * moves with Resize (:652-711) and stays allocated across Reset. */
+int  lgs_map_download_patches(lgs_ctx* ctx, const lgs_map* map, uint8_t* flags);
+/* GridMap::ComputeActualMapSize (H/grid_map/grid_map.hpp:969-1015): the
+ * bounding box of the allocated patches.  out[12] = patchIdxMin x, y;
+ * patchIdxMax x, y (exclusive, after the reference's +1); gridCellIdxMin x, y;
+ * gridCellIdxMax x, y; mapSizeInPatches x, y; mapSizeInGridCells x, y.
+ * *num_allocated = allocated patches; with none the reference's bounds are
+ * INT_MAX/INT_MIN (undefined sizes) and out is all zero here. */
+int  lgs_map_actual_size(lgs_ctx* ctx, const lgs_map* map, int* num_allocated, int* out);
 /* Copy cells and per-cell hit/miss update counts (since create/construct) to
  * the host; any pointer may be NULL.  Sizes: num_cells_x * num_cells_y. */
 int  lgs_map_download(lgs_ctx* ctx, const lgs_map* map, double* cells, uint32_t* hit_count,

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <array>
 #include <cfloat>
+#include <climits>
 #include <cstring>
 
 using namespace lgs;
@@ -42,6 +43,13 @@ struct lgs_map {
     uint32_t* d_hit = nullptr;
     uint32_t* d_miss = nullptr;
     size_t cap = 0;  // cells allocated (>= w*h; construct reuses a large enough allocation)
+    // Patch::IsAllocated per patch (npx*npy bytes, H/grid_map/grid_map_patch.hpp:40):
+    // set by k_apply for every patch a ray updates (GridCellAt allocates,
+    // H/grid_map/grid_map.hpp:807-823), moved by Resize (:676-697), kept by
+    // Reset (grid_map_patch.hpp:194-203).  d_palloc2 is the spare of a remap.
+    uint8_t* d_palloc = nullptr;
+    uint8_t* d_palloc2 = nullptr;
+    size_t pcap = 0, pcap2 = 0;
     lgs_grid view;
 };
 
@@ -84,6 +92,8 @@ struct RayMap {
     double* cells;
     uint32_t* hit;
     uint32_t* miss;
+    uint8_t* palloc;   // patch allocation flags (lgs_map::d_palloc)
+    int ps, npx;
 };
 
 // One thread per ray: Bresenham walk (H/util.hpp:256-303), start cell
@@ -293,6 +303,10 @@ __global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys
     const double oph = cph / (1.0 - cph), opm = cpm / (1.0 - cpm);
     const RayMap mp = maps[find_map(maps, nmaps, cell)];
     const unsigned long long local = cell - mp.base;
+    // the first Update of a cell allocates its patch (GridCellAt, :817-819);
+    // every thread of the patch stores the same byte
+    const unsigned lx = (unsigned)(local % (unsigned)mp.w), ly = (unsigned)(local / (unsigned)mp.w);
+    mp.palloc[(ly / (unsigned)mp.ps) * (unsigned)mp.npx + lx / (unsigned)mp.ps] = 1;
     double v = mp.cells[local];
     uint32_t nh = 0, nm = 0;
     const double a0 = ch->a[0], a1 = ch->a[1], a2 = ch->a[2], a3 = ch->a[3];
@@ -372,25 +386,40 @@ __global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys
     mp.miss[local] += nm;
 }
 
-// MapSaver::DrawMap (C/io/map_saver.cpp:276-313) for every cell of the map:
-// gray = (uint8)((1 - p) * 255) for 0 < p <= 1, else the background 192;
-// rows flipped up-down as the PNG is written (:455-456).  One thread per
-// 4 consecutive cells of a row (4-byte stores).
-__global__ __launch_bounds__(256) void k_render_gray(const double* __restrict__ cells, int W, int H,
-                                                     uint8_t* __restrict__ img)
+// MapSaver::DrawMap (C/io/map_saver.cpp:276-313) for the W x H cells of the
+// map (row stride `stride`) starting at cell (x0, y0): gray = (uint8)((1 - p)
+// * 255) for 0 < p <= 1, else the background 192 (unallocated patches hold
+// 0.0 and so render as the background too); rows flipped up-down if `flip`,
+// as the PNG is written (:455-456).  One thread per 4 consecutive cells of a
+// row.
+__global__ __launch_bounds__(256) void k_render_gray(const double* __restrict__ cells, int stride, int x0c, int y0c,
+                                                     int W, int H, int flip, uint8_t* __restrict__ img)
 {
     const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const int qw = (W + 3) / 4;
     if (q >= (long long)qw * H) return;
     const int y = (int)(q / qw), x0 = (int)(q % qw) * 4;
-    uint8_t* row = img + (size_t)(H - 1 - y) * W;
+    uint8_t* row = img + (size_t)(flip ? H - 1 - y : y) * W;
+    const double* src = cells + (size_t)(y0c + y) * stride + x0c;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int x = x0 + i;
         if (x >= W) break;
-        const double v = cells[(size_t)y * W + x];
+        const double v = src[x];
         row[x] = (v <= 0.0 || v > 1.0) ? (uint8_t)192 : (uint8_t)((1.0 - v) * 255.0);
     }
+}
+
+// Resize (:676-697) of the patch allocation flags: new patch (x, y) is old
+// patch (x + pminx, y + pminy), or unallocated outside the old grid.
+__global__ __launch_bounds__(256) void k_patch_remap(const uint8_t* __restrict__ src, int snpx, int snpy,
+                                                     uint8_t* __restrict__ dst, int npx, int npy, int pminx,
+                                                     int pminy)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npx * npy) return;
+    const int x = i % npx + pminx, y = i / npx + pminy;
+    dst[i] = (x >= 0 && x < snpx && y >= 0 && y < snpy) ? src[(size_t)y * snpx + x] : (uint8_t)0;
 }
 
 // ---------------------------------------------------------------------------
@@ -423,6 +452,23 @@ void map_free(lgs_map* m)
     hipFree(m->d_cells);
     m->d_cells = nullptr;
     m->d_hit = m->d_miss = nullptr;
+}
+
+// Patch flags of a new map (all unallocated)
+void palloc_init(lgs_map* m)
+{
+    const size_t n = std::max<size_t>(1, (size_t)m->npx * m->npy);
+    if (hipMalloc(&m->d_palloc, n) != hipSuccess) throw Error(LGS_ERR_OOM, "hipMalloc failed for map patches");
+    m->pcap = n;
+    LGS_HIP_CHECK(hipMemsetAsync(m->d_palloc, 0, n, m->ctx->stream));
+}
+
+void palloc_free(lgs_map* m)
+{
+    hipFree(m->d_palloc);
+    hipFree(m->d_palloc2);
+    m->d_palloc = m->d_palloc2 = nullptr;
+    m->pcap = m->pcap2 = 0;
 }
 
 void map_sync_view(lgs_map* m)
@@ -459,6 +505,29 @@ ResizeGeom resize_geom(const lgs_map* m, double minX, double minY, double maxX, 
     g.w = g.npx * ps;
     g.h = g.npy * ps;
     return g;
+}
+
+// Resize of the patch flags (before map_set_geom: m->npx/npy are the old
+// counts).  A resize that keeps the patch grid leaves them in place.
+void palloc_remap(lgs_map* m, const ResizeGeom& g)
+{
+    if (g.pminx == 0 && g.pminy == 0 && g.npx == m->npx && g.npy == m->npy) return;
+    const size_t n = std::max<size_t>(1, (size_t)g.npx * g.npy);
+    if (n > m->pcap2) {
+        hipFree(m->d_palloc2);
+        m->d_palloc2 = nullptr;
+        m->pcap2 = 0;
+        if (hipMalloc(&m->d_palloc2, 2 * n) != hipSuccess)
+            throw Error(LGS_ERR_OOM, "hipMalloc failed for map patches");
+        m->pcap2 = 2 * n;
+    }
+    if (g.npx * g.npy > 0)
+        hipLaunchKernelGGL(k_patch_remap, dim3((unsigned)((g.npx * g.npy + 255) / 256)), dim3(256), 0,
+                           m->ctx->stream, m->d_palloc, m->npx, m->npy, m->d_palloc2, g.npx, g.npy, g.pminx,
+                           g.pminy);
+    LGS_HIP_CHECK(hipGetLastError());
+    std::swap(m->d_palloc, m->d_palloc2);
+    std::swap(m->pcap, m->pcap2);
 }
 
 void map_set_geom(lgs_map* m, const ResizeGeom& g)
@@ -502,6 +571,7 @@ void map_resize(lgs_map* m, double minX, double minY, double maxX, double maxY)
     m->d_hit = hit;
     m->d_miss = miss;
     m->cap = std::max<size_t>(1, (size_t)nw * nh);
+    palloc_remap(m, g);
     map_set_geom(m, g);
 }
 
@@ -530,6 +600,7 @@ void map_resize_reset(lgs_map* m, double minX, double minY, double maxX, double 
         m->d_miss = (uint32_t*)((char*)m->d_cells + 12 * need);
         LGS_HIP_CHECK(hipMemsetAsync(m->d_cells, 0, need * 16, st));
     }
+    palloc_remap(m, g);   // Reset keeps the patches allocated (grid_map_patch.hpp:194-203)
     map_set_geom(m, g);
 }
 
@@ -728,7 +799,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
             for (size_t q = 0; q < units.size(); ++q)
                 if (q == 0 || units[q].job != units[q - 1].job) {
                     const lgs_map* m = jobs[units[q].job].m;
-                    maps.push_back(RayMap{cells, m->w, m->h, m->d_cells, m->d_hit, m->d_miss});
+                    maps.push_back(RayMap{cells, m->w, m->h, m->d_cells, m->d_hit, m->d_miss, m->d_palloc, m->ps, m->npx});
                     cells += (unsigned long long)m->w * m->h;
                 }
             keys = total_keys, nr = total_rays, eu = units.size(), er = 0;
@@ -745,7 +816,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
                 const lgs_map* m = jobs[U.job].m;
                 const unsigned long long mc = (unsigned long long)m->w * m->h;
                 if (nr > 0 && cells + mc > (1ull << 31)) break;
-                maps.push_back(RayMap{cells, m->w, m->h, m->d_cells, m->d_hit, m->d_miss});
+                maps.push_back(RayMap{cells, m->w, m->h, m->d_cells, m->d_hit, m->d_miss, m->d_palloc, m->ps, m->npx});
                 cells += mc;
                 cur = U.job;
             }
@@ -898,7 +969,10 @@ extern "C" int lgs_map_create(lgs_ctx* ctx, double res, int ps, int ncx, int ncy
         try {
             map_alloc(m, m->w, m->h, &m->d_cells, &m->d_hit, &m->d_miss);
             m->cap = std::max<size_t>(1, (size_t)m->w * m->h);
+            palloc_init(m);
         } catch (...) {
+            map_free(m);
+            palloc_free(m);
             delete m;
             throw;
         }
@@ -912,6 +986,7 @@ extern "C" void lgs_map_destroy(lgs_map* m)
     if (!m) return;
     hipSetDevice(m->device);
     map_free(m);
+    palloc_free(m);
     delete m;
 }
 
@@ -1057,7 +1132,7 @@ extern "C" int lgs_map_render_gray(lgs_ctx* ctx, const lgs_map* m, uint8_t* imag
         uint8_t* d_img = (uint8_t*)ctx->ensure(S_RAY2, n);
         const long long threads = (long long)((m->w + 3) / 4) * m->h;
         hipLaunchKernelGGL(k_render_gray, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, m->d_cells,
-                           m->w, m->h, d_img);
+                           m->w, 0, 0, m->w, m->h, 1, d_img);
         LGS_HIP_CHECK(hipGetLastError());
         LGS_HIP_CHECK(hipMemcpyAsync(image, d_img, n, hipMemcpyDeviceToHost, st));
         LGS_HIP_CHECK(hipStreamSynchronize(st));
@@ -1080,4 +1155,65 @@ extern "C" int lgs_map_download(lgs_ctx* ctx, const lgs_map* m, double* cells, u
             LGS_HIP_CHECK(hipMemcpyAsync(miss, m->d_miss, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         LGS_HIP_CHECK(hipStreamSynchronize(st));
     });
+}
+
+extern "C" int lgs_map_render_gray_region(lgs_ctx* ctx, const lgs_map* m, int x0, int y0, int w, int h,
+                                          int flip_rows, uint8_t* image)
+{
+    if (!ctx || !m || !image || x0 < 0 || y0 < 0 || w < 0 || h < 0 || x0 + (long long)w > m->w ||
+        y0 + (long long)h > m->h)
+        return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        const size_t n = (size_t)w * h;
+        if (!n) return;
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        hipStream_t st = ctx->stream;
+        uint8_t* d_img = (uint8_t*)ctx->ensure(S_RAY2, n);
+        const long long threads = (long long)((w + 3) / 4) * h;
+        hipLaunchKernelGGL(k_render_gray, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, m->d_cells,
+                           m->w, x0, y0, w, h, flip_rows ? 1 : 0, d_img);
+        LGS_HIP_CHECK(hipGetLastError());
+        LGS_HIP_CHECK(hipMemcpyAsync(image, d_img, n, hipMemcpyDeviceToHost, st));
+        LGS_HIP_CHECK(hipStreamSynchronize(st));
+    });
+}
+
+extern "C" int lgs_map_download_patches(lgs_ctx* ctx, const lgs_map* m, uint8_t* flags)
+{
+    if (!ctx || !m || !flags) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        const size_t n = (size_t)m->npx * m->npy;
+        if (!n) return;
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        LGS_HIP_CHECK(hipMemcpyAsync(flags, m->d_palloc, n, hipMemcpyDeviceToHost, ctx->stream));
+        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+extern "C" int lgs_map_actual_size(lgs_ctx* ctx, const lgs_map* m, int* num_allocated, int* out)
+{
+    if (!ctx || !m || !num_allocated || !out) return LGS_ERR_INVALID_ARG;
+    std::vector<uint8_t> f((size_t)m->npx * m->npy);
+    const int rc = f.empty() ? LGS_OK : lgs_map_download_patches(ctx, m, f.data());
+    if (rc != LGS_OK) return rc;
+    // GridMap::ComputeActualMapSize (H/grid_map/grid_map.hpp:969-1015)
+    int pminx = INT_MAX, pminy = INT_MAX, pmaxx = INT_MIN, pmaxy = INT_MIN, n = 0;
+    for (int y = 0; y < m->npy; ++y)
+        for (int x = 0; x < m->npx; ++x)
+            if (f[(size_t)y * m->npx + x]) {
+                ++n;
+                pminx = std::min(pminx, x);
+                pminy = std::min(pminy, y);
+                pmaxx = std::max(pmaxx, x);
+                pmaxy = std::max(pmaxy, y);
+            }
+    *num_allocated = n;
+    for (int i = 0; i < 12; ++i) out[i] = 0;
+    if (!n) return LGS_OK;
+    const int ps = m->ps;
+    out[0] = pminx, out[1] = pminy, out[2] = pmaxx + 1, out[3] = pmaxy + 1;                 // patchIdxMin/Max
+    out[4] = pminx * ps, out[5] = pminy * ps, out[6] = pmaxx * ps + ps, out[7] = pmaxy * ps + ps;  // :918-929
+    out[8] = out[2] - out[0], out[9] = out[3] - out[1];                                     // mapSizeInPatches
+    out[10] = out[6] - out[4], out[11] = out[7] - out[5];                                   // mapSizeInGridCells
+    return LGS_OK;
 }

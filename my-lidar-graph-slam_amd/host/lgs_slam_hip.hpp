@@ -306,6 +306,8 @@ public:
     // non-owning view of the current cells (valid until the next geometry change)
     DeviceGridPtr Grid() const;
     void Download(std::vector<double>* cells, std::vector<uint32_t>* hits, std::vector<uint32_t>* misses) const;
+    lgs_map* Handle() const { return mMap; }
+    const DevicePtr& Dev() const { return mDev; }
 
 private:
     GridMapHip(DevicePtr dev, lgs_map* map) : mDev(std::move(dev)), mMap(map) {}

@@ -219,6 +219,10 @@ _PROTOS = [
     ("lgs_map_construct_global", C.c_int, [_P, C.c_double, C.c_int, C.POINTER(_P), C.POINTER(Pose2D), C.c_int,
                                            C.POINTER(BuilderParams), C.POINTER(_P)]),
     ("lgs_map_render_gray", C.c_int, [_P, _P, C.POINTER(C.c_uint8)]),
+    ("lgs_map_render_gray_region", C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                             C.POINTER(C.c_uint8)]),
+    ("lgs_map_download_patches", C.c_int, [_P, _P, C.POINTER(C.c_uint8)]),
+    ("lgs_map_actual_size", C.c_int, [_P, _P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("lgs_map_download", C.c_int, [_P, _P, C.POINTER(C.c_double), C.POINTER(C.c_uint32),
                                    C.POINTER(C.c_uint32)]),
     ("lgs_grid_precompute_pyramid", C.c_int, [_P, _P, C.c_int, C.POINTER(_P)]),
@@ -653,6 +657,31 @@ class Map:
                                                             img.ctypes.data_as(C.POINTER(C.c_uint8))),
                            "map_render_gray")
         return img
+
+    def render_gray_region(self, x0, y0, w, h, flip=True) -> np.ndarray:
+        """DrawMap of the w x h cells at (x0, y0), uint8 [h, w] (lgs_map_render_gray_region)."""
+        img = np.zeros((h, w), dtype=np.uint8)
+        self.ctx.check(self.ctx.lib.lgs_map_render_gray_region(self.ctx.h, self.h, x0, y0, w, h, int(flip),
+                                                               img.ctypes.data_as(C.POINTER(C.c_uint8))),
+                       "map_render_gray_region")
+        return img
+
+    def patches(self) -> np.ndarray:
+        """Patch::IsAllocated per patch, uint8 [npy, npx]."""
+        g = self.geometry()
+        f = np.zeros((g["npy"], g["npx"]), dtype=np.uint8)
+        if f.size:
+            self.ctx.check(self.ctx.lib.lgs_map_download_patches(self.ctx.h, self.h,
+                                                                 f.ctypes.data_as(C.POINTER(C.c_uint8))),
+                           "map_download_patches")
+        return f
+
+    def actual_size(self):
+        """GridMap::ComputeActualMapSize -> (allocated patches, 12 ints)."""
+        n = C.c_int()
+        out = (C.c_int * 12)()
+        self.ctx.check(self.ctx.lib.lgs_map_actual_size(self.ctx.h, self.h, C.byref(n), out), "map_actual_size")
+        return n.value, list(out)
 
     def download(self):
         g = self.geometry()

@@ -18,6 +18,7 @@
 #include "lgs_oracle.h"
 
 #include <float.h>
+#include <limits.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -669,7 +670,8 @@ int orc_map_init(orc_map* m, double res, int ps, int ncx, int ncy, double cx, do
     m->cells = (double*)calloc(n + 1, sizeof(double));
     m->hit_count = (uint32_t*)calloc(n + 1, sizeof(uint32_t));
     m->miss_count = (uint32_t*)calloc(n + 1, sizeof(uint32_t));
-    return (m->cells && m->hit_count && m->miss_count) ? 0 : 1;
+    m->patch_alloc = (uint8_t*)calloc((size_t)m->npx * (size_t)m->npy + 1, 1);
+    return (m->cells && m->hit_count && m->miss_count && m->patch_alloc) ? 0 : 1;
 }
 
 void orc_map_free(orc_map* m)
@@ -677,6 +679,7 @@ void orc_map_free(orc_map* m)
     free(m->cells);
     free(m->hit_count);
     free(m->miss_count);
+    free(m->patch_alloc);
     memset(m, 0, sizeof(*m));
 }
 
@@ -696,11 +699,13 @@ void orc_map_resize(orc_map* m, double minX, double minY, double maxX, double ma
     double* cells = (double*)calloc(n + 1, sizeof(double));
     uint32_t* hc = (uint32_t*)calloc(n + 1, sizeof(uint32_t));
     uint32_t* mc = (uint32_t*)calloc(n + 1, sizeof(uint32_t));
+    uint8_t* pa = (uint8_t*)calloc((size_t)npx * (size_t)npy + 1, 1);
 
     const int x0 = imax(0, pminx), y0 = imax(0, pminy);
     const int x1 = imin(m->npx, pmaxx + 1), y1 = imin(m->npy, pmaxy + 1);
     for (int py = y0; py < y1; ++py) {
         for (int px = x0; px < x1; ++px) {
+            pa[(size_t)(py - pminy) * npx + (px - pminx)] = m->patch_alloc[(size_t)py * m->npx + px];
             const int nx = (px - pminx) * ps, ny = (py - pminy) * ps;
             const int ox = px * ps, oy = py * ps;
             for (int yy = 0; yy < ps; ++yy) {
@@ -715,9 +720,11 @@ void orc_map_resize(orc_map* m, double minX, double minY, double maxX, double ma
     free(m->cells);
     free(m->hit_count);
     free(m->miss_count);
+    free(m->patch_alloc);
     m->cells = cells;
     m->hit_count = hc;
     m->miss_count = mc;
+    m->patch_alloc = pa;
     m->npx = npx;
     m->npy = npy;
     m->w = nw;
@@ -757,11 +764,145 @@ void orc_map_reset(orc_map* m)
     memset(m->miss_count, 0, n * sizeof(uint32_t));
 }
 
+int orc_map_actual_size(const orc_map* m, int out[12])
+{
+    /* GridMap::ComputeActualMapSize (H/grid_map/grid_map.hpp:969-1015) */
+    int pminx = INT_MAX, pminy = INT_MAX, pmaxx = INT_MIN, pmaxy = INT_MIN, n = 0;
+    for (int y = 0; y < m->npy; ++y)
+        for (int x = 0; x < m->npx; ++x) {
+            if (!m->patch_alloc[(size_t)y * m->npx + x])
+                continue;
+            ++n;
+            pminx = imin(pminx, x);
+            pminy = imin(pminy, y);
+            pmaxx = imax(pmaxx, x);
+            pmaxy = imax(pmaxy, y);
+        }
+    memset(out, 0, sizeof(int) * 12);
+    if (n == 0)
+        return 0;
+    const int ps = m->patch_size;
+    /* PatchIndexToGridCellIndexRange (:918-929): min corner of the min patch,
+     * max corner (exclusive) of the max patch */
+    out[4] = pminx * ps;
+    out[5] = pminy * ps;
+    out[6] = pmaxx * ps + ps;
+    out[7] = pmaxy * ps + ps;
+    out[0] = pminx;
+    out[1] = pminy;
+    out[2] = pmaxx + 1;
+    out[3] = pmaxy + 1;
+    out[8] = out[2] - out[0];
+    out[9] = out[3] - out[1];
+    out[10] = out[6] - out[4];
+    out[11] = out[7] - out[5];
+    return n;
+}
+
+/* gil::fill_pixels(subimage_view(view, x, y, s, s), px): an s x s block
+ * (pixels outside the image are dropped) */
+static void fill_block(uint8_t* rgb, int w, int h, int x, int y, int s, uint8_t r, uint8_t g, uint8_t b)
+{
+    for (int yy = y; yy < y + s; ++yy)
+        for (int xx = x; xx < x + s; ++xx) {
+            if (xx < 0 || xx >= w || yy < 0 || yy >= h)
+                continue;
+            uint8_t* p = rgb + 3 * ((size_t)yy * w + xx);
+            p[0] = r;
+            p[1] = g;
+            p[2] = b;
+        }
+}
+
+int orc_map_draw_image(const orc_map* m, const orc_pose* nodes, int n_nodes, int draw_trajectory,
+                       int node_min, int node_max, const orc_scan* scan, orc_pose scan_pose,
+                       uint8_t* rgb, int* w_out, int* h_out)
+{
+    int a[12];
+    *w_out = *h_out = 0;
+    if (!orc_map_actual_size(m, a))
+        return 1;
+    const int W = a[10], H = a[11], ps = m->patch_size;
+    const int gx0 = a[4], gy0 = a[5], gx1 = a[6], gy1 = a[7];
+    uint8_t* img = (uint8_t*)malloc((size_t)W * H * 3 + 1);
+    memset(img, 192, (size_t)W * H * 3);          /* :430-433 */
+    /* DrawMap (:278-317): allocated patches of the bounding box */
+    for (int py = 0; py < a[9]; ++py)
+        for (int px = 0; px < a[8]; ++px) {
+            const int qx = a[0] + px, qy = a[1] + py;
+            if (!m->patch_alloc[(size_t)qy * m->npx + qx])
+                continue;
+            for (int yy = 0; yy < ps; ++yy)
+                for (int xx = 0; xx < ps; ++xx) {
+                    const double v = m->cells[(size_t)(qy * ps + yy) * m->w + (size_t)(qx * ps + xx)];
+                    if (v <= 0.0 || v > 1.0)
+                        continue;
+                    const uint8_t g = (uint8_t)((1.0 - v) * 255.0);
+                    uint8_t* p = img + 3 * ((size_t)(py * ps + yy) * W + (size_t)(px * ps + xx));
+                    p[0] = p[1] = p[2] = g;
+                }
+        }
+    /* DrawTrajectory (:320-362) */
+    if (draw_trajectory && n_nodes > 0 && node_min >= 0 && node_min < n_nodes && node_max < n_nodes) {
+        int pxc, pyc;
+        world_to_cell(m->min_x, m->min_y, m->res, nodes[node_min].x, nodes[node_min].y, &pxc, &pyc);
+        int* buf = NULL;
+        int cap = 0;
+        for (int i = node_min + 1; i <= node_max; ++i) {
+            int cx, cy;
+            world_to_cell(m->min_x, m->min_y, m->res, nodes[i].x, nodes[i].y, &cx, &cy);
+            const int need = imax(abs(cx - pxc), abs(cy - pyc)) + 2;
+            if (need > cap) {
+                cap = 2 * need;
+                buf = (int*)realloc(buf, sizeof(int) * 2 * (size_t)cap);
+            }
+            const int nl = orc_bresenham(pxc, pyc, cx, cy, buf, cap);
+            for (int j = 0; j < nl; ++j) {
+                const int ix = buf[2 * j], iy = buf[2 * j + 1];
+                if (ix < gx0 || ix >= gx1 - 1 || iy < gy0 || iy >= gy1 - 1)
+                    continue;
+                fill_block(img, W, H, ix - gx0, iy - gy0, 2, 255, 0, 0);
+            }
+            pxc = cx;
+            pyc = cy;
+        }
+        free(buf);
+    }
+    /* DrawScan (:365-410); note the reference tests the pose's y index
+     * against gridCellIdxMax.mX (:380) */
+    if (scan) {
+        int sx, sy;
+        world_to_cell(m->min_x, m->min_y, m->res, scan_pose.x, scan_pose.y, &sx, &sy);
+        if (sx >= gx0 && sx < gx1 - 2 && sy >= gy0 && sy < gx1 - 2)
+            fill_block(img, W, H, sx - gx0, sy - gy0, 3, 0, 255, 0);
+        const orc_pose sp = orc_compound(scan_pose, scan->rel_sensor_pose);
+        for (int i = 0; i < scan->n; ++i) {
+            double sinT, cosT;
+            sincos(sp.theta + scan->angles[i], &sinT, &cosT);   /* HitPoint, H/sensor/sensor_data.hpp:162-173 */
+            const double hx = sp.x + scan->ranges[i] * cosT;
+            const double hy = sp.y + scan->ranges[i] * sinT;
+            int ix, iy;
+            world_to_cell(m->min_x, m->min_y, m->res, hx, hy, &ix, &iy);
+            if (ix < gx0 || ix >= gx1 - 1 || iy < gy0 || iy >= gy1 - 1)
+                continue;
+            fill_block(img, W, H, ix - gx0, iy - gy0, 2, 0, 0, 255);
+        }
+    }
+    /* flipped_up_down_view (:455-462) */
+    for (int y = 0; y < H; ++y)
+        memcpy(rgb + (size_t)y * W * 3, img + (size_t)(H - 1 - y) * W * 3, (size_t)W * 3);
+    free(img);
+    *w_out = W;
+    *h_out = H;
+    return 0;
+}
+
 static inline void map_update(orc_map* m, int x, int y, double p, int is_hit)
 {
     /* GridMap::Update (:876-881) -> GridCellAt (:807-823) -> Bayes update */
     const size_t k = (size_t)y * (size_t)m->w + (size_t)x;
     m->cells[k] = orc_bayes_update(m->cells[k], p);
+    m->patch_alloc[(size_t)(y / m->patch_size) * m->npx + (size_t)(x / m->patch_size)] = 1;
     if (is_hit)
         m->hit_count[k]++;
     else

@@ -148,6 +148,9 @@ typedef struct {
     double* cells;           /* dense w*h, 0.0 = unknown */
     uint32_t* hit_count;     /* per-cell number of pHit updates (diagnostic) */
     uint32_t* miss_count;    /* per-cell number of pMiss updates (diagnostic) */
+    uint8_t* patch_alloc;    /* npx*npy: Patch::IsAllocated (H/grid_map/grid_map_patch.hpp:40) --
+                              * set by the first Update of a cell of the patch (GridCellAt :807-823),
+                              * moved by Resize (:676-697), kept by Reset (grid_map_patch.hpp:194-203) */
 } orc_map;
 
 /* GridMap(res, ps, numCellsX, numCellsY, center) (:337-391) */
@@ -158,6 +161,21 @@ void orc_map_resize(orc_map* m, double min_x, double min_y, double max_x, double
 void orc_map_expand(orc_map* m, double min_x, double min_y, double max_x, double max_y,
                     double enlarge_step);                                            /* :714-736 */
 void orc_map_reset(orc_map* m);                                                       /* :739-753 */
+/* GridMap::ComputeActualMapSize (:969-1015): out[12] = patchIdxMin x,y; patchIdxMax x,y
+ * (after the +1 correction); gridCellIdxMin x,y; gridCellIdxMax x,y; mapSizeInPatches x,y;
+ * mapSizeInGridCells x,y.  Returns the number of allocated patches (0: the
+ * reference's result is undefined -- INT_MAX/INT_MIN bounds -- and out is zeroed). */
+int orc_map_actual_size(const orc_map* m, int out[12]);
+/* MapSaver::SaveMapCore's image (C/io/map_saver.cpp:413-463) before PNG
+ * encoding: DrawMap (:278-317) on a 192-gray canvas of the actual map size,
+ * DrawTrajectory (:320-362) of nodes[node_min..node_max] if draw_trajectory,
+ * DrawScan (:365-410) of `scan` at scan_pose if scan != NULL, then flipped
+ * up-down (:455-462).  rgb receives w*h*3 bytes (w, h = mapSizeInGridCells);
+ * returns 0, or 1 if the map has no allocated patch.  Pixels a reference
+ * subimage_view would place outside the image are dropped. */
+int orc_map_draw_image(const orc_map* m, const orc_pose* node_poses, int n_nodes, int draw_trajectory,
+                       int node_min, int node_max, const orc_scan* scan, orc_pose scan_pose,
+                       uint8_t* rgb, int* w, int* h);
 
 typedef struct { orc_pose pose; orc_scan scan; } orc_node;
 

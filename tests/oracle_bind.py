@@ -52,7 +52,7 @@ class Map(C.Structure):
     _fields_ = [("res", C.c_double), ("patch_size", C.c_int), ("npx", C.c_int), ("npy", C.c_int),
                 ("w", C.c_int), ("h", C.c_int), ("min_x", C.c_double), ("min_y", C.c_double),
                 ("cells", C.POINTER(C.c_double)), ("hit_count", C.POINTER(C.c_uint32)),
-                ("miss_count", C.POINTER(C.c_uint32))]
+                ("miss_count", C.POINTER(C.c_uint32)), ("patch_alloc", C.POINTER(C.c_uint8))]
 
 
 class Node(C.Structure):
@@ -129,6 +129,12 @@ def lib():
                                                    C.POINTER(BuilderParams)]
         L.orc_integrate_scan.restype = C.c_int
         L.orc_integrate_scan.argtypes = [C.POINTER(Map), Pose, C.POINTER(Scan), C.POINTER(BuilderParams)]
+        L.orc_map_actual_size.restype = C.c_int
+        L.orc_map_actual_size.argtypes = [C.POINTER(Map), C.POINTER(C.c_int)]
+        L.orc_map_draw_image.restype = C.c_int
+        L.orc_map_draw_image.argtypes = [C.POINTER(Map), C.POINTER(Pose), C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.POINTER(Scan), Pose, C.POINTER(C.c_uint8), C.POINTER(C.c_int),
+                                         C.POINTER(C.c_int)]
         L.orc_sq_smoothed_value.restype = C.c_double
         L.orc_sq_smoothed_value.argtypes = [C.POINTER(Grid), C.c_double, C.c_double]
         L.orc_sq_cost.restype = C.c_double
@@ -237,6 +243,34 @@ class OMap:
     def geometry(self):
         m = self.m
         return dict(w=m.w, h=m.h, min_x=m.min_x, min_y=m.min_y, npx=m.npx, npy=m.npy)
+
+    def patches(self):
+        """Patch::IsAllocated per patch, [npy, npx]"""
+        m = self.m
+        return np.ctypeslib.as_array(m.patch_alloc, shape=(m.npy, m.npx)).copy()
+
+    def actual_size(self):
+        """GridMap::ComputeActualMapSize -> (count, 12 ints)"""
+        out = (C.c_int * 12)()
+        n = lib().orc_map_actual_size(C.byref(self.m), out)
+        return n, list(out)
+
+    def draw_image(self, node_poses, draw_trajectory=False, node_min=0, node_max=-1, scan=None,
+                   scan_pose=(0.0, 0.0, 0.0)):
+        """MapSaver::SaveMapCore's image (flipped), [h, w, 3] uint8, or None"""
+        n, a = self.actual_size()
+        if n == 0:
+            return None
+        k = len(node_poses)
+        nodes = (Pose * max(1, k))(*[Pose(*p) for p in node_poses])
+        buf = np.zeros(a[10] * a[11] * 3, dtype=np.uint8)
+        w, h = C.c_int(), C.c_int()
+        rc = lib().orc_map_draw_image(C.byref(self.m), nodes, k, int(draw_trajectory), node_min,
+                                      node_max if node_max >= 0 else k - 1,
+                                      C.byref(scan.s) if scan is not None else None, Pose(*scan_pose),
+                                      buf.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(w), C.byref(h))
+        assert rc == 0
+        return buf.reshape(h.value, w.value, 3)
 
     def integrate(self, pose, oscan: OScan, bp: BuilderParams):
         lib().orc_integrate_scan(C.byref(self.m), Pose(*pose), C.byref(oscan.s), C.byref(bp))

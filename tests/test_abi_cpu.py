@@ -13,9 +13,9 @@ from lgs_amd import abi
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
+def declared_symbols(header="*.h"):
     syms = set()
-    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+    for h in glob.glob(os.path.join(ROOT, "include", header)):
         text = open(h).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(lgs_\w+)\s*\(", text, flags=re.M):
@@ -29,12 +29,25 @@ def test_library_built():
 
 def test_exports_every_declared_symbol():
     lib = C.CDLL(abi.LIB_PATH)
-    decl = declared_symbols()
+    decl = declared_symbols("lgs_hip.h")
     assert len(decl) >= 20
     missing = [s for s in sorted(decl) if not hasattr(lib, s)]
     assert not missing, f"declared but not exported: {missing}"
     # the Python binding covers every declared entry point
     assert decl == set(abi.SYMBOLS), decl.symmetric_difference(abi.SYMBOLS)
+
+
+def test_host_library_exports_lgs_io_h():
+    """include/lgs_io.h (f4 host components) is exported by liblgs_slam_hip.so"""
+    from lgs_amd import io
+    lib = io.load()
+    decl = declared_symbols("lgs_io.h")
+    assert len(decl) >= 7
+    missing = [s for s in sorted(decl) if not hasattr(lib, s)]
+    assert not missing, f"declared but not exported: {missing}"
+    assert decl == set(io.SYMBOLS), decl.symmetric_difference(io.SYMBOLS)
+    # every header symbol lives in one of the two libraries
+    assert declared_symbols() == declared_symbols("lgs_hip.h") | decl
 
 
 def test_abi_version():

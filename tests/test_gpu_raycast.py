@@ -21,6 +21,9 @@ def same_map(gm, om, tag=""):
     assert np.array_equal(hits, om.hits()), tag
     assert np.array_equal(misses, om.misses()), tag
     assert np.array_equal(cells, om.cells()), tag
+    # Patch::IsAllocated (moved by Resize, kept by Reset) -> ComputeActualMapSize
+    assert np.array_equal(gm.patches(), om.patches()), tag
+    assert gm.actual_size() == om.actual_size(), tag
 
 
 def test_fixed_map_ten_scans(ctx, world):
