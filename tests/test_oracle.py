@@ -341,3 +341,83 @@ def test_construct_map_geometry_kat(i):
     scans = [ob.OScan(n["ranges"], n["angles"], tuple(n["rel"]), *n["scan_range"]) for n in c["nodes"]]
     m.construct([tuple(n["pose"]) for n in c["nodes"]], scans, ob.BuilderParams(*c["usable"], 0.6, 0.45))
     assert _geo(m) == c["state"]
+
+
+def _draw_image_py(cells, patches, ps, min_x, min_y, res, nodes, traj, lo, hi, scan, scan_pose):
+    """Second restatement of MapSaver::SaveMapCore's image (C/io/map_saver.cpp:
+    278-463) and GridMap::ComputeActualMapSize (H/grid_map/grid_map.hpp:969-1015)
+    in plain Python, from the oracle map's cells and patch flags."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_kat import bresenham, sincos
+    ys, xs = np.nonzero(patches)
+    pminx, pminy, pmaxx, pmaxy = xs.min(), ys.min(), xs.max() + 1, ys.max() + 1
+    gx0, gy0, gx1, gy1 = pminx * ps, pminy * ps, pmaxx * ps, pmaxy * ps
+    W, H = gx1 - gx0, gy1 - gy0
+    img = np.full((H, W, 3), 192, dtype=np.uint8)
+    for py in range(pminy, pmaxy):
+        for px in range(pminx, pmaxx):
+            if not patches[py, px]:
+                continue
+            for yy in range(ps):
+                for xx in range(ps):
+                    v = cells[py * ps + yy, px * ps + xx]
+                    if 0.0 < v <= 1.0:
+                        img[(py - pminy) * ps + yy, (px - pminx) * ps + xx] = int((1.0 - v) * 255.0)
+
+    def cell(x, y):
+        return math.floor((x - min_x) / res), math.floor((y - min_y) / res)
+
+    def dot(x, y, s, rgb):
+        img[max(0, y):max(0, y + s), max(0, x):max(0, x + s)] = rgb
+
+    if traj:
+        prev = cell(nodes[lo][0], nodes[lo][1])
+        for i in range(lo + 1, hi + 1):
+            cur = cell(nodes[i][0], nodes[i][1])
+            for x, y in bresenham(prev[0], prev[1], cur[0], cur[1]):
+                if gx0 <= x < gx1 - 1 and gy0 <= y < gy1 - 1:
+                    dot(x - gx0, y - gy0, 2, (255, 0, 0))
+            prev = cur
+    if scan is not None:
+        r, a, rel = scan
+        sx, sy = cell(scan_pose[0], scan_pose[1])
+        if gx0 <= sx < gx1 - 2 and gy0 <= sy < gx1 - 2:        # :380 compares y with the x bound
+            dot(sx - gx0, sy - gy0, 3, (0, 255, 0))
+        s, c = sincos(scan_pose[2])
+        sp = (scan_pose[0] + c * rel[0] - s * rel[1], scan_pose[1] + s * rel[0] + c * rel[1], scan_pose[2] + rel[2])
+        for ri, ai in zip(r, a):
+            s, c = sincos(sp[2] + ai)
+            x, y = cell(sp[0] + ri * c, sp[1] + ri * s)
+            if gx0 <= x < gx1 - 1 and gy0 <= y < gy1 - 1:
+                dot(x - gx0, y - gy0, 2, (0, 0, 255))
+    return img[::-1], [pminx, pminy, pmaxx, pmaxy, gx0, gy0, gx1, gy1, pmaxx - pminx, pmaxy - pminy, W, H]
+
+
+@pytest.mark.parametrize("overlay", [0, 1, 2])
+def test_map_saver_image_restatement(world, overlay):
+    """orc_map_draw_image / orc_map_actual_size vs the Python restatement;
+    the oracle's patch flags (set by Update, moved by Resize) equal the
+    patches holding an updated cell for a map that was never reset."""
+    from lgs_amd import scene
+    ang = scene.beam_angles(91)
+    poses = [(0.2 * k - 0.8, 0.15 * k, 0.3 * k) for k in range(8)]
+    m = ob.OMap(0.05, 16, 0, 0, center=poses[0][:2])
+    bp = ob.BuilderParams(0.01, 20.0, 0.6, 0.45)
+    for p in poses:
+        m.integrate(p, ob.OScan(scene.ray_cast(world, p, ang), ang), bp)
+    g = m.geometry()
+    touched = (m.hits() + m.misses()) > 0
+    per_patch = touched.reshape(g["npy"], 16, g["npx"], 16).any(axis=(1, 3))
+    assert np.array_equal(m.patches().astype(bool), per_patch)
+    assert not per_patch.all()
+    scan, oscan, sp = None, None, poses[3]
+    if overlay == 2:
+        r = scene.ray_cast(world, sp, ang)
+        scan = (r, ang, (0.05, 0.0, 0.1))
+        oscan = ob.OScan(r, ang, rel=(0.05, 0.0, 0.1))
+    got = m.draw_image(poses, draw_trajectory=overlay >= 1, node_min=1, node_max=6, scan=oscan, scan_pose=sp)
+    want, size = _draw_image_py(m.cells(), m.patches(), 16, g["min_x"], g["min_y"], 0.05, poses, overlay >= 1, 1,
+                                6, scan, sp)
+    assert m.actual_size() == (int(per_patch.sum()), size)
+    assert np.array_equal(got, want)
