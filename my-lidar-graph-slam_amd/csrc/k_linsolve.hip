@@ -26,7 +26,10 @@
 
 #include <cfloat>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <vector>
 
 using namespace lgs;
 
@@ -145,19 +148,40 @@ __device__ __forceinline__ double smoothed(const double* __restrict__ g, int W, 
 // Per beam at one sensor pose: residual e = 1 - S(hit point) and the map
 // gradient w.r.t. the pose (ComputeMapGradient :172-229: central differences
 // of +-0.05 cells, / (0.1 res), dtheta = -r sin gx + r cos gy).
+constexpr double kDeltaIdx = 0.1;             // ComputeMapGradient's +- 0.05 cells
+constexpr double kHalfDelta = kDeltaIdx / 2.0;
+
+// hit point of a beam in (fractional) cell coordinates
+__device__ __forceinline__ void beam_cell(const LsPlan& p, const double pose[3], double r, double a, double& sn,
+                                          double& cs, double& fx, double& fy)
+{
+    sincos(pose[2] + a, &sn, &cs);
+    const double hx = pose[0] + r * cs;
+    const double hy = pose[1] + r * sn;
+    fx = (hx - p.min_x) / p.res;
+    fy = (hy - p.min_y) / p.res;
+}
+
+// residual and pose gradient from the five smoothed values
+__device__ __forceinline__ void beam_finish(const LsPlan& p, double r, double sn, double cs, double s0, double sxp,
+                                            double sxm, double syp, double sym, double& e, double gv[3])
+{
+    const double deltaDist = p.res * kDeltaIdx;
+    const double gx = (sxp - sxm) / deltaDist;
+    const double gy = (syp - sym) / deltaDist;
+    e = 1.0 - s0;
+    gv[0] = gx;
+    gv[1] = gy;
+    gv[2] = -r * sn * gx + r * cs * gy;
+}
+
 __device__ __forceinline__ void beam_terms(const LsPlan& p, const double* __restrict__ g,
                                            const double pose[3], double r, double a, double& e,
                                            double gv[3])
 {
-    double sn, cs;
-    sincos(pose[2] + a, &sn, &cs);
-    const double hx = pose[0] + r * cs;
-    const double hy = pose[1] + r * sn;
-    const double fx = (hx - p.min_x) / p.res;
-    const double fy = (hy - p.min_y) / p.res;
-    const double deltaIdx = 0.1;
-    const double deltaDist = p.res * deltaIdx;
-    const double d = deltaIdx / 2.0;
+    double sn, cs, fx, fy;
+    beam_cell(p, pose, r, a, sn, cs, fx, fy);
+    const double d = kHalfDelta;
     const Axis x0 = make_axis(fx, p.W), xp = make_axis(fx + d, p.W), xm = make_axis(fx - d, p.W);
     const Axis y0 = make_axis(fy, p.H), yp = make_axis(fy + d, p.H), ym = make_axis(fy - d, p.H);
     const double s0 = smoothed(g, p.W, x0, y0);
@@ -165,12 +189,7 @@ __device__ __forceinline__ void beam_terms(const LsPlan& p, const double* __rest
     const double sxm = smoothed(g, p.W, xm, y0);
     const double syp = smoothed(g, p.W, x0, yp);
     const double sym = smoothed(g, p.W, x0, ym);
-    const double gx = (sxp - sxm) / deltaDist;
-    const double gy = (syp - sym) / deltaDist;
-    e = 1.0 - s0;
-    gv[0] = gx;
-    gv[1] = gy;
-    gv[2] = -r * sn * gx + r * cs * gy;
+    beam_finish(p, r, sn, cs, s0, sxp, sxm, syp, sym, e, gv);
 }
 
 // sum over the workgroup of NV values per thread (wave64 butterfly + LDS);
@@ -403,13 +422,92 @@ __device__ __forceinline__ void pass(const LsPlan& p, const double* __restrict__
     }
 }
 
+// The 13 sums of one beam (zeros for a beam outside both filters)
+__device__ __forceinline__ void beam_acc(bool in_step, bool in_cost, double e, const double gv[3],
+                                         double (&t)[kAcc])
+{
+#pragma unroll
+    for (int k = 0; k < kAcc; ++k) t[k] = 0.0;
+    if (in_step) {
+        t[0] = e * gv[0];
+        t[1] = e * gv[1];
+        t[2] = e * gv[2];
+        t[3] = gv[0] * gv[0];
+        t[4] = gv[0] * gv[1];
+        t[5] = gv[0] * gv[2];
+        t[6] = gv[1] * gv[1];
+        t[7] = gv[1] * gv[2];
+        t[8] = gv[2] * gv[2];
+    }
+    if (in_cost) {
+        t[9] = e * e;   // pow(1.0 - S, 2.0): GCC folds it to the exact product
+        t[10] = 2.0 * e * (-gv[0]);
+        t[11] = 2.0 * e * (-gv[1]);
+        t[12] = 2.0 * e * (-gv[2]);
+    }
+}
+
+__device__ __forceinline__ void wave_total(double (&t)[kAcc])
+{
+#pragma unroll
+    for (int k = 0; k < kAcc; ++k)
+        for (int off = 32; off > 0; off >>= 1) t[k] += __shfl_xor(t[k], off, 64);
+}
+
+// Summation order of a refine's sums (every kernel below uses it, so a lone
+// refine, split or not, is bit-identical to the same refine in a batch):
+// beams in groups of 64 (group g = beams 64 g .. 64 g + 63), each group summed
+// by the wave64 xor butterfly (every lane ends with the same bits), the group
+// totals then added in group order.
+constexpr int kGroup = 64;
+constexpr int kMaxGroups = 512;      // 32768 beams
+
+// One pass of the batch kernel at `pose`: group g evaluated by wave g % 8,
+// group totals through LDS, every thread returns the 13 totals.  Ends with a
+// barrier, so `red` may be rewritten by the next pass.
+__device__ __forceinline__ void group_pass(const LsPlan& p, const double* __restrict__ grid, const LsScanRef& sc,
+                                           const double pose[3], double smin, double smax, double cmin,
+                                           double cmax, double* red, double (&acc)[kAcc])
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int G = (sc.n + kGroup - 1) / kGroup;
+    for (int g = wid; g < G; g += kLsThreads / 64) {
+        const int i = g * kGroup + lane;
+        bool in_step = false, in_cost = false;
+        double e = 0.0, gv[3] = { 0.0, 0.0, 0.0 };
+        if (i < sc.n) {
+            const double r = sc.ranges[i];
+            in_step = !(r >= smax || r <= smin);
+            in_cost = !(r >= cmax || r <= cmin);
+            if (in_step || in_cost) beam_terms(p, grid, pose, r, sc.angles[i], e, gv);
+        }
+        double t[kAcc];
+        beam_acc(in_step, in_cost, e, gv, t);
+        wave_total(t);
+        if (lane < kAcc) {
+            double v = t[0];
+#pragma unroll
+            for (int k = 1; k < kAcc; ++k) v = (lane == k) ? t[k] : v;
+            red[g * kAcc + lane] = v;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kAcc; ++k) {
+        double v = red[k];
+        for (int g = 1; g < G; ++g) v = v + red[g * kAcc + k];
+        acc[k] = v;
+    }
+    __syncthreads();
+}
+
 // One workgroup per scan: the whole OptimizePose loop (:48-69) + covariance.
 __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double* __restrict__ grid,
                                                          const LsScanRef* __restrict__ scans,
                                                          LsRecord* __restrict__ out,
                                                          double* __restrict__ traj)
 {
-    __shared__ double red[kAcc * (kLsThreads / 64)];
+    __shared__ double red[kMaxGroups * kAcc];
     __shared__ double spose[3];
     const LsScanRef sc = scans[blockIdx.x];
     const double smin = fmax(p.step_min, sc.min_range), smax = fmin(p.step_max, sc.max_range);
@@ -417,8 +515,7 @@ __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double*
     double pose[3] = { sc.pose0[0], sc.pose0[1], sc.pose0[2] };
     double prevCost = DBL_MAX, cost = DBL_MAX;
     double acc[kAcc];
-    pass(p, grid, sc, pose, smin, smax, cmin, cmax, acc);
-    wg_sum(acc, red);
+    group_pass(p, grid, sc, pose, smin, smax, cmin, cmax, red, acc);
     int it = 0;
     for (;;) {
         // OptimizeStep (:88-148): regularised normal equations, col-piv QR, pose += delta
@@ -439,15 +536,14 @@ __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double*
         pose[2] = spose[2];
         // cost at the new pose (and the next step's sums, and the covariance
         // gradient should the loop stop here)
-        pass(p, grid, sc, pose, smin, smax, cmin, cmax, acc);
-        wg_sum(acc, red);
+        group_pass(p, grid, sc, pose, smin, smax, cmin, cmax, red, acc);
         cost = acc[9];
         if (traj && threadIdx.x == 0) {
-            double* t = traj + ((size_t)blockIdx.x * max(1, p.max_iter) + it) * 4;
-            t[0] = pose[0];
-            t[1] = pose[1];
-            t[2] = pose[2];
-            t[3] = cost;
+            double* tr = traj + ((size_t)blockIdx.x * max(1, p.max_iter) + it) * 4;
+            tr[0] = pose[0];
+            tr[1] = pose[1];
+            tr[2] = pose[2];
+            tr[3] = cost;
         }
         if (++it >= p.max_iter || fabs(prevCost - cost) < p.conv) break;
         prevCost = cost;
@@ -468,157 +564,264 @@ __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double*
 }
 
 // --------------------------------------------------------------------------
-// Split refine (a lone OptimizePose): k_linsolve's 8 waves become 8 one-wave
-// workgroups on 8 CUs (the single workgroup is bound by one CU's gather
-// issue: ~80 gathers per beam).  Workgroup j takes exactly wave j's beams
-// (j * 64 + lane + k * 512), accumulates them in the same per-lane order and
-// reduces them with the same butterfly, and the 8 partials are added in wave
-// order like wg_sum: a split refine is bit-identical to the same refine in
-// one workgroup or in a batch (a chunk-per-workgroup order measured 0.54 ms
-// but moves the 50-iteration config-3 end points, which jitter on the
-// reference's truncation edges, past 1e-5 on 2 of 24 seeds).
-// Per pass every workgroup publishes its 13 partials as 26 write-through
-// 8-byte granules {tag = pass + 1, 32 bits of a double}
-// (cdna_hip_programming.md, publish/consume recipe R2: the data is the flag,
-// agent-scope relaxed atomics, no fence); every workgroup sweeps all 8 x 26
-// granules until every tag matches, adds the partials and runs the 3x3 solve
-// itself, so every workgroup holds the identical pose and takes the identical
-// stopping decision -- no broadcast, no second hand-off per pass.  Granules
-// are double-buffered by pass parity: a workgroup writes pass p + 2 only
-// after every workgroup has published p + 1, i.e. finished reading pass p.
-// Spins are bounded (~0.2 s of s_memrealtime): on time-out the timeout word
-// is set, every workgroup leaves, and the host reports an error.
+// Split refine (a lone OptimizePose, the frontend's case).  One workgroup of
+// 8 waves per group of 64 beams (17 workgroups on 17 CUs for 1081 beams; with
+// more than kSplitMaxWG groups a workgroup takes groups wg, wg + nwg, ...).
+// The waves share the work of a beam (lane = beam): waves 0-5 compute the
+// hit cell and one bicubic axis each (x0, y0, xp, xm, yp, ym; through LDS),
+// waves 0-4 one smoothed value each, then waves 0-3 finish the beam (the same
+// bits in each), and each sums a quarter of the 13 group sums with the
+// butterfly and publishes them -- the same functions on the same inputs as
+// beam_terms, so the bits are the batch kernel's.  Measured per pass on
+// config 3 (LGS_LS_TRACE): hit cell + axes 1.45 us, smoothed values 1.1 us,
+// finish + sums + publish 1.5 -> (8 waves) less, hand-off 1.5-3.5 us after
+// the last publisher, 3x3 col-piv QR 1.65 us.
+// Per pass every group total is published as 26 write-through 8-byte granules
+// {tag = pass + 1, 32 bits of a double} (cdna_hip_programming.md,
+// publish/consume recipe R2: the data is the flag, agent-scope relaxed
+// atomics, no fence); wave 0 of every workgroup sweeps all G x 26 granules
+// until every tag matches, adds the totals in group order and runs the 3x3
+// solve itself, so every workgroup holds the identical pose and takes the
+// identical stopping decision (no broadcast, no second hand-off per pass).
+// Granules are double-buffered by pass parity: a workgroup publishes pass
+// p + 2 only after every workgroup has published p + 1, i.e. finished reading
+// pass p.  Spins are bounded (~0.2 s of s_memrealtime): on time-out the
+// timeout word is set, every workgroup leaves, and the host reports an error.
 // --------------------------------------------------------------------------
-constexpr int kSplitWG = kLsThreads / 64;
-constexpr int kGran = 2 * kAcc;   // granules per workgroup and pass
+constexpr int kSplitThreads = 512;
+constexpr int kSplitMaxWG = 64;
+constexpr int kSplitMaxGroups = 128;     // larger scans use one workgroup (k_linsolve)
+constexpr int kGran = 2 * kAcc;          // granules per group and pass
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
-__device__ __forceinline__ bool split_exchange(gu64* __restrict__ gran, gu32* __restrict__ tmo, int pass_idx,
-                                               double (&acc)[kAcc], unsigned* __restrict__ lds)
+struct SplitLds {
+    Axis ax[6][kGroup];                  // x0, y0, xp, xm, yp, ym
+    double sv[5][kGroup];                // S(x0,y0), S(xp,y0), S(xm,y0), S(x0,yp), S(x0,ym)
+    double sc[2][kGroup];                // sin, cos of the beam angle
+    double br[kSplitMaxGroups / kSplitMaxWG][kGroup];   // the workgroup's ranges and angles, loaded once
+    double ba[kSplitMaxGroups / kSplitMaxWG][kGroup];
+    unsigned gran[kSplitMaxGroups * kGran];
+    double tot[kAcc];
+    double pose[3];
+    int stop;
+};
+
+// wave 0: wait for every group's granules of this pass, then the totals in
+// group order (every lane)
+__device__ __forceinline__ bool consume(gu64* __restrict__ slot, gu32* __restrict__ tmo, int G, unsigned epoch,
+                                        unsigned* __restrict__ lds, double (&acc)[kAcc])
 {
     const int lane = threadIdx.x;
-    const unsigned epoch = (unsigned)pass_idx + 1u;
-    gu64* slot = gran + (size_t)(pass_idx & 1) * kSplitWG * kGran;
-    // wave totals (every lane: wg_sum's butterfly), then lane g < 26
-    // publishes half g & 1 of sum g >> 1
-#pragma unroll
-    for (int k = 0; k < kAcc; ++k)
-        for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off, 64);
-    double mine = acc[0];
-#pragma unroll
-    for (int k = 1; k < kAcc; ++k) mine = ((lane >> 1) == k) ? acc[k] : mine;
-    const unsigned long long bits = (unsigned long long)__double_as_longlong(mine);
-    const unsigned half = (lane & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
-    if (lane < kGran)
-        __hip_atomic_store(slot + (size_t)blockIdx.x * kGran + lane, ((unsigned long long)epoch << 32) | half,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // sweep every workgroup's granules of this pass until all tags match
-    constexpr int total = kSplitWG * kGran;
+    const int total = G * kGran;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
+    for (unsigned polls = 1;; ++polls) {
+        // every load of a sweep chunk in flight before the first is waited on
+        // (a strided loop waits on each load in turn: 7 round trips per poll)
         bool ok = true;
-        for (int g = lane; g < total; g += 64) {
-            const unsigned long long x = __hip_atomic_load(slot + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            lds[g] = (unsigned)x;
-            ok &= (unsigned)(x >> 32) == epoch;
+        for (int base = 0; base < total; base += 64 * 8) {
+            unsigned long long x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = base + u * 64 + lane;
+                x[u] = (q < total) ? __hip_atomic_load(slot + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : ((unsigned long long)epoch << 32);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = base + u * 64 + lane;
+                if (q < total) lds[q] = (unsigned)x[u];
+                ok &= (unsigned)(x[u] >> 32) == epoch;
+            }
         }
         if (__all(ok)) break;
-        if (__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // 100 MHz clock: 0.2 s
-            if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
+        // the timeout word is one more round trip: looked at every 256 polls only
+        if ((polls & 255u) == 0u) {
+            if (__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // 100 MHz clock: 0.2 s
+                if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
         }
-        __builtin_amdgcn_s_sleep(1);
     }
-    __syncthreads();   // (one wave) the granule values in LDS
-    // lane k < 13: partial k of the workgroups in wave order (wg_sum's), then broadcast
+    __builtin_amdgcn_wave_barrier();
     double sk = 0.0;
     if (lane < kAcc)
-        for (int j = 0; j < kSplitWG; ++j) {
-            const unsigned lo = lds[j * kGran + 2 * lane], hi = lds[j * kGran + 2 * lane + 1];
+        for (int g = 0; g < G; ++g) {
+            const unsigned lo = lds[g * kGran + 2 * lane], hi = lds[g * kGran + 2 * lane + 1];
             const double v = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-            sk = (j == 0) ? v : sk + v;
+            sk = (g == 0) ? v : sk + v;
         }
 #pragma unroll
     for (int k = 0; k < kAcc; ++k) acc[k] = __shfl(sk, k, 64);
-    __syncthreads();   // LDS free for the next pass
     return true;
 }
 
-// pass() of one wave: beams blockIdx.x * 64 + lane, + kLsThreads, ...
-// (computing two of a lane's beams together measured slower: 0.91 -> 1.18 ms,
-// 256 VGPRs at one wave per SIMD)
-__device__ __forceinline__ void wave_pass(const LsPlan& p, const double* __restrict__ grid, const LsScanRef& sc,
-                                          const double pose[3], double smin, double smax, double cmin, double cmax,
-                                          double (&acc)[kAcc])
+// the workgroup's groups of one pass; wave 0 publishes each group's totals
+// diagnostics (env LGS_LS_TRACE=1): workgroup 0 stamps s_memrealtime at the
+// phase boundaries of every pass
+__device__ __forceinline__ void stamp(unsigned long long* tr, int k)
 {
+    if (tr && blockIdx.x == 0 && threadIdx.x == 0) tr[k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// wave w of the 4 finishing waves: sums kSumLo[w] .. kSumLo[w + 1] - 1
+__device__ __forceinline__ int sum_lo(int w) { return (w * kAcc + 3) / 4; }   // 0, 4, 7, 10, 13
+
+__device__ __forceinline__ void split_pass(const LsPlan& p, const double* __restrict__ grid, const LsScanRef& sc,
+                                           const double pose[3], double smin, double smax, double cmin, double cmax,
+                                           int G, gu64* __restrict__ slot, unsigned epoch, SplitLds& L,
+                                           unsigned long long* tr, unsigned long long* tr2)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int g = blockIdx.x, k = 0; g < G; g += gridDim.x, ++k) {
+        const int i = g * kGroup + lane;
+        bool in_step = false, in_cost = false;
+        double r = 0.0, sn = 0.0, cs = 0.0, fx = 0.0, fy = 0.0;
+        if (i < sc.n) {
+            r = L.br[k][lane];
+            in_step = !(r >= smax || r <= smin);
+            in_cost = !(r >= cmax || r <= cmin);
+        }
+        const bool act = in_step || in_cost;
+        // phase A: the hit cell (every wave), one axis per wave 0..5
+        if (act && wid < 6) {
+            beam_cell(p, pose, r, L.ba[k][lane], sn, cs, fx, fy);
+            const double d = kHalfDelta;
+            const bool isx = !(wid & 1);
+            const double v = (wid < 2) ? (isx ? fx : fy) : (wid < 4) ? (fx + ((wid == 2) ? d : -d))
+                                                                     : (fy + ((wid == 4) ? d : -d));
+            // ax order: x0, y0, xp, xm, yp, ym
+            L.ax[wid][lane] = make_axis(v, (wid == 0 || wid == 2 || wid == 3) ? p.W : p.H);
+            if (wid == 0) {
+                L.sc[0][lane] = sn;
+                L.sc[1][lane] = cs;
+            }
+        }
+        __syncthreads();
+        stamp(tr, 1);
+        // phase B: one smoothed value per wave 0..4
+        if (act && wid < 5) {
+            const int xa = (wid == 1) ? 2 : (wid == 2) ? 3 : 0;
+            const int ya = (wid == 3) ? 4 : (wid == 4) ? 5 : 1;
+            L.sv[wid][lane] = smoothed(grid, p.W, L.ax[xa][lane], L.ax[ya][lane]);
+        }
+        __syncthreads();
+        stamp(tr, 2);
+        // phase C: waves 0..3 finish the beam (identical bits in each), sum
+        // their share of the 13 sums over the group and publish it
+        if (wid < 4) {
+            double e = 0.0, gv[3] = { 0.0, 0.0, 0.0 };
+            if (act)
+                beam_finish(p, r, L.sc[0][lane], L.sc[1][lane], L.sv[0][lane], L.sv[1][lane], L.sv[2][lane],
+                            L.sv[3][lane], L.sv[4][lane], e, gv);
+            double t[kAcc];
+            beam_acc(in_step, in_cost, e, gv, t);
+            const int lo = sum_lo(wid), hi = sum_lo(wid + 1);
 #pragma unroll
-    for (int k = 0; k < kAcc; ++k) acc[k] = 0.0;
-    for (int i = blockIdx.x * 64 + threadIdx.x; i < sc.n; i += kLsThreads) {
-        const double r = sc.ranges[i];
-        const bool in_step = !(r >= smax || r <= smin);
-        const bool in_cost = !(r >= cmax || r <= cmin);
-        if (!in_step && !in_cost) continue;
-        double e, gv[3];
-        beam_terms(p, grid, pose, r, sc.angles[i], e, gv);
-        if (in_step) {
-            acc[0] += e * gv[0];
-            acc[1] += e * gv[1];
-            acc[2] += e * gv[2];
-            acc[3] += gv[0] * gv[0];
-            acc[4] += gv[0] * gv[1];
-            acc[5] += gv[0] * gv[2];
-            acc[6] += gv[1] * gv[1];
-            acc[7] += gv[1] * gv[2];
-            acc[8] += gv[2] * gv[2];
+            for (int k = 0; k < kAcc; ++k)
+                if (k >= lo && k < hi)
+                    for (int off = 32; off > 0; off >>= 1) t[k] += __shfl_xor(t[k], off, 64);
+            // lane j < 2 (hi - lo) publishes half j & 1 of sum lo + (j >> 1)
+            if (lane == 0)
+#pragma unroll
+                for (int k = 0; k < kAcc; ++k)
+                    if (k >= lo && k < hi) L.tot[k] = t[k];
+            __builtin_amdgcn_wave_barrier();
+            const int nk = 2 * (hi - lo);
+            if (lane < nk) {
+                const double mine = L.tot[lo + (lane >> 1)];
+                const unsigned long long bits = (unsigned long long)__double_as_longlong(mine);
+                const unsigned half = (lane & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
+                __hip_atomic_store(slot + (size_t)g * kGran + 2 * lo + lane, ((unsigned long long)epoch << 32) | half,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            stamp(tr, 3);
+            if (tr2 && threadIdx.x == 0) tr2[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
         }
-        if (in_cost) {
-            acc[9] += e * e;
-            acc[10] += 2.0 * e * (-gv[0]);
-            acc[11] += 2.0 * e * (-gv[1]);
-            acc[12] += 2.0 * e * (-gv[2]);
-        }
+        __syncthreads();   // LDS axes / values free for the next group
     }
 }
 
-__global__ __launch_bounds__(64) void k_linsolve_split(LsPlan p, const double* __restrict__ grid, LsScanRef sc,
-                                                       LsRecord* __restrict__ out, double* __restrict__ traj,
-                                                       gu64* __restrict__ gran, gu32* __restrict__ tmo)
+__global__ __launch_bounds__(kSplitThreads) void k_linsolve_split(LsPlan p, const double* __restrict__ grid,
+                                                                  LsScanRef sc, LsRecord* __restrict__ out,
+                                                                  double* __restrict__ traj,
+                                                                  gu64* __restrict__ gran, gu32* __restrict__ tmo,
+                                                                  unsigned long long* __restrict__ trace)
 {
-    __shared__ unsigned lds[kSplitWG * kGran];
+    __shared__ SplitLds L;
+    const int wid = threadIdx.x >> 6;
     const double smin = fmax(p.step_min, sc.min_range), smax = fmin(p.step_max, sc.max_range);
     const double cmin = fmax(p.cost_min, sc.min_range), cmax = fmin(p.cost_max, sc.max_range);
+    const int G = (sc.n + kGroup - 1) / kGroup;
     double pose[3] = { sc.pose0[0], sc.pose0[1], sc.pose0[2] };
+    // the workgroup's beams stay in LDS for every pass
+    for (int g = blockIdx.x, k = 0; g < G; g += gridDim.x, ++k)
+        if (threadIdx.x < kGroup && g * kGroup + (int)threadIdx.x < sc.n) {
+            L.br[k][threadIdx.x] = sc.ranges[g * kGroup + threadIdx.x];
+            L.ba[k][threadIdx.x] = sc.angles[g * kGroup + threadIdx.x];
+        }
+    __syncthreads();
     double acc[kAcc];
     int pass_idx = 0;
-    wave_pass(p, grid, sc, pose, smin, smax, cmin, cmax, acc);
-    if (!split_exchange(gran, tmo, pass_idx++, acc, lds)) return;
     double prevCost = DBL_MAX, cost = DBL_MAX;
     int it = 0;
     for (;;) {
-        // OptimizeStep (:88-148), solved by every lane of every workgroup
-        const double H[9] = { acc[3] + p.reg_t, acc[4], acc[5],
-                              acc[4], acc[6] + p.reg_t, acc[7],
-                              acc[5], acc[7], acc[8] + p.reg_r };
-        const double b[3] = { acc[0], acc[1], acc[2] };
-        double d[3];
-        solve3_colpiv_qr(H, b, d);
-        pose[0] = pose[0] + d[0];
-        pose[1] = pose[1] + d[1];
-        pose[2] = pose[2] + d[2];
-        wave_pass(p, grid, sc, pose, smin, smax, cmin, cmax, acc);
-        if (!split_exchange(gran, tmo, pass_idx++, acc, lds)) return;
-        cost = acc[9];
-        if (traj && blockIdx.x == 0 && threadIdx.x == 0) {
-            double* t = traj + (size_t)it * 4;
-            t[0] = pose[0];
-            t[1] = pose[1];
-            t[2] = pose[2];
-            t[3] = cost;
+        gu64* slot = gran + (size_t)(pass_idx & 1) * kSplitMaxGroups * kGran;
+        const unsigned epoch = (unsigned)pass_idx + 1u;
+        unsigned long long* tr = trace ? trace + (size_t)min(pass_idx, 127) * 8 : nullptr;
+        unsigned long long* tr2 = trace ? trace + 128 * 8 + (size_t)min(pass_idx, 127) * 64 : nullptr;
+        stamp(tr, 0);
+        split_pass(p, grid, sc, pose, smin, smax, cmin, cmax, G, slot, epoch, L, tr, tr2);
+        if (wid == 0) {
+            int stop = 0;
+            const bool ok = consume(slot, tmo, G, epoch, L.gran, acc);
+            stamp(tr, 4);
+            if (!ok) {
+                stop = 2;
+            } else {
+                if (pass_idx > 0) {
+                    cost = acc[9];
+                    if (traj && blockIdx.x == 0 && threadIdx.x == 0) {
+                        double* tr = traj + (size_t)it * 4;
+                        tr[0] = pose[0];
+                        tr[1] = pose[1];
+                        tr[2] = pose[2];
+                        tr[3] = cost;
+                    }
+                    if (++it >= p.max_iter || fabs(prevCost - cost) < p.conv) stop = 1;
+                    prevCost = cost;
+                }
+                if (!stop) {
+                    // OptimizeStep (:88-148), solved by every lane of wave 0 of every workgroup
+                    const double H[9] = { acc[3] + p.reg_t, acc[4], acc[5],
+                                          acc[4], acc[6] + p.reg_t, acc[7],
+                                          acc[5], acc[7], acc[8] + p.reg_r };
+                    const double b[3] = { acc[0], acc[1], acc[2] };
+                    double d[3];
+                    solve3_colpiv_qr(H, b, d);
+                    pose[0] = pose[0] + d[0];
+                    pose[1] = pose[1] + d[1];
+                    pose[2] = pose[2] + d[2];
+                }
+            }
+            stamp(tr, 5);
+            if (threadIdx.x == 0) {
+                L.pose[0] = pose[0];
+                L.pose[1] = pose[1];
+                L.pose[2] = pose[2];
+                L.stop = stop;
+            }
         }
-        if (++it >= p.max_iter || fabs(prevCost - cost) < p.conv) break;
-        prevCost = cost;
+        __syncthreads();
+        const int stop = L.stop;
+        pose[0] = L.pose[0];
+        pose[1] = L.pose[1];
+        pose[2] = L.pose[2];
+        __syncthreads();
+        if (stop == 2) return;
+        if (stop) break;
+        ++pass_idx;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         LsRecord rec;
@@ -705,6 +908,7 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     std::vector<LsScanRef> refs(n);
     for (int j = 0; j < n; ++j) {
         LGS_REQUIRE(scans[j] && scans[j]->n >= 1, "empty scan");
+        LGS_REQUIRE(scans[j]->n <= kMaxGroups * kGroup, "scan has more than 32768 beams");
         refs[j] = scan_ref(scans[j], init[j]);
     }
     // pinned staging: [refs | records | trajectory]
@@ -714,16 +918,25 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     std::memcpy(h, refs.data(), b_refs);
     char* d = (char*)ctx->ensure(S_LIN0, b_refs + b_rec + b_traj);
     LGS_HIP_CHECK(hipMemcpyAsync(d, h, b_refs, hipMemcpyHostToDevice, ctx->stream));
-    const bool split = n == 1 && ctx->linsolve_split;
-    constexpr size_t b_gran = sizeof(unsigned long long) * 2 * kSplitWG * kGran;   // multiple of 16
+    const int groups = (refs[0].n + kGroup - 1) / kGroup;
+    const bool split = n == 1 && ctx->linsolve_split && groups <= kSplitMaxGroups;
+    const int split_wg = std::min(groups, kSplitMaxWG);
+    constexpr size_t b_gran = sizeof(unsigned long long) * 2 * kSplitMaxGroups * kGran;   // multiple of 16
     char* hs = split ? (char*)ctx->ensure(S_LIN2, b_gran + 16) : nullptr;
     if (split)   // granule tags and the timeout word zeroed every call (one block from the start)
         LGS_HIP_CHECK(hipMemsetAsync(hs, 0, b_gran + 16, ctx->stream));
+    // diagnostics: LGS_LS_TRACE=1 prints the split refine's phase stamps
+    static const bool trace_on = getenv("LGS_LS_TRACE") != nullptr;
+    unsigned long long* trace_dev = nullptr;
+    if (split && trace_on) {
+        trace_dev = (unsigned long long*)ctx->ensure(S_LIN3, 128 * 72 * sizeof(unsigned long long));
+        LGS_HIP_CHECK(hipMemsetAsync(trace_dev, 0, 128 * 72 * sizeof(unsigned long long), ctx->stream));
+    }
     const int tok = ctx->timing_begin(K_LINSOLVE, 0.0);
     if (split)
-        hipLaunchKernelGGL(k_linsolve_split, dim3(kSplitWG), dim3(64), 0, ctx->stream, p, grid->d, refs[0],
+        hipLaunchKernelGGL(k_linsolve_split, dim3(split_wg), dim3(kSplitThreads), 0, ctx->stream, p, grid->d, refs[0],
                            (LsRecord*)(d + b_refs), traj ? (double*)(d + b_refs + b_rec) : nullptr, (gu64*)hs,
-                           (gu32*)(hs + b_gran));
+                           (gu32*)(hs + b_gran), trace_dev);
     else
         hipLaunchKernelGGL(k_linsolve, dim3(n), dim3(kLsThreads), 0, ctx->stream, p, grid->d,
                            (const LsScanRef*)d, (LsRecord*)(d + b_refs),
@@ -737,6 +950,22 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     ctx->sync();
     if (ctx->profile) ctx->harvest();
     if (split && *htmo != 0u) throw Error(LGS_ERR_INTERNAL, "split refine: in-launch hand-off timed out");
+    if (trace_dev) {
+        std::vector<unsigned long long> t(128 * 72);
+        LGS_HIP_CHECK(hipMemcpy(t.data(), trace_dev, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost));
+        for (int q = 0; q < 128 && t[q * 8]; ++q) {
+            fprintf(stderr, "LSTRACE pass %d:", q);
+            for (int k = 1; k < 6; ++k)
+                fprintf(stderr, " %.2f", t[q * 8 + k] ? 0.01 * (double)(t[q * 8 + k] - t[q * 8]) : -1.0);
+            if (q + 1 < 128 && t[(q + 1) * 8]) fprintf(stderr, " | next %.2f", 0.01 * (double)(t[(q + 1) * 8] - t[q * 8]));
+            fprintf(stderr, " | pub");
+            for (int w = 0; w < split_wg; ++w) {
+                const unsigned long long v = t[128 * 8 + q * 64 + w];
+                fprintf(stderr, " %.2f", v ? 0.01 * ((double)v - (double)t[q * 8]) : -1.0);
+            }
+            fprintf(stderr, "\n");
+        }
+    }
     const LsRecord* rec = (const LsRecord*)(h + b_refs);
     for (int j = 0; j < n; ++j) {
         lgs_linsolve_summary& o = out[j];

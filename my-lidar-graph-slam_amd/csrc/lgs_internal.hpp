@@ -67,6 +67,7 @@ enum Slot {
     S_LS0, S_LS1,
     S_LIN0, S_LIN1,   // K4 staging
     S_LIN2,           // K4 split refine: hand-off granules + timeout word
+    S_LIN3,           // K4 split refine: phase stamps (LGS_LS_TRACE diagnostics)
     S_SUPER,        // double: superblock planes (forward kSB x kSB max of S_DECIM)
     S_SBOUND,       // double [T * nsb2] superblock bounds
     S_UPLOAD,       // per-batch descriptors (MatchItem, PlaneJob, PrecompJob), one H2D copy
