@@ -675,17 +675,21 @@ __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __re
 // every superblock.  NaN cells are skipped by the max: a block whose sum is
 // NaN fails c > thr and is never selected anyway.
 // k_super_planes: one workgroup per (tile of kSPX padded columns x kSPY
-// padded rows, plane, set).
+// padded rows, plane, set).  A tile spans a config-2 plane's whole width
+// (Wqp = 240; 224-column tiles left a second tile per row with 16 columns).
 //  1. vertical 4-max in registers: a thread owns one footprint column
-//     (kSPX + 3 <= 256), loads its kSPY + 3 values (0 past the plane) at once
-//     and writes kSPY window maxima to LDS;
-//  2. horizontal 4-max from LDS, rounded toward +inf to fp16 (round-up is
-//     monotone, so rounding the max = max of the rounded), 8 consecutive
-//     superblocks of one sub-phase row per thread, one 16-byte store (Wq4 is a
-//     multiple of 8, so sub-phase rows are 16-byte aligned).
-constexpr int kSPX = 224, kSPY = 16;   // kSPX = 4 sub-phases x 56 (7 stores of 8)
+//     (kSPX + 3 <= kSPThreads), loads its kSPY + 3 values (0 past the plane)
+//     at once and writes the kSPY window maxima, already rounded toward +inf
+//     to fp16, to LDS (round-up is monotone: the max of the rounded values is
+//     the rounded max, so rounding before the horizontal max changes nothing
+//     and quarters the LDS);
+//  2. horizontal 4-max of the fp16 values from LDS, 8 consecutive superblocks
+//     of one sub-phase row per thread, one 16-byte store (Wq4 is a multiple of
+//     8, so sub-phase rows are 16-byte aligned).
+constexpr int kSPX = 256, kSPY = 32;   // kSPX = 4 sub-phases x 64 (8 stores of 8)
+constexpr int kSPThreads = 320;        // >= kSPX + kSB - 1 column loaders
 
-__global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
+__global__ __launch_bounds__(kSPThreads) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
 {
     const Blk wg = xcd_block();
     const PlaneJob& job = jobs[wg.z / nplanes];
@@ -697,7 +701,8 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
     const int pgen = job.pgen;
     const int Wqp = pl.Wqp, Hqp = pl.Hqp;
     constexpr int TW = kSPX + kSB - 1, TH = kSPY + kSB - 1;
-    __shared__ double vm[kSPY][TW];
+    static_assert(TW <= kSPThreads, "one loader per footprint column");
+    __shared__ SuperT vm[kSPY][TW + 1];
     const int x0 = wg.x * kSPX, y0 = wg.y * kSPY;
     SuperT* __restrict__ out = S + plane * pl.pstride4;
     const int tid = threadIdx.x;
@@ -731,21 +736,24 @@ __global__ __launch_bounds__(256) void k_super_planes(const PlaneJob* __restrict
             double m = v[r];
 #pragma unroll
             for (int i = 1; i < kSB; ++i) m = dmax2(m, v[r + i]);
-            vm[r][tid] = m;
+            vm[r][tid] = super_round_up(m);
         }
     }
     __syncthreads();
-    // horizontal 4-max, lane = padded column (conflict-free LDS reads), rounded
-    // up to fp16 and stored sub-phase-major: hs[r][sx][X4] = S at column 4 X4 + sx
+    // horizontal 4-max of the rounded values, lane = padded column, stored
+    // sub-phase-major: hs[r][sx][X4] = S at column 4 X4 + sx
     constexpr int kQ = kSPX / 4;
     __shared__ __attribute__((aligned(16))) SuperT hs[kSPY][4][kQ];
     if (tid < kSPX) {
 #pragma unroll
         for (int r = 0; r < kSPY; ++r) {
-            double m = vm[r][tid];
+            float m = (float)vm[r][tid];
 #pragma unroll
-            for (int j = 1; j < kSB; ++j) m = dmax2(m, vm[r][tid + j]);
-            hs[r][tid & 3][tid >> 2] = super_round_up(m);
+            for (int j = 1; j < kSB; ++j) {
+                const float c = (float)vm[r][tid + j];
+                m = (m < c) ? c : m;   // dmax2 on the fp16 values (exact in float)
+            }
+            hs[r][tid & 3][tid >> 2] = (SuperT)m;
         }
     }
     __syncthreads();
@@ -2670,7 +2678,7 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
         dim3 g((lp.Wqp + kSPX - 1) / kSPX, (lp.Hqp + kSPY - 1) / kSPY, np * (int)sj.npj);
         const int tok = ctx->timing_begin(K_SUPER_PLANES, 8.0 * 2.0 * (double)np * lp.pstride * sj.npj);
         if (!ctx->skipped(K_SUPER_PLANES))
-            hipLaunchKernelGGL(k_super_planes, g, dim3(256), 0, ctx->stream, up.at<PlaneJob>(sj.pj_off), np);
+            hipLaunchKernelGGL(k_super_planes, g, dim3(kSPThreads), 0, ctx->stream, up.at<PlaneJob>(sj.pj_off), np);
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
     }
