@@ -259,7 +259,13 @@ __device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
 // cells >= 1 mm that is < 1e-11 cells, far inside the 1e-9-cell guard, so
 // every projection whose glibc floor could differ is still guarded and
 // re-checked on the host.
-constexpr int kProjRows = 8;
+#ifndef LGS_PROJ_ROWS
+#define LGS_PROJ_ROWS 16
+#endif
+#ifndef LGS_PROJ_INV
+#define LGS_PROJ_INV 1
+#endif
+constexpr int kProjRows = LGS_PROJ_ROWS;
 __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, double guard_eps, int inject)
 {
     const Blk wg = xcd_block();
@@ -321,6 +327,7 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     double sa, ca;
     sincos(a, &sa, &ca);
     const int tt1 = min(pl.T, (wg.y + 1) * kProjRows);
+    const double inv_res = 1.0 / pl.res;
     for (int tt = wg.y * kProjRows; tt < tt1; ++tt) {
     // HitPoint: cos(sensorPose.mTheta + scanAngle) (H/sensor/sensor_data.hpp:168-172),
     // by rotation (see kProjRows)
@@ -329,8 +336,16 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     const double s = s_st[kr] * ca + s_ct[kr] * sa;
     const double hx = pl.sx + r * c;
     const double hy = pl.sy + r * s;
+#if LGS_PROJ_INV
+    // x / res as x * (1 / res): differs from the quotient by a few ulps, far
+    // inside the guard (eps + |q| 1e-13), so every cell whose floor could
+    // differ from the reference's division is still re-checked on the host
+    const double qx = (hx - pl.min_x) * inv_res;
+    const double qy = (hy - pl.min_y) * inv_res;
+#else
     const double qx = (hx - pl.min_x) / pl.res;
     const double qy = (hy - pl.min_y) / pl.res;
+#endif
     int ix = (int)floor(qx);
     int iy = (int)floor(qy);
     const bool guarded = near_boundary(qx, guard_eps) || near_boundary(qy, guard_eps);
@@ -686,8 +701,14 @@ __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __re
 //  2. horizontal 4-max of the fp16 values from LDS, 8 consecutive superblocks
 //     of one sub-phase row per thread, one 16-byte store (Wq4 is a multiple of
 //     8, so sub-phase rows are 16-byte aligned).
-constexpr int kSPX = 256, kSPY = 32;   // kSPX = 4 sub-phases x 64 (8 stores of 8)
-constexpr int kSPThreads = 320;        // >= kSPX + kSB - 1 column loaders
+#ifndef LGS_SPY
+#define LGS_SPY 16
+#endif
+#ifndef LGS_SPX
+#define LGS_SPX 256
+#endif
+constexpr int kSPX = LGS_SPX, kSPY = LGS_SPY;   // kSPX = 4 sub-phases x 64 (8 stores of 8)
+constexpr int kSPThreads = (kSPX + 3 + 63) / 64 * 64;   // >= kSPX + kSB - 1 column loaders
 
 __global__ __launch_bounds__(kSPThreads) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
 {

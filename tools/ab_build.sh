@@ -4,13 +4,13 @@
 set -e
 cd "$(dirname "$0")/../my-lidar-graph-slam_amd/csrc"
 name=$1; shift
-OUT=../../tools/exp/ab_$name
+OUT=../../ablib/ab_$name
 mkdir -p $OUT
 FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -fno-fast-math -fno-gpu-rdc -I../../include -I. $*"
 for f in lgs_core k_rtcsm k_raycast k_linsolve k_bb; do
   /opt/rocm/bin/hipcc $FLAGS -c -o $OUT/$f.o $f.hip &
 done
 wait
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/exp/ab_$name.so $OUT/*.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../ablib/ab_$name.so $OUT/*.o
 rm -rf $OUT
-echo built tools/exp/ab_$name.so
+echo built ablib/ab_$name.so
