@@ -210,6 +210,12 @@ __device__ __forceinline__ int super_base(int ix, int iy, const RtcsmPlan& pl)
     const bool touches = (qx0 < pl.Wq) & (qx0 + pl.ncx > (rx > 0 ? -1 : 0)) & (qy0 < pl.Hq) &
                          (qy0 + pl.ncy > (ry > 0 ? -1 : 0));
     const int Qx = qx0 + pl.M, Qy = qy0 + pl.M;
+    if (pl.oct) {
+        const int Yr = Qy >> 2;
+        return touches ? (int)((((ry * lr + rx) * pl.pstrideO + ((Qy & 3) * 4 + (Qx & 3)) * pl.subO +
+                                 (long long)(Yr >> 2) * pl.Wq4 + (Qx >> 2)) << 2) | (Yr & 3))
+                       : 0;
+    }
     return touches ? (int)((ry * lr + rx) * pl.pstride4 + ((Qy & 3) * 4 + (Qx & 3)) * pl.sub4 +
                            (long long)(Qy >> 2) * pl.Wq4 + (Qx >> 2))
                    : 0;
@@ -778,11 +784,34 @@ __global__ __launch_bounds__(kSPThreads) void k_super_planes(const PlaneJob* __r
         }
     }
     __syncthreads();
+    const int q0 = x0 >> 2;   // the tile's first superblock column (x0 is a multiple of 4)
+    if (pl.oct) {
+        // octet layout: the tile is one quad (sub-phase rows 4 qt .. 4 qt + 3,
+        // kSPY = 16 padded rows) of every sub-phase array; its 4 rows at column
+        // X are the low half of unit (qt, X) and the high half of (qt - 1, X)
+        static_assert(kSPY == 16, "one quad of sub-phase rows per tile");
+        const int qt = y0 >> 4;
+        typedef unsigned long long u64;
+        u64* __restrict__ uo = (u64*)(S + 8 * plane * pl.pstrideO);
+        for (int k = tid; k < 16 * kQ; k += blockDim.x) {   // (sub-phase, column), column fastest
+            const int sp = k / kQ, X = k % kQ;
+            const int cy = sp >> 2, sx = sp & 3, Xg = q0 + X;
+            if (Xg >= pl.Wq4) continue;
+            u64 v = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                v |= (u64)__builtin_bit_cast(unsigned short, hs[4 * i + cy][sx][X]) << (16 * i);
+            const long long u = sp * pl.subO + (long long)qt * pl.Wq4 + Xg;
+            uo[2 * u] = v;
+            if (qt > 0) uo[2 * (u - pl.Wq4) + 1] = v;
+        }
+        if (neg) *negflag = pgen;
+        return;
+    }
     // one 16-byte store of 8 consecutive superblocks of a sub-phase row per
     // task (row, sub-phase, chunk), chunk fastest
     constexpr int kChunks = kQ / 8;
     typedef SuperT s8 __attribute__((ext_vector_type(8)));
-    const int q0 = x0 >> 2;   // the tile's first superblock column (x0 is a multiple of 4)
     for (int k = tid; k < kSPY * 4 * kChunks; k += blockDim.x) {
         const int r = k / (4 * kChunks), rem = k % (4 * kChunks);
         const int sx = rem / kChunks, ch = rem % kChunks;
@@ -1043,6 +1072,101 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_hex(Items items, const
         const int a = sbi % nsbx, bb = sbi / nsbx;
         const int k = 4 * (bb * np + (a >> 2)) + (a & 3);
         for (int j = 0; j < kSupWaves; ++j) tot += red[j][k];
+    }
+    const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult;
+    if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
+    const bool seedable = own;   // k_seed_super skips unsafe members
+    double bv = seedable ? bound : -INFINITY;
+    long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(bv, off, 64);
+        const long long ok = __shfl_xor(bk, off, 64);
+        if (better(ov, ok, bv, bk)) {
+            bv = ov;
+            bk = ok;
+        }
+    }
+    if (lane == 0) {
+        it.part_c[t] = bv;
+        it.part_k[t] = bk;
+    }
+}
+
+// k_super_oct (octet layout, nsbx, nsby <= 5): lane = (beam slot, window
+// column a); one aligned 16-byte load per (beam, column) brings the column's 8
+// sub-phase rows 4q .. 4q + 7, of which rows k .. k + 4 (k = the window's
+// first row & 3) are the beam's 5 superblock rows -- a beam touches its 5
+// columns' 80 contiguous bytes (1-2 cache lines) instead of 5 rows' lines.
+// 64 / nsbx beams per wave instruction (12 for the config-2 window).  Slot
+// partials meet in LDS; the bound is the any-order sum (the rounding slack
+// sb_mult covers any order).
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+constexpr int kOctPipe = 8;
+__device__ __forceinline__ double h16(unsigned long long bits)
+{
+    return (double)__builtin_bit_cast(SuperT, (unsigned short)(bits & 0xFFFFu));
+}
+__global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const double* __restrict__ zero)
+{
+    const Blk wg = xcd_block();
+    const MatchItem& it = items[wg.z];
+    const RtcsmPlan& pl = it.pl;
+    if (wg.y >= pl.T) return;   // past this item's angles (uniform)
+    const u64x2* __restrict__ units = (const u64x2*)it.super;
+    const u64x2* __restrict__ z2 = (const u64x2*)zero;
+    extern __shared__ int srow[];   // [Nv]
+    __shared__ double part[kSupWaves][64][5];
+    const int t = wg.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nsbx = pl.nsbx, nsb2 = nsbx * pl.nsby;
+    const int nb = 64 / nsbx;               // beam slots per wave instruction
+    const int q = lane / nsbx, a = lane - nsbx * q;
+    const bool act = q < nb;
+    const int* __restrict__ cbrow = it.cbase + pl.sb_off + (size_t)t * pl.Nv;
+    stage_lds(srow, cbrow, pl.Nv);
+    __syncthreads();
+    const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
+    const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
+    const int* row = srow + lo;
+    const int nq = (cnt + nb - 1) / nb;     // slot q takes beams nb i + q
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
+    for (int i0 = 0; i0 < nq; i0 += kOctPipe) {
+        u64x2 x[kOctPipe];
+        int sh[kOctPipe];
+#pragma unroll
+        for (int j = 0; j < kOctPipe; ++j) {
+            const int v = nb * (i0 + j) + q;
+            const bool ok = act && v < cnt;
+            const int c = ok ? row[v] : 0;
+            sh[j] = 16 * (c & 3);
+            x[j] = *(ok ? units + ((c >> 2) + a) : z2);
+        }
+#pragma unroll
+        for (int j = 0; j < kOctPipe; ++j) {
+            const int k = sh[j];
+            const unsigned long long w0 = k ? ((x[j].x >> k) | (x[j].y << (64 - k))) : x[j].x;
+            const unsigned long long w1 = x[j].y >> k;
+            s0 += h16(w0);
+            s1 += h16(w0 >> 16);
+            s2 += h16(w0 >> 32);
+            s3 += h16(w0 >> 48);
+            s4 += h16(w1);
+        }
+    }
+    part[w][lane][0] = s0;
+    part[w][lane][1] = s1;
+    part[w][lane][2] = s2;
+    part[w][lane][3] = s3;
+    part[w][lane][4] = s4;
+    __syncthreads();
+    if (w != 0) return;
+    const int sbi = lane;
+    const bool own = sbi < nsb2;
+    double tot = 0.0;
+    if (own) {
+        const int ca = sbi % nsbx, rb = sbi / nsbx;
+        for (int j = 0; j < kSupWaves; ++j)
+            for (int s = 0; s < nb; ++s) tot += part[j][s * nsbx + ca][rb];
     }
     const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult;
     if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
@@ -2377,6 +2501,15 @@ void set_plane_layout(RtcsmPlan& pl)
     pl.pstride4 = 16 * pl.sub4;
     LGS_REQUIRE((long long)pl.low_res * pl.low_res * pl.pstride4 < (1LL << 31),
                 "coarse map too large for 32-bit plane offsets");
+#ifndef LGS_SUPER_OCT
+#define LGS_SUPER_OCT 1
+#endif
+    pl.oct = LGS_SUPER_OCT && pl.nsbx <= 5 && pl.nsby <= 5;
+    pl.Qo = (pl.Hq4 + 3) / 4 + 1;
+    pl.subO = (long long)pl.Qo * pl.Wq4;
+    pl.pstrideO = 16 * pl.subO;
+    LGS_REQUIRE(!pl.oct || (long long)pl.low_res * pl.low_res * pl.pstrideO < (1LL << 29),
+                "coarse map too large for 32-bit superblock unit offsets");
 }
 
 RtcsmPlan make_plan(const lgs_grid* grid, const lgs_rtcsm_params* p, const lgs_scan* scan,
@@ -2458,6 +2591,7 @@ struct BatchShape {
     bool pair = false;
     bool quad = false;      // k_super_quad (nsby * ceil(nsbx / 2) <= 16; chunks == 1)
     bool hex = false;       // k_super_hex (fp16 planes, nsby * ceil(nsbx / 4) <= 10; chunks == 1)
+    bool oct = false;       // k_super_oct (octet layout of the plan, nsbx, nsby <= 5; chunks == 1)
     bool planes = false;    // coarse map in padded phase planes
     bool pruned = false;    // superblock pruning
     bool lr5 = false;       // transposed LR = 5 evaluators
@@ -2556,6 +2690,7 @@ inline size_t plane_bytes(const RtcsmPlan& pl)
 }
 inline size_t super_bytes(const RtcsmPlan& pl)
 {
+    if (pl.oct) return align256(16 * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstrideO);
     return align256(sizeof(SuperT) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4 + 64);   // + slack: k_super_quad reads one float past a row
 }
 double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_super)
@@ -2799,7 +2934,9 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             const size_t lds = sizeof(int) * (size_t)std::max(B.NvMax, 1);
             dim3 g(B.chunks, B.Tmax, n);
             if (ctx->skipped(K_SUPER)) {
-            } else if (B.hex)
+            } else if (B.oct)
+                hipLaunchKernelGGL(k_super_oct, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+            else if (B.hex)
                 hipLaunchKernelGGL(k_super_hex, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else if (B.quad)
                 hipLaunchKernelGGL(k_super_quad, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
@@ -3139,6 +3276,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     B.chunks = B.pair ? 1 : (B.nsb2 + 63) / 64;
     B.quad = ctx->super_quad && p0.nsby * ((p0.nsbx + 1) / 2) <= 16;
     B.hex = ctx->super_hex && B.quad && p0.nsby * ((p0.nsbx + 3) / 4) <= 10;
+    B.oct = p0.oct != 0;
     B.planes = ctx->coarse_planes;
     B.pruned = uses_super(ctx, B.NvMax, B.nsb2, false);
     B.lr5 = lr5_path(B.NvMax, B.low_res);

@@ -134,6 +134,13 @@ struct RtcsmPlan {
     int Wq4, Hq4;
     long long sub4, pstride4;
     long long sb_off;           // superblock base offsets start at cbase + sb_off
+    // octet layout (windows of at most 5 x 5 superblocks):
+    // each sub-phase array is stored as 16-byte units (q, X) holding its rows
+    // 4q .. 4q + 7 at column X (every row twice), so a beam's 5 window rows at
+    // one column are one aligned 16-byte load; superblock bases are then
+    // (unit << 2) | (first row & 3)
+    int oct, Qo;
+    long long subO, pstrideO;   // units per sub-phase array / per plane
 };
 
 // Padded phase-plane geometry handed to the precompute kernel.

@@ -25,7 +25,11 @@ def layout(W, H, res, lr, rx, ry):
     Wqp = (Wq + 2 * M + 1) & ~1
     Hqp = Hq + 2 * M
     Wq4, Hq4 = ((-(-Wqp // 4)) + 7) & ~7, -(-Hqp // 4)
-    return dict(M=M, Wq=Wq, Hq=Hq, Wqp=Wqp, Hqp=Hqp, Wq4=Wq4, Hq4=Hq4, sub4=Wq4 * Hq4)
+    # octet layout (k_rtcsm.hip set_plane_layout) for windows of <= 5 x 5 superblocks
+    oct = nsbx <= 5 and nsby <= 5
+    Qo = (Hq4 + 3) // 4 + 1
+    return dict(M=M, Wq=Wq, Hq=Hq, Wqp=Wqp, Hqp=Hqp, Wq4=Wq4, Hq4=Hq4, sub4=Wq4 * Hq4, oct=oct, Qo=Qo,
+                subO=Qo * Wq4)
 
 
 def expected_planes(cells, lr, L):
@@ -68,7 +72,15 @@ def check_super(P, S, lr, L):
         got = np.zeros((Hqp, Wqp))
         for sy in range(4):
             for sx in range(4):
-                blk = S[p * pstride4 + (sy * 4 + sx) * L["sub4"]:][:L["sub4"]].reshape(L["Hq4"], L["Wq4"])
+                if L["oct"]:
+                    # units (q, X) of 8 halfs = rows 4q .. 4q + 7: rows from the low
+                    # halves, and every high half equals the next unit's low half
+                    o = (p * 16 + sy * 4 + sx) * L["subO"] * 8
+                    u = S[o:o + L["subO"] * 8].reshape(L["Qo"], L["Wq4"], 8)
+                    blk = u[:, :, :4].transpose(0, 2, 1).reshape(4 * L["Qo"], L["Wq4"])[:L["Hq4"]]
+                    assert np.array_equal(u[:-2, :, 4:], u[1:-1, :, :4]), (p, sy, sx)
+                else:
+                    blk = S[p * pstride4 + (sy * 4 + sx) * L["sub4"]:][:L["sub4"]].reshape(L["Hq4"], L["Wq4"])
                 ys, xs = np.arange(sy, Hqp, 4), np.arange(sx, Wqp, 4)
                 got[np.ix_(ys, xs)] = blk[:len(ys), :len(xs)].astype(np.float64)
         assert np.all(got >= m[p]), p
