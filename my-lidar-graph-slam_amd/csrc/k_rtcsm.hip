@@ -185,26 +185,59 @@ __device__ __forceinline__ bool near_boundary(double q, double eps)
 // --------------------------------------------------------------------------
 // k_project: idx[t][v] = WorldCoordinateToGridCellIndex(HitPoint(pose_t, beam))
 // --------------------------------------------------------------------------
-__device__ __forceinline__ int floor_div(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+// floor(a / b) and the remainder in [0, b) for a runtime divisor b > 0
+// (|a| < 2^30): one fp64 multiply by 1/b, floor and a +-1 correction -- exact,
+// and a fraction of the two branchy integer divisions it replaces (k_project
+// spent most of its VALU issue on those)
+__device__ __forceinline__ void floor_divmod(int a, int b, double inv_b, int& q, int& r)
+{
+    q = (int)floor((double)a * inv_b);
+    r = a - q * b;
+    if (r < 0) {
+        --q;
+        r += b;
+    } else if (r >= b) {
+        ++q;
+        r -= b;
+    }
+}
+
+// A beam's coarse lattice start bx = ix - winX, by = iy - winY as (plane
+// column qx0 = floor(bx / lr), plane row qy0, phase rx = bx mod lr, ry).
+struct BeamLattice {
+    int qx0, qy0, rx, ry;
+};
+__device__ __forceinline__ BeamLattice beam_lattice(int ix, int iy, const RtcsmPlan& pl, double inv_lr)
+{
+    BeamLattice b;
+    floor_divmod(ix - pl.win_x, pl.low_res, inv_lr, b.qx0, b.rx);
+    floor_divmod(iy - pl.win_y, pl.low_res, inv_lr, b.qy0, b.ry);
+    return b;
+}
 
 // Per (angle, beam) base offset of the coarse stage in the padded phase-plane
-// layout (see k_decimate): the beam's lattice starts at bx = ix - winX,
-// by = iy - winY, in plane (bx mod lr, by mod lr) at (floor(bx/lr),
-// floor(by/lr)).  If its ncx x ncy window touches the map, the window lies
+// layout (see k_decimate): the beam's lattice start lies in plane (rx, ry) at
+// (qx0, qy0).  If its ncx x ncy window touches the map, the window lies
 // inside the M-wide zero margins (M >= ncx, ncy) and the base is direct;
 // otherwise every read is 0.0 (GridMap::Value out of bounds) and the base
 // points at the all-zero top-left margin of plane 0.  The coarse lanes then
 // read base + jy * Wqp + jx with no bounds test.
+__device__ __forceinline__ int coarse_base_l(const BeamLattice& b, const RtcsmPlan& pl)
+{
+    const int lr = pl.low_res;
+    const bool touches = (b.qx0 < pl.Wq) & (b.qx0 + pl.ncx > 0) & (b.qy0 < pl.Hq) & (b.qy0 + pl.ncy > 0);
+    return touches ? (int)((b.ry * lr + b.rx) * pl.pstride + (long long)(b.qy0 + pl.M) * pl.Wqp + (b.qx0 + pl.M)) : 0;
+}
+
 // Superblock base of the same beam in the compact superblock planes: the
 // padded position (Qx, Qy) of its lattice start, in sub-phase (Qx & 3, Qy & 3)
 // at (Qx >> 2, Qy >> 2); superblock (a, b) is then base + b * Wq4 + a.  0 (an
 // all-zero margin corner) when the coarse window misses the map.
-__device__ __forceinline__ int super_base(int ix, int iy, const RtcsmPlan& pl)
+__device__ __forceinline__ int super_base_l(const BeamLattice& b, const RtcsmPlan& pl)
 {
     const int lr = pl.low_res;
-    const int bx = ix - pl.win_x, by = iy - pl.win_y;
-    const int qx0 = floor_div(bx, lr), qy0 = floor_div(by, lr);
-    const int rx = bx - lr * qx0, ry = by - lr * qy0;
+    const int qx0 = b.qx0, qy0 = b.qy0, rx = b.rx, ry = b.ry;
     // the strip qx = -1 (rx > 0) / qy = -1 (ry > 0) holds the clamped values
     // of k_super_planes: a window that reaches only the strip still counts
     const bool touches = (qx0 < pl.Wq) & (qx0 + pl.ncx > (rx > 0 ? -1 : 0)) & (qy0 < pl.Hq) &
@@ -219,6 +252,15 @@ __device__ __forceinline__ int super_base(int ix, int iy, const RtcsmPlan& pl)
     return touches ? (int)((ry * lr + rx) * pl.pstride4 + ((Qy & 3) * 4 + (Qx & 3)) * pl.sub4 +
                            (long long)(Qy >> 2) * pl.Wq4 + (Qx >> 2))
                    : 0;
+}
+
+__device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
+{
+    return coarse_base_l(beam_lattice(ix, iy, pl, 1.0 / pl.low_res), pl);
+}
+__device__ __forceinline__ int super_base(int ix, int iy, const RtcsmPlan& pl)
+{
+    return super_base_l(beam_lattice(ix, iy, pl, 1.0 / pl.low_res), pl);
 }
 
 // Coarse value C(x, y) of an in-map coarse cell in the padded phase planes.
@@ -240,16 +282,6 @@ __device__ __forceinline__ bool strip_read(const double* __restrict__ cmap, int 
     const bool s = (x >= lo) & (x < pl.W) & (y >= lo) & (y < pl.H) & ((x < 0) | (y < 0));
     if (s) ext += coarse_at(cmap, max(x, 0), max(y, 0), pl);
     return s;
-}
-
-__device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
-{
-    const int lr = pl.low_res;
-    const int bx = ix - pl.win_x, by = iy - pl.win_y;
-    const int qx0 = floor_div(bx, lr), qy0 = floor_div(by, lr);
-    const int rx = bx - lr * qx0, ry = by - lr * qy0;
-    const bool touches = (qx0 < pl.Wq) & (qx0 + pl.ncx > 0) & (qy0 < pl.Hq) & (qy0 + pl.ncy > 0);
-    return touches ? (int)((ry * lr + rx) * pl.pstride + (long long)(qy0 + pl.M) * pl.Wqp + (qx0 + pl.M)) : 0;
 }
 
 // blockDim == 256.  ComputeScanIndices keeps the beams with range <
@@ -280,9 +312,12 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     if (wg.y * kProjRows >= pl.T) return;   // past this item's angles (uniform)
     const double* __restrict__ ranges = it.ranges;
     const double* __restrict__ angles = it.angles;
-    int2* __restrict__ idx = it.idx;
-    int* __restrict__ cbase = it.cbase;
-    int* __restrict__ tedge = it.tedge;
+    // global (not flat) stores: the item's pointers come through a struct
+    typedef __attribute__((address_space(1))) unsigned long long gu64_t;   // int2 {x, y}: x in the low half
+    typedef __attribute__((address_space(1))) int gint_t;
+    gu64_t* __restrict__ idx = (gu64_t*)it.idx;
+    gint_t* __restrict__ cbase = (gint_t*)it.cbase;
+    gint_t* __restrict__ tedge = (gint_t*)it.tedge;
     const int gen = it.gen;
     RtcsmRecord* rec = it.rec;
     __shared__ int s_map[256];
@@ -334,6 +369,7 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     sincos(a, &sa, &ca);
     const int tt1 = min(pl.T, (wg.y + 1) * kProjRows);
     const double inv_res = 1.0 / pl.res;
+    const double inv_lr = 1.0 / pl.low_res;
     for (int tt = wg.y * kProjRows; tt < tt1; ++tt) {
     // HitPoint: cos(sensorPose.mTheta + scanAngle) (H/sensor/sensor_data.hpp:168-172),
     // by rotation (see kProjRows)
@@ -368,9 +404,10 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
         ix += inject;
     }
     const size_t o = (size_t)tt * pl.Nv + v;
-    idx[o] = make_int2(ix, iy);
-    cbase[o] = coarse_base(ix, iy, pl);
-    cbase[pl.sb_off + o] = super_base(ix, iy, pl);
+    idx[o] = ((unsigned long long)(unsigned)iy << 32) | (unsigned)ix;
+    const BeamLattice bl = beam_lattice(ix, iy, pl, inv_lr);
+    cbase[o] = coarse_base_l(bl, pl);
+    cbase[pl.sb_off + o] = super_base_l(bl, pl);
     // this angle has a beam whose coarse lattice starts left of / below the
     // map: k_coarse must run its unsafe-block check (generation-stamped flag)
     if (ix - pl.win_x < 0 || iy - pl.win_y < 0) tedge[tt] = gen;
@@ -786,21 +823,22 @@ __global__ __launch_bounds__(kSPThreads) void k_super_planes(const PlaneJob* __r
     __syncthreads();
     const int q0 = x0 >> 2;   // the tile's first superblock column (x0 is a multiple of 4)
     if (pl.oct) {
-        // octet layout: the tile is one quad (sub-phase rows 4 qt .. 4 qt + 3,
-        // kSPY = 16 padded rows) of every sub-phase array; its 4 rows at column
-        // X are the low half of unit (qt, X) and the high half of (qt - 1, X)
-        static_assert(kSPY == 16, "one quad of sub-phase rows per tile");
-        const int qt = y0 >> 4;
+        // octet layout: the tile is kSPY / 16 quads (sub-phase rows 4 qt ..
+        // 4 qt + 3, 16 padded rows each) of every sub-phase array; a quad's 4
+        // rows at column X are the low half of unit (qt, X) and the high half
+        // of (qt - 1, X)
+        static_assert(kSPY % 16 == 0, "whole quads of sub-phase rows per tile");
         typedef unsigned long long u64;
         u64* __restrict__ uo = (u64*)(S + 8 * plane * pl.pstrideO);
-        for (int k = tid; k < 16 * kQ; k += blockDim.x) {   // (sub-phase, column), column fastest
-            const int sp = k / kQ, X = k % kQ;
+        for (int k = tid; k < kSPY * kQ; k += blockDim.x) {   // (quad, sub-phase, column), column fastest
+            const int h = k / (16 * kQ), sp = (k / kQ) % 16, X = k % kQ;
+            const int qt = (y0 >> 4) + h;
             const int cy = sp >> 2, sx = sp & 3, Xg = q0 + X;
             if (Xg >= pl.Wq4) continue;
             u64 v = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                v |= (u64)__builtin_bit_cast(unsigned short, hs[4 * i + cy][sx][X]) << (16 * i);
+                v |= (u64)__builtin_bit_cast(unsigned short, hs[16 * h + 4 * i + cy][sx][X]) << (16 * i);
             const long long u = sp * pl.subO + (long long)qt * pl.Wq4 + Xg;
             uo[2 * u] = v;
             if (qt > 0) uo[2 * (u - pl.Wq4) + 1] = v;
