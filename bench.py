@@ -513,6 +513,11 @@ def run_match(args, D, ctx):
         # latency of one batched call under the timed load
         p50_batch_call_ms=round(float(np.percentile(lat_ms, 50)), 4),
         roofline=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_lanes", "l2-gather"), cpu_baseline=cpu,
+        # the same kernel timed alone (the one-stream, fully event-timed pass
+        # after the timed region): in the timed region each launch shares the
+        # GPU with the other streams' kernels, and its duration varies with how
+        # the streams' batches overlap (0.45-0.62 ms measured for 2 streams)
+        roofline_isolated=roofline_from(all_stats, "k_coarse", args.pmc, "k_coarse_lanes", "l2-gather"),
         pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events,
         super_prune=bool(args.super_prune),
         coarse_blocks_scored_mean=round(float(results[:, 4].mean()), 1),
