@@ -307,12 +307,17 @@ __device__ __forceinline__ bool strip_read(const double* __restrict__ cmap, int 
 #define LGS_PROJ_INV 1
 #endif
 constexpr int kProjRows = LGS_PROJ_ROWS;
+#ifndef LGS_PROJ_ROWS_LONE
+#define LGS_PROJ_ROWS_LONE 4   // measured (lone config-2 scan): 16: 16.1 us, 8: 12.3, 4: 10.7, 2: 10.4
+#endif
+constexpr int kProjRowsLone = LGS_PROJ_ROWS_LONE;
+template <int ROWS>
 __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, double guard_eps, int inject)
 {
     const Blk wg = xcd_block();
     const MatchItem& it = items[wg.z];
     const RtcsmPlan& pl = it.pl;
-    if (wg.y * kProjRows >= pl.T) return;   // past this item's angles (uniform)
+    if (wg.y * ROWS >= pl.T) return;   // past this item's angles (uniform)
     const double* __restrict__ ranges = it.ranges;
     const double* __restrict__ angles = it.angles;
     // global (not flat) stores: the item's pointers come through a struct
@@ -325,11 +330,11 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     RtcsmRecord* rec = it.rec;
     __shared__ int s_map[256];
     __shared__ int s_wsum[4];
-    __shared__ double s_ct[kProjRows], s_st[kProjRows];
+    __shared__ double s_ct[ROWS], s_st[ROWS];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (tid < kProjRows) {
+    if (tid < ROWS) {
         // currentSensorPose.mTheta = sensorPose.mTheta + stepTheta * t (:90-91)
-        const int t = wg.y * kProjRows + tid - pl.win_t;
+        const int t = wg.y * ROWS + tid - pl.win_t;
         const double th = pl.st + pl.step_t * (double)t;
         double sn, cs;
         sincos(th, &sn, &cs);
@@ -370,13 +375,13 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     const double a = angles[i];
     double sa, ca;
     sincos(a, &sa, &ca);
-    const int tt1 = min(pl.T, (wg.y + 1) * kProjRows);
+    const int tt1 = min(pl.T, (wg.y + 1) * ROWS);
     const double inv_res = 1.0 / pl.res;
     const double inv_lr = 1.0 / pl.low_res;
-    for (int tt = wg.y * kProjRows; tt < tt1; ++tt) {
+    for (int tt = wg.y * ROWS; tt < tt1; ++tt) {
     // HitPoint: cos(sensorPose.mTheta + scanAngle) (H/sensor/sensor_data.hpp:168-172),
-    // by rotation (see kProjRows)
-    const int kr = tt - wg.y * kProjRows;
+    // by rotation (see ROWS)
+    const int kr = tt - wg.y * ROWS;
     const double c = s_ct[kr] * ca - s_st[kr] * sa;
     const double s = s_st[kr] * ca + s_ct[kr] * sa;
     const double hx = pl.sx + r * c;
@@ -1249,7 +1254,10 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
 // keep kRing - 1 gathers in flight, and each slot is refilled once read.
 constexpr int kRowWaves = 1;   // waves per workgroup
 constexpr int kRowSplit = 4;   // workgroups per (angle, patch row): kept superblocks e = z, z + 4, ...
-constexpr int kRing = 12;      // 1 KiB glds slots per wave
+#ifndef LGS_RING
+#define LGS_RING 16   // measured (lone config-2 scan): 12: 30.0 us, 14: 30.6, 16: 26.8, 18: 31.5, 20: 33.0, 24: 34.2, 32: 32.4
+#endif
+constexpr int kRing = LGS_RING;      // 1 KiB glds slots per wave
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14)
@@ -1777,6 +1785,16 @@ __global__ __launch_bounds__(LR > 0 ? 64 * LR : 64) void k_seed(Items items, con
 // candidate: each one's duration is its latency chain).
 constexpr int kSeedMaxNv = 2048;   // LDS: the candidate row (Nv ints / int2)
 constexpr int kSeedRegParts = 4;   // parts held in registers per thread
+// gathers per batch (one memory round trip each) in the member and fine
+// stages: a 1081-beam scan needs 17 per thread in the member stage and 34 in
+// the fine stage (25 poses padded to 32 lanes)
+#ifndef LGS_SEED_B1
+#define LGS_SEED_B1 24
+#endif
+#ifndef LGS_SEED_B2
+#define LGS_SEED_B2 36
+#endif
+constexpr int kSeedB1 = LGS_SEED_B1, kSeedB2 = LGS_SEED_B2;
 
 __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* __restrict__ zero)
 {
@@ -1841,9 +1859,13 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
     if (nc > (int)blockIdx.x) {
         const long long ck = cand[blockIdx.x];
         const int ct = (int)(ck / nsb2), csb = (int)(ck % nsb2);
-        // 2. member sums: member m = tid % 16, beam group tid / 16 (64 groups)
+        // 2. member sums: member m = tid % 16, beam group tid / 16 (64 groups);
+        // the fine stage's beam row is staged together with the coarse one
+        // (one memory round trip less on this latency chain)
         int* srow = (int*)smem;   // [Nv]
+        int2* sidx = (int2*)(smem + ((sizeof(int) * (size_t)Nv + 15) & ~(size_t)15));   // [Nv]
         stage_lds(srow, cbase + (size_t)ct * Nv, Nv);
+        stage_lds(sidx, idx + (size_t)ct * Nv, Nv);
         __syncthreads();
         const int m = tid & 15, g = tid >> 4;
         const int jx = kSB * (csb % pl.nsbx) + (m & 3);
@@ -1854,15 +1876,15 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             const double* __restrict__ lb = cmap + (jy * pl.Wqp + jx);
             const int cnt = (g < Nv) ? (Nv - g + 63) / 64 : 0;   // beams g, g + 64, ...
             double acc[4] = { 0.0, 0.0, 0.0, 0.0 };
-            for (int i0 = 0; i0 < cnt; i0 += 16) {
-                double buf[16];
+            for (int i0 = 0; i0 < cnt; i0 += kSeedB1) {
+                double buf[kSeedB1];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
+                for (int j = 0; j < kSeedB1; ++j) {
                     const int i = min(i0 + j, cnt - 1);
                     buf[j] = (i0 + j < cnt) ? lb[srow[g + 64 * i]] : 0.0;
                 }
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
+                for (int j = 0; j < kSeedB1; ++j) {
                     acc[j & 3] += buf[j];
                     sa += fabs(buf[j]);
                 }
@@ -1918,11 +1940,6 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
         const int rem = (int)(mk % pl.P);
         const int bjx = rem / pl.ncy, bjy = rem % pl.ncy;
         const int lr = pl.low_res, npose = lr * lr;
-        int2* sidx = (int2*)smem;   // [Nv]
-        __syncthreads();
-        LGS_PROBE_MARK();
-        stage_lds(sidx, idx + (size_t)ct * Nv, Nv);
-        __syncthreads();
         LGS_PROBE_MARK();
         int QP = 1;
         while (QP < npose) QP <<= 1;   // npose <= 1024
@@ -1934,17 +1951,17 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             const int xf = -pl.win_x + bjx * lr + xo, yf = -pl.win_y + bjy * lr + yo;
             const int W = pl.W, H = pl.H;
             const int cnt = (gq < Nv) ? (Nv - gq + G - 1) / G : 0;   // beams gq, gq + G, ...
-            for (int i0 = 0; i0 < cnt; i0 += 16) {
-                double buf[16];
+            for (int i0 = 0; i0 < cnt; i0 += kSeedB2) {
+                double buf[kSeedB2];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
+                for (int j = 0; j < kSeedB2; ++j) {
                     const int2 c = sidx[gq + G * min(i0 + j, cnt - 1)];
                     const int x = c.x + xf, y = c.y + yf;
                     const bool inb = (i0 + j < cnt) & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
                     buf[j] = *(inb ? grid + (unsigned)(y * W + x) : zero);
                 }
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
+                for (int j = 0; j < kSeedB2; ++j) {
                     fs += buf[j];
                     fa += fabs(buf[j]);
                 }
@@ -2102,6 +2119,9 @@ __device__ __forceinline__ int seg_of(const int* pref, int nseg, int b)
 // memory pipeline are what a block evaluation waits on); fval/fpos are
 // indexed by item and k_replay combines a block's rows.  LR == 0: one wave
 // per block, indexed by dense position.
+#ifndef LGS_FINE_DEPTH
+#define LGS_FINE_DEPTH 6   // measured (lone config-2 scan): 4: 33.7 us, 5: 34.2, 6: 23.8, 7: 24.0, 8: 34.1
+#endif
 template <int LR>
 __global__ __launch_bounds__(64) void k_fine(Items items, const double* __restrict__ zero, unsigned eval_smem)
 {
@@ -2133,7 +2153,7 @@ __global__ __launch_bounds__(64) void k_fine(Items items, const double* __restri
         double f;
         int pos;
         if constexpr (LR > 0)
-            eval_block_t<LR, 4>(pl, grid, idx, zero, k, smem, sv, sk, f, pos, it % R);
+            eval_block_t<LR, LGS_FINE_DEPTH>(pl, grid, idx, zero, k, smem, sv, sk, f, pos, it % R);
         else
             eval_block(pl, grid, idx, zero, k, (int2*)smem, f, pos);
         if (threadIdx.x == 0) {
@@ -2959,10 +2979,19 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         hipLaunchKernelGGL(k_cinfo, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, d_items);
         LGS_HIP_CHECK(hipGetLastError());
     } else {
-        dim3 g(std::max(1, (B.NvMax + 255) / 256), (B.Tmax + kProjRows - 1) / kProjRows, n);
+        // a lone scan: fewer angles per workgroup (its ~400 angles then fill
+        // the GPU; a batch fills it anyway and shares each sincos over more)
+        const bool lone = n < ctx->lanes_min_batch;
+        const int rows = lone ? kProjRowsLone : kProjRows;
+        dim3 g(std::max(1, (B.NvMax + 255) / 256), (B.Tmax + rows - 1) / rows, n);
         const int tok_ = ctx->timing_begin(K_PROJECT, 24.0 * beams_T);
-        if (!ctx->skipped(K_PROJECT))
-            hipLaunchKernelGGL(k_project, g, dim3(256), 0, st, d_items, ctx->guard_cap, ctx->guard_eps, inject);
+        if (ctx->skipped(K_PROJECT)) {
+        } else if (lone)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_project<kProjRowsLone>), g, dim3(256), 0, st, d_items, ctx->guard_cap,
+                               ctx->guard_eps, inject);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_project<kProjRows>), g, dim3(256), 0, st, d_items, ctx->guard_cap,
+                               ctx->guard_eps, inject);
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
         if (opt.patches && !opt.patches->empty()) {
@@ -2996,7 +3025,8 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         }
         {
             const int tok = ctx->timing_begin(K_SEED, 8.0 * kSeedCands * (B.low_res * B.low_res + 16.0) * B.NvMax * n);
-            const size_t lds = sizeof(int2) * (size_t)std::max(B.NvMax, 1);
+            const size_t lds = ((sizeof(int) * (size_t)std::max(B.NvMax, 1) + 15) & ~(size_t)15) +
+                               sizeof(int2) * (size_t)std::max(B.NvMax, 1);   // coarse + fine beam rows
             if (!ctx->skipped(K_SEED))
                 hipLaunchKernelGGL(k_seed_super, dim3(kSeedCands, n), dim3(1024), lds, st, d_items, zero);
             ctx->timing_end(tok);
@@ -3751,7 +3781,7 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
         launch_sets(ctx, pl, sets, sj, up);
         Items d_items = up.at<MatchItem>(off);
         dim3 g(std::max(1, (nv + 255) / 256), (pl.T + kProjRows - 1) / kProjRows, 1);
-        hipLaunchKernelGGL(k_project, g, dim3(256), 0, ctx->stream, d_items, 0, -1.0, 0);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_project<kProjRows>), g, dim3(256), 0, ctx->stream, d_items, 0, -1.0, 0);
         LGS_HIP_CHECK(hipGetLastError());
         if (coarse_scores) {
             dim3 gc((pl.P + cb - 1) / cb, pl.T, 1);
