@@ -761,8 +761,16 @@ __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __re
 constexpr int kSPX = LGS_SPX, kSPY = LGS_SPY;   // kSPX = 4 sub-phases x 64 (8 stores of 8)
 constexpr int kSPThreads = (kSPX + 3 + 63) / 64 * 64;   // >= kSPX + kSB - 1 column loaders
 
-__global__ __launch_bounds__(kSPThreads) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
+// SPX: tile width (kSPX for a batch's sets; a lone set takes narrower tiles,
+// more workgroups for its few hundred tiles: latency-bound, like the precompute)
+#ifndef LGS_SPX_LONE
+#define LGS_SPX_LONE 128   // measured (lone config-2 set): 256: 12.9 us, 128: 11.3, 64: 11.2
+#endif
+template <int SPX>
+__global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
 {
+    constexpr int kSPX = SPX;
+    constexpr int kSPThreads = (kSPX + 3 + 63) / 64 * 64;
     const Blk wg = xcd_block();
     const PlaneJob& job = jobs[wg.z / nplanes];
     const int plane = wg.z % nplanes;
@@ -2898,10 +2906,18 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
     if (sj.njobs) launch_precompute_jobs(ctx, up.at<PrecompJob>(sj.jobs_off), (int)sj.njobs, maxW, maxH, lp.low_res);
     if (sj.npj) {
         const int np = lp.low_res * lp.low_res;
-        dim3 g((lp.Wqp + kSPX - 1) / kSPX, (lp.Hqp + kSPY - 1) / kSPY, np * (int)sj.npj);
+        const bool lone = sj.npj == 1;
+        const int spx = lone ? LGS_SPX_LONE : kSPX;
+        dim3 g((lp.Wqp + spx - 1) / spx, (lp.Hqp + kSPY - 1) / kSPY, np * (int)sj.npj);
         const int tok = ctx->timing_begin(K_SUPER_PLANES, 8.0 * 2.0 * (double)np * lp.pstride * sj.npj);
-        if (!ctx->skipped(K_SUPER_PLANES))
-            hipLaunchKernelGGL(k_super_planes, g, dim3(kSPThreads), 0, ctx->stream, up.at<PlaneJob>(sj.pj_off), np);
+        if (!ctx->skipped(K_SUPER_PLANES)) {
+            if (lone)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_planes<LGS_SPX_LONE>), g,
+                                   dim3((LGS_SPX_LONE + 3 + 63) / 64 * 64), 0, ctx->stream, up.at<PlaneJob>(sj.pj_off), np);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_planes<kSPX>), g, dim3(kSPThreads), 0, ctx->stream,
+                                   up.at<PlaneJob>(sj.pj_off), np);
+        }
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
     }

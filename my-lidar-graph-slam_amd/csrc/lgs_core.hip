@@ -529,13 +529,18 @@ __global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restri
 //     16-byte store (padded plane rows are even, so the pair is aligned); the
 //     lanes of a wave walk a plane row, so a wave writes 512-byte runs.
 // Same values as the reference's passes (max is exact).
-constexpr int kPTY = 16;
+// tile rows: 16 for a batch's maps; a lone map (one job) takes 8-row tiles,
+// twice the workgroups for its ~250 tiles (latency, not bandwidth, bounds a
+// single 1000 x 1000 map)
+#ifndef LGS_PTY_LONE
+#define LGS_PTY_LONE 4   // measured (lone config-2 map): 16: 16.4 us, 8: 13.3, 4: 11.5
+#endif
 // coarse columns per tile: the footprint (kPQX * LR + LR - 1 fine columns) fits
 // the 256 threads of the y pass, and kPQX is even (column pairs)
 template <int LR>
 constexpr int pqx() { return ((257 - LR) / LR) & ~1; }
 typedef double d2a16 __attribute__((ext_vector_type(2)));
-template <int LR>
+template <int LR, int kPTY = 16>
 __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __restrict__ jobs)
 {
     const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
@@ -727,8 +732,16 @@ void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, i
     } else if (win <= 8) {
         // plane-ordered tiles (every job of this path writes planes)
         switch (win) {
-#define LGS_PP_CASE(L) case L: hipLaunchKernelGGL(k_precompute_planes<L>, \
-            dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + kPTY - 1) / kPTY, njobs), dim3(256), 0, ctx->stream, d_jobs); break;
+#define LGS_PP_CASE(L) case L: \
+            if (njobs == 1) \
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_precompute_planes<L, LGS_PTY_LONE>), \
+                    dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + LGS_PTY_LONE - 1) / LGS_PTY_LONE, njobs), \
+                    dim3(256), 0, ctx->stream, d_jobs); \
+            else \
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_precompute_planes<L, 16>), \
+                    dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + 15) / 16, njobs), dim3(256), 0, ctx->stream, \
+                    d_jobs); \
+            break;
         LGS_PP_CASE(1) LGS_PP_CASE(2) LGS_PP_CASE(3) LGS_PP_CASE(4) LGS_PP_CASE(5) LGS_PP_CASE(6)
         LGS_PP_CASE(7) LGS_PP_CASE(8)
 #undef LGS_PP_CASE
