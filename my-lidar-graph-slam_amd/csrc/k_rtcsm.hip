@@ -2329,17 +2329,20 @@ __global__ __launch_bounds__(64) void k_replay(Items items)
             }
             if (cflag[k] && c < L && f >= L) dangerous = true;
         }
+        // the sequential rule in as many steps as it accepts blocks: the
+        // first lane (from `from` on) whose block passes under the current s
+        // is the next one the walk would accept; the lanes before it fail
+        // under this s and are passed over exactly as the walk does
         const int cnt = min(64, n - b0);
-        for (int j = 0; j < cnt; ++j) {
-            const double cj = __shfl(c, j, 64);
-            const double fj = __shfl(f, j, 64);
-            const long long kj = __shfl(k, j, 64);
-            const int pj = __shfl(pos, j, 64);
-            if (cj > s && fj > s) {
-                s = fj;
-                bestk = kj;
-                bestpos = pj;
-            }
+        for (int from = 0;;) {   // wave-uniform
+            const bool cand = lane >= from && lane < cnt && c > s && f > s;
+            const unsigned long long m = __ballot(cand);
+            if (m == 0ull) break;
+            const int j = __ffsll((long long)m) - 1;
+            s = __shfl(f, j, 64);
+            bestk = __shfl(k, j, 64);
+            bestpos = __shfl(pos, j, 64);
+            from = j + 1;
         }
     }
     dangerous = __ballot(dangerous) != 0ull;
