@@ -190,7 +190,7 @@ __device__ __forceinline__ bool near_boundary(double q, double eps)
 // --------------------------------------------------------------------------
 
 // floor(a / b) and the remainder in [0, b) for a runtime divisor b > 0
-// (|a| < 2^30): one fp64 multiply by 1/b, floor and a +-1 correction -- exact,
+// (any int a): one fp64 multiply by 1/b, floor and a +-1 correction -- exact,
 // and a fraction of the two branchy integer divisions it replaces (k_project
 // spent most of its VALU issue on those)
 __device__ __forceinline__ void floor_divmod(int a, int b, double inv_b, int& q, int& r)
