@@ -2039,46 +2039,61 @@ constexpr int kSelSeg = 1024;
 // sbound (superblock pruning, else nullptr): blocks of superblocks
 // k_coarse_rows did not keep were never scored and are never taken (the
 // same keep rule, evaluated again here).
-__global__ __launch_bounds__(kSelSeg) void k_select(Items items, int use_sbound)
+// kSelThreads threads per segment, kSelSeg / kSelThreads keys each: the
+// segment's keys in chunks of kSelThreads, each chunk compacted in key order
+// after the previous ones (fewer, fuller waves than one key per thread: the
+// kernel was launch-bound on ~120k mostly idle waves per batch)
+// (batches: 256 threads, 36.4 -> 26.7 us per 64 scans; a lone scan keeps one
+// key per thread, 6.4 vs 8.3 us: its ~120 segments do not fill the GPU)
+template <int kSelThreads>
+__global__ __launch_bounds__(kSelThreads) void k_select(Items items, int use_sbound)
 {
+    static_assert(kSelSeg % kSelThreads == 0 && kSelThreads % 64 == 0, "whole chunks of whole waves");
     const MatchItem& it = items[blockIdx.y];
     if ((int)blockIdx.x >= it.nseg) return;   // past this item's segments (uniform)
     const RtcsmPlan& pl = it.pl;
     const double* __restrict__ cscore = it.cscore;
     const uint8_t* __restrict__ cflag = it.cflag;
-    const double* __restrict__ Lp = it.Lp;
     const double* __restrict__ sbound = use_sbound ? it.sbound : nullptr;
     int* __restrict__ list = it.list;
     int* __restrict__ segcnt = it.segcnt;
-    __shared__ int s_w[kSelSeg / 64];
-    const long long k = (long long)blockIdx.x * kSelSeg + threadIdx.x;
-    bool f = false;
-    if (k < pl.K) {
-        bool kp = true;
-        const double L = *Lp;
-        if (sbound) {
-            const int t = (int)(k / pl.P), rem = (int)(k % pl.P);
-            const int jx = rem / pl.ncy, jy = rem % pl.ncy;
-            const double bnd = sbound[(size_t)t * pl.nsbx * pl.nsby + (jy / kSB) * pl.nsbx + jx / kSB];
-            kp = (bnd > pl.thr) && bnd >= L;
-        }
-        if (kp) {
-            const double c = cscore[k];
-            f = (c > pl.thr) && (cflag[k] || c >= L);
-        }
-    }
-    const unsigned long long bal = __ballot(f);
+    constexpr int kW = kSelThreads / 64, kChunks = kSelSeg / kSelThreads;
+    __shared__ int s_w[kChunks][kW];
+    const double L = *it.Lp;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) s_w[wid] = __popcll(bal);
-    __syncthreads();
-    int off = 0;
-    for (int j = 0; j < wid; ++j) off += s_w[j];
-    if (f) list[(size_t)blockIdx.x * kSelSeg + off + __popcll(bal & ((1ull << lane) - 1ull))] = (int)k;
-    if (threadIdx.x == 0) {
-        int t = 0;
-        for (int j = 0; j < kSelSeg / 64; ++j) t += s_w[j];
-        segcnt[blockIdx.x] = t;
+    bool f[kChunks];
+#pragma unroll
+    for (int j = 0; j < kChunks; ++j) {
+        const long long k = (long long)blockIdx.x * kSelSeg + j * kSelThreads + threadIdx.x;
+        f[j] = false;
+        if (k < pl.K) {
+            bool kp = true;
+            if (sbound) {
+                const int t = (int)(k / pl.P), rem = (int)(k % pl.P);
+                const int jx = rem / pl.ncy, jy = rem % pl.ncy;
+                const double bnd = sbound[(size_t)t * pl.nsbx * pl.nsby + (jy / kSB) * pl.nsbx + jx / kSB];
+                kp = (bnd > pl.thr) && bnd >= L;
+            }
+            if (kp) {
+                const double c = cscore[k];
+                f[j] = (c > pl.thr) && (cflag[k] || c >= L);
+            }
+        }
+        const unsigned long long bal = __ballot(f[j]);
+        if (lane == 0) s_w[j][wid] = __popcll(bal);
     }
+    __syncthreads();
+    int off = 0;   // keys of the earlier chunks, then of the earlier waves of this chunk
+#pragma unroll
+    for (int j = 0; j < kChunks; ++j) {
+        const unsigned long long bal = __ballot(f[j]);
+        int o = off;
+        for (int w = 0; w < wid; ++w) o += s_w[j][w];
+        if (f[j]) list[(size_t)blockIdx.x * kSelSeg + o + __popcll(bal & ((1ull << lane) - 1ull))] =
+            (int)((long long)blockIdx.x * kSelSeg + j * kSelThreads + threadIdx.x);
+        for (int w = 0; w < kW; ++w) off += s_w[j][w];
+    }
+    if (threadIdx.x == 0) segcnt[blockIdx.x] = off;
 }
 
 // pref[0..nseg] = exclusive prefix of segcnt, built in LDS by the whole
@@ -3087,9 +3102,14 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
     }
     {
         const int tok_ = ctx->timing_begin(K_SELECT, 10.0 * (double)B.Tmax * B.P * n);
-        if (!ctx->skipped(K_SELECT))
-            hipLaunchKernelGGL(k_select, dim3((unsigned)B.nsegMax, n), dim3(kSelSeg), 0, st, d_items,
-                               B.pruned ? 1 : 0);
+        if (!ctx->skipped(K_SELECT)) {
+            if (n >= ctx->lanes_min_batch)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_select<256>), dim3((unsigned)B.nsegMax, n), dim3(256), 0, st,
+                                   d_items, B.pruned ? 1 : 0);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_select<kSelSeg>), dim3((unsigned)B.nsegMax, n), dim3(kSelSeg), 0,
+                                   st, d_items, B.pruned ? 1 : 0);
+        }
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
     }
