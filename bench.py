@@ -65,9 +65,10 @@ def parse():
                     help="A/B: 1 superblock pruning of the coarse stage, 0 score every coarse block")
     ap.add_argument("--streams", type=int, default=2,
                     help="match workload: concurrent HIP streams (lgs contexts) per GPU, one host thread each")
-    ap.add_argument("--batch", type=int, default=64,
-                    help="match workload: queries per call (lgs_rtcsm_optimize_pose_query_batch; 1 = one "
-                         "lgs_rtcsm_optimize_pose_query call per scan)")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="match workload: queries per call (lgs_rtcsm_optimize_pose_query_batch, which launches "
+                         "64-query chunks back to back; 1 = one lgs_rtcsm_optimize_pose_query call per scan). "
+                         "128 per call: 45.1k vs 41.6k scans/s for 64 (one host synchronisation per two chunks)")
     ap.add_argument("--lanes-min-batch", type=int, default=None,
                     help="A/B: LGS_OPT_LANES_MIN_BATCH (pruned coarse stage kernel choice by batch size)")
     ap.add_argument("--super-quad", type=int, default=None, help="A/B: LGS_OPT_SUPER_QUAD")
@@ -505,8 +506,8 @@ def run_match(args, D, ctx):
                     search_range=[4.0, 4.0, 1.0471976], scans_per_rank=args.steps * B, batch=B,
                     streams_per_gpu=S,
                     parallelism=f"replicas x{D.world} (independent scans per rank), {S} concurrent HIP streams "
-                                f"per GPU, each issuing batches of {B} OptimizePose(query) matches "
-                                f"(one launch per stage per batch) + RCCL all-gather of poses"),
+                                f"per GPU, each issuing calls of {B} OptimizePose(query) matches "
+                                f"(one launch per stage per 64-query chunk) + RCCL all-gather of poses"),
         # latency of one lone OptimizePose(query) call (what the frontend waits for)
         p50_scan_match_ms=round(1e3 * float(np.median(lat1)), 4) if lat1 else None,
         p90_scan_match_ms=round(1e3 * float(np.percentile(lat1, 90)), 4) if lat1 else None,
