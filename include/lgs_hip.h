@@ -171,7 +171,6 @@ int  lgs_abi_version(void);
 #define LGS_OPT_RAY_CHUNK_KEYS 13  /* ray-cast keys per emit/sort/apply pass (default 2^28, max 2^30); more keys are cast in scan order over several passes */
 #define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: lane-per-block kernel for batches of at least this many matches (default 2; 1 = always), else the row kernel */
 #define LGS_OPT_FINE_LANES    16  /* 1 (default) = fine stage with one lane per pose over the batch's block list, 0 = transposed row evaluator (A/B) */
-#define LGS_OPT_LINSOLVE_SPLIT 17 /* 1 (default) = a lone ScanMatcherLinearSolver refine spreads its beams over up to 32 one-wave workgroups (in-launch hand-off per pass), 0 = one workgroup (A/B) */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 
@@ -183,6 +182,12 @@ int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
  * 6 idx [T*Nv int2], 7 cscore [K f64], 8 coarse phase planes [lr*lr planes
  * of Hqp x Wqp f64, DESIGN.md §2], 9 superblock planes [fp16]. */
 int  lgs_debug_item_buffer(lgs_ctx* ctx, int item, int which, void* out, size_t cap, size_t* bytes);
+
+/* Diagnostics: the device's restatements of glibc's sincos() (op 0: out[2i] =
+ * sin x[i], out[2i+1] = cos x[i]) and pow(x, 3.0) (op 1: out[i]) evaluated on
+ * the GPU for n host inputs (csrc/glibc_math.hpp; tests compare them with the
+ * host libm bit for bit). */
+int  lgs_debug_libm(lgs_ctx* ctx, int op, const double* x, int n, double* out);
 
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is
  * the algorithmic byte count of DESIGN.md §Roofline (e.g. 8 B per coarse-score

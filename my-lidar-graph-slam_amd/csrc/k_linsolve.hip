@@ -6,23 +6,26 @@
 // :112-135, ComputeMapGradient :172-229, ComputeSmoothedValue :276-346).
 //
 // One workgroup runs one whole refine (all iterations) without returning to
-// the host: per iteration every thread takes beams i = tid, tid + 512, ...,
-// evaluates the bicubic smoothed value and its central-difference map
-// gradient (5 x 16 gathers per beam, all independent), and accumulates
-// b = sum res*g and H = sum g*g^T in registers; wave64 shuffle butterflies
-// plus one LDS pass reduce the 9 sums; lane 0 solves the regularised 3x3
-// system with the column-pivoting Householder QR Eigen's colPivHouseholderQr
-// uses (restated, Eigen is not vendored), updates the pose, and the cost at
-// the new pose is reduced the same way for the convergence test.  A batch
-// launches one workgroup per scan.
+// the host; a batch launches one workgroup per scan.  Per pass every thread
+// evaluates beams of the current chunk (the bicubic smoothed value and its
+// central-difference map gradient: 5 x 16 independent gathers per beam) and
+// writes the beam's 13 terms to LDS; lanes 0..12 of wave 0 then add the
+// terms in beam order, one lane per sum -- the reference's own sequential
+// fp64 sums (scan_matcher_linear_solver.cpp:105-133,
+// cost_function_square_error.cpp:21-58, :61-109).  Lane 0 solves the
+// regularised 3x3 system with the column-pivoting Householder QR Eigen's
+// colPivHouseholderQr uses (restated, Eigen is not vendored) and updates the
+// pose; the same pass at the new pose gives the cost for the convergence
+// test and the next step's sums.
 //
-// Numerics: the reference's own result moves by up to ~1e-5
-// under a 1-ulp change of its input pose (ComputeSmoothedValue truncates
-// coordinates that sit on integers +- rounding), so parity with the oracle is
-// judged within the north-star tolerance, not bitwise.  Device sin/cos/pow
-// follow ocml; pow(x, 2.0) is the exact x*x GCC folds it to, pow(x, 3.0) is
-// the correctly rounded cube (glibc's pow agrees with it in 99.9% of inputs).
+// Numerics: sin/cos of a beam are glibc's sincos() and
+// pow(x, 3.0) is glibc's pow(), both restated bit-exactly (glibc_math.hpp,
+// pinned against this image's libm by tests/test_libm_pin.py); pow(x, 2.0) is
+// the exact x*x GCC folds it to; every sum runs in beam order.  The device
+// therefore performs the oracle's arithmetic operation for operation, and its
+// trajectory is the oracle's bit for bit.
 #include "lgs_internal.hpp"
+#include "glibc_math.hpp"
 
 #include <cfloat>
 #include <climits>
@@ -34,8 +37,6 @@
 using namespace lgs;
 
 namespace {
-
-constexpr int kLsThreads = 512;
 
 struct LsPlan {
     double min_x, min_y, res;
@@ -62,26 +63,17 @@ __device__ __forceinline__ int host_trunc(double x)
     return (x > -2147483649.0 && x < 2147483648.0) ? (int)x : INT_MIN;
 }
 
-// pow(a, 3.0), correctly rounded: a^3 = c + ce + pe*a exactly up to 2^-106 relative
-__device__ __forceinline__ double cube(double a)
-{
-    const double p = a * a;
-    const double pe = fma(a, a, -p);
-    const double c = p * a;
-    const double ce = fma(p, a, -c);
-    return c + (ce + pe * a);
-}
-
-// bicubic kernel h(t) (:281-295); pow(at, 2.0) is at*at after GCC folding
+// bicubic kernel h(t) (:281-295): pow(at, 3.0) is glibc's pow (restated bit-exactly),
+// pow(at, 2.0) is at*at after GCC folding
 __device__ __forceinline__ double bicubic_h(double t)
 {
     const double at = fabs(t);
     if (at <= 1.0) {
-        const double at3 = cube(at);
+        const double at3 = glm::gl_pow3(at);
         const double at2 = at * at;
         return (at3 - 2.0 * at2 + 1.0);
     } else if (at <= 2.0) {
-        const double at3 = cube(at);
+        const double at3 = glm::gl_pow3(at);
         const double at2 = at * at;
         return (-at3 + 5.0 * at2 - 8.0 * at + 4.0);
     }
@@ -155,7 +147,7 @@ constexpr double kHalfDelta = kDeltaIdx / 2.0;
 __device__ __forceinline__ void beam_cell(const LsPlan& p, const double pose[3], double r, double a, double& sn,
                                           double& cs, double& fx, double& fy)
 {
-    sincos(pose[2] + a, &sn, &cs);
+    glm::gl_sincos(pose[2] + a, &sn, &cs);   // GCC fuses the reference's cos/sin pair into sincos()
     const double hx = pose[0] + r * cs;
     const double hy = pose[1] + r * sn;
     fx = (hx - p.min_x) / p.res;
@@ -190,29 +182,6 @@ __device__ __forceinline__ void beam_terms(const LsPlan& p, const double* __rest
     const double syp = smoothed(g, p.W, x0, yp);
     const double sym = smoothed(g, p.W, x0, ym);
     beam_finish(p, r, sn, cs, s0, sxp, sxm, syp, sym, e, gv);
-}
-
-// sum over the workgroup of NV values per thread (wave64 butterfly + LDS);
-// every thread gets the totals
-template <int NV>
-__device__ void wg_sum(double (&v)[NV], double* red)
-{
-#pragma unroll
-    for (int k = 0; k < NV; ++k)
-        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    constexpr int nw = kLsThreads / 64;
-    __syncthreads();
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < NV; ++k) red[k * nw + wid] = v[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        double s = red[k * nw];
-        for (int w = 1; w < nw; ++w) s += red[k * nw + w];
-        v[k] = s;
-    }
 }
 
 // Eigen ColPivHouseholderQR<Matrix3d>::compute + solve (published algorithm,
@@ -386,43 +355,12 @@ struct LsScanRef {
 //   [9]      CostSquareError::Cost = sum e^2 over beams in (cost_min, cost_max);
 //   [10..12] ComputeGradient's sum 2*e*(-g) over the same beams (:61-109).
 // The reference's loop (step; cost at the new pose; convergence test) then
-// needs one pass per iteration plus the first (:48-69).
+// needs one pass per iteration plus the first (:48-69).  A beam outside a
+// filter contributes +0.0 to that filter's sums, which leaves a sum that
+// started at +0.0 unchanged bit for bit (it is never -0.0).
 constexpr int kAcc = 13;
 
-__device__ __forceinline__ void pass(const LsPlan& p, const double* __restrict__ grid, const LsScanRef& sc,
-                                     const double pose[3], double smin, double smax, double cmin,
-                                     double cmax, double (&acc)[kAcc])
-{
-#pragma unroll
-    for (int k = 0; k < kAcc; ++k) acc[k] = 0.0;
-    for (int i = threadIdx.x; i < sc.n; i += kLsThreads) {
-        const double r = sc.ranges[i];
-        const bool in_step = !(r >= smax || r <= smin);
-        const bool in_cost = !(r >= cmax || r <= cmin);
-        if (!in_step && !in_cost) continue;
-        double e, gv[3];
-        beam_terms(p, grid, pose, r, sc.angles[i], e, gv);
-        if (in_step) {
-            acc[0] += e * gv[0];
-            acc[1] += e * gv[1];
-            acc[2] += e * gv[2];
-            acc[3] += gv[0] * gv[0];
-            acc[4] += gv[0] * gv[1];
-            acc[5] += gv[0] * gv[2];
-            acc[6] += gv[1] * gv[1];
-            acc[7] += gv[1] * gv[2];
-            acc[8] += gv[2] * gv[2];
-        }
-        if (in_cost) {
-            acc[9] += e * e;   // pow(1.0 - S, 2.0): GCC folds it to the exact product
-            acc[10] += 2.0 * e * (-gv[0]);
-            acc[11] += 2.0 * e * (-gv[1]);
-            acc[12] += 2.0 * e * (-gv[2]);
-        }
-    }
-}
-
-// The 13 sums of one beam (zeros for a beam outside both filters)
+// The 13 terms of one beam (zeros for a beam outside both filters)
 __device__ __forceinline__ void beam_acc(bool in_step, bool in_cost, double e, const double gv[3],
                                          double (&t)[kAcc])
 {
@@ -447,58 +385,74 @@ __device__ __forceinline__ void beam_acc(bool in_step, bool in_cost, double e, c
     }
 }
 
-__device__ __forceinline__ void wave_total(double (&t)[kAcc])
+// Workgroup shape: kLsThreads threads evaluate up to kChunk beams per chunk
+// (a 1081-beam scan is one chunk), their terms staged in LDS rows of
+// kTermStride doubles (16-byte aligned rows; the 13 summing lanes read
+// distinct banks).
+constexpr int kLsThreads = 512;
+constexpr int kChunk = 1280;
+constexpr int kTermStride = kChunk + 2;
+
+struct LsLds {
+    double terms[kAcc][kTermStride];
+    double pose[3];
+};
+
+// s + row[0] + row[1] + ... + row[m-1], strictly in that order
+__device__ __forceinline__ double seq_add(double s, const double* __restrict__ row, int m)
 {
-#pragma unroll
-    for (int k = 0; k < kAcc; ++k)
-        for (int off = 32; off > 0; off >>= 1) t[k] += __shfl_xor(t[k], off, 64);
+    int j = 0;
+    for (; j + 8 <= m; j += 8) {
+        const double2 a = *(const double2*)(row + j);
+        const double2 b = *(const double2*)(row + j + 2);
+        const double2 c = *(const double2*)(row + j + 4);
+        const double2 d = *(const double2*)(row + j + 6);
+        s = s + a.x;
+        s = s + a.y;
+        s = s + b.x;
+        s = s + b.y;
+        s = s + c.x;
+        s = s + c.y;
+        s = s + d.x;
+        s = s + d.y;
+    }
+    for (; j < m; ++j) s = s + row[j];
+    return s;
 }
 
-// Summation order of a refine's sums (every kernel below uses it, so a lone
-// refine, split or not, is bit-identical to the same refine in a batch):
-// beams in groups of 64 (group g = beams 64 g .. 64 g + 63), each group summed
-// by the wave64 xor butterfly (every lane ends with the same bits), the group
-// totals then added in group order.
-constexpr int kGroup = 64;
-constexpr int kMaxGroups = 512;      // 32768 beams
-
-// One pass of the batch kernel at `pose`: group g evaluated by wave g % 8,
-// group totals through LDS, every thread returns the 13 totals.  Ends with a
-// barrier, so `red` may be rewritten by the next pass.
-__device__ __forceinline__ void group_pass(const LsPlan& p, const double* __restrict__ grid, const LsScanRef& sc,
+// One pass at `pose`: lane k < 13 of wave 0 returns sum k in beam order
+// (other threads return 0).  Ends with a barrier, so the LDS rows may be
+// rewritten by the next pass.
+__device__ __forceinline__ double seq_pass(const LsPlan& p, const double* __restrict__ grid, const LsScanRef& sc,
                                            const double pose[3], double smin, double smax, double cmin,
-                                           double cmax, double* red, double (&acc)[kAcc])
+                                           double cmax, LsLds& L)
 {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int G = (sc.n + kGroup - 1) / kGroup;
-    for (int g = wid; g < G; g += kLsThreads / 64) {
-        const int i = g * kGroup + lane;
-        bool in_step = false, in_cost = false;
-        double e = 0.0, gv[3] = { 0.0, 0.0, 0.0 };
-        if (i < sc.n) {
-            const double r = sc.ranges[i];
-            in_step = !(r >= smax || r <= smin);
-            in_cost = !(r >= cmax || r <= cmin);
-            if (in_step || in_cost) beam_terms(p, grid, pose, r, sc.angles[i], e, gv);
-        }
-        double t[kAcc];
-        beam_acc(in_step, in_cost, e, gv, t);
-        wave_total(t);
-        if (lane < kAcc) {
-            double v = t[0];
+    double s = 0.0;
+    for (int c0 = 0; c0 < sc.n; c0 += kChunk) {
+        const int m = min(kChunk, sc.n - c0);
+        for (int j = threadIdx.x; j < m; j += kLsThreads) {
+            const double r = sc.ranges[c0 + j];
+            const bool in_step = !(r >= smax || r <= smin);
+            const bool in_cost = !(r >= cmax || r <= cmin);
+            double e = 0.0, gv[3] = { 0.0, 0.0, 0.0 };
+            if (in_step || in_cost) beam_terms(p, grid, pose, r, sc.angles[c0 + j], e, gv);
+            double t[kAcc];
+            beam_acc(in_step, in_cost, e, gv, t);
 #pragma unroll
-            for (int k = 1; k < kAcc; ++k) v = (lane == k) ? t[k] : v;
-            red[g * kAcc + lane] = v;
+            for (int k = 0; k < kAcc; ++k) L.terms[k][j] = t[k];
         }
+        __syncthreads();
+        if (threadIdx.x < kAcc) s = seq_add(s, L.terms[threadIdx.x], m);
+        __syncthreads();
     }
-    __syncthreads();
+    return s;
+}
+
+// the 13 sums from lanes 0..12 of wave 0 into every lane of wave 0
+__device__ __forceinline__ void gather_sums(double s, double (&acc)[kAcc])
+{
 #pragma unroll
-    for (int k = 0; k < kAcc; ++k) {
-        double v = red[k];
-        for (int g = 1; g < G; ++g) v = v + red[g * kAcc + k];
-        acc[k] = v;
-    }
-    __syncthreads();
+    for (int k = 0; k < kAcc; ++k) acc[k] = __shfl(s, k, 64);
 }
 
 // One workgroup per scan: the whole OptimizePose loop (:48-69) + covariance.
@@ -507,15 +461,14 @@ __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double*
                                                          LsRecord* __restrict__ out,
                                                          double* __restrict__ traj)
 {
-    __shared__ double red[kMaxGroups * kAcc];
-    __shared__ double spose[3];
+    __shared__ LsLds L;
     const LsScanRef sc = scans[blockIdx.x];
     const double smin = fmax(p.step_min, sc.min_range), smax = fmin(p.step_max, sc.max_range);
     const double cmin = fmax(p.cost_min, sc.min_range), cmax = fmin(p.cost_max, sc.max_range);
     double pose[3] = { sc.pose0[0], sc.pose0[1], sc.pose0[2] };
     double prevCost = DBL_MAX, cost = DBL_MAX;
     double acc[kAcc];
-    group_pass(p, grid, sc, pose, smin, smax, cmin, cmax, red, acc);
+    gather_sums(seq_pass(p, grid, sc, pose, smin, smax, cmin, cmax, L), acc);   // wave 0 only is meaningful
     int it = 0;
     for (;;) {
         // OptimizeStep (:88-148): regularised normal equations, col-piv QR, pose += delta
@@ -526,18 +479,22 @@ __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double*
             const double b[3] = { acc[0], acc[1], acc[2] };
             double d[3];
             solve3_colpiv_qr(H, b, d);
-            spose[0] = pose[0] + d[0];
-            spose[1] = pose[1] + d[1];
-            spose[2] = pose[2] + d[2];
+            L.pose[0] = pose[0] + d[0];
+            L.pose[1] = pose[1] + d[1];
+            L.pose[2] = pose[2] + d[2];
         }
         __syncthreads();
-        pose[0] = spose[0];
-        pose[1] = spose[1];
-        pose[2] = spose[2];
+        pose[0] = L.pose[0];
+        pose[1] = L.pose[1];
+        pose[2] = L.pose[2];
         // cost at the new pose (and the next step's sums, and the covariance
-        // gradient should the loop stop here)
-        group_pass(p, grid, sc, pose, smin, smax, cmin, cmax, red, acc);
-        cost = acc[9];
+        // gradient should the loop stop here); every thread needs the cost
+        // for the stopping rule: through LDS
+        gather_sums(seq_pass(p, grid, sc, pose, smin, smax, cmin, cmax, L), acc);
+        if (threadIdx.x == 0) L.pose[0] = acc[9];
+        __syncthreads();
+        cost = L.pose[0];
+        __syncthreads();
         if (traj && threadIdx.x == 0) {
             double* tr = traj + ((size_t)blockIdx.x * max(1, p.max_iter) + it) * 4;
             tr[0] = pose[0];
@@ -563,292 +520,16 @@ __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double*
     }
 }
 
-// --------------------------------------------------------------------------
-// Split refine (a lone OptimizePose, the frontend's case).  One workgroup of
-// 8 waves per group of 64 beams (17 workgroups on 17 CUs for 1081 beams; with
-// more than kSplitMaxWG groups a workgroup takes groups wg, wg + nwg, ...).
-// The waves share the work of a beam (lane = beam): waves 0-5 compute the
-// hit cell and one bicubic axis each (x0, y0, xp, xm, yp, ym; through LDS),
-// waves 0-4 one smoothed value each, then waves 0-3 finish the beam (the same
-// bits in each), and each sums a quarter of the 13 group sums with the
-// butterfly and publishes them -- the same functions on the same inputs as
-// beam_terms, so the bits are the batch kernel's.  Measured per pass on
-// config 3 (LGS_LS_TRACE): hit cell + axes 1.45 us, smoothed values 1.1 us,
-// finish + sums + publish 1.5 -> (8 waves) less, hand-off 1.5-3.5 us after
-// the last publisher, 3x3 col-piv QR 1.65 us.
-// Per pass every group total is published as 26 write-through 8-byte granules
-// {tag = pass + 1, 32 bits of a double} (cdna_hip_programming.md,
-// publish/consume recipe R2: the data is the flag, agent-scope relaxed
-// atomics, no fence); wave 0 of every workgroup sweeps all G x 26 granules
-// until every tag matches, adds the totals in group order and runs the 3x3
-// solve itself, so every workgroup holds the identical pose and takes the
-// identical stopping decision (no broadcast, no second hand-off per pass).
-// Granules are double-buffered by pass parity: a workgroup publishes pass
-// p + 2 only after every workgroup has published p + 1, i.e. finished reading
-// pass p.  Spins are bounded (~0.2 s of s_memrealtime): on time-out the
-// timeout word is set, every workgroup leaves, and the host reports an error.
-// --------------------------------------------------------------------------
-constexpr int kSplitThreads = 512;
-constexpr int kSplitMaxWG = 64;
-constexpr int kSplitMaxGroups = 128;     // larger scans use one workgroup (k_linsolve)
-constexpr int kGran = 2 * kAcc;          // granules per group and pass
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned gu32;
-
-struct SplitLds {
-    Axis ax[6][kGroup];                  // x0, y0, xp, xm, yp, ym
-    double sv[5][kGroup];                // S(x0,y0), S(xp,y0), S(xm,y0), S(x0,yp), S(x0,ym)
-    double sc[2][kGroup];                // sin, cos of the beam angle
-    double br[kSplitMaxGroups / kSplitMaxWG][kGroup];   // the workgroup's ranges and angles, loaded once
-    double ba[kSplitMaxGroups / kSplitMaxWG][kGroup];
-    unsigned gran[kSplitMaxGroups * kGran];
-    double tot[kAcc];
-    double pose[3];
-    int stop;
-};
-
-// wave 0: wait for every group's granules of this pass, then the totals in
-// group order (every lane)
-__device__ __forceinline__ bool consume(gu64* __restrict__ slot, gu32* __restrict__ tmo, int G, unsigned epoch,
-                                        unsigned* __restrict__ lds, double (&acc)[kAcc])
-{
-    const int lane = threadIdx.x;
-    const int total = G * kGran;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (unsigned polls = 1;; ++polls) {
-        // every load of a sweep chunk in flight before the first is waited on
-        // (a strided loop waits on each load in turn: 7 round trips per poll)
-        bool ok = true;
-        for (int base = 0; base < total; base += 64 * 8) {
-            unsigned long long x[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int q = base + u * 64 + lane;
-                x[u] = (q < total) ? __hip_atomic_load(slot + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : ((unsigned long long)epoch << 32);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int q = base + u * 64 + lane;
-                if (q < total) lds[q] = (unsigned)x[u];
-                ok &= (unsigned)(x[u] >> 32) == epoch;
-            }
-        }
-        if (__all(ok)) break;
-        // the timeout word is one more round trip: looked at every 256 polls only
-        if ((polls & 255u) == 0u) {
-            if (__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {   // 100 MHz clock: 0.2 s
-                if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return false;
-            }
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    double sk = 0.0;
-    if (lane < kAcc)
-        for (int g = 0; g < G; ++g) {
-            const unsigned lo = lds[g * kGran + 2 * lane], hi = lds[g * kGran + 2 * lane + 1];
-            const double v = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-            sk = (g == 0) ? v : sk + v;
-        }
-#pragma unroll
-    for (int k = 0; k < kAcc; ++k) acc[k] = __shfl(sk, k, 64);
-    return true;
-}
-
-// the workgroup's groups of one pass; wave 0 publishes each group's totals
-// diagnostics (env LGS_LS_TRACE=1): workgroup 0 stamps s_memrealtime at the
-// phase boundaries of every pass
-__device__ __forceinline__ void stamp(unsigned long long* tr, int k)
-{
-    if (tr && blockIdx.x == 0 && threadIdx.x == 0) tr[k] = __builtin_amdgcn_s_memrealtime();
-}
-
-// wave w of the 4 finishing waves: sums kSumLo[w] .. kSumLo[w + 1] - 1
-__device__ __forceinline__ int sum_lo(int w) { return (w * kAcc + 3) / 4; }   // 0, 4, 7, 10, 13
-
-__device__ __forceinline__ void split_pass(const LsPlan& p, const double* __restrict__ grid, const LsScanRef& sc,
-                                           const double pose[3], double smin, double smax, double cmin, double cmax,
-                                           int G, gu64* __restrict__ slot, unsigned epoch, SplitLds& L,
-                                           unsigned long long* tr, unsigned long long* tr2)
-{
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int g = blockIdx.x, k = 0; g < G; g += gridDim.x, ++k) {
-        const int i = g * kGroup + lane;
-        bool in_step = false, in_cost = false;
-        double r = 0.0, sn = 0.0, cs = 0.0, fx = 0.0, fy = 0.0;
-        if (i < sc.n) {
-            r = L.br[k][lane];
-            in_step = !(r >= smax || r <= smin);
-            in_cost = !(r >= cmax || r <= cmin);
-        }
-        const bool act = in_step || in_cost;
-        // phase A: the hit cell (every wave), one axis per wave 0..5
-        if (act && wid < 6) {
-            beam_cell(p, pose, r, L.ba[k][lane], sn, cs, fx, fy);
-            const double d = kHalfDelta;
-            const bool isx = !(wid & 1);
-            const double v = (wid < 2) ? (isx ? fx : fy) : (wid < 4) ? (fx + ((wid == 2) ? d : -d))
-                                                                     : (fy + ((wid == 4) ? d : -d));
-            // ax order: x0, y0, xp, xm, yp, ym
-            L.ax[wid][lane] = make_axis(v, (wid == 0 || wid == 2 || wid == 3) ? p.W : p.H);
-            if (wid == 0) {
-                L.sc[0][lane] = sn;
-                L.sc[1][lane] = cs;
-            }
-        }
-        __syncthreads();
-        stamp(tr, 1);
-        // phase B: one smoothed value per wave 0..4
-        if (act && wid < 5) {
-            const int xa = (wid == 1) ? 2 : (wid == 2) ? 3 : 0;
-            const int ya = (wid == 3) ? 4 : (wid == 4) ? 5 : 1;
-            L.sv[wid][lane] = smoothed(grid, p.W, L.ax[xa][lane], L.ax[ya][lane]);
-        }
-        __syncthreads();
-        stamp(tr, 2);
-        // phase C: waves 0..3 finish the beam (identical bits in each), sum
-        // their share of the 13 sums over the group and publish it
-        if (wid < 4) {
-            double e = 0.0, gv[3] = { 0.0, 0.0, 0.0 };
-            if (act)
-                beam_finish(p, r, L.sc[0][lane], L.sc[1][lane], L.sv[0][lane], L.sv[1][lane], L.sv[2][lane],
-                            L.sv[3][lane], L.sv[4][lane], e, gv);
-            double t[kAcc];
-            beam_acc(in_step, in_cost, e, gv, t);
-            const int lo = sum_lo(wid), hi = sum_lo(wid + 1);
-#pragma unroll
-            for (int k = 0; k < kAcc; ++k)
-                if (k >= lo && k < hi)
-                    for (int off = 32; off > 0; off >>= 1) t[k] += __shfl_xor(t[k], off, 64);
-            // lane j < 2 (hi - lo) publishes half j & 1 of sum lo + (j >> 1)
-            if (lane == 0)
-#pragma unroll
-                for (int k = 0; k < kAcc; ++k)
-                    if (k >= lo && k < hi) L.tot[k] = t[k];
-            __builtin_amdgcn_wave_barrier();
-            const int nk = 2 * (hi - lo);
-            if (lane < nk) {
-                const double mine = L.tot[lo + (lane >> 1)];
-                const unsigned long long bits = (unsigned long long)__double_as_longlong(mine);
-                const unsigned half = (lane & 1) ? (unsigned)(bits >> 32) : (unsigned)bits;
-                __hip_atomic_store(slot + (size_t)g * kGran + 2 * lo + lane, ((unsigned long long)epoch << 32) | half,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            stamp(tr, 3);
-            if (tr2 && threadIdx.x == 0) tr2[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-        }
-        __syncthreads();   // LDS axes / values free for the next group
-    }
-}
-
-__global__ __launch_bounds__(kSplitThreads) void k_linsolve_split(LsPlan p, const double* __restrict__ grid,
-                                                                  LsScanRef sc, LsRecord* __restrict__ out,
-                                                                  double* __restrict__ traj,
-                                                                  gu64* __restrict__ gran, gu32* __restrict__ tmo,
-                                                                  unsigned long long* __restrict__ trace)
-{
-    __shared__ SplitLds L;
-    const int wid = threadIdx.x >> 6;
-    const double smin = fmax(p.step_min, sc.min_range), smax = fmin(p.step_max, sc.max_range);
-    const double cmin = fmax(p.cost_min, sc.min_range), cmax = fmin(p.cost_max, sc.max_range);
-    const int G = (sc.n + kGroup - 1) / kGroup;
-    double pose[3] = { sc.pose0[0], sc.pose0[1], sc.pose0[2] };
-    // the workgroup's beams stay in LDS for every pass
-    for (int g = blockIdx.x, k = 0; g < G; g += gridDim.x, ++k)
-        if (threadIdx.x < kGroup && g * kGroup + (int)threadIdx.x < sc.n) {
-            L.br[k][threadIdx.x] = sc.ranges[g * kGroup + threadIdx.x];
-            L.ba[k][threadIdx.x] = sc.angles[g * kGroup + threadIdx.x];
-        }
-    __syncthreads();
-    double acc[kAcc];
-    int pass_idx = 0;
-    double prevCost = DBL_MAX, cost = DBL_MAX;
-    int it = 0;
-    for (;;) {
-        gu64* slot = gran + (size_t)(pass_idx & 1) * kSplitMaxGroups * kGran;
-        const unsigned epoch = (unsigned)pass_idx + 1u;
-        unsigned long long* tr = trace ? trace + (size_t)min(pass_idx, 127) * 8 : nullptr;
-        unsigned long long* tr2 = trace ? trace + 128 * 8 + (size_t)min(pass_idx, 127) * 64 : nullptr;
-        stamp(tr, 0);
-        split_pass(p, grid, sc, pose, smin, smax, cmin, cmax, G, slot, epoch, L, tr, tr2);
-        if (wid == 0) {
-            int stop = 0;
-            const bool ok = consume(slot, tmo, G, epoch, L.gran, acc);
-            stamp(tr, 4);
-            if (!ok) {
-                stop = 2;
-            } else {
-                if (pass_idx > 0) {
-                    cost = acc[9];
-                    if (traj && blockIdx.x == 0 && threadIdx.x == 0) {
-                        double* tr = traj + (size_t)it * 4;
-                        tr[0] = pose[0];
-                        tr[1] = pose[1];
-                        tr[2] = pose[2];
-                        tr[3] = cost;
-                    }
-                    if (++it >= p.max_iter || fabs(prevCost - cost) < p.conv) stop = 1;
-                    prevCost = cost;
-                }
-                if (!stop) {
-                    // OptimizeStep (:88-148), solved by every lane of wave 0 of every workgroup
-                    const double H[9] = { acc[3] + p.reg_t, acc[4], acc[5],
-                                          acc[4], acc[6] + p.reg_t, acc[7],
-                                          acc[5], acc[7], acc[8] + p.reg_r };
-                    const double b[3] = { acc[0], acc[1], acc[2] };
-                    double d[3];
-                    solve3_colpiv_qr(H, b, d);
-                    pose[0] = pose[0] + d[0];
-                    pose[1] = pose[1] + d[1];
-                    pose[2] = pose[2] + d[2];
-                }
-            }
-            stamp(tr, 5);
-            if (threadIdx.x == 0) {
-                L.pose[0] = pose[0];
-                L.pose[1] = pose[1];
-                L.pose[2] = pose[2];
-                L.stop = stop;
-            }
-        }
-        __syncthreads();
-        const int stop = L.stop;
-        pose[0] = L.pose[0];
-        pose[1] = L.pose[1];
-        pose[2] = L.pose[2];
-        __syncthreads();
-        if (stop == 2) return;
-        if (stop) break;
-        ++pass_idx;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        LsRecord rec;
-        rec.pose[0] = pose[0];
-        rec.pose[1] = pose[1];
-        rec.pose[2] = pose[2];
-        rec.cost = cost;
-        rec.grad[0] = acc[10];
-        rec.grad[1] = acc[11];
-        rec.grad[2] = acc[12];
-        rec.iterations = it;
-        rec.pad = 0;
-        out[0] = rec;
-    }
-}
-
 // CostSquareError::Cost and ComputeGradient sums at one pose (diagnostics):
 // out[0] = cost, out[1..3] = sum 2 e (-grad)
 __global__ __launch_bounds__(kLsThreads) void k_sq_cost(LsPlan p, const double* __restrict__ grid,
                                                         LsScanRef sc, double* __restrict__ out)
 {
-    __shared__ double red[kAcc * (kLsThreads / 64)];
+    __shared__ LsLds L;
     const double cmin = fmax(p.cost_min, sc.min_range), cmax = fmin(p.cost_max, sc.max_range);
     double acc[kAcc];
     // step filter empty: only the cost-side sums are accumulated
-    pass(p, grid, sc, sc.pose0, 0.0, 0.0, cmin, cmax, acc);
-    wg_sum(acc, red);
+    gather_sums(seq_pass(p, grid, sc, sc.pose0, 0.0, 0.0, cmin, cmax, L), acc);
     if (threadIdx.x == 0) {
         out[0] = acc[9];
         out[1] = acc[10];
@@ -908,64 +589,24 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     std::vector<LsScanRef> refs(n);
     for (int j = 0; j < n; ++j) {
         LGS_REQUIRE(scans[j] && scans[j]->n >= 1, "empty scan");
-        LGS_REQUIRE(scans[j]->n <= kMaxGroups * kGroup, "scan has more than 32768 beams");
         refs[j] = scan_ref(scans[j], init[j]);
     }
     // pinned staging: [refs | records | trajectory]
     const size_t b_refs = sizeof(LsScanRef) * n, b_rec = sizeof(LsRecord) * n;
     const size_t b_traj = traj ? sizeof(double) * 4 * (size_t)iters * n : 0;
-    char* h = (char*)ctx->ensure_pinned(b_refs + b_rec + b_traj + 16);   // + the split refine's timeout word
+    char* h = (char*)ctx->ensure_pinned(b_refs + b_rec + b_traj);
     std::memcpy(h, refs.data(), b_refs);
     char* d = (char*)ctx->ensure(S_LIN0, b_refs + b_rec + b_traj);
     LGS_HIP_CHECK(hipMemcpyAsync(d, h, b_refs, hipMemcpyHostToDevice, ctx->stream));
-    const int groups = (refs[0].n + kGroup - 1) / kGroup;
-    const bool split = n == 1 && ctx->linsolve_split && groups <= kSplitMaxGroups;
-    const int split_wg = std::min(groups, kSplitMaxWG);
-    constexpr size_t b_gran = sizeof(unsigned long long) * 2 * kSplitMaxGroups * kGran;   // multiple of 16
-    char* hs = split ? (char*)ctx->ensure(S_LIN2, b_gran + 16) : nullptr;
-    if (split)   // granule tags and the timeout word zeroed every call (one block from the start)
-        LGS_HIP_CHECK(hipMemsetAsync(hs, 0, b_gran + 16, ctx->stream));
-    // diagnostics: LGS_LS_TRACE=1 prints the split refine's phase stamps
-    static const bool trace_on = getenv("LGS_LS_TRACE") != nullptr;
-    unsigned long long* trace_dev = nullptr;
-    if (split && trace_on) {
-        trace_dev = (unsigned long long*)ctx->ensure(S_LIN3, 128 * 72 * sizeof(unsigned long long));
-        LGS_HIP_CHECK(hipMemsetAsync(trace_dev, 0, 128 * 72 * sizeof(unsigned long long), ctx->stream));
-    }
     const int tok = ctx->timing_begin(K_LINSOLVE, 0.0);
-    if (split)
-        hipLaunchKernelGGL(k_linsolve_split, dim3(split_wg), dim3(kSplitThreads), 0, ctx->stream, p, grid->d, refs[0],
-                           (LsRecord*)(d + b_refs), traj ? (double*)(d + b_refs + b_rec) : nullptr, (gu64*)hs,
-                           (gu32*)(hs + b_gran), trace_dev);
-    else
-        hipLaunchKernelGGL(k_linsolve, dim3(n), dim3(kLsThreads), 0, ctx->stream, p, grid->d,
-                           (const LsScanRef*)d, (LsRecord*)(d + b_refs),
-                           traj ? (double*)(d + b_refs + b_rec) : nullptr);
+    hipLaunchKernelGGL(k_linsolve, dim3(n), dim3(kLsThreads), 0, ctx->stream, p, grid->d,
+                       (const LsScanRef*)d, (LsRecord*)(d + b_refs), traj ? (double*)(d + b_refs + b_rec) : nullptr);
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
     LGS_HIP_CHECK(hipMemcpyAsync(h + b_refs, d + b_refs, b_rec + b_traj, hipMemcpyDeviceToHost,
                                  ctx->stream));
-    unsigned* htmo = (unsigned*)(h + b_refs + b_rec + b_traj);
-    if (split) LGS_HIP_CHECK(hipMemcpyAsync(htmo, hs + b_gran, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
     ctx->sync();
     if (ctx->profile) ctx->harvest();
-    if (split && *htmo != 0u) throw Error(LGS_ERR_INTERNAL, "split refine: in-launch hand-off timed out");
-    if (trace_dev) {
-        std::vector<unsigned long long> t(128 * 72);
-        LGS_HIP_CHECK(hipMemcpy(t.data(), trace_dev, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost));
-        for (int q = 0; q < 128 && t[q * 8]; ++q) {
-            fprintf(stderr, "LSTRACE pass %d:", q);
-            for (int k = 1; k < 6; ++k)
-                fprintf(stderr, " %.2f", t[q * 8 + k] ? 0.01 * (double)(t[q * 8 + k] - t[q * 8]) : -1.0);
-            if (q + 1 < 128 && t[(q + 1) * 8]) fprintf(stderr, " | next %.2f", 0.01 * (double)(t[(q + 1) * 8] - t[q * 8]));
-            fprintf(stderr, " | pub");
-            for (int w = 0; w < split_wg; ++w) {
-                const unsigned long long v = t[128 * 8 + q * 64 + w];
-                fprintf(stderr, " %.2f", v ? 0.01 * ((double)v - (double)t[q * 8]) : -1.0);
-            }
-            fprintf(stderr, "\n");
-        }
-    }
     const LsRecord* rec = (const LsRecord*)(h + b_refs);
     for (int j = 0; j < n; ++j) {
         lgs_linsolve_summary& o = out[j];
@@ -1043,5 +684,38 @@ extern "C" int lgs_cost_square_error(lgs_ctx* ctx, const lgs_grid* grid, double 
             out_cov[4] += 0.01;
             out_cov[8] += 0.01;
         }
+    });
+}
+
+namespace {
+__global__ void k_debug_libm(int op, const double* __restrict__ x, int n, double* __restrict__ out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (op == 0) {
+        double s, c;
+        glm::gl_sincos(x[i], &s, &c);
+        out[2 * i] = s;
+        out[2 * i + 1] = c;
+    } else {
+        out[i] = glm::gl_pow3(x[i]);
+    }
+}
+}  // namespace
+
+extern "C" int lgs_debug_libm(lgs_ctx* ctx, int op, const double* x, int n, double* out)
+{
+    if (!ctx || !x || !out || n < 0 || (op != 0 && op != 1)) return LGS_ERR_INVALID_ARG;
+    if (n == 0) return LGS_OK;
+    return guarded(ctx, [&] {
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        const size_t bin = sizeof(double) * n, bout = bin * (op == 0 ? 2 : 1);
+        char* d = (char*)ctx->ensure(S_LIN1, bin + bout);
+        LGS_HIP_CHECK(hipMemcpyAsync(d, x, bin, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_debug_libm, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, op, (const double*)d, n,
+                           (double*)(d + bin));
+        LGS_HIP_CHECK(hipGetLastError());
+        LGS_HIP_CHECK(hipMemcpyAsync(out, d + bin, bout, hipMemcpyDeviceToHost, ctx->stream));
+        ctx->sync();
     });
 }

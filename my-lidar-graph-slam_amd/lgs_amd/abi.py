@@ -31,7 +31,6 @@ LGS_OPT_RAY_CHUNK_KEYS = 13
 LGS_OPT_SUPER_HEX = 14
 LGS_OPT_POISON_WS = 15   # diagnostics only
 LGS_OPT_FINE_LANES = 16
-LGS_OPT_LINSOLVE_SPLIT = 17
 LGS_OPT_SKIP_MASK = 10   # diagnostics only
 KERNEL_IDS = ["k_project", "k_coarse", "k_seed", "k_select", "k_fine", "k_replay", "k_cost", "k_precompute",
               "k_linsolve", "k_ray_emit", "k_ray_apply", "k_super", "k_super_planes", "k_bb_score",
@@ -247,6 +246,7 @@ _PROTOS = [
     ("lgs_cost_square_error", C.c_int, [_P, _P, C.c_double, C.c_double, _P, Pose2D, C.POINTER(C.c_double),
                                         C.POINTER(C.c_double)]),
     ("lgs_debug_item_buffer", C.c_int, [_P, C.c_int, C.c_int, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("lgs_debug_libm", C.c_int, [_P, C.c_int, _P, C.c_int, _P]),
 ]
 
 SYMBOLS = [p[0] for p in _PROTOS]
@@ -565,6 +565,15 @@ class Context:
         self.check(self.lib.lgs_debug_item_buffer(self.h, item, which, out.ctypes.data_as(_P), out.nbytes,
                                                   C.byref(n)),
                    "debug_item_buffer")
+        return out
+
+    def debug_libm(self, op: int, x) -> np.ndarray:
+        """Diagnostics: the device's glibc sincos (op 0, rows of (sin, cos)) or
+        pow(x, 3.0) (op 1) on the GPU (lgs_debug_libm)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.zeros((len(x), 2) if op == 0 else len(x), dtype=np.float64)
+        self.check(self.lib.lgs_debug_libm(self.h, op, x.ctypes.data_as(_P), len(x), out.ctypes.data_as(_P)),
+                   "debug_libm")
         return out
 
     def cost_greedy_endpoint(self, grid, cost: CostGEParams, scan, pose) -> float:
