@@ -171,6 +171,8 @@ int  lgs_abi_version(void);
 #define LGS_OPT_RAY_CHUNK_KEYS 13  /* ray-cast keys per emit/sort/apply pass (default 2^28, max 2^30); more keys are cast in scan order over several passes */
 #define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: lane-per-block kernel for batches of at least this many matches (default 2; 1 = always), else the row kernel */
 #define LGS_OPT_FINE_LANES    16  /* 1 (default) = fine stage with one lane per pose over the batch's block list, 0 = transposed row evaluator (A/B) */
+#define LGS_OPT_LINSOLVE_SPLIT 17 /* 1 (default) = a lone ScanMatcherLinearSolver refine of <= 1280 beams runs one workgroup per 64 beams (in-launch hand-off per pass) when they fit the device at once, 0 = one workgroup */
+#define LGS_OPT_HANDOFF_SPIN_US 18 /* split refine: bound of a workgroup's wait for the others (default 200000 us); on time-out the refine is rerun on one workgroup.  0 = force that fallback (tests) */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

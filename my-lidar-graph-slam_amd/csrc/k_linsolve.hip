@@ -393,28 +393,56 @@ constexpr int kLsThreads = 512;
 constexpr int kChunk = 1280;
 constexpr int kTermStride = kChunk + 2;
 
-struct LsLds {
+struct alignas(16) LsLds {
     double terms[kAcc][kTermStride];
     double pose[3];
 };
 
-// s + row[0] + row[1] + ... + row[m-1], strictly in that order
+// s + row[0] + row[1] + ... + row[m-1], strictly in that order (LDS row,
+// 16-byte aligned).  Software-pipelined with two register buffers of 12
+// terms: one buffer's loads are in flight while the other's are added, so
+// the chain waits on the adds only.
+constexpr int kSeqBuf = 6;   // double2 per buffer (two buffers in flight stay within lgkmcnt's 15)
+
+__device__ __forceinline__ double add_buf(double s, const double2 (&a)[kSeqBuf])
+{
+#pragma unroll
+    for (int q = 0; q < kSeqBuf; ++q) {
+        s = s + a[q].x;
+        s = s + a[q].y;
+    }
+    return s;
+}
+
+__device__ __forceinline__ void load_buf(double2 (&a)[kSeqBuf], const double* __restrict__ p)
+{
+#pragma unroll
+    for (int q = 0; q < kSeqBuf; ++q) a[q] = *(const double2*)(p + 2 * q);
+}
+
 __device__ __forceinline__ double seq_add(double s, const double* __restrict__ row, int m)
 {
+    constexpr int B = 2 * kSeqBuf;   // terms per buffer
     int j = 0;
-    for (; j + 8 <= m; j += 8) {
-        const double2 a = *(const double2*)(row + j);
-        const double2 b = *(const double2*)(row + j + 2);
-        const double2 c = *(const double2*)(row + j + 4);
-        const double2 d = *(const double2*)(row + j + 6);
-        s = s + a.x;
-        s = s + a.y;
-        s = s + b.x;
-        s = s + b.y;
-        s = s + c.x;
-        s = s + c.y;
-        s = s + d.x;
-        s = s + d.y;
+    if (m >= 2 * B) {
+        double2 a[kSeqBuf], b[kSeqBuf];
+        load_buf(a, row);
+        load_buf(b, row + B);
+        for (j = 2 * B; j + 2 * B <= m; j += 2 * B) {
+            // the scheduling barriers keep each buffer's loads issued a whole
+            // buffer of adds before its first use
+            __builtin_amdgcn_sched_barrier(0);
+            s = add_buf(s, a);
+            __builtin_amdgcn_sched_barrier(0);
+            load_buf(a, row + j);
+            __builtin_amdgcn_sched_barrier(0);
+            s = add_buf(s, b);
+            __builtin_amdgcn_sched_barrier(0);
+            load_buf(b, row + j + B);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        s = add_buf(s, a);
+        s = add_buf(s, b);
     }
     for (; j < m; ++j) s = s + row[j];
     return s;
@@ -520,6 +548,235 @@ __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double*
     }
 }
 
+// --------------------------------------------------------------------------
+// Split refine (a lone OptimizePose, the frontend's case): one workgroup of 8
+// waves per group of 64 beams (17 workgroups on 17 CUs for 1081 beams), all
+// passes in one launch.  The waves share the work of a beam (lane = beam):
+// waves 0-5 compute the hit point and one bicubic axis each (x0, y0, xp, xm,
+// yp, ym; 4 glibc pow() per axis) into LDS, waves 0-4 one smoothed value
+// each, wave 0 finishes the beam -- the functions of beam_terms on the same
+// inputs, so the bits are the batch kernel's.  Every workgroup publishes its
+// beams' 13 terms (write-through stores, one flag per group;
+// cdna_hip_programming.md Guideline 16, recipe R1), then EVERY workgroup
+// waits for all groups, stages all terms into LDS and adds them in beam order
+// (13 lanes of wave 0) and solves the 3x3 system itself: every workgroup
+// holds the identical pose and takes the identical stopping decision, no
+// broadcast.  Terms and flags are double-buffered by pass parity: a
+// workgroup publishes pass p + 2 only after every group has published p + 1,
+// i.e. finished reading pass p.
+// Residency: the host launches it only when the device can hold all its
+// workgroups at once (occupancy query); spins are bounded (~0.2 s of
+// s_memrealtime) and on time-out every workgroup leaves and the host reruns
+// the refine with k_linsolve (one workgroup), which computes the same bits.
+// --------------------------------------------------------------------------
+constexpr int kGroup = 64;
+constexpr int kSplitThreads = 512;
+constexpr int kSplitMaxGroups = kChunk / kGroup;          // 20 groups: 1280 beams
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+struct alignas(16) SplitLds {
+    union {
+        struct {
+            Axis ax[6][kGroup];       // x0, y0, xp, xm, yp, ym
+            double sv[5][kGroup];     // S(x0,y0), S(xp,y0), S(xm,y0), S(x0,yp), S(x0,ym)
+            double sc[2][kGroup];     // sin, cos of the beam angle
+        } b;
+        double terms[kAcc][kTermStride];   // all groups' terms of one pass, beam order per row
+    } u;
+    double pose[3];
+    int stop;
+};
+
+__device__ __forceinline__ bool spin_expired(unsigned long long t0, unsigned long long limit)
+{
+    return __builtin_amdgcn_s_memrealtime() - t0 > limit;
+}
+
+__global__ __launch_bounds__(kSplitThreads) void k_linsolve_split(LsPlan p, const double* __restrict__ grid,
+                                                                  LsScanRef sc, LsRecord* __restrict__ out,
+                                                                  double* __restrict__ traj, gu64* __restrict__ tbuf,
+                                                                  gu32* __restrict__ flags, gu32* __restrict__ tmo,
+                                                                  unsigned long long spin_limit,
+                                                                  unsigned long long* __restrict__ trace)
+{
+    __shared__ SplitLds L;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const double smin = fmax(p.step_min, sc.min_range), smax = fmin(p.step_max, sc.max_range);
+    const double cmin = fmax(p.cost_min, sc.min_range), cmax = fmin(p.cost_max, sc.max_range);
+    const int G = (sc.n + kGroup - 1) / kGroup;
+    const int g = blockIdx.x;                      // this workgroup's group (gridDim.x == G)
+    const int i = g * kGroup + lane;
+    // the workgroup's beam (lane) stays in registers for every pass
+    double r = 0.0, ang = 0.0;
+    bool in_step = false, in_cost = false;
+    if (i < sc.n) {
+        r = sc.ranges[i];
+        ang = sc.angles[i];
+        in_step = !(r >= smax || r <= smin);
+        in_cost = !(r >= cmax || r <= cmin);
+    }
+    const bool act = in_step || in_cost;
+    if (spin_limit == 0ull) {                      // diagnostics: the host's time-out fallback
+        if (threadIdx.x == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    double pose[3] = { sc.pose0[0], sc.pose0[1], sc.pose0[2] };
+    double acc[kAcc];
+    double prevCost = DBL_MAX, cost = DBL_MAX;
+    int it = 0;
+    for (int pass = 0;; ++pass) {
+        const unsigned epoch = (unsigned)pass + 1u;
+        gu64* tb = tbuf + (size_t)(pass & 1) * kSplitMaxGroups * kAcc * kGroup;
+        gu32* fl = flags + (pass & 1) * kSplitMaxGroups;
+        unsigned long long* tr = (trace && blockIdx.x == 0 && threadIdx.x == 0) ? trace + (size_t)min(pass, 127) * 8
+                                                                                : nullptr;
+        if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
+        // phase A: the hit point (every wave), one axis per wave 0..5
+        if (act && wid < 6) {
+            double sn, cs, fx, fy;
+            beam_cell(p, pose, r, ang, sn, cs, fx, fy);
+            const double d = kHalfDelta;
+            const bool isx = !(wid & 1);
+            const double v = (wid < 2) ? (isx ? fx : fy) : (wid < 4) ? (fx + ((wid == 2) ? d : -d))
+                                                                     : (fy + ((wid == 4) ? d : -d));
+            L.u.b.ax[wid][lane] = make_axis(v, (wid == 0 || wid == 2 || wid == 3) ? p.W : p.H);
+            if (wid == 0) {
+                L.u.b.sc[0][lane] = sn;
+                L.u.b.sc[1][lane] = cs;
+            }
+        }
+        __syncthreads();
+        if (tr) tr[1] = __builtin_amdgcn_s_memrealtime();
+        // phase B: one smoothed value per wave 0..4
+        if (act && wid < 5) {
+            const int xa = (wid == 1) ? 2 : (wid == 2) ? 3 : 0;
+            const int ya = (wid == 3) ? 4 : (wid == 4) ? 5 : 1;
+            L.u.b.sv[wid][lane] = smoothed(grid, p.W, L.u.b.ax[xa][lane], L.u.b.ax[ya][lane]);
+        }
+        __syncthreads();
+        if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
+        // phase C: wave 0 finishes the beam and publishes its 13 terms
+        // write-through (sc1) with the group's flag (recipe R1)
+        if (wid == 0) {
+            double e = 0.0, gv[3] = { 0.0, 0.0, 0.0 };
+            if (act)
+                beam_finish(p, r, L.u.b.sc[0][lane], L.u.b.sc[1][lane], L.u.b.sv[0][lane], L.u.b.sv[1][lane],
+                            L.u.b.sv[2][lane], L.u.b.sv[3][lane], L.u.b.sv[4][lane], e, gv);
+            double t[kAcc];
+            beam_acc(in_step, in_cost, e, gv, t);
+#pragma unroll
+            for (int k = 0; k < kAcc; ++k)
+                __hip_atomic_store(tb + ((size_t)g * kAcc + k) * kGroup + lane,
+                                   (unsigned long long)__double_as_longlong(t[k]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(fl + g, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
+            // wait for every group's flag (lane j polls group j), then one acquire
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            int stop = 0;
+            for (unsigned polls = 1;; ++polls) {
+                bool ok = true;
+                if (lane < G)
+                    ok = __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+                if (__all(ok)) break;
+                if ((polls & 255u) == 0u &&
+                    (__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                     spin_expired(t0, spin_limit))) {
+                    if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stop = 2;
+                    break;
+                }
+            }
+            // every load of the handed-off terms below is an sc1 (agent-scope
+            // atomic) load, so no acquire fence is needed (Guideline 16)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane == 0) L.stop = stop;
+        }
+        __syncthreads();
+        if (tr) tr[4] = __builtin_amdgcn_s_memrealtime();
+        if (L.stop == 2) return;
+        // every wave stages rows (group, term) of the pass into LDS rows in
+        // beam order: one coalesced 512-byte row per load, all of a wave's
+        // loads in flight before the first LDS store
+        {
+            constexpr int kRowsPerWave = (kSplitMaxGroups * kAcc + kSplitThreads / 64 - 1) / (kSplitThreads / 64);
+            const int rows = G * kAcc;
+            unsigned long long v[kRowsPerWave];
+#pragma unroll
+            for (int q = 0; q < kRowsPerWave; ++q) {
+                const int row = wid + q * (kSplitThreads / 64);
+                v[q] = row < rows ? __hip_atomic_load(tb + (size_t)row * kGroup + lane, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0ull;
+            }
+#pragma unroll
+            for (int q = 0; q < kRowsPerWave; ++q) {
+                const int row = wid + q * (kSplitThreads / 64);
+                if (row < rows) {
+                    const int gg = row / kAcc, k = row - gg * kAcc;
+                    L.u.terms[k][gg * kGroup + lane] = __longlong_as_double((long long)v[q]);
+                }
+            }
+        }
+        __syncthreads();
+        if (tr) tr[5] = __builtin_amdgcn_s_memrealtime();
+        if (wid == 0) {
+            const double sk = (lane < kAcc) ? seq_add(0.0, L.u.terms[lane], sc.n) : 0.0;
+            gather_sums(sk, acc);
+            if (tr) tr[6] = __builtin_amdgcn_s_memrealtime();
+            int stop = 0;
+            if (pass > 0) {
+                cost = acc[9];
+                if (traj && g == 0 && lane == 0) {
+                    double* tr = traj + (size_t)it * 4;
+                    tr[0] = pose[0];
+                    tr[1] = pose[1];
+                    tr[2] = pose[2];
+                    tr[3] = cost;
+                }
+                if (++it >= p.max_iter || fabs(prevCost - cost) < p.conv) stop = 1;
+                prevCost = cost;
+            }
+            if (!stop && lane == 0) {
+                // OptimizeStep (:88-148), solved by lane 0 of every workgroup
+                const double H[9] = { acc[3] + p.reg_t, acc[4], acc[5],
+                                      acc[4], acc[6] + p.reg_t, acc[7],
+                                      acc[5], acc[7], acc[8] + p.reg_r };
+                const double b[3] = { acc[0], acc[1], acc[2] };
+                double dd[3];
+                solve3_colpiv_qr(H, b, dd);
+                L.pose[0] = pose[0] + dd[0];
+                L.pose[1] = pose[1] + dd[1];
+                L.pose[2] = pose[2] + dd[2];
+            }
+            if (lane == 0) L.stop = stop;
+            if (tr) tr[7] = __builtin_amdgcn_s_memrealtime();
+        }
+        __syncthreads();
+        const int stop = L.stop;
+        if (stop) break;
+        pose[0] = L.pose[0];
+        pose[1] = L.pose[1];
+        pose[2] = L.pose[2];
+        __syncthreads();
+    }
+    if (g == 0 && threadIdx.x == 0) {
+        LsRecord rec;
+        rec.pose[0] = pose[0];
+        rec.pose[1] = pose[1];
+        rec.pose[2] = pose[2];
+        rec.cost = cost;
+        rec.grad[0] = acc[10];
+        rec.grad[1] = acc[11];
+        rec.grad[2] = acc[12];
+        rec.iterations = it;
+        rec.pad = 0;
+        out[0] = rec;
+    }
+}
+
 // CostSquareError::Cost and ComputeGradient sums at one pose (diagnostics):
 // out[0] = cost, out[1..3] = sum 2 e (-grad)
 __global__ __launch_bounds__(kLsThreads) void k_sq_cost(LsPlan p, const double* __restrict__ grid,
@@ -594,19 +851,84 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     // pinned staging: [refs | records | trajectory]
     const size_t b_refs = sizeof(LsScanRef) * n, b_rec = sizeof(LsRecord) * n;
     const size_t b_traj = traj ? sizeof(double) * 4 * (size_t)iters * n : 0;
-    char* h = (char*)ctx->ensure_pinned(b_refs + b_rec + b_traj);
+    char* h = (char*)ctx->ensure_pinned(b_refs + b_rec + b_traj + 16);   // + the split refine's timeout word
     std::memcpy(h, refs.data(), b_refs);
     char* d = (char*)ctx->ensure(S_LIN0, b_refs + b_rec + b_traj);
     LGS_HIP_CHECK(hipMemcpyAsync(d, h, b_refs, hipMemcpyHostToDevice, ctx->stream));
+    // a lone refine of at most kSplitMaxGroups groups runs split over one
+    // workgroup per group when the device can hold all of them at once
+    const int groups = (refs[0].n + kGroup - 1) / kGroup;
+    bool split = n == 1 && ctx->linsolve_split && groups <= kSplitMaxGroups && groups > 1;
+    if (split) {
+        static int cus = -1, per_cu = -1;
+        if (cus < 0) {
+            hipDeviceProp_t prop;
+            LGS_HIP_CHECK(hipGetDeviceProperties(&prop, ctx->device));
+            cus = prop.multiProcessorCount;
+            LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_linsolve_split, kSplitThreads, 0));
+        }
+        split = per_cu * cus >= groups;
+    }
+    // split hand-off state: [flags (2 x kSplitMaxGroups) | timeout word | pad] then the terms
+    constexpr size_t b_flags = 16 * ((sizeof(unsigned) * (2 * kSplitMaxGroups + 1) + 15) / 16);
+    constexpr size_t b_terms = sizeof(double) * 2 * kSplitMaxGroups * kAcc * kGroup;
+    char* hs = split ? (char*)ctx->ensure(S_LIN2, b_flags + b_terms) : nullptr;
+    unsigned* htmo = (unsigned*)(h + b_refs + b_rec + b_traj);
+    // diagnostics: LGS_LS_TRACE=1 prints the split refine's per-pass phase
+    // stamps of workgroup 0 (us after the pass start: axes, smoothed values,
+    // published, all groups seen, terms staged, summed, solved | next pass)
+    static const bool trace_on = getenv("LGS_LS_TRACE") != nullptr;
+    unsigned long long* trace_dev = nullptr;
+    if (split && trace_on) {
+        trace_dev = (unsigned long long*)ctx->ensure(S_LIN3, 128 * 8 * sizeof(unsigned long long));
+        LGS_HIP_CHECK(hipMemsetAsync(trace_dev, 0, 128 * 8 * sizeof(unsigned long long), ctx->stream));
+    }
+    *htmo = 0u;
+    const auto launch_one_wg = [&] {
+        hipLaunchKernelGGL(k_linsolve, dim3(n), dim3(kLsThreads), 0, ctx->stream, p, grid->d, (const LsScanRef*)d,
+                           (LsRecord*)(d + b_refs), traj ? (double*)(d + b_refs + b_rec) : nullptr);
+    };
     const int tok = ctx->timing_begin(K_LINSOLVE, 0.0);
-    hipLaunchKernelGGL(k_linsolve, dim3(n), dim3(kLsThreads), 0, ctx->stream, p, grid->d,
-                       (const LsScanRef*)d, (LsRecord*)(d + b_refs), traj ? (double*)(d + b_refs + b_rec) : nullptr);
+    if (split) {
+        LGS_HIP_CHECK(hipMemsetAsync(hs, 0, b_flags, ctx->stream));   // flags + timeout word, every call
+        hipLaunchKernelGGL(k_linsolve_split, dim3(groups), dim3(kSplitThreads), 0, ctx->stream, p, grid->d, refs[0],
+                           (LsRecord*)(d + b_refs), traj ? (double*)(d + b_refs + b_rec) : nullptr,
+                           (gu64*)(hs + b_flags), (gu32*)hs, (gu32*)(hs + sizeof(unsigned) * 2 * kSplitMaxGroups),
+                           (unsigned long long)ctx->handoff_spin_us * 100ull,    // s_memrealtime: 100 MHz
+                           trace_dev);
+    } else {
+        launch_one_wg();
+    }
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
+    if (split)
+        LGS_HIP_CHECK(hipMemcpyAsync(htmo, hs + sizeof(unsigned) * 2 * kSplitMaxGroups, sizeof(unsigned),
+                                     hipMemcpyDeviceToHost, ctx->stream));
     LGS_HIP_CHECK(hipMemcpyAsync(h + b_refs, d + b_refs, b_rec + b_traj, hipMemcpyDeviceToHost,
                                  ctx->stream));
     ctx->sync();
+    if (split && *htmo != 0u) {
+        // the split refine's workgroups were not all resident (time-out): the
+        // one-workgroup kernel computes the same bits
+        ++ctx->handoff_fallbacks;
+        launch_one_wg();
+        LGS_HIP_CHECK(hipGetLastError());
+        LGS_HIP_CHECK(hipMemcpyAsync(h + b_refs, d + b_refs, b_rec + b_traj, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+        ctx->sync();
+    }
     if (ctx->profile) ctx->harvest();
+    if (trace_dev) {
+        std::vector<unsigned long long> t(128 * 8);
+        LGS_HIP_CHECK(hipMemcpy(t.data(), trace_dev, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost));
+        for (int q = 0; q < 128 && t[q * 8]; ++q) {
+            fprintf(stderr, "LSTRACE pass %d:", q);
+            for (int k = 1; k < 8; ++k)
+                fprintf(stderr, " %.2f", t[q * 8 + k] ? 0.01 * (double)(t[q * 8 + k] - t[q * 8]) : -1.0);
+            if (q + 1 < 128 && t[(q + 1) * 8]) fprintf(stderr, " | next %.2f", 0.01 * (double)(t[(q + 1) * 8] - t[q * 8]));
+            fprintf(stderr, "\n");
+        }
+    }
     const LsRecord* rec = (const LsRecord*)(h + b_refs);
     for (int j = 0; j < n; ++j) {
         lgs_linsolve_summary& o = out[j];

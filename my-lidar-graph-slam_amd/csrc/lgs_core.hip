@@ -309,6 +309,11 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_SKIP_MASK: ctx->skip_mask = (unsigned)value; return LGS_OK;
     case LGS_OPT_POISON_WS: ctx->poison_ws = value != 0.0; return LGS_OK;
     case LGS_OPT_FINE_LANES: ctx->fine_lanes = value != 0.0; return LGS_OK;
+    case LGS_OPT_LINSOLVE_SPLIT: ctx->linsolve_split = value != 0.0; return LGS_OK;
+    case LGS_OPT_HANDOFF_SPIN_US:
+        if (value < 0.0) return LGS_ERR_INVALID_ARG;
+        ctx->handoff_spin_us = (long long)value;
+        return LGS_OK;
     case LGS_OPT_GUARD_CAP:
         ctx->guard_cap = (int)value;
         if (ctx->guard_cap < 0) ctx->guard_cap = 0;

@@ -186,18 +186,31 @@ def test_linsolve_batch_equals_single(ctx, world, small_map):
         inits.append((true[0] + 0.02, true[1] - 0.03, true[2] + 0.01))
     lp = abi.LinsolveParams(*CONFIG3)
     batch = ctx.linsolve_batch(g, lp, scans, inits)
-    for s, i, b in zip(scans, inits, batch):
-        one = ctx.linsolve(g, lp, s, i)
-        assert (one.estimated_pose.x, one.estimated_pose.y, one.estimated_pose.theta) == \
-            (b.estimated_pose.x, b.estimated_pose.y, b.estimated_pose.theta)
-        assert one.normalized_cost == b.normalized_cost and list(one.covariance) == list(b.covariance)
-        assert one.iterations == b.iterations
+    # a lone refine runs split over one workgroup per 64 beams (the default),
+    # on one workgroup (LGS_OPT_LINSOLVE_SPLIT 0), or -- after a hand-off
+    # time-out, forced here with LGS_OPT_HANDOFF_SPIN_US 0 -- split first and
+    # then rerun on one workgroup: every path computes the batch kernel's bits
+    for split, spin in ((1, 200000), (0, 200000), (1, 0)):
+        ctx.set_option(abi.LGS_OPT_LINSOLVE_SPLIT, split)
+        ctx.set_option(abi.LGS_OPT_HANDOFF_SPIN_US, spin)
+        try:
+            for s, i, b in zip(scans, inits, batch):
+                one = ctx.linsolve(g, lp, s, i)
+                assert (one.estimated_pose.x, one.estimated_pose.y, one.estimated_pose.theta) == \
+                    (b.estimated_pose.x, b.estimated_pose.y, b.estimated_pose.theta), (split, spin)
+                assert one.normalized_cost == b.normalized_cost and list(one.covariance) == list(b.covariance)
+                assert one.iterations == b.iterations
+        finally:
+            ctx.set_option(abi.LGS_OPT_LINSOLVE_SPLIT, 1)
+            ctx.set_option(abi.LGS_OPT_HANDOFF_SPIN_US, 200000)
 
 
 @pytest.mark.parametrize("n_beams", [1, 63, 65, 1280, 1281, 3000, 8300])
 def test_linsolve_shapes(ctx, world, small_map, n_beams):
-    """Beam counts at the kernel's chunk edges (one chunk holds 1280 beams'
-    terms; larger scans run several chunks whose sums continue in beam order)."""
+    """Beam counts at the kernels' edges: 1 beam (one workgroup), 63/65 (one
+    and two split groups), 1280/1281 (the split refine's 20-group limit and one
+    k_linsolve chunk; beyond, the one-workgroup kernel runs several chunks whose
+    sums continue in beam order)."""
     cells, mx, my = small_map
     g = ctx.grid_from_array(cells, mx, my, 0.05)
     og = ob.OGrid(cells, mx, my, 0.05)
