@@ -399,10 +399,10 @@ struct alignas(16) LsLds {
 };
 
 // s + row[0] + row[1] + ... + row[m-1], strictly in that order (LDS row,
-// 16-byte aligned).  Software-pipelined with two register buffers of 12
+// 16-byte aligned).  Software-pipelined with two register buffers of 8
 // terms: one buffer's loads are in flight while the other's are added, so
 // the chain waits on the adds only.
-constexpr int kSeqBuf = 6;   // double2 per buffer (two buffers in flight stay within lgkmcnt's 15)
+constexpr int kSeqBuf = 4;   // double2 per buffer: a 64-beam group is 4 buffer pairs, 8 loads in flight
 
 __device__ __forceinline__ double add_buf(double s, const double2 (&a)[kSeqBuf])
 {
@@ -559,7 +559,8 @@ __global__ __launch_bounds__(kLsThreads) void k_linsolve(LsPlan p, const double*
 // beams' 13 terms (write-through stores, one flag per group;
 // cdna_hip_programming.md Guideline 16, recipe R1), then EVERY workgroup
 // waits for all groups, stages all terms into LDS and adds them in beam order
-// (13 lanes of wave 0) and solves the 3x3 system itself: every workgroup
+// (13 lanes of wave 0, group by group as the other 7 waves stage the groups
+// into LDS in beam order) and solves the 3x3 system itself: every workgroup
 // holds the identical pose and takes the identical stopping decision, no
 // broadcast.  Terms and flags are double-buffered by pass parity: a
 // workgroup publishes pass p + 2 only after every group has published p + 1,
@@ -576,17 +577,47 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
 struct alignas(16) SplitLds {
-    union {
-        struct {
-            Axis ax[6][kGroup];       // x0, y0, xp, xm, yp, ym
-            double sv[5][kGroup];     // S(x0,y0), S(xp,y0), S(xm,y0), S(x0,yp), S(x0,ym)
-            double sc[2][kGroup];     // sin, cos of the beam angle
-        } b;
-        double terms[kAcc][kTermStride];   // all groups' terms of one pass, beam order per row
-    } u;
+    double terms[kAcc][kTermStride];   // all groups' terms of one pass, beam order per row
+    struct {
+        Axis ax[6][kGroup];            // x0, y0, xp, xm, yp, ym
+        double sv[5][kGroup];          // S(x0,y0), S(xp,y0), S(xm,y0), S(x0,yp), S(x0,ym)
+        double sc[2][kGroup];          // sin, cos of the beam angle
+    } b;
     double pose[3];
+    unsigned ready[kSplitMaxGroups];   // group staged in `terms` for pass epoch
     int stop;
+    int abort;
 };
+
+// seq_add over a row whose 64-beam groups are staged by other waves: each
+// group is added once its LDS flag shows (an acquire, so its loads stay
+// behind it); a full group is one fully unrolled block of 32 16-byte loads and
+// 64 adds, so the compiler pipelines the loads against the add chain without
+// loop-carried copies.  Returns 0 early if another wave set *abort.
+__device__ __forceinline__ double seq_add_staged(const double* __restrict__ row, int m, const unsigned* ready,
+                                                 const int* abort, unsigned epoch)
+{
+    double s = 0.0;
+    for (int gg = 0; gg * kGroup < m; ++gg) {
+        while (__hip_atomic_load(&ready[gg], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != epoch)
+            if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return 0.0;
+        const double* r = row + gg * kGroup;
+        const int cnt = min(kGroup, m - gg * kGroup);
+        if (cnt == kGroup) {
+            double2 v[kGroup / 2];
+#pragma unroll
+            for (int q = 0; q < kGroup / 2; ++q) v[q] = *(const double2*)(r + 2 * q);
+#pragma unroll
+            for (int q = 0; q < kGroup / 2; ++q) {
+                s = s + v[q].x;
+                s = s + v[q].y;
+            }
+        } else {
+            s = seq_add(s, r, cnt);
+        }
+    }
+    return s;
+}
 
 __device__ __forceinline__ bool spin_expired(unsigned long long t0, unsigned long long limit)
 {
@@ -621,6 +652,9 @@ __global__ __launch_bounds__(kSplitThreads) void k_linsolve_split(LsPlan p, cons
         if (threadIdx.x == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
+    if (threadIdx.x < kSplitMaxGroups) L.ready[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) L.abort = 0;
+    __syncthreads();
     double pose[3] = { sc.pose0[0], sc.pose0[1], sc.pose0[2] };
     double acc[kAcc];
     double prevCost = DBL_MAX, cost = DBL_MAX;
@@ -629,9 +663,14 @@ __global__ __launch_bounds__(kSplitThreads) void k_linsolve_split(LsPlan p, cons
         const unsigned epoch = (unsigned)pass + 1u;
         gu64* tb = tbuf + (size_t)(pass & 1) * kSplitMaxGroups * kAcc * kGroup;
         gu32* fl = flags + (pass & 1) * kSplitMaxGroups;
-        unsigned long long* tr = (trace && blockIdx.x == 0 && threadIdx.x == 0) ? trace + (size_t)min(pass, 127) * 8
+        unsigned long long* tr = (trace && blockIdx.x == 0 && threadIdx.x == 0) ? trace + (size_t)min(pass, 127) * 32
                                                                                 : nullptr;
+        unsigned long long* trs = (trace && blockIdx.x == 0 && lane == 0) ? trace + (size_t)min(pass, 127) * 32 + 8
+                                                                          : nullptr;
         if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
+        unsigned long long* twg = (trace && threadIdx.x == 0) ? trace + 128 * 32 + (size_t)min(pass, 127) * 64 + 3 * g
+                                                              : nullptr;
+        if (twg) twg[0] = __builtin_amdgcn_s_memrealtime();
         // phase A: the hit point (every wave), one axis per wave 0..5
         if (act && wid < 6) {
             double sn, cs, fx, fy;
@@ -640,10 +679,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_linsolve_split(LsPlan p, cons
             const bool isx = !(wid & 1);
             const double v = (wid < 2) ? (isx ? fx : fy) : (wid < 4) ? (fx + ((wid == 2) ? d : -d))
                                                                      : (fy + ((wid == 4) ? d : -d));
-            L.u.b.ax[wid][lane] = make_axis(v, (wid == 0 || wid == 2 || wid == 3) ? p.W : p.H);
+            L.b.ax[wid][lane] = make_axis(v, (wid == 0 || wid == 2 || wid == 3) ? p.W : p.H);
             if (wid == 0) {
-                L.u.b.sc[0][lane] = sn;
-                L.u.b.sc[1][lane] = cs;
+                L.b.sc[0][lane] = sn;
+                L.b.sc[1][lane] = cs;
             }
         }
         __syncthreads();
@@ -652,7 +691,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_linsolve_split(LsPlan p, cons
         if (act && wid < 5) {
             const int xa = (wid == 1) ? 2 : (wid == 2) ? 3 : 0;
             const int ya = (wid == 3) ? 4 : (wid == 4) ? 5 : 1;
-            L.u.b.sv[wid][lane] = smoothed(grid, p.W, L.u.b.ax[xa][lane], L.u.b.ax[ya][lane]);
+            L.b.sv[wid][lane] = smoothed(grid, p.W, L.b.ax[xa][lane], L.b.ax[ya][lane]);
         }
         __syncthreads();
         if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
@@ -661,8 +700,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_linsolve_split(LsPlan p, cons
         if (wid == 0) {
             double e = 0.0, gv[3] = { 0.0, 0.0, 0.0 };
             if (act)
-                beam_finish(p, r, L.u.b.sc[0][lane], L.u.b.sc[1][lane], L.u.b.sv[0][lane], L.u.b.sv[1][lane],
-                            L.u.b.sv[2][lane], L.u.b.sv[3][lane], L.u.b.sv[4][lane], e, gv);
+                beam_finish(p, r, L.b.sc[0][lane], L.b.sc[1][lane], L.b.sv[0][lane], L.b.sv[1][lane],
+                            L.b.sv[2][lane], L.b.sv[3][lane], L.b.sv[4][lane], e, gv);
             double t[kAcc];
             beam_acc(in_step, in_cost, e, gv, t);
 #pragma unroll
@@ -673,59 +712,52 @@ __global__ __launch_bounds__(kSplitThreads) void k_linsolve_split(LsPlan p, cons
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) __hip_atomic_store(fl + g, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
-            // wait for every group's flag (lane j polls group j), then one acquire
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            int stop = 0;
-            for (unsigned polls = 1;; ++polls) {
-                bool ok = true;
-                if (lane < G)
-                    ok = __hip_atomic_load(fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-                if (__all(ok)) break;
-                if ((polls & 255u) == 0u &&
-                    (__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-                     spin_expired(t0, spin_limit))) {
-                    if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    stop = 2;
-                    break;
-                }
-            }
-            // every load of the handed-off terms below is an sc1 (agent-scope
-            // atomic) load, so no acquire fence is needed (Guideline 16)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane == 0) L.stop = stop;
-        }
-        __syncthreads();
-        if (tr) tr[4] = __builtin_amdgcn_s_memrealtime();
-        if (L.stop == 2) return;
-        // every wave stages rows (group, term) of the pass into LDS rows in
-        // beam order: one coalesced 512-byte row per load, all of a wave's
-        // loads in flight before the first LDS store
-        {
-            constexpr int kRowsPerWave = (kSplitMaxGroups * kAcc + kSplitThreads / 64 - 1) / (kSplitThreads / 64);
-            const int rows = G * kAcc;
-            unsigned long long v[kRowsPerWave];
-#pragma unroll
-            for (int q = 0; q < kRowsPerWave; ++q) {
-                const int row = wid + q * (kSplitThreads / 64);
-                v[q] = row < rows ? __hip_atomic_load(tb + (size_t)row * kGroup + lane, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                  : 0ull;
-            }
-#pragma unroll
-            for (int q = 0; q < kRowsPerWave; ++q) {
-                const int row = wid + q * (kSplitThreads / 64);
-                if (row < rows) {
-                    const int gg = row / kAcc, k = row - gg * kAcc;
-                    L.u.terms[k][gg * kGroup + lane] = __longlong_as_double((long long)v[q]);
-                }
-            }
-        }
-        __syncthreads();
-        if (tr) tr[5] = __builtin_amdgcn_s_memrealtime();
-        if (wid == 0) {
-            const double sk = (lane < kAcc) ? seq_add(0.0, L.u.terms[lane], sc.n) : 0.0;
+            if (twg) twg[1] = __builtin_amdgcn_s_memrealtime();
+            // the 13 sums in beam order, group by group as the staging waves
+            // deliver them (LDS flag per group)
+            const double sk = (lane < kAcc) ? seq_add_staged(L.terms[lane], sc.n, L.ready, &L.abort, epoch) : 0.0;
             gather_sums(sk, acc);
-            if (tr) tr[6] = __builtin_amdgcn_s_memrealtime();
+            if (tr) tr[4] = __builtin_amdgcn_s_memrealtime();
+            if (twg) twg[2] = __builtin_amdgcn_s_memrealtime();
+        } else {
+            // staging waves 1..7: group gg (gg = wid - 1, wid + 6, ...) once its
+            // flag shows this pass: its 13 rows with sc1 loads (every load of
+            // the handed-off terms is agent-scope, so no acquire fence;
+            // Guideline 16), into the LDS rows in beam order, then the group's
+            // LDS flag
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (int gg = wid - 1; gg < G; gg += kSplitThreads / 64 - 1) {
+                bool ok = true;
+                for (unsigned polls = 1;; ++polls) {
+                    if (__hip_atomic_load(fl + gg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) break;
+                    if ((polls & 255u) == 0u &&
+                        (__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                         spin_expired(t0, spin_limit))) {
+                        if (lane == 0) {
+                            __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(&L.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        ok = false;
+                        break;
+                    }
+                }
+                if (!ok) break;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                unsigned long long v[kAcc];
+#pragma unroll
+                for (int k = 0; k < kAcc; ++k)
+                    v[k] = __hip_atomic_load(tb + ((size_t)gg * kAcc + k) * kGroup + lane, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int k = 0; k < kAcc; ++k) L.terms[k][gg * kGroup + lane] = __longlong_as_double((long long)v[k]);
+                // LDS ops of a wave complete in order: the rows land before the flag
+                if (lane == 0) __hip_atomic_store(&L.ready[gg], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (trs) trs[gg] = __builtin_amdgcn_s_memrealtime();
+            }
+        }
+        __syncthreads();
+        if (L.abort) return;
+        if (wid == 0) {
             int stop = 0;
             if (pass > 0) {
                 cost = acc[9];
@@ -876,12 +908,12 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     unsigned* htmo = (unsigned*)(h + b_refs + b_rec + b_traj);
     // diagnostics: LGS_LS_TRACE=1 prints the split refine's per-pass phase
     // stamps of workgroup 0 (us after the pass start: axes, smoothed values,
-    // published, all groups seen, terms staged, summed, solved | next pass)
+    // published, summed (-1), (-1), solved | next pass)
     static const bool trace_on = getenv("LGS_LS_TRACE") != nullptr;
     unsigned long long* trace_dev = nullptr;
     if (split && trace_on) {
-        trace_dev = (unsigned long long*)ctx->ensure(S_LIN3, 128 * 8 * sizeof(unsigned long long));
-        LGS_HIP_CHECK(hipMemsetAsync(trace_dev, 0, 128 * 8 * sizeof(unsigned long long), ctx->stream));
+        trace_dev = (unsigned long long*)ctx->ensure(S_LIN3, 128 * 96 * sizeof(unsigned long long));
+        LGS_HIP_CHECK(hipMemsetAsync(trace_dev, 0, 128 * 96 * sizeof(unsigned long long), ctx->stream));
     }
     *htmo = 0u;
     const auto launch_one_wg = [&] {
@@ -919,13 +951,21 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     }
     if (ctx->profile) ctx->harvest();
     if (trace_dev) {
-        std::vector<unsigned long long> t(128 * 8);
+        std::vector<unsigned long long> t(128 * 96);
         LGS_HIP_CHECK(hipMemcpy(t.data(), trace_dev, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost));
-        for (int q = 0; q < 128 && t[q * 8]; ++q) {
+        for (int q = 0; q < 128 && t[q * 32]; ++q) {
+            const unsigned long long* u = &t[q * 32];
             fprintf(stderr, "LSTRACE pass %d:", q);
-            for (int k = 1; k < 8; ++k)
-                fprintf(stderr, " %.2f", t[q * 8 + k] ? 0.01 * (double)(t[q * 8 + k] - t[q * 8]) : -1.0);
-            if (q + 1 < 128 && t[(q + 1) * 8]) fprintf(stderr, " | next %.2f", 0.01 * (double)(t[(q + 1) * 8] - t[q * 8]));
+            for (int k = 1; k < 8; ++k) fprintf(stderr, " %.2f", u[k] ? 0.01 * (double)(u[k] - u[0]) : -1.0);
+            if (q + 1 < 128 && t[(q + 1) * 32]) fprintf(stderr, " | next %.2f", 0.01 * (double)(t[(q + 1) * 32] - u[0]));
+            fprintf(stderr, " | staged");
+            for (int k = 8; k < 28 && u[k]; ++k) fprintf(stderr, " %.2f", 0.01 * (double)(u[k] - u[0]));
+            fprintf(stderr, "\n");
+            fprintf(stderr, "LSWG pass %d (start publish summed per workgroup, us after wg 0's start):", q);
+            const unsigned long long* w = &t[128 * 32 + q * 64];
+            for (int k = 0; k < groups; ++k)
+                fprintf(stderr, " [%d %.2f %.2f %.2f]", k, 0.01 * ((double)w[3 * k] - (double)u[0]),
+                        0.01 * ((double)w[3 * k + 1] - (double)u[0]), 0.01 * ((double)w[3 * k + 2] - (double)u[0]));
             fprintf(stderr, "\n");
         }
     }
