@@ -280,7 +280,8 @@ class DropinIn(C.Structure):
 
 class DropinOut(C.Structure):
     _fields_ = [("flatten_s", C.c_double), ("upload_s", C.c_double), ("match_uploaded_s", C.c_double),
-                ("match_resident_s", C.c_double), ("same", C.c_int)]
+                ("match_resident_s", C.c_double), ("same", C.c_int), ("patch_ingest_s", C.c_double),
+                ("match_patch_s", C.c_double), ("same_patch", C.c_int), ("allocated_patches", C.c_int)]
 
 
 def bench_drivers():
@@ -317,11 +318,17 @@ def dropin_line(args, D, n_queries=32):
     if rc != 0:
         raise RuntimeError(f"lgs_dropin_bench failed with status {rc}")
     ms = lambda v: round(1e3 * v / n_queries, 4)   # noqa: E731
-    return dict(queries=n_queries, flatten_ms=ms(dout.flatten_s), upload_ms=ms(dout.upload_s),
-                match_uploaded_ms=ms(dout.match_uploaded_s), match_resident_ms=ms(dout.match_resident_s),
-                per_query_ms=ms(dout.flatten_s + dout.upload_s + dout.match_uploaded_s), same_poses=bool(dout.same),
-                note="unchanged reference frontend: Flatten(GridMapType) + 8 MB upload per OptimizePose; "
-                     "GridMapHip keeps the latest map resident instead (INTEGRATION.md §4)")
+    return dict(queries=n_queries, per_query_ms=ms(dout.patch_ingest_s + dout.match_patch_s),
+                patch_ingest_ms=ms(dout.patch_ingest_s), match_patch_ms=ms(dout.match_patch_s),
+                same_poses=bool(dout.same_patch and dout.same), allocated_patches=dout.allocated_patches,
+                patches=(h // 100) * (w // 100),
+                flatten_path=dict(per_query_ms=ms(dout.flatten_s + dout.upload_s + dout.match_uploaded_s),
+                                  flatten_ms=ms(dout.flatten_s), upload_ms=ms(dout.upload_s),
+                                  match_uploaded_ms=ms(dout.match_uploaded_s)),
+                match_resident_ms=ms(dout.match_resident_s),
+                note="unchanged reference frontend: a GridMapType copy per OptimizePose, ingested patch-natively "
+                     "(lgs_grid_upload_patches: only allocated patches' raw 16-byte cells cross PCIe); "
+                     "flatten_path = the Flatten + dense upload ingest it replaces")
 
 
 def timed(budget_s, items, fn):

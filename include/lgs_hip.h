@@ -216,6 +216,20 @@ int  lgs_grid_wrap(lgs_ctx* ctx, double* device_cells, int w, int h, double min_
                    double min_y, double resolution, lgs_grid** out);
 void lgs_grid_destroy(lgs_grid* grid);
 int  lgs_grid_upload(lgs_ctx* ctx, lgs_grid* grid, const double* host_cells);
+/* Patch-native upload of a reference GridMapType (GridMap<BinaryBayesGridCell
+ * <double>>, H/grid_map/grid_map.hpp:295-317 mPatches, H/grid_map/
+ * grid_map_patch.hpp:15-193): patches[py * npx + px] = PatchAt(px, py).Data()
+ * (its patch_size^2 cells, cell (x, y) of the patch at y * patch_size + x) or
+ * NULL for an unallocated patch (reads Unknown = 0.0, as GridMap::Value
+ * does).  Each cell is cell_bytes bytes with its fp64 value at value_offset
+ * (BinaryBayesGridCell<double>: 16 and 8 -- vptr, mValue).  The grid must be
+ * npx*patch_size x npy*patch_size.  Only allocated patches cross PCIe, as
+ * their raw cells (host copies into pinned staging overlap the DMA); a kernel
+ * extracts the values into the dense grid and zero-fills unallocated patches.
+ * Replaces INTEGRATION.md §2's Flatten (one virtual Value() per cell) +
+ * lgs_grid_upload of the whole dense map. */
+int  lgs_grid_upload_patches(lgs_ctx* ctx, lgs_grid* grid, const void* const* patches, int npx, int npy,
+                             int patch_size, int cell_bytes, int value_offset);
 int  lgs_grid_download(lgs_ctx* ctx, const lgs_grid* grid, double* host_cells);
 int  lgs_grid_fill(lgs_ctx* ctx, lgs_grid* grid, double value);
 int  lgs_grid_info(const lgs_grid* grid, int* w, int* h, double* min_x, double* min_y,

@@ -76,6 +76,21 @@ void* lgs_ctx::ensure_pinned(size_t bytes)
     return pinned;
 }
 
+void* lgs_ctx::ensure_pinned_in(size_t bytes)
+{
+    if (pinned_in_bytes >= bytes) return pinned_in;
+    if (pinned_in) {
+        LGS_HIP_CHECK(hipStreamSynchronize(stream));
+        LGS_HIP_CHECK(hipHostFree(pinned_in));
+        pinned_in = nullptr;
+        pinned_in_bytes = 0;
+    }
+    size_t want = bytes + bytes / 4;
+    LGS_HIP_CHECK(hipHostMalloc(&pinned_in, want, hipHostMallocDefault));
+    pinned_in_bytes = want;
+    return pinned_in;
+}
+
 void* lgs_ctx::ensure_pinned_up(size_t bytes)
 {
     if (pinned_up_bytes >= bytes) return pinned_up;
@@ -185,6 +200,8 @@ void lgs_ctx::release()
     event_pool.clear();
     if (pinned_up) hipHostFree(pinned_up);
     pinned_up = nullptr;
+    if (pinned_in) hipHostFree(pinned_in);
+    pinned_in = nullptr;
     if (stream) hipStreamDestroy(stream);
     stream = nullptr;
 }
@@ -402,6 +419,75 @@ extern "C" int lgs_grid_upload(lgs_ctx* ctx, lgs_grid* g, const double* host)
         size_t bytes = (size_t)g->w * (size_t)g->h * sizeof(double);
         if (!bytes) return;
         LGS_HIP_CHECK(hipMemcpyAsync(g->d, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+        ctx->sync();
+    });
+}
+
+namespace {
+// Dense grid from staged raw patch cells: one thread per cell, x fastest;
+// slot[p] = staging index of patch p or -1 (unallocated: Unknown 0.0).  The
+// value is one 8-byte load at value_offset of the cell (the vptr half of a
+// 16-byte BinaryBayesGridCell is never read).
+__global__ __launch_bounds__(256) void k_patch_ingest(double* __restrict__ grid, int W, int ps, int npx,
+                                                      const int* __restrict__ slot,
+                                                      const unsigned char* __restrict__ cells, int cell_bytes,
+                                                      int value_offset)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    const int s = slot[(y / ps) * npx + x / ps];
+    double v = 0.0;
+    if (s >= 0) {
+        const size_t c = (size_t)s * ps * ps + (size_t)(y % ps) * ps + (x % ps);
+        v = *(const double*)(cells + c * cell_bytes + value_offset);
+    }
+    grid[(size_t)y * W + x] = v;
+}
+}  // namespace
+
+extern "C" int lgs_grid_upload_patches(lgs_ctx* ctx, lgs_grid* g, const void* const* patches, int npx, int npy,
+                                       int ps, int cell_bytes, int value_offset)
+{
+    if (!ctx || !g || (!patches && npx * npy > 0)) return LGS_ERR_INVALID_ARG;
+    return guarded(ctx, [&] {
+        LGS_REQUIRE(npx >= 0 && npy >= 0 && ps >= 1, "invalid patch geometry");
+        LGS_REQUIRE((long long)npx * ps == g->w && (long long)npy * ps == g->h,
+                    "grid size must be npx*patch_size x npy*patch_size");
+        LGS_REQUIRE(cell_bytes >= 8 && cell_bytes % 8 == 0 && value_offset >= 0 && value_offset % 8 == 0 &&
+                        value_offset + 8 <= cell_bytes,
+                    "cell_bytes / value_offset must describe an aligned fp64 inside each cell");
+        if (!g->w || !g->h) return;
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        const int np = npx * npy;
+        const size_t patch_bytes = (size_t)ps * ps * cell_bytes;
+        // slot table first (16-byte padded), then the allocated patches in table order
+        const size_t b_slot = ((size_t)np * sizeof(int) + 15) / 16 * 16;
+        std::vector<int> slot(np);
+        std::vector<int> order;
+        for (int p = 0; p < np; ++p) {
+            slot[p] = patches[p] ? (int)order.size() : -1;
+            if (patches[p]) order.push_back(p);
+        }
+        const int na = (int)order.size();
+        const size_t total = b_slot + (size_t)na * patch_bytes;
+        char* h = (char*)ctx->ensure_pinned_in(total);
+        char* d = (char*)ctx->ensure(S_INGEST, total);
+        std::memcpy(h, slot.data(), (size_t)np * sizeof(int));
+        LGS_HIP_CHECK(hipMemcpyAsync(d, h, b_slot, hipMemcpyHostToDevice, ctx->stream));
+        // host copies of chunk c (parallel over patches) overlap the DMA of chunk c - 1
+        constexpr size_t kChunkBytes = 2u << 20;
+        const int per_chunk = (int)std::max<size_t>(1, kChunkBytes / patch_bytes);
+        for (int c0 = 0; c0 < na; c0 += per_chunk) {
+            const int c1 = std::min(na, c0 + per_chunk);
+            host_parallel_for(c1 - c0, 1, [&](int k) {
+                std::memcpy(h + b_slot + (size_t)(c0 + k) * patch_bytes, patches[order[c0 + k]], patch_bytes);
+            });
+            LGS_HIP_CHECK(hipMemcpyAsync(d + b_slot + (size_t)c0 * patch_bytes, h + b_slot + (size_t)c0 * patch_bytes,
+                                         (size_t)(c1 - c0) * patch_bytes, hipMemcpyHostToDevice, ctx->stream));
+        }
+        hipLaunchKernelGGL(k_patch_ingest, dim3((g->w + 255) / 256, g->h), dim3(256), 0, ctx->stream, g->d, g->w, ps,
+                           npx, (const int*)d, (const unsigned char*)(d + b_slot), cell_bytes, value_offset);
+        LGS_HIP_CHECK(hipGetLastError());
         ctx->sync();
     });
 }

@@ -58,6 +58,7 @@ enum Slot {
     S_COST_IDX,     // int4 [7*N]
     S_COST_TERM,    // double [7*N]
     S_PATCH,        // int4 [patches]
+    S_INGEST,       // lgs_grid_upload_patches: slot table + staged raw patch cells
     S_DENSE_FINE,   // double (dense diagnostics)
     S_COARSE_GRID,  // double (coarse map for OptimizePose(query))
     S_DECIM,        // double (phase-plane coarse map)
@@ -240,6 +241,8 @@ struct lgs_ctx {
     size_t pinned_bytes = 0;
     void* pinned_up = nullptr;   // staging of the per-batch descriptor upload
     size_t pinned_up_bytes = 0;
+    void* pinned_in = nullptr;   // staging of lgs_grid_upload_patches
+    size_t pinned_in_bytes = 0;
     // padded phase-plane buffer: margins zeroed once per (buffer, layout, set count)
     void* planes_ptr = nullptr;
     int planes_sets = 0;
@@ -278,6 +281,7 @@ struct lgs_ctx {
     void* ensure_aux(int i, size_t bytes);
     void* ensure_pinned(size_t bytes);
     void* ensure_pinned_up(size_t bytes);
+    void* ensure_pinned_in(size_t bytes);
     void release();
 };
 

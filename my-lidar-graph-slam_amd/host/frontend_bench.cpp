@@ -12,9 +12,10 @@
 // The synthetic sensor (exact segment ray cast) is outside every timer.
 //
 // lgs_dropin_bench: the cost of the unchanged reference frontend's query path
-// (INTEGRATION.md §2): its latest map is a patch-based GridMapType on the host,
-// so every OptimizePose first flattens it (one virtual Value() per cell) and
-// uploads it.  A patch map with the reference's layout (row-major patches,
+// (INTEGRATION.md §2): its latest map is a patch-based GridMapType on the host.
+// Two ingests per query are timed: the Flatten path (one virtual Value() per
+// cell + a dense upload) and the patch-native one (the patch pointer table +
+// lgs_grid_upload_patches: only allocated patches' raw cells cross PCIe).  A patch map with the reference's layout (row-major patches,
 // unallocated = nullptr, cells with a virtual Value(), GridMap::Value's
 // patch-index arithmetic) is built from a dense map once; each query then
 // times Flatten, the upload and the match, next to the match on the resident
@@ -75,6 +76,9 @@ struct lgs_dropin_in {
 struct lgs_dropin_out {
     double flatten_s, upload_s, match_uploaded_s, match_resident_s;   // sums over the queries
     int same;               // 1 if both matches agree on every query
+    double patch_ingest_s, match_patch_s;   // patch-native path: table + lgs_grid_upload_patches, match
+    int same_patch;         // 1 if the patch-native match agrees with the resident one on every query
+    int allocated_patches;  // of npx * npy
 };
 
 int lgs_frontend_bench(const lgs_fb_in* in, lgs_fb_out* out);
@@ -277,6 +281,12 @@ extern "C" int lgs_dropin_bench(const lgs_dropin_in* in, lgs_dropin_out* out)
         const std::vector<double> ang(in->angles, in->angles + in->n_beams);
         std::memset(out, 0, sizeof(*out));
         out->same = 1;
+        out->same_patch = 1;
+        // the patch-native path's grid lives across queries (same geometry)
+        auto pgrid = std::make_shared<DeviceGrid>(dev, in->w, in->h, in->min_x, in->min_y, in->res);
+        static_assert(sizeof(BayesCell) == 16, "BinaryBayesGridCell<double> layout: vptr + double");
+        std::vector<const void*> table(pm.patches.size());
+        for (const Patch& p : pm.patches) out->allocated_patches += p.mData ? 1 : 0;
         for (int q = -1; q < in->n_queries; ++q) {   // q = -1: untimed warm-up
             const int qi = std::max(q, 0);
             const std::vector<double> r(in->ranges + (size_t)qi * in->n_beams,
@@ -294,7 +304,21 @@ extern "C" int lgs_dropin_bench(const lgs_dropin_in* in, lgs_dropin_out* out)
             const Clock::time_point d = Clock::now();
             const ScanMatchingSummary s2 = matcher.OptimizePose(ScanMatchingQuery(resident, scan, init));
             const Clock::time_point e = Clock::now();
+            // patch-native ingest: PatchAt(px, py).Data() per patch, then one call
+            for (std::size_t k = 0; k < table.size(); ++k) table[k] = pm.patches[k].mData.get();
+            pgrid->UploadPatches(table.data(), pm.npx, pm.npy, pm.ps, (int)sizeof(BayesCell),
+                                 (int)(sizeof(BayesCell) - sizeof(double)));
+            const Clock::time_point f = Clock::now();
+            const ScanMatchingSummary s3 = matcher.OptimizePose(ScanMatchingQuery(pgrid, scan, init));
+            const Clock::time_point g = Clock::now();
             if (q < 0) continue;
+            out->patch_ingest_s += secs(e, f);
+            out->match_patch_s += secs(f, g);
+            out->same_patch &= (s3.mEstimatedPose.mX == s2.mEstimatedPose.mX &&
+                                s3.mEstimatedPose.mY == s2.mEstimatedPose.mY &&
+                                s3.mEstimatedPose.mTheta == s2.mEstimatedPose.mTheta && s3.mNormalizedCost == s2.mNormalizedCost)
+                                   ? 1
+                                   : 0;
             out->flatten_s += secs(a, b);
             out->upload_s += secs(b, c);
             out->match_uploaded_s += secs(c, d);

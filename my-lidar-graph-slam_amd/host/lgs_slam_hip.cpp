@@ -90,6 +90,13 @@ void DeviceGrid::Upload(const std::vector<double>& cells)
     mDev->Check(lgs_grid_upload(mDev->Handle(), mGrid, cells.data()), "lgs_grid_upload");
 }
 
+void DeviceGrid::UploadPatches(const void* const* patches, int npx, int npy, int patchSize, int cellBytes,
+                               int valueOffset)
+{
+    mDev->Check(lgs_grid_upload_patches(mDev->Handle(), mGrid, patches, npx, npy, patchSize, cellBytes, valueOffset),
+                "lgs_grid_upload_patches");
+}
+
 std::vector<double> DeviceGrid::Download() const
 {
     std::vector<double> out((std::size_t)mW * mH);

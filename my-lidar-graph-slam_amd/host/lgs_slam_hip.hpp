@@ -87,6 +87,11 @@ public:
     DeviceGrid& operator=(const DeviceGrid&) = delete;
     DeviceGrid(DeviceGrid&& o) noexcept;
     void Upload(const std::vector<double>& cells);
+    // GridMapType ingest without Flatten: patches[py * npx + px] =
+    // PatchAt(px, py).Data() or nullptr (lgs_grid_upload_patches); the grid
+    // must be npx*patchSize x npy*patchSize
+    void UploadPatches(const void* const* patches, int npx, int npy, int patchSize, int cellBytes = 16,
+                       int valueOffset = 8);
     std::vector<double> Download() const;
     int NumCellsX() const { return mW; }
     int NumCellsY() const { return mH; }

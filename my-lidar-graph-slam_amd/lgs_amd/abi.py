@@ -180,6 +180,7 @@ _PROTOS = [
     ("lgs_grid_wrap", C.c_int, [_P, _P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.POINTER(_P)]),
     ("lgs_grid_destroy", None, [_P]),
     ("lgs_grid_upload", C.c_int, [_P, _P, C.POINTER(C.c_double)]),
+    ("lgs_grid_upload_patches", C.c_int, [_P, _P, C.POINTER(_P), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     ("lgs_grid_download", C.c_int, [_P, _P, C.POINTER(C.c_double)]),
     ("lgs_grid_fill", C.c_int, [_P, _P, C.c_double]),
     ("lgs_grid_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
@@ -346,6 +347,22 @@ class Context:
         h, w = cells.shape
         g = self.grid(w, h, min_x, min_y, res)
         g.upload(cells)
+        return g
+
+    def grid_from_patches(self, patches, npx: int, npy: int, patch_size: int, min_x: float, min_y: float,
+                          res: float, cell_bytes: int = 16, value_offset: int = 8,
+                          into: Optional["Grid"] = None) -> "Grid":
+        """lgs_grid_upload_patches: `patches` is a row-major list (py * npx + px)
+        of host arrays holding patch_size^2 cells of cell_bytes bytes each (the
+        fp64 value at value_offset), or None for an unallocated patch."""
+        g = into or self.grid(npx * patch_size, npy * patch_size, min_x, min_y, res)
+        keep = [None if p is None else np.ascontiguousarray(p) for p in patches]
+        for p in keep:
+            if p is not None and p.nbytes != patch_size * patch_size * cell_bytes:
+                raise ValueError("patch array size does not match patch_size^2 * cell_bytes")
+        table = (_P * max(1, len(keep)))(*[None if p is None else p.ctypes.data for p in keep])
+        self.check(self.lib.lgs_grid_upload_patches(self.h, g.h, table, npx, npy, patch_size, cell_bytes,
+                                                    value_offset), "grid_upload_patches")
         return g
 
     def wrap_device(self, ptr: int, w: int, h: int, min_x: float, min_y: float, res: float) -> "Grid":
