@@ -1166,6 +1166,10 @@ __device__ __forceinline__ double h16(unsigned long long bits)
 {
     return (double)__builtin_bit_cast(SuperT, (unsigned short)(bits & 0xFFFFu));
 }
+// NR = the superblock rows a lane sums per beam: 5 (nsby <= 5: the beam's
+// rows sit in one unit) or 9 (nsby <= 9: one unit + the high half of the next
+// unit, rows 4q + 8 .. 4q + 11).
+template <int NR>
 __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const double* __restrict__ zero)
 {
     const Blk wg = xcd_block();
@@ -1174,8 +1178,9 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
     if (wg.y >= pl.T) return;   // past this item's angles (uniform)
     const u64x2* __restrict__ units = (const u64x2*)it.super;
     const u64x2* __restrict__ z2 = (const u64x2*)zero;
+    const unsigned long long* __restrict__ hi8 = (const unsigned long long*)it.super;   // unit halves
     extern __shared__ int srow[];   // [Nv]
-    __shared__ double part[kSupWaves][64][5];
+    __shared__ double part[kSupWaves][64][NR];
     const int t = wg.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nsbx = pl.nsbx, nsb2 = nsbx * pl.nsby;
@@ -1189,9 +1194,13 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
     const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
     const int* row = srow + lo;
     const int nq = (cnt + nb - 1) / nb;     // slot q takes beams nb i + q
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
+    const long long wq4 = pl.Wq4;
+    double sr[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) sr[r] = 0.0;
     for (int i0 = 0; i0 < nq; i0 += kOctPipe) {
         u64x2 x[kOctPipe];
+        unsigned long long y[kOctPipe];
         int sh[kOctPipe];
 #pragma unroll
         for (int j = 0; j < kOctPipe; ++j) {
@@ -1199,25 +1208,33 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
             const bool ok = act && v < cnt;
             const int c = ok ? row[v] : 0;
             sh[j] = 16 * (c & 3);
-            x[j] = *(ok ? units + ((c >> 2) + a) : z2);
+            const long long u = (long long)(c >> 2) + a;
+            x[j] = *(ok ? units + u : z2);
+            if constexpr (NR > 5) y[j] = ok ? hi8[2 * (u + wq4) + 1] : 0ull;
         }
 #pragma unroll
         for (int j = 0; j < kOctPipe; ++j) {
             const int k = sh[j];
+            // rows 0..3 of the beam's window from bits k.. of (x.x, x.y, y)
             const unsigned long long w0 = k ? ((x[j].x >> k) | (x[j].y << (64 - k))) : x[j].x;
-            const unsigned long long w1 = x[j].y >> k;
-            s0 += h16(w0);
-            s1 += h16(w0 >> 16);
-            s2 += h16(w0 >> 32);
-            s3 += h16(w0 >> 48);
-            s4 += h16(w1);
+            sr[0] += h16(w0);
+            sr[1] += h16(w0 >> 16);
+            sr[2] += h16(w0 >> 32);
+            sr[3] += h16(w0 >> 48);
+            if constexpr (NR == 5) {
+                sr[4] += h16(x[j].y >> k);
+            } else {
+                const unsigned long long w1 = k ? ((x[j].y >> k) | (y[j] << (64 - k))) : x[j].y;
+                sr[4] += h16(w1);
+                sr[5] += h16(w1 >> 16);
+                sr[6] += h16(w1 >> 32);
+                sr[7] += h16(w1 >> 48);
+                sr[8] += h16(y[j] >> k);
+            }
         }
     }
-    part[w][lane][0] = s0;
-    part[w][lane][1] = s1;
-    part[w][lane][2] = s2;
-    part[w][lane][3] = s3;
-    part[w][lane][4] = s4;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) part[w][lane][r] = sr[r];
     __syncthreads();
     if (w != 0) return;
     const int sbi = lane;
@@ -1444,7 +1461,14 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, con
 // A wave then carries 64 blocks' add chains at once instead of k_coarse_rows'
 // 4 adder lanes, which is what a batch of many scans needs (k_coarse_rows
 // keeps the lower latency for a lone scan).
+// Angles whose beams reach left of / below the map (tedge) need the unsafe
+// test of every kept block over those beams; the workgroup first compacts the
+// angle's edge beams (in beam order) into LDS, so each block walks only them
+// instead of all Nv beams (the loop detector's local maps put most angles
+// there).
 constexpr int kLaneWaves = 4;
+constexpr int kEdgeMax = 1024;     // edge beams compacted in LDS (more: the full walk); 8 KB keeps
+constexpr int kEdgeMaxNv = 4096;   // the occupancy of the kernel (measured: 32 KB cost config 2 30%)
 __global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, const double* __restrict__ zero)
 {
     const MatchItem& it = items[blockIdx.y];
@@ -1486,6 +1510,36 @@ __global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, c
     }
     __syncthreads();
     const int cnt = s_cnt;
+    // edge beams of this angle: q = idx[t][v] with q.x - win_x < 0 or
+    // q.y - win_y < 0, compacted in beam order (chunk counts, then offsets)
+    __shared__ int2 s_edge[kEdgeMax];
+    __shared__ int s_ccnt[kEdgeMaxNv / 64];
+    int ne = -1;   // -1: walk every beam
+    const int2* __restrict__ idr = idx + (size_t)t * pl.Nv;
+    if (te && cnt > 0 && pl.Nv <= kEdgeMaxNv) {
+        const int nch = (pl.Nv + 63) / 64;
+        for (int c = w; c < nch; c += kLaneWaves) {
+            const int v = c * 64 + lane;
+            const int2 q = v < pl.Nv ? idr[v] : make_int2(pl.win_x, pl.win_y);
+            const bool e = (q.x - pl.win_x < 0) | (q.y - pl.win_y < 0);
+            const unsigned long long bal = __ballot(e);
+            if (lane == 0) s_ccnt[c] = __popcll(bal);
+        }
+        __syncthreads();
+        ne = 0;
+        for (int k = 0; k < nch; ++k) ne += s_ccnt[k];
+        for (int c = w; c < nch && ne <= kEdgeMax; c += kLaneWaves) {
+            int off = 0;
+            for (int k = 0; k < c; ++k) off += s_ccnt[k];
+            const int v = c * 64 + lane;
+            const int2 q = v < pl.Nv ? idr[v] : make_int2(pl.win_x, pl.win_y);
+            const bool e = (q.x - pl.win_x < 0) | (q.y - pl.win_y < 0);
+            const unsigned long long bal = __ballot(e);
+            if (e) s_edge[off + __popcll(bal & ((1ull << lane) - 1ull))] = q;
+        }
+        if (ne > kEdgeMax) ne = -1;
+        __syncthreads();
+    }
     for (int e0 = 4 * w; e0 < cnt; e0 += 4 * kLaneWaves) {   // wave-uniform
         const int e = e0 + (lane >> 4), m = lane & 15;
         const bool has = e < cnt;
@@ -1502,12 +1556,19 @@ __global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, c
         bool unsafe = false;
         double ext = 0.0;
         if (te && active) {
-            const int2* __restrict__ id = idx + (size_t)t * pl.Nv;
             const int lr = pl.low_res;
             const int x0 = -pl.win_x + jx * lr, y0 = -pl.win_y + jy * lr;
-            for (int v = 0; v < pl.Nv; ++v) {
-                const int2 q = id[v];
-                if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0) unsafe |= strip_read(cmap, q.x + x0, q.y + y0, pl, ext);
+            if (ne >= 0) {
+                for (int v = 0; v < ne; ++v) {
+                    const int2 q = s_edge[v];
+                    unsafe |= strip_read(cmap, q.x + x0, q.y + y0, pl, ext);
+                }
+            } else {
+                for (int v = 0; v < pl.Nv; ++v) {
+                    const int2 q = idr[v];
+                    if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0)
+                        unsafe |= strip_read(cmap, q.x + x0, q.y + y0, pl, ext);
+                }
             }
         }
         if (active) {
@@ -2597,7 +2658,9 @@ void set_plane_layout(RtcsmPlan& pl)
 #ifndef LGS_SUPER_OCT
 #define LGS_SUPER_OCT 1
 #endif
-    pl.oct = LGS_SUPER_OCT && pl.nsbx <= 5 && pl.nsby <= 5;
+    // octet layout: one 16-byte unit holds 5 superblock rows of a beam's
+    // window (nsby <= 5), one unit + the high half of the next holds 9
+    pl.oct = LGS_SUPER_OCT && pl.nsbx <= 9 && pl.nsby <= 9 && pl.nsbx * pl.nsby <= 64;
     pl.Qo = (pl.Hq4 + 3) / 4 + 1;
     pl.subO = (long long)pl.Qo * pl.Wq4;
     pl.pstrideO = 16 * pl.subO;
@@ -2684,7 +2747,8 @@ struct BatchShape {
     bool pair = false;
     bool quad = false;      // k_super_quad (nsby * ceil(nsbx / 2) <= 16; chunks == 1)
     bool hex = false;       // k_super_hex (fp16 planes, nsby * ceil(nsbx / 4) <= 10; chunks == 1)
-    bool oct = false;       // k_super_oct (octet layout of the plan, nsbx, nsby <= 5; chunks == 1)
+    bool oct = false;       // k_super_oct (octet layout of the plan, nsbx, nsby <= 9; chunks == 1)
+    int nsby = 0;
     bool planes = false;    // coarse map in padded phase planes
     bool pruned = false;    // superblock pruning
     bool lr5 = false;       // transposed LR = 5 evaluators
@@ -3044,8 +3108,10 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             const size_t lds = sizeof(int) * (size_t)std::max(B.NvMax, 1);
             dim3 g(B.chunks, B.Tmax, n);
             if (ctx->skipped(K_SUPER)) {
-            } else if (B.oct)
-                hipLaunchKernelGGL(k_super_oct, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+            } else if (B.oct && B.nsby <= 5)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<5>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+            else if (B.oct)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else if (B.hex)
                 hipLaunchKernelGGL(k_super_hex, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else if (B.quad)
@@ -3393,6 +3459,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     B.quad = ctx->super_quad && p0.nsby * ((p0.nsbx + 1) / 2) <= 16;
     B.hex = ctx->super_hex && B.quad && p0.nsby * ((p0.nsbx + 3) / 4) <= 10;
     B.oct = p0.oct != 0;
+    B.nsby = p0.nsby;
     B.planes = ctx->coarse_planes;
     B.pruned = uses_super(ctx, B.NvMax, B.nsb2, false);
     B.lr5 = lr5_path(B.NvMax, B.low_res);

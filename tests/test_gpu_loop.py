@@ -131,3 +131,33 @@ def test_loop_detect_multi_context_identical(ctx, n_shards):
     assert multi == one
     assert again == one
     assert len(cands) >= n_shards
+
+
+def test_loop_detect_config5_shape(ctx, world):
+    """BASELINE config 5 at its own shape: 600x600 @ 5 cm local
+    maps built by the oracle's UpdateGridMap, 1081-beam candidates whose
+    initial poses are perturbed by U(+-2 m, +-0.4 rad), the JSON loop window
+    (+-2.5 m, +-0.5 rad, LowRes 5, threshold 0.6,
+    launcher_settings_default.json:102-126), 32 candidates over 8 maps --
+    the pruned device batch against the oracle's Detect, record by record
+    (loop_detector_real_time_correlative.cpp:26-125)."""
+    import oracle_bind as ob
+
+    def build(poses, ang):
+        m = ob.OMap(0.05, 100, 600, 600)
+        for q in poses:
+            m.integrate(q, ob.OScan(scene.ray_cast(world, q, ang), ang), ob.BuilderParams(0.01, 20.0, 0.6, 0.45))
+        return m.cells(), m.m.min_x, m.m.min_y, 0.05
+
+    maps, cands = scene.loop_problem(world, build, n_maps=8, nodes_per_map=4, n_beams=1081, seed=33,
+                                     perturb=(2.0, 0.4), arc_scans=10)
+    assert all(m.cells.shape == (600, 600) for m in maps)
+    p, c = abi.RtcsmParams(*LOOP_JSON), abi.CostGEParams(*small.COST)
+    ctx.reset_stats()
+    dev = loopbatch.run_sharded(cands, loopbatch.hip_detect_fn(ctx, maps, cands, p, c, 0.6))
+    cnt = ctx.match_counters()
+    orc = loopbatch.run_sharded(cands, oracle_detect_fn(maps, cands, LOOP_JSON, small.COST, 0.6))
+    compare(loopbatch.decode(dev), loopbatch.decode(orc))
+    found = loopbatch.loop_results(dev)
+    assert 0 < len(found) <= len(cands)
+    assert cnt["pruned"] == len(cands) and cnt["coarse_blocks"] < cnt["coarse_blocks_dense"], cnt
