@@ -191,6 +191,11 @@ int  lgs_debug_item_buffer(lgs_ctx* ctx, int item, int which, void* out, size_t 
  * host libm bit for bit). */
 int  lgs_debug_libm(lgs_ctx* ctx, int op, const double* x, int n, double* out);
 
+/* Diagnostics: the K3 sort (csrc/k_sort.hip, the stable radix sort behind
+ * every ray-cast pass) of n host keys on bits [lo, lo + bits), through the
+ * device; out receives the sorted keys. */
+int  lgs_debug_keysort(lgs_ctx* ctx, const unsigned* keys, unsigned* out, long long n, int lo, int bits);
+
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is
  * the algorithmic byte count of DESIGN.md §Roofline (e.g. 8 B per coarse-score
  * lookup), summed over launches; total_ms sums hipEventElapsedTime. */
@@ -349,6 +354,13 @@ int  lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* map, const lgs_scan* co
  * two calls; both ray-casts share one device pass.  local != latest. */
 int  lgs_map_append_scan(lgs_ctx* ctx, lgs_map* local, lgs_map* latest, const lgs_scan* const* scans,
                          const lgs_pose2d* robot_poses, int n, const lgs_builder_params* params);
+
+/* Diagnostics: how a map's ConstructMapFromScans / AppendScan rebuilds ran
+ * (DESIGN.md §4.4b): incremental steps (the window gained one scan and lost
+ * at most its oldest, same geometry: only the touched cells recomputed) and
+ * full rebuilds.  Both zero for a map never rebuilt. */
+int  lgs_debug_map_rebuilds(const lgs_map* m, long long* incremental, long long* full);
+
 /* GridMapBuilder::AfterLoopClosure's map loop (C/mapping/grid_map_builder.cpp:62-80):
  * ConstructMapFromScans(maps[i], poseGraph, idx_min[i], idx_max[i]) for every
  * i, where node k of the pose graph is (scans[k], robot_poses[k]) and

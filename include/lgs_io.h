@@ -32,12 +32,14 @@ extern "C" {
  *   scan:     1, timestamp, n, odom x y theta, velocity x y theta,
  *             relative sensor pose x y theta, minRange, maxRange, minAngle,
  *             maxAngle, angles[n], ranges[n]
- * and the sensor ids NUL-terminated one after another into ids.  Returns the
- * number of doubles of the stream (at most cap are written; call again with a
- * larger buffer), or -1 when the reader throws (e.g. a PARAM value stod()
- * rejects -- the reference would terminate). */
+ * and the sensor ids NUL-terminated one after another into ids (*ids_bytes,
+ * if not NULL, receives the bytes they need, terminators included).  Returns
+ * the number of doubles of the stream (at most cap doubles and ids_cap id
+ * bytes are written; call again with larger buffers), or -1 when the reader
+ * throws (e.g. a PARAM value stod() rejects -- the reference would
+ * terminate). */
 long long lgs_carmen_load(const char* text, double* out, long long cap, char* ids, long long ids_cap,
-                          int* num_records);
+                          long long* ids_bytes, int* num_records);
 
 /* PoseGraph::Edge (H/mapping/pose_graph.hpp:120-170) */
 typedef struct {

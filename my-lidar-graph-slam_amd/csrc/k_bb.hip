@@ -330,6 +330,7 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
             const double* const* const* pyr, lgs_scan* const* scans, const lgs_pose2d* init, int n, double nthr,
             lgs_rtcsm_summary* out, bool no_path = false)
 {
+    for (int k = 0; k < n; ++k) grid_acquire(ctx, grids[k]);
     LGS_HIP_CHECK(hipSetDevice(ctx->device));
     std::memset(out, 0, sizeof(lgs_rtcsm_summary) * (size_t)n);
     // LGS_BB_TIMING=1: per-phase host wall times on stderr (diagnostics)
@@ -720,6 +721,7 @@ void check_bb(const lgs_bb_params* p, const lgs_cost_ge_params* c)
 // PrecomputeGridMaps into n_maps x (H+1) scratch maps of S_BB2; returns the pointers
 std::vector<std::vector<const double*>> pyramids(lgs_ctx* ctx, const lgs_grid* const* maps, int n_maps, int Hm)
 {
+    for (int k = 0; k < n_maps; ++k) grid_acquire(ctx, maps[k]);
     size_t total = 0;
     for (int m = 0; m < n_maps; ++m) total += (size_t)(Hm + 1) * align256(sizeof(double) * (size_t)maps[m]->w * maps[m]->h);
     char* base = (char*)ctx->ensure(S_BB2, std::max<size_t>(total, 16));

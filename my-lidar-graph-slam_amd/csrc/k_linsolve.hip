@@ -870,6 +870,7 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
                   const lgs_scan* const* scans, const lgs_pose2d* init, int n,
                   lgs_linsolve_summary* out, double* traj)
 {
+    grid_acquire(ctx, grid);
     check_grid(grid);
     LGS_REQUIRE(prm, "null params");
     LGS_HIP_CHECK(hipSetDevice(ctx->device));
@@ -1024,6 +1025,7 @@ extern "C" int lgs_cost_square_error(lgs_ctx* ctx, const lgs_grid* grid, double 
     return guarded(ctx, [&] {
         check_grid(grid);
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        grid_acquire(ctx, grid);
         lgs_linsolve_params prm{};
         prm.cost_usable_range_min = umin;
         prm.cost_usable_range_max = umax;

@@ -13,15 +13,13 @@
 //   k_emit     one thread per ray walks Bresenham (H/util.hpp:256-303) and emits
 //              a 32-bit key (cell << 1 | is_hit) per visited cell at the ray's
 //              offset, so the key array is in ray order
-//   sort       stable hipcub radix sort on the cell bits only: each cell's
-//              updates become a contiguous run that keeps ray order = the
-//              reference's update order (a ray visits a cell at most once)
+//   sort       stable radix sort on the cell bits only (k_sort.hip): each
+//              cell's updates become a contiguous run that keeps ray order =
+//              the reference's update order (a ray visits a cell at most once)
 //   k_runmask  hit and run-end bitmaps of the sorted keys (one ballot per 64)
 //   k_apply    one thread per run applies the Bayes updates sequentially and
 //              counts hits/misses
 #include "lgs_internal.hpp"
-
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <array>
@@ -30,6 +28,10 @@
 #include <cstring>
 
 using namespace lgs;
+
+namespace {
+struct LatestCache;
+}
 
 struct lgs_map {
     lgs_ctx* ctx = nullptr;
@@ -51,6 +53,7 @@ struct lgs_map {
     uint8_t* d_palloc2 = nullptr;
     size_t pcap = 0, pcap2 = 0;
     lgs_grid view;
+    LatestCache* cache = nullptr;   // the latest map's window lists (§4.4b), created on first use
 };
 
 namespace {
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
                                              const int* __restrict__ rmap, int nrays,
                                              long long nkeys, const RayMap* __restrict__ maps,
                                              unsigned* __restrict__ keys,
-                                             int* __restrict__ outside)
+                                             int* __restrict__ outside, int ksh)
 {
     __shared__ unsigned buf[kEmitLds > 0 ? kEmitLds : 1];
     const int r0 = blockIdx.x * 64;
@@ -119,7 +122,9 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
     const bool staged = kEmitLds > 0 && end - base <= kEmitLds;   // uniform
     if (r < nrays) {
         const int4 ry = rays[r];
-        const RayMap mp = maps[rmap ? rmap[r] : 0];
+        const int rm = rmap ? rmap[r] : 0;       // map index | slot tag << 16
+        const RayMap mp = maps[rm & 0xffff];
+        const unsigned tag = ((unsigned)rm >> 16) << 1;
         const int W = mp.w, H = mp.h;
         const unsigned cbase = (unsigned)mp.base;
         unsigned* out = staged ? buf + (offs[r] - base) : keys + offs[r];
@@ -135,7 +140,7 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
             const bool in = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
             bad |= !in;
             const unsigned cell = cbase + (in ? (unsigned)y * (unsigned)W + (unsigned)x : 0u);
-            *out++ = (cell << 1) | hit;
+            *out++ = (cell << ksh) | tag | hit;
         };
         if (deltaX > deltaY) {
             int err = deltaY - deltaX / 2;
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
             }
         }
         emit(nx, ny, 1u);  // == (hx, hy): the hit cell, updated last
-        if (bad) atomicAdd(outside, 1);
+        if (bad) *outside = 1;
     }
     if (!staged) return;
     __syncthreads();
@@ -171,20 +176,38 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
 
 // k_runmask: one thread per sorted key; each wavefront covers 64 consecutive
 // keys (64-aligned) and writes two 64-bit words with ballots -- bit j of
-// hitw = key j is a hit, bit j of endw = key j is the last of its cell's run.
-__global__ __launch_bounds__(256) void k_runmask(const unsigned* __restrict__ keys, long long n,
+// hitw = key j is a hit, bit j of endw = key j is the last of its run (keys
+// equal above bit rsh: rsh = ksh, runs of one cell; rsh = 1, runs of one
+// (cell, slot) pair in the latest map's slot lists).  With an index table,
+// the key at the start of each run below `nidx` also records its position:
+// tbl[cell * kSlots + slot] = stamp(slot) << 32 | position.
+constexpr int kSlots = 16;          // latest-map scan slots (slot tag: key bits 1..4)
+constexpr int kTagShift = 5;        // tagged keys: cell << 5 | slot << 1 | hit
+struct SlotStamps {
+    unsigned s[kSlots];
+};
+struct RunIndex {
+    unsigned long long* tbl;        // null: no index
+    long long nidx;
+    SlotStamps st;
+};
+__global__ __launch_bounds__(256) void k_runmask(const unsigned* __restrict__ keys, long long n, int rsh,
                                                  unsigned long long* __restrict__ hitw,
-                                                 unsigned long long* __restrict__ endw)
+                                                 unsigned long long* __restrict__ endw, RunIndex ix)
 {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = i < n;
     const unsigned k = in ? keys[i] : 0u;
-    const bool last = in && (i + 1 >= n || (keys[i + 1] >> 1) != (k >> 1));
+    const bool last = in && (i + 1 >= n || (keys[i + 1] >> rsh) != (k >> rsh));
     const unsigned long long hb = __ballot(in && (k & 1u));
     const unsigned long long eb = __ballot(last);
     if ((threadIdx.x & 63) == 0 && in) {
         hitw[i >> 6] = hb;
         endw[i >> 6] = eb;
+    }
+    if (ix.tbl && i < ix.nidx && (i == 0 || (keys[i - 1] >> rsh) != (k >> rsh))) {
+        const unsigned slot = (k >> 1) & (kSlots - 1);
+        ix.tbl[(size_t)(k >> kTagShift) * kSlots + slot] = ((unsigned long long)ix.st.s[slot] << 32) | (unsigned)i;
     }
 }
 
@@ -276,52 +299,48 @@ BayesChains make_chains(double p_hit, double p_miss)
     return c;
 }
 
-// k_apply: one thread per run of equal cells (the thread at the run's first
-// key) applies BinaryBayesGridCell::Update in key order = the reference's
-// order.  The run is read 64 keys at a time from the hit/end words, not key by
-// key, and the updates that are exact fixed points -- a miss at v == 1e-3
-// with odds(pMiss) <= 1, a hit at v == 1 - 1e-3 -- are jumped over with the
-// masks after the kernel has checked on the device that they are identities
-// (cells next to the sensor see thousands of such misses).
-__global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys, long long n,
-                                               const unsigned long long* __restrict__ hitw,
-                                               const unsigned long long* __restrict__ endw,
-                                               const unsigned long long* __restrict__ hit2,
-                                               const unsigned long long* __restrict__ miss2,
-                                               const unsigned long long* __restrict__ end2,
-                                               const RayMap* __restrict__ maps, int nmaps,
-                                               const BayesChains* __restrict__ ch,
-                                               double p_hit, double p_miss)
+// The run bitmaps of one sorted key array (k_runmask / k_runsummary).
+struct RunBits {
+    const unsigned long long *hitw, *endw, *hit2, *miss2, *end2;
+};
+
+// Constants of the Bayes walk, evaluated once per thread.
+struct BayesK {
+    bool miss_fixed, hit_fixed;
+    double cph, cpm, oph, opm;
+    __device__ BayesK(double p_hit, double p_miss)
+    {
+        miss_fixed = bayes_update(kPMin, p_miss) == kPMin;
+        hit_fixed = bayes_update(kPMax, p_hit) == kPMax;
+        cph = clampv(p_hit, kPMin, kPMax), cpm = clampv(p_miss, kPMin, kPMax);
+        oph = cph / (1.0 - cph), opm = cpm / (1.0 - cpm);
+    }
+};
+
+// Apply BinaryBayesGridCell::Update for the run that starts at key position i
+// (in key order = the reference's order) to the value v; counts hits/misses.
+// The run is read 64 keys at a time from the hit/end words, not key by key,
+// and the updates that are exact fixed points -- a miss at v == 1e-3 with
+// odds(pMiss) <= 1, a hit at v == 1 - 1e-3 -- are jumped over with the masks
+// after the kernel has checked on the device that they are identities (cells
+// next to the sensor see thousands of such misses).
+__device__ double walk_run(long long i, double v, uint32_t& nh, uint32_t& nm, const RunBits& rb,
+                           const BayesChains* __restrict__ ch, const BayesK& K)
 {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (i > 0 && !((endw[(i - 1) >> 6] >> ((i - 1) & 63)) & 1ull)) return;  // not a run start
-    const unsigned cell = keys[i] >> 1;
-    const bool miss_fixed = bayes_update(kPMin, p_miss) == kPMin;
-    const bool hit_fixed = bayes_update(kPMax, p_hit) == kPMax;
-    const double cph = clampv(p_hit, kPMin, kPMax), cpm = clampv(p_miss, kPMin, kPMax);
-    const double oph = cph / (1.0 - cph), opm = cpm / (1.0 - cpm);
-    const RayMap mp = maps[find_map(maps, nmaps, cell)];
-    const unsigned long long local = cell - mp.base;
-    // the first Update of a cell allocates its patch (GridCellAt, :817-819);
-    // every thread of the patch stores the same byte
-    const unsigned lx = (unsigned)(local % (unsigned)mp.w), ly = (unsigned)(local / (unsigned)mp.w);
-    mp.palloc[(ly / (unsigned)mp.ps) * (unsigned)mp.npx + lx / (unsigned)mp.ps] = 1;
-    double v = mp.cells[local];
-    uint32_t nh = 0, nm = 0;
     const double a0 = ch->a[0], a1 = ch->a[1], a2 = ch->a[2], a3 = ch->a[3];
     // the miss chain and the hit chain v is on (-1: none) and the index in it
     int cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, ck = (v == a1) ? 1 : (v == a3) ? 3 : -1;
     int jm = 0, jk = 0;
     for (long long p = i;;) {
         const int sh = (int)(p & 63);
-        const bool id_miss = miss_fixed && v == kPMin, id_hit = hit_fixed && v == kPMax;
+        const bool id_miss = K.miss_fixed && v == kPMin, id_hit = K.hit_fixed && v == kPMax;
         if (sh == 0 && (id_miss || id_hit)) {
             // whole words inside the run whose updates are all identities:
             // no run end and no hit (resp. miss) in them
             const long long w = p >> 6;
             const int b = (int)(w & 63);
-            const unsigned long long stop = (end2[w >> 6] | (id_miss ? hit2[w >> 6] : miss2[w >> 6])) >> b;
+            const unsigned long long stop =
+                (rb.end2[w >> 6] | (id_miss ? rb.hit2[w >> 6] : rb.miss2[w >> 6])) >> b;
             const int k = stop ? __ffsll((long long)stop) - 1 : 64 - b;
             if (k > 0) {
                 if (id_miss) nm += 64u * (unsigned)k; else nh += 64u * (unsigned)k;
@@ -329,8 +348,8 @@ __global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys
                 continue;
             }
         }
-        const unsigned long long hm = hitw[p >> 6] >> sh;
-        const unsigned long long em = endw[p >> 6] >> sh;
+        const unsigned long long hm = rb.hitw[p >> 6] >> sh;
+        const unsigned long long em = rb.endw[p >> 6] >> sh;
         const int cnt = em ? __ffsll((long long)em) : 64 - sh;  // keys of the run in this word
         const unsigned long long inm = (cnt == 64) ? ~0ull : ((1ull << cnt) - 1ull);
         const unsigned long long h = hm & inm, m = inm & ~hm;
@@ -338,11 +357,11 @@ __global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys
         nm += cnt - __popcll(h);
         int pos = 0;
         while (pos < cnt) {
-            if (miss_fixed && v == kPMin) {        // misses are identities: next hit
+            if (K.miss_fixed && v == kPMin) {        // misses are identities: next hit
                 const unsigned long long rest = h >> pos;
                 if (!rest) break;
                 pos += __ffsll((long long)rest) - 1;
-            } else if (hit_fixed && v == kPMax) {  // hits are identities: next miss
+            } else if (K.hit_fixed && v == kPMax) {  // hits are identities: next miss
                 const unsigned long long rest = m >> pos;
                 if (!rest) break;
                 pos += __ffsll((long long)rest) - 1;
@@ -373,17 +392,123 @@ __global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys
                 }
                 continue;
             }
-            v = bayes_update_k(v, is_hit ? cph : cpm, is_hit ? oph : opm);
+            v = bayes_update_k(v, is_hit ? K.cph : K.cpm, is_hit ? K.oph : K.opm);
             ++pos;
             cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, jm = 0;
             ck = (v == a1) ? 1 : (v == a3) ? 3 : -1, jk = 0;
         }
-        if (em) break;
+        if (em) return v;
         p += cnt;
     }
+}
+
+__device__ __forceinline__ bool run_start(const unsigned long long* __restrict__ endw, long long i)
+{
+    return i == 0 || ((endw[(i - 1) >> 6] >> ((i - 1) & 63)) & 1ull);
+}
+
+// the first Update of a cell allocates its patch (GridCellAt, :817-819);
+// every thread of the patch stores the same byte
+__device__ __forceinline__ void mark_patch(const RayMap& mp, unsigned long long local)
+{
+    const unsigned lx = (unsigned)(local % (unsigned)mp.w), ly = (unsigned)(local / (unsigned)mp.w);
+    mp.palloc[(ly / (unsigned)mp.ps) * (unsigned)mp.npx + lx / (unsigned)mp.ps] = 1;
+}
+
+// k_apply: one thread per run of equal cells (the thread at the run's first
+// key) continues the cell from its current value with the run's updates.
+__global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys, long long n, RunBits rb,
+                                               const RayMap* __restrict__ maps, int nmaps,
+                                               const BayesChains* __restrict__ ch, double p_hit, double p_miss,
+                                               int ksh)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !run_start(rb.endw, i)) return;
+    const unsigned cell = keys[i] >> ksh;
+    const BayesK K(p_hit, p_miss);
+    const RayMap mp = maps[find_map(maps, nmaps, cell)];
+    const unsigned long long local = cell - mp.base;
+    mark_patch(mp, local);
+    uint32_t nh = 0, nm = 0;
+    const double v = walk_run(i, mp.cells[local], nh, nm, rb, ch, K);
     mp.cells[local] = v;
     mp.hit[local] += nh;
     mp.miss[local] += nm;
+}
+
+// One step of the latest map's incremental rebuild: the
+// window's scans keep their sorted key lists (one per ring slot, tagged keys,
+// runs of one (cell, slot)); tbl[cell * kSlots + slot] locates a cell's run
+// in a slot's list.  A cell touched by the entering scan E or the leaving
+// scan L is recomputed from Unknown over the window's slots oldest first --
+// the exact update sequence ConstructMapFromScans applies after Reset; every
+// other cell's sequence, and so its value and counters, is unchanged.
+struct SlotView {
+    const unsigned* keys;
+    RunBits rb;
+};
+struct WindowJob {
+    SlotView slot[kSlots];
+    SlotStamps st;
+    int order[kSlots];              // the window's ring slots, oldest first
+    int nwin;
+    int eslot;                      // E's slot
+    RayMap latest, local;           // latest map (cell base 0), local map (insert of E)
+    long long nE, nloc;             // E's latest keys [0, nE), local keys [nE, nE + nloc) of slot[eslot]
+    const unsigned* lkeys;          // L's list: [lbeg, lbeg + nL) of lrb's array (nL = 0: no L)
+    RunBits lrb;
+    long long lbeg, nL;
+    const unsigned long long* tbl;
+};
+
+__device__ void recompute_cell(const WindowJob& J, unsigned cell, const BayesChains* __restrict__ ch,
+                               const BayesK& K)
+{
+    const unsigned long long* e = J.tbl + (size_t)cell * kSlots;
+    double v = 0.0;   // Reset (:290): Unknown
+    uint32_t nh = 0, nm = 0;
+    bool any = false;
+    for (int q = 0; q < J.nwin; ++q) {
+        const int s = J.order[q];
+        const unsigned long long x = e[s];
+        if ((unsigned)(x >> 32) != J.st.s[s]) continue;
+        v = walk_run((long long)(unsigned)x, v, nh, nm, J.slot[s].rb, ch, K);
+        any = true;
+    }
+    if (any) mark_patch(J.latest, cell);
+    J.latest.cells[cell] = v;
+    J.latest.hit[cell] = nh;
+    J.latest.miss[cell] = nm;
+}
+
+__global__ __launch_bounds__(256) void k_apply_window(const WindowJob* __restrict__ jp,
+                                                      const BayesChains* __restrict__ ch, double p_hit,
+                                                      double p_miss)
+{
+    const WindowJob& J = *jp;
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const BayesK K(p_hit, p_miss);
+    const SlotView& E = J.slot[J.eslot];
+    if (i < J.nE) {                                   // cells of E
+        if (!run_start(E.rb.endw, i)) return;
+        recompute_cell(J, E.keys[i] >> kTagShift, ch, K);
+    } else if (i < J.nE + J.nloc) {                   // E into the local map
+        if (!run_start(E.rb.endw, i)) return;
+        const unsigned long long local = (E.keys[i] >> kTagShift) - J.local.base;
+        mark_patch(J.local, local);
+        uint32_t nh = 0, nm = 0;
+        const double v = walk_run(i, J.local.cells[local], nh, nm, E.rb, ch, K);
+        J.local.cells[local] = v;
+        J.local.hit[local] += nh;
+        J.local.miss[local] += nm;
+    } else if (i < J.nE + J.nloc + J.nL) {            // cells of L not in E
+        const long long p = J.lbeg + (i - J.nE - J.nloc);
+        if (p != J.lbeg && !run_start(J.lrb.endw, p)) return;
+        const unsigned cell = J.lkeys[p] >> kTagShift;
+        const unsigned long long x = J.tbl[(size_t)cell * kSlots + J.eslot];
+        if ((unsigned)(x >> 32) == J.st.s[J.eslot]) return;   // E's thread recomputes it
+        recompute_cell(J, cell, ch, K);
+    }
 }
 
 // MapSaver::DrawMap (C/io/map_saver.cpp:276-313) for the W x H cells of the
@@ -682,6 +807,18 @@ HitsPtr cached_hits(const lgs_scan* s, lgs_pose2d robot, const lgs_builder_param
 struct MapJob {
     lgs_map* m;
     std::vector<HitsPtr> hs;
+    std::vector<int> tags;   // per scan: slot tag of its keys (tagged passes; empty: 0)
+};
+
+// A tagged pass (the latest map's bootstrap, §4.4b): keys cell << 5 | slot
+// << 1 | hit, one pass; the sorted keys stay in the pass's scratch for the
+// caller (stream order) -- sorted[0, keys) by cell, jobs' maps in order.
+struct TagPass {
+    bool ok = false;                   // the pass ran tagged
+    const unsigned* sorted = nullptr;
+    long long keys = 0;
+    long long job_keys[2] = {};
+    long long tag_keys[kSlots] = {};   // keys of job 0 per slot tag
 };
 
 // Hit points of every job's scans (one parallel region over all of them) and
@@ -718,25 +855,17 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
         }
 }
 
-// Stable sort of the 32-bit keys on the cell bits [1, 1 + cell_bits): hipcub's
-// onesweep radix sort (8-bit digits; rocprim onesweep with 11-bit digits was
-// measured slower, 3.2 -> 4.8 ms per rebuild step).
-hipError_t ray_sort(void* temp, size_t& bytes, const unsigned* in, unsigned* out, long long n, int cell_bits,
-                    hipStream_t st)
-{
-    return hipcub::DeviceRadixSort::SortKeys(temp, bytes, in, out, (int)n, 1, 1 + cell_bits, st);
-}
-
 // Ray-cast every job's scans (already in its map's geometry), jobs in order,
 // each job's scans in order.  The rays of all jobs share emit/sort/apply
 // passes; a pass holds at most ctx->ray_chunk_keys keys and 2^31 cells of
 // maps, and passes run in ray order, so each cell still sees its updates in
 // the reference's order.
-void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_params* bp)
+void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_params* bp, TagPass* tp = nullptr)
 {
     hipStream_t st = ctx->stream;
     struct Unit {
         int job;
+        int tag;
         const ScanHits* h;
         std::vector<int4> rays;
         std::vector<int> len;
@@ -744,11 +873,11 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
     };
     std::vector<Unit> units;
     for (int j = 0; j < (int)jobs.size(); ++j)
-        for (const HitsPtr& h : jobs[j].hs)
-            if (h->xy.size() >= 2) units.push_back(Unit{j, h.get(), {}, {}, 0});
+        for (size_t k = 0; k < jobs[j].hs.size(); ++k)
+            if (jobs[j].hs[k]->xy.size() >= 2)
+                units.push_back(Unit{j, jobs[j].tags.empty() ? 0 : jobs[j].tags[k], jobs[j].hs[k].get(), {}, {}, 0});
+    if (tp) *tp = TagPass{};
     if (units.empty()) return;
-    for (const MapJob& J : jobs)
-        LGS_REQUIRE((size_t)J.m->w * J.m->h < (1ull << 31), "map too large for 31-bit cell keys");
     // sensor/hit cells and ray lengths (parallel over scans)
     host_parallel_for((int)units.size(), 2, [&](int u) {
         Unit& U = units[u];
@@ -778,6 +907,20 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
             total_cells += (unsigned long long)jobs[units[q].job].m->w * jobs[units[q].job].m->h;
     }
     const long long budget = std::max(1LL, std::min(ctx->ray_chunk_keys, 1LL << 30));
+    // a tagged pass needs one pass and 27 cell bits; otherwise it runs untagged
+    if (tp && !(total_keys <= budget && total_rays < (1LL << 30) && total_cells < (1ull << (32 - kTagShift))))
+        tp = nullptr;
+    const int ksh = tp ? kTagShift : 1;
+    for (const MapJob& J : jobs)
+        LGS_REQUIRE((size_t)J.m->w * J.m->h < (1ull << (32 - ksh)), "map too large for the cell bits of the keys");
+    if (tp) {
+        tp->ok = true;
+        for (const Unit& U : units) {
+            LGS_REQUIRE(U.job < 2 && U.tag < kSlots, "tagged pass: two maps, 16 slots");
+            tp->job_keys[U.job] += U.keys;
+            if (U.job == 0) tp->tag_keys[U.tag] += U.keys;
+        }
+    }
     // [0] rays leaving the map (int), [2..3] runs of equal cells applied (u64)
     int* d_bad = (int*)ctx->ensure(S_RAY4, 16);
     unsigned long long* d_runs = (unsigned long long*)(d_bad + 2);
@@ -794,7 +937,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
         long long keys = 0, nr = 0;
         int cur = -1;
         size_t eu = u, er = r;
-        if (pass == 0 && total_keys <= budget && total_rays < (1LL << 30) && total_cells <= (1ull << 31)) {
+        if (pass == 0 && total_keys <= budget && total_rays < (1LL << 30) && total_cells < (1ull << (32 - ksh))) {
             // everything in one pass (the usual case): whole units
             for (size_t q = 0; q < units.size(); ++q)
                 if (q == 0 || units[q].job != units[q - 1].job) {
@@ -815,7 +958,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
             if (U.job != cur) {
                 const lgs_map* m = jobs[U.job].m;
                 const unsigned long long mc = (unsigned long long)m->w * m->h;
-                if (nr > 0 && cells + mc > (1ull << 31)) break;
+                if (nr > 0 && cells + mc > (1ull << (32 - ksh))) break;
                 maps.push_back(RayMap{cells, m->w, m->h, m->d_cells, m->d_hit, m->d_miss, m->d_palloc, m->ps, m->npx});
                 cells += mc;
                 cur = U.job;
@@ -823,7 +966,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
             keys += L, ++nr, ++er;
         }
         const int nmaps = (int)maps.size();
-        const bool multi = nmaps > 1;
+        const bool multi = nmaps > 1 || tp;   // per-ray map | tag words
         // stage the map table, rays, key offsets and ray->map indices
         auto al = [](size_t b) { return (b + 63) & ~(size_t)63; };
         const size_t cb = al(sizeof(BayesChains));
@@ -843,6 +986,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
                 size_t unit, r0, r1;
                 long long ray0, key0;
                 int map;
+                int tag;
             };
             std::vector<Seg> segs;
             long long ray0 = 0, key0 = 0;
@@ -853,7 +997,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
                 const size_t r1 = std::min(U.len.size(), r0 + (size_t)(nr - ray0));
                 if (r1 <= r0) continue;
                 if (U.job != cj) cj = U.job, ++mi;
-                segs.push_back(Seg{cu, r0, r1, ray0, key0, mi});
+                segs.push_back(Seg{cu, r0, r1, ray0, key0, mi, U.tag});
                 long long kk = 0;
                 if (r0 == 0 && r1 == U.len.size()) kk = U.keys;
                 else
@@ -868,7 +1012,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
                 for (size_t q = S.r0; q < S.r1; ++q, ++k) {
                     prays[k] = U.rays[q];
                     poffs[k] = off;
-                    if (multi) pmap[k] = S.map;
+                    if (multi) pmap[k] = S.map | (S.tag << 16);
                     off += U.len[q];
                 }
             });
@@ -887,15 +1031,13 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
         // and written once; the run count is added after the last pass)
         int tok = ctx->timing_begin(K_RAY_EMIT, 4.0 * (double)keys);
         hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, st, d_rays, d_offs,
-                           d_rmap, (int)nr, keys, d_maps, d_keys, d_bad);
+                           d_rmap, (int)nr, keys, d_maps, d_keys, d_bad, ksh);
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
         int cell_bits = 1;
         while (cell_bits < 32 && (1ull << cell_bits) < cells) ++cell_bits;
-        size_t tbytes = 0;
-        LGS_HIP_CHECK(ray_sort(nullptr, tbytes, d_keys, d_sorted, keys, cell_bits, st));
-        void* temp = ctx->ensure(S_RAY5, tbytes);
-        LGS_HIP_CHECK(ray_sort(temp, tbytes, d_keys, d_sorted, keys, cell_bits, st));
+        unsigned* d_tmp = (unsigned*)ctx->ensure(S_RAY5, sizeof(unsigned) * keys);
+        keysort(ctx, d_keys, d_sorted, d_tmp, keys, ksh, cell_bits);
         tok = ctx->timing_begin(K_RAY_APPLY, 4.0 * (double)keys);
         if (tok >= 0) apply_tok = tok;
         const long long nw = (keys + 63) / 64;
@@ -907,16 +1049,22 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
         unsigned long long* d_miss2 = d_hit2 + nw2;
         unsigned long long* d_end2 = d_miss2 + nw2;
         const unsigned blocks = (unsigned)((keys + 255) / 256);
-        hipLaunchKernelGGL(k_runmask, dim3(blocks), dim3(256), 0, st, d_sorted, keys, d_hitw, d_endw);
+        hipLaunchKernelGGL(k_runmask, dim3(blocks), dim3(256), 0, st, d_sorted, keys, ksh, d_hitw, d_endw,
+                           RunIndex{});
         hipLaunchKernelGGL(k_runsummary, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, d_hitw, d_endw, nw,
                            d_hit2, d_miss2, d_end2);
-        hipLaunchKernelGGL(k_apply, dim3(blocks), dim3(256), 0, st, d_sorted, keys, d_hitw, d_endw, d_hit2,
-                           d_miss2, d_end2, d_maps, nmaps, d_chains, bp->prob_hit, bp->prob_miss);
+        hipLaunchKernelGGL(k_apply, dim3(blocks), dim3(256), 0, st, d_sorted, keys,
+                           RunBits{d_hitw, d_endw, d_hit2, d_miss2, d_end2}, d_maps, nmaps, d_chains, bp->prob_hit,
+                           bp->prob_miss, ksh);
         ctx->timing_end(tok);
         if (tok >= 0)
             hipLaunchKernelGGL(k_count_runs, dim3((unsigned)std::min<long long>((nw + 255) / 256, 512)), dim3(256), 0,
                                st, d_endw, nw, d_runs);
         LGS_HIP_CHECK(hipGetLastError());
+        if (tp) {
+            tp->sorted = d_sorted;
+            tp->keys = keys;
+        }
         u = eu, r = er;
         ++pass;
     }
@@ -938,6 +1086,429 @@ void raycast(lgs_map* m, std::vector<HitsPtr>&& scans, const lgs_builder_params*
     jobs[0].m = m;
     jobs[0].hs = std::move(scans);
     raycast_maps(m->ctx, jobs, bp);
+}
+
+// ---------------------------------------------------------------------------
+// The latest map's incremental rebuild
+//
+// UpdateLatestMap (C/mapping/grid_map_builder.cpp:196-207) rebuilds the latest
+// map from the last n scans after every scan: Resize to the scans' bounding box,
+// Reset, then every scan's rays in order.  When the box keeps the map's
+// geometry and the window only gained the new scan E (and lost its oldest L),
+// the result differs from the previous latest map only in the cells E or L
+// touches: every other cell sees the same update sequence from Unknown.  The
+// window's scans therefore keep their sorted key lists on the device (tagged
+// keys, one slot per scan), and a step casts E alone (plus its insert into the
+// local map, one pass), sorts its keys, indexes its runs and recomputes the
+// touched cells over the window's lists -- the other scans are neither re-cast
+// nor re-sorted.  Any other change (geometry, window, parameters) rebuilds in
+// full, which also re-seeds the lists.
+// ---------------------------------------------------------------------------
+struct KeyBuf {
+    void* base = nullptr;
+    long long cap = 0;
+    unsigned* keys = nullptr;
+    unsigned long long *hitw = nullptr, *endw = nullptr, *hit2 = nullptr, *miss2 = nullptr, *end2 = nullptr;
+    KeyBuf() = default;
+    KeyBuf(const KeyBuf&) = delete;
+    KeyBuf& operator=(const KeyBuf&) = delete;
+    ~KeyBuf()
+    {
+        if (base) hipFree(base);
+    }
+    RunBits bits() const { return RunBits{ hitw, endw, hit2, miss2, end2 }; }
+};
+typedef std::shared_ptr<KeyBuf> KeyBufPtr;
+
+KeyBufPtr keybuf_new(long long cap)
+{
+    KeyBufPtr b = std::make_shared<KeyBuf>();
+    const long long nw = (cap + 63) / 64 + 1, nw2 = (nw + 63) / 64 + 1;
+    const size_t kb = ((size_t)cap * 4 + 255) & ~(size_t)255;
+    if (hipMalloc(&b->base, kb + 8 * (size_t)(2 * nw + 3 * nw2)) != hipSuccess)
+        throw Error(LGS_ERR_OOM, "hipMalloc failed for latest-map key lists");
+    b->cap = cap;
+    b->keys = (unsigned*)b->base;
+    b->hitw = (unsigned long long*)((char*)b->base + kb);
+    b->endw = b->hitw + nw;
+    b->hit2 = b->endw + nw;
+    b->miss2 = b->hit2 + nw2;
+    b->end2 = b->miss2 + nw2;
+    return b;
+}
+
+struct LatestSlot {
+    unsigned long long uid = 0;
+    lgs_pose2d pose{ 0, 0, 0 };
+    unsigned stamp = 0;
+    KeyBufPtr buf;
+    long long beg = 0, end = 0;   // the scan's keys in buf
+};
+
+constexpr int kMaxWindow = kSlots - 1;              // E takes a free slot before L leaves
+constexpr size_t kMaxTblCells = 4u << 20;           // index table: 128 B per latest-map cell
+
+struct LatestCache {
+    bool valid = false;
+    int w = 0, h = 0;             // geometry the lists were cast in
+    double min_x = 0, min_y = 0;
+    double bpv[4] = {};           // usable range min/max, pHit, pMiss
+    std::vector<int> window;      // ring slots, oldest first
+    LatestSlot slot[kSlots];
+    unsigned long long* d_tbl = nullptr;
+    size_t tbl_cells = 0;
+    std::vector<KeyBufPtr> pool, retired;
+    int* h_bad = nullptr;         // mapped pinned word: a ray left the map (set by k_emit, never cleared)
+    int* d_bad = nullptr;
+    std::shared_ptr<WriterEvent> wev;   // end of the last step (the maps' pending writer)
+    bool pending = false;
+    char* pin = nullptr;
+    size_t pin_cap = 0;
+    long long n_incremental = 0, n_full = 0;
+    ~LatestCache()
+    {
+        for (auto& s : slot) s.buf.reset();
+        pool.clear();
+        retired.clear();
+        if (d_tbl) hipFree(d_tbl);
+        if (h_bad) hipHostFree(h_bad);
+        if (pin) hipHostFree(pin);
+    }
+    // the previous step has finished: its error word is final, the staging
+    // buffer is free, the lists it released can be reused
+    void finish()
+    {
+        if (pending) {
+            LGS_HIP_CHECK(hipEventSynchronize(wev->ev));
+            pending = false;
+        }
+        std::vector<KeyBufPtr> r;
+        r.swap(retired);
+        for (auto& b : r) {
+            if (b.use_count() == 1) pool.push_back(std::move(b));
+            else b.reset();
+        }
+        if (*h_bad) {
+            drop_lists();
+            *h_bad = 0;
+            throw Error(LGS_ERR_INTERNAL, "ray cell outside the map geometry");
+        }
+    }
+    KeyBufPtr acquire(long long need)
+    {
+        for (size_t i = 0; i < pool.size(); ++i)
+            if (pool[i]->cap >= need) {
+                KeyBufPtr b = std::move(pool[i]);
+                pool.erase(pool.begin() + (long)i);
+                return b;
+            }
+        if (pool.size() > 4) pool.erase(pool.begin());
+        return keybuf_new(need + need / 2 + 4096);
+    }
+    void drop_lists()
+    {
+        valid = false;
+        for (auto& s : slot) {
+            if (s.buf) retired.push_back(std::move(s.buf));
+            s = LatestSlot{};
+        }
+        window.clear();
+    }
+};
+
+LatestCache& cache_of(lgs_map* m)
+{
+    if (!m->cache) {
+        LatestCache* c = new LatestCache();
+        c->wev = std::make_shared<WriterEvent>();
+        if (hipHostMalloc((void**)&c->h_bad, 16, hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&c->d_bad, c->h_bad, 0) != hipSuccess ||
+            hipEventCreateWithFlags(&c->wev->ev, hipEventDisableTiming) != hipSuccess) {
+            delete c;
+            throw Error(LGS_ERR_OOM, "latest-map cache allocation failed");
+        }
+        *c->h_bad = 0;
+        m->cache = c;
+    }
+    return *m->cache;
+}
+
+// any other change of the map's cells invalidates its lists
+void invalidate_cache(lgs_map* m)
+{
+    if (!m->cache) return;
+    m->cache->finish();
+    m->cache->drop_lists();
+}
+
+bool same_pose(lgs_pose2d a, lgs_pose2d b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
+
+// The step's device work stays queued when the call returns: readers of the
+// maps on other streams wait for this event (grid_acquire).
+void record_writer(LatestCache& C, hipStream_t st, lgs_map* latest, lgs_map* local)
+{
+    LGS_HIP_CHECK(hipEventRecord(C.wev->ev, st));
+    C.wev->st = st;
+    C.pending = true;
+    latest->view.writer = C.wev;
+    if (local) local->view.writer = C.wev;
+}
+
+// Sensor/hit cells of one scan's rays in a map's geometry (as raycast_maps),
+// appended to rays/lens; returns the scan's key count.
+long long scan_rays(const lgs_map* m, const ScanHits& h, std::vector<int4>& rays, std::vector<int>& lens)
+{
+    int sx, sy;
+    world_to_cell(m, h.sensor.x, h.sensor.y, sx, sy);
+    long long keys = 0;
+    for (size_t k = 0; k + 1 < h.xy.size(); k += 2) {
+        int hx, hy;
+        world_to_cell(m, h.xy[k], h.xy[k + 1], hx, hy);
+        rays.push_back(make_int4(sx, sy, hx, hy));
+        const int L = std::max(std::abs(hx - sx), std::abs(hy - sy)) + 1;
+        lens.push_back(L);
+        keys += L;
+    }
+    return keys;
+}
+
+inline int bits_for(unsigned long long cells)
+{
+    int b = 1;
+    while (b < 32 && (1ull << b) < cells) ++b;
+    return b;
+}
+
+RayMap raymap_of(const lgs_map* m, unsigned long long base)
+{
+    return RayMap{ base, m->w, m->h, m->d_cells, m->d_hit, m->d_miss, m->d_palloc, m->ps, m->npx };
+}
+
+// One incremental step: E = the window's newest scan; L = its oldest (evict).
+void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, const lgs_scan* escan,
+                 lgs_pose2d epose, const HitsPtr& E, bool evict, const lgs_builder_params* bp)
+{
+    hipStream_t st = ctx->stream;
+    LatestSlot L;
+    int es = -1;
+    if (evict) {
+        es = C.window.front();
+        L = C.slot[es];
+        C.window.erase(C.window.begin());
+    } else {
+        bool used[kSlots] = {};
+        for (int q : C.window) used[q] = true;
+        for (int q = 0; q < kSlots && es < 0; ++q)
+            if (!used[q]) es = q;
+    }
+    // E's rays in the latest map's and the local map's geometry
+    std::vector<int4> rays;
+    std::vector<int> lens;
+    rays.reserve(E->xy.size());
+    lens.reserve(E->xy.size());
+    const long long nE = scan_rays(latest, *E, rays, lens);
+    const size_t nrE = rays.size();
+    const long long nloc = local ? scan_rays(local, *E, rays, lens) : 0;
+    const long long keys = nE + nloc;
+    const long long nr = (long long)rays.size();
+    const unsigned long long lat_cells = (unsigned long long)latest->w * latest->h;
+    const unsigned long long cells = lat_cells + (local ? (unsigned long long)local->w * local->h : 0ull);
+    LGS_REQUIRE(cells < (1ull << (32 - kTagShift)), "latest step: cell bits");
+    KeyBufPtr buf = C.acquire(std::max(1LL, keys));
+    const unsigned stamp = (unsigned)ctx->next_stamp();
+    // staging: chains | maps[2] | job | rays | offsets | ray->(map, tag)
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_maps = al(sizeof(BayesChains)), o_job = o_maps + al(2 * sizeof(RayMap));
+    const size_t o_rays = o_job + al(sizeof(WindowJob)), o_offs = o_rays + al(sizeof(int4) * nr);
+    const size_t o_rmap = o_offs + al(sizeof(long long) * nr), total = o_rmap + al(sizeof(int) * nr);
+    if (C.pin_cap < total) {
+        if (C.pin) hipHostFree(C.pin);
+        C.pin = nullptr;
+        C.pin_cap = 0;
+        if (hipHostMalloc((void**)&C.pin, 2 * total) != hipSuccess) throw Error(LGS_ERR_OOM, "hipHostMalloc failed");
+        C.pin_cap = 2 * total;
+    }
+    char* pin = C.pin;
+    char* d_stage = (char*)ctx->ensure(S_RAY6, total);
+    const BayesChains chains = make_chains(bp->prob_hit, bp->prob_miss);
+    std::memcpy(pin, &chains, sizeof(chains));
+    RayMap* pm = (RayMap*)(pin + o_maps);
+    pm[0] = raymap_of(latest, 0);
+    if (local) pm[1] = raymap_of(local, lat_cells);
+    int4* prays = (int4*)(pin + o_rays);
+    long long* poffs = (long long*)(pin + o_offs);
+    int* prm = (int*)(pin + o_rmap);
+    long long off = 0;
+    for (long long k = 0; k < nr; ++k) {
+        prays[k] = rays[k];
+        poffs[k] = off;
+        prm[k] = (k < (long long)nrE) ? (es << 16) : 1;
+        off += lens[k];
+    }
+    // the window after this step, oldest first, and its stamps
+    std::vector<int> order = C.window;
+    order.push_back(es);
+    WindowJob& J = *(WindowJob*)(pin + o_job);
+    std::memset(&J, 0, sizeof(J));
+    for (int q : order) {
+        const KeyBuf* b = (q == es) ? buf.get() : C.slot[q].buf.get();
+        J.slot[q] = SlotView{ b->keys, b->bits() };
+        J.st.s[q] = (q == es) ? stamp : C.slot[q].stamp;
+    }
+    for (size_t q = 0; q < order.size(); ++q) J.order[q] = order[q];
+    J.nwin = (int)order.size();
+    J.eslot = es;
+    J.latest = pm[0];
+    if (local) J.local = pm[1];
+    J.nE = nE;
+    J.nloc = nloc;
+    if (evict && L.buf) {
+        J.lkeys = L.buf->keys;
+        J.lrb = L.buf->bits();
+        J.lbeg = L.beg;
+        J.nL = L.end - L.beg;
+    }
+    J.tbl = C.d_tbl;
+    LGS_HIP_CHECK(hipMemcpyAsync(d_stage, pin, total, hipMemcpyHostToDevice, st));
+    unsigned* d_keys = (unsigned*)ctx->ensure(S_RAY2, sizeof(unsigned) * (size_t)std::max(1LL, keys));
+    unsigned* d_tmp = (unsigned*)ctx->ensure(S_RAY3, sizeof(unsigned) * (size_t)std::max(1LL, keys));
+    if (nr > 0) {
+        int tok = ctx->timing_begin(K_RAY_EMIT, 4.0 * (double)keys);
+        hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, st, (const int4*)(d_stage + o_rays),
+                           (const long long*)(d_stage + o_offs), (const int*)(d_stage + o_rmap), (int)nr, keys,
+                           (const RayMap*)(d_stage + o_maps), d_keys, C.d_bad, kTagShift);
+        ctx->timing_end(tok);
+        LGS_HIP_CHECK(hipGetLastError());
+    }
+    const long long nL = J.nL;
+    const int tok = ctx->timing_begin(K_RAY_APPLY, 4.0 * (double)(keys + nL));
+    if (keys > 0) {
+        keysort(ctx, d_keys, buf->keys, d_tmp, keys, kTagShift, bits_for(cells));
+        RunIndex ix{ C.d_tbl, nE, J.st };
+        const long long nw = (keys + 63) / 64;
+        hipLaunchKernelGGL(k_runmask, dim3((unsigned)((keys + 255) / 256)), dim3(256), 0, st, buf->keys, keys, 1,
+                           buf->hitw, buf->endw, ix);
+        hipLaunchKernelGGL(k_runsummary, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, buf->hitw, buf->endw,
+                           nw, buf->hit2, buf->miss2, buf->end2);
+    }
+    const long long nthreads = keys + nL;
+    if (nthreads > 0)
+        hipLaunchKernelGGL(k_apply_window, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, st,
+                           (const WindowJob*)(d_stage + o_job), (const BayesChains*)d_stage, bp->prob_hit,
+                           bp->prob_miss);
+    ctx->timing_end(tok);
+    LGS_HIP_CHECK(hipGetLastError());
+    record_writer(C, st, latest, local);
+    if (evict) C.retired.push_back(std::move(L.buf));
+    C.slot[es] = LatestSlot{ escan->uid, epose, stamp, buf, 0, nE };
+    C.window.push_back(es);
+    ++C.n_incremental;
+    if (ctx->profile) {
+        C.finish();
+        ctx->harvest();
+    }
+}
+
+// GridMapBuilder::UpdateLatestMap's ConstructMapFromScans over scans[0, n)
+// (:196-207, :227-332) and, with `local`, UpdateGridMap's insert of the newest
+// scan into the local map (:149-186) -- AppendScan (:48-59).  The two maps are
+// independent, so both ray-casts share one device pass.
+void latest_rebuild(lgs_ctx* ctx, lgs_map* latest, lgs_map* local, const lgs_scan* const* scans,
+                    const lgs_pose2d* poses, int n, const lgs_builder_params* bp)
+{
+    LatestCache& C = cache_of(latest);
+    C.finish();
+    latest->ctx = ctx;
+    if (local) local->ctx = ctx;
+    std::vector<MapJob> jobs(local ? 2 : 1);
+    jobs[0].m = latest;
+    if (local) jobs[1].m = local;
+    std::vector<std::array<double, 4>> box;
+    if (local) hits_and_boxes(jobs, { 0, n - 1 }, { n, 1 }, scans, poses, bp, box);
+    else hits_and_boxes(jobs, { 0 }, { n }, scans, poses, bp, box);
+    if (local) {
+        // the insert's box is the scan's own (sensor included, :346-352), not
+        // ConstructMapFromScans' running box with its DBL_MIN start
+        const double* bx = jobs[1].hs[0]->box;
+        map_expand(local, bx[0], bx[1], bx[2], bx[3], 5.0);                // :157-158
+    }
+    const ResizeGeom g = resize_geom(latest, box[0][0], box[0][1], box[0][2], box[0][3]);
+    const double bpv[4] = { bp->usable_range_min, bp->usable_range_max, bp->prob_hit, bp->prob_miss };
+    const bool same_geom = g.pminx == 0 && g.pminy == 0 && g.npx == latest->npx && g.npy == latest->npy &&
+                           C.w == latest->w && C.h == latest->h && C.min_x == latest->min_x &&
+                           C.min_y == latest->min_y;
+    // the new window = the cached one plus scans[n - 1], less its oldest scan (evict)
+    const int k = (int)C.window.size();
+    bool evict = false, shift_ok = false;
+    if (C.valid && n <= kMaxWindow && (n == k || n == k + 1)) {
+        evict = n == k;
+        shift_ok = true;
+        for (int i = 0; i + 1 < n && shift_ok; ++i) {
+            const LatestSlot& sl = C.slot[C.window[i + (evict ? 1 : 0)]];
+            shift_ok = sl.uid == scans[i]->uid && same_pose(sl.pose, poses[i]);
+        }
+    }
+    if (shift_ok && same_geom && std::memcmp(bpv, C.bpv, sizeof(bpv)) == 0) {
+        latest_step(ctx, C, latest, local, scans[n - 1], poses[n - 1], jobs[0].hs[n - 1], evict, bp);
+        return;
+    }
+    // full rebuild: Resize + Reset (:288-290), every scan; re-seeds the lists
+    C.drop_lists();
+    map_resize_reset(latest, box[0][0], box[0][1], box[0][2], box[0][3]);
+    const size_t lat_cells = (size_t)latest->w * latest->h;
+    const unsigned long long cells = lat_cells + (local ? (unsigned long long)local->w * local->h : 0ull);
+    const bool tagged = n <= kMaxWindow && lat_cells <= kMaxTblCells && cells < (1ull << (32 - kTagShift));
+    ++C.n_full;
+    if (!tagged) {
+        raycast_maps(ctx, jobs, bp);
+        return;
+    }
+    jobs[0].tags.resize((size_t)n);
+    for (int i = 0; i < n; ++i) jobs[0].tags[i] = i;
+    if (local) jobs[1].tags.assign(1, 0);
+    TagPass tp;
+    raycast_maps(ctx, jobs, bp, &tp);   // synchronises
+    if (!tp.ok) return;                 // too many keys for one pass: no lists
+    hipStream_t st = ctx->stream;
+    if (C.tbl_cells < lat_cells) {
+        if (C.d_tbl) LGS_HIP_CHECK(hipFree(C.d_tbl));
+        C.d_tbl = nullptr;
+        C.tbl_cells = 0;
+        if (hipMalloc(&C.d_tbl, sizeof(unsigned long long) * kSlots * lat_cells) != hipSuccess)
+            throw Error(LGS_ERR_OOM, "hipMalloc failed for the latest-map index");
+        LGS_HIP_CHECK(hipMemsetAsync(C.d_tbl, 0, sizeof(unsigned long long) * kSlots * lat_cells, st));
+        C.tbl_cells = lat_cells;
+    }
+    const long long nlat = tp.job_keys[0];
+    KeyBufPtr boot = C.acquire(std::max(1LL, nlat));
+    SlotStamps stamps{};
+    long long beg = 0;
+    C.window.clear();
+    for (int i = 0; i < n; ++i) {
+        stamps.s[i] = (unsigned)ctx->next_stamp();
+        C.slot[i] = LatestSlot{ scans[i]->uid, poses[i], stamps.s[i], boot, beg, beg + tp.tag_keys[i] };
+        beg += tp.tag_keys[i];
+        C.window.push_back(i);
+    }
+    if (nlat > 0) {
+        // the window's lists: the latest map's sorted keys partitioned by slot
+        // (stable: each slot's keys stay in cell order), runs of (cell, slot)
+        keysort(ctx, tp.sorted, boot->keys, nullptr, nlat, 1, 4);
+        const long long nw = (nlat + 63) / 64;
+        hipLaunchKernelGGL(k_runmask, dim3((unsigned)((nlat + 255) / 256)), dim3(256), 0, st, boot->keys, nlat, 1,
+                           boot->hitw, boot->endw, RunIndex{ C.d_tbl, nlat, stamps });
+        hipLaunchKernelGGL(k_runsummary, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, boot->hitw,
+                           boot->endw, nw, boot->hit2, boot->miss2, boot->end2);
+        LGS_HIP_CHECK(hipGetLastError());
+    }
+    *C.h_bad = 0;
+    C.w = latest->w;
+    C.h = latest->h;
+    C.min_x = latest->min_x;
+    C.min_y = latest->min_y;
+    std::memcpy(C.bpv, bpv, sizeof(bpv));
+    C.valid = true;
+    record_writer(C, st, latest, local);
 }
 
 }  // namespace
@@ -985,6 +1556,11 @@ extern "C" void lgs_map_destroy(lgs_map* m)
 {
     if (!m) return;
     hipSetDevice(m->device);
+    if (m->cache) {
+        if (m->cache->pending) hipEventSynchronize(m->cache->wev->ev);
+        delete m->cache;
+        m->cache = nullptr;
+    }
     map_free(m);
     palloc_free(m);
     delete m;
@@ -1018,6 +1594,7 @@ extern "C" int lgs_map_update_scan(lgs_ctx* ctx, lgs_map* m, const lgs_scan* sca
     return guarded(ctx, [&] {
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         m->ctx = ctx;
+        invalidate_cache(m);
         std::vector<HitsPtr> hs(1, cached_hits(scan, robot, bp, true));
         // bounding box starts at the sensor position (:346-352)
         const double* bx = hs[0]->box;
@@ -1034,12 +1611,7 @@ extern "C" int lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* m, const lgs_
     return guarded(ctx, [&] {
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         m->ctx = ctx;
-        std::vector<MapJob> jobs(1);
-        jobs[0].m = m;
-        std::vector<std::array<double, 4>> box;
-        hits_and_boxes(jobs, {0}, {n}, scans, poses, bp, box);       // :234-285
-        map_resize_reset(m, box[0][0], box[0][1], box[0][2], box[0][3]);  // :288-290
-        raycast_maps(ctx, jobs, bp);                                     // :293-329
+        latest_rebuild(ctx, m, nullptr, scans, poses, n, bp);   // :227-332
     });
 }
 
@@ -1052,20 +1624,9 @@ extern "C" int lgs_map_append_scan(lgs_ctx* ctx, lgs_map* local, lgs_map* latest
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         // GridMapBuilder::AppendScan (:48-59) = UpdateGridMap's insert of the
         // newest scan into the local map (:149-186) + UpdateLatestMap's
-        // ConstructMapFromScans over the last n scans (:196-207).  The two maps
-        // are independent, so both ray-casts share one device pass.
-        local->ctx = latest->ctx = ctx;
-        std::vector<MapJob> jobs(2);
-        jobs[0].m = local;
-        jobs[1].m = latest;
-        std::vector<std::array<double, 4>> box;
-        hits_and_boxes(jobs, { n - 1, 0 }, { 1, n }, scans, poses, bp, box);
-        // the insert's box is the scan's own (sensor included, :346-352), not
-        // ConstructMapFromScans' running box with its DBL_MIN start
-        const double* bx = jobs[0].hs[0]->box;
-        map_expand(local, bx[0], bx[1], bx[2], bx[3], 5.0);                     // :157-158
-        map_resize_reset(latest, box[1][0], box[1][1], box[1][2], box[1][3]);   // :288-290
-        raycast_maps(ctx, jobs, bp);
+        // ConstructMapFromScans over the last n scans (:196-207)
+        invalidate_cache(local);
+        latest_rebuild(ctx, latest, local, scans, poses, n, bp);
     });
 }
 
@@ -1084,6 +1645,7 @@ extern "C" int lgs_maps_construct_from_scans(lgs_ctx* ctx, lgs_map* const* maps,
     }
     return guarded(ctx, [&] {
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        for (int i = 0; i < n_maps; ++i) invalidate_cache(maps[i]);
         // AfterLoopClosure (:66-74): ConstructMapFromScans per local map; the
         // geometry of each is fixed before any ray is cast, so the ray-casts
         // of all maps run as one pass over the maps in order
@@ -1128,6 +1690,7 @@ extern "C" int lgs_map_render_gray(lgs_ctx* ctx, const lgs_map* m, uint8_t* imag
         const size_t n = (size_t)m->w * m->h;
         if (!n) return;
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        grid_acquire(ctx, &m->view);
         hipStream_t st = ctx->stream;
         uint8_t* d_img = (uint8_t*)ctx->ensure(S_RAY2, n);
         const long long threads = (long long)((m->w + 3) / 4) * m->h;
@@ -1147,6 +1710,7 @@ extern "C" int lgs_map_download(lgs_ctx* ctx, const lgs_map* m, double* cells, u
         const size_t n = (size_t)m->w * m->h;
         if (!n) return;
         hipStream_t st = ctx->stream;
+        grid_acquire(ctx, &m->view);
         if (cells)
             LGS_HIP_CHECK(hipMemcpyAsync(cells, m->d_cells, n * sizeof(double), hipMemcpyDeviceToHost, st));
         if (hit)
@@ -1167,6 +1731,7 @@ extern "C" int lgs_map_render_gray_region(lgs_ctx* ctx, const lgs_map* m, int x0
         const size_t n = (size_t)w * h;
         if (!n) return;
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        grid_acquire(ctx, &m->view);
         hipStream_t st = ctx->stream;
         uint8_t* d_img = (uint8_t*)ctx->ensure(S_RAY2, n);
         const long long threads = (long long)((w + 3) / 4) * h;
@@ -1185,6 +1750,7 @@ extern "C" int lgs_map_download_patches(lgs_ctx* ctx, const lgs_map* m, uint8_t*
         const size_t n = (size_t)m->npx * m->npy;
         if (!n) return;
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        grid_acquire(ctx, &m->view);
         LGS_HIP_CHECK(hipMemcpyAsync(flags, m->d_palloc, n, hipMemcpyDeviceToHost, ctx->stream));
         LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     });
@@ -1215,5 +1781,13 @@ extern "C" int lgs_map_actual_size(lgs_ctx* ctx, const lgs_map* m, int* num_allo
     out[4] = pminx * ps, out[5] = pminy * ps, out[6] = pmaxx * ps + ps, out[7] = pmaxy * ps + ps;  // :918-929
     out[8] = out[2] - out[0], out[9] = out[3] - out[1];                                     // mapSizeInPatches
     out[10] = out[6] - out[4], out[11] = out[7] - out[5];                                   // mapSizeInGridCells
+    return LGS_OK;
+}
+
+extern "C" int lgs_debug_map_rebuilds(const lgs_map* m, long long* incremental, long long* full)
+{
+    if (!m || !incremental || !full) return LGS_ERR_INVALID_ARG;
+    *incremental = m->cache ? m->cache->n_incremental : 0;
+    *full = m->cache ? m->cache->n_full : 0;
     return LGS_OK;
 }

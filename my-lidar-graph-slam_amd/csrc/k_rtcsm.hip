@@ -3433,6 +3433,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     int Nmax = 1;
     for (int j = 0; j < n; ++j) {
         check_args(grids[j], params, cost, scans[j]);
+        grid_acquire(ctx, grids[j]);
         LGS_REQUIRE(grids[j]->w == grids[0]->w && grids[j]->h == grids[0]->h && grids[j]->res == grids[0]->res,
                     "the maps of one batch must share their size and resolution");
         int nv = 0;
@@ -3660,6 +3661,7 @@ void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params
                     const lgs_pose2d* best, int n, lgs_rtcsm_summary* out)
 {
     if (n <= 0) return;
+    grid_acquire(ctx, grid);
     int Nmax = 1;
     for (int j = 0; j < n; ++j) Nmax = std::max(Nmax, scans[j]->n);
     const ItemLayout L = item_layout(1, 1, 1, 1, 1, 64, 1, Nmax);
@@ -3851,6 +3853,8 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
     if (!ctx || !grid || !coarse || !params || !scan) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        grid_acquire(ctx, grid);
+        grid_acquire(ctx, coarse);
         lgs_scan* s = const_cast<lgs_scan*>(scan);
         int nv = 0;
         scan_valid_indices(ctx, s, params->scan_range_max, &nv);
@@ -3920,6 +3924,7 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
     if (!ctx || !grid || !cost || !scan || !out_cost) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        grid_acquire(ctx, grid);
         const CostPlan cp = make_cost_plan(grid, cost, scan);
         const ItemLayout L = item_layout(1, 1, 1, 1, 1, 64, 1, scan->n);
         char* ws = (char*)ctx->ensure(S_BATCH_WS, L.total);

@@ -498,6 +498,7 @@ extern "C" int lgs_grid_download(lgs_ctx* ctx, const lgs_grid* g, double* host)
     return guarded(ctx, [&] {
         size_t bytes = (size_t)g->w * (size_t)g->h * sizeof(double);
         if (!bytes) return;
+        grid_acquire(ctx, g);
         LGS_HIP_CHECK(hipMemcpyAsync(host, g->d, bytes, hipMemcpyDeviceToHost, ctx->stream));
         ctx->sync();
     });
@@ -854,6 +855,7 @@ extern "C" int lgs_grid_precompute_max(lgs_ctx* ctx, const lgs_grid* in, int win
         LGS_REQUIRE(win >= 1, "window must be >= 1");
         LGS_REQUIRE(out->w == in->w && out->h == in->h, "precompute output geometry mismatch");
         LGS_REQUIRE(out->d != in->d, "precompute cannot run in place");
+        grid_acquire(ctx, in);
         out->min_x = in->min_x;
         out->min_y = in->min_y;
         out->res = in->res;
@@ -872,6 +874,8 @@ extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan**
         LGS_REQUIRE(hs->n >= 1 && hs->ranges && hs->angles, "scan must have >= 1 beam");
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         lgs_scan* s = new lgs_scan();
+        static std::atomic<unsigned long long> uids{ 0 };
+        s->uid = uids.fetch_add(1, std::memory_order_relaxed) + 1;
         s->ctx = ctx;
         s->device = ctx->device;
         s->n = hs->n;

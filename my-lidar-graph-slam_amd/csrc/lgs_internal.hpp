@@ -285,6 +285,23 @@ struct lgs_ctx {
     void release();
 };
 
+namespace lgs {
+// Device work still writing a map's cells when its call returned (the latest
+// map's asynchronous incremental rebuild, k_raycast.hip): an event on the
+// writer's stream.  Readers on another stream wait for it (grid_acquire).
+struct WriterEvent {
+    hipEvent_t ev = nullptr;
+    hipStream_t st = nullptr;
+    WriterEvent() = default;
+    WriterEvent(const WriterEvent&) = delete;
+    WriterEvent& operator=(const WriterEvent&) = delete;
+    ~WriterEvent()
+    {
+        if (ev) hipEventDestroy(ev);
+    }
+};
+}  // namespace lgs
+
 struct lgs_grid {
     lgs_ctx* ctx = nullptr;   // creating context (not used after its destruction)
     int device = 0;
@@ -293,11 +310,13 @@ struct lgs_grid {
     double min_x = 0, min_y = 0, res = 0;
     bool owned = false;       // device cells freed by lgs_grid_destroy
     bool map_view = false;    // handle embedded in an lgs_map: destroy is a no-op
+    std::shared_ptr<lgs::WriterEvent> writer;   // pending writer of the cells (null: none)
 };
 
 struct lgs_scan {
     lgs_ctx* ctx = nullptr;   // creating context (not used after its destruction)
     int device = 0;
+    unsigned long long uid = 0;   // process-unique id (the latest map's window identity, §4.4b)
     double* d_ranges = nullptr;
     double* d_angles = nullptr;
     int n = 0;
@@ -350,6 +369,14 @@ inline lgs_pose2d inverse_compound(lgs_pose2d s, lgs_pose2d e)
 }
 
 const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* scan, double scan_range_max, int* nv);
+
+// Order a read of g's cells on ctx's stream after a pending asynchronous write
+// from another stream (a device-side wait, no host synchronisation).
+inline void grid_acquire(lgs_ctx* ctx, const lgs_grid* g)
+{
+    if (g && g->writer && g->writer->st != ctx->stream)
+        LGS_HIP_CHECK(hipStreamWaitEvent(ctx->stream, g->writer->ev, 0));
+}
 
 // Host staging of one batch's descriptors: appended to a pinned buffer, then
 // one host-to-device copy into the S_UPLOAD slot (flush).  Offsets are
@@ -416,5 +443,10 @@ int guarded(lgs_ctx* ctx, F&& f)
 // including the caller; at most ceil(n / grain) of them).  f must not throw.
 // One parallel region runs at a time; nested calls run inline.
 void host_parallel_for(int n, int grain, const std::function<void(int)>& f);
+
+// K3 sort (k_sort.hip): stable LSD radix sort of n 32-bit keys on bits
+// [lo, lo + bits) into `out`; `tmp` (n keys) is used when the sort takes two
+// or more 8-bit passes.  in, tmp and out are distinct device buffers.
+void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, long long n, int lo, int bits);
 
 }  // namespace lgs

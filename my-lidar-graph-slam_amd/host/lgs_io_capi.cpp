@@ -79,7 +79,7 @@ int guarded(F&& f)
 }  // namespace
 
 extern "C" long long lgs_carmen_load(const char* text, double* out, long long cap, char* ids, long long ids_cap,
-                                     int* num_records)
+                                     long long* ids_bytes, int* num_records)
 {
     if (!text) return -1;
     try {
@@ -108,6 +108,7 @@ extern "C" long long lgs_carmen_load(const char* text, double* out, long long ca
             }
         }
         if (num_records) *num_records = (int)data.size();
+        if (ids_bytes) *ids_bytes = (long long)names.size();
         if (out && cap > 0)
             std::memcpy(out, v.data(), sizeof(double) * (size_t)std::min<long long>(cap, (long long)v.size()));
         if (ids && ids_cap > 0) std::memcpy(ids, names.data(), std::min<size_t>((size_t)ids_cap, names.size()));

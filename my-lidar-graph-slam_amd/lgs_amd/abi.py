@@ -248,6 +248,8 @@ _PROTOS = [
                                                    C.POINTER(Pose2D), C.c_int, C.POINTER(LinsolveSummary)]),
     ("lgs_cost_square_error", C.c_int, [_P, _P, C.c_double, C.c_double, _P, Pose2D, C.POINTER(C.c_double),
                                         C.POINTER(C.c_double)]),
+    ("lgs_debug_keysort", C.c_int, [_P, _P, _P, C.c_longlong, C.c_int, C.c_int]),
+    ("lgs_debug_map_rebuilds", C.c_int, [_P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     ("lgs_debug_item_buffer", C.c_int, [_P, C.c_int, C.c_int, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("lgs_debug_libm", C.c_int, [_P, C.c_int, _P, C.c_int, _P]),
 ]
@@ -595,6 +597,15 @@ class Context:
                    "debug_libm")
         return out
 
+    def debug_keysort(self, keys, lo: int, bits: int) -> np.ndarray:
+        """Diagnostics: the K3 stable radix sort (csrc/k_sort.hip) of host u32
+        keys on bits [lo, lo + bits) (lgs_debug_keysort)."""
+        k = np.ascontiguousarray(keys, dtype=np.uint32)
+        out = np.zeros_like(k)
+        self.check(self.lib.lgs_debug_keysort(self.h, k.ctypes.data_as(_P), out.ctypes.data_as(_P), len(k), lo, bits),
+                   "debug_keysort")
+        return out
+
     def cost_greedy_endpoint(self, grid, cost: CostGEParams, scan, pose) -> float:
         v = C.c_double()
         self.check(self.lib.lgs_cost_greedy_endpoint(self.h, grid.h, C.byref(cost), scan.h, Pose2D(*pose),
@@ -675,6 +686,13 @@ class Map:
         ps = (Pose2D * n)(*[Pose2D(*p) for p in poses])
         self.ctx.check(self.ctx.lib.lgs_map_append_scan(self.ctx.h, self.h, latest.h, arr, ps, n, C.byref(bp)),
                        "map_append_scan")
+
+    def rebuilds(self) -> dict:
+        """Diagnostics: incremental and full latest-map rebuilds of this map
+        (lgs_debug_map_rebuilds)."""
+        a, b = C.c_longlong(), C.c_longlong()
+        self.ctx.check(self.ctx.lib.lgs_debug_map_rebuilds(self.h, C.byref(a), C.byref(b)), "debug_map_rebuilds")
+        return {"incremental": a.value, "full": b.value}
 
     def render_gray(self) -> np.ndarray:
         """MapSaver::DrawMap gray image (rows flipped up-down), uint8 [h, w]."""

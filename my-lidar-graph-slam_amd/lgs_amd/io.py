@@ -41,6 +41,7 @@ class MapSaveOptions(C.Structure):
 
 _PROTOS = [
     ("lgs_carmen_load", C.c_longlong, [C.c_char_p, _D, C.c_longlong, C.c_char_p, C.c_longlong,
+                                       C.POINTER(C.c_longlong),
                                        C.POINTER(C.c_int)]),
     ("lgs_pose_graph_optimize_lm", C.c_int, [C.POINTER(LMParams), C.POINTER(Pose2D), C.c_int,
                                              C.POINTER(PoseGraphEdge), C.c_int, C.POINTER(C.c_int), _D]),
@@ -79,12 +80,13 @@ def carmen_load(text: str):
     L = load()
     raw = text.encode()
     n = C.c_int()
-    need = L.lgs_carmen_load(raw, None, 0, None, 0, C.byref(n))
+    nid = C.c_longlong()
+    need = L.lgs_carmen_load(raw, None, 0, None, 0, C.byref(nid), C.byref(n))
     if need < 0:
         raise ValueError("CarmenLogReader failed")
     out = np.zeros(max(1, need))
-    ids = C.create_string_buffer(64 * (n.value + 1) + 1024)
-    L.lgs_carmen_load(raw, _dp(out), need, ids, len(ids), C.byref(n))
+    ids = C.create_string_buffer(max(1, nid.value))
+    L.lgs_carmen_load(raw, _dp(out), need, ids, len(ids), None, C.byref(n))
     names = ids.raw.split(b"\0")[: n.value]
     return out[:need], [s.decode() for s in names], n.value
 

@@ -1,0 +1,62 @@
+"""The K3 sort (csrc/k_sort.hip): the hand-written stable LSD radix sort that
+orders every ray-cast pass's keys by cell (C/mapping/grid_map_builder.cpp:170-186
+applies a cell's updates in ray order, so the sort must be stable).  Checked
+against numpy's stable argsort on the same bit field, key for key, for empty,
+tiny, ragged and multi-million inputs, one- to four-pass bit ranges, and the
+clustered, nearly sorted key streams a Bresenham ray-cast emits."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def expected(keys, lo, bits):
+    f = (keys >> np.uint32(lo)) & np.uint32((1 << bits) - 1) if bits < 32 else keys
+    return keys[np.argsort(f, kind="stable")]
+
+
+@pytest.mark.parametrize("n,lo,bits", [(0, 1, 20), (1, 1, 20), (63, 1, 8), (1000, 1, 8), (4097, 1, 9),
+                                       (100_000, 1, 21), (300_001, 5, 20), (65_536, 0, 32), (5000, 1, 0),
+                                       (2_500_000, 1, 22), (3_000_003, 5, 24)])
+def test_keysort_random(ctx, n, lo, bits):
+    rng = np.random.default_rng(n + 7 * bits)
+    keys = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    got = ctx.debug_keysort(keys, lo, bits)
+    assert np.array_equal(got, expected(keys, lo, bits))
+
+
+def test_keysort_ray_like(ctx):
+    """Keys as k_emit writes them: per ray a run of distinct cells along a line,
+    many rays through the cells next to the sensor, hit bit in bit 0 -- equal
+    cells must keep ray order (the low bits carry the ray index here)."""
+    rng = np.random.default_rng(3)
+    W = 900
+    keys = []
+    for s in range(12):
+        sx, sy = rng.integers(300, 600, 2)
+        for r in range(1081):
+            a = 2 * np.pi * r / 1081
+            L = int(rng.integers(1, 300))
+            t = np.arange(L)
+            x = (sx + np.round(t * np.cos(a))).astype(np.int64)
+            y = (sy + np.round(t * np.sin(a))).astype(np.int64)
+            cell = y * W + x
+            k = (cell << 5) | ((s & 15) << 1) | (t == L - 1)
+            keys.append(k.astype(np.uint32))
+    keys = np.concatenate(keys)
+    for lo, bits in ((5, 20), (1, 24)):
+        got = ctx.debug_keysort(keys, lo, bits)
+        assert np.array_equal(got, expected(keys, lo, bits))
+
+
+def test_keysort_all_equal_digits(ctx):
+    """Every key in one digit bucket (the look-back's worst case: one digit's
+    run spans all tiles) and an already sorted / reverse-sorted input."""
+    n = 1_500_000
+    rng = np.random.default_rng(11)
+    same = (np.full(n, 77, dtype=np.uint32) << 1) | rng.integers(0, 2, n).astype(np.uint32)
+    assert np.array_equal(ctx.debug_keysort(same, 1, 16), expected(same, 1, 16))
+    srt = np.sort(rng.integers(0, 2 ** 22, n).astype(np.uint32))
+    assert np.array_equal(ctx.debug_keysort(srt, 0, 22), srt)
+    rev = srt[::-1].copy()
+    assert np.array_equal(ctx.debug_keysort(rev, 0, 22), expected(rev, 0, 22))

@@ -53,6 +53,24 @@ def test_carmen_reader_matches_reference_live():
             assert np.array_equal(bits(s1), bits(s2))
 
 
+def test_carmen_ids_byte_count():
+    """lgs_carmen_load reports the bytes the sensor ids need (terminators
+    included), so a caller sizes the ids buffer exactly; a short buffer gets
+    a prefix and the same count."""
+    import ctypes as C
+    text = "ODOM 1 2 3 4 5 6 7.5 host 8\n" * 40 + "ROBOTLASER1 0 -1 2 0.25 30 0.1 0 2 4 5 0 0 0.1 2 1 0.2 0 0 0 0 0 11.5 h 12\n"
+    L = io.load()
+    n, nid = C.c_int(), C.c_longlong()
+    need = L.lgs_carmen_load(text.encode(), None, 0, None, 0, C.byref(nid), C.byref(n))
+    assert need > 0 and n.value == 41 and nid.value == 40 * len("ODOM\0") + len("ROBOTLASER1\0")
+    small = C.create_string_buffer(7)
+    nid2 = C.c_longlong()
+    L.lgs_carmen_load(text.encode(), None, 0, small, 7, C.byref(nid2), None)
+    assert nid2.value == nid.value and small.raw == b"ODOM\0OD"
+    _, ids, _ = io.carmen_load(text)
+    assert ids == ["ODOM"] * 40 + ["ROBOTLASER1"]
+
+
 def test_carmen_record_layout():
     """a hand-written log: what each record type carries"""
     text = ("PARAM Laser.AngleIncrement 0.5\n"
