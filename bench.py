@@ -57,7 +57,6 @@ def parse():
     ap.add_argument("--workload", default="match", choices=["match", "refine", "loop", "loop_bb", "stream", "rebuild"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--coarse-planes", type=int, default=1, help="A/B: 1 phase-plane coarse layout, 0 plain")
     ap.add_argument("--spin-sync", type=int, default=1, help="1 spin on the stream when waiting, 0 blocking wait")
     ap.add_argument("--skip-kernels", default="",
                     help="diagnostics only: comma-separated kernel names not launched (results invalid)")
@@ -71,9 +70,6 @@ def parse():
                          "128 per call: 45.1k vs 41.6k scans/s for 64 (one host synchronisation per two chunks)")
     ap.add_argument("--lanes-min-batch", type=int, default=None,
                     help="A/B: LGS_OPT_LANES_MIN_BATCH (pruned coarse stage kernel choice by batch size)")
-    ap.add_argument("--super-quad", type=int, default=None, help="A/B: LGS_OPT_SUPER_QUAD")
-    ap.add_argument("--super-hex", type=int, default=None, help="A/B: LGS_OPT_SUPER_HEX")
-    ap.add_argument("--fine-lanes", type=int, default=None, help="A/B: LGS_OPT_FINE_LANES")
     ap.add_argument("--latency-calls", type=int, default=100,
                     help="match workload: lone OptimizePose(query) calls timed for p50/p90 (0 = skip, e.g. under "
                          "rocprofv3 so that the trace holds the batched launches only)")
@@ -398,17 +394,10 @@ def run_match(args, D, ctx):
     ctxs = [ctx] + [abi.Context(D.local) for _ in range(S - 1)]
     state = []
     for c in ctxs:
-        c.set_option(abi.LGS_OPT_COARSE_PLANES, args.coarse_planes)
         c.set_option(abi.LGS_OPT_SUPER_PRUNE, args.super_prune)
         c.set_option(abi.LGS_OPT_SPIN_SYNC, args.spin_sync)
         if args.lanes_min_batch is not None:
             c.set_option(abi.LGS_OPT_LANES_MIN_BATCH, args.lanes_min_batch)
-        if args.super_quad is not None:
-            c.set_option(abi.LGS_OPT_SUPER_QUAD, args.super_quad)
-        if args.super_hex is not None:
-            c.set_option(abi.LGS_OPT_SUPER_HEX, args.super_hex)
-        if args.fine_lanes is not None:
-            c.set_option(abi.LGS_OPT_FINE_LANES, args.fine_lanes)
         state.append((c, c.grid_from_array(cells, mx, my, 0.05), [c.scan(r, ang) for r in scans]))
     P, cost = abi.RtcsmParams(*PARAMS), abi.CostGEParams(*COST)
     n = len(scans)

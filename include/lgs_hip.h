@@ -161,16 +161,12 @@ int  lgs_abi_version(void);
 #define LGS_OPT_INJECT_INDEX  3
 #define LGS_OPT_GUARD_CAP     4
 #define LGS_OPT_PROFILE       5   /* 1 = time every kernel launch with HIP events on the ctx stream */
-#define LGS_OPT_COARSE_PLANES 6   /* 1 (default) = phase-plane coarse layout, 0 = plain layout (A/B) */
 #define LGS_OPT_PROFILE_MASK  7   /* time only the kernels whose lgs_kernel_stat index bit is set (0 = off) */
 #define LGS_OPT_SPIN_SYNC     8   /* 1 (default) = spin on the stream when waiting for results, 0 = blocking wait */
 #define LGS_OPT_SKIP_MASK     10  /* diagnostics only: bitmask of kernels (lgs_ctx_kernel_stats order) not launched -- results are invalid */
 #define LGS_OPT_SUPER_PRUNE   9   /* 1 (default) = skip coarse blocks whose 4x4-superblock bound is below the seed score, 0 = evaluate every coarse block */
-#define LGS_OPT_SUPER_QUAD    12  /* 1 (default) = superblock bounds with 8-byte gathers where the window allows, 0 = 4-byte (A/B) */
-#define LGS_OPT_SUPER_HEX     14  /* 1 (default) = superblock bounds with 4 fp16 superblocks per 8-byte gather where the window allows, 0 = k_super_quad (A/B) */
 #define LGS_OPT_RAY_CHUNK_KEYS 13  /* ray-cast keys per emit/sort/apply pass (default 2^28, max 2^30); more keys are cast in scan order over several passes */
 #define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: lane-per-block kernel for batches of at least this many matches (default 2; 1 = always), else the row kernel */
-#define LGS_OPT_FINE_LANES    16  /* 1 (default) = fine stage with one lane per pose over the batch's block list, 0 = transposed row evaluator (A/B) */
 #define LGS_OPT_LINSOLVE_SPLIT 17 /* 1 (default) = a lone ScanMatcherLinearSolver refine of <= 1280 beams runs one workgroup per 64 beams (in-launch hand-off per pass) when they fit the device at once, 0 = one workgroup */
 #define LGS_OPT_HANDOFF_SPIN_US 18 /* split refine: bound of a workgroup's wait for the others (default 200000 us); on time-out the refine is rerun on one workgroup.  0 = force that fallback (tests) */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */

@@ -10,7 +10,7 @@
 //
 //   host       hit points with glibc sin/cos (bit-exact), bounding box, map
 //              geometry (Expand/Resize), sensor/hit cells, ray lengths + offsets
-//   k_emit     one thread per ray walks Bresenham (H/util.hpp:256-303) and emits
+//   k_emit     one wave per ray computes its Bresenham cells (H/util.hpp:256-303) and emits
 //              a 32-bit key (cell << 1 | is_hit) per visited cell at the ray's
 //              offset, so the key array is in ray order
 //   sort       stable radix sort on the cell bits only (k_sort.hip): each
@@ -99,79 +99,63 @@ struct RayMap {
     int ps, npx;
 };
 
-// One thread per ray: Bresenham walk (H/util.hpp:256-303), start cell
-// inclusive, end (hit) cell last.  rmap[r] names the ray's map (null: map 0).
-// The 64 rays of a workgroup (one wave) own one contiguous key range (their
-// offsets are consecutive), so when that range fits kEmitLds keys the walk
-// writes into LDS and the wave then copies the range out with coalesced
-// stores (one thread per ray writing its own run would touch 64 lines per
-// store instruction); longer ranges are written directly.
-constexpr int kEmitLds = 8192;   // keys staged per 64-ray wave (0 = direct stores: 268 vs 213 us per rebuild)
-__global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
-                                             const long long* __restrict__ offs,
-                                             const int* __restrict__ rmap, int nrays,
-                                             long long nkeys, const RayMap* __restrict__ maps,
-                                             unsigned* __restrict__ keys,
-                                             int* __restrict__ outside, int ksh)
+// One wave per ray: the ray's Bresenham cells (H/util.hpp:256-303, start cell
+// inclusive, the hit cell last) in closed form, so the 64 lanes write 64
+// consecutive keys of the ray (coalesced) instead of one lane walking it.
+// With major axis M (|dM| >= |dm|, ties go to y as in the reference's else
+// branch), doubled deltas DM = 2|dM|, Dm = 2|dm| and err0 = Dm - DM/2, the
+// reference's loop emits at iteration k (k = 0 .. |dM| - 1) the cell
+// (M0 + k sM, m0 + j_k sm) where j_k counts the minor steps taken before it:
+// j_0 = 0 and j_k = floor((err0 + (k - 1) Dm) / DM) + 1 (its err stays in
+// [-DM, Dm), and err_k - Dm lies in [-DM, 0) after every iteration); the
+// hit cell (key k = |dM|) follows.  rmap[r] = map index | slot tag << 16.
+__global__ __launch_bounds__(256) void k_emit(const int4* __restrict__ rays,
+                                              const long long* __restrict__ offs,
+                                              const int* __restrict__ rmap, int nrays,
+                                              const RayMap* __restrict__ maps,
+                                              unsigned* __restrict__ keys,
+                                              int* __restrict__ outside, int ksh)
 {
-    __shared__ unsigned buf[kEmitLds > 0 ? kEmitLds : 1];
-    const int r0 = blockIdx.x * 64;
-    const int r = r0 + threadIdx.x;
-    const long long base = offs[r0];
-    const long long end = (r0 + 64 < nrays) ? offs[r0 + 64] : nkeys;
-    const bool staged = kEmitLds > 0 && end - base <= kEmitLds;   // uniform
-    if (r < nrays) {
-        const int4 ry = rays[r];
-        const int rm = rmap ? rmap[r] : 0;       // map index | slot tag << 16
-        const RayMap mp = maps[rm & 0xffff];
-        const unsigned tag = ((unsigned)rm >> 16) << 1;
-        const int W = mp.w, H = mp.h;
-        const unsigned cbase = (unsigned)mp.base;
-        unsigned* out = staged ? buf + (offs[r] - base) : keys + offs[r];
-        int deltaX = ry.z - ry.x;
-        int deltaY = ry.w - ry.y;
-        const int stepX = (deltaX < 0) ? -1 : 1;
-        const int stepY = (deltaY < 0) ? -1 : 1;
-        int nx = ry.x, ny = ry.y;
-        deltaX = abs(deltaX * 2);
-        deltaY = abs(deltaY * 2);
-        int bad = 0;
-        auto emit = [&](int x, int y, unsigned hit) {
-            const bool in = (unsigned)x < (unsigned)W && (unsigned)y < (unsigned)H;
-            bad |= !in;
-            const unsigned cell = cbase + (in ? (unsigned)y * (unsigned)W + (unsigned)x : 0u);
-            *out++ = (cell << ksh) | tag | hit;
-        };
-        if (deltaX > deltaY) {
-            int err = deltaY - deltaX / 2;
-            while (nx != ry.z) {
-                emit(nx, ny, 0u);
-                if (err >= 0) {
-                    ny += stepY;
-                    err -= deltaX;
-                }
-                nx += stepX;
-                err += deltaY;
-            }
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nrays) return;
+    const int4 ry = rays[r];
+    const int rm = rmap ? rmap[r] : 0;
+    const RayMap mp = maps[rm & 0xffff];
+    const unsigned tag = ((unsigned)rm >> 16) << 1;
+    const unsigned W = (unsigned)mp.w, H = (unsigned)mp.h;
+    const unsigned cbase = (unsigned)mp.base;
+    const int dx = ry.z - ry.x, dy = ry.w - ry.y;
+    const bool xmaj = 2 * abs(dx) > 2 * abs(dy);
+    const int sM = xmaj ? ((dx < 0) ? -1 : 1) : ((dy < 0) ? -1 : 1);
+    const int sm = xmaj ? ((dy < 0) ? -1 : 1) : ((dx < 0) ? -1 : 1);
+    const long long DM = 2LL * (xmaj ? abs(dx) : abs(dy)), Dm = 2LL * (xmaj ? abs(dy) : abs(dx));
+    const long long err0 = Dm - DM / 2;
+    const int L = (int)(DM / 2);               // cells before the hit cell
+    unsigned* out = keys + offs[r];
+    const bool small = err0 + (long long)L * Dm < (1LL << 31);   // 32-bit division suffices (uniform)
+    int bad = 0;
+#pragma nounroll
+    for (int k = lane; k <= L; k += 64) {
+        int x, y;
+        unsigned hit = 0u;
+        if (k == L) {
+            x = ry.z, y = ry.w, hit = 1u;
         } else {
-            int err = deltaX - deltaY / 2;
-            while (ny != ry.w) {
-                emit(nx, ny, 0u);
-                if (err >= 0) {
-                    nx += stepX;
-                    err -= deltaY;
-                }
-                ny += stepY;
-                err += deltaX;
-            }
+            const long long num = err0 + (long long)(k - 1) * Dm;
+            long long j = 0;
+            if (k > 0 && num >= 0)
+                j = (small ? (long long)((unsigned)num / (unsigned)DM) : num / DM) + 1;
+            const int M = k * sM, m = (int)j * sm;
+            x = ry.x + (xmaj ? M : m);
+            y = ry.y + (xmaj ? m : M);
         }
-        emit(nx, ny, 1u);  // == (hx, hy): the hit cell, updated last
-        if (bad) *outside = 1;
+        const bool in = (unsigned)x < W && (unsigned)y < H;
+        bad |= !in;
+        const unsigned cell = cbase + (in ? (unsigned)y * W + (unsigned)x : 0u);
+        out[k] = (cell << ksh) | tag | hit;
     }
-    if (!staged) return;
-    __syncthreads();
-    const int n = (int)(end - base);
-    for (int j = threadIdx.x; j < n; j += 64) keys[base + j] = buf[j];
+    if (bad) *outside = 1;
 }
 
 // k_runmask: one thread per sorted key; each wavefront covers 64 consecutive
@@ -179,10 +163,15 @@ __global__ __launch_bounds__(64) void k_emit(const int4* __restrict__ rays,
 // hitw = key j is a hit, bit j of endw = key j is the last of its run (keys
 // equal above bit rsh: rsh = ksh, runs of one cell; rsh = 1, runs of one
 // (cell, slot) pair in the latest map's slot lists).  With an index table,
-// the key at the start of each run below `nidx` also records its position:
-// tbl[cell * kSlots + slot] = stamp(slot) << 32 | position.
+// the key at the start of each run below `nidx` also records the run:
+// tbl[cell * kSlots + slot] = stamp(slot) << 32 | entry, where the entry of a
+// run of at most kShortRun keys inside this wave's 64 keys is the run itself
+// (length << 26 | hit bits, bit j = update j is a hit), and any other run's
+// is kLongRun | its position (walked through the bitmaps).
 constexpr int kSlots = 16;          // latest-map scan slots (slot tag: key bits 1..4)
 constexpr int kTagShift = 5;        // tagged keys: cell << 5 | slot << 1 | hit
+constexpr int kShortRun = 26;       // runs stored inline in the index
+constexpr unsigned kLongRun = 0x80000000u;
 struct SlotStamps {
     unsigned s[kSlots];
 };
@@ -207,7 +196,21 @@ __global__ __launch_bounds__(256) void k_runmask(const unsigned* __restrict__ ke
     }
     if (ix.tbl && i < ix.nidx && (i == 0 || (keys[i - 1] >> rsh) != (k >> rsh))) {
         const unsigned slot = (k >> 1) & (kSlots - 1);
-        ix.tbl[(size_t)(k >> kTagShift) * kSlots + slot] = ((unsigned long long)ix.st.s[slot] << 32) | (unsigned)i;
+        const int lane = (int)(i & 63);
+        const unsigned long long rest = eb >> lane;   // run ends at the first set bit
+        int len = rest ? __ffsll((long long)rest) : 0;
+        unsigned bits = len ? (unsigned)((hb >> lane) & ((len >= 64) ? ~0ull : ((1ull << len) - 1ull))) : 0u;
+        if (!len && 64 - lane < kShortRun) {
+            // the run continues past this wave's keys: read on up to kShortRun keys
+            len = 64 - lane;
+            bits = (unsigned)(hb >> lane);
+            while (len <= kShortRun && i + len < n && (keys[i + len] >> rsh) == (k >> rsh)) {
+                bits |= (keys[i + len] & 1u) << len;
+                ++len;
+            }
+        }
+        const unsigned entry = (len >= 1 && len <= kShortRun) ? ((unsigned)len << 26) | bits : kLongRun | (unsigned)i;
+        ix.tbl[(size_t)(k >> kTagShift) * kSlots + slot] = ((unsigned long long)ix.st.s[slot] << 32) | entry;
     }
 }
 
@@ -302,6 +305,7 @@ BayesChains make_chains(double p_hit, double p_miss)
 // The run bitmaps of one sorted key array (k_runmask / k_runsummary).
 struct RunBits {
     const unsigned long long *hitw, *endw, *hit2, *miss2, *end2;
+    long long nw;   // words of hitw / endw
 };
 
 // Constants of the Bayes walk, evaluated once per thread.
@@ -317,6 +321,69 @@ struct BayesK {
     }
 };
 
+// Where v sits on the memoised chains (-1: on none) and its index there.
+struct ChainState {
+    int cm, jm, ck, jk;
+    __device__ ChainState(double v, const BayesChains* __restrict__ ch)
+    {
+        cm = (v == ch->a[0]) ? 0 : (v == ch->a[2]) ? 2 : -1;
+        ck = (v == ch->a[1]) ? 1 : (v == ch->a[3]) ? 3 : -1;
+        jm = jk = 0;
+    }
+};
+
+// cnt updates in order (bit j of h: update j is a hit, of m: a miss) applied
+// to v: same-type stretches jump along the chains, identity updates are
+// skipped; every other update is BinaryBayesGridCell::Update itself.
+__device__ __forceinline__ double apply_word(double v, ChainState& s, unsigned long long h, unsigned long long m,
+                                             int cnt, const BayesChains* __restrict__ ch, const BayesK& K)
+{
+    const double a0 = ch->a[0], a1 = ch->a[1], a2 = ch->a[2], a3 = ch->a[3];
+    int pos = 0;
+    while (pos < cnt) {
+        if (K.miss_fixed && v == kPMin) {        // misses are identities: next hit
+            const unsigned long long rest = h >> pos;
+            if (!rest) break;
+            pos += __ffsll((long long)rest) - 1;
+        } else if (K.hit_fixed && v == kPMax) {  // hits are identities: next miss
+            const unsigned long long rest = m >> pos;
+            if (!rest) break;
+            pos += __ffsll((long long)rest) - 1;
+        }
+        const bool is_hit = (h >> pos) & 1ull;
+        const int c = is_hit ? s.ck : s.cm;
+        if (c >= 0) {
+            // k same-type updates from pos: jump along the chain
+            const unsigned long long other = (is_hit ? m : h) >> pos;
+            const int k = other ? __ffsll((long long)other) - 1 : cnt - pos;
+            const int last = ch->len[c] - 1;
+            const int j0 = is_hit ? s.jk : s.jm;
+            int j = j0 + k, used = k;
+            if (j > last) {
+                if (!ch->fixed[c]) used = last - j0;  // table ends: the rest normally
+                j = last;
+            }
+            v = ch->t[c][j];
+            pos += used;
+            if (is_hit) {
+                s.jk = j;
+                if (used < k) s.ck = -1;
+                s.cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, s.jm = 0;
+            } else {
+                s.jm = j;
+                if (used < k) s.cm = -1;
+                s.ck = (v == a1) ? 1 : (v == a3) ? 3 : -1, s.jk = 0;
+            }
+            continue;
+        }
+        v = bayes_update_k(v, is_hit ? K.cph : K.cpm, is_hit ? K.oph : K.opm);
+        ++pos;
+        s.cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, s.jm = 0;
+        s.ck = (v == a1) ? 1 : (v == a3) ? 3 : -1, s.jk = 0;
+    }
+    return v;
+}
+
 // Apply BinaryBayesGridCell::Update for the run that starts at key position i
 // (in key order = the reference's order) to the value v; counts hits/misses.
 // The run is read 64 keys at a time from the hit/end words, not key by key,
@@ -327,10 +394,7 @@ struct BayesK {
 __device__ double walk_run(long long i, double v, uint32_t& nh, uint32_t& nm, const RunBits& rb,
                            const BayesChains* __restrict__ ch, const BayesK& K)
 {
-    const double a0 = ch->a[0], a1 = ch->a[1], a2 = ch->a[2], a3 = ch->a[3];
-    // the miss chain and the hit chain v is on (-1: none) and the index in it
-    int cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, ck = (v == a1) ? 1 : (v == a3) ? 3 : -1;
-    int jm = 0, jk = 0;
+    ChainState cs(v, ch);
     for (long long p = i;;) {
         const int sh = (int)(p & 63);
         const bool id_miss = K.miss_fixed && v == kPMin, id_hit = K.hit_fixed && v == kPMax;
@@ -352,51 +416,10 @@ __device__ double walk_run(long long i, double v, uint32_t& nh, uint32_t& nm, co
         const unsigned long long em = rb.endw[p >> 6] >> sh;
         const int cnt = em ? __ffsll((long long)em) : 64 - sh;  // keys of the run in this word
         const unsigned long long inm = (cnt == 64) ? ~0ull : ((1ull << cnt) - 1ull);
-        const unsigned long long h = hm & inm, m = inm & ~hm;
+        const unsigned long long h = hm & inm;
         nh += __popcll(h);
         nm += cnt - __popcll(h);
-        int pos = 0;
-        while (pos < cnt) {
-            if (K.miss_fixed && v == kPMin) {        // misses are identities: next hit
-                const unsigned long long rest = h >> pos;
-                if (!rest) break;
-                pos += __ffsll((long long)rest) - 1;
-            } else if (K.hit_fixed && v == kPMax) {  // hits are identities: next miss
-                const unsigned long long rest = m >> pos;
-                if (!rest) break;
-                pos += __ffsll((long long)rest) - 1;
-            }
-            const bool is_hit = (h >> pos) & 1ull;
-            const int c = is_hit ? ck : cm;
-            if (c >= 0) {
-                // k same-type updates from pos: jump along the chain
-                const unsigned long long other = (is_hit ? m : h) >> pos;
-                const int k = other ? __ffsll((long long)other) - 1 : cnt - pos;
-                const int last = ch->len[c] - 1;
-                const int j0 = is_hit ? jk : jm;
-                int j = j0 + k, used = k;
-                if (j > last) {
-                    if (!ch->fixed[c]) used = last - j0;  // table ends: the rest normally
-                    j = last;
-                }
-                v = ch->t[c][j];
-                pos += used;
-                if (is_hit) {
-                    jk = j;
-                    if (used < k) ck = -1;
-                    cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, jm = 0;
-                } else {
-                    jm = j;
-                    if (used < k) cm = -1;
-                    ck = (v == a1) ? 1 : (v == a3) ? 3 : -1, jk = 0;
-                }
-                continue;
-            }
-            v = bayes_update_k(v, is_hit ? K.cph : K.cpm, is_hit ? K.oph : K.opm);
-            ++pos;
-            cm = (v == a0) ? 0 : (v == a2) ? 2 : -1, jm = 0;
-            ck = (v == a1) ? 1 : (v == a3) ? 3 : -1, jk = 0;
-        }
+        v = apply_word(v, cs, h, inm & ~hm, cnt, ch, K);
         if (em) return v;
         p += cnt;
     }
@@ -409,10 +432,13 @@ __device__ __forceinline__ bool run_start(const unsigned long long* __restrict__
 
 // the first Update of a cell allocates its patch (GridCellAt, :817-819);
 // every thread of the patch stores the same byte
+// (the flag is sticky: a thread that reads it set stores nothing -- thousands
+// of cells of a patch would otherwise store to one byte, serialised at L2)
 __device__ __forceinline__ void mark_patch(const RayMap& mp, unsigned long long local)
 {
     const unsigned lx = (unsigned)(local % (unsigned)mp.w), ly = (unsigned)(local / (unsigned)mp.w);
-    mp.palloc[(ly / (unsigned)mp.ps) * (unsigned)mp.npx + lx / (unsigned)mp.ps] = 1;
+    uint8_t* f = mp.palloc + (ly / (unsigned)mp.ps) * (unsigned)mp.npx + lx / (unsigned)mp.ps;
+    if (!*f) *f = 1;
 }
 
 // k_apply: one thread per run of equal cells (the thread at the run's first
@@ -461,19 +487,102 @@ struct WindowJob {
     const unsigned long long* tbl;
 };
 
-__device__ void recompute_cell(const WindowJob& J, unsigned cell, const BayesChains* __restrict__ ch,
-                               const BayesK& K)
+// Cells with a long run in some slot (the cells around the window's sensors,
+// crossed by many rays of every scan): one thread would walk each slot's run
+// with a chain of dependent loads per word; they are queued instead
+// (long_cells) and recomputed by k_apply_long, one wave per cell.
+struct LongList {
+    unsigned* count;     // [0] cells queued, [1] k_apply_long workgroups done (zero between steps)
+    unsigned* cells;
+};
+
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long x, int l)
 {
+    const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)x, l);
+    const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// walk_run by a whole wave: the lanes load 64 words of the run at once and
+// every lane then follows the same (uniform) walk over them from registers
+__device__ double walk_run_wave(long long i, double v, uint32_t& nh, uint32_t& nm, const RunBits& rb,
+                                const BayesChains* __restrict__ ch, const BayesK& K)
+{
+    const int lane = (int)__lane_id();
+    ChainState cs(v, ch);
+    long long w0 = -1;
+    unsigned long long hwl = 0, ewl = 0;
+    for (long long p = i;;) {
+        const long long w = p >> 6;
+        if (w0 < 0 || w - w0 >= 64) {
+            w0 = w;
+            const long long wl = w0 + lane;
+            hwl = (wl < rb.nw) ? rb.hitw[wl] : 0ull;
+            ewl = (wl < rb.nw) ? rb.endw[wl] : ~0ull;
+        }
+        const int sh = (int)(p & 63);
+        const unsigned long long hm = readlane64(hwl, (int)(w - w0)) >> sh;
+        const unsigned long long em = readlane64(ewl, (int)(w - w0)) >> sh;
+        const int cnt = em ? __ffsll((long long)em) : 64 - sh;
+        const unsigned long long inm = (cnt == 64) ? ~0ull : ((1ull << cnt) - 1ull);
+        const unsigned long long h = hm & inm;
+        nh += __popcll(h);
+        nm += cnt - __popcll(h);
+        v = apply_word(v, cs, h, inm & ~hm, cnt, ch, K);
+        if (em) return v;
+        p += cnt;
+    }
+}
+
+__device__ void recompute_cell(const WindowJob& J, unsigned cell, const BayesChains* __restrict__ ch,
+                               const BayesK& K, LongList ll)
+{
+    // the cell's run in every window slot, oldest first: one round of loads;
+    // short runs are in the index itself, long ones are walked in their list
     const unsigned long long* e = J.tbl + (size_t)cell * kSlots;
+    unsigned long long x[kSlots];
+#pragma unroll
+    for (int q = 0; q < kSlots; ++q) x[q] = (q < J.nwin) ? e[J.order[q]] : 0ull;
+    bool lng = false;
+#pragma unroll
+    for (int q = 0; q < kSlots; ++q)
+        if (q < J.nwin && (unsigned)(x[q] >> 32) == J.st.s[J.order[q]] && ((unsigned)x[q] & kLongRun)) lng = true;
+    if (lng) {
+        ll.cells[atomicAdd(ll.count, 1u)] = cell;
+        return;
+    }
+    // the slots' runs, oldest first, concatenated into 64-update words; each
+    // word is applied with the chain state carried across slots (a cell that
+    // saw only misses takes one chain look-up for the whole window)
     double v = 0.0;   // Reset (:290): Unknown
+    ChainState cs(v, ch);
     uint32_t nh = 0, nm = 0;
     bool any = false;
-    for (int q = 0; q < J.nwin; ++q) {
+    unsigned long long wb = 0;
+    int wn = 0;
+#pragma unroll
+    for (int q = 0; q < kSlots; ++q) {
+        if (q >= J.nwin) continue;
         const int s = J.order[q];
-        const unsigned long long x = e[s];
-        if ((unsigned)(x >> 32) != J.st.s[s]) continue;
-        v = walk_run((long long)(unsigned)x, v, nh, nm, J.slot[s].rb, ch, K);
+        if ((unsigned)(x[q] >> 32) != J.st.s[s]) continue;
         any = true;
+        const unsigned en = (unsigned)x[q];
+        const int len = (int)(en >> 26);
+        const unsigned long long bits = en & ((1u << 26) - 1u);
+        const int hits = __popcll(bits);
+        nh += (uint32_t)hits;
+        nm += (uint32_t)(len - hits);
+        if (wn + len > 64) {
+            const unsigned long long mk = (wn == 64) ? ~0ull : ((1ull << wn) - 1ull);
+            v = apply_word(v, cs, wb, mk & ~wb, wn, ch, K);
+            wb = 0, wn = 0;
+        }
+        wb |= bits << wn;
+        wn += len;
+    }
+    if (wn > 0) {
+        const unsigned long long mk = (wn == 64) ? ~0ull : ((1ull << wn) - 1ull);
+        v = apply_word(v, cs, wb, mk & ~wb, wn, ch, K);
     }
     if (any) mark_patch(J.latest, cell);
     J.latest.cells[cell] = v;
@@ -483,7 +592,7 @@ __device__ void recompute_cell(const WindowJob& J, unsigned cell, const BayesCha
 
 __global__ __launch_bounds__(256) void k_apply_window(const WindowJob* __restrict__ jp,
                                                       const BayesChains* __restrict__ ch, double p_hit,
-                                                      double p_miss)
+                                                      double p_miss, LongList ll)
 {
     const WindowJob& J = *jp;
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -491,7 +600,7 @@ __global__ __launch_bounds__(256) void k_apply_window(const WindowJob* __restric
     const SlotView& E = J.slot[J.eslot];
     if (i < J.nE) {                                   // cells of E
         if (!run_start(E.rb.endw, i)) return;
-        recompute_cell(J, E.keys[i] >> kTagShift, ch, K);
+        recompute_cell(J, E.keys[i] >> kTagShift, ch, K, ll);
     } else if (i < J.nE + J.nloc) {                   // E into the local map
         if (!run_start(E.rb.endw, i)) return;
         const unsigned long long local = (E.keys[i] >> kTagShift) - J.local.base;
@@ -507,7 +616,58 @@ __global__ __launch_bounds__(256) void k_apply_window(const WindowJob* __restric
         const unsigned cell = J.lkeys[p] >> kTagShift;
         const unsigned long long x = J.tbl[(size_t)cell * kSlots + J.eslot];
         if ((unsigned)(x >> 32) == J.st.s[J.eslot]) return;   // E's thread recomputes it
-        recompute_cell(J, cell, ch, K);
+        recompute_cell(J, cell, ch, K, ll);
+    }
+}
+
+// The queued cells, one wave per cell (every lane computes the same value).
+__global__ __launch_bounds__(256) void k_apply_long(const WindowJob* __restrict__ jp,
+                                                    const BayesChains* __restrict__ ch, double p_hit,
+                                                    double p_miss, LongList ll)
+{
+    const WindowJob& J = *jp;
+    const BayesK K(p_hit, p_miss);
+    const int lane = (int)__lane_id();
+    const unsigned nq = ll.count[0];
+    const unsigned waves = gridDim.x * (blockDim.x / 64);
+    for (unsigned k = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < nq; k += waves) {
+        const unsigned cell = ll.cells[k];
+        const unsigned long long* e = J.tbl + (size_t)cell * kSlots;
+        const unsigned long long xl = (lane < J.nwin) ? e[J.order[lane]] : 0ull;
+        double v = 0.0;
+        ChainState cs(v, ch);
+        uint32_t nh = 0, nm = 0;
+        bool any = false;
+        for (int q = 0; q < J.nwin; ++q) {
+            const int s = J.order[q];
+            const unsigned long long x = readlane64(xl, q);
+            if ((unsigned)(x >> 32) != J.st.s[s]) continue;
+            any = true;
+            const unsigned en = (unsigned)x;
+            if (en & kLongRun) {
+                v = walk_run_wave((long long)(en & ~kLongRun), v, nh, nm, J.slot[s].rb, ch, K);
+                cs = ChainState(v, ch);
+            } else {
+                const int len = (int)(en >> 26);
+                const unsigned long long bits = en & ((1u << 26) - 1u);
+                const int hits = __popcll(bits);
+                nh += (uint32_t)hits;
+                nm += (uint32_t)(len - hits);
+                v = apply_word(v, cs, bits, ((1ull << len) - 1ull) & ~bits, len, ch, K);
+            }
+        }
+        if (lane == 0) {
+            if (any) mark_patch(J.latest, cell);
+            J.latest.cells[cell] = v;
+            J.latest.hit[cell] = nh;
+            J.latest.miss[cell] = nm;
+        }
+    }
+    // the last workgroup clears the queue for the next step
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(ll.count + 1, 1u) == gridDim.x - 1) {
+        ll.count[0] = 0;
+        ll.count[1] = 0;
     }
 }
 
@@ -1030,8 +1190,8 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
         // key + 32 B per run of equal cells (cell, hit and miss counters read
         // and written once; the run count is added after the last pass)
         int tok = ctx->timing_begin(K_RAY_EMIT, 4.0 * (double)keys);
-        hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, st, d_rays, d_offs,
-                           d_rmap, (int)nr, keys, d_maps, d_keys, d_bad, ksh);
+        hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st, d_rays, d_offs, d_rmap,
+                           (int)nr, d_maps, d_keys, d_bad, ksh);
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
         int cell_bits = 1;
@@ -1054,7 +1214,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
         hipLaunchKernelGGL(k_runsummary, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, d_hitw, d_endw, nw,
                            d_hit2, d_miss2, d_end2);
         hipLaunchKernelGGL(k_apply, dim3(blocks), dim3(256), 0, st, d_sorted, keys,
-                           RunBits{d_hitw, d_endw, d_hit2, d_miss2, d_end2}, d_maps, nmaps, d_chains, bp->prob_hit,
+                           RunBits{d_hitw, d_endw, d_hit2, d_miss2, d_end2, nw}, d_maps, nmaps, d_chains, bp->prob_hit,
                            bp->prob_miss, ksh);
         ctx->timing_end(tok);
         if (tok >= 0)
@@ -1116,7 +1276,8 @@ struct KeyBuf {
     {
         if (base) hipFree(base);
     }
-    RunBits bits() const { return RunBits{ hitw, endw, hit2, miss2, end2 }; }
+    long long nw = 0;
+    RunBits bits() const { return RunBits{ hitw, endw, hit2, miss2, end2, nw }; }
 };
 typedef std::shared_ptr<KeyBuf> KeyBufPtr;
 
@@ -1128,6 +1289,7 @@ KeyBufPtr keybuf_new(long long cap)
     if (hipMalloc(&b->base, kb + 8 * (size_t)(2 * nw + 3 * nw2)) != hipSuccess)
         throw Error(LGS_ERR_OOM, "hipMalloc failed for latest-map key lists");
     b->cap = cap;
+    b->nw = nw;
     b->keys = (unsigned*)b->base;
     b->hitw = (unsigned long long*)((char*)b->base + kb);
     b->endw = b->hitw + nw;
@@ -1157,6 +1319,8 @@ struct LatestCache {
     LatestSlot slot[kSlots];
     unsigned long long* d_tbl = nullptr;
     size_t tbl_cells = 0;
+    unsigned* d_long = nullptr;   // k_apply_long queue: [0] count, [1] done, then cells
+    long long long_cap = 0;
     std::vector<KeyBufPtr> pool, retired;
     int* h_bad = nullptr;         // mapped pinned word: a ray left the map (set by k_emit, never cleared)
     int* d_bad = nullptr;
@@ -1171,6 +1335,7 @@ struct LatestCache {
         pool.clear();
         retired.clear();
         if (d_tbl) hipFree(d_tbl);
+        if (d_long) hipFree(d_long);
         if (h_bad) hipHostFree(h_bad);
         if (pin) hipHostFree(pin);
     }
@@ -1374,8 +1539,8 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
     unsigned* d_tmp = (unsigned*)ctx->ensure(S_RAY3, sizeof(unsigned) * (size_t)std::max(1LL, keys));
     if (nr > 0) {
         int tok = ctx->timing_begin(K_RAY_EMIT, 4.0 * (double)keys);
-        hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, st, (const int4*)(d_stage + o_rays),
-                           (const long long*)(d_stage + o_offs), (const int*)(d_stage + o_rmap), (int)nr, keys,
+        hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st, (const int4*)(d_stage + o_rays),
+                           (const long long*)(d_stage + o_offs), (const int*)(d_stage + o_rmap), (int)nr,
                            (const RayMap*)(d_stage + o_maps), d_keys, C.d_bad, kTagShift);
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
@@ -1392,10 +1557,24 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
                            nw, buf->hit2, buf->miss2, buf->end2);
     }
     const long long nthreads = keys + nL;
-    if (nthreads > 0)
+    if (nE + nL > C.long_cap) {
+        if (C.d_long) LGS_HIP_CHECK(hipFree(C.d_long));
+        C.d_long = nullptr;
+        C.long_cap = 0;
+        const long long cap = (nE + nL) * 2 + 4096;
+        if (hipMalloc(&C.d_long, sizeof(unsigned) * (size_t)(cap + 2)) != hipSuccess)
+            throw Error(LGS_ERR_OOM, "hipMalloc failed for the long-run queue");
+        LGS_HIP_CHECK(hipMemsetAsync(C.d_long, 0, 2 * sizeof(unsigned), st));
+        C.long_cap = cap;
+    }
+    const LongList ll{ C.d_long, C.d_long + 2 };
+    if (nthreads > 0) {
         hipLaunchKernelGGL(k_apply_window, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, st,
                            (const WindowJob*)(d_stage + o_job), (const BayesChains*)d_stage, bp->prob_hit,
-                           bp->prob_miss);
+                           bp->prob_miss, ll);
+        hipLaunchKernelGGL(k_apply_long, dim3(512), dim3(256), 0, st, (const WindowJob*)(d_stage + o_job),
+                           (const BayesChains*)d_stage, bp->prob_hit, bp->prob_miss, ll);
+    }
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
     record_writer(C, st, latest, local);

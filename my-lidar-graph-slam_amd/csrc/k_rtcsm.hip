@@ -127,9 +127,6 @@ struct Blk {
 };
 __device__ __forceinline__ Blk xcd_block()
 {
-#ifdef LGS_NO_XCD
-    return { (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z };
-#endif
     const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
     const int nwg = gx * gy * gz;
     const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
@@ -300,17 +297,8 @@ __device__ __forceinline__ bool strip_read(const double* __restrict__ cmap, int 
 // cells >= 1 mm that is < 1e-11 cells, far inside the 1e-9-cell guard, so
 // every projection whose glibc floor could differ is still guarded and
 // re-checked on the host.
-#ifndef LGS_PROJ_ROWS
-#define LGS_PROJ_ROWS 16
-#endif
-#ifndef LGS_PROJ_INV
-#define LGS_PROJ_INV 1
-#endif
-constexpr int kProjRows = LGS_PROJ_ROWS;
-#ifndef LGS_PROJ_ROWS_LONE
-#define LGS_PROJ_ROWS_LONE 4   // measured (lone config-2 scan): 16: 16.1 us, 8: 12.3, 4: 10.7, 2: 10.4
-#endif
-constexpr int kProjRowsLone = LGS_PROJ_ROWS_LONE;
+constexpr int kProjRows = 16;
+constexpr int kProjRowsLone = 4;   // measured (lone config-2 scan): 16: 16.1 us, 8: 12.3, 4: 10.7, 2: 10.4
 template <int ROWS>
 __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, double guard_eps, int inject)
 {
@@ -386,16 +374,11 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     const double s = s_st[kr] * ca + s_ct[kr] * sa;
     const double hx = pl.sx + r * c;
     const double hy = pl.sy + r * s;
-#if LGS_PROJ_INV
     // x / res as x * (1 / res): differs from the quotient by a few ulps, far
     // inside the guard (eps + |q| 1e-13), so every cell whose floor could
     // differ from the reference's division is still re-checked on the host
     const double qx = (hx - pl.min_x) * inv_res;
     const double qy = (hy - pl.min_y) * inv_res;
-#else
-    const double qx = (hx - pl.min_x) / pl.res;
-    const double qy = (hy - pl.min_y) / pl.res;
-#endif
     int ix = (int)floor(qx);
     int iy = (int)floor(qy);
     const bool guarded = near_boundary(qx, guard_eps) || near_boundary(qy, guard_eps);
@@ -491,7 +474,6 @@ __device__ __forceinline__ void stage_lds(T* dst, const T* __restrict__ src, int
     }
 }
 
-__device__ __forceinline__ double dmax2(double a, double b) { return (a < b) ? b : a; }
 
 constexpr int kSB = 4;   // superblock = kSB x kSB coarse blocks
 constexpr int kSeedCands = 4;   // k_seed_super workgroups (candidate superblocks)
@@ -655,7 +637,6 @@ __device__ __forceinline__ double seq_sum4(int n, Fetch fetch, Addr addr)
 //               doubles of one plane;
 //   PLANES = 0: the coarse map as is (stride lr between lanes).
 // --------------------------------------------------------------------------
-template <int PLANES>
 __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __restrict__ zero)
 {
     const MatchItem& it = items[blockIdx.z];
@@ -683,19 +664,9 @@ __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __re
     const int2* __restrict__ id = idx + o;
     const int* __restrict__ cb = cbase + o;
 
-    double sum = 0.0;
-    if (PLANES) {
-        const double* __restrict__ lane_base = cmap + (jy * pl.Wqp + jx);
-        sum = seq_sum<int>(pl.Nv, [&](int v) { return cb[v]; }, [&](const int& c) { return lane_base + c; });
-    } else {
-        const int xc = -pl.win_x + jx * lr, yc = -pl.win_y + jy * lr;
-        sum = seq_sum<int2>(pl.Nv, [&](int v) { return id[v]; }, [&](const int2& q) {
-            const int x = q.x + xc, y = q.y + yc;
-            const bool inb = ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
-            const unsigned off = (unsigned)(y * W + x);
-            return inb ? cmap + off : zero;
-        });
-    }
+    const double* __restrict__ lane_base = cmap + (jy * pl.Wqp + jx);
+    const double sum =
+        seq_sum<int>(pl.Nv, [&](int v) { return cb[v]; }, [&](const int& c) { return lane_base + c; });
     // unsafe: some coarse read left of / below the map while the block's fine
     // reads can land inside (x, y >= -(lr-1)); rare, so a separate pass
     bool unsafe = false;
@@ -752,20 +723,12 @@ __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __re
 //  2. horizontal 4-max of the fp16 values from LDS, 8 consecutive superblocks
 //     of one sub-phase row per thread, one 16-byte store (Wq4 is a multiple of
 //     8, so sub-phase rows are 16-byte aligned).
-#ifndef LGS_SPY
-#define LGS_SPY 16
-#endif
-#ifndef LGS_SPX
-#define LGS_SPX 256
-#endif
-constexpr int kSPX = LGS_SPX, kSPY = LGS_SPY;   // kSPX = 4 sub-phases x 64 (8 stores of 8)
+constexpr int kSPX = 256, kSPY = 16;   // kSPX = 4 sub-phases x 64 (8 stores of 8)
 constexpr int kSPThreads = (kSPX + 3 + 63) / 64 * 64;   // >= kSPX + kSB - 1 column loaders
 
 // SPX: tile width (kSPX for a batch's sets; a lone set takes narrower tiles,
 // more workgroups for its few hundred tiles: latency-bound, like the precompute)
-#ifndef LGS_SPX_LONE
-#define LGS_SPX_LONE 128   // measured (lone config-2 set): 256: 12.9 us, 128: 11.3, 64: 11.2
-#endif
+constexpr int kSPXLone = 128;   // measured (lone config-2 set): 256: 12.9 us, 128: 11.3, 64: 11.2
 template <int SPX>
 __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const PlaneJob* __restrict__ jobs, int nplanes)
 {
@@ -968,190 +931,6 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
     LGS_PROBE_PRINT("super(stage, sum w0, barrier, tail)");
 }
 
-// k_super_quad: k_super's bounds with 8-byte gathers.  A beam's superblocks
-// are nsby rows of nsbx consecutive floats (sub-phase layout), so a lane
-// fetches TWO neighbouring superblocks (a, a + 1) of one row with one 8-byte
-// load: 15 lanes cover a beam's 5 x 5 superblocks and one wave instruction
-// serves 4 beams (k_super<1>: 2 beams).  Used when nsby * ceil(nsbx / 2) <= 16.
-// Same outputs as k_super (sbound, one part per angle); loads are 4-byte
-// aligned, which gfx950 global loads accept.  The odd tail superblock's pair
-// reads one float past its row: inside the padded planes (the allocation has
-// >= 256 B of slack) and never added.
-typedef SuperT f2a4 __attribute__((ext_vector_type(2), aligned(sizeof(SuperT))));
-constexpr int kQuadPipe = 8;
-__global__ __launch_bounds__(64 * kSupWaves) void k_super_quad(Items items, const double* __restrict__ zero)
-{
-    const Blk wg = xcd_block();
-    const MatchItem& it = items[wg.z];
-    const RtcsmPlan& pl = it.pl;
-    if (wg.y >= pl.T) return;   // past this item's angles (uniform)
-    const SuperT* __restrict__ sp = it.super;
-    const f2a4* __restrict__ z2 = (const f2a4*)zero;
-    extern __shared__ int srow[];   // [Nv]
-    __shared__ double red[kSupWaves][32];
-    const int t = wg.y;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int nsbx = pl.nsbx, nsb2 = nsbx * pl.nsby;
-    const int np = (nsbx + 1) >> 1;
-    const int q = lane >> 4, idx = lane & 15;
-    const bool act = idx < pl.nsby * np;
-    const int b = act ? idx / np : 0, a0 = act ? 2 * (idx % np) : 0;
-    const SuperT* __restrict__ lb = sp + (b * pl.Wq4 + a0);
-    const int* __restrict__ cbrow = it.cbase + pl.sb_off + (size_t)t * pl.Nv;
-    stage_lds(srow, cbrow, pl.Nv);
-    __syncthreads();
-    const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
-    const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
-    const int* row = srow + lo;
-    const int n4 = (cnt + 3) >> 2;   // beam slot q takes beams 4 i + q
-    double s0 = 0.0, s1 = 0.0;
-    for (int i0 = 0; i0 < n4; i0 += kQuadPipe) {
-        f2a4 x[kQuadPipe];
-#pragma unroll
-        for (int j = 0; j < kQuadPipe; ++j) {
-            const int v = 4 * (i0 + j) + q;
-            const int c = (v < cnt) ? row[min(v, cnt - 1)] : 0;
-            x[j] = *((act && v < cnt) ? (const f2a4*)(lb + c) : z2);
-        }
-#pragma unroll
-        for (int j = 0; j < kQuadPipe; ++j) {
-            s0 += (double)x[j].x;
-            s1 += (double)x[j].y;
-        }
-    }
-    // the 4 beam slots, then the waves
-    s0 += __shfl_xor(s0, 16, 64);
-    s1 += __shfl_xor(s1, 16, 64);
-    s0 += __shfl_xor(s0, 32, 64);
-    s1 += __shfl_xor(s1, 32, 64);
-    if (q == 0) {
-        red[w][2 * idx] = s0;
-        red[w][2 * idx + 1] = s1;
-    }
-    __syncthreads();
-    if (w != 0) return;
-    const int sbi = lane;
-    const bool own = sbi < nsb2;
-    double tot = 0.0;
-    if (own) {
-        const int a = sbi % nsbx, bb = sbi / nsbx;
-        const int k = 2 * (bb * np + (a >> 1)) + (a & 1);
-        for (int j = 0; j < kSupWaves; ++j) tot += red[j][k];
-    }
-    const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult;
-    if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
-    const bool seedable = own;   // k_seed_super skips unsafe members
-    double bv = seedable ? bound : -INFINITY;
-    long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
-    for (int off = 32; off > 0; off >>= 1) {
-        const double ov = __shfl_xor(bv, off, 64);
-        const long long ok = __shfl_xor(bk, off, 64);
-        if (better(ov, ok, bv, bk)) {
-            bv = ov;
-            bk = ok;
-        }
-    }
-    if (lane == 0) {
-        it.part_c[t] = bv;
-        it.part_k[t] = bk;
-    }
-}
-
-// k_super_hex: k_super_quad with 8-byte gathers of FOUR fp16 superblocks
-// (a .. a + 3) of one row: a beam's 5 x 5 superblocks take 10 lanes, so one
-// wave instruction serves 6 beams (lanes 60..63 idle) instead of 4.  Used when
-// nsby * ceil(nsbx / 4) <= 10.  The beam slots are summed with shuffles
-// (slot q holds lanes 10 q .. 10 q + 9).  Tail elements past the row are read
-// from the padded planes (+ slack) and never added.
-typedef SuperT f4a2 __attribute__((ext_vector_type(4), aligned(sizeof(SuperT))));
-constexpr int kHexPipe = 16;   // gathers in flight per lane (4: 0.463, 8: 0.458, 16: 0.449 ms per 64 scans)
-__global__ __launch_bounds__(64 * kSupWaves) void k_super_hex(Items items, const double* __restrict__ zero)
-{
-    const Blk wg = xcd_block();
-    const MatchItem& it = items[wg.z];
-    const RtcsmPlan& pl = it.pl;
-    if (wg.y >= pl.T) return;   // past this item's angles (uniform)
-    const SuperT* __restrict__ sp = it.super;
-    const f4a2* __restrict__ z4 = (const f4a2*)zero;
-    extern __shared__ int srow[];   // [Nv]
-    __shared__ double red[kSupWaves][40];
-    const int t = wg.y;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int nsbx = pl.nsbx, nsb2 = nsbx * pl.nsby;
-    const int np = (nsbx + 3) >> 2;
-    const int q = lane / 10, idx = lane - 10 * q;
-    const bool act = q < 6 && idx < pl.nsby * np;
-    const int b = act ? idx / np : 0, a0 = act ? 4 * (idx % np) : 0;
-    const SuperT* __restrict__ lb = sp + (b * pl.Wq4 + a0);
-    const int* __restrict__ cbrow = it.cbase + pl.sb_off + (size_t)t * pl.Nv;
-    stage_lds(srow, cbrow, pl.Nv);
-    __syncthreads();
-    const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
-    const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
-    const int* row = srow + lo;
-    const int n6 = (cnt + 5) / 6;   // beam slot q takes beams 6 i + q
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    for (int i0 = 0; i0 < n6; i0 += kHexPipe) {
-        f4a2 x[kHexPipe];
-#pragma unroll
-        for (int j = 0; j < kHexPipe; ++j) {
-            const int v = 6 * (i0 + j) + q;
-            const int c = (v < cnt) ? row[min(v, cnt - 1)] : 0;
-            x[j] = *((act && v < cnt) ? (const f4a2*)(lb + c) : z4);
-        }
-#pragma unroll
-        for (int j = 0; j < kHexPipe; ++j) {
-            s0 += (double)x[j].x;
-            s1 += (double)x[j].y;
-            s2 += (double)x[j].z;
-            s3 += (double)x[j].w;
-        }
-    }
-    // the 6 beam slots: lanes idx, idx + 10, ..., idx + 50 into slot 0
-    double r0 = s0, r1 = s1, r2 = s2, r3 = s3;
-#pragma unroll
-    for (int k = 1; k < 6; ++k) {
-        const int src = min(idx + 10 * k, 63);
-        r0 += __shfl(s0, src, 64);
-        r1 += __shfl(s1, src, 64);
-        r2 += __shfl(s2, src, 64);
-        r3 += __shfl(s3, src, 64);
-    }
-    if (q == 0) {
-        red[w][4 * idx] = r0;
-        red[w][4 * idx + 1] = r1;
-        red[w][4 * idx + 2] = r2;
-        red[w][4 * idx + 3] = r3;
-    }
-    __syncthreads();
-    if (w != 0) return;
-    const int sbi = lane;
-    const bool own = sbi < nsb2;
-    double tot = 0.0;
-    if (own) {
-        const int a = sbi % nsbx, bb = sbi / nsbx;
-        const int k = 4 * (bb * np + (a >> 2)) + (a & 3);
-        for (int j = 0; j < kSupWaves; ++j) tot += red[j][k];
-    }
-    const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult;
-    if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
-    const bool seedable = own;   // k_seed_super skips unsafe members
-    double bv = seedable ? bound : -INFINITY;
-    long long bk = seedable ? (long long)t * nsb2 + sbi : LLONG_MAX;
-    for (int off = 32; off > 0; off >>= 1) {
-        const double ov = __shfl_xor(bv, off, 64);
-        const long long ok = __shfl_xor(bk, off, 64);
-        if (better(ov, ok, bv, bk)) {
-            bv = ov;
-            bk = ok;
-        }
-    }
-    if (lane == 0) {
-        it.part_c[t] = bv;
-        it.part_k[t] = bk;
-    }
-}
-
 // k_super_oct (octet layout, nsbx, nsby <= 5): lane = (beam slot, window
 // column a); one aligned 16-byte load per (beam, column) brings the column's 8
 // sub-phase rows 4q .. 4q + 7, of which rows k .. k + 4 (k = the window's
@@ -1279,10 +1058,9 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
 // keep kRing - 1 gathers in flight, and each slot is refilled once read.
 constexpr int kRowWaves = 1;   // waves per workgroup
 constexpr int kRowSplit = 4;   // workgroups per (angle, patch row): kept superblocks e = z, z + 4, ...
-#ifndef LGS_RING
-#define LGS_RING 16   // measured (lone config-2 scan): 12: 30.0 us, 14: 30.6, 16: 26.8, 18: 31.5, 20: 33.0, 24: 34.2, 32: 32.4
-#endif
-constexpr int kRing = LGS_RING;      // 1 KiB glds slots per wave
+// 1 KiB glds slots per wave; measured (lone config-2 scan): 12: 30.0 us, 14:
+// 30.6, 16: 26.8, 18: 31.5, 20: 33.0, 24: 34.2, 32: 32.4
+constexpr int kRing = 16;
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14)
@@ -1857,13 +1635,7 @@ constexpr int kSeedRegParts = 4;   // parts held in registers per thread
 // gathers per batch (one memory round trip each) in the member and fine
 // stages: a 1081-beam scan needs 17 per thread in the member stage and 34 in
 // the fine stage (25 poses padded to 32 lanes)
-#ifndef LGS_SEED_B1
-#define LGS_SEED_B1 24
-#endif
-#ifndef LGS_SEED_B2
-#define LGS_SEED_B2 36
-#endif
-constexpr int kSeedB1 = LGS_SEED_B1, kSeedB2 = LGS_SEED_B2;
+constexpr int kSeedB1 = 24, kSeedB2 = 36;
 
 __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* __restrict__ zero)
 {
@@ -2203,9 +1975,7 @@ __device__ __forceinline__ int seg_of(const int* pref, int nseg, int b)
 // memory pipeline are what a block evaluation waits on); fval/fpos are
 // indexed by item and k_replay combines a block's rows.  LR == 0: one wave
 // per block, indexed by dense position.
-#ifndef LGS_FINE_DEPTH
-#define LGS_FINE_DEPTH 6   // measured (lone config-2 scan): 4: 33.7 us, 5: 34.2, 6: 23.8, 7: 24.0, 8: 34.1
-#endif
+constexpr int kFineDepth = 6;   // measured (lone config-2 scan): 4: 33.7 us, 5: 34.2, 6: 23.8, 7: 24.0, 8: 34.1
 template <int LR>
 __global__ __launch_bounds__(64) void k_fine(Items items, const double* __restrict__ zero, unsigned eval_smem)
 {
@@ -2237,7 +2007,7 @@ __global__ __launch_bounds__(64) void k_fine(Items items, const double* __restri
         double f;
         int pos;
         if constexpr (LR > 0)
-            eval_block_t<LR, LGS_FINE_DEPTH>(pl, grid, idx, zero, k, smem, sv, sk, f, pos, it % R);
+            eval_block_t<LR, kFineDepth>(pl, grid, idx, zero, k, smem, sv, sk, f, pos, it % R);
         else
             eval_block(pl, grid, idx, zero, k, (int2*)smem, f, pos);
         if (threadIdx.x == 0) {
@@ -2655,12 +2425,9 @@ void set_plane_layout(RtcsmPlan& pl)
     pl.pstride4 = 16 * pl.sub4;
     LGS_REQUIRE((long long)pl.low_res * pl.low_res * pl.pstride4 < (1LL << 31),
                 "coarse map too large for 32-bit plane offsets");
-#ifndef LGS_SUPER_OCT
-#define LGS_SUPER_OCT 1
-#endif
     // octet layout: one 16-byte unit holds 5 superblock rows of a beam's
     // window (nsby <= 5), one unit + the high half of the next holds 9
-    pl.oct = LGS_SUPER_OCT && pl.nsbx <= 9 && pl.nsby <= 9 && pl.nsbx * pl.nsby <= 64;
+    pl.oct = pl.nsbx <= 9 && pl.nsby <= 9 && pl.nsbx * pl.nsby <= 64;
     pl.Qo = (pl.Hq4 + 3) / 4 + 1;
     pl.subO = (long long)pl.Qo * pl.Wq4;
     pl.pstrideO = 16 * pl.subO;
@@ -2745,11 +2512,8 @@ struct BatchShape {
     int Tmax = 0, NvMax = 0, nsegMax = 0, nparts_max = 0;
     int P = 0, nsb2 = 0, chunks = 0, low_res = 0, cb = 0;
     bool pair = false;
-    bool quad = false;      // k_super_quad (nsby * ceil(nsbx / 2) <= 16; chunks == 1)
-    bool hex = false;       // k_super_hex (fp16 planes, nsby * ceil(nsbx / 4) <= 10; chunks == 1)
     bool oct = false;       // k_super_oct (octet layout of the plan, nsbx, nsby <= 9; chunks == 1)
     int nsby = 0;
-    bool planes = false;    // coarse map in padded phase planes
     bool pruned = false;    // superblock pruning
     bool lr5 = false;       // transposed LR = 5 evaluators
     bool fine_lanes = false;   // k_compact + k_fine_lanes (lr * lr <= 64)
@@ -2768,7 +2532,7 @@ inline int item_nparts(const BatchShape& B, const RtcsmPlan& pl, bool pruned)
 inline bool uses_super(const lgs_ctx* ctx, int nv_max, int nsb2, bool dense)
 {
     // k_coarse_rows: one ballot over an angle's superblocks, Nv <= 2048
-    return !(dense || ctx->force_dense) && ctx->coarse_planes && ctx->super_prune && nv_max <= kSeedMaxNv &&
+    return !(dense || ctx->force_dense) && ctx->super_prune && nv_max <= kSeedMaxNv &&
            nsb2 <= 64;
 }
 
@@ -2848,7 +2612,7 @@ inline size_t plane_bytes(const RtcsmPlan& pl)
 inline size_t super_bytes(const RtcsmPlan& pl)
 {
     if (pl.oct) return align256(16 * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstrideO);
-    return align256(sizeof(SuperT) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4 + 64);   // + slack: k_super_quad reads one float past a row
+    return align256(sizeof(SuperT) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
 }
 double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_super)
 {
@@ -2888,8 +2652,7 @@ struct PlaneSet {
 
 // Build the coarse maps of every set: batched precompute straight into the
 // padded phase planes (query path) or a phase-plane copy of a supplied coarse
-// map, then the superblock planes of all sets in one launch.  Without phase
-// planes (LGS_OPT_COARSE_PLANES 0) the sets read plain coarse maps.
+// map, then the superblock planes of all sets in one launch.
 struct SetJobs {
     size_t jobs_off = 0, njobs = 0, pj_off = 0, npj = 0;
 };
@@ -2900,25 +2663,6 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
     const int ns = (int)sets.size();
     hipStream_t st = ctx->stream;
     const int lr = lp.low_res;
-    if (!ctx->coarse_planes) {
-        // plain layout: precomputed sets get a plain scratch map each
-        int nfine = 0;
-        for (auto& s : sets) nfine += s.fine != nullptr;
-        const size_t cells = (size_t)lp.W * lp.H;
-        double* plain = nfine ? (double*)ctx->ensure(S_COARSE_GRID, sizeof(double) * std::max<size_t>(1, cells) * nfine)
-                              : nullptr;
-        int k = 0;
-        for (auto& s : sets) {
-            if (s.fine) {
-                double* out = plain + cells * (size_t)k++;
-                launch_precompute(ctx, s.fine, lr, out, nullptr);
-                s.cmap = out;
-            } else {
-                s.cmap = s.coarse->d;
-            }
-        }
-        return SetJobs{};
-    }
     double* D = planes_buffer(ctx, lp, ns, need_super);
     SuperT* S = need_super ? (SuperT*)ctx->ensure(S_SUPER, super_bytes(lp) * (size_t)ns) : nullptr;
     int* neg = need_super ? (int*)ctx->ensure(S_NEGFLAG, sizeof(int) * (size_t)ns) : nullptr;
@@ -2978,7 +2722,6 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
 void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>& sets, const SetJobs& sj,
                  const Upload& up)
 {
-    if (!ctx->coarse_planes) return;
     int maxW = 0, maxH = 0;
     for (auto& s : sets)
         if (s.fine) {
@@ -2989,13 +2732,13 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
     if (sj.npj) {
         const int np = lp.low_res * lp.low_res;
         const bool lone = sj.npj == 1;
-        const int spx = lone ? LGS_SPX_LONE : kSPX;
+        const int spx = lone ? kSPXLone : kSPX;
         dim3 g((lp.Wqp + spx - 1) / spx, (lp.Hqp + kSPY - 1) / kSPY, np * (int)sj.npj);
         const int tok = ctx->timing_begin(K_SUPER_PLANES, 8.0 * 2.0 * (double)np * lp.pstride * sj.npj);
         if (!ctx->skipped(K_SUPER_PLANES)) {
             if (lone)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_planes<LGS_SPX_LONE>), g,
-                                   dim3((LGS_SPX_LONE + 3 + 63) / 64 * 64), 0, ctx->stream, up.at<PlaneJob>(sj.pj_off), np);
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_planes<kSPXLone>), g,
+                                   dim3((kSPXLone + 3 + 63) / 64 * 64), 0, ctx->stream, up.at<PlaneJob>(sj.pj_off), np);
             else
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_planes<kSPX>), g, dim3(kSPThreads), 0, ctx->stream,
                                    up.at<PlaneJob>(sj.pj_off), np);
@@ -3112,10 +2855,6 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<5>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else if (B.oct)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
-            else if (B.hex)
-                hipLaunchKernelGGL(k_super_hex, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
-            else if (B.quad)
-                hipLaunchKernelGGL(k_super_quad, g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else if (B.pair)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<1>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else
@@ -3149,10 +2888,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         {
             dim3 g((B.P + B.cb - 1) / B.cb, B.Tmax, n);
             const int tok = ctx->timing_begin(K_COARSE, 8.0 * beams_K);
-            if (B.planes)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1>), g, dim3(B.cb), 0, st, d_items, zero);
-            else
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<0>), g, dim3(B.cb), 0, st, d_items, zero);
+            hipLaunchKernelGGL(k_coarse, g, dim3(B.cb), 0, st, d_items, zero);
             ctx->timing_end(tok);
             LGS_HIP_CHECK(hipGetLastError());
         }
@@ -3457,16 +3193,13 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     B.cb = coarse_block(p0);
     B.pair = B.nsb2 <= 32;
     B.chunks = B.pair ? 1 : (B.nsb2 + 63) / 64;
-    B.quad = ctx->super_quad && p0.nsby * ((p0.nsbx + 1) / 2) <= 16;
-    B.hex = ctx->super_hex && B.quad && p0.nsby * ((p0.nsbx + 3) / 4) <= 10;
     B.oct = p0.oct != 0;
     B.nsby = p0.nsby;
-    B.planes = ctx->coarse_planes;
     B.pruned = uses_super(ctx, B.NvMax, B.nsb2, false);
     B.lr5 = lr5_path(B.NvMax, B.low_res);
     // lone matches keep the transposed row evaluator (LR waves per block: lower
     // latency for a handful of blocks); batches spread their blocks lane-per-pose
-    B.fine_lanes = ctx->fine_lanes && n >= ctx->lanes_min_batch && B.low_res * B.low_res <= 64 &&
+    B.fine_lanes = n >= ctx->lanes_min_batch && B.low_res * B.low_res <= 64 &&
                    B.NvMax <= kFineLanesMaxNv;
     B.frows = (B.lr5 && !B.fine_lanes) ? 5 : 1;
     B.kernel_size = cost->kernel_size;
@@ -3519,7 +3252,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
             d.bytes[k] = sz[k];
         }
         d.buf[8] = ij.cmap;   // the item's coarse phase planes and superblock planes
-        d.bytes[8] = B.planes ? plane_bytes(q) : sizeof(double) * (size_t)q.W * q.H;
+        d.bytes[8] = plane_bytes(q);
         d.buf[9] = ij.super;
         d.bytes[9] = ij.super ? super_bytes(q) : 0;
         d.gen = ij.gen;
@@ -3895,10 +3628,7 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
         LGS_HIP_CHECK(hipGetLastError());
         if (coarse_scores) {
             dim3 gc((pl.P + cb - 1) / cb, pl.T, 1);
-            if (ctx->coarse_planes)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<1>), gc, dim3(cb), 0, ctx->stream, d_items, ctx->zero);
-            else
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_coarse<0>), gc, dim3(cb), 0, ctx->stream, d_items, ctx->zero);
+            hipLaunchKernelGGL(k_coarse, gc, dim3(cb), 0, ctx->stream, d_items, ctx->zero);
             LGS_HIP_CHECK(hipGetLastError());
             LGS_HIP_CHECK(hipMemcpyAsync(coarse_scores, it.cscore, sizeof(double) * (size_t)pl.K,
                                          hipMemcpyDeviceToHost, ctx->stream));

@@ -30,13 +30,17 @@ constexpr int kSortThreads = 256;
 constexpr int kSortRadix = 256;        // bins per pass (digits of at most 8 bits)
 constexpr int kSortMaxPasses = 4;
 // control block (unsigned words, S_RAY0): zero between sorts
-constexpr int kCtlHist = 0;                                  // [pass][256] accumulators
-constexpr int kCtlDone = kSortMaxPasses * kSortRadix;        // workgroups finished k_sort_hist
+constexpr int kHistLanes = 8;                                // accumulator copies (workgroup % 8): less contention
+constexpr int kCtlHist = 0;                                  // [lane][pass][256] accumulators
+constexpr int kCtlDone = kHistLanes * kSortMaxPasses * kSortRadix;   // workgroups finished k_sort_hist
 constexpr int kCtlTicket = kCtlDone + 1;                     // [pass] tile tickets
-constexpr int kCtlOffs = 2 * kSortMaxPasses * kSortRadix;    // [pass][256] exclusive digit offsets
-constexpr int kCtlWords = 3 * kSortMaxPasses * kSortRadix;
+constexpr int kCtlBar = kCtlDone + 8;                        // k_sort_coop grid barrier, workgroups done
+constexpr int kCtlOffs = kCtlDone + 64;                      // [pass][256] exclusive digit offsets
+constexpr int kCtlWords = kCtlOffs + kSortMaxPasses * kSortRadix;
 
 constexpr unsigned long long kFlagAgg = 1ull << 30, kFlagPrefix = 2ull << 30;
+constexpr int kHistRun = 16;          // consecutive keys per thread in k_sort_hist
+constexpr int kLookback = 16;         // predecessor tiles read at once in the look-back
 constexpr unsigned long long kCountMask = (1ull << 30) - 1;
 
 __device__ __forceinline__ unsigned ld_agent(const unsigned* p)
@@ -53,18 +57,35 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_hist(const unsigned* __re
     const int tid = threadIdx.x;
     for (int p = 0; p < passes; ++p) h[p][tid] = 0;
     __syncthreads();
-    const long long stride = (long long)gridDim.x * kSortThreads;
-    for (long long i = (long long)blockIdx.x * kSortThreads + tid; i < n; i += stride) {
-        const unsigned k = keys[i];
+    // each thread counts kHistRun consecutive keys per chunk; equal digits of
+    // neighbouring keys (ray-ordered keys share their high digits) are
+    // counted in a register and added to LDS once per run
+    const long long stride = (long long)gridDim.x * kSortThreads * kHistRun;
+    for (long long i0 = ((long long)blockIdx.x * kSortThreads + tid) * kHistRun; i0 < n; i0 += stride) {
+        const int m = (int)min((long long)kHistRun, n - i0);
+        unsigned k[kHistRun];
+#pragma unroll
+        for (int q = 0; q < kHistRun; ++q) k[q] = (q < m) ? keys[i0 + q] : 0u;
         for (int p = 0; p < passes; ++p) {
             const int sh = lo + p * dbits;
-            const int nb = min(dbits, bits - p * dbits);
-            atomicAdd(&h[p][(k >> sh) & ((1u << nb) - 1u)], 1u);
+            const unsigned mask = (1u << min(dbits, bits - p * dbits)) - 1u;
+            unsigned cur = (k[0] >> sh) & mask, cnt = 0;
+#pragma unroll
+            for (int q = 0; q < kHistRun; ++q) {
+                const unsigned d = (k[q] >> sh) & mask;
+                if (q < m && d != cur) {
+                    atomicAdd(&h[p][cur], cnt);
+                    cur = d, cnt = 0;
+                }
+                cnt += (q < m) ? 1u : 0u;
+            }
+            atomicAdd(&h[p][cur], cnt);
         }
     }
     __syncthreads();
+    unsigned* acc = ctl + kCtlHist + (blockIdx.x % kHistLanes) * kSortMaxPasses * kSortRadix;
     for (int p = 0; p < passes; ++p)
-        if (h[p][tid]) __hip_atomic_fetch_add(ctl + kCtlHist + p * kSortRadix + tid, h[p][tid], __ATOMIC_RELAXED,
+        if (h[p][tid]) __hip_atomic_fetch_add(acc + p * kSortRadix + tid, h[p][tid], __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
     __threadfence();
     __syncthreads();
@@ -80,7 +101,9 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_hist(const unsigned* __re
     if (w < passes) {
         unsigned v[4], s = 0;
         for (int j = 0; j < 4; ++j) {
-            v[j] = ld_agent(ctl + kCtlHist + w * kSortRadix + lane * 4 + j);
+            v[j] = 0;
+            for (int l = 0; l < kHistLanes; ++l)
+                v[j] += ld_agent(ctl + kCtlHist + (l * kSortMaxPasses + w) * kSortRadix + lane * 4 + j);
             s += v[j];
         }
         unsigned incl = s;
@@ -95,8 +118,10 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_hist(const unsigned* __re
         }
     }
     __syncthreads();
-    for (int p = 0; p < passes; ++p)
-        __hip_atomic_store(ctl + kCtlHist + p * kSortRadix + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int l = 0; l < kHistLanes; ++l)
+        for (int p = 0; p < passes; ++p)
+            __hip_atomic_store(ctl + kCtlHist + (l * kSortMaxPasses + p) * kSortRadix + tid, 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     if (tid <= kSortMaxPasses)
         __hip_atomic_store(ctl + kCtlDone + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -166,19 +191,32 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const unsigned* __re
     }
     if (lane == 63) wsum[w] = incl;
     // decoupled look-back over the earlier tiles
+    // (kLookback predecessors per round, loads in flight together; a round
+    // consumes tiles up to the first one not yet published)
     unsigned excl = 0;
     if (tile > 0) {
         long long j = tile - 1;
-        for (;;) {
-            const unsigned long long v = __hip_atomic_load(status + (size_t)j * kSortRadix + d, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-            if ((v >> 32) != stamp || !(v & (kFlagAgg | kFlagPrefix))) {
-                __builtin_amdgcn_s_sleep(1);
-                continue;
+        for (bool done = false; !done;) {
+            unsigned long long v[kLookback];
+#pragma unroll
+            for (int q = 0; q < kLookback; ++q)
+                v[q] = (j - q >= 0) ? __hip_atomic_load(status + (size_t)(j - q) * kSortRadix + d, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0ull;
+            int used = 0;
+            bool stop = false;   // at the first unpublished tile, or after a prefix
+#pragma unroll
+            for (int q = 0; q < kLookback; ++q) {
+                const bool ready = (v[q] >> 32) == stamp && (v[q] & (kFlagAgg | kFlagPrefix));
+                if (!stop && ready) {
+                    excl += (unsigned)(v[q] & kCountMask);
+                    used = q + 1;
+                    done = (v[q] & kFlagPrefix) != 0;
+                }
+                stop = stop || !ready || done;
             }
-            excl += (unsigned)(v & kCountMask);
-            if (v & kFlagPrefix) break;
-            --j;
+            j -= used;
+            if (!done && used == 0) __builtin_amdgcn_s_sleep(1);
         }
         __hip_atomic_store(st, tag | kFlagPrefix | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -204,9 +242,158 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const unsigned* __re
     }
 }
 
+// Small sorts (every tile resident at once): all passes in ONE launch.  Each
+// workgroup ranks its tile as k_sort_pass does, stores its digit counts,
+// waits at a grid barrier, reads every tile's counts (digit totals and the
+// counts of the tiles before it: the same offsets a histogram and a look-back
+// give), scatters, and waits again before the next pass reads the keys.
+// Stores are released and loads acquired at agent scope around each barrier
+// (the tiles live on different XCDs, each with its own L2).
+__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target)
+{
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+}
+
+template <int KPT>
+__global__ __launch_bounds__(kSortThreads) void k_sort_coop(const unsigned* __restrict__ in, unsigned* __restrict__ out,
+                                                            unsigned* __restrict__ tmp, long long n, int lo,
+                                                            int dbits, int bits, int passes,
+                                                            unsigned* __restrict__ counts, unsigned* __restrict__ bar)
+{
+    constexpr int TILE = kSortThreads * KPT;
+    __shared__ unsigned keys_s[TILE];
+    __shared__ unsigned wcnt[4][kSortRadix];
+    __shared__ unsigned dstart[kSortRadix];
+    __shared__ unsigned gbase[kSortRadix];
+    __shared__ unsigned wsum[4], dsum[4];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const unsigned ntiles = gridDim.x, tile = blockIdx.x;
+    const long long t0 = (long long)tile * TILE;
+    const long long p0 = t0 + (long long)w * 64 * KPT + lane;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned nbar = 0;
+    for (int p = 0; p < passes; ++p) {
+        const unsigned* src = (p == 0) ? in : (((passes - p) % 2 == 1) ? tmp : out);
+        unsigned* dst = ((passes - 1 - p) % 2 == 0) ? out : tmp;
+        const int shift = lo + p * dbits;
+        const int nb = min(dbits, bits - p * dbits);
+        const unsigned mask = (1u << nb) - 1u;
+        wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+        __syncthreads();
+        unsigned k[KPT], rank[KPT];
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) {
+            const long long q = p0 + 64 * i;
+            k[i] = (q < n) ? src[q] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) {
+            const bool valid = p0 + 64 * i < n;
+            const unsigned d = (k[i] >> shift) & mask;
+            unsigned long long peers = __ballot(valid);
+            for (int b = 0; b < nb; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const unsigned long long m = __ballot(valid && bit);
+                peers &= bit ? m : ~m;
+            }
+            const unsigned base = wcnt[w][d];
+            rank[i] = base + (unsigned)__popcll(peers & lt);
+            if (valid && !(peers & lt)) wcnt[w][d] = base + (unsigned)__popcll(peers);
+        }
+        __syncthreads();
+        const int d = tid;
+        const unsigned c0 = wcnt[0][d], c1 = wcnt[1][d], c2 = wcnt[2][d], c3 = wcnt[3][d];
+        const unsigned tot = c0 + c1 + c2 + c3;
+        wcnt[0][d] = 0;
+        wcnt[1][d] = c0;
+        wcnt[2][d] = c0 + c1;
+        wcnt[3][d] = c0 + c1 + c2;
+        unsigned* cp = counts + (size_t)p * ntiles * kSortRadix;
+        cp[(size_t)tile * kSortRadix + d] = tot;
+        unsigned incl = tot;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+        }
+        if (lane == 63) wsum[w] = incl;
+        grid_barrier(bar, ++nbar * ntiles);
+        // digit d: its total over all tiles and the count of the tiles before this one
+        // (16 loads in flight per round: the rows were written on other XCDs)
+        unsigned all = 0, before = 0;
+        for (unsigned t0c = 0; t0c < ntiles; t0c += 16) {
+            unsigned c[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                c[q] = (t0c + q < ntiles) ? cp[(size_t)(t0c + q) * kSortRadix + d] : 0u;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                all += c[q];
+                before += (t0c + q < tile) ? c[q] : 0u;
+            }
+        }
+        unsigned ai = all;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned t = __shfl_up(ai, o);
+            if (lane >= o) ai += t;
+        }
+        if (lane == 63) dsum[w] = ai;
+        __syncthreads();
+        unsigned wo = 0, dwo = 0;
+        for (int q = 0; q < w; ++q) wo += wsum[q], dwo += dsum[q];
+        dstart[d] = wo + incl - tot;
+        gbase[d] = dwo + ai - all + before;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < KPT; ++i)
+            if (p0 + 64 * i < n) {
+                const unsigned dd = (k[i] >> shift) & mask;
+                keys_s[dstart[dd] + wcnt[w][dd] + rank[i]] = k[i];
+            }
+        __syncthreads();
+        const int nvalid = (int)max(0LL, min((long long)TILE, n - t0));
+        for (int j = tid; j < nvalid; j += kSortThreads) {
+            const unsigned key = keys_s[j];
+            const unsigned dd = (key >> shift) & mask;
+            dst[gbase[dd] + (unsigned)j - dstart[dd]] = key;
+        }
+        if (p + 1 < passes) grid_barrier(bar, ++nbar * ntiles);
+    }
+    // the last workgroup out resets the barrier for the next sort
+    __syncthreads();
+    if (tid == 0 &&
+        __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ntiles - 1) {
+        __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 }  // namespace
 
 namespace lgs {
+
+// Workgroups of k_sort_coop the device holds at once (all its tiles must be
+// resident: they wait for each other), with a margin for other streams' work.
+long long coop_capacity(lgs_ctx* ctx)
+{
+    static long long cap[64] = {};
+    const int dev = ctx->device;
+    if (dev < 0 || dev >= 64) return 0;
+    if (!cap[dev]) {
+        int per_cu = 0, cus = 0;
+        LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_coop<16>, kSortThreads, 0));
+        LGS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        cap[dev] = std::max(1LL, (long long)per_cu * cus / 2);
+    }
+    return cap[dev];
+}
 
 // Stable sort of n 32-bit keys on bits [lo, lo + bits).  `tmp` (n keys) is
 // needed when the sort takes two or more passes; in, tmp and out are distinct.
@@ -225,13 +412,25 @@ void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, lon
     const bool fresh = ctx->buf[S_RAY0] == nullptr;
     unsigned* ctl = (unsigned*)ctx->ensure(S_RAY0, sizeof(unsigned) * kCtlWords);
     if (fresh) LGS_HIP_CHECK(hipMemsetAsync(ctl, 0, sizeof(unsigned) * kCtlWords, st));
-    // small sorts: 1024-key tiles (enough workgroups to fill the chip); large: 4096
-    const bool big = n >= (1LL << 21);
+    // one launch when every tile can be resident at once (measured per device)
+    constexpr int kCoopTile = kSortThreads * 16;
+    const long long ctiles = (n + kCoopTile - 1) / kCoopTile;
+    if (ctiles <= coop_capacity(ctx) && (passes == 1 || tmp)) {
+        unsigned* counts = (unsigned*)ctx->ensure(S_RAY1, sizeof(unsigned) * (size_t)ctiles * kSortRadix * passes);
+        hipLaunchKernelGGL(k_sort_coop<16>, dim3((unsigned)ctiles), dim3(kSortThreads), 0, st, in, out, tmp, n, lo,
+                           dbits, bits, passes, counts, ctl + kCtlBar);
+        LGS_HIP_CHECK(hipGetLastError());
+        return;
+    }
+    // 4096-key tiles (a short look-back chain); 1024-key tiles only for sorts
+    // too small to give 64 workgroups
+    const bool big = n >= 64LL * 4096;
     const int tile = kSortThreads * (big ? 16 : 4);
     const long long tiles = (n + tile - 1) / tile;
     unsigned long long* status = (unsigned long long*)ctx->ensure(
         S_RAY1, sizeof(unsigned long long) * (size_t)tiles * kSortRadix * (size_t)passes);
-    const unsigned hist_blocks = (unsigned)std::min<long long>(std::max<long long>(1, n / 8192), 1024);
+    const unsigned hist_blocks =
+        (unsigned)std::min<long long>((n + kSortThreads * kHistRun - 1) / (kSortThreads * kHistRun), 2048);
     hipLaunchKernelGGL(k_sort_hist, dim3(hist_blocks), dim3(kSortThreads), 0, st, in, n, lo, dbits, bits, passes,
                        ctl);
     LGS_HIP_CHECK(hipGetLastError());

@@ -314,18 +314,14 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
         ctx->profile_mask = (unsigned)value;
         ctx->profile = ctx->profile_mask != 0;
         return LGS_OK;
-    case LGS_OPT_COARSE_PLANES: ctx->coarse_planes = value != 0.0; return LGS_OK;
     case LGS_OPT_SUPER_PRUNE: ctx->super_prune = value != 0.0; return LGS_OK;
     case LGS_OPT_LANES_MIN_BATCH: ctx->lanes_min_batch = (int)value; return LGS_OK;
-    case LGS_OPT_SUPER_QUAD: ctx->super_quad = value != 0.0; return LGS_OK;
-    case LGS_OPT_SUPER_HEX: ctx->super_hex = value != 0.0; return LGS_OK;
     case LGS_OPT_RAY_CHUNK_KEYS:
         if (!(value >= 1.0)) return LGS_ERR_INVALID_ARG;
         ctx->ray_chunk_keys = (long long)std::min(value, (double)(1LL << 30));
         return LGS_OK;
     case LGS_OPT_SKIP_MASK: ctx->skip_mask = (unsigned)value; return LGS_OK;
     case LGS_OPT_POISON_WS: ctx->poison_ws = value != 0.0; return LGS_OK;
-    case LGS_OPT_FINE_LANES: ctx->fine_lanes = value != 0.0; return LGS_OK;
     case LGS_OPT_LINSOLVE_SPLIT: ctx->linsolve_split = value != 0.0; return LGS_OK;
     case LGS_OPT_HANDOFF_SPIN_US:
         if (value < 0.0) return LGS_ERR_INVALID_ARG;

@@ -206,14 +206,10 @@ struct lgs_ctx {
     bool force_dense = false;
     bool inject_index = false;
     int guard_cap = lgs::kGuardInline;
-    bool coarse_planes = true;   // phase-plane coarse layout (LGS_OPT_COARSE_PLANES)
     bool super_prune = true;     // superblock pruning of k_coarse (LGS_OPT_SUPER_PRUNE)
-    bool super_hex = true;       // k_super_hex (fp16 planes: 4 superblocks per gather) where it applies (LGS_OPT_SUPER_HEX)
-    bool super_quad = true;      // k_super_quad (8-byte superblock gathers) where it applies (LGS_OPT_SUPER_QUAD)
     bool linsolve_split = true;  // lone refine over one workgroup per 64 beams (LGS_OPT_LINSOLVE_SPLIT)
     long long handoff_spin_us = 200000;   // split refine spin bound (LGS_OPT_HANDOFF_SPIN_US; 0 = force the fallback)
     long long handoff_fallbacks = 0;      // split refines rerun on one workgroup after a time-out
-    bool fine_lanes = true;      // fine stage: one lane per pose over the batch's global block list (LGS_OPT_FINE_LANES)
     int lanes_min_batch = 2;     // pruned coarse stage: k_coarse_lanes from this batch size on (LGS_OPT_LANES_MIN_BATCH)
     long long ray_chunk_keys = 1LL << 28;  // ray-cast keys per emit/sort/apply pass (LGS_OPT_RAY_CHUNK_KEYS)
     // Stamps come from one process-wide counter: a context's scratch may be

@@ -21,16 +21,12 @@ LGS_OPT_FORCE_DENSE = 2
 LGS_OPT_INJECT_INDEX = 3
 LGS_OPT_GUARD_CAP = 4
 LGS_OPT_PROFILE = 5
-LGS_OPT_COARSE_PLANES = 6
 LGS_OPT_PROFILE_MASK = 7
 LGS_OPT_SPIN_SYNC = 8
 LGS_OPT_SUPER_PRUNE = 9
 LGS_OPT_LANES_MIN_BATCH = 11
-LGS_OPT_SUPER_QUAD = 12
 LGS_OPT_RAY_CHUNK_KEYS = 13
-LGS_OPT_SUPER_HEX = 14
 LGS_OPT_POISON_WS = 15   # diagnostics only
-LGS_OPT_FINE_LANES = 16
 LGS_OPT_SKIP_MASK = 10   # diagnostics only
 LGS_OPT_LINSOLVE_SPLIT = 17
 LGS_OPT_HANDOFF_SPIN_US = 18

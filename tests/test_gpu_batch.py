@@ -118,9 +118,9 @@ def test_query_batch_fixups_and_dense(ctx, world, small_map):
         ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 0)
 
 
-@pytest.mark.parametrize("planes,prune", [(1, 1), (1, 0), (0, 0)])
-def test_query_batch_layouts(ctx, world, small_map, planes, prune):
-    """Superblock pruning on/off and the plain coarse layout give the same batch."""
+@pytest.mark.parametrize("prune", [1, 0])
+def test_query_batch_layouts(ctx, world, small_map, prune):
+    """Superblock pruning on and off give the same batch."""
     cells, mx, my = small_map
     rng = np.random.default_rng(9)
     ang, qs = _queries(world, rng, 5, 541)
@@ -129,11 +129,9 @@ def test_query_batch_layouts(ctx, world, small_map, planes, prune):
     g = ctx.grid_from_array(cells, mx, my, 0.05)
     scans = [ctx.scan(r, ang) for r, _ in qs]
     try:
-        ctx.set_option(abi.LGS_OPT_COARSE_PLANES, planes)
         ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, prune)
         batch = ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])
     finally:
-        ctx.set_option(abi.LGS_OPT_COARSE_PLANES, 1)
         ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 1)
     for j, ((r, init), b) in enumerate(zip(qs, batch)):
         assert_same(b, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"q{j}")
@@ -225,7 +223,7 @@ def test_pruning_is_history_independent(ctx, world, small_map, poison):
     """Every record field -- including coarse_blocks, the superblock pruning's
     work and the roofline's algorithmic bytes -- is a function of the call's
     inputs only: call A, then calls that leave other contents in the
-    workspace (another T and Nv, a batch, the dense path, the plain layout),
+    workspace (another T and Nv, a batch, the dense path, the unpruned path),
     then A again.  With LGS_OPT_POISON_WS every workspace byte is 0xFF before
     each batch, so a read-before-write would change the result."""
     cells, mx, my = small_map
@@ -249,9 +247,9 @@ def test_pruning_is_history_independent(ctx, world, small_map, poison):
                 ctx.optimize_pose_query(g, P, cost, scans[2], qs[2][1])
                 ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 0)
             if k == 2:
-                ctx.set_option(abi.LGS_OPT_COARSE_PLANES, 0)
+                ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 0)
                 ctx.optimize_pose_query(g, P, cost, scans[1], qs[1][1])
-                ctx.set_option(abi.LGS_OPT_COARSE_PLANES, 1)
+                ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 1)
             again = [_record(ctx.optimize_pose_query(g, P, cost, sc, i)) for sc, (_, i) in zip(scans, qs)]
             assert again == first, (k, _diff(again, first))
             batch = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, [i for _, i in qs])]
@@ -265,4 +263,4 @@ def test_pruning_is_history_independent(ctx, world, small_map, poison):
     finally:
         ctx.set_option(abi.LGS_OPT_POISON_WS, 0)
         ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 0)
-        ctx.set_option(abi.LGS_OPT_COARSE_PLANES, 1)
+        ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 1)

@@ -412,6 +412,25 @@ def test_super_prune_wide_window(ctx, world):
     assert_same(on, oracle_match(cells, mx, my, 0.05, params, r, ang, init), "wide")
 
 
+@pytest.mark.parametrize("rx,ry", [(9.0, 1.0), (1.0, 9.0)])
+def test_super_prune_anisotropic_windows(ctx, world, rx, ry):
+    """Windows whose superblock grid is 10 x 2 / 2 x 10: too many superblock
+    rows or columns for the octet layout, so k_super over the fp16 sub-phase
+    planes bounds them -- pruned == unpruned == oracle."""
+    cells, mx, my = build_map(world, 400, 0.05, 100, scene.arc_poses(5), n_beams=541)
+    ang = scene.beam_angles(541)
+    true = (0.4, -0.1, 0.9)
+    r = scene.ray_cast(world, true, ang)
+    init = (0.5, -0.2, 0.95)
+    params = (5, rx, ry, 0.2, 20.0)
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    sc = ctx.scan(r, ang)
+    on, off = _query_ab(ctx, g, abi.RtcsmParams(*params), sc, init)
+    _identical(on, off, "aniso")
+    assert_same(on, oracle_match(cells, mx, my, 0.05, params, r, ang, init), "aniso")
+    assert on.coarse_blocks < off.coarse_blocks, (on.coarse_blocks, off.coarse_blocks)
+
+
 def test_super_prune_batch_and_fixed_threshold(ctx, world):
     """OptimizePose with a caller coarse map (decimated per batch) and a
     fixed threshold: pruned batch == unpruned batch."""
