@@ -177,16 +177,17 @@ def lib_sha256() -> str:
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def pmc_for(pmc_path, trace_kernel):
+def pmc_for(pmc_path, trace_kernel, workload):
     """Counter bytes per launch of `trace_kernel` from a PMC summary of THIS
-    build (tools/pmc_summary.py records the library's sha256), else None.
+    build and THIS workload (tools/pmc_summary.py records the library's
+    sha256 and the bench workload profiled), else None.
     gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads
     (MI355X_MICROARCH.md §HBM): 'traffic' doubles it; the raw sum is kept too."""
     try:
         pmc = json.load(open(pmc_path))
     except (OSError, ValueError):
         return None
-    if pmc.get("lib_sha256") != lib_sha256():
+    if pmc.get("lib_sha256") != lib_sha256() or pmc.get("workload", "match") != workload:
         return None
     e = pmc.get("kernels", {}).get(trace_kernel)
     if not e or "fetch_bytes_per_launch" not in e or "write_bytes_per_launch" not in e:
@@ -196,7 +197,7 @@ def pmc_for(pmc_path, trace_kernel):
                 l2_hit_rate=e.get("l2_hit_rate"), profile=os.path.relpath(pmc_path, ROOT))
 
 
-def roofline_from(stats, kernel, pmc_path, trace_kernel, bound):
+def roofline_from(stats, kernel, pmc_path, trace_kernel, bound, workload="match"):
     """Roofline of the dominant kernel: achieved = ALGORITHMIC bytes per launch
      / event-timed average launch duration; frac against the
     8 TB/s HBM peak.  frac_hbm_counters = the PMC-counted HBM bytes of the same
@@ -207,7 +208,7 @@ def roofline_from(stats, kernel, pmc_path, trace_kernel, bound):
     per_launch = k["algo_bytes"] / k["launches"]
     avg_ms = k["total_ms"] / k["launches"]
     achieved = per_launch / (avg_ms * 1e-3) / 1e9
-    p = pmc_for(pmc_path, trace_kernel)
+    p = pmc_for(pmc_path, trace_kernel, workload)
     traffic = round(p["traffic"]) if p else None
     frac_hbm = round(traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if p else None
     return dict(bound=bound, achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
@@ -671,7 +672,8 @@ def run_loop(args, D, ctx):
                               "config5: LoopDetectorRealTimeCorrelative::Detect batch"), candidates=len(cands),
                     found=found, parallelism=f"candidates sharded in contiguous blocks over {D.world} ranks + "
                                              "RCCL all-gather of 176-B result records"),
-        roofline=roofline_from(stats, dominant, args.pmc, "k_bb_score" if bb else "k_coarse_lanes", "l2-gather"),
+        roofline=roofline_from(stats, dominant, args.pmc, "k_bb_score" if bb else "k_coarse_lanes", "l2-gather",
+                               workload="loop_bb" if bb else "loop"),
         cpu_baseline=cpu)
     return line, stats, value
 
@@ -793,7 +795,7 @@ def run_stream(args, D, ctx):
                              f"{'/'.join(str(v) for v in win)})", beams=1081,
                     scan_interpolator=bool(args.interp), latest_map_scans=10, parallelism=f"replicas x{D.world}"),
         final_drift_m=round(float(drift), 4), breakdown_per_step=breakdown,
-        roofline=roofline_from(stats, "k_ray_apply", args.pmc, "k_apply", "hbm"), cpu_baseline=cpu)
+        roofline=roofline_from(stats, "k_ray_apply", args.pmc, "k_apply", "hbm", workload=args.workload), cpu_baseline=cpu)
     return line, stats, value
 
 
@@ -946,7 +948,7 @@ def run_rebuild(args, D, ctx):
         config=dict(workload="f2: GridMapBuilder::AfterLoopClosure (all local maps, one fused ray-cast pass)",
                     nodes=n_nodes, local_maps=len(maps), beams=1081, parallelism=f"replicas x{D.world}"),
         global_map=dict(ms=round(global_ms, 3), cells=[gg["w"], gg["h"]], nodes=n_nodes),
-        roofline=roofline_from(stats, "k_ray_apply", args.pmc, "k_apply", "hbm"), cpu_baseline=cpu)
+        roofline=roofline_from(stats, "k_ray_apply", args.pmc, "k_apply", "hbm", workload=args.workload), cpu_baseline=cpu)
     return line, stats, value
 
 

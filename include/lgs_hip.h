@@ -169,6 +169,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: lane-per-block kernel for batches of at least this many matches (default 2; 1 = always), else the row kernel */
 #define LGS_OPT_LINSOLVE_SPLIT 17 /* 1 (default) = a lone ScanMatcherLinearSolver refine of <= 1280 beams runs one workgroup per 64 beams (in-launch hand-off per pass) when they fit the device at once, 0 = one workgroup */
 #define LGS_OPT_HANDOFF_SPIN_US 18 /* split refine: bound of a workgroup's wait for the others (default 200000 us); on time-out the refine is rerun on one workgroup.  0 = force that fallback (tests) */
+#define LGS_OPT_PEER_COPY     19  /* lgs_loop_detect_rtcsm_multi, on the shard's ctx: 0 (default) = maps copied device to device (peer access enabled when the devices differ and allow it, else staged through pinned host memory), 1 = always staged through host memory */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 
@@ -191,6 +192,11 @@ int  lgs_debug_libm(lgs_ctx* ctx, int op, const double* x, int n, double* out);
  * every ray-cast pass) of n host keys on bits [lo, lo + bits), through the
  * device; out receives the sorted keys. */
 int  lgs_debug_keysort(lgs_ctx* ctx, const unsigned* keys, unsigned* out, long long n, int lo, int bits);
+
+/* Diagnostics: cross-context copies made by lgs_loop_detect_rtcsm_multi onto
+ * this context since it was created: device to device (same device or peer
+ * access over xGMI) and staged through pinned host memory. */
+int  lgs_debug_copy_counters(const lgs_ctx* ctx, long long* direct, long long* staged);
 
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is
  * the algorithmic byte count of DESIGN.md §Roofline (e.g. 8 B per coarse-score
@@ -338,7 +344,15 @@ int  lgs_map_update_scan(lgs_ctx* ctx, lgs_map* map, const lgs_scan* scan, lgs_p
                          const lgs_builder_params* params);
 /* GridMapBuilder::ConstructMapFromScans (C/mapping/grid_map_builder.cpp:227-332):
  * Resize to the bounding box of all scans (topRight starts at DBL_MIN), Reset,
- * then ray-cast every scan in order. */
+ * then ray-cast every scan in order.  Called again on the same map with the
+ * window of UpdateLatestMap (:196-207: the previous scans, less at most the
+ * oldest, plus one new scan; same poses, parameters and geometry), only the
+ * cells the new or the dropped scan touch are recomputed (DESIGN.md §4.4b;
+ * same cells, counts and patch flags as a full rebuild).  Such an incremental
+ * call returns before its device work has finished: reads of the map through
+ * this library wait for it (on any context); lgs_grid_device_ptr users
+ * synchronise the context first.  An internal error of that work is reported
+ * by the map's next rebuild. */
 int  lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* map, const lgs_scan* const* scans,
                                   const lgs_pose2d* robot_poses, int n,
                                   const lgs_builder_params* params);
@@ -347,7 +361,9 @@ int  lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* map, const lgs_scan* co
  * lgs_map_update_scan does (UpdateGridMap :98-193), and `latest` rebuilt from
  * all n scans exactly as lgs_map_construct_from_scans does (UpdateLatestMap
  * :196-207; n = min(node count, NumOfScansForLatestMap)).  Same results as the
- * two calls; both ray-casts share one device pass.  local != latest. */
+ * two calls; both ray-casts share one device pass (one cast of the new scan
+ * when the two maps' cells of it differ by a whole-cell shift).  Incremental
+ * and asynchronous as lgs_map_construct_from_scans.  local != latest. */
 int  lgs_map_append_scan(lgs_ctx* ctx, lgs_map* local, lgs_map* latest, const lgs_scan* const* scans,
                          const lgs_pose2d* robot_poses, int n, const lgs_builder_params* params);
 

@@ -481,6 +481,8 @@ struct WindowJob {
     int eslot;                      // E's slot
     RayMap latest, local;           // latest map (cell base 0), local map (insert of E)
     long long nE, nloc;             // E's latest keys [0, nE), local keys [nE, nE + nloc) of slot[eslot]
+    int lshift, ldx, ldy;           // lshift: E's local cells are its latest cells + (ldx, ldy), so the
+                                    // local insert walks E's latest runs (nloc = nE, nothing emitted twice)
     const unsigned* lkeys;          // L's list: [lbeg, lbeg + nL) of lrb's array (nL = 0: no L)
     RunBits lrb;
     long long lbeg, nL;
@@ -602,11 +604,16 @@ __global__ __launch_bounds__(256) void k_apply_window(const WindowJob* __restric
         if (!run_start(E.rb.endw, i)) return;
         recompute_cell(J, E.keys[i] >> kTagShift, ch, K, ll);
     } else if (i < J.nE + J.nloc) {                   // E into the local map
-        if (!run_start(E.rb.endw, i)) return;
-        const unsigned long long local = (E.keys[i] >> kTagShift) - J.local.base;
+        const long long p = J.lshift ? i - J.nE : i;
+        if (!run_start(E.rb.endw, p)) return;
+        const unsigned c = E.keys[p] >> kTagShift;
+        const unsigned long long local =
+            J.lshift ? (unsigned long long)((int)(c / (unsigned)J.latest.w) + J.ldy) * (unsigned)J.local.w +
+                           (unsigned)((int)(c % (unsigned)J.latest.w) + J.ldx)
+                     : c - J.local.base;
         mark_patch(J.local, local);
         uint32_t nh = 0, nm = 0;
-        const double v = walk_run(i, J.local.cells[local], nh, nm, E.rb, ch, K);
+        const double v = walk_run(p, J.local.cells[local], nh, nm, E.rb, ch, K);
         J.local.cells[local] = v;
         J.local.hit[local] += nh;
         J.local.miss[local] += nm;
@@ -1473,11 +1480,30 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
     lens.reserve(E->xy.size());
     const long long nE = scan_rays(latest, *E, rays, lens);
     const size_t nrE = rays.size();
-    const long long nloc = local ? scan_rays(local, *E, rays, lens) : 0;
-    const long long keys = nE + nloc;
+    long long nloc = local ? scan_rays(local, *E, rays, lens) : 0;
+    // the local map's cells of E's rays are usually its latest-map cells
+    // shifted by whole cells (both maps keep the lattice of their common
+    // origin): then E is cast and sorted once and the local insert walks the
+    // same runs -- checked ray by ray with the host's own cell computations
+    int lshift = 0, ldx = 0, ldy = 0;
+    if (local && nrE > 0) {
+        ldx = rays[nrE].x - rays[0].x;
+        ldy = rays[nrE].y - rays[0].y;
+        lshift = 1;
+        for (size_t k = 0; k < nrE && lshift; ++k) {
+            const int4 a = rays[k], b = rays[nrE + k];
+            lshift = b.x == a.x + ldx && b.y == a.y + ldy && b.z == a.z + ldx && b.w == a.w + ldy;
+        }
+        if (lshift) {
+            rays.resize(nrE);
+            lens.resize(nrE);
+        }
+    }
+    const long long keys = lshift ? nE : nE + nloc;
     const long long nr = (long long)rays.size();
     const unsigned long long lat_cells = (unsigned long long)latest->w * latest->h;
-    const unsigned long long cells = lat_cells + (local ? (unsigned long long)local->w * local->h : 0ull);
+    const unsigned long long cells =
+        lat_cells + ((local && !lshift) ? (unsigned long long)local->w * local->h : 0ull);
     LGS_REQUIRE(cells < (1ull << (32 - kTagShift)), "latest step: cell bits");
     KeyBufPtr buf = C.acquire(std::max(1LL, keys));
     const unsigned stamp = (unsigned)ctx->next_stamp();
@@ -1527,6 +1553,9 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
     if (local) J.local = pm[1];
     J.nE = nE;
     J.nloc = nloc;
+    J.lshift = lshift;
+    J.ldx = ldx;
+    J.ldy = ldy;
     if (evict && L.buf) {
         J.lkeys = L.buf->keys;
         J.lrb = L.buf->bits();
@@ -1556,7 +1585,7 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
         hipLaunchKernelGGL(k_runsummary, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, buf->hitw, buf->endw,
                            nw, buf->hit2, buf->miss2, buf->end2);
     }
-    const long long nthreads = keys + nL;
+    const long long nthreads = nE + nloc + nL;
     if (nE + nL > C.long_cap) {
         if (C.d_long) LGS_HIP_CHECK(hipFree(C.d_long));
         C.d_long = nullptr;

@@ -32,6 +32,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <thread>
 #include <type_traits>
 
@@ -2616,25 +2618,26 @@ inline size_t super_bytes(const RtcsmPlan& pl)
 }
 double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_super)
 {
+    const int b = ctx->bank;
     const size_t bytes = plane_bytes(pl) * (size_t)nsets;
-    double* D = (double*)ctx->ensure(S_DECIM, bytes);
+    double* D = (double*)ctx->ensure(ctx->banked(S_DECIM), bytes);
     // (k_super_planes writes every superblock-plane value; they are zeroed
     // with the planes only so that no stale value is ever read)
     const size_t sbytes = super_bytes(pl) * (size_t)nsets;
-    SuperT* S = with_super ? (SuperT*)ctx->ensure(S_SUPER, sbytes) : nullptr;
+    SuperT* S = with_super ? (SuperT*)ctx->ensure(ctx->banked(S_SUPER), sbytes) : nullptr;
     const long long key[4] = { pl.low_res, pl.Wq, pl.Hq, pl.M };
-    if (D != ctx->planes_ptr || std::memcmp(key, ctx->planes_key, sizeof(key)) != 0 || nsets > ctx->planes_sets ||
-        (with_super && (S != ctx->super_ptr || nsets > ctx->super_sets))) {
+    if (D != ctx->planes_ptr[b] || std::memcmp(key, ctx->planes_key[b], sizeof(key)) != 0 ||
+        nsets > ctx->planes_sets[b] || (with_super && (S != ctx->super_ptr[b] || nsets > ctx->super_sets[b]))) {
         LGS_HIP_CHECK(hipMemsetAsync(D, 0, bytes, ctx->stream));
-        ctx->planes_ptr = D;
-        ctx->planes_sets = nsets;
-        std::memcpy(ctx->planes_key, key, sizeof(key));
-        ctx->super_ptr = nullptr;
-        ctx->super_sets = 0;
+        ctx->planes_ptr[b] = D;
+        ctx->planes_sets[b] = nsets;
+        std::memcpy(ctx->planes_key[b], key, sizeof(key));
+        ctx->super_ptr[b] = nullptr;
+        ctx->super_sets[b] = 0;
         if (with_super) {
             LGS_HIP_CHECK(hipMemsetAsync(S, 0, sbytes, ctx->stream));
-            ctx->super_ptr = S;
-            ctx->super_sets = nsets;
+            ctx->super_ptr[b] = S;
+            ctx->super_sets[b] = nsets;
         }
     }
     return D;
@@ -2664,8 +2667,8 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
     hipStream_t st = ctx->stream;
     const int lr = lp.low_res;
     double* D = planes_buffer(ctx, lp, ns, need_super);
-    SuperT* S = need_super ? (SuperT*)ctx->ensure(S_SUPER, super_bytes(lp) * (size_t)ns) : nullptr;
-    int* neg = need_super ? (int*)ctx->ensure(S_NEGFLAG, sizeof(int) * (size_t)ns) : nullptr;
+    SuperT* S = need_super ? (SuperT*)ctx->ensure(ctx->banked(S_SUPER), super_bytes(lp) * (size_t)ns) : nullptr;
+    int* neg = need_super ? (int*)ctx->ensure(ctx->banked(S_NEGFLAG), sizeof(int) * (size_t)ns) : nullptr;
     const size_t pb = plane_bytes(lp) / sizeof(double), sbb = super_bytes(lp) / sizeof(SuperT);
     // fine maps with W, H multiples of LowRes: the precompute writes the
     // planes directly (one batched launch); other maps go through a plain
@@ -3157,9 +3160,28 @@ void check_coarse(const lgs_grid* grid, const lgs_grid* coarse)
 // map geometry; sets are the distinct coarse maps (set_of[j] = item j's).
 // One host synchronisation in the common case; guarded projections and
 // dangerous blocks trigger exact single-item reruns.
-void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
-                 const lgs_grid* const* grids, lgs_scan* const* scans, const lgs_pose2d* init, int n,
-                 double nthr, std::vector<PlaneSet>& sets, const int* set_of, lgs_rtcsm_summary* out)
+// A launched batch whose results the host has not taken yet.
+struct InFlight {
+    std::vector<MatchItem> items;
+    BatchShape B;
+    std::vector<int> gens;
+    std::vector<PlaneSet> sets;
+    const lgs_grid* const* grids = nullptr;
+    lgs_scan* const* scans = nullptr;
+    const lgs_pose2d* init = nullptr;
+    lgs_rtcsm_summary* out = nullptr;
+    RtcsmRecord* h_rec = nullptr;
+    RtcsmRecord* d_rec = nullptr;
+    int n = 0, bank = 0;
+    long long id = 0;   // timing batch
+};
+
+// The device part of a batch, on ctx->bank's buffers: every stage launched,
+// the records' copy to the host queued and the bank's event recorded.
+void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
+                    const lgs_grid* const* grids, lgs_scan* const* scans, const lgs_pose2d* init, int n,
+                    double nthr, std::vector<PlaneSet>& sets, const int* set_of, lgs_rtcsm_summary* out,
+                    InFlight& F)
 {
     LGS_HIP_CHECK(hipSetDevice(ctx->device));
     LGS_REQUIRE(n >= 1 && n <= kMaxBatchItems, "batch of 1..64 matches (run_chunked splits larger ones)");
@@ -3205,9 +3227,10 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     B.kernel_size = cost->kernel_size;
     B.nsegMax = (int)(((long long)B.Tmax * B.P + kSelSeg - 1) / kSelSeg);
     const ItemLayout L = item_layout(B.Tmax, B.NvMax, B.P, B.nsb2, B.chunks, B.cb, B.frows, Nmax);
-    char* ws = (char*)ctx->ensure(S_BATCH_WS, L.total * (size_t)n);
-    RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord) * (size_t)n);
-    RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned(sizeof(RtcsmRecord) * (size_t)n);
+    char* ws = (char*)ctx->ensure(ctx->banked(S_BATCH_WS), L.total * (size_t)n);
+    RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(ctx->banked(S_RECORDS), sizeof(RtcsmRecord) * (size_t)n);
+    RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned_rec(sizeof(RtcsmRecord) * (size_t)n);
+    F.id = ++ctx->timing_batch;
     // The angle flags are only ever SET (k_project stamps an angle whose lattice
     // leaves the map low): clear every item's flags first.  (A generation stamp
     // alone is not enough -- the workspace also holds ints of other layouts,
@@ -3263,17 +3286,50 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     enqueue_items(ctx, B, up.at<MatchItem>(items_off), items, ScanOptions{});
     LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n, hipMemcpyDeviceToHost,
                                  ctx->stream));
-    ctx->sync();
+    hipEvent_t& ev = ctx->bank_ev[ctx->bank];
+    if (!ev) LGS_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    LGS_HIP_CHECK(hipEventRecord(ev, ctx->stream));
+    F.items = std::move(items);
+    F.B = B;
+    F.gens = std::move(gens);
+    F.sets = sets;
+    F.grids = grids;
+    F.scans = scans;
+    F.init = init;
+    F.out = out;
+    F.h_rec = h_rec;
+    F.d_rec = d_rec;
+    F.n = n;
+    F.bank = ctx->bank;
+}
+
+// The host part: wait for the batch's records (not for later batches), then
+// the guard checks, exactness reruns (on the batch's own bank) and summaries.
+void finish_matches(lgs_ctx* ctx, InFlight& F)
+{
+    ctx->bank = F.bank;
+    ctx->wait_event(ctx->bank_ev[F.bank]);
+    std::vector<MatchItem>& items = F.items;
+    const BatchShape& B = F.B;
+    const std::vector<int>& gens = F.gens;
+    lgs_scan* const* scans = F.scans;
+    const lgs_pose2d* init = F.init;
+    lgs_rtcsm_summary* out = F.out;
+    RtcsmRecord* h_rec = F.h_rec;
+    RtcsmRecord* d_rec = F.d_rec;
+    const int n = F.n;
     if (ctx->profile) {
         double coarse_bytes = 0.0;   // pruned k_coarse: 8 B x Nv per block it scored
         for (int j = 0; j < n; ++j) coarse_bytes += 8.0 * items[j].pl.Nv * (double)h_rec[j].coarse_evals;
         for (auto& pt : ctx->pending)
-            if (pt.coarse_evals) {
+            if (pt.coarse_evals && pt.batch == F.id) {
                 pt.algo_bytes = coarse_bytes;
                 pt.coarse_evals = false;
             }
-        ctx->harvest();
+        ctx->harvest_upto(F.id);
     }
+    const long long saved_batch = ctx->timing_batch;
+    ctx->timing_batch = F.id;   // reruns' timings belong to this batch
 
     for (int j = 0; j < n; ++j) {
         HostRecord rec(h_rec[j], gens[j]);
@@ -3342,7 +3398,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
             LGS_HIP_CHECK(hipMemcpyAsync(&h_rec[j], d_rec + j, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                          ctx->stream));
             ctx->sync();
-            if (ctx->profile) ctx->harvest();
+            if (ctx->profile) ctx->harvest_upto(F.id);
             rec = HostRecord(h_rec[j], g);
             if (opt.patches || opt.host_idx) rec.guard_count = 0;  // already exact
         }
@@ -3355,7 +3411,20 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
         ctx->count_coarse_blocks_dense += items[j].pl.K;
         ctx->count_pruned += pruned ? 1 : 0;
     }
+    ctx->timing_batch = saved_batch;
+    ctx->bank = 0;
 }
+
+void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
+                 const lgs_grid* const* grids, lgs_scan* const* scans, const lgs_pose2d* init, int n,
+                 double nthr, std::vector<PlaneSet>& sets, const int* set_of, lgs_rtcsm_summary* out)
+{
+    InFlight F;
+    ctx->bank = 0;
+    launch_matches(ctx, params, cost, grids, scans, init, n, nthr, sets, set_of, out, F);
+    finish_matches(ctx, F);
+}
+
 
 // Batches of at most kMaxBatch items (bounded scratch: ~20 MB per config-2
 // item), each with only the coarse maps its items reference.
@@ -3364,20 +3433,46 @@ void run_chunked(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
                  const lgs_grid* const* grids, lgs_scan* const* scans, const lgs_pose2d* init, int n,
                  double nthr, const std::vector<PlaneSet>& sets_all, const int* set_of, lgs_rtcsm_summary* out)
 {
-    for (int j0 = 0; j0 < n; j0 += kMaxBatch) {
-        const int m = std::min(kMaxBatch, n - j0);
-        std::vector<PlaneSet> sets;
-        std::vector<int> so((size_t)m), remap(sets_all.size(), -1);
-        for (int k = 0; k < m; ++k) {
-            const int s = set_of[j0 + k];
-            if (remap[s] < 0) {
-                remap[s] = (int)sets.size();
-                sets.push_back(sets_all[s]);
+    // two chunks in flight: chunk c + 1 is launched (on the other bank)
+    // before the host takes chunk c's results, so the device never waits for
+    // the host between chunks of one call
+    InFlight fl[2];
+    bool busy[2] = { false, false };
+    int c = 0;
+    try {
+        for (int j0 = 0; j0 < n; j0 += kMaxBatch, ++c) {
+            const int m = std::min(kMaxBatch, n - j0);
+            std::vector<PlaneSet> sets;
+            std::vector<int> so((size_t)m), remap(sets_all.size(), -1);
+            for (int k = 0; k < m; ++k) {
+                const int s = set_of[j0 + k];
+                if (remap[s] < 0) {
+                    remap[s] = (int)sets.size();
+                    sets.push_back(sets_all[s]);
+                }
+                so[k] = remap[s];
             }
-            so[k] = remap[s];
+            const int b = c & 1;
+            ctx->bank = b;
+            fl[b] = InFlight{};
+            launch_matches(ctx, params, cost, grids + j0, scans + j0, init + j0, m, nthr, sets, so.data(), out + j0,
+                           fl[b]);
+            busy[b] = true;
+            if (busy[b ^ 1]) {
+                finish_matches(ctx, fl[b ^ 1]);
+                busy[b ^ 1] = false;
+            }
         }
-        run_matches(ctx, params, cost, grids + j0, scans + j0, init + j0, m, nthr, sets, so.data(), out + j0);
+        const int last = (c - 1) & 1;
+        if (busy[last]) {
+            finish_matches(ctx, fl[last]);
+            busy[last] = false;
+        }
+    } catch (...) {
+        ctx->bank = 0;
+        throw;
     }
+    ctx->bank = 0;
 }
 
 }  // namespace
@@ -3796,19 +3891,64 @@ namespace {
 
 // A copy of `src` (any device) owned by ctx: peer copy over xGMI, or a plain
 // device copy when both live on the same GPU.
+// Peer access from ctx's device to `peer` (hipDeviceEnablePeerAccess once per
+// pair and process): true when direct device-to-device copies may be used.
+bool peer_access(int dev, int peer)
+{
+    if (dev == peer) return true;
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, bool> known;
+    std::lock_guard<std::mutex> lock(mu);
+    const auto key = std::make_pair(dev, peer);
+    auto it = known.find(key);
+    if (it != known.end()) return it->second;
+    int can = 0;
+    bool ok = hipDeviceCanAccessPeer(&can, dev, peer) == hipSuccess && can;
+    if (ok) {
+        int cur = 0;
+        hipGetDevice(&cur);
+        hipSetDevice(dev);
+        const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+        ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+        (void)hipGetLastError();
+        hipSetDevice(cur);
+    }
+    known[key] = ok;
+    return ok;
+}
+
+// A copy of another context's map on ctx: device to device (one device, or
+// peer access over xGMI), else -- or with LGS_OPT_PEER_COPY -- staged
+// through pinned host memory.  The source's pending writer is waited for.
 lgs_grid* clone_grid(lgs_ctx* ctx, const lgs_grid* src)
 {
     lgs_grid* g = nullptr;
     const int rc = lgs_grid_create(ctx, src->w, src->h, src->min_x, src->min_y, src->res, &g);
     if (rc != LGS_OK) throw Error(rc, ctx->last_error);
     const size_t bytes = sizeof(double) * (size_t)src->w * (size_t)src->h;
-    if (bytes) {
-        const hipError_t e = hipMemcpyPeerAsync(g->d, ctx->device, src->d, src->device, bytes, ctx->stream);
-        if (e == hipSuccess) ctx->sync();
-        if (e != hipSuccess) {
-            lgs_grid_destroy(g);
-            throw Error(LGS_ERR_HIP, std::string("hipMemcpyPeerAsync: ") + hipGetErrorString(e));
+    try {
+        if (bytes) {
+            if (src->writer) LGS_HIP_CHECK(hipEventSynchronize(src->writer->ev));
+            if (!ctx->peer_staged && peer_access(ctx->device, src->device)) {
+                LGS_HIP_CHECK(hipMemcpyPeerAsync(g->d, ctx->device, src->d, src->device, bytes, ctx->stream));
+                ctx->sync();
+                ++ctx->copies_direct;
+            } else {
+                // one bounce buffer: device -> host on the source's device,
+                // host -> device on ctx's
+                void* pin = nullptr;
+                LGS_HIP_CHECK(hipHostMalloc(&pin, bytes));
+                hipError_t e = hipMemcpy(pin, src->d, bytes, hipMemcpyDeviceToHost);
+                if (e == hipSuccess) e = hipMemcpyAsync(g->d, pin, bytes, hipMemcpyHostToDevice, ctx->stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+                hipHostFree(pin);
+                LGS_HIP_CHECK(e);
+                ++ctx->copies_staged;
+            }
         }
+    } catch (...) {
+        lgs_grid_destroy(g);
+        throw;
     }
     return g;
 }
@@ -3949,4 +4089,12 @@ extern "C" int lgs_loop_detect_rtcsm_multi(lgs_ctx* const* ctxs, int num_ctx, co
         // a result's start_node_index etc. come from its query, which each
         // shard saw clipped but unchanged: nothing to remap
     });
+}
+
+extern "C" int lgs_debug_copy_counters(const lgs_ctx* ctx, long long* direct, long long* staged)
+{
+    if (!ctx || !direct || !staged) return LGS_ERR_INVALID_ARG;
+    *direct = ctx->copies_direct;
+    *staged = ctx->copies_staged;
+    return LGS_OK;
 }

@@ -262,18 +262,40 @@ __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target)
     __syncthreads();
 }
 
-template <int KPT>
+// exclusive prefix over the block of one value per thread (thread order);
+// *total receives the block sum
+__device__ __forceinline__ unsigned block_excl(unsigned v, unsigned* wsum4, unsigned* total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    __syncthreads();
+    if (lane == 63) wsum4[w] = incl;
+    __syncthreads();
+    unsigned wo = 0;
+    for (int q = 0; q < w; ++q) wo += wsum4[q];
+    if (total) *total = wsum4[0] + wsum4[1] + wsum4[2] + wsum4[3];
+    return wo + incl - v;
+}
+
+template <int KPT, int RB>
 __global__ __launch_bounds__(kSortThreads) void k_sort_coop(const unsigned* __restrict__ in, unsigned* __restrict__ out,
                                                             unsigned* __restrict__ tmp, long long n, int lo,
                                                             int dbits, int bits, int passes,
                                                             unsigned* __restrict__ counts, unsigned* __restrict__ bar)
 {
     constexpr int TILE = kSortThreads * KPT;
+    constexpr int R = 1 << RB;
+    constexpr int Q = R / kSortThreads;   // consecutive digits per thread
+    static_assert(Q >= 1 && Q * kSortThreads == R, "digits per thread");
     __shared__ unsigned keys_s[TILE];
-    __shared__ unsigned wcnt[4][kSortRadix];
-    __shared__ unsigned dstart[kSortRadix];
-    __shared__ unsigned gbase[kSortRadix];
-    __shared__ unsigned wsum[4], dsum[4];
+    __shared__ unsigned wcnt[4][R];
+    __shared__ unsigned dstart[R];
+    __shared__ unsigned gbase[R];
+    __shared__ unsigned ws4[4];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const unsigned ntiles = gridDim.x, tile = blockIdx.x;
     const long long t0 = (long long)tile * TILE;
@@ -286,7 +308,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_coop(const unsigned* __re
         const int shift = lo + p * dbits;
         const int nb = min(dbits, bits - p * dbits);
         const unsigned mask = (1u << nb) - 1u;
-        wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+        for (int d = tid; d < R; d += kSortThreads) wcnt[0][d] = wcnt[1][d] = wcnt[2][d] = wcnt[3][d] = 0;
         __syncthreads();
         unsigned k[KPT], rank[KPT];
 #pragma unroll
@@ -309,47 +331,60 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_coop(const unsigned* __re
             if (valid && !(peers & lt)) wcnt[w][d] = base + (unsigned)__popcll(peers);
         }
         __syncthreads();
-        const int d = tid;
-        const unsigned c0 = wcnt[0][d], c1 = wcnt[1][d], c2 = wcnt[2][d], c3 = wcnt[3][d];
-        const unsigned tot = c0 + c1 + c2 + c3;
-        wcnt[0][d] = 0;
-        wcnt[1][d] = c0;
-        wcnt[2][d] = c0 + c1;
-        wcnt[3][d] = c0 + c1 + c2;
-        unsigned* cp = counts + (size_t)p * ntiles * kSortRadix;
-        cp[(size_t)tile * kSortRadix + d] = tot;
-        unsigned incl = tot;
-        for (int o = 1; o < 64; o <<= 1) {
-            const unsigned t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
+        // this thread's digits [tid * Q, tid * Q + Q): tile counts, the
+        // exclusive prefix over the waves, publication
+        unsigned* cp = counts + (size_t)p * ntiles * R;
+        unsigned tot[Q], tsum = 0;
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            const int d = tid * Q + j;
+            const unsigned c0 = wcnt[0][d], c1 = wcnt[1][d], c2 = wcnt[2][d], c3 = wcnt[3][d];
+            tot[j] = c0 + c1 + c2 + c3;
+            wcnt[0][d] = 0;
+            wcnt[1][d] = c0;
+            wcnt[2][d] = c0 + c1;
+            wcnt[3][d] = c0 + c1 + c2;
+            cp[(size_t)tile * R + d] = tot[j];
+            tsum += tot[j];
         }
-        if (lane == 63) wsum[w] = incl;
-        grid_barrier(bar, ++nbar * ntiles);
-        // digit d: its total over all tiles and the count of the tiles before this one
-        // (16 loads in flight per round: the rows were written on other XCDs)
-        unsigned all = 0, before = 0;
-        for (unsigned t0c = 0; t0c < ntiles; t0c += 16) {
-            unsigned c[16];
+        {
+            unsigned run = block_excl(tsum, ws4, nullptr);
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                c[q] = (t0c + q < ntiles) ? cp[(size_t)(t0c + q) * kSortRadix + d] : 0u;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                all += c[q];
-                before += (t0c + q < tile) ? c[q] : 0u;
+            for (int j = 0; j < Q; ++j) {
+                dstart[tid * Q + j] = run;
+                run += tot[j];
             }
         }
-        unsigned ai = all;
-        for (int o = 1; o < 64; o <<= 1) {
-            const unsigned t = __shfl_up(ai, o);
-            if (lane >= o) ai += t;
+        grid_barrier(bar, ++nbar * ntiles);
+        // each digit's total over all tiles and the count of the tiles before
+        // this one (16 loads in flight per round: written on other XCDs)
+        unsigned all[Q], before[Q], asum = 0;
+#pragma unroll
+        for (int j = 0; j < Q; ++j) all[j] = before[j] = 0;
+        for (unsigned tc = 0; tc < ntiles; tc += 16) {
+#pragma unroll
+            for (int j = 0; j < Q; ++j) {
+                unsigned c[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    c[q] = (tc + q < ntiles) ? cp[(size_t)(tc + q) * R + tid * Q + j] : 0u;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    all[j] += c[q];
+                    before[j] += (tc + q < tile) ? c[q] : 0u;
+                }
+            }
         }
-        if (lane == 63) dsum[w] = ai;
-        __syncthreads();
-        unsigned wo = 0, dwo = 0;
-        for (int q = 0; q < w; ++q) wo += wsum[q], dwo += dsum[q];
-        dstart[d] = wo + incl - tot;
-        gbase[d] = dwo + ai - all + before;
+#pragma unroll
+        for (int j = 0; j < Q; ++j) asum += all[j];
+        {
+            unsigned run = block_excl(asum, ws4, nullptr);
+#pragma unroll
+            for (int j = 0; j < Q; ++j) {
+                gbase[tid * Q + j] = run + before[j];
+                run += all[j];
+            }
+        }
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < KPT; ++i)
@@ -388,7 +423,7 @@ long long coop_capacity(lgs_ctx* ctx)
     if (dev < 0 || dev >= 64) return 0;
     if (!cap[dev]) {
         int per_cu = 0, cus = 0;
-        LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_coop<16>, kSortThreads, 0));
+        LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_coop<16, 8>, kSortThreads, 0));
         LGS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         cap[dev] = std::max(1LL, (long long)per_cu * cus / 2);
     }
@@ -412,13 +447,17 @@ void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, lon
     const bool fresh = ctx->buf[S_RAY0] == nullptr;
     unsigned* ctl = (unsigned*)ctx->ensure(S_RAY0, sizeof(unsigned) * kCtlWords);
     if (fresh) LGS_HIP_CHECK(hipMemsetAsync(ctl, 0, sizeof(unsigned) * kCtlWords, st));
-    // one launch when every tile can be resident at once (measured per device)
+    // one launch when every tile can be resident at once (measured per
+    // device).  (10-bit digits -- 2 passes for the latest map's 20 cell bits
+    // instead of 3 -- measured slower: 52.7 vs 46.1 us per config-4 step;
+    // the per-pass cost is the barriers and the count reads, which grow with
+    // the radix.)
     constexpr int kCoopTile = kSortThreads * 16;
     const long long ctiles = (n + kCoopTile - 1) / kCoopTile;
     if (ctiles <= coop_capacity(ctx) && (passes == 1 || tmp)) {
         unsigned* counts = (unsigned*)ctx->ensure(S_RAY1, sizeof(unsigned) * (size_t)ctiles * kSortRadix * passes);
-        hipLaunchKernelGGL(k_sort_coop<16>, dim3((unsigned)ctiles), dim3(kSortThreads), 0, st, in, out, tmp, n, lo,
-                           dbits, bits, passes, counts, ctl + kCtlBar);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_coop<16, 8>), dim3((unsigned)ctiles), dim3(kSortThreads), 0, st, in,
+                           out, tmp, n, lo, dbits, bits, passes, counts, ctl + kCtlBar);
         LGS_HIP_CHECK(hipGetLastError());
         return;
     }

@@ -91,19 +91,32 @@ void* lgs_ctx::ensure_pinned_in(size_t bytes)
     return pinned_in;
 }
 
-void* lgs_ctx::ensure_pinned_up(size_t bytes)
+namespace {
+void* grow_pinned(hipStream_t stream, void*& p, size_t& have, size_t bytes)
 {
-    if (pinned_up_bytes >= bytes) return pinned_up;
-    if (pinned_up) {
+    if (have >= bytes) return p;
+    if (p) {
         LGS_HIP_CHECK(hipStreamSynchronize(stream));
-        LGS_HIP_CHECK(hipHostFree(pinned_up));
-        pinned_up = nullptr;
-        pinned_up_bytes = 0;
+        LGS_HIP_CHECK(hipHostFree(p));
+        p = nullptr;
+        have = 0;
     }
     size_t want = bytes + bytes / 4;
-    LGS_HIP_CHECK(hipHostMalloc(&pinned_up, want, hipHostMallocDefault));
-    pinned_up_bytes = want;
-    return pinned_up;
+    LGS_HIP_CHECK(hipHostMalloc(&p, want, hipHostMallocDefault));
+    have = want;
+    return p;
+}
+}  // namespace
+
+void* lgs_ctx::ensure_pinned_up(size_t bytes)
+{
+    return bank ? grow_pinned(stream, pinned_up_b, pinned_up_b_bytes, bytes)
+                : grow_pinned(stream, pinned_up, pinned_up_bytes, bytes);
+}
+
+void* lgs_ctx::ensure_pinned_rec(size_t bytes)
+{
+    return grow_pinned(stream, pinned_rec[bank], pinned_rec_bytes[bank], bytes);
 }
 
 namespace lgs {
@@ -150,7 +163,9 @@ int lgs_ctx::timing_begin(int kernel, double algo_bytes)
         }
     }
     LGS_HIP_CHECK(hipEventRecord(ev[0], stream));
-    pending.push_back({ kernel, ev[0], ev[1], algo_bytes });
+    PendingTiming t{ kernel, ev[0], ev[1], algo_bytes };
+    t.batch = timing_batch;
+    pending.push_back(t);
     return (int)pending.size() - 1;
 }
 
@@ -173,6 +188,36 @@ void lgs_ctx::harvest()
         event_pool.push_back(p.b);
     }
     pending.clear();
+}
+
+void lgs_ctx::harvest_upto(long long b)
+{
+    size_t k = 0;
+    for (; k < pending.size() && pending[k].batch <= b; ++k) {
+        PendingTiming& p = pending[k];
+        float ms = 0.f;
+        LGS_HIP_CHECK(hipEventSynchronize(p.b));
+        LGS_HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+        stat_launches[p.kernel] += 1;
+        stat_ms[p.kernel] += ms;
+        stat_bytes[p.kernel] += p.algo_bytes;
+        event_pool.push_back(p.a);
+        event_pool.push_back(p.b);
+    }
+    pending.erase(pending.begin(), pending.begin() + (long)k);
+}
+
+void lgs_ctx::wait_event(hipEvent_t ev)
+{
+    if (!spin_sync) {
+        LGS_HIP_CHECK(hipEventSynchronize(ev));
+        return;
+    }
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) LGS_HIP_CHECK(e);
+    }
 }
 
 void lgs_ctx::release()
@@ -198,10 +243,20 @@ void lgs_ctx::release()
     pending.clear();
     for (auto e : event_pool) hipEventDestroy(e);
     event_pool.clear();
+    for (auto& e : bank_ev) {
+        if (e) hipEventDestroy(e);
+        e = nullptr;
+    }
     if (pinned_up) hipHostFree(pinned_up);
     pinned_up = nullptr;
     if (pinned_in) hipHostFree(pinned_in);
     pinned_in = nullptr;
+    if (pinned_up_b) hipHostFree(pinned_up_b);
+    pinned_up_b = nullptr;
+    for (int b = 0; b < 2; ++b) {
+        if (pinned_rec[b]) hipHostFree(pinned_rec[b]);
+        pinned_rec[b] = nullptr;
+    }
     if (stream) hipStreamDestroy(stream);
     stream = nullptr;
 }
@@ -322,6 +377,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
         return LGS_OK;
     case LGS_OPT_SKIP_MASK: ctx->skip_mask = (unsigned)value; return LGS_OK;
     case LGS_OPT_POISON_WS: ctx->poison_ws = value != 0.0; return LGS_OK;
+    case LGS_OPT_PEER_COPY: ctx->peer_staged = value != 0.0; return LGS_OK;
     case LGS_OPT_LINSOLVE_SPLIT: ctx->linsolve_split = value != 0.0; return LGS_OK;
     case LGS_OPT_HANDOFF_SPIN_US:
         if (value < 0.0) return LGS_ERR_INVALID_ARG;

@@ -76,6 +76,10 @@ enum Slot {
     S_NEGFLAG,      // int per coarse-map set: negative-cell stamp of its planes
     S_BB0, S_BB1, S_BB2, S_BB3, S_BB4, S_BB5,   // branch-and-bound (k_bb.hip)
     S_PRECOMP_TMP,  // double [W*H]: pass-1 result of the large-window precompute
+    // bank 1 of the per-batch buffers: a batched call keeps two 64-query
+    // chunks in flight (the next chunk's launches go out before the host
+    // finishes the previous one), each in its own bank (lgs_ctx::banked)
+    S_BATCH_WS_B, S_RECORDS_B, S_UPLOAD_B, S_DECIM_B, S_SUPER_B, S_NEGFLAG_B,
     S_NUM_SLOTS
 };
 
@@ -194,6 +198,7 @@ struct PendingTiming {
     // pruned k_coarse: algo_bytes is set from the batch's records (blocks
     // actually scored x 8 B x Nv) once their host copy is known
     bool coarse_evals = false;
+    long long batch = 0;   // lgs_ctx::timing_batch when launched
 };
 }  // namespace lgs
 
@@ -210,6 +215,8 @@ struct lgs_ctx {
     bool linsolve_split = true;  // lone refine over one workgroup per 64 beams (LGS_OPT_LINSOLVE_SPLIT)
     long long handoff_spin_us = 200000;   // split refine spin bound (LGS_OPT_HANDOFF_SPIN_US; 0 = force the fallback)
     long long handoff_fallbacks = 0;      // split refines rerun on one workgroup after a time-out
+    bool peer_staged = false;    // cross-context copies through host memory (LGS_OPT_PEER_COPY)
+    long long copies_direct = 0, copies_staged = 0;   // lgs_debug_copy_counters
     int lanes_min_batch = 2;     // pruned coarse stage: k_coarse_lanes from this batch size on (LGS_OPT_LANES_MIN_BATCH)
     long long ray_chunk_keys = 1LL << 28;  // ray-cast keys per emit/sort/apply pass (LGS_OPT_RAY_CHUNK_KEYS)
     // Stamps come from one process-wide counter: a context's scratch may be
@@ -237,14 +244,34 @@ struct lgs_ctx {
     size_t pinned_bytes = 0;
     void* pinned_up = nullptr;   // staging of the per-batch descriptor upload
     size_t pinned_up_bytes = 0;
+    // bank 1 (two chunks in flight): descriptor staging and record copies
+    void* pinned_up_b = nullptr;
+    size_t pinned_up_b_bytes = 0;
+    void* pinned_rec[2] = {};
+    size_t pinned_rec_bytes[2] = {};
+    int bank = 0;                // which bank the per-batch buffers come from
+    int banked(int slot) const
+    {
+        if (!bank) return slot;
+        switch (slot) {
+        case lgs::S_BATCH_WS: return lgs::S_BATCH_WS_B;
+        case lgs::S_RECORDS: return lgs::S_RECORDS_B;
+        case lgs::S_UPLOAD: return lgs::S_UPLOAD_B;
+        case lgs::S_DECIM: return lgs::S_DECIM_B;
+        case lgs::S_SUPER: return lgs::S_SUPER_B;
+        case lgs::S_NEGFLAG: return lgs::S_NEGFLAG_B;
+        default: return slot;
+        }
+    }
+    void* ensure_pinned_rec(size_t bytes);   // per bank: a batch's record copies
     void* pinned_in = nullptr;   // staging of lgs_grid_upload_patches
     size_t pinned_in_bytes = 0;
-    // padded phase-plane buffer: margins zeroed once per (buffer, layout, set count)
-    void* planes_ptr = nullptr;
-    int planes_sets = 0;
-    void* super_ptr = nullptr;   // superblock planes zeroed with them (k_planes_fused leaves far margins)
-    int super_sets = 0;
-    long long planes_key[4] = { -1, -1, -1, -1 };
+    // padded phase-plane buffer (per bank): margins zeroed once per (buffer, layout, set count)
+    void* planes_ptr[2] = {};
+    int planes_sets[2] = {};
+    void* super_ptr[2] = {};   // superblock planes zeroed with them
+    int super_sets[2] = {};
+    long long planes_key[2][4] = { { -1, -1, -1, -1 }, { -1, -1, -1, -1 } };
     double* zero = nullptr;      // 32 zero doubles: target of out-of-map gathers
     // profiling (LGS_OPT_PROFILE)
     bool profile = false;
@@ -262,6 +289,12 @@ struct lgs_ctx {
     int timing_begin(int kernel, double algo_bytes);
     void timing_end(int token);
     void harvest();
+    // timings of the launches tagged with batch <= b only (the next chunk's
+    // may still be running)
+    void harvest_upto(long long b);
+    long long timing_batch = 0;
+    hipEvent_t bank_ev[2] = {};   // end of each bank's chunk (its record copy)
+    void wait_event(hipEvent_t ev);   // spin or block, as sync()
 
     // wait for the stream: spin on hipStreamQuery (default; the host thread
     // wakes within ~1 us instead of the blocking wait's interrupt latency) or
@@ -395,7 +428,7 @@ struct Upload {
     // the host-to-device copy; flush() = both.
     char* prepare()
     {
-        dev = (char*)ctx->ensure(S_UPLOAD, std::max<size_t>(host.size(), 16));
+        dev = (char*)ctx->ensure(ctx->banked(S_UPLOAD), std::max<size_t>(host.size(), 16));
         return dev;
     }
     void copy()

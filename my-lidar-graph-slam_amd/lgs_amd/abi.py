@@ -30,6 +30,7 @@ LGS_OPT_POISON_WS = 15   # diagnostics only
 LGS_OPT_SKIP_MASK = 10   # diagnostics only
 LGS_OPT_LINSOLVE_SPLIT = 17
 LGS_OPT_HANDOFF_SPIN_US = 18
+LGS_OPT_PEER_COPY = 19
 KERNEL_IDS = ["k_project", "k_coarse", "k_seed", "k_select", "k_fine", "k_replay", "k_cost", "k_precompute",
               "k_linsolve", "k_ray_emit", "k_ray_apply", "k_super", "k_super_planes", "k_bb_score",
               "k_bb_expand"]   # lgs_ctx_kernel_stats order
@@ -246,6 +247,7 @@ _PROTOS = [
                                         C.POINTER(C.c_double)]),
     ("lgs_debug_keysort", C.c_int, [_P, _P, _P, C.c_longlong, C.c_int, C.c_int]),
     ("lgs_debug_map_rebuilds", C.c_int, [_P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
+    ("lgs_debug_copy_counters", C.c_int, [_P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     ("lgs_debug_item_buffer", C.c_int, [_P, C.c_int, C.c_int, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("lgs_debug_libm", C.c_int, [_P, C.c_int, _P, C.c_int, _P]),
 ]
@@ -592,6 +594,13 @@ class Context:
         self.check(self.lib.lgs_debug_libm(self.h, op, x.ctypes.data_as(_P), len(x), out.ctypes.data_as(_P)),
                    "debug_libm")
         return out
+
+    def copy_counters(self) -> dict:
+        """Diagnostics: cross-context map copies made onto this context by
+        lgs_loop_detect_rtcsm_multi (lgs_debug_copy_counters)."""
+        a, b = C.c_longlong(), C.c_longlong()
+        self.check(self.lib.lgs_debug_copy_counters(self.h, C.byref(a), C.byref(b)), "debug_copy_counters")
+        return {"direct": a.value, "staged": b.value}
 
     def debug_keysort(self, keys, lo: int, bits: int) -> np.ndarray:
         """Diagnostics: the K3 stable radix sort (csrc/k_sort.hip) of host u32

@@ -123,6 +123,13 @@ def test_loop_detect_multi_context_identical(ctx, n_shards):
     try:
         multi = bytes(ctx.loop_detect(p, c, small.THR, qs, cl, shards=others))
         again = bytes(ctx.loop_detect(p, c, small.THR, qs, cl, shards=others))
+        direct = [o.copy_counters() for o in others]
+        # the fallback for devices without peer access: maps staged through
+        # pinned host memory (forced here, on one device)
+        for o in others:
+            o.set_option(abi.LGS_OPT_PEER_COPY, 1)
+        staged = bytes(ctx.loop_detect(p, c, small.THR, qs, cl, shards=others))
+        after = [o.copy_counters() for o in others]
         with pytest.raises(abi.LgsError):   # the single-context contract holds (:21-22)
             ctx.loop_detect(p, c, 1.5, qs, cl, shards=others)
     finally:
@@ -130,6 +137,9 @@ def test_loop_detect_multi_context_identical(ctx, n_shards):
             o.close()
     assert multi == one
     assert again == one
+    assert staged == one
+    assert all(d["direct"] > 0 and d["staged"] == 0 for d in direct), direct
+    assert all(a["staged"] > 0 and a["direct"] == d["direct"] for a, d in zip(after, direct)), (after, direct)
     assert len(cands) >= n_shards
 
 

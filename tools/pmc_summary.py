@@ -3,7 +3,7 @@
 
     python tools/pmc_summary.py <trace_dir> <pmc_fetch_dir> <pmc_write_dir> <pmc_l2_dir> <out_prefix>
 
-    [<liblgs_hip.so profiled>]
+    [<liblgs_hip.so profiled>]   (env WORKLOAD: the bench workload profiled, default "match")
 
 Writes <out_prefix>_kernel_stats.md (kernel-trace durations) and
 <out_prefix>_pmc.json = {"lib_sha256": the profiled library's hash, "kernels":
@@ -82,6 +82,7 @@ def main():
         out[k] = e
     import hashlib
     doc = {"lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+           "workload": os.environ.get("WORKLOAD", "match"),
            "note": "rocprofv3 FETCH_SIZE / WRITE_SIZE (separate --pmc passes) per dispatch; gfx950 FETCH_SIZE counts "
                    "half the bytes of wide coalesced reads (MI355X_MICROARCH.md HBM section): bench.py doubles it",
            "kernels": out}
