@@ -65,9 +65,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="match workload: concurrent HIP streams (lgs contexts) per GPU, one host thread each")
     ap.add_argument("--batch", type=int, default=128,
-                    help="match workload: queries per call (lgs_rtcsm_optimize_pose_query_batch, which launches "
-                         "64-query chunks back to back; 1 = one lgs_rtcsm_optimize_pose_query call per scan). "
-                         "128 per call: 45.1k vs 41.6k scans/s for 64 (one host synchronisation per two chunks)")
+                    help="match workload: queries per call (lgs_rtcsm_optimize_pose_query_batch runs them as "
+                         "64-query chunks, two in flight; 1 = one lgs_rtcsm_optimize_pose_query call per scan)")
     ap.add_argument("--lanes-min-batch", type=int, default=None,
                     help="A/B: LGS_OPT_LANES_MIN_BATCH (pruned coarse stage kernel choice by batch size)")
     ap.add_argument("--latency-calls", type=int, default=100,
@@ -87,7 +86,7 @@ def parse():
     ap.add_argument("--window", default="json", choices=sorted(STREAM_WINDOWS),
                     help="stream workload: search window (json = the launcher's frontend 0.2 m/0.2 m/0.5 rad, "
                          "config2 = +-2 m/+-30 deg)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_pmc_summary.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"),
                     help="rocprofv3 PMC summary (tools/pmc_summary.py) of THIS library build: roofline.traffic "
                          "is taken from it only when its lib_sha256 matches liblgs_hip.so, else null")
     ap.add_argument("--loop-line", type=int, default=1,
@@ -462,7 +461,8 @@ def run_match(args, D, ctx):
         lat1.append(time.perf_counter() - ts)
     c0.set_option(abi.LGS_OPT_PROFILE, 1)
     c0.reset_stats()
-    for k in range(min(max(1, 50 // B), args.steps)):
+    iso_calls = min(max(1, 1024 // B), args.steps)   # ~16 coarse launches
+    for k in range(iso_calls):
         call(c0, g0, ds0, args.warmup + k)
     all_stats = c0.kernel_stats()
     c0.set_option(abi.LGS_OPT_PROFILE, 0)
@@ -510,12 +510,16 @@ def run_match(args, D, ctx):
         p90_scan_match_ms=round(1e3 * float(np.percentile(lat1, 90)), 4) if lat1 else None,
         # latency of one batched call under the timed load
         p50_batch_call_ms=round(float(np.percentile(lat_ms, 50)), 4),
-        roofline=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_lanes", "l2-gather"), cpu_baseline=cpu,
-        # the same kernel timed alone (the one-stream, fully event-timed pass
-        # after the timed region): in the timed region each launch shares the
-        # GPU with the other streams' kernels, and its duration varies with how
-        # the streams' batches overlap (0.45-0.62 ms measured for 2 streams)
-        roofline_isolated=roofline_from(all_stats, "k_coarse", args.pmc, "k_coarse_lanes", "l2-gather"),
+        # the dominant kernel timed alone: the one-stream, event-timed pass
+        # after the timed region.  In the timed region each
+        # launch shares the GPU with the other stream's kernels and its
+        # duration depends on how the streams' batches happen to overlap
+        # (0.45-0.60 ms per launch over runs of one build): that figure is
+        # roofline_timed_region.  tools/trace_coarse.py splits a kernel trace
+        # of this command the same way (dispatches overlapping no other vs
+        # the rest).
+        roofline=roofline_from(all_stats, "k_coarse", args.pmc, "k_coarse_lanes", "l2-gather"), cpu_baseline=cpu,
+        roofline_timed_region=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_lanes", "l2-gather"),
         pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events,
         super_prune=bool(args.super_prune),
         coarse_blocks_scored_mean=round(float(results[:, 4].mean()), 1),
