@@ -14,11 +14,11 @@ mkdir -p $OUT
 STEPS=${STEPS:-200} bash tools/gpu_prof.sh $TAG || exit $?
 WORKLOAD=match python3 tools/pmc_summary.py $OUT/trace_$TAG $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG $OUT/pmc_l2_$TAG $OUT/$TAG > $OUT/${TAG}_summary.log 2>&1 || exit $?
 cp $OUT/${TAG}_pmc.json profiles/pmc_summary.json
-ALGO=$(python3 -c "import json;print(json.loads(open('$OUT/trace_$TAG.log').read().strip().splitlines()[-1])['roofline']['algo_bytes_per_launch'])") || exit 1
+grep '^{' $OUT/trace_$TAG.log | tail -n 1 > $OUT/${TAG}_trace_run_bench.json
+ALGO=$(python3 -c "import json;print(json.loads(open('$OUT/${TAG}_trace_run_bench.json').read())['roofline']['algo_bytes_per_launch'])") || exit 1
 TR=$(find $OUT/trace_$TAG -name '*kernel_trace.csv' | head -1)
 python3 tools/trace_coarse.py $TR k_coarse_lanes $ALGO > $OUT/${TAG}_coarse_split.json || exit 1
 cat $OUT/${TAG}_coarse_split.json
-tail -n 1 $OUT/trace_$TAG.log > $OUT/${TAG}_trace_run_bench.json
 find $OUT/trace_$TAG -name '*kernel_stats.csv' -exec cp {} $OUT/${TAG}_run_kernel_stats.csv \;
 rm -rf $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG $OUT/pmc_l2_$TAG $OUT/trace_$TAG
 timeout -k 10 600 python -u bench.py > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err || exit $?
