@@ -83,6 +83,8 @@ def parse():
                          "the insert + the latest-map rebuild (0)")
     ap.add_argument("--driver", default="cpp", choices=["cpp", "py"],
                     help="stream workload: the frontend loop in C++ over the adapter (default) or in Python")
+    ap.add_argument("--ctx-option", type=lambda v: (int(v.split("=")[0]), float(v.split("=")[1])), default=None,
+                    help="stream workload (C++ driver), A/B: ID=VALUE, one lgs_ctx option on the device context")
     ap.add_argument("--window", default="json", choices=sorted(STREAM_WINDOWS),
                     help="stream workload: search window (json = the launcher's frontend 0.2 m/0.2 m/0.5 rad, "
                          "config2 = +-2 m/+-30 deg)")
@@ -256,7 +258,8 @@ class FbIn(C.Structure):
                 ("low_res", C.c_int),
                 ("range_x", C.c_double), ("range_y", C.c_double), ("range_theta", C.c_double),
                 ("scan_range_max", C.c_double), ("segs", C.POINTER(C.c_double)), ("angles", C.POINTER(C.c_double)),
-                ("truths", C.POINTER(C.c_double)), ("odo", C.POINTER(C.c_double)), ("n_dump", C.c_int)]
+                ("truths", C.POINTER(C.c_double)), ("odo", C.POINTER(C.c_double)), ("n_dump", C.c_int),
+                ("opt_id", C.c_int), ("opt_value", C.c_double)]
 
 
 class FbOut(C.Structure):
@@ -828,7 +831,7 @@ def run_stream_cpp(args, D, ctx):
     dump = np.zeros((n_dump, len(ang)))
     fin = FbIn(D.local, n, args.warmup, len(ang), len(segs), int(args.interp), 10, int(args.fused), 5, *win, 20.0,
                dptr(segs), dptr(ang),
-               dptr(truths), dptr(odo), n_dump)
+               dptr(truths), dptr(odo), n_dump, *(args.ctx_option or (0, 0.0)))
     fout = FbOut(dptr(est), dptr(guess), dptr(dump))
     D.barrier()
     rc = bench_drivers().lgs_frontend_bench(C.byref(fin), C.byref(fout))

@@ -170,6 +170,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_LINSOLVE_SPLIT 17 /* 1 (default) = a lone ScanMatcherLinearSolver refine of <= 1280 beams runs one workgroup per 64 beams (in-launch hand-off per pass) when they fit the device at once, 0 = one workgroup */
 #define LGS_OPT_HANDOFF_SPIN_US 18 /* split refine: bound of a workgroup's wait for the others (default 200000 us); on time-out the refine is rerun on one workgroup.  0 = force that fallback (tests) */
 #define LGS_OPT_PEER_COPY     19  /* lgs_loop_detect_rtcsm_multi, on the shard's ctx: 0 (default) = maps copied device to device (peer access enabled when the devices differ and allow it, else staged through pinned host memory), 1 = always staged through host memory */
+#define LGS_OPT_PRUNE_MIN_SUPER 21 /* superblock pruning only for windows of at least this many superblocks per angle (default 1); smaller windows score every coarse block */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

@@ -332,6 +332,7 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
 {
     for (int k = 0; k < n; ++k) grid_acquire(ctx, grids[k]);
     LGS_HIP_CHECK(hipSetDevice(ctx->device));
+    scans_to_device(ctx, scans, n);
     std::memset(out, 0, sizeof(lgs_rtcsm_summary) * (size_t)n);
     // LGS_BB_TIMING=1: per-phase host wall times on stderr (diagnostics)
     static const bool timing = std::getenv("LGS_BB_TIMING") != nullptr;

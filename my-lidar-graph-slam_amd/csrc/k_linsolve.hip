@@ -877,8 +877,9 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     const LsPlan p = make_ls_plan(grid, prm);
     const int iters = std::max(1, p.max_iter);
     std::vector<LsScanRef> refs(n);
+    for (int j = 0; j < n; ++j) LGS_REQUIRE(scans[j] && scans[j]->n >= 1, "empty scan");
+    scans_to_device(ctx, scans, n);
     for (int j = 0; j < n; ++j) {
-        LGS_REQUIRE(scans[j] && scans[j]->n >= 1, "empty scan");
         refs[j] = scan_ref(scans[j], init[j]);
     }
     // pinned staging: [refs | records | trajectory]
@@ -1030,6 +1031,7 @@ extern "C" int lgs_cost_square_error(lgs_ctx* ctx, const lgs_grid* grid, double 
         prm.cost_usable_range_min = umin;
         prm.cost_usable_range_max = umax;
         const LsPlan p = make_ls_plan(grid, &prm);
+        scan_to_device(ctx, scan);
         LsScanRef r = scan_ref(scan, { 0, 0, 0 });
         r.pose0[0] = sensor_pose.x;
         r.pose0[1] = sensor_pose.y;

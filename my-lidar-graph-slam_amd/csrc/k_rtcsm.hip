@@ -2535,13 +2535,13 @@ inline bool uses_super(const lgs_ctx* ctx, int nv_max, int nsb2, bool dense)
 {
     // k_coarse_rows: one ballot over an angle's superblocks, Nv <= 2048
     return !(dense || ctx->force_dense) && ctx->super_prune && nv_max <= kSeedMaxNv &&
-           nsb2 <= 64;
+           nsb2 <= 64 && nsb2 >= ctx->prune_min_super;
 }
 
 // Per-item workspace: one contiguous region per item carved from S_BATCH_WS
 // (sized for the batch's largest plan), field offsets below.
 struct ItemLayout {
-    size_t idx, cbase, cscore, cflag, list, segcnt, dlist, fval, fpos, part_c, part_k, tedge, sbound, poses7, cidx,
+    size_t idx, cbase, cscore, cflag, list, segcnt, dlist, fval, fpos, part_c, part_k, sbound, poses7, cidx,
         terms, count, total;
 };
 ItemLayout item_layout(int Tmax, int NvMax, int P, int nsb2, int chunks, int cb, int frows, int Nmax)
@@ -2568,7 +2568,6 @@ ItemLayout item_layout(int Tmax, int NvMax, int P, int nsb2, int chunks, int cb,
     L.fpos = take(sizeof(int) * K * frows);
     L.part_c = take(sizeof(double) * nparts);
     L.part_k = take(sizeof(long long) * nparts);
-    L.tedge = take(sizeof(int) * (size_t)Tmax);
     L.sbound = take(sizeof(double) * (size_t)Tmax * std::max(nsb2, 1));
     L.poses7 = take(sizeof(double) * 21);
     L.cidx = take(sizeof(int4) * 7 * (size_t)Nmax);
@@ -2590,7 +2589,6 @@ void bind_workspace(MatchItem& it, char* base, const ItemLayout& L, int frows)
     it.fpos = (int*)(base + L.fpos);
     it.part_c = (double*)(base + L.part_c);
     it.part_k = (long long*)(base + L.part_k);
-    it.tedge = (int*)(base + L.tedge);
     it.sbound = (double*)(base + L.sbound);
     it.poses7 = (double*)(base + L.poses7);
     it.cidx = (int4*)(base + L.cidx);
@@ -3232,20 +3230,22 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned_rec(sizeof(RtcsmRecord) * (size_t)n);
     F.id = ++ctx->timing_batch;
     // The angle flags are only ever SET (k_project stamps an angle whose lattice
-    // leaves the map low): clear every item's flags first.  (A generation stamp
-    // alone is not enough -- the workspace also holds ints of other layouts,
-    // e.g. a cost cell index equal to this match's stamp.)
+    // leaves the map low with the match's generation).  They live in a buffer
+    // of their own that holds nothing but stamps, so a stale flag can never
+    // equal this match's generation and no clearing is needed.
     if (ctx->poison_ws) {   // diagnostics: any read-before-write of this batch sees 0xFF bytes
         LGS_HIP_CHECK(hipMemsetAsync(ws, 0xFF, L.total * (size_t)n, ctx->stream));
         LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0xFF, sizeof(RtcsmRecord) * (size_t)n, ctx->stream));
     }
-    LGS_HIP_CHECK(hipMemset2DAsync(ws + L.tedge, L.total, 0, sizeof(int) * (size_t)B.Tmax, (size_t)n, ctx->stream));
+    int* tedge = ctx->tedge_buffer((size_t)n * B.Tmax);   // stamps only: no clearing per batch
+    scans_to_device(ctx, scans, n);
     Upload up(ctx);
     const SetJobs sj = build_sets(ctx, p0, sets, B.pruned, up);
     std::vector<int> gens((size_t)n);
     for (int j = 0; j < n; ++j) {
         MatchItem& it = items[j];
         bind_workspace(it, ws + L.total * (size_t)j, L, B.frows);
+        it.tedge = tedge + (size_t)j * B.Tmax;
         it.grid = grids[j]->d;
         it.ranges = scans[j]->d_ranges;
         it.angles = scans[j]->d_angles;
@@ -3389,7 +3389,6 @@ void finish_matches(lgs_ctx* ctx, InFlight& F)
             std::vector<MatchItem> one(1, items[j]);
             one[0].nparts = item_nparts(B1, one[0].pl, B1.pruned);
             const int g = one[0].gen = ctx->generation = ctx->next_stamp();
-            LGS_HIP_CHECK(hipMemsetAsync(one[0].tedge, 0, sizeof(int) * (size_t)one[0].pl.T, ctx->stream));
             if ((size_t)j < ctx->dbg.size()) ctx->dbg[j].gen = g;
             Upload u1(ctx);
             const size_t off = u1.append(one.data(), 1);
@@ -3499,6 +3498,7 @@ void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params
     std::vector<MatchItem> items((size_t)n);
     std::vector<double> P7((size_t)n * 21);
     std::vector<int> gens((size_t)n);
+    scans_to_device(ctx, scans, n);
     for (int j = 0; j < n; ++j) {
         MatchItem& it = items[j];
         std::memset(&it, 0, sizeof(it));
@@ -3701,19 +3701,20 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
         LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0, sizeof(RtcsmRecord), ctx->stream));
         std::vector<PlaneSet> sets(1);
         sets[0].coarse = coarse;
+        scan_to_device(ctx, s);
         Upload up(ctx);
         const SetJobs sj = build_sets(ctx, pl, sets, false, up);
         MatchItem it;
         std::memset(&it, 0, sizeof(it));
         it.pl = pl;
         bind_workspace(it, ws, L, 1);
+        it.tedge = ctx->tedge_buffer((size_t)pl.T);
         it.grid = grid->d;
         it.ranges = s->d_ranges;
         it.angles = s->d_angles;
         it.cmap = sets[0].cmap;
         it.gen = ctx->generation = ctx->next_stamp();
         it.rec = d_rec;
-        LGS_HIP_CHECK(hipMemsetAsync(it.tedge, 0, sizeof(int) * (size_t)pl.T, ctx->stream));
         const size_t off = up.append(&it, 1);
         up.flush();
         launch_sets(ctx, pl, sets, sj, up);
@@ -3751,6 +3752,7 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         grid_acquire(ctx, grid);
         const CostPlan cp = make_cost_plan(grid, cost, scan);
+        scan_to_device(ctx, scan);
         const ItemLayout L = item_layout(1, 1, 1, 1, 1, 64, 1, scan->n);
         char* ws = (char*)ctx->ensure(S_BATCH_WS, L.total);
         RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(S_RECORDS, sizeof(RtcsmRecord));

@@ -114,6 +114,17 @@ void* lgs_ctx::ensure_pinned_up(size_t bytes)
                 : grow_pinned(stream, pinned_up, pinned_up_bytes, bytes);
 }
 
+int* lgs_ctx::tedge_buffer(size_t n)
+{
+    const int slot = banked(S_TEDGE);
+    int* p = (int*)ensure(slot, sizeof(int) * std::max<size_t>(n, 1));
+    if (buf_bytes[slot] != tedge_zeroed[bank]) {
+        LGS_HIP_CHECK(hipMemsetAsync(p, 0, buf_bytes[slot], stream));
+        tedge_zeroed[bank] = buf_bytes[slot];
+    }
+    return p;
+}
+
 void* lgs_ctx::ensure_pinned_rec(size_t bytes)
 {
     return grow_pinned(stream, pinned_rec[bank], pinned_rec_bytes[bank], bytes);
@@ -256,6 +267,10 @@ void lgs_ctx::release()
     for (int b = 0; b < 2; ++b) {
         if (pinned_rec[b]) hipHostFree(pinned_rec[b]);
         pinned_rec[b] = nullptr;
+        if (pinned_scan[b]) hipHostFree(pinned_scan[b]);
+        pinned_scan[b] = nullptr;
+        if (scan_ev[b]) hipEventDestroy(scan_ev[b]);
+        scan_ev[b] = nullptr;
     }
     if (stream) hipStreamDestroy(stream);
     stream = nullptr;
@@ -378,6 +393,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_SKIP_MASK: ctx->skip_mask = (unsigned)value; return LGS_OK;
     case LGS_OPT_POISON_WS: ctx->poison_ws = value != 0.0; return LGS_OK;
     case LGS_OPT_PEER_COPY: ctx->peer_staged = value != 0.0; return LGS_OK;
+    case LGS_OPT_PRUNE_MIN_SUPER: ctx->prune_min_super = (int)value; return LGS_OK;
     case LGS_OPT_LINSOLVE_SPLIT: ctx->linsolve_split = value != 0.0; return LGS_OK;
     case LGS_OPT_HANDOFF_SPIN_US:
         if (value < 0.0) return LGS_ERR_INVALID_ARG;
@@ -918,6 +934,71 @@ extern "C" int lgs_grid_precompute_max(lgs_ctx* ctx, const lgs_grid* in, int win
 // ---------------------------------------------------------------------------
 // scans
 // ---------------------------------------------------------------------------
+namespace {
+// A scan's device copy (ranges then angles, one allocation) comes from a small
+// per-device pool: a frontend creates and drops two scans per step, and a
+// hipMalloc/hipFree pair costs ~26 us each (hipFree also waits for the whole
+// device).  A buffer goes back to the pool when its scan is destroyed; every
+// library call that reads a scan's device copy finishes with it before it
+// returns (the asynchronous latest-map step reads the host copy), so the
+// buffer can be handed out again at once.  Buffers are binned by power-of-two
+// size; the pool keeps at most kScanPoolBytes per device.
+constexpr size_t kScanPoolBytes = size_t(64) << 20;
+struct ScanPool {
+    std::mutex mu;
+    std::vector<std::vector<void*>> bins;   // bins[log2 bytes]
+    size_t held = 0;
+};
+ScanPool& scan_pool(int device)
+{
+    static std::mutex mu;
+    static std::vector<std::unique_ptr<ScanPool>> pools;
+    std::lock_guard<std::mutex> g(mu);
+    if ((int)pools.size() <= device) pools.resize((size_t)device + 1);
+    if (!pools[device]) pools[device].reset(new ScanPool());
+    return *pools[device];
+}
+int scan_bin(size_t bytes)
+{
+    int b = 8;
+    while ((size_t(1) << b) < bytes) ++b;
+    return b;
+}
+void* scan_buffer_get(int device, size_t bytes)
+{
+    const int b = scan_bin(bytes);
+    ScanPool& P = scan_pool(device);
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        if ((int)P.bins.size() > b && !P.bins[b].empty()) {
+            void* p = P.bins[b].back();
+            P.bins[b].pop_back();
+            P.held -= size_t(1) << b;
+            return p;
+        }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, size_t(1) << b) != hipSuccess) throw Error(LGS_ERR_OOM, "hipMalloc failed for scan");
+    return p;
+}
+void scan_buffer_put(int device, void* p, size_t bytes)
+{
+    const int b = scan_bin(bytes);
+    ScanPool& P = scan_pool(device);
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        if (P.held + (size_t(1) << b) <= kScanPoolBytes) {
+            if ((int)P.bins.size() <= b) P.bins.resize((size_t)b + 1);
+            P.bins[b].push_back(p);
+            P.held += size_t(1) << b;
+            return;
+        }
+    }
+    hipSetDevice(device);
+    hipFree(p);
+}
+}  // namespace
+
 extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan** out)
 {
     if (!ctx || !hs || !out) return LGS_ERR_INVALID_ARG;
@@ -926,6 +1007,7 @@ extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan**
         LGS_REQUIRE(hs->n >= 1 && hs->ranges && hs->angles, "scan must have >= 1 beam");
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         lgs_scan* s = new lgs_scan();
+        std::unique_ptr<lgs_scan> own(s);
         static std::atomic<unsigned long long> uids{ 0 };
         s->uid = uids.fetch_add(1, std::memory_order_relaxed) + 1;
         s->ctx = ctx;
@@ -940,18 +1022,7 @@ extern "C" int lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* hs, lgs_scan**
         for (int i = 1; i < hs->n; ++i)
             if (m < hs->ranges[i]) m = hs->ranges[i];
         s->max_elem = m;
-        const size_t bytes = sizeof(double) * (size_t)hs->n;
-        if (hipMalloc(&s->d_ranges, bytes) != hipSuccess ||
-            hipMalloc(&s->d_angles, bytes) != hipSuccess) {
-            hipFree(s->d_ranges);
-            hipFree(s->d_angles);
-            delete s;
-            throw Error(LGS_ERR_OOM, "hipMalloc failed for scan");
-        }
-        LGS_HIP_CHECK(hipMemcpyAsync(s->d_ranges, hs->ranges, bytes, hipMemcpyHostToDevice, ctx->stream));
-        LGS_HIP_CHECK(hipMemcpyAsync(s->d_angles, hs->angles, bytes, hipMemcpyHostToDevice, ctx->stream));
-        ctx->sync();
-        *out = s;
+        *out = own.release();   // the device copy is made at first use (lgs::scans_to_device)
     });
 }
 
@@ -1032,13 +1103,67 @@ extern "C" int lgs_scan_interpolate(lgs_ctx* ctx, const lgs_scan* in, double dis
 extern "C" void lgs_scan_destroy(lgs_scan* s)
 {
     if (!s) return;
-    hipSetDevice(s->device);
-    hipFree(s->d_ranges);
-    hipFree(s->d_angles);
+    if (s->d_ranges) scan_buffer_put(s->device, s->d_ranges, 2 * sizeof(double) * (size_t)s->n);
     delete s;
 }
 
 namespace lgs {
+void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n)
+{
+    // scans without a copy yet (each once), and copies made by other contexts
+    std::vector<lgs_scan*> todo;
+    bool foreign = false;
+    for (int j = 0; j < n; ++j) {
+        lgs_scan* s = const_cast<lgs_scan*>(scans[j]);
+        if (!s || s->dev_done.load(std::memory_order_acquire)) continue;
+        std::lock_guard<std::mutex> g(s->dev_mu);
+        if (!s->d_ranges) {
+            if (std::find(todo.begin(), todo.end(), s) == todo.end()) todo.push_back(s);
+        } else if (s->dev_ctx != ctx) {
+            foreign = true;
+        }
+    }
+    if (foreign) {   // enqueued on another context's stream, maybe still pending
+        LGS_HIP_CHECK(hipDeviceSynchronize());
+        for (int j = 0; j < n; ++j) {
+            lgs_scan* s = const_cast<lgs_scan*>(scans[j]);
+            if (!s) continue;
+            std::lock_guard<std::mutex> g(s->dev_mu);
+            if (s->d_ranges && s->dev_ctx != ctx) s->dev_done.store(true, std::memory_order_release);
+        }
+    }
+    if (todo.empty()) return;
+    size_t total = 0;
+    for (lgs_scan* s : todo) total += 2 * sizeof(double) * (size_t)s->n;
+    const int b = ctx->bank;
+    if (ctx->scan_ev_live[b]) {   // the staging's previous copies are done
+        LGS_HIP_CHECK(hipEventSynchronize(ctx->scan_ev[b]));
+        ctx->scan_ev_live[b] = false;
+    }
+    char* pin = (char*)grow_pinned(ctx->stream, ctx->pinned_scan[b], ctx->pinned_scan_bytes[b], total);
+    size_t off = 0;
+    for (lgs_scan* s : todo) {
+        std::lock_guard<std::mutex> g(s->dev_mu);
+        if (s->d_ranges) continue;   // another thread got there first
+        const size_t bytes = sizeof(double) * (size_t)s->n;
+        double* d = (double*)scan_buffer_get(ctx->device, 2 * bytes);
+        std::memcpy(pin + off, s->h_ranges.data(), bytes);
+        std::memcpy(pin + off + bytes, s->h_angles.data(), bytes);
+        const hipError_t e = hipMemcpyAsync(d, pin + off, 2 * bytes, hipMemcpyHostToDevice, ctx->stream);
+        if (e != hipSuccess) {
+            scan_buffer_put(ctx->device, d, 2 * bytes);
+            LGS_HIP_CHECK(e);
+        }
+        off += 2 * bytes;
+        s->d_angles = d + s->n;
+        s->dev_ctx = ctx;
+        s->d_ranges = d;
+    }
+    if (!ctx->scan_ev[b]) LGS_HIP_CHECK(hipEventCreateWithFlags(&ctx->scan_ev[b], hipEventDisableTiming));
+    LGS_HIP_CHECK(hipEventRecord(ctx->scan_ev[b], ctx->stream));
+    ctx->scan_ev_live[b] = true;
+}
+
 // Beams with range < ScanRangeMax in beam order (ComputeScanIndices filter,
 // C/mapping/scan_matcher_real_time_correlative.cpp:189-193).  Cached per
 // ScanRangeMax; the upload happens once per (scan, matcher).

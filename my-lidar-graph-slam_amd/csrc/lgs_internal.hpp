@@ -16,6 +16,8 @@
 #include <stdexcept>
 #include <string>
 #include <memory>
+#include <mutex>
+#include <atomic>
 #include <vector>
 
 #include "lgs_hip.h"
@@ -63,7 +65,8 @@ enum Slot {
     S_COARSE_GRID,  // double (coarse map for OptimizePose(query))
     S_DECIM,        // double (phase-plane coarse map)
     S_CINFO,        // int4 [T*Nv] phase-plane addressing per (angle, beam)
-    S_TEDGE,        // int [T] generation-stamped 'angle touches the low map edge' flags
+    S_TEDGE,        // int [items][T]: generation-stamped 'angle touches the low map edge' flags; holds
+                    // nothing else, so stamps never need clearing (zeroed once when allocated)
     S_RAY0, S_RAY1, S_RAY2, S_RAY3, S_RAY4, S_RAY5, S_RAY6, S_RAY7,
     S_LS0, S_LS1,
     S_LIN0, S_LIN1,   // K4 staging
@@ -79,7 +82,7 @@ enum Slot {
     // bank 1 of the per-batch buffers: a batched call keeps two 64-query
     // chunks in flight (the next chunk's launches go out before the host
     // finishes the previous one), each in its own bank (lgs_ctx::banked)
-    S_BATCH_WS_B, S_RECORDS_B, S_UPLOAD_B, S_DECIM_B, S_SUPER_B, S_NEGFLAG_B,
+    S_BATCH_WS_B, S_RECORDS_B, S_UPLOAD_B, S_DECIM_B, S_SUPER_B, S_NEGFLAG_B, S_TEDGE_B,
     S_NUM_SLOTS
 };
 
@@ -216,6 +219,7 @@ struct lgs_ctx {
     long long handoff_spin_us = 200000;   // split refine spin bound (LGS_OPT_HANDOFF_SPIN_US; 0 = force the fallback)
     long long handoff_fallbacks = 0;      // split refines rerun on one workgroup after a time-out
     bool peer_staged = false;    // cross-context copies through host memory (LGS_OPT_PEER_COPY)
+    int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
     long long copies_direct = 0, copies_staged = 0;   // lgs_debug_copy_counters
     int lanes_min_batch = 2;     // pruned coarse stage: k_coarse_lanes from this batch size on (LGS_OPT_LANES_MIN_BATCH)
     long long ray_chunk_keys = 1LL << 28;  // ray-cast keys per emit/sort/apply pass (LGS_OPT_RAY_CHUNK_KEYS)
@@ -250,6 +254,9 @@ struct lgs_ctx {
     void* pinned_rec[2] = {};
     size_t pinned_rec_bytes[2] = {};
     int bank = 0;                // which bank the per-batch buffers come from
+    size_t tedge_zeroed[2] = {}; // bytes of the S_TEDGE allocation already zeroed, per bank
+                                 // (a reallocation always grows the slot)
+    int* tedge_buffer(size_t n); // n flags, zeroed at allocation only
     int banked(int slot) const
     {
         if (!bank) return slot;
@@ -260,10 +267,17 @@ struct lgs_ctx {
         case lgs::S_DECIM: return lgs::S_DECIM_B;
         case lgs::S_SUPER: return lgs::S_SUPER_B;
         case lgs::S_NEGFLAG: return lgs::S_NEGFLAG_B;
+        case lgs::S_TEDGE: return lgs::S_TEDGE_B;
         default: return slot;
         }
     }
     void* ensure_pinned_rec(size_t bytes);   // per bank: a batch's record copies
+    // staging of scans' first device copies (lgs::scans_to_device), per bank;
+    // scan_ev[bank] marks the end of the copies out of it
+    void* pinned_scan[2] = {};
+    size_t pinned_scan_bytes[2] = {};
+    hipEvent_t scan_ev[2] = {};
+    bool scan_ev_live[2] = {};
     void* pinned_in = nullptr;   // staging of lgs_grid_upload_patches
     size_t pinned_in_bytes = 0;
     // padded phase-plane buffer (per bank): margins zeroed once per (buffer, layout, set count)
@@ -346,8 +360,15 @@ struct lgs_scan {
     lgs_ctx* ctx = nullptr;   // creating context (not used after its destruction)
     int device = 0;
     unsigned long long uid = 0;   // process-unique id (the latest map's window identity, §4.4b)
+    // device copy (ranges then angles, one pooled buffer): made by the first
+    // call that reads it, on that call's stream (lgs::scans_to_device); null
+    // until then -- a frontend's raw scans, only ever interpolated on the
+    // host, never get one
     double* d_ranges = nullptr;
     double* d_angles = nullptr;
+    std::mutex dev_mu;
+    const lgs_ctx* dev_ctx = nullptr;   // whose stream the copy went on
+    std::atomic<bool> dev_done{ false };  // the copy is known to be complete
     int n = 0;
     lgs_pose2d rel{0, 0, 0};
     double min_range = 0, max_range = 0;
@@ -398,6 +419,13 @@ inline lgs_pose2d inverse_compound(lgs_pose2d s, lgs_pose2d e)
 }
 
 const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* scan, double scan_range_max, int* nv);
+// Device copies of the scans' ranges/angles, ordered before the ctx stream's
+// next work: the first use of a scan stages its host copy (pinned, per bank)
+// and enqueues the copy on ctx->stream.  Every caller synchronises its
+// stream before returning, after which the copy is complete; a scan whose
+// copy was enqueued by another context is waited for (device-wide) once.
+void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n);
+inline void scan_to_device(lgs_ctx* ctx, const lgs_scan* s) { scans_to_device(ctx, &s, 1); }
 
 // Order a read of g's cells on ctx's stream after a pending asynchronous write
 // from another stream (a device-side wait, no host synchronisation).
