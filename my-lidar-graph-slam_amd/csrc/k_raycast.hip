@@ -1516,7 +1516,8 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
         if (C.pin) hipHostFree(C.pin);
         C.pin = nullptr;
         C.pin_cap = 0;
-        if (hipHostMalloc((void**)&C.pin, 2 * total) != hipSuccess) throw Error(LGS_ERR_OOM, "hipHostMalloc failed");
+        if (hipHostMalloc((void**)&C.pin, 2 * total, hipHostMallocCoherent) != hipSuccess)
+            throw Error(LGS_ERR_OOM, "hipHostMalloc failed");
         C.pin_cap = 2 * total;
     }
     char* pin = C.pin;
@@ -1563,7 +1564,7 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
         J.nL = L.end - L.beg;
     }
     J.tbl = C.d_tbl;
-    LGS_HIP_CHECK(hipMemcpyAsync(d_stage, pin, total, hipMemcpyHostToDevice, st));
+    fetch_async(ctx, d_stage, pin, total);
     unsigned* d_keys = (unsigned*)ctx->ensure(S_RAY2, sizeof(unsigned) * (size_t)std::max(1LL, keys));
     unsigned* d_tmp = (unsigned*)ctx->ensure(S_RAY3, sizeof(unsigned) * (size_t)std::max(1LL, keys));
     if (nr > 0) {

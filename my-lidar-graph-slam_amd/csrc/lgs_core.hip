@@ -71,7 +71,7 @@ void* lgs_ctx::ensure_pinned(size_t bytes)
         pinned_bytes = 0;
     }
     size_t want = bytes + bytes / 4;
-    LGS_HIP_CHECK(hipHostMalloc(&pinned, want, hipHostMallocDefault));
+    LGS_HIP_CHECK(hipHostMalloc(&pinned, want, hipHostMallocCoherent));
     pinned_bytes = want;
     return pinned;
 }
@@ -102,11 +102,42 @@ void* grow_pinned(hipStream_t stream, void*& p, size_t& have, size_t bytes)
         have = 0;
     }
     size_t want = bytes + bytes / 4;
-    LGS_HIP_CHECK(hipHostMalloc(&p, want, hipHostMallocDefault));
+    // coherent: k_fetch reads it uncached (fresh on every launch)
+    LGS_HIP_CHECK(hipHostMalloc(&p, want, hipHostMallocCoherent));
     have = want;
     return p;
 }
+
+struct FetchSeg {
+    const unsigned char* src;
+    unsigned char* dst;
+    unsigned long long bytes;
+};
+__global__ __launch_bounds__(256) void k_fetch(FetchSeg s)
+{
+    const unsigned long long n16 = s.bytes / 16;
+    const unsigned long long g = (unsigned long long)blockIdx.x * 256 + threadIdx.x;
+    const uint4* __restrict__ a = (const uint4*)s.src;
+    uint4* __restrict__ b = (uint4*)s.dst;
+    for (unsigned long long i = g; i < n16; i += (unsigned long long)gridDim.x * 256) b[i] = a[i];
+    if (n16 * 16 + g < s.bytes) s.dst[n16 * 16 + g] = s.src[n16 * 16 + g];   // the tail bytes
+}
 }  // namespace
+
+namespace lgs {
+void fetch_async(lgs_ctx* ctx, void* dst, const void* src, size_t bytes)
+{
+    if (bytes == 0) return;
+    LGS_REQUIRE(((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0, "fetch_async: 16-byte alignment");
+    void* dsrc = nullptr;
+    LGS_HIP_CHECK(hipHostGetDevicePointer(&dsrc, const_cast<void*>(src), 0));
+    const unsigned long long n16 = bytes / 16;
+    const unsigned blocks = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>((n16 + 255) / 256, 64));
+    hipLaunchKernelGGL(k_fetch, dim3(blocks), dim3(256), 0, ctx->stream,
+                       FetchSeg{ (const unsigned char*)dsrc, (unsigned char*)dst, (unsigned long long)bytes });
+    LGS_HIP_CHECK(hipGetLastError());
+}
+}  // namespace lgs
 
 void* lgs_ctx::ensure_pinned_up(size_t bytes)
 {
@@ -1149,10 +1180,11 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n)
         double* d = (double*)scan_buffer_get(ctx->device, 2 * bytes);
         std::memcpy(pin + off, s->h_ranges.data(), bytes);
         std::memcpy(pin + off + bytes, s->h_angles.data(), bytes);
-        const hipError_t e = hipMemcpyAsync(d, pin + off, 2 * bytes, hipMemcpyHostToDevice, ctx->stream);
-        if (e != hipSuccess) {
+        try {
+            fetch_async(ctx, d, pin + off, 2 * bytes);
+        } catch (...) {
             scan_buffer_put(ctx->device, d, 2 * bytes);
-            LGS_HIP_CHECK(e);
+            throw;
         }
         off += 2 * bytes;
         s->d_angles = d + s->n;

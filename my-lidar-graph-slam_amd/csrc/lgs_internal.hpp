@@ -425,6 +425,12 @@ const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* scan, double scan_range_ma
 // stream before returning, after which the copy is complete; a scan whose
 // copy was enqueued by another context is waited for (device-wide) once.
 void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n);
+// Host-to-device copy of pinned staging (the ctx's coherent hipHostMalloc
+// buffers) by a kernel on ctx->stream (k_fetch): a small hipMemcpyAsync waits
+// ~11 us in the copy engine's queue and takes ~6 us more (r03 trace of the
+// config-4 frontend), a kernel reads the staging over the host link in one
+// round trip.  dst and src 16-byte aligned.
+void fetch_async(lgs_ctx* ctx, void* dst, const void* src, size_t bytes);
 inline void scan_to_device(lgs_ctx* ctx, const lgs_scan* s) { scans_to_device(ctx, &s, 1); }
 
 // Order a read of g's cells on ctx's stream after a pending asynchronous write
@@ -464,7 +470,7 @@ struct Upload {
         const size_t b = std::max<size_t>(host.size(), 16);
         char* pin = (char*)ctx->ensure_pinned_up(b);
         std::memcpy(pin, host.data(), host.size());
-        LGS_HIP_CHECK(hipMemcpyAsync(dev, pin, host.size(), hipMemcpyHostToDevice, ctx->stream));
+        fetch_async(ctx, dev, pin, host.size());
     }
     void flush()
     {
