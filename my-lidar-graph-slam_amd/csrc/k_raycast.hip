@@ -21,6 +21,8 @@
 //              counts hits/misses
 #include "lgs_internal.hpp"
 
+#include <unordered_map>
+
 #include <algorithm>
 #include <array>
 #include <cfloat>
@@ -953,6 +955,8 @@ ScanHits scan_hits(const lgs_scan* s, lgs_pose2d robot, const lgs_builder_params
     return h;
 }
 
+bool same_pose(lgs_pose2d a, lgs_pose2d b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
+
 // scan_hits through the scan's one-entry cache (lgs_scan::hits_cache), keyed
 // bitwise on the robot pose and the usable range.  Callers that may run in
 // parallel over the same scan pass store = false and store afterwards.
@@ -996,15 +1000,41 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
                     const lgs_scan* const* scans, const lgs_pose2d* poses, const lgs_builder_params* bp,
                     std::vector<std::array<double, 4>>& boxes)
 {
+    // one computation per distinct (scan, pose): AppendScan's newest scan is
+    // both the latest map's last scan and the local map's insert
     std::vector<std::pair<int, int>> work;
+    std::vector<std::pair<int, int>> same;   // (job, k) -> the work item it shares
+    std::unordered_map<const lgs_scan*, int> seen;
     for (size_t j = 0; j < jobs.size(); ++j) {
         jobs[j].hs.resize(count[j]);
-        for (int k = 0; k < count[j]; ++k) work.emplace_back((int)j, k);
+        for (int k = 0; k < count[j]; ++k) {
+            const int i = first[j] + k;
+            int w = -1;
+            const auto it = seen.find(scans[i]);
+            if (it != seen.end()) {
+                const int iq = first[work[it->second].first] + work[it->second].second;
+                if (same_pose(poses[iq], poses[i])) w = it->second;
+            }
+            if (w < 0) {
+                w = (int)work.size();
+                work.emplace_back((int)j, k);
+                seen.emplace(scans[i], w);
+            }
+            same.emplace_back((int)j, w);
+        }
     }
     host_parallel_for((int)work.size(), 2, [&](int w) {
         const int j = work[w].first, k = work[w].second;
         jobs[j].hs[k] = cached_hits(scans[first[j] + k], poses[first[j] + k], bp, false);
     });
+    {
+        size_t u = 0;
+        for (size_t j = 0; j < jobs.size(); ++j)
+            for (int k = 0; k < count[j]; ++k, ++u) {
+                const auto& src = work[same[u].second];
+                jobs[j].hs[k] = jobs[src.first].hs[src.second];
+            }
+    }
     boxes.assign(jobs.size(), std::array<double, 4>{DBL_MAX, DBL_MAX, DBL_MIN, DBL_MIN});
     for (size_t j = 0; j < jobs.size(); ++j)
         for (int k = 0; k < count[j]; ++k) {
@@ -1413,7 +1443,6 @@ void invalidate_cache(lgs_map* m)
     m->cache->drop_lists();
 }
 
-bool same_pose(lgs_pose2d a, lgs_pose2d b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
 
 // The step's device work stays queued when the call returns: readers of the
 // maps on other streams wait for this event (grid_acquire).

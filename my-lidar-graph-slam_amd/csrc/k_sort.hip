@@ -12,7 +12,7 @@
 //                 between sorts, no memset per call)
 //   k_sort_pass   one launch per digit (<= 8 bits): tiles of 256 x KPT keys
 //                 taken in ticket order; per wave a stable rank of each key
-//                 among equal digits (digit-bit ballots), per tile the digit
+//                 among equal digits (LDS peer masks), per tile the digit
 //                 counts published as aggregates and turned into inclusive
 //                 prefixes by a decoupled look-back over earlier tiles (status
 //                 words tagged with a per-pass stamp: no clearing); keys are
@@ -20,6 +20,12 @@
 //
 // Each workgroup only waits on tiles with lower tickets, which belong to
 // workgroups that started before it, so the look-back always drains.
+//
+//   k_sort_wide   sorts that fit the device at once: every pass in one
+//                 launch, 8192-key tiles, digits of up to 10 bits, ranks from
+//                 per-wave LDS peer masks, grid barriers around the count
+//                 exchange (a config-4 step's ~160k keys, 20 cell bits: 20
+//                 workgroups, 2 passes)
 #include "lgs_internal.hpp"
 
 #include <algorithm>
@@ -34,7 +40,7 @@ constexpr int kHistLanes = 8;                                // accumulator copi
 constexpr int kCtlHist = 0;                                  // [lane][pass][256] accumulators
 constexpr int kCtlDone = kHistLanes * kSortMaxPasses * kSortRadix;   // workgroups finished k_sort_hist
 constexpr int kCtlTicket = kCtlDone + 1;                     // [pass] tile tickets
-constexpr int kCtlBar = kCtlDone + 8;                        // k_sort_coop grid barrier, workgroups done
+constexpr int kCtlBar = kCtlDone + 8;                        // k_sort_wide grid barrier, workgroups done
 constexpr int kCtlOffs = kCtlDone + 64;                      // [pass][256] exclusive digit offsets
 constexpr int kCtlWords = kCtlOffs + kSortMaxPasses * kSortRadix;
 
@@ -140,9 +146,11 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const unsigned* __re
     __shared__ unsigned gbase[kSortRadix];
     __shared__ unsigned wsum[4];
     __shared__ unsigned tile_s;
+    __shared__ unsigned long long wmask[4][kSortRadix];   // per-wave peer masks (k_sort_wide)
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const unsigned mask = (1u << nb) - 1u;
     wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+    wmask[0][tid] = wmask[1][tid] = wmask[2][tid] = wmask[3][tid] = 0ull;
     if (tid == 0) tile_s = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const long long tile = tile_s;
@@ -155,20 +163,23 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const unsigned* __re
         const long long p = p0 + 64 * i;
         k[i] = (p < n) ? in[p] : 0u;
     }
-    const unsigned long long lt = (1ull << lane) - 1ull;
+    const unsigned long long me = 1ull << lane, lt = me - 1ull;
+    unsigned long long* mw = wmask[w];
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
         const bool valid = p0 + 64 * i < n;
         const unsigned d = (k[i] >> shift) & mask;
-        unsigned long long peers = __ballot(valid);
-        for (int b = 0; b < nb; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const unsigned long long m = __ballot(valid && bit);
-            peers &= bit ? m : ~m;
+        unsigned long long peers = 0;
+        if (valid) {
+            __hip_atomic_fetch_or(&mw[d], me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            peers = __hip_atomic_load(&mw[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        const unsigned base = wcnt[w][d];
+        const unsigned base = valid ? wcnt[w][d] : 0u;
         rank[i] = base + (unsigned)__popcll(peers & lt);
-        if (valid && !(peers & lt)) wcnt[w][d] = base + (unsigned)__popcll(peers);
+        if (valid && !(peers & lt)) {
+            wcnt[w][d] = base + (unsigned)__popcll(peers);
+            __hip_atomic_store(&mw[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
     __syncthreads();
     // per digit: exclusive prefix over the waves, tile total, publication
@@ -262,53 +273,55 @@ __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target)
     __syncthreads();
 }
 
-// exclusive prefix over the block of one value per thread (thread order);
-// *total receives the block sum
-__device__ __forceinline__ unsigned block_excl(unsigned v, unsigned* wsum4, unsigned* total)
+// Wide tiles for the cooperative sort: 512 threads x 16 keys (8192 keys per
+// tile), digits of up to 10 bits.  A config-4 step's ~160k keys are then 20
+// tiles and 20 cell bits take 2 passes -- the cross-XCD barriers and count
+// exchange, not the key traffic, are the cost of a small sort.
+//
+// Ranking: a key's peers (the lanes of its wave with the same digit) come
+// from a per-wave LDS mask table -- every lane ORs its lane bit into
+// mask[digit], reads the word back and the lowest peer clears it -- instead
+// of one ballot per digit bit (10 ballots and 64-bit selects per key made the
+// ranking VALU-bound: 12.8 of a pass's ~27 us on 10 CUs).  A wave's LDS
+// instructions execute in order, so the read sees every lane's OR and the
+// next key's ORs see the clear.
+constexpr int kWideThreads = 512, kWideKPT = 16, kWideTile = kWideThreads * kWideKPT;
+template <int RB>
+__global__ __launch_bounds__(kWideThreads) void k_sort_wide(const unsigned* __restrict__ in,
+                                                            unsigned* __restrict__ out, unsigned* __restrict__ tmp,
+                                                            long long n, int lo, int dbits, int bits, int passes,
+                                                            unsigned* __restrict__ counts,
+                                                            unsigned* __restrict__ bar)
 {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    unsigned incl = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
-    __syncthreads();
-    if (lane == 63) wsum4[w] = incl;
-    __syncthreads();
-    unsigned wo = 0;
-    for (int q = 0; q < w; ++q) wo += wsum4[q];
-    if (total) *total = wsum4[0] + wsum4[1] + wsum4[2] + wsum4[3];
-    return wo + incl - v;
-}
-
-template <int KPT, int RB>
-__global__ __launch_bounds__(kSortThreads) void k_sort_coop(const unsigned* __restrict__ in, unsigned* __restrict__ out,
-                                                            unsigned* __restrict__ tmp, long long n, int lo,
-                                                            int dbits, int bits, int passes,
-                                                            unsigned* __restrict__ counts, unsigned* __restrict__ bar)
-{
-    constexpr int TILE = kSortThreads * KPT;
+    constexpr int NT = kWideThreads, NW = NT / 64, KPT = kWideKPT, TILE = kWideTile;
     constexpr int R = 1 << RB;
-    constexpr int Q = R / kSortThreads;   // consecutive digits per thread
-    static_assert(Q >= 1 && Q * kSortThreads == R, "digits per thread");
+    constexpr int Q = R >= NT ? R / NT : 1;   // digits per digit-owning thread
+    constexpr int ND = R / Q;                 // digit-owning threads (whole waves)
+    static_assert(ND % 64 == 0 && ND <= NT, "digit threads");
     __shared__ unsigned keys_s[TILE];
-    __shared__ unsigned wcnt[4][R];
+    __shared__ unsigned wcnt[NW][R];
+    __shared__ unsigned long long wmask[NW][R];
     __shared__ unsigned dstart[R];
     __shared__ unsigned gbase[R];
-    __shared__ unsigned ws4[4];
+    __shared__ unsigned wsa[NW], wsb[NW];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const unsigned ntiles = gridDim.x, tile = blockIdx.x;
     const long long t0 = (long long)tile * TILE;
     const long long p0 = t0 + (long long)w * 64 * KPT + lane;
-    const unsigned long long lt = (1ull << lane) - 1ull;
+    const unsigned long long me = 1ull << lane, lt = me - 1ull;
+    const bool dig = tid < ND;
+    const int d0 = tid * Q;   // this thread's first digit
     unsigned nbar = 0;
+    LGS_PROBE_DECL;
+    LGS_PROBE_MARK();
+    for (int i = tid; i < NW * R; i += NT) (&wmask[0][0])[i] = 0ull;
     for (int p = 0; p < passes; ++p) {
         const unsigned* src = (p == 0) ? in : (((passes - p) % 2 == 1) ? tmp : out);
         unsigned* dst = ((passes - 1 - p) % 2 == 0) ? out : tmp;
         const int shift = lo + p * dbits;
         const int nb = min(dbits, bits - p * dbits);
         const unsigned mask = (1u << nb) - 1u;
-        for (int d = tid; d < R; d += kSortThreads) wcnt[0][d] = wcnt[1][d] = wcnt[2][d] = wcnt[3][d] = 0;
+        for (int i = tid; i < NW * R; i += NT) (&wcnt[0][0])[i] = 0;
         __syncthreads();
         unsigned k[KPT], rank[KPT];
 #pragma unroll
@@ -316,92 +329,129 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_coop(const unsigned* __re
             const long long q = p0 + 64 * i;
             k[i] = (q < n) ? src[q] : 0u;
         }
+#ifdef LGS_PROBE
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        LGS_PROBE_MARK();
+        unsigned* cw = wcnt[w];
+        unsigned long long* mw = wmask[w];
 #pragma unroll
         for (int i = 0; i < KPT; ++i) {
             const bool valid = p0 + 64 * i < n;
             const unsigned d = (k[i] >> shift) & mask;
-            unsigned long long peers = __ballot(valid);
-            for (int b = 0; b < nb; ++b) {
-                const bool bit = (d >> b) & 1u;
-                const unsigned long long m = __ballot(valid && bit);
-                peers &= bit ? m : ~m;
+            unsigned long long peers = 0;
+            if (valid) {
+                __hip_atomic_fetch_or(&mw[d], me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                peers = __hip_atomic_load(&mw[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            const unsigned base = wcnt[w][d];
+            const unsigned base = valid ? cw[d] : 0u;
             rank[i] = base + (unsigned)__popcll(peers & lt);
-            if (valid && !(peers & lt)) wcnt[w][d] = base + (unsigned)__popcll(peers);
+            if (valid && !(peers & lt)) {   // the lowest peer: the digit's count, and clear the mask
+                cw[d] = base + (unsigned)__popcll(peers);
+                __hip_atomic_store(&mw[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
         __syncthreads();
-        // this thread's digits [tid * Q, tid * Q + Q): tile counts, the
-        // exclusive prefix over the waves, publication
+        LGS_PROBE_MARK();
+        // this thread's digits: exclusive prefix over the waves, the tile's
+        // counts (published), the tile-local digit starts
         unsigned* cp = counts + (size_t)p * ntiles * R;
-        unsigned tot[Q], tsum = 0;
-#pragma unroll
-        for (int j = 0; j < Q; ++j) {
-            const int d = tid * Q + j;
-            const unsigned c0 = wcnt[0][d], c1 = wcnt[1][d], c2 = wcnt[2][d], c3 = wcnt[3][d];
-            tot[j] = c0 + c1 + c2 + c3;
-            wcnt[0][d] = 0;
-            wcnt[1][d] = c0;
-            wcnt[2][d] = c0 + c1;
-            wcnt[3][d] = c0 + c1 + c2;
-            cp[(size_t)tile * R + d] = tot[j];
-            tsum += tot[j];
-        }
-        {
-            unsigned run = block_excl(tsum, ws4, nullptr);
+        unsigned tot[Q], tsum = 0, incl = 0;
+        if (dig) {
 #pragma unroll
             for (int j = 0; j < Q; ++j) {
-                dstart[tid * Q + j] = run;
+                unsigned c = 0;
+#pragma unroll
+                for (int q = 0; q < NW; ++q) {
+                    const unsigned v = wcnt[q][d0 + j];
+                    wcnt[q][d0 + j] = c;
+                    c += v;
+                }
+                tot[j] = c;
+                tsum += c;
+                cp[(size_t)tile * R + d0 + j] = c;
+            }
+            incl = tsum;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+            if (lane == 63) wsa[w] = incl;
+        }
+        __syncthreads();
+        if (dig) {
+            unsigned run = incl - tsum;
+            for (int q = 0; q < w; ++q) run += wsa[q];
+#pragma unroll
+            for (int j = 0; j < Q; ++j) {
+                dstart[d0 + j] = run;
                 run += tot[j];
             }
         }
-        grid_barrier(bar, ++nbar * ntiles);
-        // each digit's total over all tiles and the count of the tiles before
-        // this one (16 loads in flight per round: written on other XCDs)
-        unsigned all[Q], before[Q], asum = 0;
-#pragma unroll
-        for (int j = 0; j < Q; ++j) all[j] = before[j] = 0;
-        for (unsigned tc = 0; tc < ntiles; tc += 16) {
-#pragma unroll
-            for (int j = 0; j < Q; ++j) {
-                unsigned c[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q)
-                    c[q] = (tc + q < ntiles) ? cp[(size_t)(tc + q) * R + tid * Q + j] : 0u;
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    all[j] += c[q];
-                    before[j] += (tc + q < tile) ? c[q] : 0u;
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < Q; ++j) asum += all[j];
-        {
-            unsigned run = block_excl(asum, ws4, nullptr);
-#pragma unroll
-            for (int j = 0; j < Q; ++j) {
-                gbase[tid * Q + j] = run + before[j];
-                run += all[j];
-            }
-        }
         __syncthreads();
+        LGS_PROBE_MARK();
+        // reorder the tile by digit in LDS (tile-local offsets: before the
+        // barrier, so the keys and ranks need not live across it)
 #pragma unroll
         for (int i = 0; i < KPT; ++i)
             if (p0 + 64 * i < n) {
                 const unsigned dd = (k[i] >> shift) & mask;
-                keys_s[dstart[dd] + wcnt[w][dd] + rank[i]] = k[i];
+                keys_s[dstart[dd] + cw[dd] + rank[i]] = k[i];
             }
+        LGS_PROBE_MARK();
+        grid_barrier(bar, ++nbar * ntiles);
+        LGS_PROBE_MARK();
+        // digit totals over all tiles and the counts of the tiles before this one
+        unsigned all[Q], before[Q], asum = 0, incl2 = 0;
+        if (dig) {
+#pragma unroll
+            for (int j = 0; j < Q; ++j) all[j] = before[j] = 0;
+            constexpr int B = 16 / Q;   // tiles per round: 16 loads in flight
+            for (unsigned tc = 0; tc < ntiles; tc += B) {
+                unsigned c[Q][B];
+#pragma unroll
+                for (int q = 0; q < B; ++q)
+#pragma unroll
+                    for (int j = 0; j < Q; ++j) c[j][q] = (tc + q < ntiles) ? cp[(size_t)(tc + q) * R + d0 + j] : 0u;
+#pragma unroll
+                for (int q = 0; q < B; ++q)
+#pragma unroll
+                    for (int j = 0; j < Q; ++j) {
+                        all[j] += c[j][q];
+                        before[j] += (tc + q < tile) ? c[j][q] : 0u;
+                    }
+            }
+#pragma unroll
+            for (int j = 0; j < Q; ++j) asum += all[j];
+            incl2 = asum;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned t = __shfl_up(incl2, o);
+                if (lane >= o) incl2 += t;
+            }
+            if (lane == 63) wsb[w] = incl2;
+        }
         __syncthreads();
+        if (dig) {
+            unsigned run = incl2 - asum;
+            for (int q = 0; q < w; ++q) run += wsb[q];
+#pragma unroll
+            for (int j = 0; j < Q; ++j) {
+                gbase[d0 + j] = run + before[j];
+                run += all[j];
+            }
+        }
+        __syncthreads();
+        LGS_PROBE_MARK();
         const int nvalid = (int)max(0LL, min((long long)TILE, n - t0));
-        for (int j = tid; j < nvalid; j += kSortThreads) {
+        for (int j = tid; j < nvalid; j += NT) {
             const unsigned key = keys_s[j];
             const unsigned dd = (key >> shift) & mask;
             dst[gbase[dd] + (unsigned)j - dstart[dd]] = key;
         }
         if (p + 1 < passes) grid_barrier(bar, ++nbar * ntiles);
+        LGS_PROBE_MARK();
     }
-    // the last workgroup out resets the barrier for the next sort
+    LGS_PROBE_PRINT("k_sort_wide");
     __syncthreads();
     if (tid == 0 &&
         __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ntiles - 1) {
@@ -414,7 +464,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_coop(const unsigned* __re
 
 namespace lgs {
 
-// Workgroups of k_sort_coop the device holds at once (all its tiles must be
+// Workgroups of k_sort_wide the device holds at once (all its tiles must be
 // resident: they wait for each other), with a margin for other streams' work.
 long long coop_capacity(lgs_ctx* ctx)
 {
@@ -423,7 +473,7 @@ long long coop_capacity(lgs_ctx* ctx)
     if (dev < 0 || dev >= 64) return 0;
     if (!cap[dev]) {
         int per_cu = 0, cus = 0;
-        LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_coop<16, 8>, kSortThreads, 0));
+        LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_wide<10>, kWideThreads, 0));
         LGS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         cap[dev] = std::max(1LL, (long long)per_cu * cus / 2);
     }
@@ -442,25 +492,31 @@ void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, lon
         LGS_HIP_CHECK(hipMemcpyAsync(out, in, sizeof(unsigned) * (size_t)n, hipMemcpyDeviceToDevice, st));
         return;
     }
-    const int passes = (bits + 7) / 8;
-    const int dbits = (bits + passes - 1) / passes;
     const bool fresh = ctx->buf[S_RAY0] == nullptr;
     unsigned* ctl = (unsigned*)ctx->ensure(S_RAY0, sizeof(unsigned) * kCtlWords);
     if (fresh) LGS_HIP_CHECK(hipMemsetAsync(ctl, 0, sizeof(unsigned) * kCtlWords, st));
-    // one launch when every tile can be resident at once (measured per
-    // device).  (10-bit digits -- 2 passes for the latest map's 20 cell bits
-    // instead of 3 -- measured slower: 52.7 vs 46.1 us per config-4 step;
-    // the per-pass cost is the barriers and the count reads, which grow with
-    // the radix.)
-    constexpr int kCoopTile = kSortThreads * 16;
-    const long long ctiles = (n + kCoopTile - 1) / kCoopTile;
-    if (ctiles <= coop_capacity(ctx) && (passes == 1 || tmp)) {
-        unsigned* counts = (unsigned*)ctx->ensure(S_RAY1, sizeof(unsigned) * (size_t)ctiles * kSortRadix * passes);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_coop<16, 8>), dim3((unsigned)ctiles), dim3(kSortThreads), 0, st, in,
-                           out, tmp, n, lo, dbits, bits, passes, counts, ctl + kCtlBar);
-        LGS_HIP_CHECK(hipGetLastError());
-        return;
+    // one launch (k_sort_wide) when every tile can be resident at once
+    // (measured per device)
+    {
+        // wide tiles, digits of up to 10 bits (8 when that takes as many passes)
+        const int wp = bits > 16 ? (bits + 9) / 10 : (bits + 7) / 8;
+        const int wd = (bits + wp - 1) / wp;
+        const long long ctiles = (n + kWideTile - 1) / kWideTile;
+        if (ctiles <= coop_capacity(ctx) && (wp == 1 || tmp)) {
+            const int rb = wd > 8 ? 10 : 8;
+            unsigned* counts = (unsigned*)ctx->ensure(S_RAY1, sizeof(unsigned) * (size_t)ctiles * (1u << rb) * wp);
+            if (rb == 10)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_wide<10>), dim3((unsigned)ctiles), dim3(kWideThreads), 0, st,
+                                   in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_wide<8>), dim3((unsigned)ctiles), dim3(kWideThreads), 0, st,
+                                   in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar);
+            LGS_HIP_CHECK(hipGetLastError());
+            return;
+        }
     }
+    const int passes = (bits + 7) / 8;
+    const int dbits = (bits + passes - 1) / passes;
     // 4096-key tiles (a short look-back chain); 1024-key tiles only for sorts
     // too small to give 64 workgroups
     const bool big = n >= 64LL * 4096;

@@ -178,8 +178,8 @@ struct CostPlan {
 // Phase probes (diagnostics build only, make probe): block 0 / thread 0
 // stamps the 100 MHz wall clock at phase boundaries and prints the deltas.
 #ifdef LGS_PROBE
-#define LGS_PROBE_DECL unsigned long long lgs_probe_t[12]; int lgs_probe_n = 0
-#define LGS_PROBE_MARK() do { if (threadIdx.x == 0) lgs_probe_t[lgs_probe_n < 12 ? lgs_probe_n++ : 11] = wall_clock64(); } while (0)
+#define LGS_PROBE_DECL unsigned long long lgs_probe_t[16]; int lgs_probe_n = 0
+#define LGS_PROBE_MARK() do { if (threadIdx.x == 0) lgs_probe_t[lgs_probe_n < 16 ? lgs_probe_n++ : 15] = wall_clock64(); } while (0)
 #define LGS_PROBE_PRINT(name) do { if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) { \
     printf("probe %s:", name); for (int i_ = 1; i_ < lgs_probe_n; ++i_) printf(" %.2f", 0.01 * (double)(lgs_probe_t[i_] - lgs_probe_t[i_ - 1])); \
     printf(" us\n"); } } while (0)
