@@ -21,6 +21,9 @@
 //              counts hits/misses
 #include "lgs_internal.hpp"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <unordered_map>
 
 #include <algorithm>
@@ -1023,8 +1026,22 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
             same.emplace_back((int)j, w);
         }
     }
-    host_parallel_for((int)work.size(), 2, [&](int w) {
+    // cached hits first (a key compare each), then the missing ones -- on the
+    // worker pool only when there are several (a frontend step computes one:
+    // waking the pool would cost more than the scan's sincos)
+    std::vector<int> todo;
+    for (size_t w = 0; w < work.size(); ++w) {
         const int j = work[w].first, k = work[w].second;
+        const lgs_scan* s = scans[first[j] + k];
+        const lgs_pose2d p = poses[first[j] + k];
+        const double key[5] = { p.x, p.y, p.theta, bp->usable_range_min, bp->usable_range_max };
+        if (s->hits_cache && std::memcmp(key, s->hits_key, sizeof(key)) == 0)
+            jobs[j].hs[k] = std::static_pointer_cast<const ScanHits>(s->hits_cache);
+        else
+            todo.push_back((int)w);
+    }
+    host_parallel_for((int)todo.size(), 2, [&](int t) {
+        const int j = work[todo[t]].first, k = work[todo[t]].second;
         jobs[j].hs[k] = cached_hits(scans[first[j] + k], poses[first[j] + k], bp, false);
     });
     {
@@ -1461,10 +1478,12 @@ long long scan_rays(const lgs_map* m, const ScanHits& h, std::vector<int4>& rays
 {
     int sx, sy;
     world_to_cell(m, h.sensor.x, h.sensor.y, sx, sy);
+    const size_t n2 = h.xy.size() & ~(size_t)1;
+    std::vector<int> c(n2);
+    cells_of_points(h.xy.data(), (long long)n2, m->min_x, m->min_y, m->res, c.data());
     long long keys = 0;
-    for (size_t k = 0; k + 1 < h.xy.size(); k += 2) {
-        int hx, hy;
-        world_to_cell(m, h.xy[k], h.xy[k + 1], hx, hy);
+    for (size_t k = 0; k < n2; k += 2) {
+        const int hx = c[k], hy = c[k + 1];
         rays.push_back(make_int4(sx, sy, hx, hy));
         const int L = std::max(std::abs(hx - sx), std::abs(hy - sy)) + 1;
         lens.push_back(L);
@@ -1483,6 +1502,39 @@ inline int bits_for(unsigned long long cells)
 RayMap raymap_of(const lgs_map* m, unsigned long long base)
 {
     return RayMap{ base, m->w, m->h, m->d_cells, m->d_hit, m->d_miss, m->d_palloc, m->ps, m->npx };
+}
+
+// LGS_STEP_TIMING=1: host wall time of the latest-map step's phases, averaged
+// over every 2000 steps, on stderr (diagnostics)
+struct StepTiming {
+    bool on = std::getenv("LGS_STEP_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point prev;
+    double us[8] = {};
+    long long steps = 0;
+    void start()
+    {
+        if (on) prev = std::chrono::steady_clock::now();
+    }
+    void lap(int k)
+    {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        us[k] += std::chrono::duration<double, std::micro>(now - prev).count();
+        prev = now;
+    }
+    void done()
+    {
+        if (!on || ++steps % 2000) return;
+        std::fprintf(stderr, "latest step host us: finish %.1f hits %.1f geom %.1f pre %.1f rays(latest) %.1f "
+                     "rays(local)+shift %.1f stage %.1f launch %.1f\n", us[0] / 2000, us[1] / 2000, us[2] / 2000,
+                     us[6] / 2000, us[7] / 2000, us[3] / 2000, us[4] / 2000, us[5] / 2000);
+        for (double& u : us) u = 0;
+    }
+};
+StepTiming& step_timing()
+{
+    static StepTiming t;
+    return t;
 }
 
 // One incremental step: E = the window's newest scan; L = its oldest (evict).
@@ -1507,8 +1559,11 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
     std::vector<int> lens;
     rays.reserve(E->xy.size());
     lens.reserve(E->xy.size());
+    StepTiming& tm = step_timing();
+    tm.lap(6);
     const long long nE = scan_rays(latest, *E, rays, lens);
     const size_t nrE = rays.size();
+    tm.lap(7);
     long long nloc = local ? scan_rays(local, *E, rays, lens) : 0;
     // the local map's cells of E's rays are usually its latest-map cells
     // shifted by whole cells (both maps keep the lattice of their common
@@ -1528,6 +1583,7 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
             lens.resize(nrE);
         }
     }
+    tm.lap(3);
     const long long keys = lshift ? nE : nE + nloc;
     const long long nr = (long long)rays.size();
     const unsigned long long lat_cells = (unsigned long long)latest->w * latest->h;
@@ -1594,6 +1650,7 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
     }
     J.tbl = C.d_tbl;
     fetch_async(ctx, d_stage, pin, total);
+    tm.lap(4);
     unsigned* d_keys = (unsigned*)ctx->ensure(S_RAY2, sizeof(unsigned) * (size_t)std::max(1LL, keys));
     unsigned* d_tmp = (unsigned*)ctx->ensure(S_RAY3, sizeof(unsigned) * (size_t)std::max(1LL, keys));
     if (nr > 0) {
@@ -1637,6 +1694,8 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
     record_writer(C, st, latest, local);
+    tm.lap(5);
+    tm.done();
     if (evict) C.retired.push_back(std::move(L.buf));
     C.slot[es] = LatestSlot{ escan->uid, epose, stamp, buf, 0, nE };
     C.window.push_back(es);
@@ -1655,7 +1714,9 @@ void latest_rebuild(lgs_ctx* ctx, lgs_map* latest, lgs_map* local, const lgs_sca
                     const lgs_pose2d* poses, int n, const lgs_builder_params* bp)
 {
     LatestCache& C = cache_of(latest);
+    step_timing().start();
     C.finish();
+    step_timing().lap(0);
     latest->ctx = ctx;
     if (local) local->ctx = ctx;
     std::vector<MapJob> jobs(local ? 2 : 1);
@@ -1664,6 +1725,7 @@ void latest_rebuild(lgs_ctx* ctx, lgs_map* latest, lgs_map* local, const lgs_sca
     std::vector<std::array<double, 4>> box;
     if (local) hits_and_boxes(jobs, { 0, n - 1 }, { n, 1 }, scans, poses, bp, box);
     else hits_and_boxes(jobs, { 0 }, { n }, scans, poses, bp, box);
+    step_timing().lap(1);
     if (local) {
         // the insert's box is the scan's own (sensor included, :346-352), not
         // ConstructMapFromScans' running box with its DBL_MIN start
@@ -1687,6 +1749,7 @@ void latest_rebuild(lgs_ctx* ctx, lgs_map* latest, lgs_map* local, const lgs_sca
         }
     }
     if (shift_ok && same_geom && std::memcmp(bpv, C.bpv, sizeof(bpv)) == 0) {
+        step_timing().lap(2);
         latest_step(ctx, C, latest, local, scans[n - 1], poses[n - 1], jobs[0].hs[n - 1], evict, bp);
         return;
     }

@@ -431,6 +431,8 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n);
 // config-4 frontend), a kernel reads the staging over the host link in one
 // round trip.  dst and src 16-byte aligned.
 void fetch_async(lgs_ctx* ctx, void* dst, const void* src, size_t bytes);
+// floor((xy[j] - (j odd ? my : mx)) / res) for j < n2 (host_simd.cpp)
+void cells_of_points(const double* xy, long long n2, double mx, double my, double res, int* out);
 inline void scan_to_device(lgs_ctx* ctx, const lgs_scan* s) { scans_to_device(ctx, &s, 1); }
 
 // Order a read of g's cells on ctx's stream after a pending asynchronous write
