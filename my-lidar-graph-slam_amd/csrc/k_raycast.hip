@@ -510,15 +510,15 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long x, i
     return ((unsigned long long)hi << 32) | lo;
 }
 
-// walk_run by a whole wave: the lanes load 64 words of the run at once and
-// every lane then follows the same (uniform) walk over them from registers
+// walk_run by a whole wave: the lanes hold 64 words of the run (from word
+// w0, preloaded by the caller) and every lane follows the same (uniform) walk
+// over them from registers; a run past them reloads
 __device__ double walk_run_wave(long long i, double v, uint32_t& nh, uint32_t& nm, const RunBits& rb,
-                                const BayesChains* __restrict__ ch, const BayesK& K)
+                                const BayesChains* __restrict__ ch, const BayesK& K, long long w0,
+                                unsigned long long hwl, unsigned long long ewl)
 {
     const int lane = (int)__lane_id();
     ChainState cs(v, ch);
-    long long w0 = -1;
-    unsigned long long hwl = 0, ewl = 0;
     for (long long p = i;;) {
         const long long w = p >> 6;
         if (w0 < 0 || w - w0 >= 64) {
@@ -528,6 +528,22 @@ __device__ double walk_run_wave(long long i, double v, uint32_t& nh, uint32_t& n
             ewl = (wl < rb.nw) ? rb.endw[wl] : ~0ull;
         }
         const int sh = (int)(p & 63);
+        const bool id_miss = K.miss_fixed && v == kPMin, id_hit = K.hit_fixed && v == kPMax;
+        if (sh == 0 && (id_miss || id_hit)) {
+            // whole words of identity updates (no run end, no hit -- resp.
+            // miss -- in them): the lanes find the first word that is not,
+            // one ballot for up to 64 words (cells next to a sensor see
+            // thousands of misses at the fixed point)
+            const int rel = (int)(w - w0);
+            const bool stop = ewl != 0ull || (id_miss ? hwl != 0ull : ~hwl != 0ull);
+            const unsigned long long b = __ballot(lane >= rel && stop);
+            const int k = (b ? __ffsll((long long)b) - 1 : 64) - rel;
+            if (k > 0) {
+                if (id_miss) nm += 64u * (unsigned)k; else nh += 64u * (unsigned)k;
+                p += 64LL * k;
+                continue;
+            }
+        }
         const unsigned long long hm = readlane64(hwl, (int)(w - w0)) >> sh;
         const unsigned long long em = readlane64(ewl, (int)(w - w0)) >> sh;
         const int cnt = em ? __ffsll((long long)em) : 64 - sh;
@@ -642,22 +658,52 @@ __global__ __launch_bounds__(256) void k_apply_long(const WindowJob* __restrict_
     const int lane = (int)__lane_id();
     const unsigned nq = ll.count[0];
     const unsigned waves = gridDim.x * (blockDim.x / 64);
+#ifdef LGS_PROBE
+    const unsigned long long t_start = wall_clock64();
+    unsigned n_cells = 0;
+#endif
     for (unsigned k = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < nq; k += waves) {
         const unsigned cell = ll.cells[k];
         const unsigned long long* e = J.tbl + (size_t)cell * kSlots;
         const unsigned long long xl = (lane < J.nwin) ? e[J.order[lane]] : 0ull;
+#ifdef LGS_PROBE
+        unsigned long long t1 = 0, t2 = 0;
+        if (blockIdx.x == 0 && threadIdx.x == 0) { (void)__builtin_amdgcn_readfirstlane((int)xl); t1 = wall_clock64(); }
+#endif
+        // the first 64 words of every slot's long run, all loads in flight at
+        // once (one memory round trip for the cell, not one per slot)
+        unsigned long long hw[kSlots], ew[kSlots];
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) {
+            hw[q] = 0ull, ew[q] = ~0ull;
+            if (q < J.nwin) {
+                const int s = J.order[q];
+                const unsigned long long x = readlane64(xl, q);
+                if ((unsigned)(x >> 32) == J.st.s[s] && ((unsigned)x & kLongRun)) {
+                    const long long wl = ((long long)((unsigned)x & ~kLongRun) >> 6) + lane;
+                    const RunBits& rb = J.slot[s].rb;
+                    if (wl < rb.nw) hw[q] = rb.hitw[wl], ew[q] = rb.endw[wl];
+                }
+            }
+        }
+#ifdef LGS_PROBE
+        if (blockIdx.x == 0 && threadIdx.x == 0) { (void)__builtin_amdgcn_readfirstlane((int)(hw[0] ^ ew[J.nwin - 1])); t2 = wall_clock64(); }
+#endif
         double v = 0.0;
         ChainState cs(v, ch);
         uint32_t nh = 0, nm = 0;
         bool any = false;
-        for (int q = 0; q < J.nwin; ++q) {
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) {
+            if (q >= J.nwin) continue;
             const int s = J.order[q];
             const unsigned long long x = readlane64(xl, q);
             if ((unsigned)(x >> 32) != J.st.s[s]) continue;
             any = true;
             const unsigned en = (unsigned)x;
             if (en & kLongRun) {
-                v = walk_run_wave((long long)(en & ~kLongRun), v, nh, nm, J.slot[s].rb, ch, K);
+                const long long p = (long long)(en & ~kLongRun);
+                v = walk_run_wave(p, v, nh, nm, J.slot[s].rb, ch, K, p >> 6, hw[q], ew[q]);
                 cs = ChainState(v, ch);
             } else {
                 const int len = (int)(en >> 26);
@@ -668,6 +714,12 @@ __global__ __launch_bounds__(256) void k_apply_long(const WindowJob* __restrict_
                 v = apply_word(v, cs, bits, ((1ull << len) - 1ull) & ~bits, len, ch, K);
             }
         }
+#ifdef LGS_PROBE
+        ++n_cells;
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            printf("probe long cell %u: tbl %.2f us, preload %.2f us, walk %.2f us; hits %u misses %u\n", cell,
+                   0.01 * (double)(t1 - t_start), 0.01 * (double)(t2 - t1), 0.01 * (double)(wall_clock64() - t2), nh, nm);
+#endif
         if (lane == 0) {
             if (any) mark_patch(J.latest, cell);
             J.latest.cells[cell] = v;
@@ -675,6 +727,11 @@ __global__ __launch_bounds__(256) void k_apply_long(const WindowJob* __restrict_
             J.latest.miss[cell] = nm;
         }
     }
+#ifdef LGS_PROBE
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+        printf("probe k_apply_long: cells %u waves %u, wave 0: %u cells in %.2f us\n", nq, waves, n_cells,
+               0.01 * (double)(wall_clock64() - t_start));
+#endif
     // the last workgroup clears the queue for the next step
     __syncthreads();
     if (threadIdx.x == 0 && atomicAdd(ll.count + 1, 1u) == gridDim.x - 1) {
