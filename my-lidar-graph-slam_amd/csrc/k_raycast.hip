@@ -184,12 +184,14 @@ struct RunIndex {
     unsigned long long* tbl;        // null: no index
     long long nidx;
     SlotStamps st;
+    unsigned* clear;                // non-null: a word zeroed by thread 0 (the long-cell queue count)
 };
 __global__ __launch_bounds__(256) void k_runmask(const unsigned* __restrict__ keys, long long n, int rsh,
                                                  unsigned long long* __restrict__ hitw,
                                                  unsigned long long* __restrict__ endw, RunIndex ix)
 {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ix.clear && i == 0) *ix.clear = 0u;
     const bool in = i < n;
     const unsigned k = in ? keys[i] : 0u;
     const bool last = in && (i + 1 >= n || (keys[i + 1] >> rsh) != (k >> rsh));
@@ -499,7 +501,7 @@ struct WindowJob {
 // with a chain of dependent loads per word; they are queued instead
 // (long_cells) and recomputed by k_apply_long, one wave per cell.
 struct LongList {
-    unsigned* count;     // [0] cells queued, [1] k_apply_long workgroups done (zero between steps)
+    unsigned* count;     // cells queued (zeroed by the step's k_runmask before k_apply_window)
     unsigned* cells;
 };
 
@@ -570,10 +572,19 @@ __device__ void recompute_cell(const WindowJob& J, unsigned cell, const BayesCha
 #pragma unroll
     for (int q = 0; q < kSlots; ++q)
         if (q < J.nwin && (unsigned)(x[q] >> 32) == J.st.s[J.order[q]] && ((unsigned)x[q] & kLongRun)) lng = true;
-    if (lng) {
-        ll.cells[atomicAdd(ll.count, 1u)] = cell;
-        return;
+    {
+        // one queue atomic per wave (hundreds of cells per step: same-address
+        // device atomics serialise)
+        const unsigned long long b = __ballot(lng);
+        if (b) {
+            const int lane = (int)__lane_id(), leader = __ffsll((long long)b) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(ll.count, (unsigned)__popcll(b));
+            base = __shfl(base, leader);
+            if (lng) ll.cells[base + (unsigned)__popcll(b & ((1ull << lane) - 1ull))] = cell;
+        }
     }
+    if (lng) return;
     // the slots' runs, oldest first, concatenated into 64-update words; each
     // word is applied with the chain state carried across slots (a cell that
     // saw only misses takes one chain look-up for the whole window)
@@ -732,12 +743,6 @@ __global__ __launch_bounds__(256) void k_apply_long(const WindowJob* __restrict_
         printf("probe k_apply_long: cells %u waves %u, wave 0: %u cells in %.2f us\n", nq, waves, n_cells,
                0.01 * (double)(wall_clock64() - t_start));
 #endif
-    // the last workgroup clears the queue for the next step
-    __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(ll.count + 1, 1u) == gridDim.x - 1) {
-        ll.count[0] = 0;
-        ll.count[1] = 0;
-    }
 }
 
 // MapSaver::DrawMap (C/io/map_saver.cpp:276-313) for the W x H cells of the
@@ -1719,17 +1724,6 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
         LGS_HIP_CHECK(hipGetLastError());
     }
     const long long nL = J.nL;
-    const int tok = ctx->timing_begin(K_RAY_APPLY, 4.0 * (double)(keys + nL));
-    if (keys > 0) {
-        keysort(ctx, d_keys, buf->keys, d_tmp, keys, kTagShift, bits_for(cells));
-        RunIndex ix{ C.d_tbl, nE, J.st };
-        const long long nw = (keys + 63) / 64;
-        hipLaunchKernelGGL(k_runmask, dim3((unsigned)((keys + 255) / 256)), dim3(256), 0, st, buf->keys, keys, 1,
-                           buf->hitw, buf->endw, ix);
-        hipLaunchKernelGGL(k_runsummary, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, buf->hitw, buf->endw,
-                           nw, buf->hit2, buf->miss2, buf->end2);
-    }
-    const long long nthreads = nE + nloc + nL;
     if (nE + nL > C.long_cap) {
         if (C.d_long) LGS_HIP_CHECK(hipFree(C.d_long));
         C.d_long = nullptr;
@@ -1737,9 +1731,20 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
         const long long cap = (nE + nL) * 2 + 4096;
         if (hipMalloc(&C.d_long, sizeof(unsigned) * (size_t)(cap + 2)) != hipSuccess)
             throw Error(LGS_ERR_OOM, "hipMalloc failed for the long-run queue");
-        LGS_HIP_CHECK(hipMemsetAsync(C.d_long, 0, 2 * sizeof(unsigned), st));
         C.long_cap = cap;
     }
+    const int tok = ctx->timing_begin(K_RAY_APPLY, 4.0 * (double)(keys + nL));
+    if (keys == 0) LGS_HIP_CHECK(hipMemsetAsync(C.d_long, 0, sizeof(unsigned), st));   // (k_runmask clears it)
+    if (keys > 0) {
+        keysort(ctx, d_keys, buf->keys, d_tmp, keys, kTagShift, bits_for(cells));
+        RunIndex ix{ C.d_tbl, nE, J.st, C.d_long };
+        const long long nw = (keys + 63) / 64;
+        hipLaunchKernelGGL(k_runmask, dim3((unsigned)((keys + 255) / 256)), dim3(256), 0, st, buf->keys, keys, 1,
+                           buf->hitw, buf->endw, ix);
+        hipLaunchKernelGGL(k_runsummary, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, buf->hitw, buf->endw,
+                           nw, buf->hit2, buf->miss2, buf->end2);
+    }
+    const long long nthreads = nE + nloc + nL;
     const LongList ll{ C.d_long, C.d_long + 2 };
     if (nthreads > 0) {
         hipLaunchKernelGGL(k_apply_window, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, st,
