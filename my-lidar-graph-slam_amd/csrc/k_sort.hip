@@ -5,21 +5,11 @@
 // key per visited cell in ray order; a STABLE sort on the cell bits of the keys
 // makes each cell's updates one contiguous run that keeps that order.
 //
-//   k_sort_hist   one read of the keys: the digit histograms of every pass
-//                 (LDS, then device-scope atomics); the last workgroup turns
-//                 them into each pass's exclusive digit offsets and clears the
-//                 accumulators for the next sort (the control block stays zero
-//                 between sorts, no memset per call)
-//   k_sort_pass   one launch per digit (<= 8 bits): tiles of 256 x KPT keys
-//                 taken in ticket order; per wave a stable rank of each key
-//                 among equal digits (LDS peer masks), per tile the digit
-//                 counts published as aggregates and turned into inclusive
-//                 prefixes by a decoupled look-back over earlier tiles (status
-//                 words tagged with a per-pass stamp: no clearing); keys are
-//                 reordered by digit in LDS and written out in digit runs
-//
-// Each workgroup only waits on tiles with lower tickets, which belong to
-// workgroups that started before it, so the look-back always drains.
+//   large sorts   one pass per 8-bit digit, reduce-then-scan: per-tile digit
+//                 counts (k_sort_up), a device scan of the digit-major count
+//                 array (k_scan_chunks + k_scan_top), then per tile stable
+//                 ranks (per-wave LDS peer masks), an LDS reorder by digit and
+//                 digit runs written at their offsets (k_sort_down)
 //
 //   k_sort_wide   sorts that fit the device at once: every pass in one
 //                 launch, 8192-key tiles, digits of up to 10 bits, ranks from
@@ -34,155 +24,169 @@ namespace {
 
 constexpr int kSortThreads = 256;
 constexpr int kSortRadix = 256;        // bins per pass (digits of at most 8 bits)
-constexpr int kSortMaxPasses = 4;
-// control block (unsigned words, S_RAY0): zero between sorts
-constexpr int kHistLanes = 8;                                // accumulator copies (workgroup % 8): less contention
-constexpr int kCtlHist = 0;                                  // [lane][pass][256] accumulators
-constexpr int kCtlDone = kHistLanes * kSortMaxPasses * kSortRadix;   // workgroups finished k_sort_hist
-constexpr int kCtlTicket = kCtlDone + 1;                     // [pass] tile tickets
-constexpr int kCtlBar = kCtlDone + 8;                        // k_sort_wide grid barrier, workgroups done
-constexpr int kCtlOffs = kCtlDone + 64;                      // [pass][256] exclusive digit offsets
-constexpr int kCtlWords = kCtlOffs + kSortMaxPasses * kSortRadix;
+// control words (S_RAY0): k_sort_wide's grid barrier [arrived, done], zero
+// between sorts (the last workgroup out resets them)
+constexpr int kCtlBar = 0;
+constexpr int kCtlWords = 8;
 
-constexpr unsigned long long kFlagAgg = 1ull << 30, kFlagPrefix = 2ull << 30;
-constexpr int kHistRun = 16;          // consecutive keys per thread in k_sort_hist
-constexpr int kLookback = 16;         // predecessor tiles read at once in the look-back
-constexpr unsigned long long kCountMask = (1ull << 30) - 1;
+// Large sorts, one digit pass = three steps with no chain between tiles
+// (a decoupled look-back propagates prefixes tile to tile at a cross-XCD
+// round trip per window of predecessors: ~0.33 ms per pass of 20M keys):
+//   k_sort_up     per 4096-key tile the digit counts, stored digit-major
+//                 (counts[d * tiles + tile])
+//   k_scan_chunks exclusive scan of 4096-entry chunks of that array in place,
+//   k_scan_top    and of the chunk totals: offset(d, tile) = chunk scan +
+//                 scanned chunk total -- every digit's start in the output
+//                 plus the keys of that digit in the tiles before this one
+//   k_sort_down   per tile: stable ranks (per-wave LDS peer masks), the tile
+//                 reordered by digit in LDS, digit runs written at the offsets
+constexpr int kTileKPT = 16, kTile = kSortThreads * kTileKPT;   // 4096 keys per tile
+constexpr int kScanChunk = kSortThreads * 16;                   // 4096 counts per scan chunk
 
-__device__ __forceinline__ unsigned ld_agent(const unsigned* p)
+// one key's stable rank among the earlier keys of its wave with the same
+// digit; wcnt/mw: the wave's digit counts and peer masks (see k_sort_wide)
+__device__ __forceinline__ unsigned wave_rank(bool valid, unsigned d, unsigned* __restrict__ wcnt,
+                                              unsigned long long* __restrict__ mw, unsigned long long me,
+                                              unsigned long long lt)
 {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long peers = 0;
+    if (valid) {
+        __hip_atomic_fetch_or(&mw[d], me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        peers = __hip_atomic_load(&mw[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    const unsigned base = valid ? wcnt[d] : 0u;
+    if (valid && !(peers & lt)) {
+        wcnt[d] = base + (unsigned)__popcll(peers);
+        __hip_atomic_store(&mw[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return base + (unsigned)__popcll(peers & lt);
 }
 
-__global__ __launch_bounds__(kSortThreads) void k_sort_hist(const unsigned* __restrict__ keys, long long n, int lo,
-                                                            int dbits, int bits, int passes,
-                                                            unsigned* __restrict__ ctl)
+__global__ __launch_bounds__(kSortThreads) void k_sort_up(const unsigned* __restrict__ in, long long n, int shift,
+                                                          int nb, unsigned* __restrict__ counts, unsigned ntiles)
 {
-    __shared__ unsigned h[kSortMaxPasses][kSortRadix];
-    __shared__ int last;
-    const int tid = threadIdx.x;
-    for (int p = 0; p < passes; ++p) h[p][tid] = 0;
-    __syncthreads();
-    // each thread counts kHistRun consecutive keys per chunk; equal digits of
-    // neighbouring keys (ray-ordered keys share their high digits) are
-    // counted in a register and added to LDS once per run
-    const long long stride = (long long)gridDim.x * kSortThreads * kHistRun;
-    for (long long i0 = ((long long)blockIdx.x * kSortThreads + tid) * kHistRun; i0 < n; i0 += stride) {
-        const int m = (int)min((long long)kHistRun, n - i0);
-        unsigned k[kHistRun];
-#pragma unroll
-        for (int q = 0; q < kHistRun; ++q) k[q] = (q < m) ? keys[i0 + q] : 0u;
-        for (int p = 0; p < passes; ++p) {
-            const int sh = lo + p * dbits;
-            const unsigned mask = (1u << min(dbits, bits - p * dbits)) - 1u;
-            unsigned cur = (k[0] >> sh) & mask, cnt = 0;
-#pragma unroll
-            for (int q = 0; q < kHistRun; ++q) {
-                const unsigned d = (k[q] >> sh) & mask;
-                if (q < m && d != cur) {
-                    atomicAdd(&h[p][cur], cnt);
-                    cur = d, cnt = 0;
-                }
-                cnt += (q < m) ? 1u : 0u;
-            }
-            atomicAdd(&h[p][cur], cnt);
-        }
-    }
-    __syncthreads();
-    unsigned* acc = ctl + kCtlHist + (blockIdx.x % kHistLanes) * kSortMaxPasses * kSortRadix;
-    for (int p = 0; p < passes; ++p)
-        if (h[p][tid]) __hip_atomic_fetch_add(acc + p * kSortRadix + tid, h[p][tid], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence();
-    __syncthreads();
-    if (tid == 0)
-        last = __hip_atomic_fetch_add(ctl + kCtlDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-               gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    // last workgroup: exclusive scan of each pass's histogram (one wave per
-    // pass, 4 digits per lane), then clear the accumulators and counters
-    const int w = tid >> 6, lane = tid & 63;
-    if (w < passes) {
-        unsigned v[4], s = 0;
-        for (int j = 0; j < 4; ++j) {
-            v[j] = 0;
-            for (int l = 0; l < kHistLanes; ++l)
-                v[j] += ld_agent(ctl + kCtlHist + (l * kSortMaxPasses + w) * kSortRadix + lane * 4 + j);
-            s += v[j];
-        }
-        unsigned incl = s;
-        for (int o = 1; o < 64; o <<= 1) {
-            const unsigned t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
-        }
-        unsigned run = incl - s;
-        for (int j = 0; j < 4; ++j) {
-            ctl[kCtlOffs + w * kSortRadix + lane * 4 + j] = run;
-            run += v[j];
-        }
-    }
-    __syncthreads();
-    for (int l = 0; l < kHistLanes; ++l)
-        for (int p = 0; p < passes; ++p)
-            __hip_atomic_store(ctl + kCtlHist + (l * kSortMaxPasses + p) * kSortRadix + tid, 0u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    if (tid <= kSortMaxPasses)
-        __hip_atomic_store(ctl + kCtlDone + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int KPT>
-__global__ __launch_bounds__(kSortThreads) void k_sort_pass(const unsigned* __restrict__ in,
-                                                            unsigned* __restrict__ out, long long n, int shift,
-                                                            int nb, const unsigned* __restrict__ offs,
-                                                            unsigned long long* __restrict__ status,
-                                                            unsigned* __restrict__ ticket, unsigned stamp)
-{
-    constexpr int TILE = kSortThreads * KPT;
-    __shared__ unsigned keys_s[TILE];
     __shared__ unsigned wcnt[4][kSortRadix];
-    __shared__ unsigned dstart[kSortRadix];
-    __shared__ unsigned gbase[kSortRadix];
-    __shared__ unsigned wsum[4];
-    __shared__ unsigned tile_s;
-    __shared__ unsigned long long wmask[4][kSortRadix];   // per-wave peer masks (k_sort_wide)
+    __shared__ unsigned long long wmask[4][kSortRadix];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const unsigned mask = (1u << nb) - 1u;
     wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
     wmask[0][tid] = wmask[1][tid] = wmask[2][tid] = wmask[3][tid] = 0ull;
-    if (tid == 0) tile_s = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    const long long tile = tile_s;
-    const long long t0 = tile * TILE;
-    // wave w ranks tile positions [w * 64 KPT, (w + 1) * 64 KPT) in order
-    unsigned k[KPT], rank[KPT];
-    const long long p0 = t0 + (long long)w * 64 * KPT + lane;
+    const long long p0 = (long long)blockIdx.x * kTile + (long long)w * 64 * kTileKPT + lane;
+    unsigned k[kTileKPT];
 #pragma unroll
-    for (int i = 0; i < KPT; ++i) {
+    for (int i = 0; i < kTileKPT; ++i) {
         const long long p = p0 + 64 * i;
         k[i] = (p < n) ? in[p] : 0u;
     }
     const unsigned long long me = 1ull << lane, lt = me - 1ull;
-    unsigned long long* mw = wmask[w];
 #pragma unroll
-    for (int i = 0; i < KPT; ++i) {
-        const bool valid = p0 + 64 * i < n;
-        const unsigned d = (k[i] >> shift) & mask;
-        unsigned long long peers = 0;
-        if (valid) {
-            __hip_atomic_fetch_or(&mw[d], me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            peers = __hip_atomic_load(&mw[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int i = 0; i < kTileKPT; ++i)
+        (void)wave_rank(p0 + 64 * i < n, (k[i] >> shift) & mask, wcnt[w], wmask[w], me, lt);
+    __syncthreads();
+    counts[(size_t)tid * ntiles + blockIdx.x] = wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+}
+
+// exclusive scan of the 256 values of the block (thread order); *total: their sum
+__device__ __forceinline__ unsigned block_scan256(unsigned v, unsigned* ws4, unsigned* total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) ws4[w] = incl;
+    __syncthreads();
+    unsigned wo = 0;
+    for (int q = 0; q < w; ++q) wo += ws4[q];
+    if (total) *total = ws4[0] + ws4[1] + ws4[2] + ws4[3];
+    return wo + incl - v;
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_scan_chunks(unsigned* __restrict__ a, long long m,
+                                                              unsigned* __restrict__ csum)
+{
+    __shared__ unsigned ws4[4];
+    const long long b0 = (long long)blockIdx.x * kScanChunk + (long long)threadIdx.x * 16;
+    unsigned v[16], s = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        v[i] = (b0 + i < m) ? a[b0 + i] : 0u;
+        s += v[i];
+    }
+    unsigned tot = 0;
+    unsigned run = block_scan256(s, ws4, &tot);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (b0 + i < m) {
+            a[b0 + i] = run;
+            run += v[i];
         }
-        const unsigned base = valid ? wcnt[w][d] : 0u;
-        rank[i] = base + (unsigned)__popcll(peers & lt);
-        if (valid && !(peers & lt)) {
-            wcnt[w][d] = base + (unsigned)__popcll(peers);
-            __hip_atomic_store(&mw[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (threadIdx.x == 0) csum[blockIdx.x] = tot;
+}
+
+// one workgroup: exclusive scan of the chunk totals, in place
+__global__ __launch_bounds__(kSortThreads) void k_scan_top(unsigned* __restrict__ csum, int nc)
+{
+    __shared__ unsigned ws4[4];
+    unsigned carry = 0;
+    for (int c0 = 0; c0 < nc; c0 += kSortThreads * 16) {
+        const int b0 = c0 + (int)threadIdx.x * 16;
+        unsigned v[16], s = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            v[i] = (b0 + i < nc) ? csum[b0 + i] : 0u;
+            s += v[i];
         }
+        unsigned tot = 0;
+        unsigned run = carry + block_scan256(s, ws4, &tot);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (b0 + i < nc) {
+                csum[b0 + i] = run;
+                run += v[i];
+            }
+        carry += tot;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_sort_down(const unsigned* __restrict__ in,
+                                                            unsigned* __restrict__ out, long long n, int shift,
+                                                            int nb, const unsigned* __restrict__ offs,
+                                                            const unsigned* __restrict__ csum, unsigned ntiles)
+{
+    __shared__ unsigned keys_s[kTile];
+    __shared__ unsigned wcnt[4][kSortRadix];
+    __shared__ unsigned long long wmask[4][kSortRadix];
+    __shared__ unsigned dstart[kSortRadix];
+    __shared__ unsigned gbase[kSortRadix];
+    __shared__ unsigned ws4[4];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const unsigned mask = (1u << nb) - 1u;
+    const unsigned tile = blockIdx.x;
+    wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+    wmask[0][tid] = wmask[1][tid] = wmask[2][tid] = wmask[3][tid] = 0ull;
+    {
+        const size_t q = (size_t)tid * ntiles + tile;   // digit tid's offset for this tile
+        gbase[tid] = offs[q] + csum[q / kScanChunk];
     }
     __syncthreads();
-    // per digit: exclusive prefix over the waves, tile total, publication
+    const long long t0 = (long long)tile * kTile;
+    const long long p0 = t0 + (long long)w * 64 * kTileKPT + lane;
+    unsigned k[kTileKPT], rank[kTileKPT];
+#pragma unroll
+    for (int i = 0; i < kTileKPT; ++i) {
+        const long long p = p0 + 64 * i;
+        k[i] = (p < n) ? in[p] : 0u;
+    }
+    const unsigned long long me = 1ull << lane, lt = me - 1ull;
+#pragma unroll
+    for (int i = 0; i < kTileKPT; ++i)
+        rank[i] = wave_rank(p0 + 64 * i < n, (k[i] >> shift) & mask, wcnt[w], wmask[w], me, lt);
+    __syncthreads();
+    // digit tid: exclusive prefix over the waves and the tile-local start
     const int d = tid;
     const unsigned c0 = wcnt[0][d], c1 = wcnt[1][d], c2 = wcnt[2][d], c3 = wcnt[3][d];
     const unsigned tot = c0 + c1 + c2 + c3;
@@ -190,62 +194,16 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_pass(const unsigned* __re
     wcnt[1][d] = c0;
     wcnt[2][d] = c0 + c1;
     wcnt[3][d] = c0 + c1 + c2;
-    const unsigned long long tag = (unsigned long long)stamp << 32;
-    unsigned long long* st = status + (size_t)tile * kSortRadix + d;
-    __hip_atomic_store(st, tag | (tile == 0 ? kFlagPrefix : kFlagAgg) | tot, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    // tile-local digit starts: exclusive scan of tot over the 256 digits
-    unsigned incl = tot;
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
-    if (lane == 63) wsum[w] = incl;
-    // decoupled look-back over the earlier tiles
-    // (kLookback predecessors per round, loads in flight together; a round
-    // consumes tiles up to the first one not yet published)
-    unsigned excl = 0;
-    if (tile > 0) {
-        long long j = tile - 1;
-        for (bool done = false; !done;) {
-            unsigned long long v[kLookback];
-#pragma unroll
-            for (int q = 0; q < kLookback; ++q)
-                v[q] = (j - q >= 0) ? __hip_atomic_load(status + (size_t)(j - q) * kSortRadix + d, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT)
-                                    : 0ull;
-            int used = 0;
-            bool stop = false;   // at the first unpublished tile, or after a prefix
-#pragma unroll
-            for (int q = 0; q < kLookback; ++q) {
-                const bool ready = (v[q] >> 32) == stamp && (v[q] & (kFlagAgg | kFlagPrefix));
-                if (!stop && ready) {
-                    excl += (unsigned)(v[q] & kCountMask);
-                    used = q + 1;
-                    done = (v[q] & kFlagPrefix) != 0;
-                }
-                stop = stop || !ready || done;
-            }
-            j -= used;
-            if (!done && used == 0) __builtin_amdgcn_s_sleep(1);
-        }
-        __hip_atomic_store(st, tag | kFlagPrefix | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    gbase[d] = offs[d] + excl;
+    dstart[d] = block_scan256(tot, ws4, nullptr);
     __syncthreads();
-    unsigned wo = 0;
-    for (int q = 0; q < w; ++q) wo += wsum[q];
-    dstart[d] = wo + incl - tot;
-    __syncthreads();
-    // reorder the tile by digit in LDS (stable), then write digit runs
 #pragma unroll
-    for (int i = 0; i < KPT; ++i)
+    for (int i = 0; i < kTileKPT; ++i)
         if (p0 + 64 * i < n) {
             const unsigned dd = (k[i] >> shift) & mask;
             keys_s[dstart[dd] + wcnt[w][dd] + rank[i]] = k[i];
         }
     __syncthreads();
-    const int nvalid = (int)min((long long)TILE, n - t0);
+    const int nvalid = (int)min((long long)kTile, n - t0);
     for (int j = tid; j < nvalid; j += kSortThreads) {
         const unsigned key = keys_s[j];
         const unsigned dd = (key >> shift) & mask;
@@ -515,33 +473,25 @@ void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, lon
             return;
         }
     }
+    // reduce-then-scan passes of 8-bit digits
     const int passes = (bits + 7) / 8;
     const int dbits = (bits + passes - 1) / passes;
-    // 4096-key tiles (a short look-back chain); 1024-key tiles only for sorts
-    // too small to give 64 workgroups
-    const bool big = n >= 64LL * 4096;
-    const int tile = kSortThreads * (big ? 16 : 4);
-    const long long tiles = (n + tile - 1) / tile;
-    unsigned long long* status = (unsigned long long*)ctx->ensure(
-        S_RAY1, sizeof(unsigned long long) * (size_t)tiles * kSortRadix * (size_t)passes);
-    const unsigned hist_blocks =
-        (unsigned)std::min<long long>((n + kSortThreads * kHistRun - 1) / (kSortThreads * kHistRun), 2048);
-    hipLaunchKernelGGL(k_sort_hist, dim3(hist_blocks), dim3(kSortThreads), 0, st, in, n, lo, dbits, bits, passes,
-                       ctl);
-    LGS_HIP_CHECK(hipGetLastError());
+    const long long tiles = (n + kTile - 1) / kTile;
+    const long long m = tiles * kSortRadix;
+    const long long nc = (m + kScanChunk - 1) / kScanChunk;
+    unsigned* counts = (unsigned*)ctx->ensure(S_RAY1, sizeof(unsigned) * (size_t)(m + nc));
+    unsigned* csum = counts + m;
     for (int p = 0; p < passes; ++p) {
         const unsigned* src = (p == 0) ? in : (((passes - p) % 2 == 1) ? tmp : out);
         unsigned* dst = ((passes - 1 - p) % 2 == 0) ? out : tmp;
         LGS_REQUIRE(dst != nullptr && src != nullptr, "keysort: tmp buffer needed for several passes");
-        const int nb = std::min(dbits, bits - p * dbits);
-        const unsigned stamp = (unsigned)ctx->next_stamp();
-        unsigned long long* stp = status + (size_t)p * tiles * kSortRadix;
-        if (big)
-            hipLaunchKernelGGL(k_sort_pass<16>, dim3((unsigned)tiles), dim3(kSortThreads), 0, st, src, dst, n,
-                               lo + p * dbits, nb, ctl + kCtlOffs + p * kSortRadix, stp, ctl + kCtlTicket + p, stamp);
-        else
-            hipLaunchKernelGGL(k_sort_pass<4>, dim3((unsigned)tiles), dim3(kSortThreads), 0, st, src, dst, n,
-                               lo + p * dbits, nb, ctl + kCtlOffs + p * kSortRadix, stp, ctl + kCtlTicket + p, stamp);
+        const int nb = std::min(dbits, bits - p * dbits), sh = lo + p * dbits;
+        hipLaunchKernelGGL(k_sort_up, dim3((unsigned)tiles), dim3(kSortThreads), 0, st, src, n, sh, nb, counts,
+                           (unsigned)tiles);
+        hipLaunchKernelGGL(k_scan_chunks, dim3((unsigned)nc), dim3(kSortThreads), 0, st, counts, m, csum);
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kSortThreads), 0, st, csum, (int)nc);
+        hipLaunchKernelGGL(k_sort_down, dim3((unsigned)tiles), dim3(kSortThreads), 0, st, src, dst, n, sh, nb,
+                           (const unsigned*)counts, (const unsigned*)csum, (unsigned)tiles);
         LGS_HIP_CHECK(hipGetLastError());
     }
 }
