@@ -1,4 +1,8 @@
 #!/bin/bash
+# r03 A/B (rejected): k_coarse_lanes with one wave per angle
+# (LGS_LANES1=1 selected the variant kernel in the experiment build; the
+# variant is not in the library).  Tests with the variant, then alternated
+# config-2 and config-5 lines, then a rebuild-workload kernel trace.
 cd "${GRAFT_REPO_ROOT}" || exit 2
 export TMPDIR=/tmp
 O=gpurun_out/ab_lanes1; rm -rf $O; mkdir -p $O
