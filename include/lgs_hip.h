@@ -247,7 +247,14 @@ double* lgs_grid_device_ptr(lgs_grid* grid);
 /* PrecomputeGridMap(grid, win) into `out` (same geometry). */
 int  lgs_grid_precompute_max(lgs_ctx* ctx, const lgs_grid* in, int win, lgs_grid* out);
 
-/* ---- scans: uploaded once, resident in HBM ---- */
+/* ---- scans: a host copy, and a device copy resident in HBM once made ----
+ * lgs_scan_create copies the ranges/angles (host memory only: no device
+ * work, no synchronisation).  The first call that reads the scan on the
+ * device copies it there, on that call's context (pooled device buffers), and
+ * it stays resident until lgs_scan_destroy.  A scan belongs to the context
+ * that created it; other contexts use clones (lgs_loop_detect_rtcsm_multi
+ * re-creates them from the host copy).  Copies are waited for where a scan is
+ * read on a context other than the one that made them. */
 int  lgs_scan_create(lgs_ctx* ctx, const lgs_scan_host* host, lgs_scan** out);
 void lgs_scan_destroy(lgs_scan* scan);
 /* Number of beams, and (if the pointers are non-null) a copy of the ranges and
@@ -259,7 +266,7 @@ int  lgs_scan_get(const lgs_scan* scan, int* n, double* ranges, double* angles);
  * (launcher JSON "ScanInterpolator": DistScans 0.05, DistThresholdEmpty 0.25).
  * The relative sensor pose and min/max range are copied.  The recurrence is
  * sequential and uses glibc sincos/atan2/sqrt, so it runs on the host; the
- * result is uploaded once, like lgs_scan_create.  LGS_ERR_INVALID_ARG unless
+ * result is a scan like lgs_scan_create's.  LGS_ERR_INVALID_ARG unless
  * 0 < dist_scans <= dist_threshold_empty (both finite) and every point of
  * `in` is finite: the reference's loop would never end otherwise. */
 int  lgs_scan_interpolate(lgs_ctx* ctx, const lgs_scan* in, double dist_scans, double dist_threshold_empty,
