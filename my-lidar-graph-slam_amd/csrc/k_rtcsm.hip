@@ -51,20 +51,7 @@ namespace {
 // Superblock plane element: fp16 rounded toward +inf from the fp64 maxima, so
 // every stored value is >= the coarse values it bounds (the bound's sum is
 // taken in fp64).
-typedef _Float16 SuperT;
-__device__ __forceinline__ SuperT super_round_up(double m)
-{
-    // nearest float, then nearest half: one of the two fp16 neighbours of m
-    // (double rounding never skips past one), so a one-ulp step away from
-    // the lower neighbour gives the round-up; zeros are stored as +0, so
-    // nonnegative values order like their bit patterns (k_super_planes'
-    // horizontal max; a negative cell disables the bounds altogether)
-    const SuperT h = (SuperT)(float)m;
-    unsigned short b = __builtin_bit_cast(unsigned short, h);
-    if ((double)(float)h < m) b = (m > 0.0) ? (unsigned short)(b + 1) : (unsigned short)(b - 1);
-    if (m == 0.0) b = 0;
-    return __builtin_bit_cast(SuperT, b);
-}
+typedef _Float16 SuperT;   // built from the planes' fp16 round-up copies (half_round_up_bits)
 
 constexpr int kMaxBatchItems = 64;   // matches per batched launch chain (run_chunked)
 constexpr int kPipe = 16;   // seq_sum gathers in flight per batch (index arrays padded by 2*kPipe)
@@ -140,11 +127,22 @@ __device__ __forceinline__ Blk xcd_block()
 // Per-set superblock-plane job: one coarse map's padded phase planes.
 struct PlaneJob {
     RtcsmPlan pl;            // layout fields (Wqp, Hqp, pstride, pstride4, sub4, Wq4)
-    const double* planes;
+    const unsigned short* planes16;   // the planes rounded up to fp16 (same layout)
     SuperT* super;
-    int* negflag;
-    int pgen;
 };
+
+// The fp16 round-up copy of padded planes and the negative-cell stamp, for
+// planes the batched precompute did not write (phase-plane copies of
+// supplied or odd-sized coarse maps, windows > 8): one thread per cell.
+__global__ __launch_bounds__(256) void k_planes16(const double* __restrict__ P, unsigned short* __restrict__ P16,
+                                                  long long n, int* __restrict__ negflag, int pgen)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double v = P[i];
+    P16[i] = half_round_up_bits(v);
+    if (v < 0.0) *negflag = pgen;
+}
 
 // Generation-tagged counter (gen << 32 | count): a word left by an earlier
 // match counts as zero, so records need no memset.  Returns this caller's slot.
@@ -710,9 +708,10 @@ __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __re
 // with c < L is never selected, so superblocks with sbound < L are skipped.
 // --------------------------------------------------------------------------
 // The bound needs nonnegative terms (occupancy probabilities are); a negative
-// cell stamps *negflag with this build's generation and k_super then keeps
-// every superblock.  NaN cells are skipped by the max: a block whose sum is
-// NaN fails c > thr and is never selected anyway.
+// cell stamps *negflag with this build's generation (the precompute or
+// k_planes16, which write the planes' fp16 round-ups) and k_super then keeps
+// every superblock.  NaN cells round to +0 and so are skipped by the max: a
+// block whose sum is NaN fails c > thr and is never selected anyway.
 // k_super_planes: one workgroup per (tile of kSPX padded columns x kSPY
 // padded rows, plane, set).  A tile spans a config-2 plane's whole width
 // (Wqp = 240; 224-column tiles left a second tile per row with 16 columns).
@@ -740,10 +739,8 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
     const PlaneJob& job = jobs[wg.z / nplanes];
     const int plane = wg.z % nplanes;
     const RtcsmPlan& pl = job.pl;
-    const double* __restrict__ P = job.planes;
+    const unsigned short* __restrict__ P = job.planes16;
     SuperT* __restrict__ S = job.super;
-    int* __restrict__ negflag = job.negflag;
-    const int pgen = job.pgen;
     const int Wqp = pl.Wqp, Hqp = pl.Hqp;
     constexpr int TW = kSPX + kSB - 1, TH = kSPY + kSB - 1;
     static_assert(TW <= kSPThreads, "one loader per footprint column");
@@ -759,34 +756,33 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
     // the coarse planes themselves keep the reference's zeros there
     const int lr = pl.low_res, M = pl.M;
     const int rx = plane % lr, ry = plane / lr;
-    bool neg = false;
     if (tid < TW) {
         const int x = x0 + tid;
         const bool cx = (x == M - 1) && rx > 0;
         const int sx = cx ? M : x;
         // global (not flat) loads: the plane pointer comes through a struct
-        typedef const __attribute__((address_space(1))) double gdouble_t;
-        gdouble_t* __restrict__ colp = (gdouble_t*)(P + (long long)(cx ? ry * lr : plane) * pl.pstride);   // plane (ry, 0)
-        gdouble_t* __restrict__ rowp = (gdouble_t*)(P + (long long)(cx ? 0 : rx) * pl.pstride);           // plane (0, rx)
-        double v[TH];
+        typedef const __attribute__((address_space(1))) unsigned short ghalf_t;
+        ghalf_t* __restrict__ colp = (ghalf_t*)(P + (long long)(cx ? ry * lr : plane) * pl.pstride);   // plane (ry, 0)
+        ghalf_t* __restrict__ rowp = (ghalf_t*)(P + (long long)(cx ? 0 : rx) * pl.pstride);           // plane (0, rx)
+        unsigned short v[TH];
 #pragma unroll
         for (int k = 0; k < TH; ++k) {
             const int y = y0 + k;
             const bool cy = (y == M - 1) && ry > 0;
-            gdouble_t* __restrict__ src = cy ? rowp + (long long)M * Wqp : colp + (long long)y * Wqp;
-            v[k] = (x < Wqp && y < Hqp) ? src[sx] : 0.0;   // 0 past the plane (measured: clamped
-                                                            // unconditional loads, 0.27 -> 0.48 ms)
+            ghalf_t* __restrict__ src = cy ? rowp + (long long)M * Wqp : colp + (long long)y * Wqp;
+            v[k] = (x < Wqp && y < Hqp) ? src[sx] : (unsigned short)0;   // 0 past the plane
         }
-#pragma unroll
-        for (int k = 0; k < TH; ++k) neg |= v[k] < 0.0;
-        // forward 4-max as two pair maxima (fmax: no NaN here, and a zero of
-        // either sign rounds to +0)
+        // forward 4-max as two pair maxima of the fp16 round-ups (the values
+        // are +0 or positive unless a negative cell disabled the bounds, so
+        // their bit patterns order like the values; round-up is monotone, so
+        // this is the round-up of the fp64 maximum)
         static_assert(kSB == 4, "pairwise forward 4-max");
-        double m2[TH - 1];
+        unsigned short m2[TH - 1];
 #pragma unroll
-        for (int k = 0; k < TH - 1; ++k) m2[k] = fmax(v[k], v[k + 1]);
+        for (int k = 0; k < TH - 1; ++k) m2[k] = v[k] > v[k + 1] ? v[k] : v[k + 1];
 #pragma unroll
-        for (int r = 0; r < kSPY; ++r) vm[r][tid] = super_round_up(fmax(m2[r], m2[r + 2]));
+        for (int r = 0; r < kSPY; ++r)
+            vm[r][tid] = __builtin_bit_cast(SuperT, m2[r] > m2[r + 2] ? m2[r] : m2[r + 2]);
     }
     __syncthreads();
     // horizontal 4-max of the rounded values, lane = padded column, stored
@@ -830,7 +826,6 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
             uo[2 * u] = v;
             if (qt > 0) uo[2 * (u - pl.Wq4) + 1] = v;
         }
-        if (neg) *negflag = pgen;
         return;
     }
     // one 16-byte store of 8 consecutive superblocks of a sub-phase row per
@@ -845,7 +840,6 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
         if (y >= Hqp || xq >= pl.Wq4) continue;
         *(s8*)(out + ((y & 3) * 4 + sx) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + xq) = *(const s8*)&hs[r][sx][8 * ch];
     }
-    if (neg) *negflag = pgen;
 }
 
 // k_super: one workgroup (kSupWaves waves) per (chunk of superblocks, search
@@ -2609,6 +2603,13 @@ inline size_t plane_bytes(const RtcsmPlan& pl)
 {
     return align256(sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride);
 }
+// the planes' fp16 round-up copies (k_super_planes' input), right after each
+// set's fp64 planes: a fixed place per set, so their zero margins stay zero
+inline size_t plane16_bytes(const RtcsmPlan& pl)
+{
+    return align256(sizeof(unsigned short) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride);
+}
+inline size_t set_bytes(const RtcsmPlan& pl) { return plane_bytes(pl) + plane16_bytes(pl); }
 inline size_t super_bytes(const RtcsmPlan& pl)
 {
     if (pl.oct) return align256(16 * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstrideO);
@@ -2617,7 +2618,7 @@ inline size_t super_bytes(const RtcsmPlan& pl)
 double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_super)
 {
     const int b = ctx->bank;
-    const size_t bytes = plane_bytes(pl) * (size_t)nsets;
+    const size_t bytes = set_bytes(pl) * (size_t)nsets;
     double* D = (double*)ctx->ensure(ctx->banked(S_DECIM), bytes);
     // (k_super_planes writes every superblock-plane value; they are zeroed
     // with the planes only so that no stale value is ever read)
@@ -2649,6 +2650,8 @@ struct PlaneSet {
     const SuperT* super = nullptr;
     const int* negflag = nullptr;
     int pgen = 0;
+    bool half_copy = false;             // the fp16 copy comes from k_planes16 (not the precompute)
+    unsigned short* planes16 = nullptr;
 };
 
 // Build the coarse maps of every set: batched precompute straight into the
@@ -2668,6 +2671,7 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
     SuperT* S = need_super ? (SuperT*)ctx->ensure(ctx->banked(S_SUPER), super_bytes(lp) * (size_t)ns) : nullptr;
     int* neg = need_super ? (int*)ctx->ensure(ctx->banked(S_NEGFLAG), sizeof(int) * (size_t)ns) : nullptr;
     const size_t pb = plane_bytes(lp) / sizeof(double), sbb = super_bytes(lp) / sizeof(SuperT);
+    const size_t ssz = set_bytes(lp) / sizeof(double);   // one set: fp64 planes, then their fp16 copies
     // fine maps with W, H multiples of LowRes: the precompute writes the
     // planes directly (one batched launch); other maps go through a plain
     // scratch map and the phase-plane copy, and supplied coarse maps through
@@ -2678,34 +2682,40 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
     std::vector<PlaneJob> pj;
     for (int s = 0; s < ns; ++s) {
         PlaneSet& ps = sets[s];
-        ps.cmap = D + pb * (size_t)s;
+        ps.cmap = D + ssz * (size_t)s;
         PlaneJob j{};
         j.pl = lp;
-        j.planes = D + pb * (size_t)s;
+        ps.half_copy = need_super;
         if (need_super) {
+            ps.planes16 = (unsigned short*)(D + ssz * (size_t)s + pb);
+            j.planes16 = ps.planes16;
             j.super = S + sbb * (size_t)s;
-            j.negflag = neg + s;
-            j.pgen = ctx->next_stamp();
             ps.super = j.super;
-            ps.negflag = j.negflag;
-            ps.pgen = j.pgen;
+            ps.negflag = neg + s;
+            ps.pgen = ctx->next_stamp();
         }
         if (ps.fine && precompute_planes_ok(ps.fine, lr)) {
             PrecompJob q{};
             q.in = ps.fine->d;
-            q.out = D + pb * (size_t)s;
+            q.out = D + ssz * (size_t)s;
             q.W = ps.fine->w;
             q.H = ps.fine->h;
             q.pg = PlaneGeom{ lp.M, lp.Wqp, lp.pstride };
+            if (need_super && lr <= 8) {   // k_precompute_planes writes the fp16 copy itself
+                q.out16 = ps.planes16;
+                q.negflag = neg + s;
+                q.pgen = ps.pgen;
+                ps.half_copy = false;
+            }
             jobs.push_back(q);
         } else if (ps.fine) {
             // rare (odd map sizes): one set at a time through the shared scratch
             const size_t cells = (size_t)lp.W * lp.H;
             double* plain = (double*)ctx->ensure(S_COARSE_GRID, sizeof(double) * std::max<size_t>(1, cells));
             launch_precompute(ctx, ps.fine, lr, plain, nullptr);
-            launch_decimate(plain, lp, D + pb * (size_t)s, st);
+            launch_decimate(plain, lp, D + ssz * (size_t)s, st);
         } else {
-            launch_decimate(ps.coarse->d, lp, D + pb * (size_t)s, st);
+            launch_decimate(ps.coarse->d, lp, D + ssz * (size_t)s, st);
         }
         if (need_super) pj.push_back(j);
     }
@@ -2730,6 +2740,13 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
             maxH = std::max(maxH, s.fine->h);
         }
     if (sj.njobs) launch_precompute_jobs(ctx, up.at<PrecompJob>(sj.jobs_off), (int)sj.njobs, maxW, maxH, lp.low_res);
+    for (const auto& s : sets)
+        if (s.half_copy) {   // planes the batched precompute did not write: their fp16 copy here
+            const long long n = (long long)lp.low_res * lp.low_res * lp.pstride;
+            hipLaunchKernelGGL(k_planes16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, s.cmap,
+                               s.planes16, n, const_cast<int*>(s.negflag), s.pgen);
+            LGS_HIP_CHECK(hipGetLastError());
+        }
     if (sj.npj) {
         const int np = lp.low_res * lp.low_res;
         const bool lone = sj.npj == 1;

@@ -810,7 +810,8 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
 #pragma unroll
         for (int i = 1; i < LR; ++i) ma = dmax(ma, ca[i]);
         const int y = y0 + oy, qy = y / LR, ry = y - qy * LR;
-        double* dst = out + (ry * LR + rx) * pg.pstride + (long long)(qy + pg.M) * pg.Wqp + (x0 / LR + qxl) + pg.M;
+        const long long o = (ry * LR + rx) * pg.pstride + (long long)(qy + pg.M) * pg.Wqp + (x0 / LR + qxl) + pg.M;
+        double* dst = out + o;
         if (qxl + 1 < nq) {
             const int xb = xa + LR;
             const double* cb = &m1[oy][win_start(xb, W, LR) - sx0];
@@ -821,8 +822,16 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
             v.x = ma;
             v.y = mb;
             *(d2a16*)dst = v;
+            if (j.out16) {   // the pair's fp16 round-ups (o is even: 4-byte aligned)
+                *(unsigned*)(j.out16 + o) = (unsigned)half_round_up_bits(ma) | ((unsigned)half_round_up_bits(mb) << 16);
+                if (ma < 0.0 || mb < 0.0) *j.negflag = j.pgen;
+            }
         } else {
             *dst = ma;
+            if (j.out16) {
+                j.out16[o] = half_round_up_bits(ma);
+                if (ma < 0.0) *j.negflag = j.pgen;
+            }
         }
     }
 }

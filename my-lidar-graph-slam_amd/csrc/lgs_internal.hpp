@@ -163,7 +163,27 @@ struct PrecompJob {
     double* out;
     int W, H;
     PlaneGeom pg;   // pg.Wqp > 0: write the padded phase planes
+    // k_precompute_planes also writes every plane value rounded up to fp16
+    // (same layout, 2 B per cell; null: not) and stamps *negflag with pgen
+    // when a value is negative: what k_super_planes reads
+    unsigned short* out16;
+    int* negflag;
+    int pgen;
 };
+
+// fp16 (bit pattern) of m rounded toward +inf; zeros as +0 (so nonnegative
+// values order like their bit patterns) and NaN as +0 (a max skips it)
+__device__ __forceinline__ unsigned short half_round_up_bits(double m)
+{
+    // nearest float, then nearest half: one of the two fp16 neighbours of m
+    // (double rounding never skips past one), so a one-ulp step away from the
+    // lower neighbour gives the round-up
+    const _Float16 h = (_Float16)(float)m;
+    unsigned short b = __builtin_bit_cast(unsigned short, h);
+    if ((double)(float)h < m) b = (m > 0.0) ? (unsigned short)(b + 1) : (unsigned short)(b - 1);
+    if (m == 0.0 || m != m) b = 0;
+    return b;
+}
 
 struct CostPlan {
     double min_range, max_range;   // filter (open interval)
