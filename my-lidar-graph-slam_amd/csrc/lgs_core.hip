@@ -71,7 +71,7 @@ void* lgs_ctx::ensure_pinned(size_t bytes)
         pinned_bytes = 0;
     }
     size_t want = bytes + bytes / 4;
-    LGS_HIP_CHECK(hipHostMalloc(&pinned, want, hipHostMallocCoherent));
+    LGS_HIP_CHECK(hipHostMalloc(&pinned, want, hipHostMallocDefault));
     pinned_bytes = want;
     return pinned;
 }
@@ -92,7 +92,7 @@ void* lgs_ctx::ensure_pinned_in(size_t bytes)
 }
 
 namespace {
-void* grow_pinned(hipStream_t stream, void*& p, size_t& have, size_t bytes)
+void* grow_pinned(hipStream_t stream, void*& p, size_t& have, size_t bytes, bool coherent)
 {
     if (have >= bytes) return p;
     if (p) {
@@ -102,8 +102,8 @@ void* grow_pinned(hipStream_t stream, void*& p, size_t& have, size_t bytes)
         have = 0;
     }
     size_t want = bytes + bytes / 4;
-    // coherent: k_fetch reads it uncached (fresh on every launch)
-    LGS_HIP_CHECK(hipHostMalloc(&p, want, hipHostMallocCoherent));
+    // coherent where k_fetch reads it: uncached on the device, fresh on every launch
+    LGS_HIP_CHECK(hipHostMalloc(&p, want, coherent ? hipHostMallocCoherent : hipHostMallocDefault));
     have = want;
     return p;
 }
@@ -141,8 +141,8 @@ void fetch_async(lgs_ctx* ctx, void* dst, const void* src, size_t bytes)
 
 void* lgs_ctx::ensure_pinned_up(size_t bytes)
 {
-    return bank ? grow_pinned(stream, pinned_up_b, pinned_up_b_bytes, bytes)
-                : grow_pinned(stream, pinned_up, pinned_up_bytes, bytes);
+    return bank ? grow_pinned(stream, pinned_up_b, pinned_up_b_bytes, bytes, true)
+                : grow_pinned(stream, pinned_up, pinned_up_bytes, bytes, true);
 }
 
 int* lgs_ctx::tedge_buffer(size_t n)
@@ -158,7 +158,7 @@ int* lgs_ctx::tedge_buffer(size_t n)
 
 void* lgs_ctx::ensure_pinned_rec(size_t bytes)
 {
-    return grow_pinned(stream, pinned_rec[bank], pinned_rec_bytes[bank], bytes);
+    return grow_pinned(stream, pinned_rec[bank], pinned_rec_bytes[bank], bytes, false);
 }
 
 namespace lgs {
@@ -1180,7 +1180,7 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n)
         LGS_HIP_CHECK(hipEventSynchronize(ctx->scan_ev[b]));
         ctx->scan_ev_live[b] = false;
     }
-    char* pin = (char*)grow_pinned(ctx->stream, ctx->pinned_scan[b], ctx->pinned_scan_bytes[b], total);
+    char* pin = (char*)grow_pinned(ctx->stream, ctx->pinned_scan[b], ctx->pinned_scan_bytes[b], total, true);
     size_t off = 0;
     for (lgs_scan* s : todo) {
         std::lock_guard<std::mutex> g(s->dev_mu);

@@ -451,6 +451,9 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n);
 // config-4 frontend), a kernel reads the staging over the host link in one
 // round trip.  dst and src 16-byte aligned.
 void fetch_async(lgs_ctx* ctx, void* dst, const void* src, size_t bytes);
+// above this, staging goes through hipMemcpyAsync (a kernel reading host
+// memory over the link is slower than the copy engine for bulk data)
+constexpr size_t kFetchMaxBytes = size_t(1) << 20;
 // floor((xy[j] - (j odd ? my : mx)) / res) for j < n2 (host_simd.cpp)
 void cells_of_points(const double* xy, long long n2, double mx, double my, double res, int* out);
 inline void scan_to_device(lgs_ctx* ctx, const lgs_scan* s) { scans_to_device(ctx, &s, 1); }
@@ -492,7 +495,10 @@ struct Upload {
         const size_t b = std::max<size_t>(host.size(), 16);
         char* pin = (char*)ctx->ensure_pinned_up(b);
         std::memcpy(pin, host.data(), host.size());
-        fetch_async(ctx, dev, pin, host.size());
+        if (host.size() <= kFetchMaxBytes)
+            fetch_async(ctx, dev, pin, host.size());
+        else   // bulk (branch-and-bound node lists): the copy engine
+            LGS_HIP_CHECK(hipMemcpyAsync(dev, pin, host.size(), hipMemcpyHostToDevice, ctx->stream));
     }
     void flush()
     {
