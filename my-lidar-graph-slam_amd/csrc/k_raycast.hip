@@ -450,16 +450,30 @@ __device__ __forceinline__ void mark_patch(const RayMap& mp, unsigned long long 
 
 // k_apply: one thread per run of equal cells (the thread at the run's first
 // key) continues the cell from its current value with the run's updates.
+// The pass's maps (up to kApplyMapsLds) are staged in LDS first: the map of a
+// run is then a binary search in LDS instead of a chain of dependent global
+// loads on every run's critical path (the kernel is latency-bound).
+constexpr int kApplyMapsLds = 64;
 __global__ __launch_bounds__(256) void k_apply(const unsigned* __restrict__ keys, long long n, RunBits rb,
                                                const RayMap* __restrict__ maps, int nmaps,
                                                const BayesChains* __restrict__ ch, double p_hit, double p_miss,
                                                int ksh)
 {
+    __shared__ RayMap s_maps[kApplyMapsLds];
+    const bool lds = nmaps <= kApplyMapsLds;
+    if (lds) {
+        static_assert(sizeof(RayMap) % 8 == 0, "RayMap copied as 8-byte words");
+        constexpr int kw = (int)(sizeof(RayMap) / 8);
+        const unsigned long long* src = (const unsigned long long*)maps;
+        unsigned long long* dst = (unsigned long long*)s_maps;
+        for (int k = threadIdx.x; k < nmaps * kw; k += blockDim.x) dst[k] = src[k];
+        __syncthreads();
+    }
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || !run_start(rb.endw, i)) return;
     const unsigned cell = keys[i] >> ksh;
     const BayesK K(p_hit, p_miss);
-    const RayMap mp = maps[find_map(maps, nmaps, cell)];
+    const RayMap mp = lds ? s_maps[find_map(s_maps, nmaps, cell)] : maps[find_map(maps, nmaps, cell)];
     const unsigned long long local = cell - mp.base;
     mark_patch(mp, local);
     uint32_t nh = 0, nm = 0;
