@@ -61,11 +61,11 @@
  * context owns one HIP stream and its scratch; calls on one context must not
  * overlap, calls on different contexts may.
  *
- * Numerics: fp64 throughout.  Cell indices, hit/miss counts, map cells and the
- * correlative argmax/score are bit-exact with the reference CPU path; greedy-
- * endpoint costs/covariances agree to within 1e-5 (device exp differs from glibc
- * in the last ulp); the Gauss-Newton refine agrees per step and within 1e-5 end
- * to end on 1081-beam scans (DESIGN.md §K4 explains why not bitwise).
+ * Numerics: fp64 throughout.  Cell indices, hit/miss counts, map cells, the
+ * correlative argmax/score and the Gauss-Newton refine (glibc's
+ * sincos/pow restated on the device, sums in beam order) are bit-exact with the
+ * reference CPU path; greedy-endpoint costs/covariances agree to within 1e-5
+ * (device exp differs from glibc in the last ulp).
  */
 #ifndef LGS_HIP_H
 #define LGS_HIP_H
