@@ -3255,8 +3255,8 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
         LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0xFF, sizeof(RtcsmRecord) * (size_t)n, ctx->stream));
     }
     int* tedge = ctx->tedge_buffer((size_t)n * B.Tmax);   // stamps only: no clearing per batch
-    scans_to_device(ctx, scans, n);
     Upload up(ctx);
+    scans_to_device(ctx, scans, n, &up);
     const SetJobs sj = build_sets(ctx, p0, sets, B.pruned, up);
     std::vector<int> gens((size_t)n);
     for (int j = 0; j < n; ++j) {

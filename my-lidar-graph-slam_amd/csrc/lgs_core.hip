@@ -108,13 +108,9 @@ void* grow_pinned(hipStream_t stream, void*& p, size_t& have, size_t bytes, bool
     return p;
 }
 
-struct FetchSeg {
-    const unsigned char* src;
-    unsigned char* dst;
-    unsigned long long bytes;
-};
-__global__ __launch_bounds__(256) void k_fetch(FetchSeg s)
+__global__ __launch_bounds__(256) void k_fetch(FetchList L)
 {
+    const FetchSeg& s = L.s[blockIdx.y];   // one segment per grid row
     const unsigned long long n16 = s.bytes / 16;
     const unsigned long long g = (unsigned long long)blockIdx.x * 256 + threadIdx.x;
     const uint4* __restrict__ a = (const uint4*)s.src;
@@ -125,17 +121,36 @@ __global__ __launch_bounds__(256) void k_fetch(FetchSeg s)
 }  // namespace
 
 namespace lgs {
+FetchSeg fetch_seg(void* dst, const void* src, size_t bytes)
+{
+    LGS_REQUIRE(((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0, "fetch: 16-byte alignment");
+    void* dsrc = nullptr;
+    LGS_HIP_CHECK(hipHostGetDevicePointer(&dsrc, const_cast<void*>(src), 0));
+    return FetchSeg{ (const unsigned char*)dsrc, (unsigned char*)dst, (unsigned long long)bytes };
+}
+
+void fetch_list(lgs_ctx* ctx, const std::vector<FetchSeg>& segs)
+{
+    for (size_t k0 = 0; k0 < segs.size(); k0 += kFetchSegs) {
+        FetchList L{};
+        unsigned long long mx = 0;
+        int n = 0;
+        for (size_t k = k0; k < segs.size() && n < kFetchSegs; ++k)
+            if (segs[k].bytes) {
+                L.s[n++] = segs[k];
+                mx = std::max(mx, segs[k].bytes / 16);
+            }
+        if (!n) continue;
+        const unsigned blocks = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>((mx + 255) / 256, 64));
+        hipLaunchKernelGGL(k_fetch, dim3(blocks, (unsigned)n), dim3(256), 0, ctx->stream, L);
+        LGS_HIP_CHECK(hipGetLastError());
+    }
+}
+
 void fetch_async(lgs_ctx* ctx, void* dst, const void* src, size_t bytes)
 {
     if (bytes == 0) return;
-    LGS_REQUIRE(((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0, "fetch_async: 16-byte alignment");
-    void* dsrc = nullptr;
-    LGS_HIP_CHECK(hipHostGetDevicePointer(&dsrc, const_cast<void*>(src), 0));
-    const unsigned long long n16 = bytes / 16;
-    const unsigned blocks = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>((n16 + 255) / 256, 64));
-    hipLaunchKernelGGL(k_fetch, dim3(blocks), dim3(256), 0, ctx->stream,
-                       FetchSeg{ (const unsigned char*)dsrc, (unsigned char*)dst, (unsigned long long)bytes });
-    LGS_HIP_CHECK(hipGetLastError());
+    fetch_list(ctx, { fetch_seg(dst, src, bytes) });
 }
 }  // namespace lgs
 
@@ -1148,7 +1163,7 @@ extern "C" void lgs_scan_destroy(lgs_scan* s)
 }
 
 namespace lgs {
-void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n)
+void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n, Upload* up)
 {
     // scans without a copy yet (each once), and copies made by other contexts
     std::vector<lgs_scan*> todo;
@@ -1182,6 +1197,7 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n)
     }
     char* pin = (char*)grow_pinned(ctx->stream, ctx->pinned_scan[b], ctx->pinned_scan_bytes[b], total, true);
     size_t off = 0;
+    std::vector<FetchSeg> segs;
     for (lgs_scan* s : todo) {
         std::lock_guard<std::mutex> g(s->dev_mu);
         if (s->d_ranges) continue;   // another thread got there first
@@ -1190,7 +1206,7 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n)
         std::memcpy(pin + off, s->h_ranges.data(), bytes);
         std::memcpy(pin + off + bytes, s->h_angles.data(), bytes);
         try {
-            fetch_async(ctx, d, pin + off, 2 * bytes);
+            segs.push_back(fetch_seg(d, pin + off, 2 * bytes));
         } catch (...) {
             scan_buffer_put(ctx->device, d, 2 * bytes);
             throw;
@@ -1200,6 +1216,13 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n)
         s->dev_ctx = ctx;
         s->d_ranges = d;
     }
+    if (up) {
+        // copied with the call's upload (one launch); the upload is flushed
+        // before any kernel of the call reads the scans
+        up->extra.insert(up->extra.end(), segs.begin(), segs.end());
+        return;
+    }
+    fetch_list(ctx, segs);
     if (!ctx->scan_ev[b]) LGS_HIP_CHECK(hipEventCreateWithFlags(&ctx->scan_ev[b], hipEventDisableTiming));
     LGS_HIP_CHECK(hipEventRecord(ctx->scan_ev[b], ctx->stream));
     ctx->scan_ev_live[b] = true;

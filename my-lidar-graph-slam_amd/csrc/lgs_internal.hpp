@@ -444,13 +444,29 @@ const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* scan, double scan_range_ma
 // and enqueues the copy on ctx->stream.  Every caller synchronises its
 // stream before returning, after which the copy is complete; a scan whose
 // copy was enqueued by another context is waited for (device-wide) once.
-void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n);
+// With an Upload, the copies join that upload's (one launch when it flushes;
+// the staging is reused only after the call's synchronisation).
+struct Upload;
+void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n, Upload* up = nullptr);
 // Host-to-device copy of pinned staging (the ctx's coherent hipHostMalloc
 // buffers) by a kernel on ctx->stream (k_fetch): a small hipMemcpyAsync waits
 // ~11 us in the copy engine's queue and takes ~6 us more (r03 trace of the
 // config-4 frontend), a kernel reads the staging over the host link in one
 // round trip.  dst and src 16-byte aligned.
 void fetch_async(lgs_ctx* ctx, void* dst, const void* src, size_t bytes);
+// several copies in one launch (k_fetch: one segment per grid row, kFetchSegs
+// per launch)
+struct FetchSeg {
+    const unsigned char* src;   // device-visible address of the pinned staging
+    unsigned char* dst;
+    unsigned long long bytes;
+};
+constexpr int kFetchSegs = 8;
+struct FetchList {
+    FetchSeg s[kFetchSegs];
+};
+FetchSeg fetch_seg(void* dst, const void* src, size_t bytes);
+void fetch_list(lgs_ctx* ctx, const std::vector<FetchSeg>& segs);
 // above this, staging goes through hipMemcpyAsync (a kernel reading host
 // memory over the link is slower than the copy engine for bulk data)
 constexpr size_t kFetchMaxBytes = size_t(1) << 20;
@@ -473,7 +489,21 @@ struct Upload {
     lgs_ctx* ctx;
     std::vector<char> host;
     char* dev = nullptr;
+    std::vector<FetchSeg> extra;   // other staged copies launched with this one (scans' first copies)
     explicit Upload(lgs_ctx* c) : ctx(c) {}
+    Upload(const Upload&) = delete;
+    Upload& operator=(const Upload&) = delete;
+    ~Upload()
+    {
+        // copies joined to an upload that was never flushed (an error path)
+        // still run: their scans already point at the destination
+        if (!extra.empty()) {
+            try {
+                fetch_list(ctx, extra);
+            } catch (...) {
+            }
+        }
+    }
     template <class T>
     size_t append(const T* p, size_t n)
     {
@@ -495,10 +525,14 @@ struct Upload {
         const size_t b = std::max<size_t>(host.size(), 16);
         char* pin = (char*)ctx->ensure_pinned_up(b);
         std::memcpy(pin, host.data(), host.size());
+        std::vector<FetchSeg> segs;
         if (host.size() <= kFetchMaxBytes)
-            fetch_async(ctx, dev, pin, host.size());
+            segs.push_back(fetch_seg(dev, pin, host.size()));
         else   // bulk (branch-and-bound node lists): the copy engine
             LGS_HIP_CHECK(hipMemcpyAsync(dev, pin, host.size(), hipMemcpyHostToDevice, ctx->stream));
+        segs.insert(segs.end(), extra.begin(), extra.end());
+        extra.clear();
+        fetch_list(ctx, segs);
     }
     void flush()
     {
