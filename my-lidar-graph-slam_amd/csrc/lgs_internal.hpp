@@ -173,7 +173,7 @@ struct PrecompJob {
 
 // fp16 (bit pattern) of m rounded toward +inf; zeros as +0 (so nonnegative
 // values order like their bit patterns) and NaN as +0 (a max skips it)
-__device__ __forceinline__ unsigned short half_round_up_bits(double m)
+__device__ __forceinline__ unsigned short half_round_up_bits_cvt(double m)
 {
     // nearest float, then nearest half: one of the two fp16 neighbours of m
     // (double rounding never skips past one), so a one-ulp step away from the
@@ -183,6 +183,22 @@ __device__ __forceinline__ unsigned short half_round_up_bits(double m)
     if ((double)(float)h < m) b = (m > 0.0) ? (unsigned short)(b + 1) : (unsigned short)(b - 1);
     if (m == 0.0 || m != m) b = 0;
     return b;
+}
+// The same from the fp64 bit fields (32-bit integer operations only) for the
+// fp16 normal range and above; zeros, fp16 subnormals, negatives and NaN take
+// the conversion path
+__device__ __forceinline__ unsigned short half_round_up_bits(double m)
+{
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, m);
+    const unsigned hi = (unsigned)(b >> 32), lo = (unsigned)b;
+    const unsigned e = (hi >> 20) & 0x7FFu;   // biased exponent (sign 0 below)
+    if ((hi >> 31) == 0u && e >= 1009u && e < 2047u) {
+        if (e > 1038u) return 0x7C00u;         // above the fp16 range: +inf
+        unsigned h = ((e - 1008u) << 10) | ((hi >> 10) & 0x3FFu);
+        h += ((hi & 0x3FFu) | lo) != 0u;       // dropped bits: round up (a carry steps the exponent)
+        return (unsigned short)h;
+    }
+    return half_round_up_bits_cvt(m);
 }
 
 struct CostPlan {
