@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_down(const unsigned* __re
 }
 
 // Small sorts (every tile resident at once): all passes in ONE launch.  Each
-// workgroup ranks its tile as k_sort_pass does, stores its digit counts,
+// workgroup ranks its tile as k_sort_down does, stores its digit counts,
 // waits at a grid barrier, reads every tile's counts (digit totals and the
 // counts of the tiles before it: the same offsets a histogram and a look-back
 // give), scatters, and waits again before the next pass reads the keys.
