@@ -221,10 +221,28 @@ def roofline_from(stats, kernel, pmc_path, trace_kernel, bound, workload="match"
                 kernel=trace_kernel, avg_launch_ms=round(avg_ms, 5), algo_bytes_per_launch=per_launch)
 
 
+def coarse_stage(stats):
+    """The whole batched coarse stage: k_coarse_list (the 'k_coarse' kernel of
+    the roofline, every coarse lookup) plus the work-list passes around it
+    (k_keep, k_unsafe_list: 'k_coarse_aux'), per k_coarse launch, with the
+    same algorithmic bytes."""
+    k, a = stats.get("k_coarse"), stats.get("k_coarse_aux")
+    if not k or not a or not k["launches"] or not k["algo_bytes"]:
+        return None
+    ms = (k["total_ms"] + a["total_ms"]) / k["launches"]
+    per = k["algo_bytes"] / k["launches"]
+    return dict(kernels="k_keep + k_coarse_list + k_unsafe_list", ms_per_launch=round(ms, 5),
+                aux_ms_per_launch=round(a["total_ms"] / k["launches"], 5),
+                frac=round(per / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+
+
 def set_timed_events(ctx, args, dominant):
-    """HIP-event timing during the timed region (LGS_OPT_PROFILE_MASK)."""
-    mask = {"dominant": 1 << abi.KERNEL_IDS.index(dominant), "all": (1 << len(abi.KERNEL_IDS)) - 1,
-            "none": 0}[args.timed_events]
+    """HIP-event timing during the timed region (LGS_OPT_PROFILE_MASK); the
+    coarse kernel's work-list passes (k_coarse_aux) are timed with it."""
+    dom = 1 << abi.KERNEL_IDS.index(dominant)
+    if dominant == "k_coarse":
+        dom |= 1 << abi.KERNEL_IDS.index("k_coarse_aux")
+    mask = {"dominant": dom, "all": (1 << len(abi.KERNEL_IDS)) - 1, "none": 0}[args.timed_events]
     ctx.set_option(abi.LGS_OPT_PROFILE_MASK, mask)
     ctx.reset_stats()
 
@@ -521,8 +539,9 @@ def run_match(args, D, ctx):
         # roofline_timed_region.  tools/trace_coarse.py splits a kernel trace
         # of this command the same way (dispatches overlapping no other vs
         # the rest).
-        roofline=roofline_from(all_stats, "k_coarse", args.pmc, "k_coarse_lanes", "l2-gather"), cpu_baseline=cpu,
-        roofline_timed_region=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_lanes", "l2-gather"),
+        roofline=roofline_from(all_stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"), cpu_baseline=cpu,
+        roofline_timed_region=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"),
+        coarse_stage=coarse_stage(all_stats),
         pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events,
         super_prune=bool(args.super_prune),
         coarse_blocks_scored_mean=round(float(results[:, 4].mean()), 1),
@@ -679,8 +698,9 @@ def run_loop(args, D, ctx):
                               "config5: LoopDetectorRealTimeCorrelative::Detect batch"), candidates=len(cands),
                     found=found, parallelism=f"candidates sharded in contiguous blocks over {D.world} ranks + "
                                              "RCCL all-gather of 176-B result records"),
-        roofline=roofline_from(stats, dominant, args.pmc, "k_bb_score" if bb else "k_coarse_lanes", "l2-gather",
+        roofline=roofline_from(stats, dominant, args.pmc, "k_bb_score" if bb else "k_coarse_list", "l2-gather",
                                workload="loop_bb" if bb else "loop"),
+        coarse_stage=None if bb else coarse_stage(stats),
         cpu_baseline=cpu)
     return line, stats, value
 

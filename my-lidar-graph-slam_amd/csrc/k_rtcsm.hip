@@ -77,6 +77,7 @@ struct MatchItem {
     int pgen;                // build stamp of the planes
     int gen;                 // this match's generation stamp
     RtcsmRecord* rec;
+    int* keepc;              // this item's two work-list counters (k_keep; null: no list), zeroed by k_seed_super
     int2* idx;
     int* cbase;
     int* tedge;
@@ -1243,12 +1244,15 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, con
 constexpr int kLaneWaves = 4;
 constexpr int kEdgeMax = 1024;     // edge beams compacted in LDS (more: the full walk); 8 KB keeps
 constexpr int kEdgeMaxNv = 4096;   // the occupancy of the kernel (measured: 32 KB cost config 2 30%)
-__global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, const double* __restrict__ zero)
+// One angle t of item `it`: its kept superblocks (the selection ballot), the
+// edge-beam compaction, then per kept block the sequential sum (unless
+// UNSAFE_ONLY: the sum is already in cscore, written by k_coarse_list) and the
+// unsafe test.  Called by a whole workgroup of kLaneWaves waves; the LDS
+// arrays are reused when a workgroup takes several angles (k_unsafe_list).
+template <bool UNSAFE_ONLY>
+__device__ __forceinline__ void coarse_angle(const MatchItem& it, int t, const double* __restrict__ zero)
 {
-    const MatchItem& it = items[blockIdx.y];
     const RtcsmPlan& pl = it.pl;
-    const int t = blockIdx.x;
-    if (t >= pl.T) return;   // past this item's angles (uniform)
     const double* __restrict__ cmap = it.cmap;
     const int2* __restrict__ idx = it.idx;
     const int* __restrict__ cb = it.cbase + (size_t)t * pl.Nv;
@@ -1260,8 +1264,9 @@ __global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, c
     double L = -INFINITY;
 #pragma unroll
     for (int b = 0; b < kSeedCands; ++b) L = fmax(L, it.Lc[b]);
-    if (t == 0 && tid == 0) *it.Lp = L;
+    if (!UNSAFE_ONLY && t == 0 && tid == 0) *it.Lp = L;
     const bool te = it.tedge[t] == gen;
+    __syncthreads();   // the previous angle's LDS is read
     // kept superblocks of this angle (nsb2 <= 64 on this path), in key order
     if (w == 0) {
         bool kp = false;
@@ -1271,8 +1276,8 @@ __global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, c
         }
         const unsigned long long bal = __ballot(kp);
         if (kp) s_sb[__popcll(bal & ((1ull << lane) - 1ull))] = lane;
-        if (lane == 0) {
-            s_cnt = __popcll(bal);
+        if (lane == 0) s_cnt = __popcll(bal);
+        if (!UNSAFE_ONLY && lane == 0) {
             unsigned long long nb = 0;
             for (unsigned long long mm = bal; mm; mm &= mm - 1) {
                 const int sb = __ffsll((long long)mm) - 1;
@@ -1321,9 +1326,11 @@ __global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, c
         const int jx = kSB * (sb % pl.nsbx) + (m & 3), jy = kSB * (sb / pl.nsbx) + (m >> 2);
         const bool active = has && jx < pl.ncx && jy < pl.ncy;
         const double* __restrict__ lane_base = cmap + (active ? jy * pl.Wqp + jx : 0);
+        const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
         // inactive lanes (partial superblocks, the wave's tail) read the zero cell
-        const double sum = seq_sum<int>(pl.Nv, [&](int v) { return cb[v]; },
-                                        [&](const int& c) { return active ? lane_base + c : zero; });
+        const double sum = UNSAFE_ONLY ? (active ? it.cscore[k] : 0.0)
+                                       : seq_sum<int>(pl.Nv, [&](int v) { return cb[v]; },
+                                                      [&](const int& c) { return active ? lane_base + c : zero; });
         // unsafe: some coarse read left of / below the map while the block's
         // fine reads can land inside (x, y >= -(lr-1)); rare, so a separate pass
         // (+ ext: the strip reads' bound of the fine values, see strip_read)
@@ -1346,12 +1353,166 @@ __global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, c
             }
         }
         if (active) {
-            const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
-            it.cscore[k] = sum;
+            if (!UNSAFE_ONLY) it.cscore[k] = sum;
             // an unsafe block whose fine scores all stay below L can change
             // nothing: it is treated as safe (c <= bound < L)
             it.cflag[k] = (unsafe && (sum + ext) * pl.sb_mult >= L) ? 1 : 0;
         }
+    }
+}
+
+__global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, const double* __restrict__ zero)
+{
+    const MatchItem& it = items[blockIdx.y];
+    if ((int)blockIdx.x >= it.pl.T) return;   // past this item's angles (uniform)
+    coarse_angle<false>(it, blockIdx.x, zero);
+}
+
+// Kept-superblock work list (the batched default; k_coarse_lanes above is the
+// fallback for rows longer than kListMaxNv).  Most angles of a batch keep 0-3
+// superblocks (loop closure: 76% keep none), so one workgroup per angle leaves
+// most lanes idle.  k_keep lists every kept (angle, superblock) of each item
+// -- the same selection, counted into the item's record -- and the angles
+// with edge beams among them; k_coarse_list gives each wave four listed
+// superblocks from any angles and items (16 lanes each), so the waves that
+// walk the beams are full; k_unsafe_list then runs the unsafe test of the
+// listed edge angles only.  The lists' order does not matter: every entry
+// writes its own blocks.
+// WorkList: cnt = 2 counters per item, 16 ints apart (zeroed by k_seed_super
+// through MatchItem::keepc); sbl = per item `region` entries t << 6 | sb;
+// al = per item Tmax edge angles.
+struct WorkList {
+    int* cnt;
+    int* sbl;
+    int* al;
+    int region, tmax;
+};
+constexpr int kListMaxNv = 4096;   // k_coarse_list stages four beam rows in LDS (64 KB)
+// grid sizes measured (config 5 / config 2 stage ms): list 2048 + unsafe 1024: 0.272 / 0.373; 2048 + 4096:
+// 0.241 / 0.375; 4096 + 4096: 0.226 / 0.364; 2304 + 4096: 0.226 / 0.365; 1024 + 4096: 0.288 / 0.528
+constexpr int kListWaves = 4096;   // k_coarse_list workgroups (one wave each, grid-stride)
+constexpr int kUnsafeGroups = 4096;
+
+__global__ __launch_bounds__(64) void k_keep(Items items, WorkList W)
+{
+    const int j = blockIdx.y;
+    const MatchItem& it = items[j];
+    const RtcsmPlan& pl = it.pl;
+    const int t = blockIdx.x;
+    if (t >= pl.T) return;   // past this item's angles (uniform)
+    const int lane = threadIdx.x;
+    const int nsb2 = pl.nsbx * pl.nsby;
+    double L = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < kSeedCands; ++b) L = fmax(L, it.Lc[b]);
+    if (t == 0 && lane == 0) *it.Lp = L;
+    bool kp = false;
+    if (lane < nsb2) {
+        const double bnd = it.sbound[(size_t)t * nsb2 + lane];
+        kp = (bnd > pl.thr) && bnd >= L;
+    }
+    const unsigned long long bal = __ballot(kp);
+    if (!bal) return;
+    int base = 0;
+    if (lane == 0) {
+        unsigned long long nb = 0;
+        for (unsigned long long mm = bal; mm; mm &= mm - 1) {
+            const int sb = __ffsll((long long)mm) - 1;
+            const int a = sb % pl.nsbx, b = sb / pl.nsbx;
+            nb += (unsigned long long)(min(kSB, pl.ncx - kSB * a) * min(kSB, pl.ncy - kSB * b));
+        }
+        atomicAdd(&it.rec->coarse_evals, nb);
+        base = atomicAdd(W.cnt + 16 * j, __popcll(bal));
+        if (it.tedge[t] == it.gen) W.al[(size_t)j * W.tmax + atomicAdd(W.cnt + 16 * j + 1, 1)] = t;
+    }
+    base = __shfl(base, 0, 64);
+    if (kp) W.sbl[(size_t)j * W.region + base + __popcll(bal & ((1ull << lane) - 1ull))] = t << 6 | lane;
+}
+
+// Inclusive prefix of the items' counters `which` over lanes 0..n-1 (every
+// lane of the wave computes it); returns the total.
+__device__ __forceinline__ int list_prefix(const WorkList& W, int which, int n, int& c)
+{
+    const int lane = threadIdx.x & 63;
+    c = lane < n ? W.cnt[16 * lane + which] : 0;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(c, off, 64);
+        if (lane >= off) c += u;
+    }
+    return __shfl(c, 63, 64);
+}
+
+// Four listed superblocks per wave (grid-stride over the list): the same
+// sequential fp64 sums as k_coarse_lanes'.  cflag is 0 here; k_unsafe_list
+// then redoes the edge angles' blocks.
+__global__ __launch_bounds__(64) void k_coarse_list(Items items, WorkList W, int n, int rowlen,
+                                                    const double* __restrict__ zero)
+{
+    extern __shared__ int s_cb[];   // [4][rowlen]: each group's coarse-base row
+    const int lane = threadIdx.x, g4 = lane >> 4, m = lane & 15;
+    int c;
+    const int total = list_prefix(W, 0, n, c);
+    for (int e0 = 4 * blockIdx.x; e0 < total; e0 += 4 * gridDim.x) {   // wave-uniform
+        const int e = e0 + g4;
+        const bool has = e < total;
+        // item of entry e = the number of items whose inclusive prefix is <= e
+        int j = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int jq = __popcll(__ballot(lane < n && c <= e0 + q));
+            if (g4 == q) j = jq;
+        }
+        if (!has) j = 0;
+        const int cprev = __shfl(c, max(j - 1, 0), 64);
+        const int before = j > 0 ? cprev : 0;
+        const MatchItem& it = items[j];
+        const RtcsmPlan& pl = it.pl;
+        const int ent = has ? W.sbl[(size_t)j * W.region + (e - before)] : 0;
+        const int t = ent >> 6, sb = ent & 63;
+        const int Nv = has ? pl.Nv : 0;
+        const int* __restrict__ cbr = it.cbase + (size_t)t * pl.Nv;
+        __syncthreads();   // the previous round's rows are read
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int nq = __shfl(Nv, 16 * q, 64);
+            const int* row = (const int*)__shfl((unsigned long long)cbr, 16 * q, 64);
+            for (int v = lane; v < nq; v += 64) s_cb[q * rowlen + v] = row[v];
+        }
+        __syncthreads();
+        int nmax = Nv;
+#pragma unroll
+        for (int off = 16; off < 64; off <<= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
+        const int nsbx = max(pl.nsbx, 1);
+        const int jx = kSB * (sb % nsbx) + (m & 3), jy = kSB * (sb / nsbx) + (m >> 2);
+        const bool active = has && jx < pl.ncx && jy < pl.ncy;
+        const double* __restrict__ lane_base = it.cmap + (active ? jy * pl.Wqp + jx : 0);
+        const int* __restrict__ my = s_cb + g4 * rowlen;
+        // past this lane's own row (v >= Nv, within the look-ahead): the zero cell
+        constexpr int kOff = -(1 << 30);
+        const double sum = seq_sum<int>(nmax, [&](int v) { return v < Nv ? my[min(v, rowlen - 1)] : kOff; },
+                                        [&](const int& cc) { return (active && cc != kOff) ? lane_base + cc : zero; });
+        if (active) {
+            const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
+            it.cscore[k] = sum;
+            it.cflag[k] = 0;
+        }
+    }
+}
+
+// The unsafe test of the listed edge angles (k_keep), one angle at a time per
+// workgroup (grid-stride), as k_coarse_lanes runs it.
+__global__ __launch_bounds__(64 * kLaneWaves) void k_unsafe_list(Items items, WorkList W, int n,
+                                                                 const double* __restrict__ zero)
+{
+    const int lane = threadIdx.x & 63;
+    int c;
+    const int total = list_prefix(W, 1, n, c);
+    for (int a = blockIdx.x; a < total; a += gridDim.x) {   // workgroup-uniform
+        const int j = __popcll(__ballot(lane < n && c <= a));
+        const int cprev = __shfl(c, max(j - 1, 0), 64);
+        const int before = j > 0 ? cprev : 0;
+        coarse_angle<true>(items[j], W.al[(size_t)j * W.tmax + (a - before)], zero);
     }
 }
 
@@ -1646,6 +1807,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
     const int nparts = it.nparts;
     double* __restrict__ Lc = it.Lc;
     RtcsmRecord* rec = it.rec;
+    if (blockIdx.x == 0 && threadIdx.x < 2 && it.keepc) it.keepc[threadIdx.x] = 0;   // before k_keep
     extern __shared__ char smem[];
     __shared__ double sv[16];
     __shared__ long long sk[16];
@@ -2515,6 +2677,7 @@ struct BatchShape {
     bool fine_lanes = false;   // k_compact + k_fine_lanes (lr * lr <= 64)
     int frows = 1;
     int kernel_size = 0;
+    WorkList wl{};          // kept-superblock work list (wl.cnt null: k_coarse_lanes)
 };
 
 // per-(chunk|tile, angle) best entries the seed kernel scans: k_super's
@@ -2889,11 +3052,26 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             ctx->timing_end(tok);
             LGS_HIP_CHECK(hipGetLastError());
         }
+        // the work list's passes are timed apart (K_COARSE_AUX): K_COARSE is the
+        // kernel that makes every coarse lookup (its algorithmic bytes)
+        const bool wl = n >= ctx->lanes_min_batch && B.wl.cnt && !ctx->skipped(K_COARSE);
+        if (wl) {
+            const int tk = ctx->timing_begin(K_COARSE_AUX, 8.0 * (double)B.Tmax * B.nsb2 * n);   // bound reads
+            hipLaunchKernelGGL(k_keep, dim3(B.Tmax, n), dim3(64), 0, st, d_items, B.wl);
+            ctx->timing_end(tk);
+            LGS_HIP_CHECK(hipGetLastError());
+        }
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * beams_K);
         if (tok >= 0) ctx->pending[tok].coarse_evals = true;   // algorithmic bytes from the records
         if (ctx->skipped(K_COARSE)) {
         } else if (n >= ctx->lanes_min_batch) {
-            hipLaunchKernelGGL(k_coarse_lanes, dim3(B.Tmax, n), dim3(64 * kLaneWaves), 0, st, d_items, zero);
+            if (wl) {
+                const int rowlen = std::max(B.NvMax, 1);
+                hipLaunchKernelGGL(k_coarse_list, dim3(kListWaves), dim3(64), sizeof(int) * 4 * (size_t)rowlen, st,
+                                   d_items, B.wl, n, rowlen, zero);
+            } else {
+                hipLaunchKernelGGL(k_coarse_lanes, dim3(B.Tmax, n), dim3(64 * kLaneWaves), 0, st, d_items, zero);
+            }
         } else {
             const size_t lds = ((sizeof(int) * (size_t)B.NvMax + 15) & ~(size_t)15) +
                                sizeof(double) * 128 * kRing * kRowWaves;
@@ -2902,6 +3080,13 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         }
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
+        if (wl) {
+            const int tk = ctx->timing_begin(K_COARSE_AUX, 0.0);
+            hipLaunchKernelGGL(k_unsafe_list, dim3(std::min(kUnsafeGroups, n * B.Tmax)), dim3(64 * kLaneWaves), 0, st,
+                               d_items, B.wl, n, zero);
+            ctx->timing_end(tk);
+            LGS_HIP_CHECK(hipGetLastError());
+        }
     } else {
         {
             dim3 g((B.P + B.cb - 1) / B.cb, B.Tmax, n);
@@ -3241,6 +3426,13 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     B.frows = (B.lr5 && !B.fine_lanes) ? 5 : 1;
     B.kernel_size = cost->kernel_size;
     B.nsegMax = (int)(((long long)B.Tmax * B.P + kSelSeg - 1) / kSelSeg);
+    if (B.pruned && n >= ctx->lanes_min_batch && B.NvMax <= kListMaxNv && B.Tmax < (1 << 24) && B.nsb2 <= 64) {
+        // the kept-superblock work list: counters | superblock entries | edge angles
+        int region = 1;
+        for (auto& it : items) region = std::max(region, it.pl.T * it.pl.nsbx * it.pl.nsby);
+        int* wl = (int*)ctx->ensure(S_KEEP, sizeof(int) * (size_t)n * (16 + (size_t)region + (size_t)B.Tmax));
+        B.wl = WorkList{ wl, wl + 16 * (size_t)n, wl + 16 * (size_t)n + (size_t)region * n, region, B.Tmax };
+    }
     const ItemLayout L = item_layout(B.Tmax, B.NvMax, B.P, B.nsb2, B.chunks, B.cb, B.frows, Nmax);
     char* ws = (char*)ctx->ensure(ctx->banked(S_BATCH_WS), L.total * (size_t)n);
     RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(ctx->banked(S_RECORDS), sizeof(RtcsmRecord) * (size_t)n);
@@ -3273,6 +3465,7 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
         it.pgen = s.pgen;
         it.gen = gens[j] = ctx->generation = ctx->next_stamp();
         it.rec = d_rec + j;
+        it.keepc = B.wl.cnt ? B.wl.cnt + 16 * j : nullptr;
         it.nparts = item_nparts(B, it.pl, B.pruned);
     }
     ctx->dbg.assign((size_t)n, lgs_ctx::DbgItem{});

@@ -180,7 +180,8 @@ namespace lgs {
 const char* const kKernelNames[K_NUM_KERNELS] = { "k_project", "k_coarse", "k_seed", "k_select",
                                                   "k_fine", "k_replay", "k_cost", "k_precompute",
                                                   "k_linsolve", "k_ray_emit", "k_ray_apply",
-                                                  "k_super", "k_super_planes", "k_bb_score", "k_bb_expand" };
+                                                  "k_super", "k_super_planes", "k_bb_score", "k_bb_expand",
+                                                  "k_coarse_aux" };
 }
 
 int lgs_ctx::next_stamp()

@@ -79,6 +79,7 @@ enum Slot {
     S_NEGFLAG,      // int per coarse-map set: negative-cell stamp of its planes
     S_BB0, S_BB1, S_BB2, S_BB3, S_BB4, S_BB5,   // branch-and-bound (k_bb.hip)
     S_PRECOMP_TMP,  // double [W*H]: pass-1 result of the large-window precompute
+    S_KEEP,         // int: kept-superblock work list of a batch (k_keep / k_coarse_list)
     // bank 1 of the per-batch buffers: a batched call keeps two 64-query
     // chunks in flight (the next chunk's launches go out before the host
     // finishes the previous one), each in its own bank (lgs_ctx::banked)
@@ -228,6 +229,7 @@ struct CostPlan {
 namespace lgs {
 enum KernelId { K_PROJECT = 0, K_COARSE, K_SEED, K_SELECT, K_FINE, K_REPLAY, K_COST, K_PRECOMPUTE,
                 K_LINSOLVE, K_RAY_EMIT, K_RAY_APPLY, K_SUPER, K_SUPER_PLANES, K_BB_SCORE, K_BB_EXPAND,
+                K_COARSE_AUX,   // k_keep + k_unsafe_list: the work-list passes around k_coarse_list
                 K_NUM_KERNELS };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 struct PendingTiming {

@@ -34,7 +34,7 @@ LGS_OPT_PEER_COPY = 19
 LGS_OPT_PRUNE_MIN_SUPER = 21
 KERNEL_IDS = ["k_project", "k_coarse", "k_seed", "k_select", "k_fine", "k_replay", "k_cost", "k_precompute",
               "k_linsolve", "k_ray_emit", "k_ray_apply", "k_super", "k_super_planes", "k_bb_score",
-              "k_bb_expand"]   # lgs_ctx_kernel_stats order
+              "k_bb_expand", "k_coarse_aux"]   # lgs_ctx_kernel_stats order
 
 
 class Pose2D(C.Structure):
@@ -306,8 +306,8 @@ class Context:
 
     def kernel_stats(self) -> dict:
         """{name: dict(launches, total_ms, algo_bytes)} since the last reset."""
-        buf = (KernelStat * 16)()
-        n = self.lib.lgs_ctx_kernel_stats(self.h, buf, 16)
+        buf = (KernelStat * len(KERNEL_IDS))()
+        n = self.lib.lgs_ctx_kernel_stats(self.h, buf, len(KERNEL_IDS))
         if n < 0:
             self.check(-n, "kernel_stats")
         return {buf[i].name.decode(): dict(launches=buf[i].launches, total_ms=buf[i].total_ms,

@@ -17,7 +17,7 @@ cp $OUT/${TAG}_pmc.json profiles/pmc_summary.json
 grep '^{' $OUT/trace_$TAG.log | tail -n 1 > $OUT/${TAG}_trace_run_bench.json
 ALGO=$(python3 -c "import json;print(json.loads(open('$OUT/${TAG}_trace_run_bench.json').read())['roofline']['algo_bytes_per_launch'])") || exit 1
 TR=$(find $OUT/trace_$TAG -name '*kernel_trace.csv' | head -1)
-python3 tools/trace_coarse.py $TR k_coarse_lanes $ALGO > $OUT/${TAG}_coarse_split.json || exit 1
+python3 tools/trace_coarse.py $TR k_coarse_list $ALGO > $OUT/${TAG}_coarse_split.json || exit 1
 cat $OUT/${TAG}_coarse_split.json
 find $OUT/trace_$TAG -name '*kernel_stats.csv' -exec cp {} $OUT/${TAG}_run_kernel_stats.csv \;
 rm -rf $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG $OUT/pmc_l2_$TAG $OUT/trace_$TAG

@@ -87,7 +87,7 @@ def main():
                    "half the bytes of wide coalesced reads (MI355X_MICROARCH.md HBM section): bench.py doubles it",
            "kernels": out}
     json.dump(doc, open(prefix + "_pmc.json", "w"), indent=1)
-    print(json.dumps(out.get("k_coarse_lanes", {}), indent=1))
+    print(json.dumps(out.get("k_coarse_list", {}), indent=1))
 
 
 if __name__ == "__main__":

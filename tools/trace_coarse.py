@@ -17,7 +17,7 @@ import sys
 
 def main():
     path = sys.argv[1]
-    name = sys.argv[2] if len(sys.argv) > 2 else "k_coarse_lanes"
+    name = sys.argv[2] if len(sys.argv) > 2 else "k_coarse_list"
     algo = float(sys.argv[3]) if len(sys.argv) > 3 else None
     rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], int(r["Stream_Id"]))
             for r in csv.DictReader(open(path))]
