@@ -3049,6 +3049,8 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
                                sizeof(int2) * (size_t)std::max(B.NvMax, 1);   // coarse + fine beam rows
             if (!ctx->skipped(K_SEED))
                 hipLaunchKernelGGL(k_seed_super, dim3(kSeedCands, n), dim3(1024), lds, st, d_items, zero);
+            else if (B.wl.cnt)   // (diagnostics) the work-list counters k_seed_super zeroes
+                LGS_HIP_CHECK(hipMemsetAsync(B.wl.cnt, 0, sizeof(int) * 16 * (size_t)n, st));
             ctx->timing_end(tok);
             LGS_HIP_CHECK(hipGetLastError());
         }
