@@ -7,7 +7,7 @@ O=gpurun_out/${TAG:-r03ab4}; rm -rf $O; mkdir -p $O
 uptime
 for i in 1 2 3; do
 for v in prune dense; do
-opt=""; [ $v = dense ] && opt="--ctx-option 9=0"
+opt=""; [ $v = dense ] && opt="${ALT:---ctx-option 9=0}"
 timeout -k 10 300 python -u bench.py --workload stream --no-cpu $opt > $O/s_$v$i.json 2> $O/s_$v$i.err || { tail -5 $O/s_$v$i.err; exit 1; }
 python3 -c "import json;d=json.loads([l for l in open('$O/s_$v$i.json') if l.startswith('{')][-1]);print('$v', d['value'], d['ms_per_step'])"
 done
