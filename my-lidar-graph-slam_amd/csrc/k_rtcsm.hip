@@ -938,9 +938,9 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
 // sb_mult covers any order).
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 constexpr int kOctPipe = 8;
-__device__ __forceinline__ double h16(unsigned long long bits)
+__device__ __forceinline__ float h16(unsigned long long bits)
 {
-    return (double)__builtin_bit_cast(SuperT, (unsigned short)(bits & 0xFFFFu));
+    return (float)__builtin_bit_cast(SuperT, (unsigned short)(bits & 0xFFFFu));
 }
 // NR = the superblock rows a lane sums per beam: 5 (nsby <= 5: the beam's
 // rows sit in one unit) or 9 (nsby <= 9: one unit + the high half of the next
@@ -971,9 +971,12 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
     const int* row = srow + lo;
     const int nq = (cnt + nb - 1) / nb;     // slot q takes beams nb i + q
     const long long wq4 = pl.Wq4;
-    double sr[NR];
+    // fp32 partial sums of the fp16 values (exact conversions; the rounding
+    // of up to Nv nonnegative fp32 additions is covered by the bound's
+    // factor m32 below)
+    float sr[NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) sr[r] = 0.0;
+    for (int r = 0; r < NR; ++r) sr[r] = 0.0f;
     for (int i0 = 0; i0 < nq; i0 += kOctPipe) {
         u64x2 x[kOctPipe];
         unsigned long long y[kOctPipe];
@@ -1010,7 +1013,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
         }
     }
 #pragma unroll
-    for (int r = 0; r < NR; ++r) part[w][lane][r] = sr[r];
+    for (int r = 0; r < NR; ++r) part[w][lane][r] = (double)sr[r];
     __syncthreads();
     if (w != 0) return;
     const int sbi = lane;
@@ -1021,7 +1024,10 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
         for (int j = 0; j < kSupWaves; ++j)
             for (int s = 0; s < nb; ++s) tot += part[j][s * nsbx + ca][rb];
     }
-    const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult;
+    // fp32 slack: a sum of m <= Nv nonnegative fp32 terms is at least the
+    // real sum times 1 - (m - 1) 2^-24 (to first order); twice that covers it
+    const double m32 = 1.0 + 2.0 * (double)(pl.Nv + 1) * 0x1p-24;
+    const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult * m32;
     if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
     const bool seedable = own;   // k_seed_super skips unsafe members
     double bv = seedable ? bound : -INFINITY;
