@@ -90,7 +90,8 @@ def parse():
                          "config2 = +-2 m/+-30 deg)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"),
                     help="rocprofv3 PMC summary (tools/pmc_summary.py) of THIS library build: roofline.traffic "
-                         "is taken from it only when its lib_sha256 matches liblgs_hip.so, else null")
+                         "is taken from it only when its lib_sha256 matches liblgs_hip.so, else null; other "
+                         "workloads read <pmc>_<workload>.json beside it")
     ap.add_argument("--loop-line", type=int, default=1,
                     help="match workload: also run config 5 (512 loop candidates sharded over the ranks, strong "
                          "scaling) after the timed region and report it as 'config5_strong_scaling'")
@@ -184,6 +185,10 @@ def pmc_for(pmc_path, trace_kernel, workload):
     sha256 and the bench workload profiled), else None.
     gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads
     (MI355X_MICROARCH.md §HBM): 'traffic' doubles it; the raw sum is kept too."""
+    if workload != "match":
+        # other workloads' passes sit beside the match summary as pmc_summary_<workload>.json
+        root, ext = os.path.splitext(pmc_path)
+        pmc_path = f"{root}_{workload}{ext}"
     try:
         pmc = json.load(open(pmc_path))
     except (OSError, ValueError):
