@@ -77,7 +77,9 @@
 extern "C" {
 #endif
 
-#define LGS_ABI_VERSION 1
+/* 2: lgs_carmen_load gained ids_bytes (include/lgs_io.h), options 6/12/14/16
+ * retired, options 22/23 and lgs_loop_records_allgather added */
+#define LGS_ABI_VERSION 2
 
 /* status codes */
 #define LGS_OK               0
@@ -166,11 +168,13 @@ int  lgs_abi_version(void);
 #define LGS_OPT_SKIP_MASK     10  /* diagnostics only: bitmask of kernels (lgs_ctx_kernel_stats order) not launched -- results are invalid */
 #define LGS_OPT_SUPER_PRUNE   9   /* 1 (default) = skip coarse blocks whose 4x4-superblock bound is below the seed score, 0 = evaluate every coarse block */
 #define LGS_OPT_RAY_CHUNK_KEYS 13  /* ray-cast keys per emit/sort/apply pass (default 2^28, max 2^30); more keys are cast in scan order over several passes */
-#define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: lane-per-block kernel for batches of at least this many matches (default 2; 1 = always), else the row kernel */
+#define LGS_OPT_LANES_MIN_BATCH 11 /* pruned coarse stage: the kept-superblock work list (lane-per-block sums) for batches of at least this many matches (default 2; 1 = always), else the row kernel */
 #define LGS_OPT_LINSOLVE_SPLIT 17 /* 1 (default) = a lone ScanMatcherLinearSolver refine of <= 1280 beams runs one workgroup per 64 beams (in-launch hand-off per pass) when they fit the device at once, 0 = one workgroup */
 #define LGS_OPT_HANDOFF_SPIN_US 18 /* split refine: bound of a workgroup's wait for the others (default 200000 us); on time-out the refine is rerun on one workgroup.  0 = force that fallback (tests) */
 #define LGS_OPT_PEER_COPY     19  /* lgs_loop_detect_rtcsm_multi, on the shard's ctx: 0 (default) = maps copied device to device (peer access enabled when the devices differ and allow it, else staged through pinned host memory), 1 = always staged through host memory */
 #define LGS_OPT_PRUNE_MIN_SUPER 21 /* superblock pruning only for windows of at least this many superblocks per angle (default 1); smaller windows score every coarse block */
+#define LGS_OPT_COOP_TILES    22  /* K3 one-launch sort (k_sort_wide): at most this many tiles for this ctx's launches (default -1 = the device's co-residency capacity, shared by every ctx of the process; 0 = always the multi-pass sort) */
+#define LGS_OPT_SORT_BARRIER_US 23 /* bound of a one-launch sort tile's wait at its grid barrier (default 50000 us); on time-out the call reports LGS_ERR_INTERNAL.  0 = time out at once (tests) */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

@@ -894,14 +894,21 @@ void run_linsolve(lgs_ctx* ctx, const lgs_grid* grid, const lgs_linsolve_params*
     const int groups = (refs[0].n + kGroup - 1) / kGroup;
     bool split = n == 1 && ctx->linsolve_split && groups <= kSplitMaxGroups && groups > 1;
     if (split) {
-        static int cus = -1, per_cu = -1;
-        if (cus < 0) {
-            hipDeviceProp_t prop;
-            LGS_HIP_CHECK(hipGetDeviceProperties(&prop, ctx->device));
-            cus = prop.multiProcessorCount;
-            LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_linsolve_split, kSplitThreads, 0));
+        // workgroups the device holds at once, per device (filled once under a lock)
+        static std::mutex mu;
+        static int cap[64] = {};
+        int c = 0;
+        if (ctx->device >= 0 && ctx->device < 64) {
+            std::lock_guard<std::mutex> g(mu);
+            if (!cap[ctx->device]) {
+                int cus = 0, per_cu = 0;
+                LGS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+                LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_linsolve_split, kSplitThreads, 0));
+                cap[ctx->device] = std::max(1, per_cu * cus);
+            }
+            c = cap[ctx->device];
         }
-        split = per_cu * cus >= groups;
+        split = c >= groups;
     }
     // split hand-off state: [flags (2 x kSplitMaxGroups) | timeout word | pad] then the terms
     constexpr size_t b_flags = 16 * ((sizeof(unsigned) * (2 * kSplitMaxGroups + 1) + 15) / 16);

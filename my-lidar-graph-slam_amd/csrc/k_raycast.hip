@@ -997,6 +997,13 @@ void map_expand(lgs_map* m, double minX, double minY, double maxX, double maxY, 
     map_resize(m, minPX, minPY, maxPX, maxPY);
 }
 
+// the ray-cast passes' device error word: 1 a ray cell outside the map (k_emit),
+// 2 the one-launch sort's grid barrier timed out (k_sort.hip)
+inline const char* bad_message(int bad)
+{
+    return (bad & 2) ? "k_sort_wide: grid barrier timed out (cooperative tiles not co-resident)"
+                     : "ray cell outside the map geometry";
+}
 inline double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
 inline double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
 
@@ -1327,7 +1334,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
         int cell_bits = 1;
         while (cell_bits < 32 && (1ull << cell_bits) < cells) ++cell_bits;
         unsigned* d_tmp = (unsigned*)ctx->ensure(S_RAY5, sizeof(unsigned) * keys);
-        keysort(ctx, d_keys, d_sorted, d_tmp, keys, ksh, cell_bits);
+        keysort(ctx, d_keys, d_sorted, d_tmp, keys, ksh, cell_bits, d_bad);
         tok = ctx->timing_begin(K_RAY_APPLY, 4.0 * (double)keys);
         if (tok >= 0) apply_tok = tok;
         const long long nw = (keys + 63) / 64;
@@ -1367,7 +1374,7 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
     std::memcpy(&runs, pin + 8, sizeof(runs));
     if (apply_tok >= 0) ctx->pending[apply_tok].algo_bytes += 32.0 * (double)runs;
     if (ctx->profile) ctx->harvest();
-    if (bad) throw Error(LGS_ERR_INTERNAL, "ray cell outside the map geometry");
+    if (bad) throw Error(LGS_ERR_INTERNAL, bad_message(bad));
 }
 
 void raycast(lgs_map* m, std::vector<HitsPtr>&& scans, const lgs_builder_params* bp)
@@ -1484,9 +1491,10 @@ struct LatestCache {
             else b.reset();
         }
         if (*h_bad) {
+            const int bad = *h_bad;
             drop_lists();
             *h_bad = 0;
-            throw Error(LGS_ERR_INTERNAL, "ray cell outside the map geometry");
+            throw Error(LGS_ERR_INTERNAL, bad_message(bad));
         }
     }
     KeyBufPtr acquire(long long need)
@@ -1750,7 +1758,7 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
     const int tok = ctx->timing_begin(K_RAY_APPLY, 4.0 * (double)(keys + nL));
     if (keys == 0) LGS_HIP_CHECK(hipMemsetAsync(C.d_long, 0, sizeof(unsigned), st));   // (k_runmask clears it)
     if (keys > 0) {
-        keysort(ctx, d_keys, buf->keys, d_tmp, keys, kTagShift, bits_for(cells));
+        keysort(ctx, d_keys, buf->keys, d_tmp, keys, kTagShift, bits_for(cells), C.d_bad);
         RunIndex ix{ C.d_tbl, nE, J.st, C.d_long };
         const long long nw = (keys + 63) / 64;
         hipLaunchKernelGGL(k_runmask, dim3((unsigned)((keys + 255) / 256)), dim3(256), 0, st, buf->keys, keys, 1,
@@ -1870,7 +1878,7 @@ void latest_rebuild(lgs_ctx* ctx, lgs_map* latest, lgs_map* local, const lgs_sca
     if (nlat > 0) {
         // the window's lists: the latest map's sorted keys partitioned by slot
         // (stable: each slot's keys stay in cell order), runs of (cell, slot)
-        keysort(ctx, tp.sorted, boot->keys, nullptr, nlat, 1, 4);
+        keysort(ctx, tp.sorted, boot->keys, nullptr, nlat, 1, 4, C.d_bad);
         const long long nw = (nlat + 63) / 64;
         hipLaunchKernelGGL(k_runmask, dim3((unsigned)((nlat + 255) / 256)), dim3(256), 0, st, boot->keys, nlat, 1,
                            boot->hitw, boot->endw, RunIndex{ C.d_tbl, nlat, stamps });

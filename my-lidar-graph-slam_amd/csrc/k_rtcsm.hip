@@ -1234,34 +1234,25 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, con
 #endif
 }
 
-// k_coarse_lanes (superblock pruning, batched launches): the same scores as
-// k_coarse_rows with one LANE per coarse block: workgroup (angle t, item) of
-// 4 waves, wave w takes kept superblocks 4w .. 4w + 3 (+16, ...), lane =
-// (superblock, member block), and every lane walks the beams in order with
-// pipelined gathers (seq_sum: the reference's sequential fp64 sum, no LDS).
-// A wave then carries 64 blocks' add chains at once instead of k_coarse_rows'
-// 4 adder lanes, which is what a batch of many scans needs (k_coarse_rows
-// keeps the lower latency for a lone scan).
-// Angles whose beams reach left of / below the map (tedge) need the unsafe
-// test of every kept block over those beams; the workgroup first compacts the
-// angle's edge beams (in beam order) into LDS, so each block walks only them
-// instead of all Nv beams (the loop detector's local maps put most angles
-// there).
+// The unsafe test of one angle (batched launches, k_unsafe_list): angles
+// whose beams reach left of / below the map (tedge) need the unsafe test of
+// every kept block over those beams; the workgroup first compacts the angle's
+// edge beams (in beam order) into LDS, so each block walks only them instead
+// of all Nv beams (the loop detector's local maps put most angles there).
+// Lane = (kept superblock, member block), four superblocks per wave.
 constexpr int kLaneWaves = 4;
 constexpr int kEdgeMax = 1024;     // edge beams compacted in LDS (more: the full walk); 8 KB keeps
 constexpr int kEdgeMaxNv = 4096;   // the occupancy of the kernel (measured: 32 KB cost config 2 30%)
 // One angle t of item `it`: its kept superblocks (the selection ballot), the
-// edge-beam compaction, then per kept block the sequential sum (unless
-// UNSAFE_ONLY: the sum is already in cscore, written by k_coarse_list) and the
-// unsafe test.  Called by a whole workgroup of kLaneWaves waves; the LDS
-// arrays are reused when a workgroup takes several angles (k_unsafe_list).
-template <bool UNSAFE_ONLY>
-__device__ __forceinline__ void coarse_angle(const MatchItem& it, int t, const double* __restrict__ zero)
+// edge-beam compaction, then per kept block the unsafe test (the sum is
+// already in cscore, written by k_coarse_list).  Called by a whole workgroup
+// of kLaneWaves waves; the LDS arrays are reused when a workgroup takes
+// several angles.
+__device__ __forceinline__ void unsafe_angle(const MatchItem& it, int t)
 {
     const RtcsmPlan& pl = it.pl;
     const double* __restrict__ cmap = it.cmap;
     const int2* __restrict__ idx = it.idx;
-    const int* __restrict__ cb = it.cbase + (size_t)t * pl.Nv;
     const int gen = it.gen;
     __shared__ int s_sb[64];
     __shared__ int s_cnt;
@@ -1270,7 +1261,6 @@ __device__ __forceinline__ void coarse_angle(const MatchItem& it, int t, const d
     double L = -INFINITY;
 #pragma unroll
     for (int b = 0; b < kSeedCands; ++b) L = fmax(L, it.Lc[b]);
-    if (!UNSAFE_ONLY && t == 0 && tid == 0) *it.Lp = L;
     const bool te = it.tedge[t] == gen;
     __syncthreads();   // the previous angle's LDS is read
     // kept superblocks of this angle (nsb2 <= 64 on this path), in key order
@@ -1283,15 +1273,6 @@ __device__ __forceinline__ void coarse_angle(const MatchItem& it, int t, const d
         const unsigned long long bal = __ballot(kp);
         if (kp) s_sb[__popcll(bal & ((1ull << lane) - 1ull))] = lane;
         if (lane == 0) s_cnt = __popcll(bal);
-        if (!UNSAFE_ONLY && lane == 0) {
-            unsigned long long nb = 0;
-            for (unsigned long long mm = bal; mm; mm &= mm - 1) {
-                const int sb = __ffsll((long long)mm) - 1;
-                const int a = sb % pl.nsbx, b = sb / pl.nsbx;
-                nb += (unsigned long long)(min(kSB, pl.ncx - kSB * a) * min(kSB, pl.ncy - kSB * b));
-            }
-            if (nb) atomicAdd(&it.rec->coarse_evals, nb);
-        }
     }
     __syncthreads();
     const int cnt = s_cnt;
@@ -1331,12 +1312,8 @@ __device__ __forceinline__ void coarse_angle(const MatchItem& it, int t, const d
         const int sb = has ? s_sb[e] : 0;
         const int jx = kSB * (sb % pl.nsbx) + (m & 3), jy = kSB * (sb / pl.nsbx) + (m >> 2);
         const bool active = has && jx < pl.ncx && jy < pl.ncy;
-        const double* __restrict__ lane_base = cmap + (active ? jy * pl.Wqp + jx : 0);
         const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
-        // inactive lanes (partial superblocks, the wave's tail) read the zero cell
-        const double sum = UNSAFE_ONLY ? (active ? it.cscore[k] : 0.0)
-                                       : seq_sum<int>(pl.Nv, [&](int v) { return cb[v]; },
-                                                      [&](const int& c) { return active ? lane_base + c : zero; });
+        const double sum = active ? it.cscore[k] : 0.0;
         // unsafe: some coarse read left of / below the map while the block's
         // fine reads can land inside (x, y >= -(lr-1)); rare, so a separate pass
         // (+ ext: the strip reads' bound of the fine values, see strip_read)
@@ -1359,7 +1336,6 @@ __device__ __forceinline__ void coarse_angle(const MatchItem& it, int t, const d
             }
         }
         if (active) {
-            if (!UNSAFE_ONLY) it.cscore[k] = sum;
             // an unsafe block whose fine scores all stay below L can change
             // nothing: it is treated as safe (c <= bound < L)
             it.cflag[k] = (unsafe && (sum + ext) * pl.sb_mult >= L) ? 1 : 0;
@@ -1367,15 +1343,8 @@ __device__ __forceinline__ void coarse_angle(const MatchItem& it, int t, const d
     }
 }
 
-__global__ __launch_bounds__(64 * kLaneWaves) void k_coarse_lanes(Items items, const double* __restrict__ zero)
-{
-    const MatchItem& it = items[blockIdx.y];
-    if ((int)blockIdx.x >= it.pl.T) return;   // past this item's angles (uniform)
-    coarse_angle<false>(it, blockIdx.x, zero);
-}
-
-// Kept-superblock work list (the batched default; k_coarse_lanes above is the
-// fallback for rows longer than kListMaxNv).  Most angles of a batch keep 0-3
+// Kept-superblock work list (every pruned batch; a lone match takes
+// k_coarse_rows).  Most angles of a batch keep 0-3
 // superblocks (loop closure: 76% keep none), so one workgroup per angle leaves
 // most lanes idle.  k_keep lists every kept (angle, superblock) of each item
 // -- the same selection, counted into the item's record -- and the angles
@@ -1449,8 +1418,9 @@ __device__ __forceinline__ int list_prefix(const WorkList& W, int which, int n, 
     return __shfl(c, 63, 64);
 }
 
-// Four listed superblocks per wave (grid-stride over the list): the same
-// sequential fp64 sums as k_coarse_lanes'.  cflag is 0 here; k_unsafe_list
+// Four listed superblocks per wave (grid-stride over the list): lane =
+// (superblock, member block), every lane walks the beams in order with
+// pipelined gathers (seq_sum: the reference's sequential fp64 sum).  cflag is 0 here; k_unsafe_list
 // then redoes the edge angles' blocks.
 __global__ __launch_bounds__(64) void k_coarse_list(Items items, WorkList W, int n, int rowlen,
                                                     const double* __restrict__ zero)
@@ -1507,7 +1477,7 @@ __global__ __launch_bounds__(64) void k_coarse_list(Items items, WorkList W, int
 }
 
 // The unsafe test of the listed edge angles (k_keep), one angle at a time per
-// workgroup (grid-stride), as k_coarse_lanes runs it.
+// workgroup (grid-stride).
 __global__ __launch_bounds__(64 * kLaneWaves) void k_unsafe_list(Items items, WorkList W, int n,
                                                                  const double* __restrict__ zero)
 {
@@ -1518,7 +1488,7 @@ __global__ __launch_bounds__(64 * kLaneWaves) void k_unsafe_list(Items items, Wo
         const int j = __popcll(__ballot(lane < n && c <= a));
         const int cprev = __shfl(c, max(j - 1, 0), 64);
         const int before = j > 0 ? cprev : 0;
-        coarse_angle<true>(items[j], W.al[(size_t)j * W.tmax + (a - before)], zero);
+        unsafe_angle(items[j], W.al[(size_t)j * W.tmax + (a - before)]);
     }
 }
 
@@ -2683,7 +2653,7 @@ struct BatchShape {
     bool fine_lanes = false;   // k_compact + k_fine_lanes (lr * lr <= 64)
     int frows = 1;
     int kernel_size = 0;
-    WorkList wl{};          // kept-superblock work list (wl.cnt null: k_coarse_lanes)
+    WorkList wl{};          // kept-superblock work list (wl.cnt null: k_coarse_rows)
 };
 
 // per-(chunk|tile, angle) best entries the seed kernel scans: k_super's
@@ -3072,14 +3042,10 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * beams_K);
         if (tok >= 0) ctx->pending[tok].coarse_evals = true;   // algorithmic bytes from the records
         if (ctx->skipped(K_COARSE)) {
-        } else if (n >= ctx->lanes_min_batch) {
-            if (wl) {
-                const int rowlen = std::max(B.NvMax, 1);
-                hipLaunchKernelGGL(k_coarse_list, dim3(kListWaves), dim3(64), sizeof(int) * 4 * (size_t)rowlen, st,
-                                   d_items, B.wl, n, rowlen, zero);
-            } else {
-                hipLaunchKernelGGL(k_coarse_lanes, dim3(B.Tmax, n), dim3(64 * kLaneWaves), 0, st, d_items, zero);
-            }
+        } else if (wl) {
+            const int rowlen = std::max(B.NvMax, 1);
+            hipLaunchKernelGGL(k_coarse_list, dim3(kListWaves), dim3(64), sizeof(int) * 4 * (size_t)rowlen, st,
+                               d_items, B.wl, n, rowlen, zero);
         } else {
             const size_t lds = ((sizeof(int) * (size_t)B.NvMax + 15) & ~(size_t)15) +
                                sizeof(double) * 128 * kRing * kRowWaves;

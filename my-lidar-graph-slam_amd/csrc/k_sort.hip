@@ -19,13 +19,16 @@
 #include "lgs_internal.hpp"
 
 #include <algorithm>
+#include <mutex>
+#include <utility>
+#include <vector>
 
 namespace {
 
 constexpr int kSortThreads = 256;
 constexpr int kSortRadix = 256;        // bins per pass (digits of at most 8 bits)
-// control words (S_RAY0): k_sort_wide's grid barrier [arrived, done], zero
-// between sorts (the last workgroup out resets them)
+// control words (S_RAY0): k_sort_wide's grid barrier [arrived, done, abort],
+// zero between sorts (the last workgroup out resets them)
 constexpr int kCtlBar = 0;
 constexpr int kCtlWords = 8;
 
@@ -218,17 +221,34 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_down(const unsigned* __re
 // give), scatters, and waits again before the next pass reads the keys.
 // Stores are released and loads acquired at agent scope around each barrier
 // (the tiles live on different XCDs, each with its own L2).
-__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target)
+// The wait is bounded (`ticks` of s_memrealtime, 100 MHz; LGS_OPT_SORT_BARRIER_US):
+// a tile that waits longer -- its peers cannot all be resident -- raises the
+// abort word, every tile leaves, and the caller's error word reads 2 (a loud
+// failure instead of a hung GPU; the host reservation below keeps it from
+// happening within one process).
+__device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned target, unsigned long long ticks)
 {
+    __shared__ int s_ok;
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        int ok = 1;
+        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(bar + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                __builtin_amdgcn_s_memrealtime() - t0 >= ticks) {
+                __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        s_ok = ok;
     }
     __syncthreads();
+    return s_ok != 0;
 }
 
 // Wide tiles for the cooperative sort: 512 threads x 16 keys (8192 keys per
@@ -249,7 +269,8 @@ __global__ __launch_bounds__(kWideThreads) void k_sort_wide(const unsigned* __re
                                                             unsigned* __restrict__ out, unsigned* __restrict__ tmp,
                                                             long long n, int lo, int dbits, int bits, int passes,
                                                             unsigned* __restrict__ counts,
-                                                            unsigned* __restrict__ bar)
+                                                            unsigned* __restrict__ bar, int* __restrict__ err,
+                                                            unsigned long long ticks)
 {
     constexpr int NT = kWideThreads, NW = NT / 64, KPT = kWideKPT, TILE = kWideTile;
     constexpr int R = 1 << RB;
@@ -357,7 +378,7 @@ __global__ __launch_bounds__(kWideThreads) void k_sort_wide(const unsigned* __re
                 keys_s[dstart[dd] + cw[dd] + rank[i]] = k[i];
             }
         LGS_PROBE_MARK();
-        grid_barrier(bar, ++nbar * ntiles);
+        if (!grid_barrier(bar, ++nbar * ntiles, ticks)) break;
         LGS_PROBE_MARK();
         // digit totals over all tiles and the counts of the tiles before this one
         unsigned all[Q], before[Q], asum = 0, incl2 = 0;
@@ -406,15 +427,18 @@ __global__ __launch_bounds__(kWideThreads) void k_sort_wide(const unsigned* __re
             const unsigned dd = (key >> shift) & mask;
             dst[gbase[dd] + (unsigned)j - dstart[dd]] = key;
         }
-        if (p + 1 < passes) grid_barrier(bar, ++nbar * ntiles);
+        if (p + 1 < passes && !grid_barrier(bar, ++nbar * ntiles, ticks)) break;
         LGS_PROBE_MARK();
     }
     LGS_PROBE_PRINT("k_sort_wide");
     __syncthreads();
-    if (tid == 0 &&
-        __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ntiles - 1) {
-        __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+        if (__hip_atomic_load(bar + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) && err) *err = 2;
+        if (__hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ntiles - 1) {
+            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(bar + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -422,25 +446,79 @@ __global__ __launch_bounds__(kWideThreads) void k_sort_wide(const unsigned* __re
 
 namespace lgs {
 
-// Workgroups of k_sort_wide the device holds at once (all its tiles must be
-// resident: they wait for each other), with a margin for other streams' work.
-long long coop_capacity(lgs_ctx* ctx)
+// Co-residency of k_sort_wide across the process: its tiles wait for each
+// other, so the tiles of every k_sort_wide in flight on a device -- from any
+// lgs_ctx, on any stream -- must fit the device at once.  Each launch
+// reserves its tiles against the device's capacity (half its occupancy: a
+// margin for other streams' and processes' work) and holds them until an
+// event recorded after the launch has completed; a sort that does not fit
+// beside the others takes the reduce-then-scan passes.  Reserve, launch and
+// record happen under the device's lock, so no event is queried before it is
+// recorded.
+struct CoopDevice {
+    std::mutex mu;
+    long long cap = 0, used = 0;
+    std::vector<std::pair<hipEvent_t, long long>> live;   // (event after the launch, tiles)
+    std::vector<hipEvent_t> spare;
+    void reclaim()
+    {
+        for (size_t i = 0; i < live.size();) {
+            if (hipEventQuery(live[i].first) == hipSuccess) {
+                used -= live[i].second;
+                spare.push_back(live[i].first);
+                live[i] = live.back();
+                live.pop_back();
+            } else {
+                ++i;
+            }
+        }
+    }
+};
+CoopDevice g_coop[64];
+
+// Launches the one-launch sort when its tiles fit beside the device's other
+// cooperative launches; false: not launched (take the multi-pass sort).
+template <typename Launch>
+bool coop_launch(lgs_ctx* ctx, long long tiles, Launch&& launch)
 {
-    static long long cap[64] = {};
     const int dev = ctx->device;
-    if (dev < 0 || dev >= 64) return 0;
-    if (!cap[dev]) {
+    if (dev < 0 || dev >= 64) return false;
+    CoopDevice& D = g_coop[dev];
+    std::lock_guard<std::mutex> lk(D.mu);
+    if (!D.cap) {
         int per_cu = 0, cus = 0;
         LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_wide<10>, kWideThreads, 0));
         LGS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        cap[dev] = std::max(1LL, (long long)per_cu * cus / 2);
+        D.cap = std::max(1LL, (long long)per_cu * cus / 2);
     }
-    return cap[dev];
+    const long long cap = ctx->coop_tiles >= 0 ? std::min(D.cap, ctx->coop_tiles) : D.cap;
+    if (tiles > cap) return false;
+    if (D.used + tiles > cap || D.live.size() >= 16) D.reclaim();
+    if (D.used + tiles > cap) return false;
+    hipEvent_t ev = nullptr;
+    if (!D.spare.empty()) {
+        ev = D.spare.back();
+        D.spare.pop_back();
+    } else {
+        LGS_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    launch();
+    const hipError_t le = hipGetLastError();
+    if (le != hipSuccess) {
+        D.spare.push_back(ev);
+        LGS_HIP_CHECK(le);
+    }
+    LGS_HIP_CHECK(hipEventRecord(ev, ctx->stream));
+    D.used += tiles;
+    D.live.emplace_back(ev, tiles);
+    return true;
 }
 
 // Stable sort of n 32-bit keys on bits [lo, lo + bits).  `tmp` (n keys) is
 // needed when the sort takes two or more passes; in, tmp and out are distinct.
-void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, long long n, int lo, int bits)
+// `err` (device-visible, may be null): set to 2 if the one-launch sort's grid
+// barrier timed out (its output is then invalid).
+void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, long long n, int lo, int bits, int* err)
 {
     hipStream_t st = ctx->stream;
     LGS_REQUIRE(n >= 0 && n < (1LL << 30), "keysort: at most 2^30 keys");
@@ -460,17 +538,19 @@ void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, lon
         const int wp = bits > 16 ? (bits + 9) / 10 : (bits + 7) / 8;
         const int wd = (bits + wp - 1) / wp;
         const long long ctiles = (n + kWideTile - 1) / kWideTile;
-        if (ctiles <= coop_capacity(ctx) && (wp == 1 || tmp)) {
+        if (wp == 1 || tmp) {
             const int rb = wd > 8 ? 10 : 8;
             unsigned* counts = (unsigned*)ctx->ensure(S_RAY1, sizeof(unsigned) * (size_t)ctiles * (1u << rb) * wp);
-            if (rb == 10)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_wide<10>), dim3((unsigned)ctiles), dim3(kWideThreads), 0, st,
-                                   in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar);
-            else
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_wide<8>), dim3((unsigned)ctiles), dim3(kWideThreads), 0, st,
-                                   in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar);
-            LGS_HIP_CHECK(hipGetLastError());
-            return;
+            const unsigned long long ticks = (unsigned long long)ctx->sort_barrier_us * 100ull;   // 100 MHz
+            const bool done = coop_launch(ctx, ctiles, [&] {
+                if (rb == 10)
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_wide<10>), dim3((unsigned)ctiles), dim3(kWideThreads), 0,
+                                       st, in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar, err, ticks);
+                else
+                    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_wide<8>), dim3((unsigned)ctiles), dim3(kWideThreads), 0,
+                                       st, in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar, err, ticks);
+            });
+            if (done) return;
         }
     }
     // reduce-then-scan passes of 8-bit digits
@@ -499,7 +579,8 @@ void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, lon
 }  // namespace lgs
 
 // Diagnostics entry (tests): stable sort of host keys on bits [lo, lo + bits)
-// through the device path.
+// through the device path; LGS_ERR_INTERNAL if the one-launch sort's grid
+// barrier timed out.
 extern "C" int lgs_debug_keysort(lgs_ctx* ctx, const unsigned* keys, unsigned* out, long long n, int lo, int bits)
 {
     using namespace lgs;
@@ -508,16 +589,21 @@ extern "C" int lgs_debug_keysort(lgs_ctx* ctx, const unsigned* keys, unsigned* o
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
         if (n == 0) return;
         unsigned* d = nullptr;
-        LGS_HIP_CHECK(hipMalloc(&d, sizeof(unsigned) * 3 * (size_t)n));
+        LGS_HIP_CHECK(hipMalloc(&d, sizeof(unsigned) * (3 * (size_t)n + 1)));
+        int err = 0;
         try {
+            int* d_err = (int*)(d + 3 * n);
+            LGS_HIP_CHECK(hipMemsetAsync(d_err, 0, sizeof(int), ctx->stream));
             LGS_HIP_CHECK(hipMemcpyAsync(d, keys, sizeof(unsigned) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-            keysort(ctx, d, d + n, d + 2 * n, n, lo, bits);
+            keysort(ctx, d, d + n, d + 2 * n, n, lo, bits, d_err);
             LGS_HIP_CHECK(hipMemcpyAsync(out, d + n, sizeof(unsigned) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+            LGS_HIP_CHECK(hipMemcpyAsync(&err, d_err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
             ctx->sync();
         } catch (...) {
             hipFree(d);
             throw;
         }
         LGS_HIP_CHECK(hipFree(d));
+        if (err) throw Error(LGS_ERR_INTERNAL, "k_sort_wide: grid barrier timed out (cooperative tiles not co-resident)");
     });
 }

@@ -441,6 +441,11 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_POISON_WS: ctx->poison_ws = value != 0.0; return LGS_OK;
     case LGS_OPT_PEER_COPY: ctx->peer_staged = value != 0.0; return LGS_OK;
     case LGS_OPT_PRUNE_MIN_SUPER: ctx->prune_min_super = (int)value; return LGS_OK;
+    case LGS_OPT_COOP_TILES: ctx->coop_tiles = (long long)value; return LGS_OK;
+    case LGS_OPT_SORT_BARRIER_US:
+        if (value < 0) return LGS_ERR_INVALID_ARG;
+        ctx->sort_barrier_us = (long long)value;
+        return LGS_OK;
     case LGS_OPT_LINSOLVE_SPLIT: ctx->linsolve_split = value != 0.0; return LGS_OK;
     case LGS_OPT_HANDOFF_SPIN_US:
         if (value < 0.0) return LGS_ERR_INVALID_ARG;
@@ -531,8 +536,10 @@ extern "C" int lgs_grid_upload(lgs_ctx* ctx, lgs_grid* g, const double* host)
 {
     if (!ctx || !g || !host) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
+        LGS_REQUIRE(!g->map_view, "cannot upload into a map's grid view");
         size_t bytes = (size_t)g->w * (size_t)g->h * sizeof(double);
         if (!bytes) return;
+        grid_acquire(ctx, g);
         LGS_HIP_CHECK(hipMemcpyAsync(g->d, host, bytes, hipMemcpyHostToDevice, ctx->stream));
         ctx->sync();
     });
@@ -543,20 +550,22 @@ namespace {
 // slot[p] = staging index of patch p or -1 (unallocated: Unknown 0.0).  The
 // value is one 8-byte load at value_offset of the cell (the vptr half of a
 // 16-byte BinaryBayesGridCell is never read).
-__global__ __launch_bounds__(256) void k_patch_ingest(double* __restrict__ grid, int W, int ps, int npx,
+__global__ __launch_bounds__(256) void k_patch_ingest(double* __restrict__ grid, int W, int H, int ps, int npx,
                                                       const int* __restrict__ slot,
                                                       const unsigned char* __restrict__ cells, int cell_bytes,
                                                       int value_offset)
 {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= W) return;
-    const int s = slot[(y / ps) * npx + x / ps];
-    double v = 0.0;
-    if (s >= 0) {
-        const size_t c = (size_t)s * ps * ps + (size_t)(y % ps) * ps + (x % ps);
-        v = *(const double*)(cells + c * cell_bytes + value_offset);
+    for (int y = blockIdx.y; y < H; y += gridDim.y) {   // rows grid-stride (gridDim.y <= 65535)
+        const int s = slot[(y / ps) * npx + x / ps];
+        double v = 0.0;
+        if (s >= 0) {
+            const size_t c = (size_t)s * ps * ps + (size_t)(y % ps) * ps + (x % ps);
+            v = *(const double*)(cells + c * cell_bytes + value_offset);
+        }
+        grid[(size_t)y * W + x] = v;
     }
-    grid[(size_t)y * W + x] = v;
 }
 }  // namespace
 
@@ -565,6 +574,8 @@ extern "C" int lgs_grid_upload_patches(lgs_ctx* ctx, lgs_grid* g, const void* co
 {
     if (!ctx || !g || (!patches && npx * npy > 0)) return LGS_ERR_INVALID_ARG;
     return guarded(ctx, [&] {
+        // a map's view: its cells change only through the map (counters, patch flags)
+        LGS_REQUIRE(!g->map_view, "cannot upload into a map's grid view");
         LGS_REQUIRE(npx >= 0 && npy >= 0 && ps >= 1, "invalid patch geometry");
         LGS_REQUIRE((long long)npx * ps == g->w && (long long)npy * ps == g->h,
                     "grid size must be npx*patch_size x npy*patch_size");
@@ -573,6 +584,7 @@ extern "C" int lgs_grid_upload_patches(lgs_ctx* ctx, lgs_grid* g, const void* co
                     "cell_bytes / value_offset must describe an aligned fp64 inside each cell");
         if (!g->w || !g->h) return;
         LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        grid_acquire(ctx, g);   // after any pending asynchronous writer of g
         const int np = npx * npy;
         const size_t patch_bytes = (size_t)ps * ps * cell_bytes;
         // slot table first (16-byte padded), then the allocated patches in table order
@@ -600,8 +612,8 @@ extern "C" int lgs_grid_upload_patches(lgs_ctx* ctx, lgs_grid* g, const void* co
             LGS_HIP_CHECK(hipMemcpyAsync(d + b_slot + (size_t)c0 * patch_bytes, h + b_slot + (size_t)c0 * patch_bytes,
                                          (size_t)(c1 - c0) * patch_bytes, hipMemcpyHostToDevice, ctx->stream));
         }
-        hipLaunchKernelGGL(k_patch_ingest, dim3((g->w + 255) / 256, g->h), dim3(256), 0, ctx->stream, g->d, g->w, ps,
-                           npx, (const int*)d, (const unsigned char*)(d + b_slot), cell_bytes, value_offset);
+        hipLaunchKernelGGL(k_patch_ingest, dim3((g->w + 255) / 256, std::min(g->h, 65535)), dim3(256), 0, ctx->stream,
+                           g->d, g->w, g->h, ps, npx, (const int*)d, (const unsigned char*)(d + b_slot), cell_bytes, value_offset);
         LGS_HIP_CHECK(hipGetLastError());
         ctx->sync();
     });
@@ -1164,11 +1176,38 @@ extern "C" void lgs_scan_destroy(lgs_scan* s)
 }
 
 namespace lgs {
+void wait_foreign_scans(ForeignScans& f)
+{
+    for (auto& e : f)
+        if (e.second && e.second->wait() == 2)
+            throw Error(LGS_ERR_INTERNAL, "a scan's device copy was abandoned by the context that made it");
+    // enqueued on another context's stream, maybe still pending
+    LGS_HIP_CHECK(hipDeviceSynchronize());
+    for (auto& e : f) {
+        std::lock_guard<std::mutex> g(e.first->dev_mu);
+        if (e.first->dev_fence == e.second) e.first->dev_done.store(true, std::memory_order_release);
+    }
+    f.clear();
+}
+
+void abandon_scan_copies(lgs_ctx* ctx, const std::shared_ptr<CopyFence>& fence, const std::vector<lgs_scan*>& scans)
+{
+    for (lgs_scan* s : scans) {
+        std::lock_guard<std::mutex> g(s->dev_mu);
+        if (s->dev_fence != fence || !s->d_ranges) continue;
+        scan_buffer_put(ctx->device, s->d_ranges, 2 * sizeof(double) * (size_t)s->n);
+        s->d_ranges = s->d_angles = nullptr;
+        s->dev_ctx = nullptr;
+        s->dev_fence.reset();
+    }
+    fence->set(2);
+}
+
 void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n, Upload* up)
 {
     // scans without a copy yet (each once), and copies made by other contexts
     std::vector<lgs_scan*> todo;
-    bool foreign = false;
+    ForeignScans foreign;
     for (int j = 0; j < n; ++j) {
         lgs_scan* s = const_cast<lgs_scan*>(scans[j]);
         if (!s || s->dev_done.load(std::memory_order_acquire)) continue;
@@ -1176,57 +1215,70 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n, Upload* 
         if (!s->d_ranges) {
             if (std::find(todo.begin(), todo.end(), s) == todo.end()) todo.push_back(s);
         } else if (s->dev_ctx != ctx) {
-            foreign = true;
+            foreign.emplace_back(s, s->dev_fence);
         }
     }
-    if (foreign) {   // enqueued on another context's stream, maybe still pending
-        LGS_HIP_CHECK(hipDeviceSynchronize());
-        for (int j = 0; j < n; ++j) {
-            lgs_scan* s = const_cast<lgs_scan*>(scans[j]);
-            if (!s) continue;
-            std::lock_guard<std::mutex> g(s->dev_mu);
-            if (s->d_ranges && s->dev_ctx != ctx) s->dev_done.store(true, std::memory_order_release);
-        }
-    }
-    if (todo.empty()) return;
     size_t total = 0;
     for (lgs_scan* s : todo) total += 2 * sizeof(double) * (size_t)s->n;
-    const int b = ctx->bank;
-    if (ctx->scan_ev_live[b]) {   // the staging's previous copies are done
-        LGS_HIP_CHECK(hipEventSynchronize(ctx->scan_ev[b]));
-        ctx->scan_ev_live[b] = false;
-    }
-    char* pin = (char*)grow_pinned(ctx->stream, ctx->pinned_scan[b], ctx->pinned_scan_bytes[b], total, true);
-    size_t off = 0;
     std::vector<FetchSeg> segs;
-    for (lgs_scan* s : todo) {
-        std::lock_guard<std::mutex> g(s->dev_mu);
-        if (s->d_ranges) continue;   // another thread got there first
-        const size_t bytes = sizeof(double) * (size_t)s->n;
-        double* d = (double*)scan_buffer_get(ctx->device, 2 * bytes);
-        std::memcpy(pin + off, s->h_ranges.data(), bytes);
-        std::memcpy(pin + off + bytes, s->h_angles.data(), bytes);
-        try {
-            segs.push_back(fetch_seg(d, pin + off, 2 * bytes));
-        } catch (...) {
-            scan_buffer_put(ctx->device, d, 2 * bytes);
-            throw;
+    std::vector<lgs_scan*> mine;
+    auto fence = std::make_shared<CopyFence>();
+    const int b = ctx->bank;
+    if (!todo.empty()) {
+        if (ctx->scan_ev_live[b]) {   // the staging's previous copies are done
+            LGS_HIP_CHECK(hipEventSynchronize(ctx->scan_ev[b]));
+            ctx->scan_ev_live[b] = false;
         }
-        off += 2 * bytes;
-        s->d_angles = d + s->n;
-        s->dev_ctx = ctx;
-        s->d_ranges = d;
+        char* pin = (char*)grow_pinned(ctx->stream, ctx->pinned_scan[b], ctx->pinned_scan_bytes[b], total, true);
+        size_t off = 0;
+        for (lgs_scan* s : todo) {
+            std::lock_guard<std::mutex> g(s->dev_mu);
+            if (s->d_ranges) {   // another thread got there first
+                if (s->dev_ctx != ctx) foreign.emplace_back(s, s->dev_fence);
+                continue;
+            }
+            const size_t bytes = sizeof(double) * (size_t)s->n;
+            double* d = (double*)scan_buffer_get(ctx->device, 2 * bytes);
+            std::memcpy(pin + off, s->h_ranges.data(), bytes);
+            std::memcpy(pin + off + bytes, s->h_angles.data(), bytes);
+            try {
+                segs.push_back(fetch_seg(d, pin + off, 2 * bytes));
+            } catch (...) {
+                scan_buffer_put(ctx->device, d, 2 * bytes);
+                throw;
+            }
+            off += 2 * bytes;
+            s->d_angles = d + s->n;
+            s->dev_ctx = ctx;
+            s->dev_fence = fence;   // published now; other contexts wait for the fence
+            s->d_ranges = d;
+            mine.push_back(s);
+        }
     }
     if (up) {
         // copied with the call's upload (one launch); the upload is flushed
-        // before any kernel of the call reads the scans
+        // before any kernel of the call reads the scans, and sets the fence
         up->extra.insert(up->extra.end(), segs.begin(), segs.end());
+        if (!mine.empty()) {
+            up->fence = fence;
+            up->fence_scans = mine;
+        }
+        up->foreign.insert(up->foreign.end(), foreign.begin(), foreign.end());
         return;
     }
-    fetch_list(ctx, segs);
-    if (!ctx->scan_ev[b]) LGS_HIP_CHECK(hipEventCreateWithFlags(&ctx->scan_ev[b], hipEventDisableTiming));
-    LGS_HIP_CHECK(hipEventRecord(ctx->scan_ev[b], ctx->stream));
-    ctx->scan_ev_live[b] = true;
+    if (!mine.empty()) {
+        try {
+            fetch_list(ctx, segs);
+        } catch (...) {
+            abandon_scan_copies(ctx, fence, mine);
+            throw;
+        }
+        if (!ctx->scan_ev[b]) LGS_HIP_CHECK(hipEventCreateWithFlags(&ctx->scan_ev[b], hipEventDisableTiming));
+        LGS_HIP_CHECK(hipEventRecord(ctx->scan_ev[b], ctx->stream));
+        ctx->scan_ev_live[b] = true;
+        fence->set(1);
+    }
+    if (!foreign.empty()) wait_foreign_scans(foreign);
 }
 
 // Beams with range < ScanRangeMax in beam order (ComputeScanIndices filter,

@@ -18,6 +18,8 @@
 #include <memory>
 #include <mutex>
 #include <atomic>
+#include <condition_variable>
+#include <utility>
 #include <vector>
 
 #include "lgs_hip.h"
@@ -255,11 +257,13 @@ struct lgs_ctx {
     bool super_prune = true;     // superblock pruning of k_coarse (LGS_OPT_SUPER_PRUNE)
     bool linsolve_split = true;  // lone refine over one workgroup per 64 beams (LGS_OPT_LINSOLVE_SPLIT)
     long long handoff_spin_us = 200000;   // split refine spin bound (LGS_OPT_HANDOFF_SPIN_US; 0 = force the fallback)
+    long long coop_tiles = -1;   // one-launch sort: tile limit for this ctx (LGS_OPT_COOP_TILES; -1 = device capacity)
+    long long sort_barrier_us = 50000;   // one-launch sort: barrier wait bound (LGS_OPT_SORT_BARRIER_US)
     long long handoff_fallbacks = 0;      // split refines rerun on one workgroup after a time-out
     bool peer_staged = false;    // cross-context copies through host memory (LGS_OPT_PEER_COPY)
     int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
     long long copies_direct = 0, copies_staged = 0;   // lgs_debug_copy_counters
-    int lanes_min_batch = 2;     // pruned coarse stage: k_coarse_lanes from this batch size on (LGS_OPT_LANES_MIN_BATCH)
+    int lanes_min_batch = 2;     // pruned coarse stage: the work list (k_coarse_list) from this batch size on (LGS_OPT_LANES_MIN_BATCH)
     long long ray_chunk_keys = 1LL << 28;  // ray-cast keys per emit/sort/apply pass (LGS_OPT_RAY_CHUNK_KEYS)
     // Stamps come from one process-wide counter: a context's scratch may be
     // memory a destroyed context used, and its stale tags must never match.
@@ -394,6 +398,35 @@ struct lgs_grid {
     std::shared_ptr<lgs::WriterEvent> writer;   // pending writer of the cells (null: none)
 };
 
+namespace lgs {
+// A scan's first device copy, as other contexts see it: 0 published but not
+// yet enqueued (the copy rides on its call's upload, flushed later in that
+// call), 1 enqueued on the copying context's stream, 2 abandoned (the flush
+// failed; the scan was unpublished).  A context that finds a scan copied by
+// another waits for 1 -- after enqueueing its own copies, so two calls that
+// first touch each other's scans cannot wait for each other -- and then for
+// the device.
+struct CopyFence {
+    std::mutex mu;
+    std::condition_variable cv;
+    int state = 0;
+    void set(int s)
+    {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            state = s;
+        }
+        cv.notify_all();
+    }
+    int wait()
+    {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return state != 0; });
+        return state;
+    }
+};
+}  // namespace lgs
+
 struct lgs_scan {
     lgs_ctx* ctx = nullptr;   // creating context (not used after its destruction)
     int device = 0;
@@ -406,6 +439,7 @@ struct lgs_scan {
     double* d_angles = nullptr;
     std::mutex dev_mu;
     const lgs_ctx* dev_ctx = nullptr;   // whose stream the copy went on
+    std::shared_ptr<lgs::CopyFence> dev_fence;   // when the copy is enqueued
     std::atomic<bool> dev_done{ false };  // the copy is known to be complete
     int n = 0;
     lgs_pose2d rel{0, 0, 0};
@@ -466,6 +500,12 @@ const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* scan, double scan_range_ma
 // the staging is reused only after the call's synchronisation).
 struct Upload;
 void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n, Upload* up = nullptr);
+// scans whose first copy another context made: wait until it is enqueued
+// there, then for the device (lgs_core.hip)
+using ForeignScans = std::vector<std::pair<lgs_scan*, std::shared_ptr<CopyFence>>>;
+void wait_foreign_scans(ForeignScans& f);
+// a first copy that was never enqueued: the scans lose their device copy
+void abandon_scan_copies(lgs_ctx* ctx, const std::shared_ptr<CopyFence>& fence, const std::vector<lgs_scan*>& scans);
 // Host-to-device copy of pinned staging (the ctx's coherent hipHostMalloc
 // buffers) by a kernel on ctx->stream (k_fetch): a small hipMemcpyAsync waits
 // ~11 us in the copy engine's queue and takes ~6 us more (r03 trace of the
@@ -508,6 +548,9 @@ struct Upload {
     std::vector<char> host;
     char* dev = nullptr;
     std::vector<FetchSeg> extra;   // other staged copies launched with this one (scans' first copies)
+    std::shared_ptr<CopyFence> fence;   // those scans' copy fence (set once enqueued)
+    std::vector<lgs_scan*> fence_scans;
+    ForeignScans foreign;               // scans another context copied (waited for after our copies)
     explicit Upload(lgs_ctx* c) : ctx(c) {}
     Upload(const Upload&) = delete;
     Upload& operator=(const Upload&) = delete;
@@ -519,8 +562,11 @@ struct Upload {
             try {
                 fetch_list(ctx, extra);
             } catch (...) {
+                if (fence) abandon_scan_copies(ctx, fence, fence_scans);
+                fence.reset();
             }
         }
+        if (fence) fence->set(1);
     }
     template <class T>
     size_t append(const T* p, size_t n)
@@ -551,6 +597,10 @@ struct Upload {
         segs.insert(segs.end(), extra.begin(), extra.end());
         extra.clear();
         fetch_list(ctx, segs);
+        if (fence) fence->set(1);
+        fence.reset();
+        fence_scans.clear();
+        if (!foreign.empty()) wait_foreign_scans(foreign);
     }
     void flush()
     {
@@ -590,6 +640,8 @@ void host_parallel_for(int n, int grain, const std::function<void(int)>& f);
 // K3 sort (k_sort.hip): stable LSD radix sort of n 32-bit keys on bits
 // [lo, lo + bits) into `out`; `tmp` (n keys) is used when the sort takes two
 // or more 8-bit passes.  in, tmp and out are distinct device buffers.
-void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, long long n, int lo, int bits);
+// err: device-visible error word, set to 2 if the one-launch sort's grid
+// barrier timed out (null: not reported)
+void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, long long n, int lo, int bits, int* err);
 
 }  // namespace lgs

@@ -51,7 +51,7 @@ def test_host_library_exports_lgs_io_h():
 
 
 def test_abi_version():
-    assert abi.load().lgs_abi_version() == 1
+    assert abi.load().lgs_abi_version() == 2
 
 
 def test_no_device_is_reported_cleanly():

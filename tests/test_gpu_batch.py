@@ -264,3 +264,50 @@ def test_pruning_is_history_independent(ctx, world, small_map, poison):
         ctx.set_option(abi.LGS_OPT_POISON_WS, 0)
         ctx.set_option(abi.LGS_OPT_FORCE_DENSE, 0)
         ctx.set_option(abi.LGS_OPT_SUPER_PRUNE, 1)
+
+
+def test_scans_first_touched_by_two_contexts_at_once(ctx, world, small_map):
+    """Fresh scans (no device copy yet) passed to two contexts' batches at the
+    same moment, in opposite orders: whichever call copies a scan first
+    publishes it, the other waits until that copy is enqueued and done
+    (lgs::CopyFence) -- every record equals the one from scans copied
+    beforehand."""
+    import threading
+    cells, mx, my = small_map
+    rng = np.random.default_rng(33)
+    ang, qs = _queries(world, rng, 8, 541)
+    params = (5, 1.0, 1.0, 0.6, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    other = abi.Context(0)
+    try:
+        grids = [ctx.grid_from_array(cells, mx, my, 0.05), other.grid_from_array(cells, mx, my, 0.05)]
+        inits = [i for _, i in qs]
+        ref = [_record(b) for b in ctx.optimize_pose_query_batch(grids[0], P, cost,
+                                                                 [ctx.scan(r, ang) for r, _ in qs], inits)]
+        for rnd in range(12):
+            fresh = [ctx.scan(r, ang) for r, _ in qs]     # created, not yet copied
+            got, errs = {}, []
+            gate = threading.Barrier(2)
+
+            def run(k):
+                try:
+                    order = list(range(8)) if k == 0 else list(range(7, -1, -1))
+                    gate.wait()
+                    c = (ctx, other)[k]
+                    outs = c.optimize_pose_query_batch(grids[k], P, cost, [fresh[j] for j in order],
+                                                       [inits[j] for j in order])
+                    got[k] = {j: _record(o) for j, o in zip(order, outs)}
+                except Exception as e:   # noqa: BLE001 -- reported below
+                    errs.append((k, repr(e)))
+
+            th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            assert not errs, errs
+            for k in range(2):
+                for j in range(8):
+                    assert got[k][j] == ref[j], (rnd, k, j)
+    finally:
+        other.close()

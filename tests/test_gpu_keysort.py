@@ -60,3 +60,69 @@ def test_keysort_all_equal_digits(ctx):
     assert np.array_equal(ctx.debug_keysort(srt, 0, 22), srt)
     rev = srt[::-1].copy()
     assert np.array_equal(ctx.debug_keysort(rev, 0, 22), expected(rev, 0, 22))
+
+
+def test_keysort_coop_limit_takes_multipass(ctx):
+    """LGS_OPT_COOP_TILES below a sort's tile count: the multi-pass sort runs
+    instead of the one-launch k_sort_wide, same keys."""
+    from lgs_amd import abi
+    rng = np.random.default_rng(5)
+    keys = rng.integers(0, 2 ** 32, 100_000, dtype=np.uint64).astype(np.uint32)   # 13 wide tiles
+    try:
+        for lim in (0, 3, -1):
+            ctx.set_option(abi.LGS_OPT_COOP_TILES, lim)
+            assert np.array_equal(ctx.debug_keysort(keys, 1, 20), expected(keys, 1, 20)), lim
+    finally:
+        ctx.set_option(abi.LGS_OPT_COOP_TILES, -1)
+
+
+def test_keysort_barrier_timeout_fails_loudly(ctx):
+    """A grid-barrier wait past LGS_OPT_SORT_BARRIER_US (0 here) ends every
+    tile and reports LGS_ERR_INTERNAL instead of spinning; the barrier words
+    are reset, so the next sort is right."""
+    from lgs_amd import abi
+    rng = np.random.default_rng(6)
+    keys = rng.integers(0, 2 ** 32, 100_000, dtype=np.uint64).astype(np.uint32)
+    try:
+        ctx.set_option(abi.LGS_OPT_SORT_BARRIER_US, 0)
+        with pytest.raises(abi.LgsError, match="grid barrier timed out"):
+            ctx.debug_keysort(keys, 1, 20)
+    finally:
+        ctx.set_option(abi.LGS_OPT_SORT_BARRIER_US, 50000)
+    for _ in range(2):
+        assert np.array_equal(ctx.debug_keysort(keys, 1, 20), expected(keys, 1, 20))
+
+
+def test_keysort_concurrent_contexts(ctx):
+    """Four contexts sorting at once from four host threads, each sort close to
+    the device's co-residency capacity: together they exceed it, so the
+    process-wide reservation sends some to the multi-pass sort -- every result
+    right, no barrier time-out."""
+    import threading
+
+    from lgs_amd import abi
+    ctxs = [abi.Context(0) for _ in range(4)]
+    rng = np.random.default_rng(8)
+    inputs = [rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+              for n in (900_000, 700_000, 1_000_000, 800_000)]
+    errs = []
+
+    def run(i):
+        try:
+            for k in range(6):
+                got = ctxs[i].debug_keysort(inputs[i], 1, 20)
+                if not np.array_equal(got, expected(inputs[i], 1, 20)):
+                    errs.append((i, k, "mismatch"))
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errs.append((i, repr(e)))
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+    try:
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    finally:
+        for c in ctxs:
+            c.close()
+    assert not errs, errs

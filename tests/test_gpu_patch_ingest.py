@@ -100,3 +100,25 @@ def test_match_on_patch_ingest_equals_dense(ctx, world):
         assert (a.estimated_pose.x, a.estimated_pose.y, a.estimated_pose.theta) == \
             (b.estimated_pose.x, b.estimated_pose.y, b.estimated_pose.theta)
         assert a.normalized_cost == b.normalized_cost and list(a.covariance) == list(b.covariance)
+
+
+def test_patch_ingest_taller_than_grid_y_limit(ctx):
+    """65,600 rows (> the 65,535 grid-y limit): rows are grid-strided."""
+    rng = np.random.default_rng(12)
+    ps, npx, npy = 8, 1, 8200
+    cells = np.where(rng.random((npy * ps, npx * ps)) < 0.5, rng.random((npy * ps, npx * ps)), 0.0)
+    patches, npx, npy = to_patches(cells, ps, rng)
+    g = ctx.grid_from_patches(patches, npx, npy, ps, 0.0, 0.0, 0.05)
+    assert np.array_equal(g.download().view(np.uint64), reference_value_grid(patches, npx, npy, ps).view(np.uint64))
+
+
+def test_upload_into_map_view_rejected(ctx):
+    """A map's grid view changes only through the map (its counters and patch
+    flags): dense and patch uploads into it are refused."""
+    m = ctx.map(0.05, 10, 20, 20)
+    view = m.grid()
+    with pytest.raises(abi.LgsError, match="map's grid view"):
+        view.upload(np.zeros((view.hgt, view.w)))
+    with pytest.raises(abi.LgsError, match="map's grid view"):
+        ctx.grid_from_patches([None] * ((view.w // 10) * (view.hgt // 10)), view.w // 10, view.hgt // 10, 10,
+                              view.min_x, view.min_y, 0.05, into=view)
