@@ -95,6 +95,9 @@ def parse():
     ap.add_argument("--loop-line", type=int, default=1,
                     help="match workload: also run config 5 (512 loop candidates sharded over the ranks, strong "
                          "scaling) after the timed region and report it as 'config5_strong_scaling'")
+    ap.add_argument("--sub-lines", type=int, default=1,
+                    help="match workload: also report configs 4 (config4_stream), 3 (config3_refine) and f2 "
+                         "(f2_rebuild) after the timed region, each with its own CPU baseline and kernel times")
     ap.add_argument("--timed-events", default="dominant", choices=["dominant", "all", "none"],
                     help="HIP-event timing inside the timed region: the roofline kernel only (default), "
                          "every kernel, or none (A/B of the event overhead)")
@@ -287,13 +290,14 @@ class FbIn(C.Structure):
                 ("range_x", C.c_double), ("range_y", C.c_double), ("range_theta", C.c_double),
                 ("scan_range_max", C.c_double), ("segs", C.POINTER(C.c_double)), ("angles", C.POINTER(C.c_double)),
                 ("truths", C.POINTER(C.c_double)), ("odo", C.POINTER(C.c_double)), ("n_dump", C.c_int),
-                ("opt_id", C.c_int), ("opt_value", C.c_double)]
+                ("opt_id", C.c_int), ("opt_value", C.c_double), ("profile_warmup", C.c_int)]
 
 
 class FbOut(C.Structure):
     _fields_ = [("est", C.POINTER(C.c_double)), ("guess", C.POINTER(C.c_double)),
                 ("dump_ranges", C.POINTER(C.c_double)), ("total_s", C.c_double), ("phase_s", C.c_double * 4),
-                ("steps_timed", C.c_int), ("not_found", C.c_int)]
+                ("steps_timed", C.c_int), ("not_found", C.c_int), ("kstats", C.POINTER(abi.KernelStat)),
+                ("kstats_cap", C.c_int), ("kstats_n", C.c_int)]
 
 
 class DropinIn(C.Structure):
@@ -865,8 +869,9 @@ def run_stream_cpp(args, D, ctx):
     dump = np.zeros((n_dump, len(ang)))
     fin = FbIn(D.local, n, args.warmup, len(ang), len(segs), int(args.interp), 10, int(args.fused), 5, *win, 20.0,
                dptr(segs), dptr(ang),
-               dptr(truths), dptr(odo), n_dump, *(args.ctx_option or (0, 0.0)))
-    fout = FbOut(dptr(est), dptr(guess), dptr(dump))
+               dptr(truths), dptr(odo), n_dump, *(args.ctx_option or (0, 0.0)), 1)
+    kst = (abi.KernelStat * len(abi.KERNEL_IDS))()
+    fout = FbOut(dptr(est), dptr(guess), dptr(dump), kstats=kst, kstats_cap=len(abi.KERNEL_IDS))
     D.barrier()
     rc = bench_drivers().lgs_frontend_bench(C.byref(fin), C.byref(fout))
     if rc != 0:
@@ -874,10 +879,16 @@ def run_stream_cpp(args, D, ctx):
     steps = fout.steps_timed
     elapsed = D.max(fout.total_s)
     value = steps * D.world / elapsed
+    # per-kernel HIP-event times of the (untimed) warmup steps, per step
+    wsteps = max(1, args.warmup)
+    stats = {kst[i].name.decode(): dict(launches=kst[i].launches, total_ms=kst[i].total_ms,
+                                        algo_bytes=kst[i].algo_bytes)
+             for i in range(fout.kstats_n) if kst[i].launches}
+    kernel_ms_per_step = {k: round(v["total_ms"] / wsteps, 5) for k, v in stats.items()}
     names = ("scan_upload", "interpolate", "match", "append_scan")
     breakdown = {f"{nm}_ms": round(1e3 * fout.phase_s[i] / steps, 4) for i, nm in enumerate(names)}
     drift = float(np.max(np.abs(est[-1, :2] - truths[-1, :2])))
-    cpu = None
+    cpu = replay = None
     if D.rank == 0 and not args.no_cpu and D.world == 1:
         ob = oracle_lib()
         obp = ob.BuilderParams(*BUILDER)
@@ -894,7 +905,8 @@ def run_stream_cpp(args, D, ctx):
         olocal.integrate(oest[0], oscans[0], obp)
         times = []
         t_start = time.perf_counter()
-        for j in range(1, n_dump):
+        o_steps = min(n_dump, 1 + getattr(args, "oracle_steps", n_dump))
+        for j in range(1, o_steps):
             t1 = time.perf_counter()
             oscans.append(oscan(j))
             lo = max(0, j - 10)
@@ -911,6 +923,7 @@ def run_stream_cpp(args, D, ctx):
             if time.perf_counter() - t_start > args.cpu_seconds and len(times) >= 3:
                 break
         same = all(tuple(est[j]) == oest[j] for j in range(len(oest)))
+        replay = dict(steps=len(times), poses_identical=bool(same))
         cpu = dict(value=round(len(times) / sum(times), 3), unit="scans/s", cores=1, kind="port",
                    sample=f"the first {len(times)} frontend steps through the oracle (interpolate, 10-scan "
                           f"ConstructMapFromScans, OptimizePose(query) from the C++ run's guesses, insert; "
@@ -926,8 +939,10 @@ def run_stream_cpp(args, D, ctx):
                     append_scan="fused (lgs_map_append_scan)" if args.fused else "UpdateScan + ConstructMapFromScans",
                     parallelism=f"replicas x{D.world}"),
         final_drift_m=round(drift, 4), not_found=fout.not_found, breakdown_per_step=breakdown,
+        oracle_replay=replay, kernel_ms_per_step=kernel_ms_per_step,
+        kernel_ms_per_step_note=f"HIP-event times of the {wsteps} untimed warmup steps (every kernel timed), per step",
         roofline=None, cpu_baseline=cpu)
-    return line, {}, value
+    return line, stats, value
 
 
 # ------------------------------------------------------------------- rebuild
@@ -993,6 +1008,28 @@ def run_rebuild(args, D, ctx):
     return line, stats, value
 
 
+SUB_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "scaling", "dtype", "config",
+            "cpu_baseline", "roofline", "p50_refine_ms", "batched_refines_per_s_per_gpu", "kernel_avg_ms",
+            "final_drift_m", "not_found", "breakdown_per_step", "oracle_replay", "kernel_ms_per_step",
+            "kernel_ms_per_step_note", "global_map")
+
+
+def sub_line(args, D, ctx, workload, steps, warmup, cpu_seconds, **extra):
+    """Another workload's line inside the default run (its own steps, warmup
+    and bounded CPU baseline), with its per-kernel event times."""
+    sa = argparse.Namespace(**vars(args))
+    sa.workload, sa.steps, sa.warmup, sa.cpu_seconds = workload, steps, warmup, cpu_seconds
+    for k, v in extra.items():
+        setattr(sa, k, v)
+    fn = dict(refine=run_refine, stream=run_stream_cpp, rebuild=run_rebuild)[workload]
+    ln, stats, _ = fn(sa, D, ctx)
+    sub = {k: ln[k] for k in SUB_KEYS if k in ln}
+    if workload != "stream":
+        sub["kernels"] = {k: dict(launches=v["launches"], avg_ms=round(v["total_ms"] / max(1, v["launches"]), 5))
+                          for k, v in stats.items() if v["launches"]}
+    return sub
+
+
 def spawn_ranks(args) -> None:
     """--gpus N without a launcher: start N ranks (one process per GPU) with
     torch.distributed.run as a CHILD process, before anything here touches the
@@ -1031,6 +1068,13 @@ def main():
                                                               "roofline_super")}
     if args.workload == "match" and args.dropin_line:
         line["dropin"] = dropin_line(args, D)
+    if args.workload == "match" and args.sub_lines:
+        # configs 4 and 3 and f2 next to the headline, on the same run
+        # (replicas over the ranks; CPU baselines on rank 0 at N = 1)
+        line["config4_stream"] = sub_line(args, D, ctx, "stream", 2000, 100, 8.0, oracle_steps=200, window="json",
+                                          interp=1, fused=1, driver="cpp", ctx_option=None)
+        line["config3_refine"] = sub_line(args, D, ctx, "refine", 100, 5, 3.0)
+        line["f2_rebuild"] = sub_line(args, D, ctx, "rebuild", 10, 2, 3.0)
     if D.rank == 0:
         print(json.dumps(line), flush=True)
     D.close()

@@ -50,6 +50,7 @@ struct lgs_fb_in {
     int n_dump;             // first scans whose raw ranges are returned
     int opt_id;             // A/B: one lgs_ctx option set on the device context (0: none)
     double opt_value;
+    int profile_warmup;     // 1: every kernel HIP-event-timed during the (untimed) warmup steps
 };
 
 struct lgs_fb_out {
@@ -60,6 +61,9 @@ struct lgs_fb_out {
     double phase_s[4];      // upload, interpolate, match, AppendScan (insert + latest map)
     int steps_timed;
     int not_found;          // matches with mPoseFound == false
+    lgs_kernel_stat* kstats;   // [kstats_cap]: per-kernel times of the profiled warmup steps
+    int kstats_cap;
+    int kstats_n;
 };
 
 struct lgs_dropin_in {
@@ -222,9 +226,22 @@ extern "C" int lgs_frontend_bench(const lgs_fb_in* in, lgs_fb_out* out)
         }
         double ph[4] = { 0, 0, 0, 0 };
         out->not_found = 0;
+        out->kstats_n = 0;
+        const bool prof = in->profile_warmup && in->warmup > 0 && out->kstats && out->kstats_cap > 0;
         for (int k = 0; k < n; ++k) {
+            if (prof && k == 1) {
+                dev->Synchronize();
+                dev->Check(lgs_ctx_set_option(dev->Handle(), LGS_OPT_PROFILE, 1.0), "lgs_ctx_set_option");
+                dev->Check(lgs_ctx_reset_stats(dev->Handle()), "lgs_ctx_reset_stats");
+            }
             if (k == in->warmup + 1) {   // timed steps from here
                 dev->Synchronize();
+                if (prof) {
+                    const int m = lgs_ctx_kernel_stats(dev->Handle(), out->kstats, out->kstats_cap);
+                    if (m < 0) dev->Check(-m, "lgs_ctx_kernel_stats");
+                    out->kstats_n = m;
+                    dev->Check(lgs_ctx_set_option(dev->Handle(), LGS_OPT_PROFILE, 0.0), "lgs_ctx_set_option");
+                }
                 for (double& p : ph) p = 0.0;
                 out->not_found = 0;
             }
