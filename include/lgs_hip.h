@@ -492,6 +492,27 @@ int  lgs_loop_detect_rtcsm_multi(lgs_ctx* const* ctxs, int num_ctx, const lgs_rt
                                  const lgs_loop_candidate* candidates, int num_candidates,
                                  lgs_loop_result* results);
 
+/* ---- the loop batch over several processes (one per GPU) ----
+ * Candidates are independent (C/mapping/loop_detector_real_time_correlative.cpp:38, :66):
+ * rank r of `world` matches the contiguous block [lo_r, hi_r) of the n
+ * candidates (lgs_loop_shard_bounds: block sizes differ by at most one, the
+ * larger blocks first) with lgs_loop_detect_rtcsm, then
+ * lgs_loop_records_allgather gathers every rank's records into `all` (host,
+ * n records, candidate order -- the order the reference's
+ * LoopDetectionResultVector keeps) with ONE ncclAllGather of fixed-size rows
+ * on ctx's stream (RCCL over xGMI), and synchronises the stream.  `comm` is an
+ * ncclComm_t of `world` ranks whose rank `rank` lives on ctx's device (made
+ * by the caller, or with lgs_rccl_comm_init).  RCCL is resolved at run time
+ * (librccl.so.1, an already loaded copy first). */
+int  lgs_loop_shard_bounds(int n, int world, int rank, int* lo, int* hi);
+int  lgs_loop_records_allgather(lgs_ctx* ctx, void* comm, int rank, int world, int n,
+                                const lgs_loop_result* local, lgs_loop_result* all);
+/* RCCL communicator helpers: a 128-byte ncclUniqueId made on one rank and
+ * sent to the others by the caller, then one lgs_rccl_comm_init per rank. */
+int  lgs_rccl_unique_id(unsigned char* id128);
+int  lgs_rccl_comm_init(lgs_ctx* ctx, const unsigned char* id128, int world, int rank, void** comm);
+int  lgs_rccl_comm_destroy(void* comm);
+
 /* ---- branch-and-bound matcher ----
  * ScanMatcherBranchBound (C/mapping/scan_matcher_branch_bound.cpp:8-200,
  * H/mapping/scan_matcher_branch_bound.hpp) with ScorePixelAccurate

@@ -82,6 +82,7 @@ enum Slot {
     S_BB0, S_BB1, S_BB2, S_BB3, S_BB4, S_BB5,   // branch-and-bound (k_bb.hip)
     S_PRECOMP_TMP,  // double [W*H]: pass-1 result of the large-window precompute
     S_KEEP,         // int: kept-superblock work list of a batch (k_keep / k_coarse_list)
+    S_COLL,         // lgs_loop_records_allgather: send block + gathered rows (lgs_coll.hip)
     // bank 1 of the per-batch buffers: a batched call keeps two 64-query
     // chunks in flight (the next chunk's launches go out before the host
     // finishes the previous one), each in its own bank (lgs_ctx::banked)

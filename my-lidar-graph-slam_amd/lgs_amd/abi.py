@@ -242,6 +242,12 @@ _PROTOS = [
     ("lgs_loop_detect_rtcsm_multi", C.c_int, [C.POINTER(_P), C.c_int, C.POINTER(RtcsmParams),
                                               C.POINTER(CostGEParams), C.c_double, C.POINTER(LoopQuery), C.c_int,
                                               C.POINTER(LoopCandidate), C.c_int, C.POINTER(LoopResult)]),
+    ("lgs_loop_shard_bounds", C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("lgs_loop_records_allgather", C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.POINTER(LoopResult),
+                                             C.POINTER(LoopResult)]),
+    ("lgs_rccl_unique_id", C.c_int, [C.POINTER(C.c_ubyte)]),
+    ("lgs_rccl_comm_init", C.c_int, [_P, C.POINTER(C.c_ubyte), C.c_int, C.c_int, C.POINTER(_P)]),
+    ("lgs_rccl_comm_destroy", C.c_int, [_P]),
     ("lgs_linsolve_optimize_pose", C.c_int, [_P, _P, C.POINTER(LinsolveParams), _P, Pose2D,
                                              C.POINTER(LinsolveSummary), C.POINTER(C.c_double)]),
     ("lgs_linsolve_optimize_pose_batch", C.c_int, [_P, _P, C.POINTER(LinsolveParams), C.POINTER(_P),
@@ -474,6 +480,32 @@ class Context:
             return out
         self.check(self.lib.lgs_loop_detect_rtcsm(self.h, C.byref(params), C.byref(cost), float(thr), qs,
                                                   len(queries), cs, len(candidates), out), "loop_detect_rtcsm")
+        return out
+
+    # ---- the loop batch over several processes (RCCL) ----
+    def rccl_comm(self, world: int = 1, rank: int = 0, unique_id: Optional[bytes] = None):
+        """An ncclComm_t of `world` ranks on this context's device (lgs_rccl_comm_init);
+        unique_id: the 128 bytes of lgs_rccl_unique_id, made on one rank (new if None)."""
+        if unique_id is None:
+            buf = (C.c_ubyte * 128)()
+            self.check(self.lib.lgs_rccl_unique_id(buf), "rccl_unique_id")
+        else:
+            buf = (C.c_ubyte * 128).from_buffer_copy(unique_id)
+        comm = _P()
+        self.check(self.lib.lgs_rccl_comm_init(self.h, buf, world, rank, C.byref(comm)), "rccl_comm_init")
+        return comm
+
+    def rccl_comm_destroy(self, comm):
+        self.check(self.lib.lgs_rccl_comm_destroy(comm), "rccl_comm_destroy")
+
+    def loop_records_allgather(self, comm, rank: int, world: int, n: int, local):
+        """lgs_loop_records_allgather: this rank's block of LoopResult records ->
+        all n records in candidate order."""
+        cnt = len(local)
+        loc = (LoopResult * max(1, cnt))(*local) if cnt else (LoopResult * 1)()
+        out = (LoopResult * max(1, n))()
+        self.check(self.lib.lgs_loop_records_allgather(self.h, comm, rank, world, n, loc, out),
+                   "loop_records_allgather")
         return out
 
     # ---- branch-and-bound matcher (SURVEY f1) ----

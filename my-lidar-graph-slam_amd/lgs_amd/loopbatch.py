@@ -139,14 +139,21 @@ def run_sharded(cands: Sequence[Candidate], detect_fn, rank: int = 0, world: int
     rows = shard_bounds(n, world, 0)[1]        # largest block
     buf = torch.zeros((rows, RECORD_BYTES), dtype=torch.uint8)
     buf[: hi - lo] = torch.from_numpy(local.copy())
-    if device is not None:
-        buf = buf.to(device)
-    gathered = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(gathered, buf)
+    if device is not None and str(device).startswith("cuda"):
+        # RCCL: one all-gather into one device tensor, one copy back
+        out = torch.empty((world * rows, RECORD_BYTES), dtype=torch.uint8, device=device)
+        dist.all_gather_into_tensor(out, buf.to(device))
+        allrows = out.cpu().numpy().reshape(world, rows, RECORD_BYTES)
+    else:
+        if device is not None:
+            buf = buf.to(device)
+        gathered = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(gathered, buf)
+        allrows = np.stack([g.cpu().numpy() for g in gathered])
     parts = []
     for r in range(world):
         a, b = shard_bounds(n, world, r)
-        parts.append(gathered[r][: b - a].cpu().numpy())
+        parts.append(allrows[r, : b - a])
     return np.concatenate(parts, axis=0)
 
 

@@ -171,3 +171,23 @@ def test_loop_detect_config5_shape(ctx, world):
     found = loopbatch.loop_results(dev)
     assert 0 < len(found) <= len(cands)
     assert cnt["pruned"] == len(cands) and cnt["coarse_blocks"] < cnt["coarse_blocks_dense"], cnt
+
+
+def test_loop_records_allgather_world1(ctx):
+    """lgs_loop_records_allgather over an RCCL communicator of one rank: the
+    records of a real loop batch come back byte for byte (the multi-process
+    path's collective; N > 1 runs on the driver's nodes)."""
+    import ctypes as C
+
+    maps, cands = small.make_problem()
+    p, c = abi.RtcsmParams(*small.PARAMS), abi.CostGEParams(*small.COST)
+    rec = loopbatch.run_sharded(cands, loopbatch.hip_detect_fn(ctx, maps, cands, p, c, small.THR))
+    n = len(cands)
+    local = (abi.LoopResult * n).from_buffer_copy(rec.tobytes())
+    comm = ctx.rccl_comm(1, 0)
+    try:
+        out = ctx.loop_records_allgather(comm, 0, 1, n, list(local))
+        assert bytes(out) == rec.tobytes()
+        assert bytes(ctx.loop_records_allgather(comm, 0, 1, 0, [])) == bytes(C.sizeof(abi.LoopResult))
+    finally:
+        ctx.rccl_comm_destroy(comm)

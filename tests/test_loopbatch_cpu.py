@@ -40,6 +40,21 @@ def test_shard_bounds_cover_in_order():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_c_abi_shard_bounds_equal_python():
+    """lgs_loop_shard_bounds (the C-ABI's sharding, lgs_coll.hip) == loopbatch.shard_bounds."""
+    import ctypes as C
+
+    from lgs_amd import abi
+    lib = abi.load()
+    lo, hi = C.c_int(), C.c_int()
+    for n in (0, 1, 7, 64, 511, 512, 513):
+        for w in (1, 2, 3, 4, 7, 8):
+            for r in range(w):
+                assert lib.lgs_loop_shard_bounds(n, w, r, C.byref(lo), C.byref(hi)) == 0
+                assert (lo.value, hi.value) == loopbatch.shard_bounds(n, w, r), (n, w, r)
+    assert lib.lgs_loop_shard_bounds(5, 2, 2, C.byref(lo), C.byref(hi)) == 1   # LGS_ERR_INVALID_ARG
+
+
 def test_sub_queries_rebase():
     C = loopbatch.Candidate
     cands = [C(q, None, None, (0, 0, 0), i) for i, q in enumerate([0, 0, 1, 1, 1, 2])]
