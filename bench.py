@@ -95,6 +95,9 @@ def parse():
     ap.add_argument("--loop-line", type=int, default=1,
                     help="match workload: also run config 5 (512 loop candidates sharded over the ranks, strong "
                          "scaling) after the timed region and report it as 'config5_strong_scaling'")
+    ap.add_argument("--distinct-maps", type=int, default=0,
+                    help="match workload: 1 = every query of a call against its own copy of the map (distinct "
+                         "device buffers: the per-query coarse-map precompute is not served from the cache)")
     ap.add_argument("--sub-lines", type=int, default=1,
                     help="match workload: also report configs 4 (config4_stream), 3 (config3_refine) and f2 "
                          "(f2_rebuild) after the timed region, each with its own CPU baseline and kernel times")
@@ -102,7 +105,7 @@ def parse():
                     help="HIP-event timing inside the timed region: the roofline kernel only (default), "
                          "every kernel, or none (A/B of the event overhead)")
     a = ap.parse_args()
-    d_steps = dict(match=200, refine=200, loop=4, loop_bb=2, stream=10000 if a.driver == "cpp" else 500,
+    d_steps = dict(match=200, refine=200, loop=12, loop_bb=12, stream=10000 if a.driver == "cpp" else 500,
                    rebuild=20)[a.workload]
     d_warm = dict(match=10, refine=5, loop=1, loop_bb=1, stream=10, rebuild=2)[a.workload]
     a.steps = d_steps if a.steps is None else a.steps
@@ -428,21 +431,26 @@ def run_match(args, D, ctx):
     S = max(1, args.streams)
     ctxs = [ctx] + [abi.Context(D.local) for _ in range(S - 1)]
     state = []
+    B = max(1, args.batch)
+    # --distinct-maps: every query of a call matches against its own copy of
+    # the map (distinct device buffers), so no query's coarse-map precompute
+    # reads a map another query of the batch already brought into L2/MALL
+    nmaps = B if args.distinct_maps else 1
     for c in ctxs:
         c.set_option(abi.LGS_OPT_SUPER_PRUNE, args.super_prune)
         c.set_option(abi.LGS_OPT_SPIN_SYNC, args.spin_sync)
         if args.lanes_min_batch is not None:
             c.set_option(abi.LGS_OPT_LANES_MIN_BATCH, args.lanes_min_batch)
-        state.append((c, c.grid_from_array(cells, mx, my, 0.05), [c.scan(r, ang) for r in scans]))
+        gs = [c.grid_from_array(cells, mx, my, 0.05) for _ in range(nmaps)]
+        state.append((c, gs if args.distinct_maps else gs[0], [c.scan(r, ang) for r in scans]))
     P, cost = abi.RtcsmParams(*PARAMS), abi.CostGEParams(*COST)
     n = len(scans)
-    B = max(1, args.batch)
 
     def call(c, g, ds, k):
         """step k: scans k*B .. k*B + B - 1 (cyclic over the generated scans)"""
         if B == 1:
             j = k % n
-            return [c.optimize_pose_query(g, P, cost, ds[j], inits[j])], [j]
+            return [c.optimize_pose_query(g[0] if isinstance(g, list) else g, P, cost, ds[j], inits[j])], [j]
         js = [(k * B + i) % n for i in range(B)]
         return c.optimize_pose_query_batch(g, P, cost, [ds[j] for j in js], [inits[j] for j in js]), js
 
@@ -492,7 +500,7 @@ def run_match(args, D, ctx):
     for k in range(args.latency_calls):
         j = (args.warmup + k) % n
         ts = time.perf_counter()
-        c0.optimize_pose_query(g0, P, cost, ds0[j], inits[j])
+        c0.optimize_pose_query(g0[0] if isinstance(g0, list) else g0, P, cost, ds0[j], inits[j])
         lat1.append(time.perf_counter() - ts)
     c0.set_option(abi.LGS_OPT_PROFILE, 1)
     c0.reset_stats()
@@ -536,7 +544,7 @@ def run_match(args, D, ctx):
                              "vs 1000x1000@5cm grid, PatchSize 100",
                     beams=1081, grid=[1000, 1000], resolution=0.05, low_resolution=5,
                     search_range=[4.0, 4.0, 1.0471976], scans_per_rank=args.steps * B, batch=B,
-                    streams_per_gpu=S,
+                    streams_per_gpu=S, distinct_map_buffers=bool(args.distinct_maps),
                     parallelism=f"replicas x{D.world} (independent scans per rank), {S} concurrent HIP streams "
                                 f"per GPU, each issuing calls of {B} OptimizePose(query) matches "
                                 f"(one launch per stage per 64-query chunk) + RCCL all-gather of poses"),
@@ -655,8 +663,11 @@ def run_loop(args, D, ctx):
     set_timed_events(ctx, args, dominant, extra=() if bb else ("k_super",))
     D.barrier()
     t0 = time.perf_counter()
+    step_s = []
     for _ in range(args.steps):
+        ts = time.perf_counter()
         rec = loopbatch.run_sharded(cands, fn, D.rank, D.world, D.d, D.device())
+        step_s.append(time.perf_counter() - ts)
     elapsed = D.max(time.perf_counter() - t0)
     stats = ctx.kernel_stats()
     ctx.set_option(abi.LGS_OPT_PROFILE, 0)
@@ -716,9 +727,11 @@ def run_loop(args, D, ctx):
                                workload="loop_bb" if bb else "loop"),
         # config 5's largest kernel by time is the 9-row superblock-bound pass,
         # not the coarse sums: its own roofline (2 B per angle x superblock x beam)
-        roofline_super=None if bb else roofline_from(stats, "k_super", args.pmc, "k_super_oct<9>", "l2-gather",
+        roofline_super=None if bb else roofline_from(stats, "k_super", args.pmc, "k_super_oct<9, 3>", "l2-gather",
                                                      workload="loop", bytes_scale=0.25),
         coarse_stage=None if bb else coarse_stage(stats),
+        step_ms_p10_p50_p90=[round(1e3 * float(np.percentile(step_s, q)), 4) for q in (10, 50, 90)],
+        step_spread=round(float((np.percentile(step_s, 90) - np.percentile(step_s, 10)) / np.median(step_s)), 4),
         cpu_baseline=cpu)
     return line, stats, value
 
@@ -1061,13 +1074,23 @@ def main():
         # config 5 next to the config-2 replicas line: the 512 loop candidates
         # split over the ranks (strong scaling), measured after the main timed region
         la = argparse.Namespace(**vars(args))
-        la.workload, la.steps, la.warmup, la.no_cpu = "loop", 4, 1, True
+        la.workload, la.steps, la.warmup, la.no_cpu = "loop", 12, 2, True
         ll, _, _ = run_loop(la, D, ctx)
         line["config5_strong_scaling"] = {k: ll[k] for k in ("metric", "value", "unit", "n_gpus", "steps",
                                                               "ms_per_step", "scaling", "config", "roofline",
-                                                              "roofline_super")}
+                                                              "roofline_super", "step_ms_p10_p50_p90", "step_spread")}
     if args.workload == "match" and args.dropin_line:
         line["dropin"] = dropin_line(args, D)
+    if args.workload == "match" and args.sub_lines and not args.distinct_maps:
+        # config 2 with a distinct map buffer per query
+        da = argparse.Namespace(**vars(args))
+        da.distinct_maps, da.steps, da.warmup, da.no_cpu, da.latency_calls = 1, 30, 3, True, 0
+        dl, dstats, _ = run_match(da, D, ctx)
+        line["config2_distinct_maps"] = {k: dl[k] for k in ("value", "unit", "steps", "ms_per_step", "config",
+                                                             "roofline")}
+        line["config2_distinct_maps"]["kernels"] = {
+            k: dict(launches=v["launches"], avg_ms=round(v["total_ms"] / max(1, v["launches"]), 5))
+            for k, v in dstats.items() if v["launches"]}
     if args.workload == "match" and args.sub_lines:
         # configs 4 and 3 and f2 next to the headline, on the same run
         # (replicas over the ranks; CPU baselines on rank 0 at N = 1)

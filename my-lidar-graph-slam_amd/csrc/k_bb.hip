@@ -126,8 +126,8 @@ __global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ ite
 #pragma unroll
         for (int j = 0; j < kBBPipe; ++j) {   // independent loads first
             const int v = min(v0 + j, Nv - 1);
-            cx[j] = rc[v];
-            cy[j] = rs[v];
+            cx[j] = gload(rc + v);
+            cy[j] = gload(rs + v);
         }
 #pragma unroll
         for (int j = 0; j < kBBPipe; ++j) {
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ ite
             // GridMap::Value(idx, unknown): 0.0 outside; unknown cells (0.0)
             // are skipped by the reference (:55-56), adding 0.0 is the same
             const bool inb = (v < Nv) & ((unsigned)ix < (unsigned)W) & ((unsigned)iy < (unsigned)H);
-            val[j] = inb ? map[(size_t)iy * W + ix] : 0.0;
+            val[j] = inb ? gload(map + ((size_t)iy * W + ix)) : 0.0;
         }
 #pragma unroll
         for (int j = 0; j < kBBPipe; ++j) sum += val[j];
@@ -265,6 +265,53 @@ inline uint64_t node_key(int h, int x, int y, int t)
     return ((uint64_t)(unsigned)h << 60) | ((uint64_t)((unsigned)(x + (1 << 19)) & 0xFFFFFu) << 40) |
            ((uint64_t)((unsigned)(y + (1 << 19)) & 0xFFFFFu) << 20) | (uint64_t)((unsigned)(t + (1 << 19)) & 0xFFFFFu);
 }
+
+// Node -> score table of one candidate for the host replay: open addressing
+// (linear probing) over a power-of-two array, reused by the worker thread
+// across candidates and calls (an std::unordered_map per candidate allocated
+// one node per entry: the replay's cost swung with the host's allocator load).
+struct NodeTable {
+    std::vector<uint64_t> keys;   // key + 1 (0 = empty)
+    std::vector<double> vals;
+    uint64_t mask = 0;
+    void reset(size_t n)
+    {
+        size_t cap = 16;
+        while (cap < 2 * n + 16) cap <<= 1;
+        if (keys.size() < cap) {
+            keys.assign(cap, 0);
+            vals.resize(cap);
+        } else {
+            cap = keys.size();
+            std::fill(keys.begin(), keys.end(), 0);
+        }
+        mask = cap - 1;
+    }
+    static uint64_t mix(uint64_t k)
+    {
+        k ^= k >> 31;
+        k *= 0x9E3779B97F4A7C15ull;
+        return k ^ (k >> 29);
+    }
+    void put(uint64_t key, double v)
+    {
+        for (uint64_t i = mix(key) & mask;; i = (i + 1) & mask)
+            if (keys[i] == 0 || keys[i] == key + 1) {   // first entry wins (as emplace)
+                if (keys[i] == 0) {
+                    keys[i] = key + 1;
+                    vals[i] = v;
+                }
+                return;
+            }
+    }
+    const double* find(uint64_t key) const
+    {
+        for (uint64_t i = mix(key) & mask;; i = (i + 1) & mask) {
+            if (keys[i] == key + 1) return &vals[i];
+            if (keys[i] == 0) return nullptr;
+        }
+    }
+};
 
 BBHost make_bb_plan(const lgs_grid* grid, const lgs_bb_params* p, const lgs_scan* scan, lgs_pose2d init,
                     double nthr)
@@ -590,13 +637,13 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
     std::vector<char> failed((size_t)n, 0);
     struct SNode { int x, y, t, h; };
     auto replay = [&](int j) {
-        std::unordered_map<uint64_t, double> tab;
-        tab.reserve(bucket[(size_t)j].size() * 2 + 16);
+        static thread_local NodeTable tab;
+        static thread_local std::vector<SNode> st;
+        tab.reset(bucket[(size_t)j].size());
         for (const auto& li : bucket[(size_t)j]) {
             const int4 nd = levels[(size_t)li.first].nodes[(size_t)li.second];
-            tab.emplace(node_key(nd.x & 15, nd.y, nd.z, nd.w), levels[(size_t)li.first].scores[(size_t)li.second]);
+            tab.put(node_key(nd.x & 15, nd.y, nd.z, nd.w), levels[(size_t)li.first].scores[(size_t)li.second]);
         }
-        std::vector<SNode> st;
         const BBHost& b = plans[j];
         double scoreMax = b.thr0;
         lgs_pose2d bestPose = b.sensor;
@@ -609,12 +656,12 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         while (!st.empty()) {
             const SNode cur = st.back();
             st.pop_back();
-            const auto f = tab.find(node_key(cur.h, cur.x, cur.y, cur.t));
-            if (f == tab.end()) {
+            const double* f = tab.find(node_key(cur.h, cur.x, cur.y, cur.t));
+            if (!f) {
                 failed[(size_t)j] = no_path ? 2 : 1;   // 1: rerun with the thr0 superset
                 break;
             }
-            const double score = f->second;
+            const double score = *f;
             ++visited;
             if (score <= scoreMax) continue;   // :105-109
             if (cur.h == 0) {                  // :112-119
@@ -655,16 +702,7 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         o.fine_blocks = visited;
         best[j] = bestPose;
     };
-    {
-        const int nt = std::max(1, std::min(n, std::min(16, (int)std::thread::hardware_concurrency())));
-        std::vector<std::thread> th;
-        for (int w = 1; w < nt; ++w)
-            th.emplace_back([&, w] {
-                for (int j = w; j < n; j += nt) replay(j);
-            });
-        for (int j = 0; j < n; j += nt) replay(j);
-        for (auto& t : th) t.join();
-    }
+    host_parallel_for(n, 1, replay);   // the persistent host pool (no thread creation per call)
     for (int j = 0; j < n; ++j)
         LGS_REQUIRE(failed[(size_t)j] != 2, "branch-and-bound: the search reached a node the device did not score");
     lap(2);

@@ -540,8 +540,8 @@ __device__ double walk_run_wave(long long i, double v, uint32_t& nh, uint32_t& n
         if (w0 < 0 || w - w0 >= 64) {
             w0 = w;
             const long long wl = w0 + lane;
-            hwl = (wl < rb.nw) ? rb.hitw[wl] : 0ull;
-            ewl = (wl < rb.nw) ? rb.endw[wl] : ~0ull;
+            hwl = (wl < rb.nw) ? gload(rb.hitw + wl) : 0ull;
+            ewl = (wl < rb.nw) ? gload(rb.endw + wl) : ~0ull;
         }
         const int sh = (int)(p & 63);
         const bool id_miss = K.miss_fixed && v == kPMin, id_hit = K.hit_fixed && v == kPMax;
@@ -581,7 +581,7 @@ __device__ void recompute_cell(const WindowJob& J, unsigned cell, const BayesCha
     const unsigned long long* e = J.tbl + (size_t)cell * kSlots;
     unsigned long long x[kSlots];
 #pragma unroll
-    for (int q = 0; q < kSlots; ++q) x[q] = (q < J.nwin) ? e[J.order[q]] : 0ull;
+    for (int q = 0; q < kSlots; ++q) x[q] = (q < J.nwin) ? gload(e + J.order[q]) : 0ull;
     bool lng = false;
 #pragma unroll
     for (int q = 0; q < kSlots; ++q)
@@ -690,7 +690,7 @@ __global__ __launch_bounds__(256) void k_apply_long(const WindowJob* __restrict_
     for (unsigned k = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); k < nq; k += waves) {
         const unsigned cell = ll.cells[k];
         const unsigned long long* e = J.tbl + (size_t)cell * kSlots;
-        const unsigned long long xl = (lane < J.nwin) ? e[J.order[lane]] : 0ull;
+        const unsigned long long xl = (lane < J.nwin) ? gload(e + J.order[lane]) : 0ull;
 #ifdef LGS_PROBE
         unsigned long long t1 = 0, t2 = 0;
         if (blockIdx.x == 0 && threadIdx.x == 0) { (void)__builtin_amdgcn_readfirstlane((int)xl); t1 = wall_clock64(); }
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(256) void k_apply_long(const WindowJob* __restrict_
                 if ((unsigned)(x >> 32) == J.st.s[s] && ((unsigned)x & kLongRun)) {
                     const long long wl = ((long long)((unsigned)x & ~kLongRun) >> 6) + lane;
                     const RunBits& rb = J.slot[s].rb;
-                    if (wl < rb.nw) hw[q] = rb.hitw[wl], ew[q] = rb.endw[wl];
+                    if (wl < rb.nw) hw[q] = gload(rb.hitw + wl), ew[q] = gload(rb.endw + wl);
                 }
             }
         }

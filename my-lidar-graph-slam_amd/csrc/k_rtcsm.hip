@@ -563,7 +563,7 @@ __device__ __forceinline__ void issue_batch(int v0, Fetch& fetch, Addr& addr, do
 #pragma unroll
     for (int j = 0; j < kPipe; ++j) rc[j] = fetch(v0 + j);
 #pragma unroll
-    for (int j = 0; j < kPipe; ++j) buf[j] = *addr(rc[j]);
+    for (int j = 0; j < kPipe; ++j) buf[j] = gload(addr(rc[j]));
 }
 
 __device__ __forceinline__ void add_batch(double& s, const double (&buf)[kPipe], int left)
@@ -813,7 +813,8 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
         // of (qt - 1, X)
         static_assert(kSPY % 16 == 0, "whole quads of sub-phase rows per tile");
         typedef unsigned long long u64;
-        u64* __restrict__ uo = (u64*)(S + 8 * plane * pl.pstrideO);
+        const int u8 = pl.unit8;   // 2: 16-byte units (8 rows), 3: 24-byte units (12 rows)
+        u64* __restrict__ uo = (u64*)(S + 4 * u8 * plane * pl.pstrideO);
         for (int k = tid; k < kSPY * kQ; k += blockDim.x) {   // (quad, sub-phase, column), column fastest
             const int h = k / (16 * kQ), sp = (k / kQ) % 16, X = k % kQ;
             const int qt = (y0 >> 4) + h;
@@ -824,8 +825,9 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
             for (int i = 0; i < 4; ++i)
                 v |= (u64)__builtin_bit_cast(unsigned short, hs[16 * h + 4 * i + cy][sx][X]) << (16 * i);
             const long long u = sp * pl.subO + (long long)qt * pl.Wq4 + Xg;
-            uo[2 * u] = v;
-            if (qt > 0) uo[2 * (u - pl.Wq4) + 1] = v;
+            uo[u8 * u] = v;                                    // rows 4 qt .. of unit qt
+            if (qt > 0) uo[u8 * (u - pl.Wq4) + 1] = v;         // .. of unit qt - 1
+            if (u8 == 3 && qt > 1) uo[3 * (u - 2 * pl.Wq4) + 2] = v;   // .. of unit qt - 2
         }
         return;
     }
@@ -937,7 +939,14 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
 // partials meet in LDS; the bound is the any-order sum (the rounding slack
 // sb_mult covers any order).
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-constexpr int kOctPipe = 8;
+#ifndef LGS_OCT_PIPE9
+#define LGS_OCT_PIPE9 4   // load batches in flight per lane, 9-row windows (measured r04: 2-6: 0.280 ms per config-5 launch, 8: 0.304, 12: 0.376, 16: 0.445)
+#endif
+#ifndef LGS_OCT_PIPE5
+#define LGS_OCT_PIPE5 8
+#endif
+template <int NR>
+constexpr int oct_pipe() { return NR > 5 ? LGS_OCT_PIPE9 : LGS_OCT_PIPE5; }
 __device__ __forceinline__ float h16(unsigned long long bits)
 {
     return (float)__builtin_bit_cast(SuperT, (unsigned short)(bits & 0xFFFFu));
@@ -945,7 +954,10 @@ __device__ __forceinline__ float h16(unsigned long long bits)
 // NR = the superblock rows a lane sums per beam: 5 (nsby <= 5: the beam's
 // rows sit in one unit) or 9 (nsby <= 9: one unit + the high half of the next
 // unit, rows 4q + 8 .. 4q + 11).
-template <int NR>
+// U8: the unit size in 8-byte words (2: 16-byte units, 3: 24-byte units whose
+// third word holds rows 4q + 8 .. 4q + 11, read with the first two at once)
+typedef unsigned long long u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+template <int NR, int U8>
 __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const double* __restrict__ zero)
 {
     const Blk wg = xcd_block();
@@ -954,7 +966,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
     if (wg.y >= pl.T) return;   // past this item's angles (uniform)
     const u64x2* __restrict__ units = (const u64x2*)it.super;
     const u64x2* __restrict__ z2 = (const u64x2*)zero;
-    const unsigned long long* __restrict__ hi8 = (const unsigned long long*)it.super;   // unit halves
+    const unsigned long long* __restrict__ hi8 = (const unsigned long long*)it.super;   // unit words
     extern __shared__ int srow[];   // [Nv]
     __shared__ double part[kSupWaves][64][NR];
     const int t = wg.y;
@@ -977,6 +989,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
     float sr[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) sr[r] = 0.0f;
+    constexpr int kOctPipe = oct_pipe<NR>();
     for (int i0 = 0; i0 < nq; i0 += kOctPipe) {
         u64x2 x[kOctPipe];
         unsigned long long y[kOctPipe];
@@ -988,8 +1001,18 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
             const int c = ok ? row[v] : 0;
             sh[j] = 16 * (c & 3);
             const long long u = (long long)(c >> 2) + a;
-            x[j] = *(ok ? units + u : z2);
-            if constexpr (NR > 5) y[j] = ok ? hi8[2 * (u + wq4) + 1] : 0ull;
+            typedef const __attribute__((address_space(1))) u64x2a8 gu64x2a8_t;
+            typedef const __attribute__((address_space(1))) u64x2 gu64x2_t;
+            typedef const __attribute__((address_space(1))) unsigned long long gu64c_t;
+            if constexpr (U8 == 3) {   // one contiguous 24-byte unit: rows 4q .. 4q + 11
+                const u64x2a8 t = *(gu64x2a8_t*)(ok ? hi8 + 3 * u : (const unsigned long long*)z2);
+                x[j].x = t.x;
+                x[j].y = t.y;
+                y[j] = ok ? *(gu64c_t*)(hi8 + 3 * u + 2) : 0ull;
+            } else {
+                x[j] = *(gu64x2_t*)(ok ? units + u : z2);
+                if constexpr (NR > 5) y[j] = ok ? *(gu64c_t*)(hi8 + 2 * (u + wq4) + 1) : 0ull;
+            }
         }
 #pragma unroll
         for (int j = 0; j < kOctPipe; ++j) {
@@ -1605,20 +1628,21 @@ __device__ void eval_block_t(const RtcsmPlan& pl, const double* __restrict__ gri
         if constexpr (LR == 5 && DEPTH == 2) full = bv & ((unsigned)y < (unsigned)H) & (x0 >= 0) & (x0 + LR - 1 < W);
         if (full) {
             const double* p = grid + (unsigned)(y * W + x0);
-            const d2a8 a = *(const d2a8*)p;
-            const d2a8 e = *(const d2a8*)(p + 2);
+            typedef const __attribute__((address_space(1))) d2a8 gd2a8_t;
+            const d2a8 a = *(gd2a8_t*)p;
+            const d2a8 e = *(gd2a8_t*)(p + 2);
             r[0] = a.x;
             r[1] = a.y;
             r[2] = e.x;
             r[3] = e.y;
-            r[LR - 1] = p[4];
+            r[LR - 1] = gload(p + 4);
         } else {
 #pragma unroll
             for (int q = 0; q < LR; ++q) {
                 const int x = x0 + q;
                 const bool inb = bv & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
                 const unsigned off = (unsigned)(y * W + x);
-                r[q] = *(inb ? grid + off : zero);
+                r[q] = gload(inb ? grid + off : zero);
             }
         }
     };
@@ -1856,7 +1880,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
 #pragma unroll
                 for (int j = 0; j < kSeedB1; ++j) {
                     const int i = min(i0 + j, cnt - 1);
-                    buf[j] = (i0 + j < cnt) ? lb[srow[g + 64 * i]] : 0.0;
+                    buf[j] = (i0 + j < cnt) ? gload(lb + srow[g + 64 * i]) : 0.0;
                 }
 #pragma unroll
                 for (int j = 0; j < kSeedB1; ++j) {
@@ -1933,7 +1957,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
                     const int2 c = sidx[gq + G * min(i0 + j, cnt - 1)];
                     const int x = c.x + xf, y = c.y + yf;
                     const bool inb = (i0 + j < cnt) & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
-                    buf[j] = *(inb ? grid + (unsigned)(y * W + x) : zero);
+                    buf[j] = gload(inb ? grid + (unsigned)(y * W + x) : zero);
                 }
 #pragma unroll
                 for (int j = 0; j < kSeedB2; ++j) {
@@ -2257,6 +2281,153 @@ __global__ __launch_bounds__(64 * kFineLanesWaves) void k_fine_lanes(Items items
     }
 }
 
+// k_fine_regs (LowRes 5, W even, 16-byte aligned grid, at most 8192 cells per
+// side): k_fine_lanes with each beam's 5 x 5 window staged through LDS
+// instead of one 25-lane gather per beam.  The gather made ~34 L1 tag
+// accesses per instruction (its 25 addresses spread over 5 rows,
+// profiles/raw/r03_v7_k1_pipeline_counters.csv) and was bound by that rate.
+// Here 16 lanes per beam each load one aligned 16-byte segment -- row yo
+// (0..4), segment s (0..2) of columns X0 .. X0 + 5, X0 = the window's first
+// column rounded down to even, so a segment never straddles the map's x = 0
+// or x = W edge (W is even); the 16th lane idles -- 4 beams per load
+// instruction, two batches of kFrI instructions in flight in registers.  Each
+// segment is written to LDS shifted by the window's column parity (a pose
+// lane then reads column xo + 1 of its row whatever the window's start), and
+// pose lane (xo, yo) adds the batch's beams in beam order (the reference's
+// sequential fp64 sum).  Segments outside the map load the zero cells, what
+// the per-beam gather reads there.  The beam index row is staged packed (x,
+// y as int16).  Measured (config 2, 64 scans, one stream): 0.147 ms
+// (k_fine_lanes) -> 0.084 ms with kFrI = 4 (2: 0.092, 6: 0.103, 8: 0.118);
+// the same staging by global_load_lds (LDS DMA, a ring of 4-16 slots) ran
+// 0.094-0.158 ms.
+#ifndef LGS_FR_I
+#define LGS_FR_I 4
+#endif
+constexpr int kFrI = LGS_FR_I;            // load instructions per batch (4 beams each)
+constexpr int kFrRow = 13;                // doubles per staged row (bank-conflict-free reads of 5 x 5)
+constexpr int kFrBeam = 5 * kFrRow;       // doubles per staged beam
+constexpr int kFrPad = 4 * kFrI + 4;      // sentinel entries past the row (the last batch's tail)
+__device__ __forceinline__ int2 unpack16(unsigned u)
+{
+    return make_int2((int)(short)(u & 0xFFFFu), (int)(short)(u >> 16));
+}
+__global__ __launch_bounds__(64) void k_fine_regs(Items items, int n, const double* __restrict__ zero)
+{
+    __shared__ int ipref[kMaxBatchItems + 1];
+    __shared__ double stage[4 * kFrI * kFrBeam];
+    extern __shared__ unsigned pidx[];   // [Nv + kFrPad] packed (x, y)
+    {
+        const int j = threadIdx.x;
+        const int c = (j < n) ? *items[j].nsel : 0;
+        int incl = c;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off, 64);
+            if (j >= off) incl += t;
+        }
+        if (j < n) ipref[j + 1] = incl;
+        if (j == 0) ipref[0] = 0;
+    }
+    __syncthreads();
+    const int total = ipref[n];
+    const int lane = threadIdx.x & 63;
+    constexpr int LR = 5;
+    const int lb = lane >> 4, ls = lane & 15;
+    const int lrow = ls / 3, lseg = ls - 3 * (ls / 3);
+    const bool act = lane < LR * LR;
+    const int xo = lane / LR, yo = lane - (lane / LR) * LR;
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    for (int g = blockIdx.x; g < total; g += gridDim.x) {   // workgroup-uniform
+        int lo = 0, hi = n - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (ipref[mid] <= g) lo = mid;
+            else hi = mid - 1;
+        }
+        const int j = __builtin_amdgcn_readfirstlane(lo);
+        const MatchItem& it = items[j];
+        const RtcsmPlan& pl = it.pl;
+        const int b = __builtin_amdgcn_readfirstlane(g - ipref[j]);
+        const int k = it.dlist[b];
+        const int tt = k / pl.P, rem = k % pl.P;
+        const int jx = rem / pl.ncy, jy = rem % pl.ncy;
+        const int xf0 = -pl.win_x + jx * LR, yf0 = -pl.win_y + jy * LR;
+        const int W = pl.W, H = pl.H, Nv = pl.Nv;
+        const double* __restrict__ grid = it.grid;
+        const int2* __restrict__ src_idx = it.idx + (size_t)tt * Nv;
+        __syncthreads();   // the previous block's row is read
+        for (int v = lane; v < Nv + kFrPad; v += 64) {
+            int2 c = v < Nv ? src_idx[v] : make_int2(-(1 << 28), -(1 << 28));
+            c.x = min(max(c.x, -16384), 16383);   // far outside the map either way (W, H <= 8192)
+            c.y = min(max(c.y, -16384), 16383);
+            pidx[v] = (unsigned)(c.x & 0xFFFF) | ((unsigned)c.y << 16);
+        }
+        __syncthreads();
+        const int nb = (Nv + 4 * kFrI - 1) / (4 * kFrI);   // batches
+        auto load = [&](int bt, d2v (&r)[kFrI], int (&dx)[kFrI]) {
+#pragma unroll
+            for (int q = 0; q < kFrI; ++q) {
+                const int2 c = unpack16(pidx[(bt * kFrI + q) * 4 + lb]);
+                const int x = c.x + xf0;
+                const int X = (x & ~1) + 2 * lseg, y = c.y + yf0 + lrow;
+                dx[q] = x & 1;
+                const bool in = ls < 15 && (unsigned)y < (unsigned)H && X >= 0 && X < W;
+                typedef const __attribute__((address_space(1))) d2v gd2v_t;
+                r[q] = *(gd2v_t*)(in ? grid + ((size_t)y * W + X) : zero);
+            }
+        };
+        auto put = [&](const d2v (&r)[kFrI], const int (&dx)[kFrI]) {
+            if (ls < 15) {
+#pragma unroll
+                for (int q = 0; q < kFrI; ++q) {
+                    double* row = stage + (q * 4 + lb) * kFrBeam + lrow * kFrRow + 1 + 2 * lseg - dx[q];
+                    row[0] = r[q].x;
+                    row[1] = r[q].y;
+                }
+            }
+        };
+        d2v ra[kFrI], rb[kFrI];
+        int da[kFrI], db[kFrI];
+        load(0, ra, da);
+        load(1, rb, db);
+        double acc = 0.0;
+        const int pose_off = yo * kFrRow + 1 + xo;
+        auto consume = [&](d2v (&r)[kFrI], int (&dx)[kFrI], int next) {
+            put(r, dx);   // LDS ops of a wave run in order: the reads below see these writes
+            double v[4 * kFrI];
+#pragma unroll
+            for (int q = 0; q < 4 * kFrI; ++q) v[q] = stage[q * kFrBeam + pose_off];
+            __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+            __builtin_amdgcn_sched_barrier(0);
+            if (next < nb) load(next, r, dx);   // refill (the last batch's tail: sentinel beams, zero cells)
+            __builtin_amdgcn_sched_barrier(0);
+            double s = acc;
+#pragma unroll
+            for (int q = 0; q < 4 * kFrI; ++q) s += v[q];   // beams past the row add +0.0: exact
+            acc = s;
+        };
+        for (int bt = 0; bt < nb; bt += 2) {
+            consume(ra, da, bt + 2);
+            if (bt + 1 >= nb) break;
+            consume(rb, db, bt + 3);
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        double bv = act ? acc : -INFINITY;
+        long long bo = act ? (long long)lane : LLONG_MAX;
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ov = __shfl_xor(bv, off, 64);
+            const long long ok = __shfl_xor(bo, off, 64);
+            if (better(ov, ok, bv, bo)) {
+                bv = ov;
+                bo = ok;
+            }
+        }
+        if (lane == 0) {
+            it.fval[b] = bv;
+            it.fpos[b] = (int)bo;
+        }
+    }
+}
+
 // k_replay (one wave): the reference's sequential acceptance (:98-114 with the
 // strict update of :246) over the selected blocks in block order.  Lanes load
 // 64 consecutive entries at once; the acceptance itself walks them in lane
@@ -2297,11 +2468,12 @@ __global__ __launch_bounds__(64) void k_replay(Items items)
             c = cscore[k];
             // k_fine's frows row results of the block: max, ties to the
             // smallest order index (the reference's x-outer, y-inner walk)
-            f = fval[(size_t)b * frows];
-            pos = fpos[(size_t)b * frows];
+            const size_t fi = (size_t)b * frows;
+            f = fval[fi];
+            pos = fpos[fi];
             for (int r = 1; r < frows; ++r) {
-                const double fr = fval[(size_t)b * frows + r];
-                const int pr = fpos[(size_t)b * frows + r];
+                const double fr = fval[fi + r];
+                const int pr = fpos[fi + r];
                 if (fr > f || (fr == f && pr < pos)) {
                     f = fr;
                     pos = pr;
@@ -2374,7 +2546,7 @@ __device__ __forceinline__ double gval(const CostPlan& cp, const double* __restr
 {
     const bool inb = ((unsigned)x < (unsigned)cp.W) & ((unsigned)y < (unsigned)cp.H);
     const size_t off = inb ? (size_t)y * cp.W + x : 0;
-    const double v = g[off];
+    const double v = gload(g + off);
     return inb ? v : 0.0;
 }
 
@@ -2562,6 +2734,10 @@ void set_plane_layout(RtcsmPlan& pl)
     // octet layout: one 16-byte unit holds 5 superblock rows of a beam's
     // window (nsby <= 5), one unit + the high half of the next holds 9
     pl.oct = pl.nsbx <= 9 && pl.nsby <= 9 && pl.nsbx * pl.nsby <= 64;
+#ifndef LGS_OCT12
+#define LGS_OCT12 1
+#endif
+    pl.unit8 = (LGS_OCT12 && pl.oct && pl.nsby > 5) ? 3 : 2;
     pl.Qo = (pl.Hq4 + 3) / 4 + 1;
     pl.subO = (long long)pl.Qo * pl.Wq4;
     pl.pstrideO = 16 * pl.subO;
@@ -2647,10 +2823,12 @@ struct BatchShape {
     int P = 0, nsb2 = 0, chunks = 0, low_res = 0, cb = 0;
     bool pair = false;
     bool oct = false;       // k_super_oct (octet layout of the plan, nsbx, nsby <= 9; chunks == 1)
+    int unit8 = 2;          // its unit size in 8-byte words (3: 24-byte units for 6-9 rows)
     int nsby = 0;
     bool pruned = false;    // superblock pruning
     bool lr5 = false;       // transposed LR = 5 evaluators
     bool fine_lanes = false;   // k_compact + k_fine_lanes (lr * lr <= 64)
+    bool fine_staged = false;  // ... as k_fine_regs (LowRes 5, every map W even, <= 8192, 16-byte aligned)
     int frows = 1;
     int kernel_size = 0;
     WorkList wl{};          // kept-superblock work list (wl.cnt null: k_coarse_rows)
@@ -2751,7 +2929,7 @@ inline size_t plane16_bytes(const RtcsmPlan& pl)
 inline size_t set_bytes(const RtcsmPlan& pl) { return plane_bytes(pl) + plane16_bytes(pl); }
 inline size_t super_bytes(const RtcsmPlan& pl)
 {
-    if (pl.oct) return align256(16 * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstrideO);
+    if (pl.oct) return align256(8 * (size_t)pl.unit8 * pl.low_res * pl.low_res * (size_t)pl.pstrideO);
     return align256(sizeof(SuperT) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
 }
 double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_super)
@@ -3009,9 +3187,11 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             dim3 g(B.chunks, B.Tmax, n);
             if (ctx->skipped(K_SUPER)) {
             } else if (B.oct && B.nsby <= 5)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<5>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<5, 2>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+            else if (B.oct && B.unit8 == 3)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9, 3>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else if (B.oct)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9, 2>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else if (B.pair)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<1>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else
@@ -3096,9 +3276,14 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         hipLaunchKernelGGL(k_compact, dim3(n), dim3(256), pref_bytes(B.nsegMax), st, d_items);
         LGS_HIP_CHECK(hipGetLastError());
         const int tok_ = ctx->timing_begin(K_FINE, 0.0);
-        if (!ctx->skipped(K_FINE))
+        if (ctx->skipped(K_FINE)) {
+        } else if (B.fine_staged && ctx->fine_staged) {
+            hipLaunchKernelGGL(k_fine_regs, dim3(4096), dim3(64), sizeof(unsigned) * (size_t)(B.NvMax + kFrPad), st,
+                               d_items, n, zero);
+        } else {
             hipLaunchKernelGGL(k_fine_lanes, dim3(4096), dim3(64 * kFineLanesWaves),
                                sizeof(int2) * (size_t)(B.NvMax + 4 * kPipe), st, d_items, n, zero);
+        }
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
     } else {
@@ -3390,6 +3575,7 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     B.pair = B.nsb2 <= 32;
     B.chunks = B.pair ? 1 : (B.nsb2 + 63) / 64;
     B.oct = p0.oct != 0;
+    B.unit8 = p0.unit8;
     B.nsby = p0.nsby;
     B.pruned = uses_super(ctx, B.NvMax, B.nsb2, false);
     B.lr5 = lr5_path(B.NvMax, B.low_res);
@@ -3398,6 +3584,10 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     B.fine_lanes = n >= ctx->lanes_min_batch && B.low_res * B.low_res <= 64 &&
                    B.NvMax <= kFineLanesMaxNv;
     B.frows = (B.lr5 && !B.fine_lanes) ? 5 : 1;
+    B.fine_staged = B.fine_lanes && B.low_res == 5;
+    for (int j = 0; j < n && B.fine_staged; ++j)
+        B.fine_staged = grids[j]->w % 2 == 0 && ((uintptr_t)grids[j]->d & 15) == 0 && grids[j]->w <= 8192 &&
+                        grids[j]->h <= 8192;
     B.kernel_size = cost->kernel_size;
     B.nsegMax = (int)(((long long)B.Tmax * B.P + kSelSeg - 1) / kSelSeg);
     if (B.pruned && n >= ctx->lanes_min_batch && B.NvMax <= kListMaxNv && B.Tmax < (1 << 24) && B.nsb2 <= 64) {

@@ -442,6 +442,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_PEER_COPY: ctx->peer_staged = value != 0.0; return LGS_OK;
     case LGS_OPT_PRUNE_MIN_SUPER: ctx->prune_min_super = (int)value; return LGS_OK;
     case LGS_OPT_COOP_TILES: ctx->coop_tiles = (long long)value; return LGS_OK;
+    case LGS_OPT_FINE_STAGED: ctx->fine_staged = value != 0.0; return LGS_OK;
     case LGS_OPT_SORT_BARRIER_US:
         if (value < 0) return LGS_ERR_INVALID_ARG;
         ctx->sort_barrier_us = (long long)value;
@@ -793,7 +794,7 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
 #pragma unroll
         for (int k = 0; k < FH; ++k) {
             const int yy = sy0 + k;
-            v[k] = (xx < W && yy < H) ? in[(size_t)yy * W + xx] : 0.0;   // reads past the end are 0
+            v[k] = (xx < W && yy < H) ? gload(in + ((size_t)yy * W + xx)) : 0.0;   // reads past the end are 0
         }
         // window maxima of every start row (static register indices), then row
         // oy takes the window starting at win_start(y0 + oy) - sy0 =

@@ -150,8 +150,11 @@ struct RtcsmPlan {
     // each sub-phase array is stored as 16-byte units (q, X) holding its rows
     // 4q .. 4q + 7 at column X (every row twice), so a beam's 5 window rows at
     // one column are one aligned 16-byte load; superblock bases are then
-    // (unit << 2) | (first row & 3)
-    int oct, Qo;
+    // (unit << 2) | (first row & 3).  Windows of 6-9 superblock rows use
+    // 24-byte units (rows 4q .. 4q + 11, every row three times): a beam's 9
+    // rows at one column are then one contiguous 24-byte read (unit8 = 3,
+    // else 2: the unit's size in 8-byte words)
+    int oct, Qo, unit8;
     long long subO, pstrideO;   // units per sub-phase array / per plane
 };
 
@@ -258,6 +261,10 @@ struct lgs_ctx {
     bool super_prune = true;     // superblock pruning of k_coarse (LGS_OPT_SUPER_PRUNE)
     bool linsolve_split = true;  // lone refine over one workgroup per 64 beams (LGS_OPT_LINSOLVE_SPLIT)
     long long handoff_spin_us = 200000;   // split refine spin bound (LGS_OPT_HANDOFF_SPIN_US; 0 = force the fallback)
+#ifndef LGS_FINE_STAGED_DEFAULT
+#define LGS_FINE_STAGED_DEFAULT 1
+#endif
+    bool fine_staged = LGS_FINE_STAGED_DEFAULT;   // batched LowRes-5 fine evaluator: LDS-staged windows (LGS_OPT_FINE_STAGED)
     long long coop_tiles = -1;   // one-launch sort: tile limit for this ctx (LGS_OPT_COOP_TILES; -1 = device capacity)
     long long sort_barrier_us = 50000;   // one-launch sort: barrier wait bound (LGS_OPT_SORT_BARRIER_US)
     long long handoff_fallbacks = 0;      // split refines rerun on one workgroup after a time-out
@@ -427,6 +434,31 @@ struct CopyFence {
     }
 };
 }  // namespace lgs
+
+// Loads from global memory through a generic pointer (a descriptor field)
+// compile to flat_load, which also counts against lgkmcnt: every LDS wait of
+// the kernel then waits for the gathers in flight too.  gload issues them as
+// global_load (address space 1); every target passed to it is device memory.
+#ifndef LGS_GLOBAL_GATHER
+#define LGS_GLOBAL_GATHER 1
+#endif
+#ifdef __HIP_DEVICE_COMPILE__
+template <class T>
+__device__ __forceinline__ T gload(const T* p)
+{
+#if LGS_GLOBAL_GATHER
+    return *(const __attribute__((address_space(1))) T*)p;
+#else
+    return *p;
+#endif
+}
+#else
+template <class T>
+__device__ __forceinline__ T gload(const T* p)
+{
+    return *p;
+}
+#endif
 
 struct lgs_scan {
     lgs_ctx* ctx = nullptr;   // creating context (not used after its destruction)

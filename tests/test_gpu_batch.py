@@ -311,3 +311,36 @@ def test_scans_first_touched_by_two_contexts_at_once(ctx, world, small_map):
                     assert got[k][j] == ref[j], (rnd, k, j)
     finally:
         other.close()
+
+
+@pytest.mark.parametrize("n_cells,low_edge", [(400, False), (401, False), (400, True)])
+def test_fine_staged_equals_gathers(ctx, world, n_cells, low_edge):
+    """The LDS-staged batched fine evaluator (k_fine_regs, LowRes 5, even W)
+    == the per-beam gather one (k_fine_lanes) == the oracle, field for field;
+    an odd-width map (401) takes the gather kernel either way, and a map
+    cropped at its low edges puts windows across x = 0 / y = 0."""
+    cells, mx, my = build_map(world, 600 if low_edge else n_cells, 0.05, 100, scene.arc_poses(5), n_beams=541)
+    if low_edge:
+        cells, mx, my = cells[40:440, 40:440].copy(), mx + 2.0, my + 2.0
+    elif n_cells % 2:
+        cells = cells[:, :n_cells]
+    rng = np.random.default_rng(n_cells + low_edge)
+    ang, qs = _queries(world, rng, 9, 541)
+    if low_edge:
+        qs = [(scene.ray_cast(world, (t[0] - 0.8, t[1] - 0.8, t[2]), ang), (t[0] - 0.7, t[1] - 0.9, t[2]))
+              for (_, t) in qs]
+    params = (5, 1.0, 1.0, 0.6, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    scans = [ctx.scan(r, ang) for r, _ in qs]
+    inits = [i for _, i in qs]
+    try:
+        ctx.set_option(abi.LGS_OPT_FINE_STAGED, 0)
+        gath = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, inits)]
+        ctx.set_option(abi.LGS_OPT_FINE_STAGED, 1)
+        stag = ctx.optimize_pose_query_batch(g, P, cost, scans, inits)
+    finally:
+        ctx.set_option(abi.LGS_OPT_FINE_STAGED, 1)
+    assert [_record(b) for b in stag] == gath
+    for j, ((r, init), b) in enumerate(zip(qs, stag)):
+        assert_same(b, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"q{j}")
