@@ -577,7 +577,22 @@ __device__ __forceinline__ void add_batch(double& s, const double (&buf)[kPipe],
 }
 
 // Two register buffers alternate roles (no copies), so while batch k is being
-// added, batch k+1's gathers are in flight.
+// added, batch k+1's gathers are in flight.  seq_sum_from continues a sum
+// (the same additions, in order, as one longer seq_sum).
+template <class Rec, class Fetch, class Addr>
+__device__ __forceinline__ double seq_sum_from(double s, int n, Fetch fetch, Addr addr)
+{
+    double a[kPipe], b[kPipe];
+    issue_batch<Rec>(0, fetch, addr, a);
+    for (int v0 = 0; v0 < n; v0 += 2 * kPipe) {
+        issue_batch<Rec>(v0 + kPipe, fetch, addr, b);
+        add_batch(s, a, n - v0);
+        if (v0 + kPipe >= n) break;
+        issue_batch<Rec>(v0 + 2 * kPipe, fetch, addr, a);
+        add_batch(s, b, n - v0 - kPipe);
+    }
+    return s;
+}
 template <class Rec, class Fetch, class Addr>
 __device__ __forceinline__ double seq_sum(int n, Fetch fetch, Addr addr)
 {
@@ -825,9 +840,9 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
             for (int i = 0; i < 4; ++i)
                 v |= (u64)__builtin_bit_cast(unsigned short, hs[16 * h + 4 * i + cy][sx][X]) << (16 * i);
             const long long u = sp * pl.subO + (long long)qt * pl.Wq4 + Xg;
-            uo[u8 * u] = v;                                    // rows 4 qt .. of unit qt
-            if (qt > 0) uo[u8 * (u - pl.Wq4) + 1] = v;         // .. of unit qt - 1
-            if (u8 == 3 && qt > 1) uo[3 * (u - 2 * pl.Wq4) + 2] = v;   // .. of unit qt - 2
+            gstore(uo + u8 * u, v);                                          // rows 4 qt .. of unit qt
+            if (qt > 0) gstore(uo + (u8 * (u - pl.Wq4) + 1), v);             // .. of unit qt - 1
+            if (u8 == 3 && qt > 1) gstore(uo + (3 * (u - 2 * pl.Wq4) + 2), v);   // .. of unit qt - 2
         }
         return;
     }
@@ -841,7 +856,7 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
         const int y = y0 + r;
         const int xq = q0 + 8 * ch;
         if (y >= Hqp || xq >= pl.Wq4) continue;
-        *(s8*)(out + ((y & 3) * 4 + sx) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + xq) = *(const s8*)&hs[r][sx][8 * ch];
+        gstore((s8*)(out + ((y & 3) * 4 + sx) * pl.sub4 + (long long)(y >> 2) * pl.Wq4 + xq), *(const s8*)&hs[r][sx][8 * ch]);
     }
 }
 
@@ -1388,7 +1403,10 @@ struct WorkList {
 constexpr int kListMaxNv = 4096;   // k_coarse_list stages four beam rows in LDS (64 KB)
 // grid sizes measured (config 5 / config 2 stage ms): list 2048 + unsafe 1024: 0.272 / 0.373; 2048 + 4096:
 // 0.241 / 0.375; 4096 + 4096: 0.226 / 0.364; 2304 + 4096: 0.226 / 0.365; 1024 + 4096: 0.288 / 0.528
-constexpr int kListWaves = 4096;   // k_coarse_list workgroups (one wave each, grid-stride)
+#ifndef LGS_LIST_WAVES
+#define LGS_LIST_WAVES 4096
+#endif
+constexpr int kListWaves = LGS_LIST_WAVES;   // k_coarse_list workgroups (one wave each, grid-stride)
 constexpr int kUnsafeGroups = 4096;
 
 __global__ __launch_bounds__(64) void k_keep(Items items, WorkList W)
@@ -1491,6 +1509,87 @@ __global__ __launch_bounds__(64) void k_coarse_list(Items items, WorkList W, int
         constexpr int kOff = -(1 << 30);
         const double sum = seq_sum<int>(nmax, [&](int v) { return v < Nv ? my[min(v, rowlen - 1)] : kOff; },
                                         [&](const int& cc) { return (active && cc != kOff) ? lane_base + cc : zero; });
+        if (active) {
+            const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
+            it.cscore[k] = sum;
+            it.cflag[k] = 0;
+        }
+    }
+}
+
+// k_coarse_list with the four beam rows staged in chunks of kLC beams (4 KB
+// of LDS per wave instead of 4 * Nv ints, 17 KB for config 2, which capped
+// the kernel at 9 waves per CU): the next chunk is loaded into registers
+// while the current one is summed, then written to LDS; the sum carries over
+// the chunks in beam order (seq_sum_from).  The same sums as k_coarse_list.
+#ifndef LGS_LIST_CHUNK
+#define LGS_LIST_CHUNK 256
+#endif
+constexpr int kLC = LGS_LIST_CHUNK > 0 ? LGS_LIST_CHUNK : 256;
+static_assert(kLC % 64 == 0, "whole waves per chunk row");
+__global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, int n, const double* __restrict__ zero)
+{
+    __shared__ int s_cb[4][kLC + 2 * kPipe];
+    const int lane = threadIdx.x, g4 = lane >> 4, m = lane & 15;
+    int c;
+    const int total = list_prefix(W, 0, n, c);
+    constexpr int kOff = -(1 << 30);
+    constexpr int PER = kLC / 64;
+    for (int e0 = 4 * blockIdx.x; e0 < total; e0 += 4 * gridDim.x) {   // wave-uniform
+        const int e = e0 + g4;
+        const bool has = e < total;
+        int j = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int jq = __popcll(__ballot(lane < n && c <= e0 + q));
+            if (g4 == q) j = jq;
+        }
+        if (!has) j = 0;
+        const int cprev = __shfl(c, max(j - 1, 0), 64);
+        const int before = j > 0 ? cprev : 0;
+        const MatchItem& it = items[j];
+        const RtcsmPlan& pl = it.pl;
+        const int ent = has ? W.sbl[(size_t)j * W.region + (e - before)] : 0;
+        const int t = ent >> 6, sb = ent & 63;
+        const int Nv = has ? pl.Nv : 0;
+        const int* __restrict__ cbr = it.cbase + (size_t)t * pl.Nv;
+        int nmax = Nv;
+#pragma unroll
+        for (int off = 16; off < 64; off <<= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
+        const int nsbx = max(pl.nsbx, 1);
+        const int jx = kSB * (sb % nsbx) + (m & 3), jy = kSB * (sb / nsbx) + (m >> 2);
+        const bool active = has && jx < pl.ncx && jy < pl.ncy;
+        const double* __restrict__ lane_base = it.cmap + (active ? jy * pl.Wqp + jx : 0);
+        int pre[4][PER];
+        auto fetch_chunk = [&](int v0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int nq = __shfl(Nv, 16 * q, 64);
+                const int* row = (const int*)__shfl((unsigned long long)cbr, 16 * q, 64);
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int v = v0 + lane + 64 * i;
+                    pre[q][i] = v < nq ? gload(row + v) : kOff;   // past a row: the zero cell
+                }
+            }
+        };
+        fetch_chunk(0);
+        double sum = 0.0;
+        for (int v0 = 0; v0 < nmax; v0 += kLC) {   // wave-uniform
+            // one wave: its LDS operations run in order, so the previous
+            // chunk's reads are done before these writes
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int i = 0; i < PER; ++i) s_cb[q][lane + 64 * i] = pre[q][i];
+                if (lane < 2 * kPipe) s_cb[q][kLC + lane] = kOff;   // seq_sum's look-ahead
+            }
+            if (v0 + kLC < nmax) fetch_chunk(v0 + kLC);
+            const int cnt = min(kLC, nmax - v0);
+            const int* __restrict__ my = s_cb[g4];
+            sum = seq_sum_from<int>(sum, cnt, [&](int v) { return my[v]; },
+                                    [&](const int& cc) { return (active && cc != kOff) ? lane_base + cc : zero; });
+        }
         if (active) {
             const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
             it.cscore[k] = sum;
@@ -3222,6 +3321,8 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * beams_K);
         if (tok >= 0) ctx->pending[tok].coarse_evals = true;   // algorithmic bytes from the records
         if (ctx->skipped(K_COARSE)) {
+        } else if (wl && LGS_LIST_CHUNK > 0) {
+            hipLaunchKernelGGL(k_coarse_list_c, dim3(kListWaves), dim3(64), 0, st, d_items, B.wl, n, zero);
         } else if (wl) {
             const int rowlen = std::max(B.NvMax, 1);
             hipLaunchKernelGGL(k_coarse_list, dim3(kListWaves), dim3(64), sizeof(int) * 4 * (size_t)rowlen, st,

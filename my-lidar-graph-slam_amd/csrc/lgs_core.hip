@@ -850,16 +850,17 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
             d2a16 v;
             v.x = ma;
             v.y = mb;
-            *(d2a16*)dst = v;
+            gstore((d2a16*)dst, v);
             if (j.out16) {   // the pair's fp16 round-ups (o is even: 4-byte aligned)
-                *(unsigned*)(j.out16 + o) = (unsigned)half_round_up_bits(ma) | ((unsigned)half_round_up_bits(mb) << 16);
-                if (ma < 0.0 || mb < 0.0) *j.negflag = j.pgen;
+                gstore((unsigned*)(j.out16 + o),
+                       (unsigned)half_round_up_bits(ma) | ((unsigned)half_round_up_bits(mb) << 16));
+                if (ma < 0.0 || mb < 0.0) gstore(j.negflag, j.pgen);
             }
         } else {
-            *dst = ma;
+            gstore(dst, ma);
             if (j.out16) {
-                j.out16[o] = half_round_up_bits(ma);
-                if (ma < 0.0) *j.negflag = j.pgen;
+                gstore(j.out16 + o, half_round_up_bits(ma));
+                if (ma < 0.0) gstore(j.negflag, j.pgen);
             }
         }
     }

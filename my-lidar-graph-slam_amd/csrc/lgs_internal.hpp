@@ -452,11 +452,25 @@ __device__ __forceinline__ T gload(const T* p)
     return *p;
 #endif
 }
+template <class T>
+__device__ __forceinline__ void gstore(T* p, T v)
+{
+#if LGS_GLOBAL_GATHER
+    *(__attribute__((address_space(1))) T*)p = v;
+#else
+    *p = v;
+#endif
+}
 #else
 template <class T>
 __device__ __forceinline__ T gload(const T* p)
 {
     return *p;
+}
+template <class T>
+__device__ __forceinline__ void gstore(T* p, T v)
+{
+    *p = v;
 }
 #endif
 
