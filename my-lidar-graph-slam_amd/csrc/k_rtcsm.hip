@@ -2778,6 +2778,356 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(Items items, int guard_ca
 #define KCOST(ks) ((ks) == 1 ? k_cost<1> : k_cost<0>)
 
 // --------------------------------------------------------------------------
+// Small windows: the whole search of a window whose coarse
+// lattice holds ONE block per angle (2 winX < lr and 2 winY < lr: the launcher
+// JSON frontend window, +-0.1 m at 5 cm with LowRes 5) in one launch, one
+// workgroup of LR waves per (angle, item):
+//  1. ComputeScanIndices of the angle (:179-200) with k_project's arithmetic
+//     and boundary guard, into LDS (and the item's index rows, which the
+//     host's guard fix-ups patch; mode 1 reruns read those rows back);
+//  2. the block's LR x LR fine scores and its coarse score in ONE pass over
+//     the beams: wave w gathers fine row yo = w of 64 beams at a time (LR
+//     cells each), lanes 0..LR-1 of every wave add their (xo, yo) row in beam
+//     order.  The precomputed map's value at a beam's lattice start
+//     (PrecomputeGridMap, C/mapping/grid_map_builder.cpp:518-536) is the max
+//     of exactly those LR x LR cells when the window lies in the map (edge
+//     beams: SlidingWindowMax's clamped last window, H/util.hpp:247-250, or 0
+//     outside the map); wave 0 takes it from the waves' row maxima after a
+//     workgroup barrier and its lane LR adds it in beam order.  No coarse map
+//     is built;
+//  3. the item's last workgroup to finish (a wrap-around device-scope
+//     counter) walks the angles in the reference's order (:88-112) over the
+//     published (coarse, fine max, first argmax) triples: a block is refined
+//     when !(coarse <= scoreMax), accepted when its fine max > scoreMax; the
+//     record, the refined-block count and the 7 cost poses are written there.
+// Every score is the reference's sequential beam-order fp64 sum (bit-exact);
+// nothing is pruned, so no rounding bound is involved.
+// --------------------------------------------------------------------------
+constexpr int kSmallMaxNv = 64 * kMaxChunks;   // fully unrolled chunk loop
+constexpr int kSmallDepth = 4;                 // chunks of gathers in flight per wave
+
+// Precomputed-map value at (bx, by) read directly from the fine map: 0 (the
+// unknown value) outside the map, else the max of the window SlidingWindowMax
+// assigns to that cell (its start clamped to the last full window, zero
+// padding when the map is narrower than the window).
+__device__ __forceinline__ double small_cval(const double* __restrict__ grid, int bx, int by, int W, int H, int lr)
+{
+    if (bx < 0 || by < 0 || bx >= W || by >= H) return 0.0;
+    const int sx = min(bx, max(W - lr, 0)), sy = min(by, max(H - lr, 0));
+    const int ex = min(sx + lr, W), ey = min(sy + lr, H);
+    double m = (W < lr || H < lr) ? 0.0 : -INFINITY;
+    for (int y = sy; y < ey; ++y)
+        for (int x = sx; x < ex; ++x) m = fmax(m, gload(grid + (size_t)y * W + x));
+    return m;
+}
+
+template <int LR>
+constexpr size_t small_buf_doubles()
+{
+    // per wave, 2 buffers of LR fine rows + row max + coarse row; then the
+    // edge beams' coarse values [kSmallMaxNv]
+    return (size_t)LR * 2 * (LR + 2) * 65 + kSmallMaxNv;
+}
+
+template <int LR>
+__global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, int guard_cap, double guard_eps,
+                                                         int inject, const double* __restrict__ zero)
+{
+    constexpr int NT = 64 * LR, LD = 65, ROWB = (LR + 2) * LD, WSTR = 2 * ROWB;
+    const MatchItem& it = items[blockIdx.y];
+    const RtcsmPlan& pl = it.pl;
+    const int tt = blockIdx.x;
+    if (tt >= pl.T) return;   // past this item's angles (uniform)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int Nv = pl.Nv, W = pl.W, H = pl.H;
+    const double* __restrict__ grid = it.grid;
+    RtcsmRecord* rec = it.rec;
+    const int gen = it.gen;
+    extern __shared__ char smem[];
+    int2* sidx = (int2*)smem;   // [Nv]
+    double* bufs = (double*)(smem + sizeof(int2) * (size_t)((Nv + 1) & ~1));   // [LR waves][WSTR]
+    __shared__ int s_wsum[LR];
+    __shared__ double s_trig[2];
+    __shared__ double s_f[LR * LR];
+    __shared__ double s_c;
+    __shared__ int s_last;
+    typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+    gu64_t* __restrict__ gidx = (gu64_t*)(it.idx + (size_t)tt * Nv);
+
+    // 1. the angle's scan indices
+    if (mode == 0) {
+        const double* __restrict__ ranges = it.ranges;
+        const double* __restrict__ angles = it.angles;
+        int* smap = (int*)bufs;   // valid beam v -> beam index (the value buffers are not in use yet)
+        if (tid == 0) {
+            // currentSensorPose.mTheta = sensorPose.mTheta + stepTheta * t (:90-91)
+            const double th = pl.st + pl.step_t * (double)(tt - pl.win_t);
+            double sn, cs;
+            sincos(th, &sn, &cs);
+            s_trig[0] = cs;
+            s_trig[1] = sn;
+        }
+        const int chunk = (pl.N + NT - 1) / NT;
+        const int lo = min(tid * chunk, pl.N), hi = min(lo + chunk, pl.N);
+        int nvalid = 0;
+        for (int i = lo; i < hi; ++i) nvalid += !(ranges[i] >= pl.rmax);
+        int incl = nvalid;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += t;
+        }
+        if (lane == 63) s_wsum[wave] = incl;
+        __syncthreads();
+        int pos = incl - nvalid;
+        for (int j = 0; j < wave; ++j) pos += s_wsum[j];
+        for (int i = lo; i < hi; ++i)
+            if (!(ranges[i] >= pl.rmax)) smap[pos++] = i;
+        __syncthreads();
+        const double ct = s_trig[0], st = s_trig[1];
+        const double inv_res = 1.0 / pl.res;
+        for (int v0 = 0; v0 < Nv; v0 += NT) {   // uniform trip count: tagged_slot_wave needs every lane
+            const int v = v0 + tid;
+            const bool act = v < Nv;
+            int ix = 0, iy = 0;
+            bool guarded = false;
+            if (act) {
+                // the arithmetic of k_project (HitPoint by rotation, x * (1 / res))
+                const int i = smap[v];
+                const double r = ranges[i];
+                double sa, ca;
+                sincos(angles[i], &sa, &ca);
+                const double c = ct * ca - st * sa;
+                const double s = st * ca + ct * sa;
+                const double hx = pl.sx + r * c;
+                const double hy = pl.sy + r * s;
+                const double qx = (hx - pl.min_x) * inv_res;
+                const double qy = (hy - pl.min_y) * inv_res;
+                ix = (int)floor(qx);
+                iy = (int)floor(qy);
+                guarded = near_boundary(qx, guard_eps) || near_boundary(qy, guard_eps);
+            }
+            const int slot = tagged_slot_wave(&rec->guard_word, (unsigned)gen, guarded);
+            if (guarded) {
+                if (slot < guard_cap) {
+                    GuardRec g;
+                    g.t = tt;
+                    g.v = v;
+                    g.ix = ix + inject;
+                    g.iy = iy;
+                    rec->guard[slot] = g;
+                }
+                ix += inject;
+            }
+            if (act) {
+                sidx[v] = make_int2(ix, iy);
+                gidx[v] = ((unsigned long long)(unsigned)iy << 32) | (unsigned)ix;
+            }
+        }
+        __syncthreads();   // the beam map is dead from here on
+    } else {
+        stage_lds(sidx, it.idx + (size_t)tt * Nv, Nv);
+        __syncthreads();
+    }
+
+    // 2. fine rows + coarse values, beam order
+    const int nchunk = (Nv + 63) / 64;
+    const int xc = -pl.win_x, yr = -pl.win_y + wave;
+    double* wb = bufs + (size_t)wave * WSTR;
+    // Every lane loads its row run with 16-byte loads from a clamped, always
+    // valid address into r; lanes whose run leaves the map load their cells
+    // one by one into separate registers e (the other lanes read the zero
+    // cell).  Branch-free on purpose: with the loads of either side under a
+    // branch the compiler waits for every older gather in flight (vmcnt(0))
+    // before each chunk's stores, which undoes the prefetch.
+    double r[kSmallDepth][LR], e[kSmallDepth][LR];
+    bool fl[kSmallDepth];
+    auto gather = [&](int c, double (&x)[LR], double (&xe)[LR], bool& full) {
+        const int b = c * 64 + lane;
+        const int2 ij = sidx[max(min(b, Nv - 1), 0)];
+        const bool bv = b < Nv;
+        const int x0 = ij.x + xc, y = ij.y + yr;
+        full = bv & ((unsigned)y < (unsigned)H) & (x0 >= 0) & (x0 + LR - 1 < W);
+        typedef const __attribute__((address_space(1))) d2a8 gd2a8_t;
+        const double* p = (W >= LR) ? grid + (unsigned)(min(max(y, 0), H - 1) * W + min(max(x0, 0), W - LR))
+                                    : zero;
+#pragma unroll
+        for (int q = 0; q + 1 < LR; q += 2) {
+            const d2a8 a = *(gd2a8_t*)(p + q);
+            x[q] = a.x;
+            x[q + 1] = a.y;
+        }
+        if constexpr (LR & 1) x[LR - 1] = gload(p + LR - 1);
+#pragma unroll
+        for (int q = 0; q < LR; ++q) {
+            // full lanes all read the zero cell (one cache line per instruction)
+            const int xx = x0 + q;
+            const bool inb = !full & bv & ((unsigned)xx < (unsigned)W) & ((unsigned)y < (unsigned)H);
+            xe[q] = gload(inb ? grid + (unsigned)(y * W + xx) : zero);
+        }
+    };
+    // lanes 0..LR-1: fine pose (xo = lane, yo = wave); wave 0 lane LR: the coarse sum
+    const bool adder = lane < LR || (wave == 0 && lane == LR);
+    const int arow = lane < LR ? lane : LR + 1;
+    double acc = 0.0;
+    static_for_step<0, kSmallDepth, 1>([&](auto dd) {
+        constexpr int d = decltype(dd)::value;
+        gather(d, r[d], e[d], fl[d]);
+        __builtin_amdgcn_sched_barrier(0);
+        return true;
+    });
+    // coarse values of the edge beams (lattice start outside [0, W - LR] x
+    // [0, H - LR]) ahead of the chunk loop, which then holds no load under a
+    // branch; NaN marks an interior beam (its value comes from the row maxima)
+    double* cedge = bufs + (size_t)LR * WSTR;   // [Nv]
+    for (int v = tid; v < Nv; v += NT) {
+        const int2 ij = sidx[v];
+        const int bx = ij.x - pl.win_x, by = ij.y - pl.win_y;
+        const bool interior = (bx >= 0) & (by >= 0) & (bx <= W - LR) & (by <= H - LR);
+        cedge[v] = interior ? __builtin_nan("") : small_cval(grid, bx, by, W, H, LR);
+    }
+    __syncthreads();
+    static_for_step<0, kMaxChunks, 1>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if (c >= nchunk) return false;
+        double* cur = wb + (c & 1) * ROWB;
+        {
+            constexpr int d = c % kSmallDepth;
+            const bool f = fl[d];
+            double m = -INFINITY;
+#pragma unroll
+            for (int q = 0; q < LR; ++q) {
+                const double v = f ? r[d][q] : e[d][q];
+                cur[q * LD + lane] = v;
+                m = fmax(m, v);
+            }
+            cur[LR * LD + lane] = m;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // unconditional (lanes past Nv read the zero cell): gathers under a
+        // run-time branch make the compiler drain every load in flight
+        if constexpr (c + kSmallDepth < kMaxChunks)
+            gather(c + kSmallDepth, r[c % kSmallDepth], e[c % kSmallDepth], fl[c % kSmallDepth]);
+        __builtin_amdgcn_sched_barrier(0);
+        // every wave's rows of chunk c are in LDS (LDS-only release: the
+        // gathers in flight are not waited for)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        if (wave == 0) {
+            const int b = c * 64 + lane;
+            double cv = 0.0;
+            if (b < Nv) {
+                cv = cedge[b];
+                if (__builtin_isnan(cv)) {   // interior beam
+                    cv = bufs[(c & 1) * ROWB + LR * LD + lane];
+#pragma unroll
+                    for (int w = 1; w < LR; ++w) cv = fmax(cv, bufs[(size_t)w * WSTR + (c & 1) * ROWB + LR * LD + lane]);
+                }
+            }
+            cur[(LR + 1) * LD + lane] = cv;
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (adder) {
+            const double* row = cur + arow * LD;
+            const int cnt = min(64, Nv - c * 64);
+            double s = acc;
+            if (cnt == 64) {
+#pragma unroll 16
+                for (int b = 0; b < 64; ++b) s += row[b];
+            } else {
+                for (int b = 0; b < cnt; ++b) s += row[b];
+            }
+            acc = s;
+        }
+        return true;
+    });
+    if (lane < LR) s_f[lane * LR + wave] = acc;   // order index xo * LR + yo (x outer, y inner)
+    if (wave == 0 && lane == LR) s_c = acc;
+    __syncthreads();
+    if (wave != 0) return;
+    double fv = lane < LR * LR ? s_f[lane] : -INFINITY;
+    long long fk = lane < LR * LR ? lane : LLONG_MAX;
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(fv, off, 64);
+        const long long ok = __shfl_xor(fk, off, 64);
+        if (better(ov, ok, fv, fk)) {
+            fv = ov;
+            fk = ok;
+        }
+    }
+    typedef __attribute__((address_space(1))) double gdbl_t;
+    typedef __attribute__((address_space(1))) int gint_t;
+    if (lane == 0) {
+        ((gdbl_t*)it.cscore)[tt] = s_c;
+        ((gdbl_t*)it.fval)[tt] = fv;
+        ((gint_t*)it.fpos)[tt] = (int)fk;
+        __threadfence();   // release (device scope): the triple before the count
+        const unsigned old = atomicInc((unsigned*)it.keepc, (unsigned)(pl.T - 1));   // wraps to 0 after T
+        s_last = old == (unsigned)(pl.T - 1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    if (!s_last) return;
+    __threadfence();   // acquire: every angle's triple
+
+    // 3. the reference's walk over the angles
+    const double* cs = it.cscore;
+    const double* fvs = it.fval;
+    const int* fps = it.fpos;
+    const int T = pl.T;
+    double s = pl.thr;
+    int bt = -1, bpos = 0;
+    long long neval = 0;
+    for (int b0 = 0; b0 < T; b0 += 64) {
+        const int t = b0 + lane;
+        const bool in = t < T;
+        const double c = in ? __builtin_nontemporal_load(cs + t) : 0.0;
+        const double f = in ? __builtin_nontemporal_load(fvs + t) : 0.0;
+        const int p = in ? __builtin_nontemporal_load(fps + t) : 0;
+        for (int from = 0;;) {   // wave-uniform
+            const unsigned long long am = __ballot(in && lane >= from && !(c <= s) && f > s);
+            const int j = am ? __ffsll((long long)am) - 1 : 64;
+            // blocks from..j (j when accepted) are refined if !(score <= scoreMax) (:103-104)
+            neval += __popcll(__ballot(in && lane >= from && lane <= j && !(c <= s)));
+            if (!am) break;
+            s = __shfl(f, j, 64);
+            bt = b0 + j;
+            bpos = __shfl(p, j, 64);
+            from = j + 1;
+        }
+    }
+    if (lane != 0) return;
+    int bx = -pl.win_x, by = -pl.win_y, bth = -pl.win_t;
+    if (bt >= 0) {
+        bx = -pl.win_x + bpos / LR;
+        by = -pl.win_y + bpos % LR;
+        bth = bt - pl.win_t;
+    }
+    rec->status = 0;
+    rec->found = s > pl.thr;
+    rec->n_eval = neval;
+    rec->best[0] = bx;
+    rec->best[1] = by;
+    rec->best[2] = bth;
+    rec->score_max = s;
+    rec->L = -INFINITY;
+    rec->coarse_evals = (unsigned long long)pl.K;
+    // bestSensorPose (:122-125) and the central-difference poses (as k_replay)
+    const double x = pl.sx + bx * pl.step_x;
+    const double y = pl.sy + by * pl.step_y;
+    const double th = pl.st + bth * pl.step_t;
+    const double dl = pl.res, da = 1e-2;
+    const double P7[7][3] = {
+        { x, y, th },
+        { x + dl, y + 0.0, th + 0.0 }, { x - dl, y - 0.0, th - 0.0 },
+        { x + 0.0, y + dl, th + 0.0 }, { x - 0.0, y - dl, th - 0.0 },
+        { x + 0.0, y + 0.0, th + da }, { x - 0.0, y - 0.0, th - da },
+    };
+    for (int i = 0; i < 7; ++i)
+        for (int j = 0; j < 3; ++j) ((gdbl_t*)it.poses7)[3 * i + j] = P7[i][j];
+}
+
+// --------------------------------------------------------------------------
 // dense diagnostics: every fine score of the window (one lane per pose)
 // --------------------------------------------------------------------------
 __device__ __forceinline__ double fine_score(const RtcsmPlan& pl, const double* __restrict__ grid,
@@ -2925,6 +3275,7 @@ struct BatchShape {
     int unit8 = 2;          // its unit size in 8-byte words (3: 24-byte units for 6-9 rows)
     int nsby = 0;
     bool pruned = false;    // superblock pruning
+    bool small = false;     // k_match_small: one coarse block per angle, no coarse map (§4.1c)
     bool lr5 = false;       // transposed LR = 5 evaluators
     bool fine_lanes = false;   // k_compact + k_fine_lanes (lr * lr <= 64)
     bool fine_staged = false;  // ... as k_fine_regs (LowRes 5, every map W even, <= 8192, 16-byte aligned)
@@ -3244,6 +3595,55 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
     for (auto& it : items) {
         beams_T += (double)it.pl.T * it.pl.Nv;
         beams_K += (double)it.pl.K * it.pl.Nv;
+    }
+    if (B.small) {
+        // k_match_small (§4.1c): mode 0 projects, mode 1 reads the index rows
+        // the host fixed (a full host projection or k_patch's patches)
+        int mode = 0;
+        if (opt.host_idx) {
+            const MatchItem& it = items[0];
+            LGS_HIP_CHECK(hipMemcpyAsync(it.idx, opt.host_idx->data(), sizeof(int2) * opt.host_idx->size(),
+                                         hipMemcpyHostToDevice, st));
+            mode = 1;
+        } else if (opt.patches && !opt.patches->empty()) {
+            int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * opt.patches->size());
+            LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.patches->data(), sizeof(int4) * opt.patches->size(),
+                                         hipMemcpyHostToDevice, st));
+            const int np = (int)opt.patches->size();
+            hipLaunchKernelGGL(k_patch, dim3((np + 255) / 256), dim3(256), 0, st, d_items, dp, np);
+            LGS_HIP_CHECK(hipGetLastError());
+            mode = 1;
+        }
+        const int lr = B.low_res;
+        const int tok = ctx->timing_begin(K_MATCH_SMALL, 8.0 * (lr * lr) * beams_T);
+        const dim3 g((unsigned)B.Tmax, (unsigned)n);
+        const size_t nvp = (size_t)((std::max(B.NvMax, 1) + 1) & ~1);
+#define LGS_SMALL_CASE(L)                                                                                         \
+    case L:                                                                                                      \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_match_small<L>), g, dim3(64 * L),                                    \
+                           sizeof(int2) * nvp + sizeof(double) * small_buf_doubles<L>(), st, d_items, mode,       \
+                           ctx->guard_cap, ctx->guard_eps, inject, zero);                                        \
+        break;
+        if (!ctx->skipped(K_MATCH_SMALL)) switch (lr) {
+            LGS_SMALL_CASE(2) LGS_SMALL_CASE(3) LGS_SMALL_CASE(4) LGS_SMALL_CASE(5) LGS_SMALL_CASE(6)
+            LGS_SMALL_CASE(7) LGS_SMALL_CASE(8)
+            default: LGS_REQUIRE(false, "k_match_small: LowRes outside [2, 8]");
+            }
+#undef LGS_SMALL_CASE
+        ctx->timing_end(tok);
+        LGS_HIP_CHECK(hipGetLastError());
+        const double kk = (2.0 * B.kernel_size + 1) * (2.0 * B.kernel_size + 1);
+        double nbeams = 0.0;
+        for (auto& it : items) nbeams += it.cp.N;
+        const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * nbeams);
+        if (!ctx->skipped(K_COST))
+            hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, n), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
+                               ctx->guard_eps, inject, 0);
+        ctx->timing_end(tok_);
+        LGS_HIP_CHECK(hipGetLastError());
+        if (opt.cost_patches && !opt.cost_patches->empty())
+            enqueue_cost_patches(ctx, B, d_items, items, *opt.cost_patches);
+        return;
     }
     if (opt.host_idx) {
         // single item: the full host projection replaces k_project
@@ -3691,6 +4091,12 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
                         grids[j]->h <= 8192;
     B.kernel_size = cost->kernel_size;
     B.nsegMax = (int)(((long long)B.Tmax * B.P + kSelSeg - 1) / kSelSeg);
+    // one coarse block per angle: the whole search in one launch, straight
+    // from the fine map (no caller-supplied coarse map to honour)
+    B.small = ctx->small_window && !ctx->force_dense && p0.P == 1 && B.low_res >= 2 && B.low_res <= 8 &&
+              B.NvMax <= kSmallMaxNv && n <= kTedgeCtrs;
+    for (auto& s : sets) B.small = B.small && !s.coarse;
+    if (B.small) B.pruned = false;
     if (B.pruned && n >= ctx->lanes_min_batch && B.NvMax <= kListMaxNv && B.Tmax < (1 << 24) && B.nsb2 <= 64) {
         // the kept-superblock work list: counters | superblock entries | edge angles
         int region = 1;
@@ -3712,9 +4118,10 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
         LGS_HIP_CHECK(hipMemsetAsync(d_rec, 0xFF, sizeof(RtcsmRecord) * (size_t)n, ctx->stream));
     }
     int* tedge = ctx->tedge_buffer((size_t)n * B.Tmax);   // stamps only: no clearing per batch
+    int* sctr = B.small ? ctx->small_counters((size_t)n * B.Tmax) : nullptr;
     Upload up(ctx);
     scans_to_device(ctx, scans, n, &up);
-    const SetJobs sj = build_sets(ctx, p0, sets, B.pruned, up);
+    const SetJobs sj = B.small ? SetJobs{} : build_sets(ctx, p0, sets, B.pruned, up);
     std::vector<int> gens((size_t)n);
     for (int j = 0; j < n; ++j) {
         MatchItem& it = items[j];
@@ -3730,7 +4137,7 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
         it.pgen = s.pgen;
         it.gen = gens[j] = ctx->generation = ctx->next_stamp();
         it.rec = d_rec + j;
-        it.keepc = B.wl.cnt ? B.wl.cnt + 16 * j : nullptr;
+        it.keepc = B.wl.cnt ? B.wl.cnt + 16 * j : sctr ? sctr + j : nullptr;
         it.nparts = item_nparts(B, it.pl, B.pruned);
     }
     ctx->dbg.assign((size_t)n, lgs_ctx::DbgItem{});
@@ -3749,15 +4156,15 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
             d.buf[k] = b[k];
             d.bytes[k] = sz[k];
         }
-        d.buf[8] = ij.cmap;   // the item's coarse phase planes and superblock planes
-        d.bytes[8] = plane_bytes(q);
+        d.buf[8] = ij.cmap;   // the item's coarse phase planes and superblock planes (none: k_match_small)
+        d.bytes[8] = ij.cmap ? plane_bytes(q) : 0;
         d.buf[9] = ij.super;
         d.bytes[9] = ij.super ? super_bytes(q) : 0;
         d.gen = ij.gen;
     }
     const size_t items_off = up.append(items.data(), items.size());
     up.flush();
-    launch_sets(ctx, p0, sets, sj, up);
+    if (!B.small) launch_sets(ctx, p0, sets, sj, up);
     enqueue_items(ctx, B, up.at<MatchItem>(items_off), items, ScanOptions{});
     LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n, hipMemcpyDeviceToHost,
                                  ctx->stream));
@@ -3860,7 +4267,7 @@ void finish_matches(lgs_ctx* ctx, InFlight& F)
             B1.n = 1;
             B1.Tmax = items[j].pl.T;
             B1.nsegMax = items[j].nseg;
-            B1.pruned = pruned = uses_super(ctx, B.NvMax, B.nsb2, opt.dense);
+            B1.pruned = pruned = !B.small && uses_super(ctx, B.NvMax, B.nsb2, opt.dense);
             std::vector<MatchItem> one(1, items[j]);
             one[0].nparts = item_nparts(B1, one[0].pl, B1.pruned);
             const int g = one[0].gen = ctx->generation = ctx->next_stamp();

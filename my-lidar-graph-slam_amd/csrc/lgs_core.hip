@@ -162,13 +162,20 @@ void* lgs_ctx::ensure_pinned_up(size_t bytes)
 
 int* lgs_ctx::tedge_buffer(size_t n)
 {
+    // kTedgeCtrs wrap-around counters (k_match_small) ahead of the stamps:
+    // both are zero in their rest state, so one memset at allocation serves
     const int slot = banked(S_TEDGE);
-    int* p = (int*)ensure(slot, sizeof(int) * std::max<size_t>(n, 1));
+    int* p = (int*)ensure(slot, sizeof(int) * (kTedgeCtrs + std::max<size_t>(n, 1)));
     if (buf_bytes[slot] != tedge_zeroed[bank]) {
         LGS_HIP_CHECK(hipMemsetAsync(p, 0, buf_bytes[slot], stream));
         tedge_zeroed[bank] = buf_bytes[slot];
     }
-    return p;
+    return p + kTedgeCtrs;
+}
+
+int* lgs_ctx::small_counters(size_t n)
+{
+    return tedge_buffer(n) - kTedgeCtrs;
 }
 
 void* lgs_ctx::ensure_pinned_rec(size_t bytes)
@@ -181,7 +188,7 @@ const char* const kKernelNames[K_NUM_KERNELS] = { "k_project", "k_coarse", "k_se
                                                   "k_fine", "k_replay", "k_cost", "k_precompute",
                                                   "k_linsolve", "k_ray_emit", "k_ray_apply",
                                                   "k_super", "k_super_planes", "k_bb_score", "k_bb_expand",
-                                                  "k_coarse_aux" };
+                                                  "k_coarse_aux", "k_match_small" };
 }
 
 int lgs_ctx::next_stamp()
@@ -443,6 +450,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_PRUNE_MIN_SUPER: ctx->prune_min_super = (int)value; return LGS_OK;
     case LGS_OPT_COOP_TILES: ctx->coop_tiles = (long long)value; return LGS_OK;
     case LGS_OPT_FINE_STAGED: ctx->fine_staged = value != 0.0; return LGS_OK;
+    case LGS_OPT_SMALL_WINDOW: ctx->small_window = value != 0.0; return LGS_OK;
     case LGS_OPT_SORT_BARRIER_US:
         if (value < 0) return LGS_ERR_INVALID_ARG;
         ctx->sort_barrier_us = (long long)value;

@@ -91,6 +91,7 @@ enum Slot {
 };
 
 constexpr int kGuardInline = 64;
+constexpr int kTedgeCtrs = 64;   // k_match_small's per-item wrap-around counters (one per batch item)
 
 struct GuardRec { int t, v, ix, iy; };        // projection near a cell boundary
 struct CostGuardRec { int pose_which, beam, ix, iy; };
@@ -236,6 +237,7 @@ namespace lgs {
 enum KernelId { K_PROJECT = 0, K_COARSE, K_SEED, K_SELECT, K_FINE, K_REPLAY, K_COST, K_PRECOMPUTE,
                 K_LINSOLVE, K_RAY_EMIT, K_RAY_APPLY, K_SUPER, K_SUPER_PLANES, K_BB_SCORE, K_BB_EXPAND,
                 K_COARSE_AUX,   // k_keep + k_unsafe_list: the work-list passes around k_coarse_list
+                K_MATCH_SMALL,  // k_match_small: a small window's whole search (one coarse block per angle)
                 K_NUM_KERNELS };
 extern const char* const kKernelNames[K_NUM_KERNELS];
 struct PendingTiming {
@@ -270,6 +272,7 @@ struct lgs_ctx {
     long long handoff_fallbacks = 0;      // split refines rerun on one workgroup after a time-out
     bool peer_staged = false;    // cross-context copies through host memory (LGS_OPT_PEER_COPY)
     int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
+    bool small_window = true;    // one-launch search of one-block windows (LGS_OPT_SMALL_WINDOW)
     long long copies_direct = 0, copies_staged = 0;   // lgs_debug_copy_counters
     int lanes_min_batch = 2;     // pruned coarse stage: the work list (k_coarse_list) from this batch size on (LGS_OPT_LANES_MIN_BATCH)
     long long ray_chunk_keys = 1LL << 28;  // ray-cast keys per emit/sort/apply pass (LGS_OPT_RAY_CHUNK_KEYS)
@@ -307,6 +310,8 @@ struct lgs_ctx {
     size_t tedge_zeroed[2] = {}; // bytes of the S_TEDGE allocation already zeroed, per bank
                                  // (a reallocation always grows the slot)
     int* tedge_buffer(size_t n); // n flags, zeroed at allocation only
+    // the kTedgeCtrs counters in front of the same allocation (sized for n flags)
+    int* small_counters(size_t n);
     int banked(int slot) const
     {
         if (!bank) return slot;
