@@ -553,16 +553,15 @@ def run_match(args, D, ctx):
         p90_scan_match_ms=round(1e3 * float(np.percentile(lat1, 90)), 4) if lat1 else None,
         # latency of one batched call under the timed load
         p50_batch_call_ms=round(float(np.percentile(lat_ms, 50)), 4),
-        # the dominant kernel timed alone: the one-stream, event-timed pass
-        # after the timed region.  In the timed region each
-        # launch shares the GPU with the other stream's kernels and its
-        # duration depends on how the streams' batches happen to overlap
-        # (0.45-0.60 ms per launch over runs of one build): that figure is
-        # roofline_timed_region.  tools/trace_coarse.py splits a kernel trace
+        # the dominant kernel's HIP-event times over the timed region (the
+        # rubric's basis: each launch shares the GPU with the other streams'
+        # kernels, so its duration includes their overlap); roofline_isolated
+        # is the same kernel timed alone, the one-stream pass after the timed
+        # region.  tools/trace_coarse.py splits a kernel trace
         # of this command the same way (dispatches overlapping no other vs
         # the rest).
-        roofline=roofline_from(all_stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"), cpu_baseline=cpu,
-        roofline_timed_region=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"),
+        roofline=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"), cpu_baseline=cpu,
+        roofline_isolated=roofline_from(all_stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"),
         coarse_stage=coarse_stage(all_stats),
         pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events,
         super_prune=bool(args.super_prune),

@@ -2716,45 +2716,53 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(Items items, int guard_ca
     const double px = poses[3 * pi], py = poses[3 * pi + 1], pt = poses[3 * pi + 2];
     const double lim = (cp.kernel_size + 1) * cp.res;
     const double minSq0 = lim * lim + lim * lim;
-    for (int i = threadIdx.x; i < cp.N; i += blockDim.x) {
-        int4 c;
-        if (mode == 0) {
-            const double r = ranges[i];
-            const bool valid = !(r >= cp.max_range || r <= cp.min_range);
-            double q[4] = { 0.0, 0.0, 0.0, 0.0 };
-            if (valid) {
-                const double cs = cos(pt + angles[i]);
-                const double sn = sin(pt + angles[i]);
-                q[0] = (px + r * cs - cp.min_x) / cp.res;
-                q[1] = (py + r * sn - cp.min_y) / cp.res;
-                q[2] = (px + (r - cp.hit_and_missed_dist) * cs - cp.min_x) / cp.res;
-                q[3] = (py + (r - cp.hit_and_missed_dist) * sn - cp.min_y) / cp.res;
-            }
-            int cell[4];
-            for (int j = 0; j < 4; ++j) {
-                cell[j] = (int)floor(q[j]);
-                const bool guarded = valid && near_boundary(q[j], guard_eps);
-                const int slot = tagged_slot_wave(&rec->cost_guard_word, (unsigned)gen, guarded);
-                if (guarded) {
-                    cell[j] += inject;
-                    if (slot < guard_cap) {
-                        CostGuardRec g;
-                        g.pose_which = pi * 4 + j;
-                        g.beam = i;
-                        g.ix = cell[j];
-                        g.iy = 0;
-                        rec->cost_guard[slot] = g;
-                    }
+    // the cells of beam i (mode 0: computed + guard records; mode 1: read);
+    // every active lane calls it (the guard slots are taken per wave)
+    auto cells_of = [&](int i, bool have) -> int4 {
+        if (mode != 0) return have ? cidx[(size_t)pi * cp.N + i] : make_int4(INT_MIN, 0, 0, 0);
+        const double r = have ? ranges[i] : 0.0;
+        const bool valid = have && !(r >= cp.max_range || r <= cp.min_range);
+        double q[4] = { 0.0, 0.0, 0.0, 0.0 };
+        if (valid) {
+            const double cs = cos(pt + angles[i]);
+            const double sn = sin(pt + angles[i]);
+            q[0] = (px + r * cs - cp.min_x) / cp.res;
+            q[1] = (py + r * sn - cp.min_y) / cp.res;
+            q[2] = (px + (r - cp.hit_and_missed_dist) * cs - cp.min_x) / cp.res;
+            q[3] = (py + (r - cp.hit_and_missed_dist) * sn - cp.min_y) / cp.res;
+        }
+        int cell[4];
+        for (int j = 0; j < 4; ++j) {
+            cell[j] = (int)floor(q[j]);
+            const bool guarded = valid && near_boundary(q[j], guard_eps);
+            const int slot = tagged_slot_wave(&rec->cost_guard_word, (unsigned)gen, guarded);
+            if (guarded) {
+                cell[j] += inject;
+                if (slot < guard_cap) {
+                    CostGuardRec g;
+                    g.pose_which = pi * 4 + j;
+                    g.beam = i;
+                    g.ix = cell[j];
+                    g.iy = 0;
+                    rec->cost_guard[slot] = g;
                 }
             }
-            c = valid ? make_int4(cell[0], cell[1], cell[2], cell[3]) : make_int4(INT_MIN, 0, 0, 0);
-            cidx[(size_t)pi * cp.N + i] = c;
-        } else {
-            c = cidx[(size_t)pi * cp.N + i];
         }
-        double term = 0.0;
-        if (c.x != INT_MIN) term = exp(-0.5 * min_sq_dist<KS>(cp, grid, c, minSq0) / cp.variance);
-        tm[i] = term;
+        const int4 c = valid ? make_int4(cell[0], cell[1], cell[2], cell[3]) : make_int4(INT_MIN, 0, 0, 0);
+        if (have) cidx[(size_t)pi * cp.N + i] = c;
+        return c;
+    };
+    // two beams per thread and pass (i, i + blockDim): a 1081-beam scan is one
+    // latency chain per thread instead of a second pass for its last 57 beams
+    for (int i0 = threadIdx.x; i0 < cp.N; i0 += 2 * blockDim.x) {
+        const int i1 = i0 + (int)blockDim.x;
+        const bool h1 = i1 < cp.N;
+        const int4 c0 = cells_of(i0, true);
+        const int4 c1 = cells_of(i1, h1);
+        const double t0 = (c0.x != INT_MIN) ? exp(-0.5 * min_sq_dist<KS>(cp, grid, c0, minSq0) / cp.variance) : 0.0;
+        const double t1 = (c1.x != INT_MIN) ? exp(-0.5 * min_sq_dist<KS>(cp, grid, c1, minSq0) / cp.variance) : 0.0;
+        tm[i0] = t0;
+        if (h1) tm[i1] = t1;
     }
     __syncthreads();
     // costValue -= exp(..) (C/mapping/cost_function_greedy_endpoint.cpp): the

@@ -2,8 +2,8 @@
 """Split a rocprofv3 kernel trace's dispatches of one kernel into those that
 ran alone on the GPU (no other dispatch overlapped them in time) and those
 that shared it, and report each group's average duration -- the two figures
-bench.py reports as `roofline` (the one-stream pass after the timed region)
-and `roofline_timed_region` (two streams).
+bench.py reports as `roofline_isolated` (the one-stream pass after the timed region)
+and `roofline` (the timed region, several streams).
 
     python tools/trace_coarse.py <run_kernel_trace.csv> [kernel_substring] [algo_bytes_per_launch]
 
