@@ -2861,6 +2861,8 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
     __shared__ int s_last;
     typedef __attribute__((address_space(1))) unsigned long long gu64_t;
     gu64_t* __restrict__ gidx = (gu64_t*)(it.idx + (size_t)tt * Nv);
+    LGS_PROBE_DECL;
+    LGS_PROBE_MARK();
 
     // 1. the angle's scan indices
     if (mode == 0) {
@@ -2937,27 +2939,26 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
         __syncthreads();
     }
 
+    LGS_PROBE_MARK();
     // 2. fine rows + coarse values, beam order
     const int nchunk = (Nv + 63) / 64;
     const int xc = -pl.win_x, yr = -pl.win_y + wave;
     double* wb = bufs + (size_t)wave * WSTR;
-    // Every lane loads its row run with 16-byte loads from a clamped, always
-    // valid address into r; lanes whose run leaves the map load their cells
-    // one by one into separate registers e (the other lanes read the zero
-    // cell).  Branch-free on purpose: with the loads of either side under a
-    // branch the compiler waits for every older gather in flight (vmcnt(0))
-    // before each chunk's stores, which undoes the prefetch.
-    double r[kSmallDepth][LR], e[kSmallDepth][LR];
-    bool fl[kSmallDepth];
-    auto gather = [&](int c, double (&x)[LR], double (&xe)[LR], bool& full) {
+    // Every lane loads a row run of LR cells with 16-byte loads from the run's
+    // start clamped into the map (W >= LR: always a valid address); a run
+    // that leaves the map then holds every in-map cell the lane needs, at
+    // index k = x - xs, and the cells outside are 0 -- selected in registers
+    // at the store.  No load sits under a branch: the compiler keeps four
+    // chunks of gathers in flight (vmcnt(24..28)), where a branch drained them.
+    double r[kSmallDepth][LR];
+    int sh[kSmallDepth];   // x0 - xs, or LR (every cell masked: no beam, or a row outside the map)
+    auto gather = [&](int c, double (&x)[LR], int& shift) {
         const int b = c * 64 + lane;
         const int2 ij = sidx[max(min(b, Nv - 1), 0)];
-        const bool bv = b < Nv;
         const int x0 = ij.x + xc, y = ij.y + yr;
-        full = bv & ((unsigned)y < (unsigned)H) & (x0 >= 0) & (x0 + LR - 1 < W);
+        const int xs = min(max(x0, 0), W - LR);
         typedef const __attribute__((address_space(1))) d2a8 gd2a8_t;
-        const double* p = (W >= LR) ? grid + (unsigned)(min(max(y, 0), H - 1) * W + min(max(x0, 0), W - LR))
-                                    : zero;
+        const double* p = grid + (unsigned)(min(max(y, 0), H - 1) * W + xs);
 #pragma unroll
         for (int q = 0; q + 1 < LR; q += 2) {
             const d2a8 a = *(gd2a8_t*)(p + q);
@@ -2965,13 +2966,7 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
             x[q + 1] = a.y;
         }
         if constexpr (LR & 1) x[LR - 1] = gload(p + LR - 1);
-#pragma unroll
-        for (int q = 0; q < LR; ++q) {
-            // full lanes all read the zero cell (one cache line per instruction)
-            const int xx = x0 + q;
-            const bool inb = !full & bv & ((unsigned)xx < (unsigned)W) & ((unsigned)y < (unsigned)H);
-            xe[q] = gload(inb ? grid + (unsigned)(y * W + xx) : zero);
-        }
+        shift = ((b < Nv) & ((unsigned)y < (unsigned)H)) ? x0 - xs : LR;
     };
     // lanes 0..LR-1: fine pose (xo = lane, yo = wave); wave 0 lane LR: the coarse sum
     const bool adder = lane < LR || (wave == 0 && lane == LR);
@@ -2979,7 +2974,7 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
     double acc = 0.0;
     static_for_step<0, kSmallDepth, 1>([&](auto dd) {
         constexpr int d = decltype(dd)::value;
-        gather(d, r[d], e[d], fl[d]);
+        gather(d, r[d], sh[d]);
         __builtin_amdgcn_sched_barrier(0);
         return true;
     });
@@ -2994,17 +2989,21 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
         cedge[v] = interior ? __builtin_nan("") : small_cval(grid, bx, by, W, H, LR);
     }
     __syncthreads();
+    LGS_PROBE_MARK();
     static_for_step<0, kMaxChunks, 1>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
         if (c >= nchunk) return false;
         double* cur = wb + (c & 1) * ROWB;
         {
             constexpr int d = c % kSmallDepth;
-            const bool f = fl[d];
+            const int k0 = sh[d];
             double m = -INFINITY;
 #pragma unroll
             for (int q = 0; q < LR; ++q) {
-                const double v = f ? r[d][q] : e[d][q];
+                const int k = k0 + q;   // cell x0 + q in the run (in the map iff 0 <= k < LR)
+                double v = 0.0;
+#pragma unroll
+                for (int j = 0; j < LR; ++j) v = (k == j) ? r[d][j] : v;
                 cur[q * LD + lane] = v;
                 m = fmax(m, v);
             }
@@ -3013,8 +3012,7 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
         __builtin_amdgcn_sched_barrier(0);
         // unconditional (lanes past Nv read the zero cell): gathers under a
         // run-time branch make the compiler drain every load in flight
-        if constexpr (c + kSmallDepth < kMaxChunks)
-            gather(c + kSmallDepth, r[c % kSmallDepth], e[c % kSmallDepth], fl[c % kSmallDepth]);
+        if constexpr (c + kSmallDepth < kMaxChunks) gather(c + kSmallDepth, r[c % kSmallDepth], sh[c % kSmallDepth]);
         __builtin_amdgcn_sched_barrier(0);
         // every wave's rows of chunk c are in LDS (LDS-only release: the
         // gathers in flight are not waited for)
@@ -3049,6 +3047,7 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
         }
         return true;
     });
+    LGS_PROBE_MARK();
     if (lane < LR) s_f[lane * LR + wave] = acc;   // order index xo * LR + yo (x outer, y inner)
     if (wave == 0 && lane == LR) s_c = acc;
     __syncthreads();
@@ -3075,6 +3074,8 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    LGS_PROBE_MARK();
+    LGS_PROBE_PRINT("match_small(b0: project, edge pass, chunks, publish)");
     if (!s_last) return;
     __threadfence();   // acquire: every angle's triple
 
@@ -3133,6 +3134,19 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
     };
     for (int i = 0; i < 7; ++i)
         for (int j = 0; j < 3; ++j) ((gdbl_t*)it.poses7)[3 * i + j] = P7[i][j];
+}
+
+// --------------------------------------------------------------------------
+// k_post (LGS_OPT_POST_RECORDS): the batch's records straight into the pinned
+// (coherent) host copy, then the completion flag.  One wave: its system-scope
+// release orders its own record stores before the flag store.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_post(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16,
+                                             unsigned* flag, unsigned gen)
+{
+    for (int i = threadIdx.x; i < n16; i += 64) dst[i] = src[i];
+    __threadfence_system();
+    if (threadIdx.x == 0) *(volatile unsigned*)flag = gen;
 }
 
 // --------------------------------------------------------------------------
@@ -4042,6 +4056,9 @@ struct InFlight {
     RtcsmRecord* d_rec = nullptr;
     int n = 0, bank = 0;
     long long id = 0;   // timing batch
+    bool post = false;            // records written by k_post (LGS_OPT_POST_RECORDS)
+    unsigned* flag = nullptr;     // its completion flag in the pinned record buffer
+    unsigned post_gen = 0;
 };
 
 // The device part of a batch, on ctx->bank's buffers: every stage launched,
@@ -4103,6 +4120,7 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     // from the fine map (no caller-supplied coarse map to honour)
     B.small = ctx->small_window && !ctx->force_dense && p0.P == 1 && B.low_res >= 2 && B.low_res <= 8 &&
               B.NvMax <= kSmallMaxNv && n <= kTedgeCtrs;
+    for (int j = 0; j < n; ++j) B.small = B.small && grids[j]->w >= B.low_res && grids[j]->h >= 1;   // clamped runs
     for (auto& s : sets) B.small = B.small && !s.coarse;
     if (B.small) B.pruned = false;
     if (B.pruned && n >= ctx->lanes_min_batch && B.NvMax <= kListMaxNv && B.Tmax < (1 << 24) && B.nsb2 <= 64) {
@@ -4115,7 +4133,10 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     const ItemLayout L = item_layout(B.Tmax, B.NvMax, B.P, B.nsb2, B.chunks, B.cb, B.frows, Nmax);
     char* ws = (char*)ctx->ensure(ctx->banked(S_BATCH_WS), L.total * (size_t)n);
     RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(ctx->banked(S_RECORDS), sizeof(RtcsmRecord) * (size_t)n);
-    RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned_rec(sizeof(RtcsmRecord) * (size_t)n);
+    // the records' host copy, then (k_post) a completion flag
+    const size_t rec_bytes = sizeof(RtcsmRecord) * (size_t)n;
+    RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned_rec(align256(rec_bytes) + 256);
+    unsigned* h_flag = (unsigned*)((char*)h_rec + align256(rec_bytes));
     F.id = ++ctx->timing_batch;
     // The angle flags are only ever SET (k_project stamps an angle whose lattice
     // leaves the map low with the match's generation).  They live in a buffer
@@ -4174,8 +4195,18 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     up.flush();
     if (!B.small) launch_sets(ctx, p0, sets, sj, up);
     enqueue_items(ctx, B, up.at<MatchItem>(items_off), items, ScanOptions{});
-    LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n, hipMemcpyDeviceToHost,
-                                 ctx->stream));
+    F.post = ctx->post_records;
+    if (F.post) {
+        static_assert(sizeof(RtcsmRecord) % 16 == 0, "k_post copies 16-byte words");
+        F.flag = h_flag;
+        F.post_gen = (unsigned)ctx->next_stamp();
+        *(volatile unsigned*)h_flag = 0u;   // before the launch: k_post's store comes after it
+        hipLaunchKernelGGL(k_post, dim3(1), dim3(64), 0, ctx->stream, (const uint4*)d_rec, (uint4*)h_rec,
+                           (int)(rec_bytes / 16), h_flag, F.post_gen);
+        LGS_HIP_CHECK(hipGetLastError());
+    } else {
+        LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, rec_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    }
     hipEvent_t& ev = ctx->bank_ev[ctx->bank];
     if (!ev) LGS_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     LGS_HIP_CHECK(hipEventRecord(ev, ctx->stream));
@@ -4198,7 +4229,20 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
 void finish_matches(lgs_ctx* ctx, InFlight& F)
 {
     ctx->bank = F.bank;
-    ctx->wait_event(ctx->bank_ev[F.bank]);
+    if (F.post) {
+        // spin on the flag k_post writes last; the stream's event (recorded
+        // after it) tells a fault or a lost flag apart from work in flight
+        volatile unsigned* f = F.flag;
+        for (unsigned spins = 1; *f != F.post_gen; ++spins) {
+            if (spins % 4096) continue;
+            const hipError_t e = hipEventQuery(ctx->bank_ev[F.bank]);
+            if (e == hipSuccess && *f != F.post_gen) throw Error(LGS_ERR_INTERNAL, "k_post: completion flag lost");
+            if (e != hipSuccess && e != hipErrorNotReady) LGS_HIP_CHECK(e);
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    } else {
+        ctx->wait_event(ctx->bank_ev[F.bank]);
+    }
     std::vector<MatchItem>& items = F.items;
     const BatchShape& B = F.B;
     const std::vector<int>& gens = F.gens;

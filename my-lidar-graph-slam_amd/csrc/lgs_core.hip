@@ -180,7 +180,8 @@ int* lgs_ctx::small_counters(size_t n)
 
 void* lgs_ctx::ensure_pinned_rec(size_t bytes)
 {
-    return grow_pinned(stream, pinned_rec[bank], pinned_rec_bytes[bank], bytes, false);
+    // coherent: k_post writes the records (and their flag) here directly
+    return grow_pinned(stream, pinned_rec[bank], pinned_rec_bytes[bank], bytes, true);
 }
 
 namespace lgs {
@@ -451,6 +452,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_COOP_TILES: ctx->coop_tiles = (long long)value; return LGS_OK;
     case LGS_OPT_FINE_STAGED: ctx->fine_staged = value != 0.0; return LGS_OK;
     case LGS_OPT_SMALL_WINDOW: ctx->small_window = value != 0.0; return LGS_OK;
+    case LGS_OPT_POST_RECORDS: ctx->post_records = value != 0.0; return LGS_OK;
     case LGS_OPT_SORT_BARRIER_US:
         if (value < 0) return LGS_ERR_INVALID_ARG;
         ctx->sort_barrier_us = (long long)value;
