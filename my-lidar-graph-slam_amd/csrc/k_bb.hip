@@ -52,6 +52,7 @@ void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params
 namespace {
 
 constexpr int kBBMaxH = 12;   // NodeHeightMax limit (window 4096 cells)
+constexpr int kBBBatch = 512; // matches per run_bb (one k_bb_score launch per level for all of them)
 
 // One match of a batched branch-and-bound launch (device memory).
 struct BBItem {
@@ -164,10 +165,14 @@ __global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ ite
     scores[i] = sum;
 }
 
+// child[i] = the index of node i's first child in the next level's list (its
+// four children are consecutive there), -1 when not expanded (k_bb_replay);
+// ncount[item] += 4 per expanded node (nodes scored per match)
 __global__ __launch_bounds__(256) void k_bb_expand(const BBItem* __restrict__ items, const int4* __restrict__ nodes,
                                                    const double* __restrict__ scores, int n,
                                                    int4* __restrict__ next, int* __restrict__ count, int cap,
-                                                   int* __restrict__ overflow)
+                                                   int* __restrict__ overflow, int* __restrict__ child,
+                                                   unsigned long long* __restrict__ ncount)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     bool ex = false;
@@ -183,18 +188,27 @@ __global__ __launch_bounds__(256) void k_bb_expand(const BBItem* __restrict__ it
         }
     }
     const unsigned long long bal = __ballot(ex);
-    if (bal == 0ull) return;
+    if (bal == 0ull) {
+        if (i < n) child[i] = -1;
+        return;
+    }
     const int lane = threadIdx.x & 63;
     const int leader = __ffsll((long long)bal) - 1;
     int base = 0;
     if (lane == leader) base = atomicAdd(count, 4 * __popcll(bal));
     base = __shfl(base, leader, 64);
-    if (!ex) return;
+    if (!ex) {
+        if (i < n) child[i] = -1;
+        return;
+    }
     const int pos = base + 4 * __popcll(bal & ((1ull << lane) - 1ull));
     if (pos + 4 > cap) {
         *overflow = 1;
+        child[i] = -1;
         return;
     }
+    child[i] = pos;
+    atomicAdd(ncount + node_item(nd), 4ull);
     // :123-135: children (x, y), (x + ws, y), (x, y + ws), (x + ws, y + ws)
     const int h = node_level(nd) - 1, ws = 1 << h;
     const int head = (node_item(nd) << 4) | h;
@@ -208,7 +222,7 @@ __global__ __launch_bounds__(256) void k_bb_expand(const BBItem* __restrict__ it
 // cells[k * Nmax + v] for valid beam v; lanes load, lane 0 adds in beam order.
 __global__ __launch_bounds__(64) void k_bb_rescore(const double* const* __restrict__ maps, const int* __restrict__ dims,
                                                    const int2* __restrict__ cells, const int* __restrict__ nv,
-                                                   int Nmax, double* __restrict__ out)
+                                                   int Nmax, double* const* __restrict__ out)
 {
     __shared__ double buf[64];
     const int k = blockIdx.x;
@@ -231,7 +245,119 @@ __global__ __launch_bounds__(64) void k_bb_rescore(const double* const* __restri
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[k] = sum;
+    if (threadIdx.x == 0) *out[k] = sum;   // the node's slot in its level's score list
+}
+
+// The guarded nodes' coordinates (node lists stay on the device).
+__global__ __launch_bounds__(256) void k_bb_guard_nodes(const int4* const* __restrict__ lists,
+                                                       const BBGuard* __restrict__ guards, int ng,
+                                                       int4* __restrict__ out)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ng) return;
+    out[k] = lists[guards[k].level][guards[k].node];
+}
+
+// The reference's search (:81-140) over the scored levels, one thread per
+// match: the LIFO order walked with a cursor per level instead of a stack of
+// nodes (the top nodes, pushed in (x, y, t) order, pop last first; an
+// expanded node's four children are consecutive in the next level's list and
+// pop 3, 2, 1, 0).  Expanding a node loads its four children's scores and
+// child indices at once into LDS, so a visit costs no memory round trip of
+// its own.  A node the search expands that the device did not expand (child
+// index -1) can only follow a guard-corrected path score: the match fails and
+// is rerun over the thr0 superset (as the host replay did).
+struct BBReplay {
+    const double* scores[kBBMaxH + 1];   // per level id l = Hm - h
+    const int* child[kBBMaxH + 1];
+    const int4* leaves;                  // level Hm's node list (h = 0)
+    int hm;
+};
+struct BBResult {
+    double score;
+    int x, y, t, failed;
+    long long visited;
+};
+__global__ __launch_bounds__(64) void k_bb_replay(BBReplay R, const int* __restrict__ top_off,
+                                                  const double* __restrict__ thr0, int n, BBResult* __restrict__ out)
+{
+    __shared__ double s_sc[kBBMaxH + 1][4][64];   // the group of four being walked at each level
+    __shared__ int s_cb[kBBMaxH + 1][4][64];
+    __shared__ int s_base[kBBMaxH + 1][64];
+    __shared__ int s_k[kBBMaxH + 1][64];          // next child of the group to visit (3 .. 0)
+    const int lane = threadIdx.x;
+    const int j = blockIdx.x * 64 + lane;
+    if (j >= n) return;
+    const int hm = R.hm;
+    const int t0 = top_off[j], t1 = top_off[j + 1];
+    double smax = thr0[j];
+    int leaf = -1, failed = 0;
+    long long visited = 0;
+    double ns = 0.0;
+    int ncb = -1;
+    if (t1 > t0) {
+        ns = R.scores[0][t1 - 1];
+        ncb = hm > 0 ? R.child[0][t1 - 1] : -1;
+    }
+    for (int top = t1 - 1; top >= t0 && !failed; --top) {
+        double s = ns;
+        int cb = ncb, idx = top;
+        if (top > t0) {   // the next top node's entries, ahead of this one's subtree
+            ns = R.scores[0][top - 1];
+            ncb = hm > 0 ? R.child[0][top - 1] : -1;
+        }
+        int l = 0;
+        for (;;) {
+            ++visited;
+            if (s > smax) {   // else pruned: score <= scoreMax (:105-109)
+                if (l == hm) {   // leaf (:112-119)
+                    smax = s;
+                    leaf = idx;
+                } else if (cb < 0) {
+                    failed = 1;
+                    break;
+                } else {   // expand (:120-137)
+                    ++l;
+                    double c[4];
+                    int g[4] = { 0, 0, 0, 0 };
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        c[q] = R.scores[l][cb + q];
+                        if (l < hm) g[q] = R.child[l][cb + q];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        s_sc[l][q][lane] = c[q];
+                        s_cb[l][q][lane] = g[q];
+                    }
+                    s_base[l][lane] = cb;
+                    s_k[l][lane] = 3;
+                    s = c[3];
+                    idx = cb + 3;
+                    cb = g[3];
+                    continue;
+                }
+            }
+            while (l > 0 && s_k[l][lane] == 0) --l;   // the group is done: back up
+            if (l == 0) break;
+            const int q = --s_k[l][lane];
+            s = s_sc[l][q][lane];
+            cb = s_cb[l][q][lane];
+            idx = s_base[l][lane] + q;
+        }
+    }
+    BBResult r;
+    r.score = smax;
+    r.failed = failed;
+    r.visited = visited;
+    r.x = r.y = r.t = 0;
+    if (leaf >= 0) {
+        const int4 nd = R.leaves[leaf];
+        r.x = nd.y;
+        r.y = nd.z;
+        r.t = nd.w;
+    }
+    out[j] = r;
 }
 
 // ------------------------------------------------------------------ host
@@ -258,59 +384,6 @@ struct BBHost {   // host plan of one match
     double thr0;
     std::vector<int> vidx;
     std::vector<int> top_x, top_y;
-};
-
-inline uint64_t node_key(int h, int x, int y, int t)
-{
-    return ((uint64_t)(unsigned)h << 60) | ((uint64_t)((unsigned)(x + (1 << 19)) & 0xFFFFFu) << 40) |
-           ((uint64_t)((unsigned)(y + (1 << 19)) & 0xFFFFFu) << 20) | (uint64_t)((unsigned)(t + (1 << 19)) & 0xFFFFFu);
-}
-
-// Node -> score table of one candidate for the host replay: open addressing
-// (linear probing) over a power-of-two array, reused by the worker thread
-// across candidates and calls (an std::unordered_map per candidate allocated
-// one node per entry: the replay's cost swung with the host's allocator load).
-struct NodeTable {
-    std::vector<uint64_t> keys;   // key + 1 (0 = empty)
-    std::vector<double> vals;
-    uint64_t mask = 0;
-    void reset(size_t n)
-    {
-        size_t cap = 16;
-        while (cap < 2 * n + 16) cap <<= 1;
-        if (keys.size() < cap) {
-            keys.assign(cap, 0);
-            vals.resize(cap);
-        } else {
-            cap = keys.size();
-            std::fill(keys.begin(), keys.end(), 0);
-        }
-        mask = cap - 1;
-    }
-    static uint64_t mix(uint64_t k)
-    {
-        k ^= k >> 31;
-        k *= 0x9E3779B97F4A7C15ull;
-        return k ^ (k >> 29);
-    }
-    void put(uint64_t key, double v)
-    {
-        for (uint64_t i = mix(key) & mask;; i = (i + 1) & mask)
-            if (keys[i] == 0 || keys[i] == key + 1) {   // first entry wins (as emplace)
-                if (keys[i] == 0) {
-                    keys[i] = key + 1;
-                    vals[i] = v;
-                }
-                return;
-            }
-    }
-    const double* find(uint64_t key) const
-    {
-        for (uint64_t i = mix(key) & mask;; i = (i + 1) & mask) {
-            if (keys[i] == key + 1) return &vals[i];
-            if (keys[i] == 0) return nullptr;
-        }
-    }
 };
 
 BBHost make_bb_plan(const lgs_grid* grid, const lgs_bb_params* p, const lgs_scan* scan, lgs_pose2d init,
@@ -364,9 +437,8 @@ void host_bb_cell(const BBHost& b, const lgs_grid* g, const lgs_scan* scan, int 
 struct BBLevel {
     int4* d_nodes = nullptr;
     double* d_scores = nullptr;
+    int* d_child = nullptr;   // first-child index per node (k_bb_expand), -1 = not expanded
     int n = 0;
-    std::vector<int4> nodes;
-    std::vector<double> scores;
 };
 
 // Run n branch-and-bound matches: grids[j] (fine map, its geometry) and
@@ -446,8 +518,11 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
             LGS_HIP_CHECK(hipMemcpyAsync(d_vidx[j], plans[j].vidx.data(), sizeof(int) * plans[j].vidx.size(),
                                          hipMemcpyHostToDevice, ctx->stream));
     // guards (shared by every level of the batch)
-    int* d_counts = (int*)ctx->ensure(S_BB3, 256);   // [0] guards, [1] children, [2] overflow
-    BBGuard* d_guards = (BBGuard*)ctx->ensure(S_BB4, sizeof(BBGuard) * (size_t)ctx->guard_cap);
+    // [0] guards, [1] children, [2] overflow; from byte 256 the per-match scored-node counters
+    int* d_counts = (int*)ctx->ensure(S_BB3, 256 + sizeof(unsigned long long) * (size_t)n);
+    // guard records: guard_cap per 64 matches (the batch grew from 64 to kBBBatch matches)
+    const int gcap = ctx->guard_cap * std::max(1, (n + 63) / 64);
+    BBGuard* d_guards = (BBGuard*)ctx->ensure(S_BB4, sizeof(BBGuard) * (size_t)std::max(gcap, 1));
     LGS_HIP_CHECK(hipMemsetAsync(d_counts, 0, 256, ctx->stream));
 
     // pass 1: trig tables and the first descent of every match
@@ -471,7 +546,7 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         LGS_HIP_CHECK(hipGetLastError());
         const int np = (int)path.size();
         hipLaunchKernelGGL(k_bb_score, dim3((np + 255) / 256), dim3(256), 0, ctx->stream, d_items,
-                           up.at<int4>(poff), np, -1, d_pscores, d_guards, d_counts, ctx->guard_cap, ctx->guard_eps,
+                           up.at<int4>(poff), np, -1, d_pscores, d_guards, d_counts, gcap, ctx->guard_eps,
                            ctx->inject_index ? 1 : 0);
         LGS_HIP_CHECK(hipGetLastError());
         LGS_HIP_CHECK(hipMemcpyAsync(pscores.data(), d_pscores, sizeof(double) * np, hipMemcpyDeviceToHost,
@@ -491,6 +566,7 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
 
     // pass 2: level by level, every node the search can visit
     std::vector<BBLevel> levels((size_t)Hm + 1);   // index = Hm - h
+    unsigned long long* d_ncount = nullptr;
     {
         std::vector<int4> top;
         for (int j = 0; j < n; ++j)
@@ -503,6 +579,9 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         const size_t toff = up.append(top.data(), top.size());
         up.flush();
         const BBItem* d_items = up.at<BBItem>(ioff);
+        // scored nodes per match: its top nodes + 4 per expanded node (k_bb_expand)
+        d_ncount = (unsigned long long*)((char*)d_counts + 256);
+        LGS_HIP_CHECK(hipMemsetAsync(d_ncount, 0, sizeof(unsigned long long) * (size_t)n, ctx->stream));
         // node/score buffers per level: grown by the host between levels
         int cur_n = (int)top.size();
         int4* cur_nodes = (int4*)ctx->ensure(S_BB1, sizeof(int4) * (size_t)cur_n);
@@ -520,7 +599,7 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
                 for (int j = 0; j < n; ++j) lookups += (double)plans[j].Nv;
                 const int tok = ctx->timing_begin(K_BB_SCORE, 8.0 * lookups / n * cur_n);
                 hipLaunchKernelGGL(k_bb_score, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items,
-                                   cur_nodes, cur_n, Hm - h, L.d_scores, d_guards, d_counts, ctx->guard_cap,
+                                   cur_nodes, cur_n, Hm - h, L.d_scores, d_guards, d_counts, gcap,
                                    ctx->guard_eps, ctx->inject_index ? 1 : 0);
                 ctx->timing_end(tok);
                 LGS_HIP_CHECK(hipGetLastError());
@@ -528,11 +607,13 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
             if (h == 0 || cur_n == 0) break;
             const int cap = 4 * cur_n;
             int4* next = (int4*)ctx->ensure_aux(2 * (Hm - h) + 1, sizeof(int4) * (size_t)cap);
+            L.d_child = (int*)ctx->ensure_aux(2 * (kBBMaxH + 1) + (Hm - h), sizeof(int) * (size_t)cur_n);
             LGS_HIP_CHECK(hipMemsetAsync(d_counts + 1, 0, 2 * sizeof(int), ctx->stream));
             {
                 const int tok = ctx->timing_begin(K_BB_EXPAND, 0.0);
                 hipLaunchKernelGGL(k_bb_expand, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items,
-                                   cur_nodes, L.d_scores, cur_n, next, d_counts + 1, cap, d_counts + 2);
+                                   cur_nodes, L.d_scores, cur_n, next, d_counts + 1, cap, d_counts + 2, L.d_child,
+                                   d_ncount);
                 ctx->timing_end(tok);
                 LGS_HIP_CHECK(hipGetLastError());
             }
@@ -543,60 +624,79 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
             cur_n = cnt[0];
             cur_nodes = next;
         }
-        // host copies of every level
-        for (auto& L : levels) {
-            L.nodes.resize((size_t)L.n);
-            L.scores.resize((size_t)L.n);
-            if (L.n == 0) continue;
-            LGS_HIP_CHECK(hipMemcpyAsync(L.nodes.data(), L.d_nodes, sizeof(int4) * (size_t)L.n, hipMemcpyDeviceToHost,
-                                         ctx->stream));
-            LGS_HIP_CHECK(hipMemcpyAsync(L.scores.data(), L.d_scores, sizeof(double) * (size_t)L.n,
-                                         hipMemcpyDeviceToHost, ctx->stream));
-        }
         int ng = 0;
         LGS_HIP_CHECK(hipMemcpyAsync(&ng, d_counts, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
         ctx->sync();
-        std::vector<BBGuard> guards((size_t)std::min(ng, ctx->guard_cap));
-        if (!guards.empty())
-            LGS_HIP_CHECK(hipMemcpy(guards.data(), d_guards, sizeof(BBGuard) * guards.size(), hipMemcpyDeviceToHost));
-        for (auto& L : levels) L.d_nodes = nullptr, L.d_scores = nullptr;
         if (ctx->profile) ctx->harvest();
-
+        const int ngc = std::min(ng, gcap);
+        std::vector<BBGuard> guards((size_t)ngc);
+        std::vector<int4> gnodes((size_t)ngc);
+        if (ngc > 0) {
+            // the guarded nodes' coordinates, gathered on the device
+            std::vector<const int4*> lists((size_t)Hm + 1, nullptr);
+            for (int l = 0; l <= Hm; ++l) lists[(size_t)l] = levels[(size_t)l].d_nodes;
+            Upload ug(ctx);
+            const size_t lo = ug.append(lists.data(), lists.size());
+            ug.flush();
+            int4* d_gn = (int4*)ctx->ensure(S_BB5, sizeof(int4) * (size_t)ngc);
+            hipLaunchKernelGGL(k_bb_guard_nodes, dim3((ngc + 255) / 256), dim3(256), 0, ctx->stream,
+                               ug.at<const int4*>(lo), d_guards, ngc, d_gn);
+            LGS_HIP_CHECK(hipGetLastError());
+            LGS_HIP_CHECK(hipMemcpyAsync(guards.data(), d_guards, sizeof(BBGuard) * guards.size(),
+                                         hipMemcpyDeviceToHost, ctx->stream));
+            LGS_HIP_CHECK(hipMemcpyAsync(gnodes.data(), d_gn, sizeof(int4) * gnodes.size(), hipMemcpyDeviceToHost,
+                                         ctx->stream));
+            ctx->sync();
+        }
         // guarded cells: exact glibc cells; nodes with any differing cell are
-        // re-scored from host cells (or, past guard_cap records, every node
-        // of the batch is re-checked on the host)
+        // re-scored from host cells in place (past guard_cap records every
+        // node of the batch is re-scored: the node lists then come back once)
         std::vector<std::pair<int, int>> dirty;   // (level id, node index)
-        if (ng > ctx->guard_cap) {
-            for (int l = 0; l <= Hm; ++l)
-                for (int i = 0; i < levels[(size_t)l].n; ++i) dirty.push_back({ l, i });
+        std::vector<int4> dnodes;
+        if (ng > gcap) {
+            for (int l = 0; l <= Hm; ++l) {
+                const BBLevel& L = levels[(size_t)l];
+                std::vector<int4> all((size_t)L.n);
+                if (L.n)
+                    LGS_HIP_CHECK(hipMemcpy(all.data(), L.d_nodes, sizeof(int4) * (size_t)L.n, hipMemcpyDeviceToHost));
+                for (int i = 0; i < L.n; ++i) {
+                    dirty.push_back({ l, i });
+                    dnodes.push_back(all[(size_t)i]);
+                }
+            }
         } else {
-            for (const BBGuard& g : guards) {
-                const int4 nd = levels[(size_t)g.level].nodes[(size_t)g.node];
+            std::vector<std::pair<std::pair<int, int>, int4>> dl;
+            for (int k = 0; k < ngc; ++k) {
+                const BBGuard& g = guards[(size_t)k];
+                const int4 nd = gnodes[(size_t)k];
                 const int j = nd.x >> 4;
                 int ix, iy;
                 host_bb_cell(plans[j], grids[j], scans[j], nd.y, nd.z, nd.w, g.v, ix, iy);
-                if (ix != g.ix || iy != g.iy) dirty.push_back({ g.level, g.node });
+                if (ix != g.ix || iy != g.iy) dl.push_back({ { g.level, g.node }, nd });
             }
-            std::sort(dirty.begin(), dirty.end());
-            dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+            std::sort(dl.begin(), dl.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+            for (size_t k = 0; k < dl.size(); ++k)
+                if (k == 0 || dl[k].first != dl[k - 1].first) {
+                    dirty.push_back(dl[k].first);
+                    dnodes.push_back(dl[k].second);
+                }
         }
         for (int j = 0; j < n; ++j) out[j].guard_hits = 0;
-        for (const BBGuard& g : guards) {
-            const int4 nd = levels[(size_t)g.level].nodes[(size_t)g.node];
-            out[nd.x >> 4].guard_hits += 1;
-        }
+        for (int k = 0; k < ngc; ++k) out[gnodes[(size_t)k].x >> 4].guard_hits += 1;
         if (!dirty.empty()) {
             const int nd_n = (int)dirty.size();
             std::vector<int2> cells((size_t)nd_n * NvMax);
             std::vector<int> nvs((size_t)nd_n), dims((size_t)2 * nd_n);
             std::vector<const double*> maps((size_t)nd_n);
+            std::vector<double*> slots((size_t)nd_n);
             for (int k = 0; k < nd_n; ++k) {
-                const int4 nd = levels[(size_t)dirty[k].first].nodes[(size_t)dirty[k].second];
+                const int4 nd = dnodes[(size_t)k];
                 const int j = nd.x >> 4, h = nd.x & 15;
                 nvs[k] = plans[j].Nv;
                 dims[2 * k] = grids[j]->w;
                 dims[2 * k + 1] = grids[j]->h;
                 maps[k] = pyr[j][h];
+                slots[k] = levels[(size_t)dirty[k].first].d_scores + dirty[k].second;
                 for (int v = 0; v < plans[j].Nv; ++v) {
                     int ix, iy;
                     host_bb_cell(plans[j], grids[j], scans[j], nd.y, nd.z, nd.w, v, ix, iy);
@@ -609,84 +709,73 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
             const size_t no = u2.append(nvs.data(), nvs.size());
             const size_t dof = u2.append(dims.data(), dims.size());
             const size_t mo = u2.append(maps.data(), maps.size());
+            const size_t so = u2.append(slots.data(), slots.size());
             u2.flush();
-            double* d_out = (double*)ctx->ensure(S_BB5, sizeof(double) * (size_t)nd_n);
             hipLaunchKernelGGL(k_bb_rescore, dim3(nd_n), dim3(64), 0, ctx->stream, u2.at<const double*>(mo),
-                               u2.at<int>(dof), u2.at<int2>(co), u2.at<int>(no), NvMax, d_out);
+                               u2.at<int>(dof), u2.at<int2>(co), u2.at<int>(no), NvMax, u2.at<double*>(so));
             LGS_HIP_CHECK(hipGetLastError());
-            std::vector<double> rs((size_t)nd_n);
-            LGS_HIP_CHECK(hipMemcpyAsync(rs.data(), d_out, sizeof(double) * (size_t)nd_n, hipMemcpyDeviceToHost,
-                                         ctx->stream));
-            ctx->sync();
-            for (int k = 0; k < nd_n; ++k) levels[(size_t)dirty[k].first].scores[(size_t)dirty[k].second] = rs[k];
         }
     }
 
     lap(1);
-    // host replay of the reference's search (:81-140) over the scored nodes
-    // (candidates are independent: their tables and searches run on a few
-    // host threads; each thread owns whole candidates)
-    std::vector<std::vector<std::pair<int, int>>> bucket((size_t)n);   // (level id, node index)
-    for (int l = 0; l <= Hm; ++l) {
-        const BBLevel& L = levels[(size_t)l];
-        for (int i = 0; i < L.n; ++i) bucket[(size_t)(L.nodes[(size_t)i].x >> 4)].push_back({ l, i });
+    // the reference's search (:81-140) over the scored levels on the device
+    // (k_bb_replay, one thread per match)
+    std::vector<int> top_off((size_t)n + 1, 0);
+    std::vector<double> thr0((size_t)n);
+    for (int j = 0; j < n; ++j) {
+        const BBHost& b = plans[j];
+        top_off[(size_t)j + 1] = top_off[(size_t)j] + (int)(b.top_x.size() * b.top_y.size()) * b.T;
+        thr0[(size_t)j] = b.thr0;
     }
-    std::vector<int64_t> scored((size_t)n, 0);
-    for (int j = 0; j < n; ++j) scored[(size_t)j] = (int64_t)bucket[(size_t)j].size();
+    BBReplay R;
+    std::memset(&R, 0, sizeof(R));
+    R.hm = Hm;
+    for (int l = 0; l <= Hm; ++l) {
+        R.scores[l] = levels[(size_t)l].d_scores;
+        R.child[l] = levels[(size_t)l].d_child;
+    }
+    R.leaves = levels[(size_t)Hm].d_nodes;
+    std::vector<BBResult> res((size_t)n);
+    std::vector<unsigned long long> ncount((size_t)n);
+    {
+        Upload ur(ctx);
+        const size_t to = ur.append(top_off.data(), top_off.size());
+        const size_t ho = ur.append(thr0.data(), thr0.size());
+        ur.flush();
+        BBResult* d_res = (BBResult*)ctx->ensure(S_BB5, sizeof(BBResult) * (size_t)n);
+        hipLaunchKernelGGL(k_bb_replay, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, R, ur.at<int>(to),
+                           ur.at<double>(ho), n, d_res);
+        LGS_HIP_CHECK(hipGetLastError());
+        LGS_HIP_CHECK(hipMemcpyAsync(res.data(), d_res, sizeof(BBResult) * (size_t)n, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+        LGS_HIP_CHECK(hipMemcpyAsync(ncount.data(), d_ncount, sizeof(unsigned long long) * (size_t)n,
+                                     hipMemcpyDeviceToHost, ctx->stream));
+        ctx->sync();
+    }
+    for (auto& L : levels) L.d_nodes = nullptr, L.d_scores = nullptr, L.d_child = nullptr;
     std::vector<lgs_pose2d> best((size_t)n);
     std::vector<char> failed((size_t)n, 0);
-    struct SNode { int x, y, t, h; };
-    auto replay = [&](int j) {
-        static thread_local NodeTable tab;
-        static thread_local std::vector<SNode> st;
-        tab.reset(bucket[(size_t)j].size());
-        for (const auto& li : bucket[(size_t)j]) {
-            const int4 nd = levels[(size_t)li.first].nodes[(size_t)li.second];
-            tab.put(node_key(nd.x & 15, nd.y, nd.z, nd.w), levels[(size_t)li.first].scores[(size_t)li.second]);
-        }
+    for (int j = 0; j < n; ++j) {
         const BBHost& b = plans[j];
-        double scoreMax = b.thr0;
-        lgs_pose2d bestPose = b.sensor;
-        int bx = 0, by = 0, bt = 0;
-        int64_t visited = 0;
-        st.clear();
-        for (int x : b.top_x)
-            for (int y : b.top_y)
-                for (int t = -b.win_t; t <= b.win_t; ++t) st.push_back({ x, y, t, Hm });
-        while (!st.empty()) {
-            const SNode cur = st.back();
-            st.pop_back();
-            const double* f = tab.find(node_key(cur.h, cur.x, cur.y, cur.t));
-            if (!f) {
-                failed[(size_t)j] = no_path ? 2 : 1;   // 1: rerun with the thr0 superset
-                break;
-            }
-            const double score = *f;
-            ++visited;
-            if (score <= scoreMax) continue;   // :105-109
-            if (cur.h == 0) {                  // :112-119
-                bestPose = { b.sensor.x + (double)cur.x * b.step_x, b.sensor.y + (double)cur.y * b.step_y,
-                             b.sensor.theta + (double)cur.t * b.step_t };
-                scoreMax = score;
-                bx = cur.x;
-                by = cur.y;
-                bt = cur.t;
-                continue;
-            }
-            const int h = cur.h - 1, ws = 1 << h;   // :120-137
-            st.push_back({ cur.x, cur.y, cur.t, h });
-            st.push_back({ cur.x + ws, cur.y, cur.t, h });
-            st.push_back({ cur.x, cur.y + ws, cur.t, h });
-            st.push_back({ cur.x + ws, cur.y + ws, cur.t, h });
+        const BBResult& r = res[(size_t)j];
+        if (r.failed) {
+            failed[(size_t)j] = no_path ? 2 : 1;   // 1: rerun with the thr0 superset
+            continue;
         }
+        const bool got = r.score > b.thr0;   // a leaf was accepted
+        const int bx = got ? r.x : 0, by = got ? r.y : 0, bt = got ? r.t : 0;
+        const lgs_pose2d bestPose = got ? lgs_pose2d{ b.sensor.x + (double)bx * b.step_x,
+                                                      b.sensor.y + (double)by * b.step_y,
+                                                      b.sensor.theta + (double)bt * b.step_t }
+                                        : b.sensor;
         lgs_rtcsm_summary& o = out[j];
         const int gh = o.guard_hits, fx = o.fixups;
         std::memset(&o, 0, sizeof(o));
         o.guard_hits = gh;
         o.fixups = fx;
-        o.pose_found = scoreMax > b.thr0;   // :142-144
+        o.pose_found = r.score > b.thr0;   // :142-144
         o.initial_pose = init[j];
-        o.score_max = scoreMax;
+        o.score_max = r.score;
         o.score_threshold = b.thr0;
         o.best_win[0] = bx;
         o.best_win[1] = by;
@@ -698,11 +787,10 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         o.steps[1] = b.step_y;
         o.steps[2] = b.step_t;
         o.best_sensor_pose = bestPose;
-        o.coarse_blocks = scored[(size_t)j];
-        o.fine_blocks = visited;
+        o.coarse_blocks = (int64_t)(top_off[(size_t)j + 1] - top_off[(size_t)j]) + (int64_t)ncount[(size_t)j];
+        o.fine_blocks = r.visited;
         best[j] = bestPose;
-    };
-    host_parallel_for(n, 1, replay);   // the persistent host pool (no thread creation per call)
+    }
     for (int j = 0; j < n; ++j)
         LGS_REQUIRE(failed[(size_t)j] != 2, "branch-and-bound: the search reached a node the device did not score");
     lap(2);
@@ -816,8 +904,8 @@ extern "C" int lgs_bb_optimize_pose_batch(lgs_ctx* ctx, const lgs_grid* grid, co
             LGS_REQUIRE(scans[j] && scans[j]->n >= 1, "empty scan");
             sc[j] = const_cast<lgs_scan*>(scans[j]);
         }
-        for (int j0 = 0; j0 < n; j0 += 64) {
-            const int m = std::min(64, n - j0);
+        for (int j0 = 0; j0 < n; j0 += kBBBatch) {
+            const int m = std::min(kBBBatch, n - j0);
             run_bb(ctx, params, cost, grids.data() + j0, pp.data() + j0, sc.data() + j0, initial + j0, m, nthr,
                    out + j0);
         }
@@ -862,11 +950,12 @@ extern "C" int lgs_loop_detect_bb(lgs_ctx* ctx, const lgs_bb_params* params, con
                 LGS_REQUIRE(candidates[Q.first_candidate + j].scan, "loop candidate without a scan");
         }
         LGS_REQUIRE(covered == num_candidates, "loop queries must cover every candidate");
-        // batches of whole queries, at most ~64 candidates: each query's
+        // batches of whole queries, at most ~kBBBatch candidates: each query's
         // pyramid once per batch (LocalMapInfo caches it, :45-55)
         for (int q0 = 0; q0 < num_queries;) {
             int q1 = q0, m = 0;
-            while (q1 < num_queries && (m == 0 || m + queries[q1].num_candidates <= 64)) m += queries[q1++].num_candidates;
+            while (q1 < num_queries && (m == 0 || m + queries[q1].num_candidates <= kBBBatch))
+                m += queries[q1++].num_candidates;
             std::vector<const lgs_grid*> qmaps;
             for (int q = q0; q < q1; ++q) qmaps.push_back(queries[q].map);
             auto pyr = pyramids(ctx, qmaps.data(), (int)qmaps.size(), params->node_height_max);

@@ -2832,16 +2832,24 @@ __device__ __forceinline__ double small_cval(const double* __restrict__ grid, in
 template <int LR>
 constexpr size_t small_buf_doubles()
 {
-    // per wave, 2 buffers of LR fine rows + row max + coarse row; then the
-    // edge beams' coarse values [kSmallMaxNv]
-    return (size_t)LR * 2 * (LR + 2) * 65 + kSmallMaxNv;
+    // LR + 1 waves x one LR-row (fine) / one-row (coarse) buffer of 65-double
+    // rows, then the edge beams' coarse values and the row-maxima column
+    // [kSmallMaxNv each], then the per-chunk ready counters
+    return (size_t)(LR + 1) * LR * 65 + 2 * (size_t)kSmallMaxNv + kMaxChunks;
 }
 
+// Workgroup of LR + 1 waves: wave w < LR gathers fine row yo = w and its
+// lanes 0..LR-1 add the poses (xo = lane, yo = w); wave LR adds the coarse
+// values.  No workgroup barrier inside the chunk loop: each fine wave works
+// on its own LDS buffer (a wave's LDS operations execute in order), posts its
+// row maxima with ds_max_f64 into a per-beam column and then bumps the
+// chunk's ready counter; the coarse wave waits on that counter only.
 template <int LR>
-__global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, int guard_cap, double guard_eps,
-                                                         int inject, const double* __restrict__ zero)
+__global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int mode, int guard_cap,
+                                                               double guard_eps, int inject,
+                                                               const double* __restrict__ zero)
 {
-    constexpr int NT = 64 * LR, LD = 65, ROWB = (LR + 2) * LD, WSTR = 2 * ROWB;
+    constexpr int NT = 64 * (LR + 1), LD = 65;
     const MatchItem& it = items[blockIdx.y];
     const RtcsmPlan& pl = it.pl;
     const int tt = blockIdx.x;
@@ -2853,8 +2861,11 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
     const int gen = it.gen;
     extern __shared__ char smem[];
     int2* sidx = (int2*)smem;   // [Nv]
-    double* bufs = (double*)(smem + sizeof(int2) * (size_t)((Nv + 1) & ~1));   // [LR waves][WSTR]
-    __shared__ int s_wsum[LR];
+    double* bufs = (double*)(smem + sizeof(int2) * (size_t)((Nv + 1) & ~1));   // [LR + 1 waves][LR rows][LD]
+    double* cedge = bufs + (size_t)(LR + 1) * LR * LD;   // [Nv] edge beams' coarse values (NaN: interior)
+    double* cmax = cedge + kSmallMaxNv;                  // [Nv] max of the fine rows (interior beams)
+    int* ready = (int*)(cmax + kSmallMaxNv);             // [kMaxChunks] fine waves done with the chunk
+    __shared__ int s_wsum[LR + 1];
     __shared__ double s_trig[2];
     __shared__ double s_f[LR * LR];
     __shared__ double s_c;
@@ -2938,18 +2949,19 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
         stage_lds(sidx, it.idx + (size_t)tt * Nv, Nv);
         __syncthreads();
     }
-
     LGS_PROBE_MARK();
+
     // 2. fine rows + coarse values, beam order
     const int nchunk = (Nv + 63) / 64;
     const int xc = -pl.win_x, yr = -pl.win_y + wave;
-    double* wb = bufs + (size_t)wave * WSTR;
-    // Every lane loads a row run of LR cells with 16-byte loads from the run's
-    // start clamped into the map (W >= LR: always a valid address); a run
-    // that leaves the map then holds every in-map cell the lane needs, at
-    // index k = x - xs, and the cells outside are 0 -- selected in registers
-    // at the store.  No load sits under a branch: the compiler keeps four
-    // chunks of gathers in flight (vmcnt(24..28)), where a branch drained them.
+    const bool fine = wave < LR;
+    double* wb = bufs + (size_t)wave * LR * LD;   // this wave's buffer
+    // Every fine lane loads a row run of LR cells with 16-byte loads from the
+    // run's start clamped into the map (W >= LR: always a valid address); a
+    // run that leaves the map then holds every in-map cell the lane needs, at
+    // index k = x - xs, and the cells outside are 0 -- selected in registers.
+    // No load sits under a run-time branch inside the loop: the compiler
+    // keeps kSmallDepth chunks of gathers in flight (a branch drained them).
     double r[kSmallDepth][LR];
     int sh[kSmallDepth];   // x0 - xs, or LR (every cell masked: no beam, or a row outside the map)
     auto gather = [&](int c, double (&x)[LR], int& shift) {
@@ -2967,89 +2979,99 @@ __global__ __launch_bounds__(64 * LR) void k_match_small(Items items, int mode, 
         }
         if constexpr (LR & 1) x[LR - 1] = gload(p + LR - 1);
         shift = ((b < Nv) & ((unsigned)y < (unsigned)H)) ? x0 - xs : LR;
+#ifdef LGS_SMALL_NOGATHER   // diagnostics (timing only): no loads
+        for (int q = 0; q < LR; ++q) x[q] = (double)(x0 + q);
+#endif
     };
-    // lanes 0..LR-1: fine pose (xo = lane, yo = wave); wave 0 lane LR: the coarse sum
-    const bool adder = lane < LR || (wave == 0 && lane == LR);
-    const int arow = lane < LR ? lane : LR + 1;
-    double acc = 0.0;
-    static_for_step<0, kSmallDepth, 1>([&](auto dd) {
-        constexpr int d = decltype(dd)::value;
-        gather(d, r[d], sh[d]);
-        __builtin_amdgcn_sched_barrier(0);
-        return true;
-    });
+    // one adder lane's beam-order sum of a chunk row: the 64 values loaded
+    // first, then the dependent chain
+    auto add_row = [&](const double* row, int cnt, double& acc) {
+        double s = acc;
+        if (cnt == 64) {
+            double v[64];
+#pragma unroll
+            for (int b = 0; b < 64; ++b) v[b] = row[b];
+#pragma unroll
+            for (int b = 0; b < 64; ++b) s += v[b];
+        } else {
+            for (int b = 0; b < cnt; ++b) s += row[b];
+        }
+        acc = s;
+    };
+    if (fine) {
+        static_for_step<0, kSmallDepth, 1>([&](auto dd) {
+            constexpr int d = decltype(dd)::value;
+            gather(d, r[d], sh[d]);
+            __builtin_amdgcn_sched_barrier(0);
+            return true;
+        });
+    }
     // coarse values of the edge beams (lattice start outside [0, W - LR] x
     // [0, H - LR]) ahead of the chunk loop, which then holds no load under a
-    // branch; NaN marks an interior beam (its value comes from the row maxima)
-    double* cedge = bufs + (size_t)LR * WSTR;   // [Nv]
+    // branch; NaN marks an interior beam (its value is the max of its rows)
     for (int v = tid; v < Nv; v += NT) {
         const int2 ij = sidx[v];
         const int bx = ij.x - pl.win_x, by = ij.y - pl.win_y;
         const bool interior = (bx >= 0) & (by >= 0) & (bx <= W - LR) & (by <= H - LR);
         cedge[v] = interior ? __builtin_nan("") : small_cval(grid, bx, by, W, H, LR);
+        cmax[v] = -INFINITY;
     }
+    for (int c = tid; c < kMaxChunks; c += NT) ready[c] = 0;
     __syncthreads();
     LGS_PROBE_MARK();
-    static_for_step<0, kMaxChunks, 1>([&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        if (c >= nchunk) return false;
-        double* cur = wb + (c & 1) * ROWB;
-        {
-            constexpr int d = c % kSmallDepth;
-            const int k0 = sh[d];
-            double m = -INFINITY;
+    double acc = 0.0;
+    if (fine) {
+        static_for_step<0, kMaxChunks, 1>([&](auto cc) {
+            constexpr int c = decltype(cc)::value;
+            if (c >= nchunk) return false;
+            {
+                constexpr int d = c % kSmallDepth;
+                const int k0 = sh[d];
+                double m = -INFINITY;
 #pragma unroll
-            for (int q = 0; q < LR; ++q) {
-                const int k = k0 + q;   // cell x0 + q in the run (in the map iff 0 <= k < LR)
-                double v = 0.0;
+                for (int q = 0; q < LR; ++q) {
+                    const int k = k0 + q;   // cell x0 + q in the run (in the map iff 0 <= k < LR)
+                    double v = 0.0;
 #pragma unroll
-                for (int j = 0; j < LR; ++j) v = (k == j) ? r[d][j] : v;
-                cur[q * LD + lane] = v;
-                m = fmax(m, v);
+                    for (int j = 0; j < LR; ++j) v = (k == j) ? r[d][j] : v;
+                    wb[q * LD + lane] = v;
+                    m = fmax(m, v);
+                }
+                const int b = c * 64 + lane;
+                if (b < Nv) __hip_atomic_fetch_max(cmax + b, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            cur[LR * LD + lane] = m;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // unconditional (lanes past Nv read the zero cell): gathers under a
-        // run-time branch make the compiler drain every load in flight
-        if constexpr (c + kSmallDepth < kMaxChunks) gather(c + kSmallDepth, r[c % kSmallDepth], sh[c % kSmallDepth]);
-        __builtin_amdgcn_sched_barrier(0);
-        // every wave's rows of chunk c are in LDS (LDS-only release: the
-        // gathers in flight are not waited for)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        if (wave == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (c + kSmallDepth < kMaxChunks) gather(c + kSmallDepth, r[c % kSmallDepth], sh[c % kSmallDepth]);
+            __builtin_amdgcn_sched_barrier(0);
+            // after this wave's maxima of the chunk (in-order LDS)
+            if (lane == 0) __hip_atomic_fetch_add(ready + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef LGS_SMALL_NOSUM   // diagnostics (timing only): no sequential sums
+            if (lane < LR && c == 0) add_row(wb + lane * LD, min(64, Nv - c * 64), acc);
+#else
+            if (lane < LR) add_row(wb + lane * LD, min(64, Nv - c * 64), acc);
+#endif
+            return true;
+        });
+    } else {
+        // the coarse wave: chunk c once every fine wave has posted its maxima
+        for (int c = 0; c < nchunk; ++c) {
+            while (__hip_atomic_load(ready + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < LR)
+                __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
             const int b = c * 64 + lane;
             double cv = 0.0;
             if (b < Nv) {
-                cv = cedge[b];
-                if (__builtin_isnan(cv)) {   // interior beam
-                    cv = bufs[(c & 1) * ROWB + LR * LD + lane];
-#pragma unroll
-                    for (int w = 1; w < LR; ++w) cv = fmax(cv, bufs[(size_t)w * WSTR + (c & 1) * ROWB + LR * LD + lane]);
-                }
+                const double ce = cedge[b];
+                cv = __builtin_isnan(ce) ? cmax[b] : ce;
             }
-            cur[(LR + 1) * LD + lane] = cv;
+            wb[lane] = cv;
             __builtin_amdgcn_wave_barrier();
+            if (lane == 0) add_row(wb, min(64, Nv - c * 64), acc);
         }
-        if (adder) {
-            const double* row = cur + arow * LD;
-            const int cnt = min(64, Nv - c * 64);
-            double s = acc;
-            if (cnt == 64) {
-#pragma unroll 16
-                for (int b = 0; b < 64; ++b) s += row[b];
-            } else {
-                for (int b = 0; b < cnt; ++b) s += row[b];
-            }
-            acc = s;
-        }
-        return true;
-    });
+    }
     LGS_PROBE_MARK();
-    if (lane < LR) s_f[lane * LR + wave] = acc;   // order index xo * LR + yo (x outer, y inner)
-    if (wave == 0 && lane == LR) s_c = acc;
+    if (fine && lane < LR) s_f[lane * LR + wave] = acc;   // order index xo * LR + yo (x outer, y inner)
+    if (!fine && lane == 0) s_c = acc;
     __syncthreads();
     if (wave != 0) return;
     double fv = lane < LR * LR ? s_f[lane] : -INFINITY;
@@ -3642,7 +3664,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         const size_t nvp = (size_t)((std::max(B.NvMax, 1) + 1) & ~1);
 #define LGS_SMALL_CASE(L)                                                                                         \
     case L:                                                                                                      \
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_match_small<L>), g, dim3(64 * L),                                    \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_match_small<L>), g, dim3(64 * (L + 1)),                              \
                            sizeof(int2) * nvp + sizeof(double) * small_buf_doubles<L>(), st, d_items, mode,       \
                            ctx->guard_cap, ctx->guard_eps, inject, zero);                                        \
         break;

@@ -273,7 +273,7 @@ struct lgs_ctx {
     bool peer_staged = false;    // cross-context copies through host memory (LGS_OPT_PEER_COPY)
     int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
     bool small_window = true;    // one-launch search of one-block windows (LGS_OPT_SMALL_WINDOW)
-    bool post_records = false;   // records written to pinned memory by k_post + a flag (LGS_OPT_POST_RECORDS)
+    bool post_records = true;    // records written to pinned memory by k_post + a flag (LGS_OPT_POST_RECORDS)
     long long copies_direct = 0, copies_staged = 0;   // lgs_debug_copy_counters
     int lanes_min_batch = 2;     // pruned coarse stage: the work list (k_coarse_list) from this batch size on (LGS_OPT_LANES_MIN_BATCH)
     long long ray_chunk_keys = 1LL << 28;  // ray-cast keys per emit/sort/apply pass (LGS_OPT_RAY_CHUNK_KEYS)
