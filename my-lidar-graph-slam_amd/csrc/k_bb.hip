@@ -22,7 +22,10 @@
 // reference's search over these scores, exactly, and the greedy-endpoint
 // cost/covariance of the best pose come from k_cost (k_rtcsm.hip).
 //
-//   k_bb_trig    r cos(theta_t + a), r sin(theta_t + a) per (angle, valid beam)
+//   k_bb_trig    r cos(a), r sin(a) per valid beam and cos(theta_t), sin(theta_t)
+//                per angle; a node's hit offsets come by rotation (r4), within
+//                ~1e-13 cells of the reference's r cos(theta_t + a): inside the
+//                guard band, like k_project's
 //   k_bb_score   one lane per node: hit cells at the node pose (the
 //                reference's own arithmetic), sequential fp64 beam-order sum
 //                of the level's map values; cells within guard_eps of a cell
@@ -67,8 +70,10 @@ struct BBItem {
     const double* ranges;
     const double* angles;
     const int* vidx;              // valid beams (ScorePixelAccurate filter), beam order
-    double* rc;                   // [T][Nv]
-    double* rs;
+    double* rca;                  // [Nv] r cos(a), r sin(a) of the valid beams
+    double* rsa;
+    double* tc;                   // [T] cos(theta_t), sin(theta_t) of the search angles
+    double* ts;
     const double* maps[kBBMaxH + 1];
 };
 
@@ -84,18 +89,23 @@ struct BBGuard {
 __global__ __launch_bounds__(256) void k_bb_trig(const BBItem* __restrict__ items)
 {
     const BBItem& it = items[blockIdx.z];
-    const int t = blockIdx.y;
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= it.T || v >= it.Nv) return;
-    const int i = it.vidx[v];
-    // nodePose.mTheta = sensorPose.mTheta + currentNode.mTheta * stepTheta (:96-99)
-    const double th = it.st + (double)(t - it.win_t) * it.step_t;
-    // ScanData::HitPoint (H/sensor/sensor_data.hpp:162-173)
-    double sn, cs;
-    sincos(th + it.angles[i], &sn, &cs);
-    const double r = it.ranges[i];
-    it.rc[(size_t)t * it.Nv + v] = r * cs;
-    it.rs[(size_t)t * it.Nv + v] = r * sn;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < it.Nv) {
+        const int i = it.vidx[k];
+        double sn, cs;
+        sincos(it.angles[i], &sn, &cs);
+        const double r = it.ranges[i];
+        it.rca[k] = r * cs;
+        it.rsa[k] = r * sn;
+    }
+    if (k < it.T) {
+        // nodePose.mTheta = sensorPose.mTheta + currentNode.mTheta * stepTheta (:96-99)
+        const double th = it.st + (double)(k - it.win_t) * it.step_t;
+        double sn, cs;
+        sincos(th, &sn, &cs);
+        it.tc[k] = cs;
+        it.ts[k] = sn;
+    }
 }
 
 constexpr int kBBPipe = 16;
@@ -117,8 +127,9 @@ __global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ ite
     const double nx = it.sx + (double)nd.y * it.step_x;
     const double ny = it.sy + (double)nd.z * it.step_y;
     const int Nv = it.Nv, W = it.W, H = it.H;
-    const double* __restrict__ rc = it.rc + (size_t)(nd.w + it.win_t) * Nv;
-    const double* __restrict__ rs = it.rs + (size_t)(nd.w + it.win_t) * Nv;
+    const double* __restrict__ rca = it.rca;
+    const double* __restrict__ rsa = it.rsa;
+    const double ct = it.tc[nd.w + it.win_t], st = it.ts[nd.w + it.win_t];
     const double* __restrict__ map = it.maps[h];
     const double minx = it.min_x, miny = it.min_y, inv = 1.0 / it.res;
     double sum = 0.0;
@@ -127,8 +138,10 @@ __global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ ite
 #pragma unroll
         for (int j = 0; j < kBBPipe; ++j) {   // independent loads first
             const int v = min(v0 + j, Nv - 1);
-            cx[j] = gload(rc + v);
-            cy[j] = gload(rs + v);
+            // ScanData::HitPoint (H/sensor/sensor_data.hpp:162-173) by rotation
+            const double a = gload(rca + v), b = gload(rsa + v);
+            cx[j] = ct * a - st * b;
+            cy[j] = st * a + ct * b;
         }
 #pragma unroll
         for (int j = 0; j < kBBPipe; ++j) {
@@ -278,15 +291,21 @@ struct BBResult {
     int x, y, t, failed;
     long long visited;
 };
+// One match per wave (lane 0): lanes of one wave walking different matches
+// diverge at every visit, and a wave then pays a memory round trip in every
+// step where any of its lanes expands (measured 8.7 ms for 512 matches as 8
+// waves of 64, vs one round trip per expansion of its own here).
+constexpr int kReplayLanes = 1;   // matches per wave
 __global__ __launch_bounds__(64) void k_bb_replay(BBReplay R, const int* __restrict__ top_off,
                                                   const double* __restrict__ thr0, int n, BBResult* __restrict__ out)
 {
-    __shared__ double s_sc[kBBMaxH + 1][4][64];   // the group of four being walked at each level
-    __shared__ int s_cb[kBBMaxH + 1][4][64];
-    __shared__ int s_base[kBBMaxH + 1][64];
-    __shared__ int s_k[kBBMaxH + 1][64];          // next child of the group to visit (3 .. 0)
+    __shared__ double s_sc[kBBMaxH + 1][4][kReplayLanes];   // the group of four being walked at each level
+    __shared__ int s_cb[kBBMaxH + 1][4][kReplayLanes];
+    __shared__ int s_base[kBBMaxH + 1][kReplayLanes];
+    __shared__ int s_k[kBBMaxH + 1][kReplayLanes];          // next child of the group to visit (3 .. 0)
     const int lane = threadIdx.x;
-    const int j = blockIdx.x * 64 + lane;
+    if (lane >= kReplayLanes) return;
+    const int j = blockIdx.x * kReplayLanes + lane;
     if (j >= n) return;
     const int hm = R.hm;
     const int t0 = top_off[j], t1 = top_off[j + 1];
@@ -467,21 +486,21 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
     std::vector<BBHost> plans;
     plans.reserve((size_t)n);
     int Tmax = 1, NvMax = 1;
-    size_t trig_doubles = 0;
+    size_t trig_doubles = 0, vtot = 0;
     for (int j = 0; j < n; ++j) {
         plans.push_back(make_bb_plan(grids[j], p, scans[j], init[j], nthr));
         Tmax = std::max(Tmax, plans[j].T);
         NvMax = std::max(NvMax, plans[j].Nv);
-        trig_doubles += 2 * (size_t)plans[j].T * std::max(plans[j].Nv, 1);
+        trig_doubles += 2 * ((size_t)plans[j].T + std::max(plans[j].Nv, 1));
+        vtot += plans[j].vidx.size();
     }
-    // device scratch: trig tables + valid-beam lists
-    size_t vtot = 0;
-    for (auto& b : plans) vtot += std::max<size_t>(b.vidx.size(), 1);
-    const size_t bytes = align256(sizeof(double) * trig_doubles) + 256 * (size_t)n * 2 + align256(sizeof(int) * vtot) +
-                         256 * (size_t)n;
+    // device scratch: trig tables + the valid-beam lists (one copy for the batch)
+    const size_t bytes = align256(sizeof(double) * trig_doubles) + 256 * (size_t)n * 4 + align256(sizeof(int) * vtot);
     Carver cv((char*)ctx->ensure(S_BB0, bytes));
+    int* d_vidx_all = cv.take<int>(vtot);
+    std::vector<int> h_vidx;
+    h_vidx.reserve(vtot);
     std::vector<BBItem> items((size_t)n);
-    std::vector<int*> d_vidx((size_t)n);
     for (int j = 0; j < n; ++j) {
         const BBHost& b = plans[j];
         BBItem& it = items[j];
@@ -507,16 +526,17 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         it.thr_exp = b.thr0;
         it.ranges = scans[j]->d_ranges;
         it.angles = scans[j]->d_angles;
-        it.rc = cv.take<double>((size_t)b.T * std::max(b.Nv, 1));
-        it.rs = cv.take<double>((size_t)b.T * std::max(b.Nv, 1));
-        d_vidx[j] = cv.take<int>(std::max<size_t>(b.vidx.size(), 1));
-        it.vidx = d_vidx[j];
+        it.rca = cv.take<double>((size_t)std::max(b.Nv, 1));
+        it.rsa = cv.take<double>((size_t)std::max(b.Nv, 1));
+        it.tc = cv.take<double>((size_t)b.T);
+        it.ts = cv.take<double>((size_t)b.T);
+        it.vidx = d_vidx_all + h_vidx.size();
+        h_vidx.insert(h_vidx.end(), b.vidx.begin(), b.vidx.end());
         for (int h = 0; h <= Hm; ++h) it.maps[h] = pyr[j][h];
     }
-    for (int j = 0; j < n; ++j)
-        if (!plans[j].vidx.empty())
-            LGS_HIP_CHECK(hipMemcpyAsync(d_vidx[j], plans[j].vidx.data(), sizeof(int) * plans[j].vidx.size(),
-                                         hipMemcpyHostToDevice, ctx->stream));
+    if (!h_vidx.empty())
+        LGS_HIP_CHECK(hipMemcpyAsync(d_vidx_all, h_vidx.data(), sizeof(int) * h_vidx.size(), hipMemcpyHostToDevice,
+                                     ctx->stream));
     // guards (shared by every level of the batch)
     // [0] guards, [1] children, [2] overflow; from byte 256 the per-match scored-node counters
     int* d_counts = (int*)ctx->ensure(S_BB3, 256 + sizeof(unsigned long long) * (size_t)n);
@@ -541,7 +561,7 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         const size_t poff = up.append(path.data(), path.size());
         up.flush();
         const BBItem* d_items = up.at<BBItem>(ioff);
-        dim3 g((NvMax + 255) / 256, Tmax, n);
+        dim3 g((std::max(NvMax, Tmax) + 255) / 256, 1, n);
         hipLaunchKernelGGL(k_bb_trig, g, dim3(256), 0, ctx->stream, d_items);
         LGS_HIP_CHECK(hipGetLastError());
         const int np = (int)path.size();
@@ -743,7 +763,8 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         const size_t ho = ur.append(thr0.data(), thr0.size());
         ur.flush();
         BBResult* d_res = (BBResult*)ctx->ensure(S_BB5, sizeof(BBResult) * (size_t)n);
-        hipLaunchKernelGGL(k_bb_replay, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, R, ur.at<int>(to),
+        hipLaunchKernelGGL(k_bb_replay, dim3((n + kReplayLanes - 1) / kReplayLanes), dim3(64), 0, ctx->stream, R,
+                           ur.at<int>(to),
                            ur.at<double>(ho), n, d_res);
         LGS_HIP_CHECK(hipGetLastError());
         LGS_HIP_CHECK(hipMemcpyAsync(res.data(), d_res, sizeof(BBResult) * (size_t)n, hipMemcpyDeviceToHost,
