@@ -1589,7 +1589,7 @@ RayMap raymap_of(const lgs_map* m, unsigned long long base)
 }
 
 // LGS_STEP_TIMING=1: host wall time of the latest-map step's phases, averaged
-// over every 2000 steps, on stderr (diagnostics)
+// over every 500 steps, on stderr (diagnostics)
 struct StepTiming {
     bool on = std::getenv("LGS_STEP_TIMING") != nullptr;
     std::chrono::steady_clock::time_point prev;
@@ -1608,10 +1608,10 @@ struct StepTiming {
     }
     void done()
     {
-        if (!on || ++steps % 2000) return;
+        if (!on || ++steps % 500) return;
         std::fprintf(stderr, "latest step host us: finish %.1f hits %.1f geom %.1f pre %.1f rays(latest) %.1f "
-                     "rays(local)+shift %.1f stage %.1f launch %.1f\n", us[0] / 2000, us[1] / 2000, us[2] / 2000,
-                     us[6] / 2000, us[7] / 2000, us[3] / 2000, us[4] / 2000, us[5] / 2000);
+                     "rays(local)+shift %.1f stage %.1f launch %.1f\n", us[0] / 500, us[1] / 500, us[2] / 500,
+                     us[6] / 500, us[7] / 500, us[3] / 500, us[4] / 500, us[5] / 500);
         for (double& u : us) u = 0;
     }
 };

@@ -2829,25 +2829,35 @@ __device__ __forceinline__ double small_cval(const double* __restrict__ grid, in
     return m;
 }
 
+constexpr int kSmallRing = 3;   // chunk buffers between the row waves and the adder wave
 template <int LR>
 constexpr size_t small_buf_doubles()
 {
-    // LR + 1 waves x one LR-row (fine) / one-row (coarse) buffer of 65-double
-    // rows, then the edge beams' coarse values and the row-maxima column
-    // [kSmallMaxNv each], then the per-chunk ready counters
-    return (size_t)(LR + 1) * LR * 65 + 2 * (size_t)kSmallMaxNv + kMaxChunks;
+    // the ring of chunk buffers (LR * LR pose rows of 65 doubles), then the
+    // coarse column [kSmallMaxNv], then the ready counters and the consumed count
+    return (size_t)kSmallRing * LR * LR * 65 + (size_t)kSmallMaxNv + kMaxChunks / 2 + 1;
 }
 
-// Workgroup of LR + 1 waves: wave w < LR gathers fine row yo = w and its
-// lanes 0..LR-1 add the poses (xo = lane, yo = w); wave LR adds the coarse
-// values.  No workgroup barrier inside the chunk loop: each fine wave works
-// on its own LDS buffer (a wave's LDS operations execute in order), posts its
-// row maxima with ds_max_f64 into a per-beam column and then bumps the
-// chunk's ready counter; the coarse wave waits on that counter only.
+// Workgroup of LR + 1 waves: row wave w < LR gathers fine row yo = w of 64
+// beams at a time and writes its cells of every pose (xo, w) into the chunk's
+// ring buffer and its row maxima into the coarse column (ds_max_f64); the
+// adder wave's lane k adds pose k's row, lane LR * LR the coarse column, each
+// in beam order.  No workgroup barrier inside the chunk loop: the row waves
+// bump the chunk's ready counter after their LDS writes (a wave's LDS
+// operations execute in order), the adder posts the chunks it is done with.
+// One adder wave for every chain: r04's first layout (each row wave adding
+// its own LR poses, a seventh wave the coarse column) ran the chains on waves
+// that shared SIMDs with the gather work (16 us of chunk loop + 5 us waiting
+// for the slowest wave per config-4 angle).  LowRes <= 7 (LR * LR + 1 <= 64 lanes).
 template <int LR>
+// mode 0: project; 2: project, then the host's guard patches (t, v, ix, iy);
+// 1: read the index rows the host uploaded (a full host projection).  The
+// projected rows are not written back: dirty lines would make the device-scope
+// release before the angle count write back that much more L2.
 __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int mode, int guard_cap,
                                                                double guard_eps, int inject,
-                                                               const double* __restrict__ zero)
+                                                               const double* __restrict__ zero,
+                                                               const int4* __restrict__ patches, int npatch)
 {
     constexpr int NT = 64 * (LR + 1), LD = 65;
     const MatchItem& it = items[blockIdx.y];
@@ -2861,22 +2871,18 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
     const int gen = it.gen;
     extern __shared__ char smem[];
     int2* sidx = (int2*)smem;   // [Nv]
-    double* bufs = (double*)(smem + sizeof(int2) * (size_t)((Nv + 1) & ~1));   // [LR + 1 waves][LR rows][LD]
-    double* cedge = bufs + (size_t)(LR + 1) * LR * LD;   // [Nv] edge beams' coarse values (NaN: interior)
-    double* cmax = cedge + kSmallMaxNv;                  // [Nv] max of the fine rows (interior beams)
-    int* ready = (int*)(cmax + kSmallMaxNv);             // [kMaxChunks] fine waves done with the chunk
+    double* bufs = (double*)(smem + sizeof(int2) * (size_t)((Nv + 1) & ~1));   // [kSmallRing][LR * LR rows][LD]
+    double* cmax = bufs + (size_t)kSmallRing * LR * LR * LD;   // [Nv] coarse values (interior beams: max of the rows)
+    int* ready = (int*)(cmax + kSmallMaxNv);             // [kMaxChunks] row waves done with the chunk
+    int* consumed = ready + kMaxChunks;                  // chunks the adder wave is done with
     __shared__ int s_wsum[LR + 1];
     __shared__ double s_trig[2];
-    __shared__ double s_f[LR * LR];
-    __shared__ double s_c;
     __shared__ int s_last;
-    typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-    gu64_t* __restrict__ gidx = (gu64_t*)(it.idx + (size_t)tt * Nv);
     LGS_PROBE_DECL;
     LGS_PROBE_MARK();
 
     // 1. the angle's scan indices
-    if (mode == 0) {
+    if (mode != 1) {
         const double* __restrict__ ranges = it.ranges;
         const double* __restrict__ angles = it.angles;
         int* smap = (int*)bufs;   // valid beam v -> beam index (the value buffers are not in use yet)
@@ -2939,12 +2945,16 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
                 }
                 ix += inject;
             }
-            if (act) {
-                sidx[v] = make_int2(ix, iy);
-                gidx[v] = ((unsigned long long)(unsigned)iy << 32) | (unsigned)ix;
-            }
+            if (act) sidx[v] = make_int2(ix, iy);
         }
         __syncthreads();   // the beam map is dead from here on
+        if (mode == 2) {
+            for (int k = tid; k < npatch; k += NT) {
+                const int4 pq = patches[k];
+                if (pq.x == tt) sidx[pq.y] = make_int2(pq.z, pq.w);
+            }
+            __syncthreads();
+        }
     } else {
         stage_lds(sidx, it.idx + (size_t)tt * Nv, Nv);
         __syncthreads();
@@ -2955,7 +2965,6 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
     const int nchunk = (Nv + 63) / 64;
     const int xc = -pl.win_x, yr = -pl.win_y + wave;
     const bool fine = wave < LR;
-    double* wb = bufs + (size_t)wave * LR * LD;   // this wave's buffer
     // Every fine lane loads a row run of LR cells with 16-byte loads from the
     // run's start clamped into the map (W >= LR: always a valid address); a
     // run that leaves the map then holds every in-map cell the lane needs, at
@@ -2964,7 +2973,8 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
     // keeps kSmallDepth chunks of gathers in flight (a branch drained them).
     double r[kSmallDepth][LR];
     int sh[kSmallDepth];   // x0 - xs, or LR (every cell masked: no beam, or a row outside the map)
-    auto gather = [&](int c, double (&x)[LR], int& shift) {
+    bool inr[kSmallDepth]; // an interior beam of the chunk (its coarse value is the max of its rows)
+    auto gather = [&](int c, double (&x)[LR], int& shift, bool& interior) {
         const int b = c * 64 + lane;
         const int2 ij = sidx[max(min(b, Nv - 1), 0)];
         const int x0 = ij.x + xc, y = ij.y + yr;
@@ -2979,6 +2989,8 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
         }
         if constexpr (LR & 1) x[LR - 1] = gload(p + LR - 1);
         shift = ((b < Nv) & ((unsigned)y < (unsigned)H)) ? x0 - xs : LR;
+        const int by = y - wave;   // the beam's lattice start (x0, by)
+        interior = (b < Nv) & (x0 >= 0) & (by >= 0) & (x0 <= W - LR) & (by <= H - LR);
 #ifdef LGS_SMALL_NOGATHER   // diagnostics (timing only): no loads
         for (int q = 0; q < LR; ++q) x[q] = (double)(x0 + q);
 #endif
@@ -3001,29 +3013,39 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
     if (fine) {
         static_for_step<0, kSmallDepth, 1>([&](auto dd) {
             constexpr int d = decltype(dd)::value;
-            gather(d, r[d], sh[d]);
+            gather(d, r[d], sh[d], inr[d]);
             __builtin_amdgcn_sched_barrier(0);
             return true;
         });
     }
-    // coarse values of the edge beams (lattice start outside [0, W - LR] x
-    // [0, H - LR]) ahead of the chunk loop, which then holds no load under a
-    // branch; NaN marks an interior beam (its value is the max of its rows)
+    // the coarse column: the edge beams' values (lattice start outside
+    // [0, W - LR] x [0, H - LR]) ahead of the chunk loop, which then holds no
+    // load under a branch; -inf for the interior beams, whose value the row
+    // waves' maxima build (ds_max_f64)
     for (int v = tid; v < Nv; v += NT) {
         const int2 ij = sidx[v];
         const int bx = ij.x - pl.win_x, by = ij.y - pl.win_y;
         const bool interior = (bx >= 0) & (by >= 0) & (bx <= W - LR) & (by <= H - LR);
-        cedge[v] = interior ? __builtin_nan("") : small_cval(grid, bx, by, W, H, LR);
-        cmax[v] = -INFINITY;
+        cmax[v] = interior ? -INFINITY : small_cval(grid, bx, by, W, H, LR);
     }
     for (int c = tid; c < kMaxChunks; c += NT) ready[c] = 0;
+    if (tid == 0) *consumed = 0;
     __syncthreads();
     LGS_PROBE_MARK();
-    double acc = 0.0;
+    constexpr int ROWS = LR * LR;   // pose rows of a chunk buffer, row = order index xo * LR + yo
     if (fine) {
+        // a row wave: its cells of every pose (xo = 0..LR-1, yo = wave) into
+        // the chunk's ring buffer, its row maxima into the coarse column
         static_for_step<0, kMaxChunks, 1>([&](auto cc) {
             constexpr int c = decltype(cc)::value;
             if (c >= nchunk) return false;
+            if constexpr (c >= kSmallRing) {   // the adder is done with the buffer's previous chunk
+                while (__hip_atomic_load(consumed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                       c - kSmallRing + 1) {
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+            }
+            double* cur = bufs + (size_t)(c % kSmallRing) * ROWS * LD;
             {
                 constexpr int d = c % kSmallDepth;
                 const int k0 = sh[d];
@@ -3034,47 +3056,41 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
                     double v = 0.0;
 #pragma unroll
                     for (int j = 0; j < LR; ++j) v = (k == j) ? r[d][j] : v;
-                    wb[q * LD + lane] = v;
+                    cur[(q * LR + wave) * LD + lane] = v;
                     m = fmax(m, v);
                 }
-                const int b = c * 64 + lane;
-                if (b < Nv) __hip_atomic_fetch_max(cmax + b, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (inr[d]) __hip_atomic_fetch_max(cmax + c * 64 + lane, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (c + kSmallDepth < kMaxChunks) gather(c + kSmallDepth, r[c % kSmallDepth], sh[c % kSmallDepth]);
+            if constexpr (c + kSmallDepth < kMaxChunks)
+                gather(c + kSmallDepth, r[c % kSmallDepth], sh[c % kSmallDepth], inr[c % kSmallDepth]);
             __builtin_amdgcn_sched_barrier(0);
-            // after this wave's maxima of the chunk (in-order LDS)
+            // after this wave's rows and maxima of the chunk (in-order LDS)
             if (lane == 0) __hip_atomic_fetch_add(ready + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef LGS_SMALL_NOSUM   // diagnostics (timing only): no sequential sums
-            if (lane < LR && c == 0) add_row(wb + lane * LD, min(64, Nv - c * 64), acc);
-#else
-            if (lane < LR) add_row(wb + lane * LD, min(64, Nv - c * 64), acc);
-#endif
             return true;
         });
-    } else {
-        // the coarse wave: chunk c once every fine wave has posted its maxima
-        for (int c = 0; c < nchunk; ++c) {
-            while (__hip_atomic_load(ready + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < LR)
-                __builtin_amdgcn_s_sleep(1);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-            const int b = c * 64 + lane;
-            double cv = 0.0;
-            if (b < Nv) {
-                const double ce = cedge[b];
-                cv = __builtin_isnan(ce) ? cmax[b] : ce;
-            }
-            wb[lane] = cv;
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) add_row(wb, min(64, Nv - c * 64), acc);
+        return;
+    }
+    // the adder wave: lane k < ROWS adds pose k's row, lane ROWS the coarse
+    // column, each in beam order, chunk by chunk as the row waves post them
+    double acc = 0.0;
+    for (int c = 0; c < nchunk; ++c) {
+        while (__hip_atomic_load(ready + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < LR) {
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        const double* row = lane < ROWS ? bufs + (size_t)(c % kSmallRing) * ROWS * LD + lane * LD : cmax + c * 64;
+#ifdef LGS_SMALL_NOSUM   // diagnostics (timing only): no sequential sums
+        if (lane <= ROWS && c == 0) add_row(row, min(64, Nv - c * 64), acc);
+#else
+        if (lane <= ROWS) add_row(row, min(64, Nv - c * 64), acc);
+#endif
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) __hip_atomic_store(consumed, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     LGS_PROBE_MARK();
-    if (fine && lane < LR) s_f[lane * LR + wave] = acc;   // order index xo * LR + yo (x outer, y inner)
-    if (!fine && lane == 0) s_c = acc;
-    __syncthreads();
-    if (wave != 0) return;
-    double fv = lane < LR * LR ? s_f[lane] : -INFINITY;
+    LGS_PROBE_MARK();
+    const double cval = __shfl(acc, ROWS, 64);
+    double fv = lane < ROWS ? acc : -INFINITY;
     long long fk = lane < LR * LR ? lane : LLONG_MAX;
     for (int off = 32; off > 0; off >>= 1) {
         const double ov = __shfl_xor(fv, off, 64);
@@ -3086,8 +3102,9 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
     }
     typedef __attribute__((address_space(1))) double gdbl_t;
     typedef __attribute__((address_space(1))) int gint_t;
+    LGS_PROBE_MARK();
     if (lane == 0) {
-        ((gdbl_t*)it.cscore)[tt] = s_c;
+        ((gdbl_t*)it.cscore)[tt] = cval;
         ((gdbl_t*)it.fval)[tt] = fv;
         ((gint_t*)it.fpos)[tt] = (int)fk;
         __threadfence();   // release (device scope): the triple before the count
@@ -3097,7 +3114,7 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     LGS_PROBE_MARK();
-    LGS_PROBE_PRINT("match_small(b0: project, edge pass, chunks, publish)");
+    LGS_PROBE_PRINT("match_small(b0: project, edge pass, chunks, sync, argmax, publish)");
     if (!s_last) return;
     __threadfence();   // acquire: every angle's triple
 
@@ -3641,22 +3658,23 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         beams_K += (double)it.pl.K * it.pl.Nv;
     }
     if (B.small) {
-        // k_match_small (§4.1c): mode 0 projects, mode 1 reads the index rows
-        // the host fixed (a full host projection or k_patch's patches)
+        // k_match_small (§4.1c): mode 0 projects, 2 projects and applies the
+        // host's guard patches, 1 reads the rows of a full host projection
         int mode = 0;
         if (opt.host_idx) {
             const MatchItem& it = items[0];
             LGS_HIP_CHECK(hipMemcpyAsync(it.idx, opt.host_idx->data(), sizeof(int2) * opt.host_idx->size(),
                                          hipMemcpyHostToDevice, st));
             mode = 1;
-        } else if (opt.patches && !opt.patches->empty()) {
-            int4* dp = (int4*)ctx->ensure(S_PATCH, sizeof(int4) * opt.patches->size());
-            LGS_HIP_CHECK(hipMemcpyAsync(dp, opt.patches->data(), sizeof(int4) * opt.patches->size(),
+        }
+        const int4* dp = nullptr;
+        int np = 0;
+        if (!opt.host_idx && opt.patches && !opt.patches->empty()) {
+            dp = (const int4*)ctx->ensure(S_PATCH, sizeof(int4) * opt.patches->size());
+            LGS_HIP_CHECK(hipMemcpyAsync((void*)dp, opt.patches->data(), sizeof(int4) * opt.patches->size(),
                                          hipMemcpyHostToDevice, st));
-            const int np = (int)opt.patches->size();
-            hipLaunchKernelGGL(k_patch, dim3((np + 255) / 256), dim3(256), 0, st, d_items, dp, np);
-            LGS_HIP_CHECK(hipGetLastError());
-            mode = 1;
+            np = (int)opt.patches->size();
+            mode = 2;
         }
         const int lr = B.low_res;
         const int tok = ctx->timing_begin(K_MATCH_SMALL, 8.0 * (lr * lr) * beams_T);
@@ -3666,12 +3684,12 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
     case L:                                                                                                      \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_match_small<L>), g, dim3(64 * (L + 1)),                              \
                            sizeof(int2) * nvp + sizeof(double) * small_buf_doubles<L>(), st, d_items, mode,       \
-                           ctx->guard_cap, ctx->guard_eps, inject, zero);                                        \
+                           ctx->guard_cap, ctx->guard_eps, inject, zero, dp, np);                                \
         break;
         if (!ctx->skipped(K_MATCH_SMALL)) switch (lr) {
             LGS_SMALL_CASE(2) LGS_SMALL_CASE(3) LGS_SMALL_CASE(4) LGS_SMALL_CASE(5) LGS_SMALL_CASE(6)
-            LGS_SMALL_CASE(7) LGS_SMALL_CASE(8)
-            default: LGS_REQUIRE(false, "k_match_small: LowRes outside [2, 8]");
+            LGS_SMALL_CASE(7)
+            default: LGS_REQUIRE(false, "k_match_small: LowRes outside [2, 7]");
             }
 #undef LGS_SMALL_CASE
         ctx->timing_end(tok);
@@ -4140,7 +4158,7 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     B.nsegMax = (int)(((long long)B.Tmax * B.P + kSelSeg - 1) / kSelSeg);
     // one coarse block per angle: the whole search in one launch, straight
     // from the fine map (no caller-supplied coarse map to honour)
-    B.small = ctx->small_window && !ctx->force_dense && p0.P == 1 && B.low_res >= 2 && B.low_res <= 8 &&
+    B.small = ctx->small_window && !ctx->force_dense && p0.P == 1 && B.low_res >= 2 && B.low_res <= 7 &&
               B.NvMax <= kSmallMaxNv && n <= kTedgeCtrs;
     for (int j = 0; j < n; ++j) B.small = B.small && grids[j]->w >= B.low_res && grids[j]->h >= 1;   // clamped runs
     for (auto& s : sets) B.small = B.small && !s.coarse;

@@ -460,18 +460,26 @@ struct CoopDevice {
     long long cap = 0, used = 0;
     std::vector<std::pair<hipEvent_t, long long>> live;   // (event after the launch, tiles)
     std::vector<hipEvent_t> spare;
+    void release(size_t i)
+    {
+        used -= live[i].second;
+        spare.push_back(live[i].first);
+        live.erase(live.begin() + (ptrdiff_t)i);
+    }
+    // every completed launch (when the capacity is short)
     void reclaim()
     {
         for (size_t i = 0; i < live.size();) {
-            if (hipEventQuery(live[i].first) == hipSuccess) {
-                used -= live[i].second;
-                spare.push_back(live[i].first);
-                live[i] = live.back();
-                live.pop_back();
-            } else {
-                ++i;
-            }
+            if (hipEventQuery(live[i].first) == hipSuccess) release(i);
+            else ++i;
         }
+    }
+    // the oldest launches, while completed: one event query per launch in
+    // the common case (querying all 16 live events before every launch cost
+    // ~6 us of host time on the config-4 step's dependency chain)
+    void reclaim_front()
+    {
+        while (!live.empty() && hipEventQuery(live.front().first) == hipSuccess) release(0);
     }
 };
 CoopDevice g_coop[64];
@@ -493,6 +501,7 @@ bool coop_launch(lgs_ctx* ctx, long long tiles, Launch&& launch)
     }
     const long long cap = ctx->coop_tiles >= 0 ? std::min(D.cap, ctx->coop_tiles) : D.cap;
     if (tiles > cap) return false;
+    D.reclaim_front();
     if (D.used + tiles > cap || D.live.size() >= 16) D.reclaim();
     if (D.used + tiles > cap) return false;
     hipEvent_t ev = nullptr;

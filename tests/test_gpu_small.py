@@ -50,8 +50,9 @@ def room(world):
 
 @pytest.mark.parametrize("low_res", [2, 3, 4, 5, 6, 7, 8])
 def test_small_window_low_resolutions(ctx, world, room, low_res):
-    """Every LowRes the kernel is built for, with the widest one-block window
-    (winX = winY = (LowRes - 1) // 2)."""
+    """Every LowRes the kernel is built for (2..7: the adder wave holds the
+    LowRes^2 pose chains and the coarse one), with the widest one-block window
+    (winX = winY = (LowRes - 1) // 2); LowRes 8 takes the general path."""
     cells, mx, my = room
     ang = scene.beam_angles(541)
     rng = np.random.default_rng(40 + low_res)
@@ -63,8 +64,12 @@ def test_small_window_low_resolutions(ctx, world, room, low_res):
     rng_xy = max(0.0, (2 * ((low_res - 1) // 2) - 0.01) * 0.05)
     params = (low_res, rng_xy, rng_xy, 0.5, 20.0)
     gpu, n = _match(ctx, cells, mx, my, 0.05, params, r, ang, init)
-    assert n == 1, n
-    _exact(gpu, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"lr{low_res}")
+    assert n == (1 if low_res <= 7 else 0), n
+    ora = oracle_match(cells, mx, my, 0.05, params, r, ang, init)
+    if n:
+        _exact(gpu, ora, f"lr{low_res}")
+    else:
+        assert_same(gpu, ora, f"lr{low_res}")
 
 
 @pytest.mark.parametrize("seed", range(6))

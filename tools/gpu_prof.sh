@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 TAG=${1:-r01}
 mkdir -p $OUT
-BENCH="bench.py --steps ${STEPS:-200} --warmup ${WARMUP:-10} --no-cpu --latency-calls 0 --loop-line 0 --dropin-line 0"
+BENCH="bench.py --steps ${STEPS:-200} --warmup ${WARMUP:-10} --no-cpu --latency-calls 0 --loop-line 0 --dropin-line 0 --sub-lines 0"
 run() {  # run <name> <rocprofv3 args...>
   local name=$1; shift
   echo "== $name" | tee -a $OUT/steps.log
