@@ -201,7 +201,11 @@ def pmc_for(pmc_path, trace_kernel, workload):
         return None
     if pmc.get("lib_sha256") != lib_sha256() or pmc.get("workload", "match") != workload:
         return None
-    e = pmc.get("kernels", {}).get(trace_kernel)
+    kernels = pmc.get("kernels", {})
+    e = kernels.get(trace_kernel)
+    if not e:   # the launched variant (k_coarse_list_c, the chunked list kernel since r04)
+        cands = [k for k in kernels if k.startswith(trace_kernel)]
+        e = kernels[cands[0]] if len(cands) == 1 else None
     if not e or "fetch_bytes_per_launch" not in e or "write_bytes_per_launch" not in e:
         return None
     return dict(traffic=2.0 * e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"],
