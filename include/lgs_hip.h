@@ -176,8 +176,8 @@ int  lgs_abi_version(void);
 #define LGS_OPT_COOP_TILES    22  /* K3 one-launch sort (k_sort_wide): at most this many tiles for this ctx's launches (default -1 = the device's co-residency capacity, shared by every ctx of the process; 0 = always the multi-pass sort) */
 #define LGS_OPT_SORT_BARRIER_US 23 /* bound of a one-launch sort tile's wait at its grid barrier (default 50000 us); on time-out the call reports LGS_ERR_INTERNAL.  0 = time out at once (tests) */
 #define LGS_OPT_FINE_STAGED   24  /* 1 (default) = batched fine evaluation of LowRes-5 blocks stages each beam's window in LDS (k_fine_regs), 0 = per-beam gathers (k_fine_lanes) */
-#define LGS_OPT_SMALL_WINDOW  25  /* 1 (default) = windows with one coarse block per angle (2 winX < LowRes, 2 winY < LowRes, <= 2048 valid beams) search in one launch (k_match_small: no coarse map), 0 = the general path */
-#define LGS_OPT_POST_RECORDS  26  /* 1 = a match call's result records reach the host through a kernel that writes them (and a completion flag) into pinned memory, the host spinning on the flag; 0 (default) = a device-to-host copy and a stream event */
+#define LGS_OPT_SMALL_WINDOW  25  /* 1 (default) = windows with one coarse block per angle (2 winX < LowRes, 2 winY < LowRes, LowRes 2..7, map width >= LowRes, <= 2048 valid beams) search in one launch (k_match_small: no coarse map), 0 = the general path */
+#define LGS_OPT_POST_RECORDS  26  /* 1 (default) = a match call's result records reach the host through a kernel that writes them (and a completion flag) into pinned memory, the host spinning on the flag; 0 = a device-to-host copy and a stream event */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

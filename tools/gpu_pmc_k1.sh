@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 OUT=gpurun_out; mkdir -p $OUT
-B="bench.py --steps 30 --warmup 3 --no-cpu --latency-calls 0 --loop-line 0 --dropin-line 0 --streams 1"
+B="bench.py --steps 30 --warmup 3 --no-cpu --latency-calls 0 --loop-line 0 --dropin-line 0 --sub-lines 0 --streams 1"
 i=0; dirs=""
 while read -r counters; do
   [ -z "$counters" ] && continue
