@@ -178,6 +178,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_FINE_STAGED   24  /* 1 (default) = batched fine evaluation of LowRes-5 blocks stages each beam's window in LDS (k_fine_regs), 0 = per-beam gathers (k_fine_lanes) */
 #define LGS_OPT_SMALL_WINDOW  25  /* 1 (default) = windows with one coarse block per angle (2 winX < LowRes, 2 winY < LowRes, LowRes 2..7, map width >= LowRes, <= 2048 valid beams) search in one launch (k_match_small: no coarse map), 0 = the general path */
 #define LGS_OPT_POST_RECORDS  26  /* 1 (default) = a match call's result records reach the host through a kernel that writes them (and a completion flag) into pinned memory, the host spinning on the flag; 0 = a device-to-host copy and a stream event */
+#define LGS_OPT_FUSED_PLANES  27  /* 1 (default) = the per-query coarse-map precompute writes the phase planes AND the octet superblock units in one pass from the fine map (k_planes_super, LowRes 5), 0 = the precompute + k_super_planes passes */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 
@@ -367,7 +368,13 @@ int  lgs_map_update_scan(lgs_ctx* ctx, lgs_map* map, const lgs_scan* scan, lgs_p
  * call returns before its device work has finished: reads of the map through
  * this library wait for it (on any context); lgs_grid_device_ptr users
  * synchronise the context first.  An internal error of that work is reported
- * by the map's next rebuild. */
+ * by the map's next rebuild (LGS_ERR_INTERNAL, e.g. "grid barrier timed out"
+ * when the one-launch sort's tiles could not be co-resident): the update
+ * kernels of that step have then run over unsorted keys, so the cells of this
+ * map AND of the local map an lgs_map_append_scan step inserted into are
+ * undefined.  The library drops the latest map's incremental state (its next
+ * call rebuilds it in full); the caller must rebuild the local map
+ * (lgs_map_construct_from_scans) before reading it again. */
 int  lgs_map_construct_from_scans(lgs_ctx* ctx, lgs_map* map, const lgs_scan* const* scans,
                                   const lgs_pose2d* robot_poses, int n,
                                   const lgs_builder_params* params);

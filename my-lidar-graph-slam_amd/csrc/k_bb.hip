@@ -483,6 +483,9 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         t_prev = now;
     };
     const int Hm = p->node_height_max;
+    // the thr0 rerun fixes each level's guards before expanding it: a guard-
+    // corrected score that crosses thr0 then decides the expansion too
+    const bool careful = no_path;
     std::vector<BBHost> plans;
     plans.reserve((size_t)n);
     int Tmax = 1, NvMax = 1;
@@ -584,97 +587,37 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
     LGS_HIP_CHECK(hipMemsetAsync(d_counts, 0, 256, ctx->stream));
     lap(0);
 
-    // pass 2: level by level, every node the search can visit
+    // Guard records [g0, g1) of levels lv0 .. lv1: exact glibc cells; nodes
+    // with any differing cell are re-scored from host cells in place (past
+    // guard_cap records every node of those levels is re-scored).  Called once
+    // after the last level, or (careful) after each level's scoring, before
+    // its expansion: then every expansion sees exact scores.
     std::vector<BBLevel> levels((size_t)Hm + 1);   // index = Hm - h
-    unsigned long long* d_ncount = nullptr;
-    {
-        std::vector<int4> top;
-        for (int j = 0; j < n; ++j)
-            for (int x : plans[j].top_x)
-                for (int y : plans[j].top_y)
-                    for (int t = -plans[j].win_t; t <= plans[j].win_t; ++t)
-                        top.push_back(make_int4((j << 4) | Hm, x, y, t));
-        Upload up(ctx);
-        const size_t ioff = up.append(items.data(), items.size());
-        const size_t toff = up.append(top.data(), top.size());
-        up.flush();
-        const BBItem* d_items = up.at<BBItem>(ioff);
-        // scored nodes per match: its top nodes + 4 per expanded node (k_bb_expand)
-        d_ncount = (unsigned long long*)((char*)d_counts + 256);
-        LGS_HIP_CHECK(hipMemsetAsync(d_ncount, 0, sizeof(unsigned long long) * (size_t)n, ctx->stream));
-        // node/score buffers per level: grown by the host between levels
-        int cur_n = (int)top.size();
-        int4* cur_nodes = (int4*)ctx->ensure(S_BB1, sizeof(int4) * (size_t)cur_n);
-        LGS_HIP_CHECK(hipMemcpyAsync(cur_nodes, up.at<int4>(toff), sizeof(int4) * (size_t)cur_n,
-                                     hipMemcpyDeviceToDevice, ctx->stream));
-        for (int h = Hm; h >= 0; --h) {
-            BBLevel& L = levels[(size_t)(Hm - h)];
-            L.n = cur_n;
-            L.d_nodes = cur_nodes;
-            // per-level buffers: aux 2l = scores, 2l + 1 = the next level's nodes
-            L.d_scores = (double*)ctx->ensure_aux(2 * (Hm - h), sizeof(double) * (size_t)std::max(cur_n, 1));
-            if (cur_n > 0) {
-                // algorithmic bytes: 8 B per (node, valid beam) map lookup
-                double lookups = 0.0;
-                for (int j = 0; j < n; ++j) lookups += (double)plans[j].Nv;
-                const int tok = ctx->timing_begin(K_BB_SCORE, 8.0 * lookups / n * cur_n);
-                hipLaunchKernelGGL(k_bb_score, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items,
-                                   cur_nodes, cur_n, Hm - h, L.d_scores, d_guards, d_counts, gcap,
-                                   ctx->guard_eps, ctx->inject_index ? 1 : 0);
-                ctx->timing_end(tok);
-                LGS_HIP_CHECK(hipGetLastError());
-            }
-            if (h == 0 || cur_n == 0) break;
-            const int cap = 4 * cur_n;
-            int4* next = (int4*)ctx->ensure_aux(2 * (Hm - h) + 1, sizeof(int4) * (size_t)cap);
-            L.d_child = (int*)ctx->ensure_aux(2 * (kBBMaxH + 1) + (Hm - h), sizeof(int) * (size_t)cur_n);
-            LGS_HIP_CHECK(hipMemsetAsync(d_counts + 1, 0, 2 * sizeof(int), ctx->stream));
-            {
-                const int tok = ctx->timing_begin(K_BB_EXPAND, 0.0);
-                hipLaunchKernelGGL(k_bb_expand, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items,
-                                   cur_nodes, L.d_scores, cur_n, next, d_counts + 1, cap, d_counts + 2, L.d_child,
-                                   d_ncount);
-                ctx->timing_end(tok);
-                LGS_HIP_CHECK(hipGetLastError());
-            }
-            int cnt[2] = { 0, 0 };
-            LGS_HIP_CHECK(hipMemcpyAsync(cnt, d_counts + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-            ctx->sync();
-            LGS_REQUIRE(cnt[1] == 0, "branch-and-bound: child list overflow");
-            cur_n = cnt[0];
-            cur_nodes = next;
-        }
-        int ng = 0;
-        LGS_HIP_CHECK(hipMemcpyAsync(&ng, d_counts, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-        ctx->sync();
-        if (ctx->profile) ctx->harvest();
-        const int ngc = std::min(ng, gcap);
+    auto fix_guards = [&](int g0, int g1, int lv0, int lv1) {
+        const int ngc = std::max(0, std::min(g1, gcap) - g0);
         std::vector<BBGuard> guards((size_t)ngc);
         std::vector<int4> gnodes((size_t)ngc);
-        if (ngc > 0) {
+        if (ngc > 0 && g1 <= gcap) {
             // the guarded nodes' coordinates, gathered on the device
             std::vector<const int4*> lists((size_t)Hm + 1, nullptr);
-            for (int l = 0; l <= Hm; ++l) lists[(size_t)l] = levels[(size_t)l].d_nodes;
+            for (int l = 0; l <= lv1; ++l) lists[(size_t)l] = levels[(size_t)l].d_nodes;
             Upload ug(ctx);
             const size_t lo = ug.append(lists.data(), lists.size());
             ug.flush();
             int4* d_gn = (int4*)ctx->ensure(S_BB5, sizeof(int4) * (size_t)ngc);
             hipLaunchKernelGGL(k_bb_guard_nodes, dim3((ngc + 255) / 256), dim3(256), 0, ctx->stream,
-                               ug.at<const int4*>(lo), d_guards, ngc, d_gn);
+                               ug.at<const int4*>(lo), d_guards + g0, ngc, d_gn);
             LGS_HIP_CHECK(hipGetLastError());
-            LGS_HIP_CHECK(hipMemcpyAsync(guards.data(), d_guards, sizeof(BBGuard) * guards.size(),
+            LGS_HIP_CHECK(hipMemcpyAsync(guards.data(), d_guards + g0, sizeof(BBGuard) * guards.size(),
                                          hipMemcpyDeviceToHost, ctx->stream));
             LGS_HIP_CHECK(hipMemcpyAsync(gnodes.data(), d_gn, sizeof(int4) * gnodes.size(), hipMemcpyDeviceToHost,
                                          ctx->stream));
             ctx->sync();
         }
-        // guarded cells: exact glibc cells; nodes with any differing cell are
-        // re-scored from host cells in place (past guard_cap records every
-        // node of the batch is re-scored: the node lists then come back once)
         std::vector<std::pair<int, int>> dirty;   // (level id, node index)
         std::vector<int4> dnodes;
-        if (ng > gcap) {
-            for (int l = 0; l <= Hm; ++l) {
+        if (g1 > gcap) {
+            for (int l = lv0; l <= lv1; ++l) {
                 const BBLevel& L = levels[(size_t)l];
                 std::vector<int4> all((size_t)L.n);
                 if (L.n)
@@ -701,7 +644,6 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
                     dnodes.push_back(dl[k].second);
                 }
         }
-        for (int j = 0; j < n; ++j) out[j].guard_hits = 0;
         for (int k = 0; k < ngc; ++k) out[gnodes[(size_t)k].x >> 4].guard_hits += 1;
         if (!dirty.empty()) {
             const int nd_n = (int)dirty.size();
@@ -724,6 +666,8 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
                 }
                 out[j].fixups = 1;
             }
+            // (the staging is reused by the next upload only after this
+            // copy has read it: Upload::copy waits for the stream)
             Upload u2(ctx);
             const size_t co = u2.append(cells.data(), cells.size());
             const size_t no = u2.append(nvs.data(), nvs.size());
@@ -735,8 +679,90 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
                                u2.at<int>(dof), u2.at<int2>(co), u2.at<int>(no), NvMax, u2.at<double*>(so));
             LGS_HIP_CHECK(hipGetLastError());
         }
-    }
+    };
 
+    // pass 2: level by level, every node the search can visit
+    unsigned long long* d_ncount = nullptr;
+    {
+        std::vector<int4> top;
+        for (int j = 0; j < n; ++j)
+            for (int x : plans[j].top_x)
+                for (int y : plans[j].top_y)
+                    for (int t = -plans[j].win_t; t <= plans[j].win_t; ++t)
+                        top.push_back(make_int4((j << 4) | Hm, x, y, t));
+        Upload up(ctx);
+        const size_t ioff = up.append(items.data(), items.size());
+        const size_t toff = up.append(top.data(), top.size());
+        up.flush();
+        const BBItem* d_items = up.at<BBItem>(ioff);
+        if (careful) {   // the per-level guard fixes upload through the same slot
+            BBItem* keep = (BBItem*)ctx->ensure_aux(3 * (kBBMaxH + 1), sizeof(BBItem) * (size_t)n);
+            LGS_HIP_CHECK(hipMemcpyAsync(keep, d_items, sizeof(BBItem) * (size_t)n, hipMemcpyDeviceToDevice,
+                                         ctx->stream));
+            d_items = keep;
+        }
+        int gprev = 0;   // careful: guard records already fixed
+        // scored nodes per match: its top nodes + 4 per expanded node (k_bb_expand)
+        d_ncount = (unsigned long long*)((char*)d_counts + 256);
+        LGS_HIP_CHECK(hipMemsetAsync(d_ncount, 0, sizeof(unsigned long long) * (size_t)n, ctx->stream));
+        // node/score buffers per level: grown by the host between levels
+        int cur_n = (int)top.size();
+        int4* cur_nodes = (int4*)ctx->ensure(S_BB1, sizeof(int4) * (size_t)cur_n);
+        LGS_HIP_CHECK(hipMemcpyAsync(cur_nodes, up.at<int4>(toff), sizeof(int4) * (size_t)cur_n,
+                                     hipMemcpyDeviceToDevice, ctx->stream));
+        for (int h = Hm; h >= 0; --h) {
+            BBLevel& L = levels[(size_t)(Hm - h)];
+            L.n = cur_n;
+            L.d_nodes = cur_nodes;
+            // per-level buffers: aux 2l = scores, 2l + 1 = the next level's nodes
+            L.d_scores = (double*)ctx->ensure_aux(2 * (Hm - h), sizeof(double) * (size_t)std::max(cur_n, 1));
+            if (cur_n > 0) {
+                // algorithmic bytes: 8 B per (node, valid beam) map lookup
+                double lookups = 0.0;
+                for (int j = 0; j < n; ++j) lookups += (double)plans[j].Nv;
+                const int tok = ctx->timing_begin(K_BB_SCORE, 8.0 * lookups / n * cur_n);
+                hipLaunchKernelGGL(k_bb_score, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items,
+                                   cur_nodes, cur_n, Hm - h, L.d_scores, d_guards, d_counts, gcap,
+                                   ctx->guard_eps, ctx->inject_index ? 1 : 0);
+                ctx->timing_end(tok);
+                LGS_HIP_CHECK(hipGetLastError());
+            }
+            if (careful) {   // this level's guards, before its expansion
+                int ng = 0;
+                LGS_HIP_CHECK(hipMemcpyAsync(&ng, d_counts, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+                ctx->sync();
+                fix_guards(gprev, ng, Hm - h, Hm - h);
+                gprev = ng;
+            }
+            if (h == 0 || cur_n == 0) break;
+            const int cap = 4 * cur_n;
+            int4* next = (int4*)ctx->ensure_aux(2 * (Hm - h) + 1, sizeof(int4) * (size_t)cap);
+            L.d_child = (int*)ctx->ensure_aux(2 * (kBBMaxH + 1) + (Hm - h), sizeof(int) * (size_t)cur_n);
+            LGS_HIP_CHECK(hipMemsetAsync(d_counts + 1, 0, 2 * sizeof(int), ctx->stream));
+            {
+                const int tok = ctx->timing_begin(K_BB_EXPAND, 0.0);
+                hipLaunchKernelGGL(k_bb_expand, dim3((cur_n + 255) / 256), dim3(256), 0, ctx->stream, d_items,
+                                   cur_nodes, L.d_scores, cur_n, next, d_counts + 1, cap, d_counts + 2, L.d_child,
+                                   d_ncount);
+                ctx->timing_end(tok);
+                LGS_HIP_CHECK(hipGetLastError());
+            }
+            int cnt[2] = { 0, 0 };
+            LGS_HIP_CHECK(hipMemcpyAsync(cnt, d_counts + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+            ctx->sync();
+            LGS_REQUIRE(cnt[1] == 0, "branch-and-bound: child list overflow");
+            cur_n = cnt[0];
+            cur_nodes = next;
+        }
+        if (careful && ctx->profile) ctx->harvest();
+        if (!careful) {
+            int ng = 0;
+            LGS_HIP_CHECK(hipMemcpyAsync(&ng, d_counts, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+            ctx->sync();
+            if (ctx->profile) ctx->harvest();
+            fix_guards(0, ng, 0, Hm);
+        }
+    }
     lap(1);
     // the reference's search (:81-140) over the scored levels on the device
     // (k_bb_replay, one thread per match)

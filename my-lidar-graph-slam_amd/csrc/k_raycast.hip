@@ -1047,16 +1047,26 @@ bool same_pose(lgs_pose2d a, lgs_pose2d b) { return std::memcmp(&a, &b, sizeof(a
 // bitwise on the robot pose and the usable range.  Callers that may run in
 // parallel over the same scan pass store = false and store afterwards.
 typedef std::shared_ptr<const ScanHits> HitsPtr;
+// (under the scan's cache_mu: contexts may update maps from one scan at once)
+HitsPtr hits_lookup(const lgs_scan* s, const double* key)
+{
+    std::lock_guard<std::mutex> g(s->cache_mu);
+    if (s->hits_cache && std::memcmp(key, s->hits_key, 5 * sizeof(double)) == 0)
+        return std::static_pointer_cast<const ScanHits>(s->hits_cache);
+    return nullptr;
+}
+void hits_store(const lgs_scan* s, const double* key, const HitsPtr& h)
+{
+    std::lock_guard<std::mutex> g(s->cache_mu);
+    s->hits_cache = h;
+    std::memcpy(s->hits_key, key, 5 * sizeof(double));
+}
 HitsPtr cached_hits(const lgs_scan* s, lgs_pose2d robot, const lgs_builder_params* bp, bool store)
 {
     const double key[5] = { robot.x, robot.y, robot.theta, bp->usable_range_min, bp->usable_range_max };
-    if (s->hits_cache && std::memcmp(key, s->hits_key, sizeof(key)) == 0)
-        return std::static_pointer_cast<const ScanHits>(s->hits_cache);
+    if (HitsPtr c = hits_lookup(s, key)) return c;
     HitsPtr h = std::make_shared<const ScanHits>(scan_hits(s, robot, bp));
-    if (store) {
-        s->hits_cache = h;
-        std::memcpy(s->hits_key, key, sizeof(key));
-    }
+    if (store) hits_store(s, key, h);
     return h;
 }
 
@@ -1118,8 +1128,8 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
         const lgs_scan* s = scans[first[j] + k];
         const lgs_pose2d p = poses[first[j] + k];
         const double key[5] = { p.x, p.y, p.theta, bp->usable_range_min, bp->usable_range_max };
-        if (s->hits_cache && std::memcmp(key, s->hits_key, sizeof(key)) == 0)
-            jobs[j].hs[k] = std::static_pointer_cast<const ScanHits>(s->hits_cache);
+        if (HitsPtr c = hits_lookup(s, key))
+            jobs[j].hs[k] = c;
         else
             todo.push_back((int)w);
     }
@@ -1142,8 +1152,7 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
             const lgs_scan* s = scans[first[j] + k];
             const lgs_pose2d p = poses[first[j] + k];
             const double key[5] = { p.x, p.y, p.theta, bp->usable_range_min, bp->usable_range_max };
-            s->hits_cache = jobs[j].hs[k];   // (serial: a scan may appear twice)
-            std::memcpy(s->hits_key, key, sizeof(key));
+            hits_store(s, key, jobs[j].hs[k]);   // (serial: a scan may appear twice)
             auto& b = boxes[j];
             b[0] = smin(b[0], h.box[0]);
             b[1] = smin(b[1], h.box[1]);

@@ -860,6 +860,140 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
     }
 }
 
+// --------------------------------------------------------------------------
+// k_super_hv (r05): the octet superblock units straight from the planes'
+// fp16 round-up copies, one thread per (plane, unit column X4, run of kHvSeg
+// unit rows) with both 4-maxima in registers (r04's k_super_planes: one
+// workgroup per 256 x 16 tile, vertical max in registers, horizontal max
+// through LDS, every unit written as two halves by two workgroups).
+//
+// S(Y, X) = max_{i,j<4} V(Y + j, X + i) over the strip-clamped copies V:
+// padded column M - 1 of a plane rx > 0 reads column M of plane (0, ry), row
+// M - 1 of a plane ry > 0 reads row M of plane (rx, 0) (both: plane 0's (M,
+// M)) -- the map's first coarse column / row, DESIGN.md §4.1b -- and 0 past
+// the plane.  Quad q (padded rows 16 q .. 16 q + 15) of a column needs rows
+// 16 q .. 16 q + 18 at columns 4 X4 .. 4 X4 + 6 (two 8-byte loads per row:
+// plane rows are a multiple of 4 columns); the thread walks its run of quads
+// downwards (16 new rows per quad, the 3 halo rows carried), forms the
+// horizontal then the vertical max with packed u16 max (the bit patterns of
+// the nonnegative round-ups order like the values; a negative cell disables
+// the bounds) and keeps the last U8 quads' maxima, so every unit u (sub-phase
+// rows 4 u .. 4 u + 4 U8 - 1 = quads u .. u + U8 - 1) is stored whole, once:
+// a wave's lanes (consecutive X4) write 64 consecutive units per instruction.
+// Same bits as k_super_planes.  Only units that can hold a nonzero value
+// (padded rows / columns [M - 4, M + Hq / Wq)) are written; the others keep
+// the zeros written when the buffer was allocated (planes_buffer).
+struct SuperGeom {
+    int M, Wqp, Wq4, Hqp, lr;
+    long long pstride, subO, pstrideO;
+    int X4lo, ncol, ulo, nunit;       // unit columns [X4lo, X4lo + ncol), unit rows [ulo, ulo + nunit)
+};
+constexpr int kHvSeg = 4;             // unit rows per thread
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pkmax(unsigned a, unsigned b)
+{
+    return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+template <int U8>
+__global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ jobs, int nplanes, SuperGeom g)
+{
+    const Blk wg = xcd_block();
+    const PlaneJob& job = jobs[wg.z / nplanes];
+    const int p = wg.z % nplanes;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = wg.x * 64 + lane;                  // unit column offset
+    const int seg = wg.y * 4 + w;                     // run of unit rows (one per wave)
+    if (c >= g.ncol || seg * kHvSeg >= g.nunit) return;
+    const int X4 = g.X4lo + c, u0 = g.ulo + seg * kHvSeg;
+    const int nu = min(kHvSeg, g.nunit - seg * kHvSeg);
+    const int rx = p % g.lr, ry = p / g.lr;
+    typedef unsigned long long u64;
+    typedef const __attribute__((address_space(1))) u64 gu64_t;
+    typedef const __attribute__((address_space(1))) unsigned short gu16_t;
+    const unsigned short* P = job.planes16;
+    const long long rowM = (long long)g.M * g.Wqp;
+    const bool cstrip = rx > 0 && 4 * X4 + 3 == g.M - 1;   // column 3 is the column strip
+    // horizontal forward 4-max of columns 4 X4 + k (k < 4) of padded row Y
+    auto hrow = [&](int Y) -> u64 {
+        if (Y >= g.Hqp) return 0ull;
+        const bool rs = (Y == g.M - 1) && ry > 0;            // the row strip
+        const unsigned short* row = rs ? P + rx * g.pstride + rowM : P + p * g.pstride + (long long)Y * g.Wqp;
+        u64 a = *(gu64_t*)(row + 4 * X4);
+        const u64 b = *(gu64_t*)(row + 4 * X4 + 4);
+        if (cstrip) {
+            const unsigned short* src = rs ? P + rowM + g.M : P + ry * g.lr * g.pstride + (long long)Y * g.Wqp + g.M;
+            a = (a & 0x0000FFFFFFFFFFFFull) | ((u64)*(gu16_t*)src << 48);
+        }
+        // columns 0..7 as packed pairs: a = (c0 c1)(c2 c3), b = (c4 c5)(c6 c7)
+        const unsigned a0 = (unsigned)a, a1 = (unsigned)(a >> 32), b0 = (unsigned)b, b1 = (unsigned)(b >> 32);
+        const unsigned m01 = pkmax(a0, (a0 >> 16) | (a1 << 16));   // (max c0c1, max c1c2)
+        const unsigned m23 = pkmax(a1, (a1 >> 16) | (b0 << 16));   // (max c2c3, max c3c4)
+        const unsigned m45 = pkmax(b0, (b0 >> 16) | (b1 << 16));   // (max c4c5, max c5c6)
+        return (u64)pkmax(m01, m23) | ((u64)pkmax(m23, m45) << 32);   // 4-max at columns 0, 1 | 2, 3
+    };
+    // the quads' vertical maxima, a ring of U8 (slot q % U8): [k] = row k of
+    // the quad, low word columns 0, 1, high word columns 2, 3
+    u64 V[U8][16];
+    u64 hm[19];
+    auto quad = [&](u64 (&out)[16], int q, bool first) {
+        if (first) {
+#pragma unroll
+            for (int k = 0; k < 19; ++k) hm[k] = hrow(16 * q + k);
+        } else {   // rows 16 q .. 16 q + 2 are the previous quad's halo
+#pragma unroll
+            for (int k = 0; k < 3; ++k) hm[k] = hm[16 + k];
+#pragma unroll
+            for (int k = 3; k < 19; ++k) hm[k] = hrow(16 * q + k);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const u64 m = hm[k], n1 = hm[k + 1], n2 = hm[k + 2], n3 = hm[k + 3];
+            const unsigned lo = pkmax(pkmax((unsigned)m, (unsigned)n1), pkmax((unsigned)n2, (unsigned)n3));
+            const unsigned hi = pkmax(pkmax((unsigned)(m >> 32), (unsigned)(n1 >> 32)),
+                                      pkmax((unsigned)(n2 >> 32), (unsigned)(n3 >> 32)));
+            out[k] = (u64)lo | ((u64)hi << 32);
+        }
+    };
+    // sub-phase (cy, cx)'s four rows of a quad: rows 4 i + cy, column cx
+    auto half = [&](const u64 (&v)[16], int cy, int cx) -> u64 {
+        u64 h = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h |= ((v[4 * i + cy] >> (16 * cx)) & 0xFFFFull) << (16 * i);
+        return h;
+    };
+    u64* __restrict__ uo = (u64*)job.super + (long long)U8 * p * g.pstrideO;
+    static_for_step<0, U8 - 1, 1>([&](auto ss) {
+        constexpr int s = decltype(ss)::value;
+        quad(V[s], u0 + s, s == 0);
+        return true;
+    });
+    static_for_step<0, kHvSeg, 1>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        if (k >= nu) return false;
+        constexpr int last = (k + U8 - 1) % U8;
+        quad(V[last], u0 + k + U8 - 1, k + U8 - 1 == 0);
+        const long long ub = (long long)(u0 + k) * g.Wq4 + X4;
+#pragma unroll
+        for (int cy = 0; cy < 4; ++cy)
+#pragma unroll
+            for (int cx = 0; cx < 4; ++cx) {
+                u64* dst = uo + U8 * ((cy * 4 + cx) * g.subO + ub);
+                if constexpr (U8 == 2) {
+                    typedef unsigned long long u64v2 __attribute__((ext_vector_type(2)));
+                    u64v2 v;
+                    v.x = half(V[k % 2], cy, cx);
+                    v.y = half(V[(k + 1) % 2], cy, cx);
+                    gstore((u64v2*)dst, v);
+                } else {
+                    gstore(dst, half(V[k % 3], cy, cx));
+                    gstore(dst + 1, half(V[(k + 1) % 3], cy, cx));
+                    gstore(dst + 2, half(V[(k + 2) % 3], cy, cx));
+                }
+            }
+        return true;
+    });
+}
+
 // k_super: one workgroup (kSupWaves waves) per (chunk of superblocks, search
 // angle); lane = superblock, wave w sums a quarter of the beams (any order:
 // the bound absorbs the rounding; four batches of gathers in flight), LDS
@@ -3065,7 +3199,10 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
             if constexpr (c + kSmallDepth < kMaxChunks)
                 gather(c + kSmallDepth, r[c % kSmallDepth], sh[c % kSmallDepth], inr[c % kSmallDepth]);
             __builtin_amdgcn_sched_barrier(0);
-            // after this wave's rows and maxima of the chunk (in-order LDS)
+            // after this wave's rows and maxima of the chunk: the release
+            // fence orders them before the counter (lgkmcnt(0), not left to
+            // the compiler's scheduling or the LDS unit's in-order issue)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
             if (lane == 0) __hip_atomic_fetch_add(ready + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             return true;
         });
@@ -3085,6 +3222,7 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
         if (lane <= ROWS) add_row(row, min(64, Nv - c * 64), acc);
 #endif
         __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");   // the chunk's reads are done
         if (lane == 0) __hip_atomic_store(consumed, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     LGS_PROBE_MARK();
@@ -3232,7 +3370,9 @@ void set_plane_layout(RtcsmPlan& pl)
     pl.nsbx = (pl.ncx + kSB - 1) / kSB;
     pl.nsby = (pl.ncy + kSB - 1) / kSB;
     pl.M = std::max(kSB * pl.nsbx, kSB * pl.nsby);
-    pl.Wqp = (pl.Wq + 2 * pl.M + 1) & ~1;   // even: 16-byte aligned plane rows (k_precompute_planes' paired stores)
+    // a multiple of 4: 16-byte aligned fp64 plane rows (k_precompute_planes'
+    // paired stores), 8-byte aligned fp16 rows (k_super_hv's 4-column loads)
+    pl.Wqp = (pl.Wq + 2 * pl.M + 3) & ~3;
     pl.Hqp = pl.Hq + 2 * pl.M;
     pl.pstride = (long long)pl.Wqp * pl.Hqp;
     pl.Wq4 = (((pl.Wqp + 3) / 4) + 7) & ~7;   // 16-byte aligned fp16 sub-phase rows (k_super_planes' stores)
@@ -3431,11 +3571,12 @@ inline size_t plane_bytes(const RtcsmPlan& pl)
 {
     return align256(sizeof(double) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride);
 }
-// the planes' fp16 round-up copies (k_super_planes' input), right after each
-// set's fp64 planes: a fixed place per set, so their zero margins stay zero
+// the planes' fp16 round-up copies (the superblock pass's input), right after
+// each set's fp64 planes: a fixed place per set, so their zero margins stay zero
 inline size_t plane16_bytes(const RtcsmPlan& pl)
 {
-    return align256(sizeof(unsigned short) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride);
+    // (+256: k_super_hv's 8-column loads of the last row may reach 8 bytes past it)
+    return align256(sizeof(unsigned short) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride) + 256;
 }
 inline size_t set_bytes(const RtcsmPlan& pl) { return plane_bytes(pl) + plane16_bytes(pl); }
 inline size_t super_bytes(const RtcsmPlan& pl)
@@ -3452,7 +3593,8 @@ double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_su
     // with the planes only so that no stale value is ever read)
     const size_t sbytes = super_bytes(pl) * (size_t)nsets;
     SuperT* S = with_super ? (SuperT*)ctx->ensure(ctx->banked(S_SUPER), sbytes) : nullptr;
-    const long long key[4] = { pl.low_res, pl.Wq, pl.Hq, pl.M };
+    // (the unit layout too: k_super_hv leaves the all-zero units alone)
+    const long long key[4] = { pl.low_res, pl.Wq, pl.Hq, pl.M * 16 + pl.oct * 4 + pl.unit8 };
     if (D != ctx->planes_ptr[b] || std::memcmp(key, ctx->planes_key[b], sizeof(key)) != 0 ||
         nsets > ctx->planes_sets[b] || (with_super && (S != ctx->super_ptr[b] || nsets > ctx->super_sets[b]))) {
         LGS_HIP_CHECK(hipMemsetAsync(D, 0, bytes, ctx->stream));
@@ -3487,7 +3629,30 @@ struct PlaneSet {
 // map, then the superblock planes of all sets in one launch.
 struct SetJobs {
     size_t jobs_off = 0, njobs = 0, pj_off = 0, npj = 0;
+    bool hv = false;   // k_super_hv (else k_super_planes)
 };
+
+// k_super_hv applies: octet unit layout (else k_super_planes)
+inline bool hv_mode(const lgs_ctx* ctx, const RtcsmPlan& lp) { return ctx->fused_planes && lp.oct; }
+SuperGeom super_geom(const RtcsmPlan& lp)
+{
+    SuperGeom g{};
+    g.M = lp.M;
+    g.Wqp = lp.Wqp;
+    g.Wq4 = lp.Wq4;
+    g.Hqp = lp.Hqp;
+    g.lr = lp.low_res;
+    g.pstride = lp.pstride;
+    g.subO = lp.subO;
+    g.pstrideO = lp.pstrideO;
+    // units that can hold a nonzero value: padded rows / columns [M - 4, M + Hq / Wq)
+    g.X4lo = (lp.M - kSB) >> 2;
+    g.ncol = ((lp.M + lp.Wq - 1) >> 2) - g.X4lo + 1;
+    const int qlo = (lp.M - kSB) >> 4, qhi = (lp.M + lp.Hq - 1) >> 4;   // quads (16 padded rows)
+    g.ulo = std::max(0, qlo - (lp.unit8 - 1));   // unit u holds quads u .. u + unit8 - 1
+    g.nunit = qhi - g.ulo + 1;
+    return g;
+}
 
 void launch_decimate(const double* coarse, const RtcsmPlan& pl, double* D, hipStream_t st);
 SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& sets, bool need_super, Upload& up)
@@ -3505,7 +3670,11 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
     // scratch map and the phase-plane copy, and supplied coarse maps through
     // the copy; then the superblock planes of every set (one batched launch).
     // (A fused planes + superblock-planes pass from the fine map was measured
-    // slower: 1.08-1.19 ms vs 0.40 + 0.56 ms for 64 config-2 maps.)
+    // slower: 1.08-1.19 ms vs 0.40 + 0.56 ms for 64 config-2 maps in r01, and
+    // again in r05 as one streaming workgroup per 2 x 16 padded rows of units:
+    // 0.61 ms vs 0.23 + 0.21 ms -- the 15-row halo of the vertical max and
+    // the serial strips of a workgroup; r05 keeps two passes and moves the
+    // horizontal max into the precompute, sh mode.)
     std::vector<PrecompJob> jobs;
     std::vector<PlaneJob> pj;
     for (int s = 0; s < ns; ++s) {
@@ -3554,6 +3723,7 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
     sj.jobs_off = jobs.empty() ? 0 : up.append(jobs.data(), jobs.size());
     sj.npj = pj.size();
     sj.pj_off = pj.empty() ? 0 : up.append(pj.data(), pj.size());
+    sj.hv = hv_mode(ctx, lp);
     return sj;
 }
 
@@ -3567,7 +3737,8 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
             maxW = std::max(maxW, s.fine->w);
             maxH = std::max(maxH, s.fine->h);
         }
-    if (sj.njobs) launch_precompute_jobs(ctx, up.at<PrecompJob>(sj.jobs_off), (int)sj.njobs, maxW, maxH, lp.low_res);
+    if (sj.njobs)
+        launch_precompute_jobs(ctx, up.at<PrecompJob>(sj.jobs_off), (int)sj.njobs, maxW, maxH, lp.low_res);
     for (const auto& s : sets)
         if (s.half_copy) {   // planes the batched precompute did not write: their fp16 copy here
             const long long n = (long long)lp.low_res * lp.low_res * lp.pstride;
@@ -3575,7 +3746,26 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
                                s.planes16, n, const_cast<int*>(s.negflag), s.pgen);
             LGS_HIP_CHECK(hipGetLastError());
         }
-    if (sj.npj) {
+    if (sj.npj && sj.hv) {
+        const int np = lp.low_res * lp.low_res;
+        const SuperGeom g = super_geom(lp);
+        const int nseg = (g.nunit + kHvSeg - 1) / kHvSeg;
+        dim3 grid((g.ncol + 63) / 64, (nseg + 3) / 4, np * (int)sj.npj);
+        // algorithmic bytes: the copies read once (2 B per padded cell of the
+        // written units' rows) + the units written (8 B x unit8 x 16 sub-phases)
+        const double cols = (double)np * g.ncol * sj.npj, rows16 = 16.0 * g.nunit;
+        const int tok = ctx->timing_begin(K_SUPER_PLANES, cols * (rows16 * 4.0 * 2.0 + g.nunit * 16.0 * 8.0 * lp.unit8));
+        if (!ctx->skipped(K_SUPER_PLANES)) {
+            if (lp.unit8 == 3)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_hv<3>), grid, dim3(256), 0, ctx->stream,
+                                   up.at<PlaneJob>(sj.pj_off), np, g);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_hv<2>), grid, dim3(256), 0, ctx->stream,
+                                   up.at<PlaneJob>(sj.pj_off), np, g);
+        }
+        ctx->timing_end(tok);
+        LGS_HIP_CHECK(hipGetLastError());
+    } else if (sj.npj) {
         const int np = lp.low_res * lp.low_res;
         const bool lone = sj.npj == 1;
         const int spx = lone ? kSPXLone : kSPX;
@@ -4283,6 +4473,7 @@ void finish_matches(lgs_ctx* ctx, InFlight& F)
     } else {
         ctx->wait_event(ctx->bank_ev[F.bank]);
     }
+    ctx->up_busy[F.bank] = false;   // the chunk, its descriptor copy included, is complete
     std::vector<MatchItem>& items = F.items;
     const BatchShape& B = F.B;
     const std::vector<int>& gens = F.gens;

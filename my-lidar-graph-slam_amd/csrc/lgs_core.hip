@@ -207,13 +207,14 @@ void lgs_ctx::sync()
 {
     if (!spin_sync) {
         LGS_HIP_CHECK(hipStreamSynchronize(stream));
-        return;
+    } else {
+        for (;;) {
+            const hipError_t e = hipStreamQuery(stream);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) LGS_HIP_CHECK(e);
+        }
     }
-    for (;;) {
-        const hipError_t e = hipStreamQuery(stream);
-        if (e == hipSuccess) return;
-        if (e != hipErrorNotReady) LGS_HIP_CHECK(e);
-    }
+    up_busy[0] = up_busy[1] = false;
 }
 
 int lgs_ctx::timing_begin(int kernel, double algo_bytes)
@@ -453,6 +454,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_FINE_STAGED: ctx->fine_staged = value != 0.0; return LGS_OK;
     case LGS_OPT_SMALL_WINDOW: ctx->small_window = value != 0.0; return LGS_OK;
     case LGS_OPT_POST_RECORDS: ctx->post_records = value != 0.0; return LGS_OK;
+    case LGS_OPT_FUSED_PLANES: ctx->fused_planes = value != 0.0; return LGS_OK;
     case LGS_OPT_SORT_BARRIER_US:
         if (value < 0) return LGS_ERR_INVALID_ARG;
         ctx->sort_barrier_us = (long long)value;
@@ -1298,10 +1300,13 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n, Upload* 
 // ScanRangeMax; the upload happens once per (scan, matcher).
 const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* s, double rmax, int* nv)
 {
+    std::lock_guard<std::mutex> g(s->cache_mu);   // two contexts may match this scan at once
     if (!(s->cached_rmax == rmax)) {
-        s->h_vidx.clear();
+        std::vector<int> v;
         for (int i = 0; i < s->n; ++i)
-            if (!(s->h_ranges[i] >= rmax)) s->h_vidx.push_back(i);
+            if (!(s->h_ranges[i] >= rmax)) v.push_back(i);
+        if (!s->h_vidx.empty()) s->vidx_old.push_back(std::move(s->h_vidx));
+        s->h_vidx = std::move(v);
         s->nv = (int)s->h_vidx.size();
         s->cached_rmax = rmax;
     }

@@ -273,6 +273,7 @@ struct lgs_ctx {
     bool peer_staged = false;    // cross-context copies through host memory (LGS_OPT_PEER_COPY)
     int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
     bool small_window = true;    // one-launch search of one-block windows (LGS_OPT_SMALL_WINDOW)
+    bool fused_planes = true;    // planes + superblock units in one pass (LGS_OPT_FUSED_PLANES)
     bool post_records = true;    // records written to pinned memory by k_post + a flag (LGS_OPT_POST_RECORDS)
     long long copies_direct = 0, copies_staged = 0;   // lgs_debug_copy_counters
     int lanes_min_batch = 2;     // pruned coarse stage: the work list (k_coarse_list) from this batch size on (LGS_OPT_LANES_MIN_BATCH)
@@ -305,6 +306,10 @@ struct lgs_ctx {
     // bank 1 (two chunks in flight): descriptor staging and record copies
     void* pinned_up_b = nullptr;
     size_t pinned_up_b_bytes = 0;
+    // a copy out of bank b's descriptor staging may still be reading it
+    // (set by Upload::copy, cleared by sync() and when the bank's chunk is
+    // known complete); the next Upload::copy into that staging waits first
+    bool up_busy[2] = { false, false };
     void* pinned_rec[2] = {};
     size_t pinned_rec_bytes[2] = {};
     int bank = 0;                // which bank the per-batch buffers come from
@@ -503,6 +508,11 @@ struct lgs_scan {
     double cached_rmax = NAN;
     int nv = 0;
     std::vector<int> h_vidx;      // host copy (guard re-projection); the device compacts itself
+    // the compaction is built once per ScanRangeMax, under cache_mu: contexts
+    // may match one scan at the same time; a replaced list stays alive (its
+    // readers may still hold it) in vidx_old.  cache_mu also guards hits_cache.
+    mutable std::mutex cache_mu;
+    std::vector<std::vector<int>> vidx_old;
     // hit points of the last (robot pose, usable range) they were computed for
     // (k_raycast.hip scan_hits): the frontend inserts a scan at its estimated
     // pose and then rebuilds the latest map from it at that same pose 10 times
@@ -640,16 +650,31 @@ struct Upload {
     void copy()
     {
         const size_t b = std::max<size_t>(host.size(), 16);
+        // the staging is shared by every upload of this bank: an earlier
+        // upload's copy still queued on the stream must have read it first
+        if (ctx->up_busy[ctx->bank]) ctx->sync();
         char* pin = (char*)ctx->ensure_pinned_up(b);
         std::memcpy(pin, host.data(), host.size());
         std::vector<FetchSeg> segs;
-        if (host.size() <= kFetchMaxBytes)
-            segs.push_back(fetch_seg(dev, pin, host.size()));
-        else   // bulk (branch-and-bound node lists): the copy engine
-            LGS_HIP_CHECK(hipMemcpyAsync(dev, pin, host.size(), hipMemcpyHostToDevice, ctx->stream));
-        segs.insert(segs.end(), extra.begin(), extra.end());
-        extra.clear();
-        fetch_list(ctx, segs);
+        try {
+            if (host.size() <= kFetchMaxBytes)
+                segs.push_back(fetch_seg(dev, pin, host.size()));
+            else   // bulk (branch-and-bound node lists): the copy engine
+                LGS_HIP_CHECK(hipMemcpyAsync(dev, pin, host.size(), hipMemcpyHostToDevice, ctx->stream));
+            segs.insert(segs.end(), extra.begin(), extra.end());
+            extra.clear();
+            fetch_list(ctx, segs);
+        } catch (...) {
+            // the scans' copies were never (all) enqueued: unpublish them so
+            // no other call reads their uninitialised device copies
+            extra.clear();
+            if (fence) abandon_scan_copies(ctx, fence, fence_scans);
+            fence.reset();
+            fence_scans.clear();
+            ctx->up_busy[ctx->bank] = true;   // a part may have been queued
+            throw;
+        }
+        ctx->up_busy[ctx->bank] = true;
         if (fence) fence->set(1);
         fence.reset();
         fence_scans.clear();

@@ -37,6 +37,7 @@ LGS_OPT_SORT_BARRIER_US = 23
 LGS_OPT_FINE_STAGED = 24
 LGS_OPT_SMALL_WINDOW = 25
 LGS_OPT_POST_RECORDS = 26
+LGS_OPT_FUSED_PLANES = 27
 KERNEL_IDS = ["k_project", "k_coarse", "k_seed", "k_select", "k_fine", "k_replay", "k_cost", "k_precompute",
               "k_linsolve", "k_ray_emit", "k_ray_apply", "k_super", "k_super_planes", "k_bb_score",
               "k_bb_expand", "k_coarse_aux", "k_match_small"]   # lgs_ctx_kernel_stats order
@@ -306,6 +307,10 @@ class Context:
         if rc != LGS_OK:
             raise LgsError(f"lgs_ctx_create(device={device}) failed with status {rc}")
         self.h = h
+        # A/B runs: LGS_CTX_OPTIONS="ID=VALUE,ID=VALUE" applied to every new context
+        for kv in filter(None, os.environ.get("LGS_CTX_OPTIONS", "").split(",")):
+            k, v = kv.split("=")
+            self.set_option(int(k), float(v))
 
     def check(self, rc: int, what: str):
         if rc != LGS_OK:

@@ -124,6 +124,38 @@ def test_bb_fixups(ctx, world, small_map):
     assert_bb_same(gpu, oracle_bb(cells, mx, my, 0.05, prm, r, ang, init), "inject")
 
 
+@pytest.mark.parametrize("eps", [3e-4, 1e-2])
+def test_bb_fixups_batch_small_scans(ctx, world, small_map, eps):
+    """A 64-candidate batch of 17-beam scans with injected guard corruption:
+    few dirty nodes make the re-score's upload (cells, pointer arrays) smaller
+    than the replay's upload that follows it in the same staging buffer -- the
+    replay's staging must not overwrite it before the re-score's copy read it
+    (ADVICE r04)."""
+    cells, mx, my = small_map
+    ang = scene.beam_angles(17)
+    prm = (3, 0.8, 0.8, 0.3, 20.0, 0.01, 20.0)
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    pyr = ctx.precompute_pyramid(g, 3)
+    rng = np.random.default_rng(99)
+    scans, inits, rs = [], [], []
+    for _ in range(64):
+        true = (rng.uniform(-0.8, 0.8), rng.uniform(-0.8, 0.8), rng.uniform(-3, 3))
+        r = scene.ray_cast(world, true, ang)
+        rs.append(r)
+        scans.append(ctx.scan(r, ang))
+        inits.append((true[0] + rng.uniform(-0.2, 0.2), true[1] + rng.uniform(-0.2, 0.2), true[2] + 0.05))
+    try:
+        ctx.set_option(abi.LGS_OPT_GUARD_EPS, eps)
+        ctx.set_option(abi.LGS_OPT_INJECT_INDEX, 1)
+        out = ctx.bb_optimize_pose_batch(g, pyr, abi.BBParams(*prm), launcher_cost(), scans, inits, 0.3)
+    finally:
+        ctx.set_option(abi.LGS_OPT_INJECT_INDEX, 0)
+        ctx.set_option(abi.LGS_OPT_GUARD_EPS, 1e-9)
+    assert sum(o.fixups for o in out) >= 1
+    for j, o in enumerate(out):
+        assert_bb_same(o, oracle_bb(cells, mx, my, 0.05, prm, rs[j], ang, inits[j], thr=0.3), f"cand{j}")
+
+
 def test_loop_detect_bb(ctx, world):
     """LoopDetectorBranchBound::Detect over two local maps of different size."""
     maps = [build_map(world, n, 0.05, 100, scene.arc_poses(k), n_beams=541) for n, k in ((300, 4), (400, 6))]

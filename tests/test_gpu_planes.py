@@ -22,14 +22,26 @@ def layout(W, H, res, lr, rx, ry):
     nsbx, nsby = (ncx + 3) // 4, (ncy + 3) // 4
     M = 4 * max(nsbx, nsby)
     Wq, Hq = -(-W // lr), -(-H // lr)
-    Wqp = (Wq + 2 * M + 1) & ~1
+    Wqp = (Wq + 2 * M + 3) & ~3
     Hqp = Hq + 2 * M
     Wq4, Hq4 = ((-(-Wqp // 4)) + 7) & ~7, -(-Hqp // 4)
-    # octet layout (k_rtcsm.hip set_plane_layout) for windows of <= 5 x 5 superblocks
-    oct = nsbx <= 5 and nsby <= 5
+    # octet layout (k_rtcsm.hip set_plane_layout) for windows of <= 9 x 9
+    # superblocks: 16-byte units (rows 4q .. 4q + 7), 24-byte units (rows
+    # 4q .. 4q + 11) for windows of more than 5 superblock rows
+    oct = nsbx <= 9 and nsby <= 9 and nsbx * nsby <= 64
+    u8 = 3 if oct and nsby > 5 else 2
     Qo = (Hq4 + 3) // 4 + 1
     return dict(M=M, Wq=Wq, Hq=Hq, Wqp=Wqp, Hqp=Hqp, Wq4=Wq4, Hq4=Hq4, sub4=Wq4 * Hq4, oct=oct, Qo=Qo,
-                subO=Qo * Wq4)
+                subO=Qo * Wq4, u8=u8)
+
+
+def half_round_up(x):
+    """fp16 rounded toward +inf (k_rtcsm.hip half_round_up_bits), +0 for zeros"""
+    h = x.astype(np.float16)
+    lo = h.astype(np.float64) < x
+    h[lo] = np.nextafter(h[lo], np.float16(np.inf))
+    h[x == 0] = 0
+    return h
 
 
 def expected_planes(cells, lr, L):
@@ -61,8 +73,9 @@ def clamp_strip(P, lr, M):
 
 
 def check_super(P, S, lr, L):
-    """S (fp16, sub-phase layout) >= the forward 4x4 max of every (strip-clamped)
-    plane, by at most one fp16 ulp"""
+    """S (fp16, sub-phase layout) == the forward 4x4 max of every (strip-clamped)
+    plane rounded up to fp16 (bit-exact: round-up is monotone, so the max of the
+    round-ups is the round-up of the max)"""
     Hqp, Wqp = L["Hqp"], L["Wqp"]
     pad = np.zeros((lr * lr, Hqp + 3, Wqp + 3))
     pad[:, :Hqp, :Wqp] = clamp_strip(P, lr, L["M"])
@@ -75,34 +88,47 @@ def check_super(P, S, lr, L):
                 if L["oct"]:
                     # units (q, X) of 8 halfs = rows 4q .. 4q + 7: rows from the low
                     # halves, and every high half equals the next unit's low half
-                    o = (p * 16 + sy * 4 + sx) * L["subO"] * 8
-                    u = S[o:o + L["subO"] * 8].reshape(L["Qo"], L["Wq4"], 8)
+                    h = 4 * L["u8"]   # halfs per unit
+                    o = (p * 16 + sy * 4 + sx) * L["subO"] * h
+                    u = S[o:o + L["subO"] * h].reshape(L["Qo"], L["Wq4"], h)
                     blk = u[:, :, :4].transpose(0, 2, 1).reshape(4 * L["Qo"], L["Wq4"])[:L["Hq4"]]
-                    assert np.array_equal(u[:-2, :, 4:], u[1:-1, :, :4]), (p, sy, sx)
+                    assert np.array_equal(u[:-2, :, 4:8], u[1:-1, :, :4]), (p, sy, sx)
+                    if L["u8"] == 3:
+                        assert np.array_equal(u[:-3, :, 8:12], u[2:-1, :, :4]), (p, sy, sx)
                 else:
                     blk = S[p * pstride4 + (sy * 4 + sx) * L["sub4"]:][:L["sub4"]].reshape(L["Hq4"], L["Wq4"])
                 ys, xs = np.arange(sy, Hqp, 4), np.arange(sx, Wqp, 4)
                 got[np.ix_(ys, xs)] = blk[:len(ys), :len(xs)].astype(np.float64)
-        assert np.all(got >= m[p]), p
-        ulp = np.spacing(got.astype(np.float16)).astype(np.float64)
-        assert np.all(got - m[p] <= ulp), p
+        want = half_round_up(m[p]).astype(np.float64)
+        assert np.array_equal(got, want), (p, np.argwhere(got != want)[:4])
 
 
-@pytest.mark.parametrize("lr,n,batch", [(5, 400, 1), (5, 400, 3), (4, 200, 2), (2, 150, 2), (8, 240, 1), (3, 100, 2)])
-def test_device_coarse_planes(ctx, world, lr, n, batch):
+@pytest.mark.parametrize("lr,n,batch,rxy,fused", [
+    (5, 400, 1, (1.0, 1.2), 1), (5, 400, 3, (1.0, 1.2), 1), (4, 200, 2, (1.0, 1.2), 1), (2, 150, 2, (1.0, 1.2), 1),
+    (8, 240, 1, (1.0, 1.2), 1), (3, 100, 2, (1.0, 1.2), 1),
+    # config-2 window (5 x 5 superblocks) and a 6 x 7 window (24-byte units),
+    # planes + units in one pass (k_planes_super) and in two (precompute +
+    # k_super_planes); maps not a multiple of 16 coarse rows, 80-row quads
+    (5, 400, 2, (4.0, 4.0), 1), (5, 400, 2, (4.0, 4.0), 0), (5, 455, 2, (5.0, 5.4), 1), (5, 455, 2, (5.0, 5.4), 0),
+    (5, 1000, 2, (4.0, 4.0), 1), (5, 35, 2, (1.0, 1.2), 1)])
+def test_device_coarse_planes(ctx, world, lr, n, batch, rxy, fused):
     rng = np.random.default_rng(lr * 100 + n)
     cells = np.where(rng.random((n, n)) < 0.3, rng.choice([0.001, 0.3, 0.45, 0.6, 0.999], (n, n)), 0.0)
     mx = my = -0.05 * n / 2
     g = ctx.grid_from_array(cells, mx, my, 0.05)
     ang = scene.beam_angles(361)
     scans = [ctx.scan(rng.uniform(0.5, 4.0, 361), ang) for _ in range(batch)]
-    P = abi.RtcsmParams(lr, 1.0, 1.2, 0.3, 20.0)
+    P = abi.RtcsmParams(lr, rxy[0], rxy[1], 0.3, 20.0)
     inits = [(rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5), rng.uniform(-3, 3)) for _ in range(batch)]
-    if batch == 1:
-        ctx.optimize_pose_query(g, P, launcher_cost(), scans[0], inits[0])
-    else:
-        ctx.optimize_pose_query_batch(g, P, launcher_cost(), scans, inits)
-    L = layout(n, n, 0.05, lr, 1.0, 1.2)
+    try:
+        ctx.set_option(abi.LGS_OPT_FUSED_PLANES, fused)
+        if batch == 1:
+            ctx.optimize_pose_query(g, P, launcher_cost(), scans[0], inits[0])
+        else:
+            ctx.optimize_pose_query_batch(g, P, launcher_cost(), scans, inits)
+    finally:
+        ctx.set_option(abi.LGS_OPT_FUSED_PLANES, 1)
+    L = layout(n, n, 0.05, lr, rxy[0], rxy[1])
     want = expected_planes(cells, lr, L)
     for j in range(batch):
         got = ctx.debug_buffer("planes", j)[:want.size].reshape(want.shape)
