@@ -179,6 +179,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_SMALL_WINDOW  25  /* 1 (default) = windows with one coarse block per angle (2 winX < LowRes, 2 winY < LowRes, LowRes 2..7, map width >= LowRes, <= 2048 valid beams) search in one launch (k_match_small: no coarse map), 0 = the general path */
 #define LGS_OPT_POST_RECORDS  26  /* 1 (default) = a match call's result records reach the host through a kernel that writes them (and a completion flag) into pinned memory, the host spinning on the flag; 0 = a device-to-host copy and a stream event */
 #define LGS_OPT_FUSED_PLANES  27  /* 1 (default) = the per-query coarse-map precompute writes the phase planes AND the octet superblock units in one pass from the fine map (k_planes_super, LowRes 5), 0 = the precompute + k_super_planes passes */
+#define LGS_OPT_PRIORITY_TAIL 28  /* 0 (default) = one stream; 1 = a correlative batch's stages after the coarse-map builds run on a second stream of the device's highest priority (behind an event), so that other contexts' plane builds cannot queue ahead of its latency-bound tail */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

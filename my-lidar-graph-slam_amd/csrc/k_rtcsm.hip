@@ -862,136 +862,102 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
 
 // --------------------------------------------------------------------------
 // k_super_hv (r05): the octet superblock units straight from the planes'
-// fp16 round-up copies, one thread per (plane, unit column X4, run of kHvSeg
-// unit rows) with both 4-maxima in registers (r04's k_super_planes: one
-// workgroup per 256 x 16 tile, vertical max in registers, horizontal max
-// through LDS, every unit written as two halves by two workgroups).
+// fp16 round-up copies, one thread per (plane, quad qt, unit column X4) with
+// both 4-maxima in registers (r04's k_super_planes: one workgroup per 256 x 16
+// tile, vertical max in registers, horizontal max through LDS).
 //
 // S(Y, X) = max_{i,j<4} V(Y + j, X + i) over the strip-clamped copies V:
 // padded column M - 1 of a plane rx > 0 reads column M of plane (0, ry), row
 // M - 1 of a plane ry > 0 reads row M of plane (rx, 0) (both: plane 0's (M,
 // M)) -- the map's first coarse column / row, DESIGN.md §4.1b -- and 0 past
-// the plane.  Quad q (padded rows 16 q .. 16 q + 15) of a column needs rows
-// 16 q .. 16 q + 18 at columns 4 X4 .. 4 X4 + 6 (two 8-byte loads per row:
-// plane rows are a multiple of 4 columns); the thread walks its run of quads
-// downwards (16 new rows per quad, the 3 halo rows carried), forms the
-// horizontal then the vertical max with packed u16 max (the bit patterns of
-// the nonnegative round-ups order like the values; a negative cell disables
-// the bounds) and keeps the last U8 quads' maxima, so every unit u (sub-phase
-// rows 4 u .. 4 u + 4 U8 - 1 = quads u .. u + U8 - 1) is stored whole, once:
-// a wave's lanes (consecutive X4) write 64 consecutive units per instruction.
-// Same bits as k_super_planes.  Only units that can hold a nonzero value
-// (padded rows / columns [M - 4, M + Hq / Wq)) are written; the others keep
-// the zeros written when the buffer was allocated (planes_buffer).
+// the plane.  A thread loads rows 16 qt .. 16 qt + 18 at columns 4 X4 ..
+// 4 X4 + 6 (two 8-byte loads per row: plane rows are a multiple of 4
+// columns), forms the horizontal then the vertical max with packed u16 max
+// (bit patterns of the nonnegative round-ups order like the values; a
+// negative cell disables the bounds), and stores the 16 sub-phases' halves of
+// rows 4 qt .. 4 qt + 3: the low half of unit qt, the high half of unit
+// qt - 1 (24-byte units: the top third of qt - 2).  Threads are (quad, unit
+// column) pairs, column fastest: no idle lanes, and a workgroup's quads are
+// consecutive, so the two halves of a unit meet in one L2.  Same bits as
+// k_super_planes.  Only units that can hold a nonzero value (padded rows /
+// columns [M - 4, M + Hq / Wq)) are written; the others keep the zeros
+// written when the buffer was allocated (planes_buffer).  (Measured and
+// rejected: a thread walking a run of 4 unit rows down its column, carrying
+// the halo rows and storing each unit whole -- 1.0 vs 0.18 ms per 64
+// config-2 sets: the ring of the last quads' maxima went to scratch.)
 struct SuperGeom {
-    int M, Wqp, Wq4, Hqp, lr;
+    int M, Wqp, Wq4, unit8, Hqp;
     long long pstride, subO, pstrideO;
-    int X4lo, ncol, ulo, nunit;       // unit columns [X4lo, X4lo + ncol), unit rows [ulo, ulo + nunit)
+    int X4lo, ncol, qlo, nqt, lr;     // unit columns [X4lo, X4lo + ncol), quads [qlo, qlo + nqt)
 };
-constexpr int kHvSeg = 4;             // unit rows per thread
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pkmax(unsigned a, unsigned b)
 {
     return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
 }
-template <int U8>
 __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ jobs, int nplanes, SuperGeom g)
 {
     const Blk wg = xcd_block();
     const PlaneJob& job = jobs[wg.z / nplanes];
     const int p = wg.z % nplanes;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = wg.x * 64 + lane;                  // unit column offset
-    const int seg = wg.y * 4 + w;                     // run of unit rows (one per wave)
-    if (c >= g.ncol || seg * kHvSeg >= g.nunit) return;
-    const int X4 = g.X4lo + c, u0 = g.ulo + seg * kHvSeg;
-    const int nu = min(kHvSeg, g.nunit - seg * kHvSeg);
+    const int tq = wg.x * 256 + threadIdx.x;        // (quad, unit column), column fastest
+    const int qi = tq / g.ncol, c = tq - qi * g.ncol;
+    if (qi >= g.nqt) return;
+    const int X4 = g.X4lo + c, qt = g.qlo + qi;
     const int rx = p % g.lr, ry = p / g.lr;
     typedef unsigned long long u64;
     typedef const __attribute__((address_space(1))) u64 gu64_t;
     typedef const __attribute__((address_space(1))) unsigned short gu16_t;
     const unsigned short* P = job.planes16;
     const long long rowM = (long long)g.M * g.Wqp;
-    const bool cstrip = rx > 0 && 4 * X4 + 3 == g.M - 1;   // column 3 is the column strip
-    // horizontal forward 4-max of columns 4 X4 + k (k < 4) of padded row Y
-    auto hrow = [&](int Y) -> u64 {
-        if (Y >= g.Hqp) return 0ull;
+    // the column strip: column 3 of unit column (M - 1) / 4 in planes rx > 0
+    const bool cstrip = rx > 0 && 4 * X4 + 3 == g.M - 1;
+    u64 hm[19];   // horizontal forward 4-max of columns 4 X4 + k, k < 4, per row
+#pragma unroll
+    for (int k = 0; k < 19; ++k) {
+        const int Y = 16 * qt + k;
         const bool rs = (Y == g.M - 1) && ry > 0;            // the row strip
         const unsigned short* row = rs ? P + rx * g.pstride + rowM : P + p * g.pstride + (long long)Y * g.Wqp;
-        u64 a = *(gu64_t*)(row + 4 * X4);
-        const u64 b = *(gu64_t*)(row + 4 * X4 + 4);
-        if (cstrip) {
+        const bool in = Y < g.Hqp;
+        u64 a = in ? *(gu64_t*)(row + 4 * X4) : 0ull;
+        const u64 b = in ? *(gu64_t*)(row + 4 * X4 + 4) : 0ull;
+        if (cstrip) {   // column M - 1 reads column M of plane (0, ry) (row strip: plane 0)
             const unsigned short* src = rs ? P + rowM + g.M : P + ry * g.lr * g.pstride + (long long)Y * g.Wqp + g.M;
-            a = (a & 0x0000FFFFFFFFFFFFull) | ((u64)*(gu16_t*)src << 48);
+            const u64 v = in ? (u64)*(gu16_t*)src : 0ull;
+            a = (a & 0x0000FFFFFFFFFFFFull) | (v << 48);
         }
         // columns 0..7 as packed pairs: a = (c0 c1)(c2 c3), b = (c4 c5)(c6 c7)
         const unsigned a0 = (unsigned)a, a1 = (unsigned)(a >> 32), b0 = (unsigned)b, b1 = (unsigned)(b >> 32);
         const unsigned m01 = pkmax(a0, (a0 >> 16) | (a1 << 16));   // (max c0c1, max c1c2)
         const unsigned m23 = pkmax(a1, (a1 >> 16) | (b0 << 16));   // (max c2c3, max c3c4)
         const unsigned m45 = pkmax(b0, (b0 >> 16) | (b1 << 16));   // (max c4c5, max c5c6)
-        return (u64)pkmax(m01, m23) | ((u64)pkmax(m23, m45) << 32);   // 4-max at columns 0, 1 | 2, 3
-    };
-    // the quads' vertical maxima, a ring of U8 (slot q % U8): [k] = row k of
-    // the quad, low word columns 0, 1, high word columns 2, 3
-    u64 V[U8][16];
-    u64 hm[19];
-    auto quad = [&](u64 (&out)[16], int q, bool first) {
-        if (first) {
+        hm[k] = (u64)pkmax(m01, m23) | ((u64)pkmax(m23, m45) << 32);   // 4-max at columns 0, 1 | 2, 3
+    }
+    unsigned vlo[16], vhi[16];   // vertical forward 4-max
 #pragma unroll
-            for (int k = 0; k < 19; ++k) hm[k] = hrow(16 * q + k);
-        } else {   // rows 16 q .. 16 q + 2 are the previous quad's halo
+    for (int k = 0; k < 16; ++k) {
+        vlo[k] = pkmax(pkmax((unsigned)hm[k], (unsigned)hm[k + 1]), pkmax((unsigned)hm[k + 2], (unsigned)hm[k + 3]));
+        vhi[k] = pkmax(pkmax((unsigned)(hm[k] >> 32), (unsigned)(hm[k + 1] >> 32)),
+                       pkmax((unsigned)(hm[k + 2] >> 32), (unsigned)(hm[k + 3] >> 32)));
+    }
+    u64* __restrict__ uo = (u64*)job.super + (long long)g.unit8 * p * g.pstrideO;
+    const int u8 = g.unit8;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) hm[k] = hm[16 + k];
+    for (int cy = 0; cy < 4; ++cy) {
 #pragma unroll
-            for (int k = 3; k < 19; ++k) hm[k] = hrow(16 * q + k);
-        }
+        for (int cx = 0; cx < 4; ++cx) {
+            u64 h = 0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const u64 m = hm[k], n1 = hm[k + 1], n2 = hm[k + 2], n3 = hm[k + 3];
-            const unsigned lo = pkmax(pkmax((unsigned)m, (unsigned)n1), pkmax((unsigned)n2, (unsigned)n3));
-            const unsigned hi = pkmax(pkmax((unsigned)(m >> 32), (unsigned)(n1 >> 32)),
-                                      pkmax((unsigned)(n2 >> 32), (unsigned)(n3 >> 32)));
-            out[k] = (u64)lo | ((u64)hi << 32);
-        }
-    };
-    // sub-phase (cy, cx)'s four rows of a quad: rows 4 i + cy, column cx
-    auto half = [&](const u64 (&v)[16], int cy, int cx) -> u64 {
-        u64 h = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) h |= ((v[4 * i + cy] >> (16 * cx)) & 0xFFFFull) << (16 * i);
-        return h;
-    };
-    u64* __restrict__ uo = (u64*)job.super + (long long)U8 * p * g.pstrideO;
-    static_for_step<0, U8 - 1, 1>([&](auto ss) {
-        constexpr int s = decltype(ss)::value;
-        quad(V[s], u0 + s, s == 0);
-        return true;
-    });
-    static_for_step<0, kHvSeg, 1>([&](auto kk) {
-        constexpr int k = decltype(kk)::value;
-        if (k >= nu) return false;
-        constexpr int last = (k + U8 - 1) % U8;
-        quad(V[last], u0 + k + U8 - 1, k + U8 - 1 == 0);
-        const long long ub = (long long)(u0 + k) * g.Wq4 + X4;
-#pragma unroll
-        for (int cy = 0; cy < 4; ++cy)
-#pragma unroll
-            for (int cx = 0; cx < 4; ++cx) {
-                u64* dst = uo + U8 * ((cy * 4 + cx) * g.subO + ub);
-                if constexpr (U8 == 2) {
-                    typedef unsigned long long u64v2 __attribute__((ext_vector_type(2)));
-                    u64v2 v;
-                    v.x = half(V[k % 2], cy, cx);
-                    v.y = half(V[(k + 1) % 2], cy, cx);
-                    gstore((u64v2*)dst, v);
-                } else {
-                    gstore(dst, half(V[k % 3], cy, cx));
-                    gstore(dst + 1, half(V[(k + 1) % 3], cy, cx));
-                    gstore(dst + 2, half(V[(k + 2) % 3], cy, cx));
-                }
+            for (int i = 0; i < 4; ++i) {
+                const unsigned wv = (cx < 2) ? vlo[4 * i + cy] : vhi[4 * i + cy];
+                h |= (u64)((cx & 1) ? (wv >> 16) : (wv & 0xFFFFu)) << (16 * i);
             }
-        return true;
-    });
+            const long long u = (cy * 4 + cx) * g.subO + (long long)qt * g.Wq4 + X4;
+            gstore(uo + u8 * u, h);                                          // rows 4 qt .. of unit qt
+            if (qt > 0) gstore(uo + (u8 * (u - g.Wq4) + 1), h);              // .. of unit qt - 1
+            if (u8 == 3 && qt > 1) gstore(uo + (3 * (u - 2 * g.Wq4) + 2), h);   // .. of unit qt - 2
+        }
+    }
 }
 
 // k_super: one workgroup (kSupWaves waves) per (chunk of superblocks, search
@@ -1534,7 +1500,7 @@ struct WorkList {
     int* al;
     int region, tmax;
 };
-constexpr int kListMaxNv = 4096;   // k_coarse_list stages four beam rows in LDS (64 KB)
+constexpr int kListMaxNv = 4096;   // work-list batches: Nv bound (the unsafe test stages an angle's edge beams)
 // grid sizes measured (config 5 / config 2 stage ms): list 2048 + unsafe 1024: 0.272 / 0.373; 2048 + 4096:
 // 0.241 / 0.375; 4096 + 4096: 0.226 / 0.364; 2304 + 4096: 0.226 / 0.365; 1024 + 4096: 0.288 / 0.528
 #ifndef LGS_LIST_WAVES
@@ -1595,71 +1561,14 @@ __device__ __forceinline__ int list_prefix(const WorkList& W, int which, int n, 
 
 // Four listed superblocks per wave (grid-stride over the list): lane =
 // (superblock, member block), every lane walks the beams in order with
-// pipelined gathers (seq_sum: the reference's sequential fp64 sum).  cflag is 0 here; k_unsafe_list
-// then redoes the edge angles' blocks.
-__global__ __launch_bounds__(64) void k_coarse_list(Items items, WorkList W, int n, int rowlen,
-                                                    const double* __restrict__ zero)
-{
-    extern __shared__ int s_cb[];   // [4][rowlen]: each group's coarse-base row
-    const int lane = threadIdx.x, g4 = lane >> 4, m = lane & 15;
-    int c;
-    const int total = list_prefix(W, 0, n, c);
-    for (int e0 = 4 * blockIdx.x; e0 < total; e0 += 4 * gridDim.x) {   // wave-uniform
-        const int e = e0 + g4;
-        const bool has = e < total;
-        // item of entry e = the number of items whose inclusive prefix is <= e
-        int j = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int jq = __popcll(__ballot(lane < n && c <= e0 + q));
-            if (g4 == q) j = jq;
-        }
-        if (!has) j = 0;
-        const int cprev = __shfl(c, max(j - 1, 0), 64);
-        const int before = j > 0 ? cprev : 0;
-        const MatchItem& it = items[j];
-        const RtcsmPlan& pl = it.pl;
-        const int ent = has ? W.sbl[(size_t)j * W.region + (e - before)] : 0;
-        const int t = ent >> 6, sb = ent & 63;
-        const int Nv = has ? pl.Nv : 0;
-        const int* __restrict__ cbr = it.cbase + (size_t)t * pl.Nv;
-        __syncthreads();   // the previous round's rows are read
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int nq = __shfl(Nv, 16 * q, 64);
-            const int* row = (const int*)__shfl((unsigned long long)cbr, 16 * q, 64);
-            for (int v = lane; v < nq; v += 64) s_cb[q * rowlen + v] = row[v];
-        }
-        __syncthreads();
-        int nmax = Nv;
-#pragma unroll
-        for (int off = 16; off < 64; off <<= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
-        const int nsbx = max(pl.nsbx, 1);
-        const int jx = kSB * (sb % nsbx) + (m & 3), jy = kSB * (sb / nsbx) + (m >> 2);
-        const bool active = has && jx < pl.ncx && jy < pl.ncy;
-        const double* __restrict__ lane_base = it.cmap + (active ? jy * pl.Wqp + jx : 0);
-        const int* __restrict__ my = s_cb + g4 * rowlen;
-        // past this lane's own row (v >= Nv, within the look-ahead): the zero cell
-        constexpr int kOff = -(1 << 30);
-        const double sum = seq_sum<int>(nmax, [&](int v) { return v < Nv ? my[min(v, rowlen - 1)] : kOff; },
-                                        [&](const int& cc) { return (active && cc != kOff) ? lane_base + cc : zero; });
-        if (active) {
-            const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
-            it.cscore[k] = sum;
-            it.cflag[k] = 0;
-        }
-    }
-}
-
-// k_coarse_list with the four beam rows staged in chunks of kLC beams (4 KB
-// of LDS per wave instead of 4 * Nv ints, 17 KB for config 2, which capped
-// the kernel at 9 waves per CU): the next chunk is loaded into registers
-// while the current one is summed, then written to LDS; the sum carries over
-// the chunks in beam order (seq_sum_from).  The same sums as k_coarse_list.
-#ifndef LGS_LIST_CHUNK
-#define LGS_LIST_CHUNK 256
-#endif
-constexpr int kLC = LGS_LIST_CHUNK > 0 ? LGS_LIST_CHUNK : 256;
+// pipelined gathers (seq_sum: the reference's sequential fp64 sum); cflag is
+// 0 here, k_unsafe_list then redoes the edge angles' blocks.  The four beam
+// rows are staged in chunks of kLC beams (4 KB of LDS per wave; r03's whole
+// rows, 4 * Nv ints = 17 KB for config 2, capped the kernel at 9 waves per
+// CU): the next chunk is loaded into registers while the current one is
+// summed, then written to LDS; the sum carries over the chunks in beam order
+// (seq_sum_from).
+constexpr int kLC = 256;
 static_assert(kLC % 64 == 0, "whole waves per chunk row");
 __global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, int n, const double* __restrict__ zero)
 {
@@ -3640,17 +3549,17 @@ SuperGeom super_geom(const RtcsmPlan& lp)
     g.M = lp.M;
     g.Wqp = lp.Wqp;
     g.Wq4 = lp.Wq4;
+    g.unit8 = lp.unit8;
     g.Hqp = lp.Hqp;
-    g.lr = lp.low_res;
     g.pstride = lp.pstride;
     g.subO = lp.subO;
     g.pstrideO = lp.pstrideO;
     // units that can hold a nonzero value: padded rows / columns [M - 4, M + Hq / Wq)
     g.X4lo = (lp.M - kSB) >> 2;
     g.ncol = ((lp.M + lp.Wq - 1) >> 2) - g.X4lo + 1;
-    const int qlo = (lp.M - kSB) >> 4, qhi = (lp.M + lp.Hq - 1) >> 4;   // quads (16 padded rows)
-    g.ulo = std::max(0, qlo - (lp.unit8 - 1));   // unit u holds quads u .. u + unit8 - 1
-    g.nunit = qhi - g.ulo + 1;
+    g.qlo = (lp.M - kSB) >> 4;
+    g.nqt = ((lp.M + lp.Hq - 1) >> 4) - g.qlo + 1;
+    g.lr = lp.low_res;
     return g;
 }
 
@@ -3749,20 +3658,14 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
     if (sj.npj && sj.hv) {
         const int np = lp.low_res * lp.low_res;
         const SuperGeom g = super_geom(lp);
-        const int nseg = (g.nunit + kHvSeg - 1) / kHvSeg;
-        dim3 grid((g.ncol + 63) / 64, (nseg + 3) / 4, np * (int)sj.npj);
+        dim3 grid((g.ncol * g.nqt + 255) / 256, 1, np * (int)sj.npj);
         // algorithmic bytes: the copies read once (2 B per padded cell of the
-        // written units' rows) + the units written (8 B x unit8 x 16 sub-phases)
-        const double cols = (double)np * g.ncol * sj.npj, rows16 = 16.0 * g.nunit;
-        const int tok = ctx->timing_begin(K_SUPER_PLANES, cols * (rows16 * 4.0 * 2.0 + g.nunit * 16.0 * 8.0 * lp.unit8));
-        if (!ctx->skipped(K_SUPER_PLANES)) {
-            if (lp.unit8 == 3)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_hv<3>), grid, dim3(256), 0, ctx->stream,
-                                   up.at<PlaneJob>(sj.pj_off), np, g);
-            else
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_hv<2>), grid, dim3(256), 0, ctx->stream,
-                                   up.at<PlaneJob>(sj.pj_off), np, g);
-        }
+        // quads' rows and the units' columns) + the unit halves written (8 B x
+        // 16 sub-phases x unit8 copies per quad and column)
+        const double cq = (double)np * g.ncol * g.nqt * sj.npj;
+        const int tok = ctx->timing_begin(K_SUPER_PLANES, cq * (16.0 * 4.0 * 2.0 + 16.0 * 8.0 * g.unit8));
+        if (!ctx->skipped(K_SUPER_PLANES))
+            hipLaunchKernelGGL(k_super_hv, grid, dim3(256), 0, ctx->stream, up.at<PlaneJob>(sj.pj_off), np, g);
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
     } else if (sj.npj) {
@@ -3973,12 +3876,8 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         const int tok = ctx->timing_begin(K_COARSE, 8.0 * beams_K);
         if (tok >= 0) ctx->pending[tok].coarse_evals = true;   // algorithmic bytes from the records
         if (ctx->skipped(K_COARSE)) {
-        } else if (wl && LGS_LIST_CHUNK > 0) {
-            hipLaunchKernelGGL(k_coarse_list_c, dim3(kListWaves), dim3(64), 0, st, d_items, B.wl, n, zero);
         } else if (wl) {
-            const int rowlen = std::max(B.NvMax, 1);
-            hipLaunchKernelGGL(k_coarse_list, dim3(kListWaves), dim3(64), sizeof(int) * 4 * (size_t)rowlen, st,
-                               d_items, B.wl, n, rowlen, zero);
+            hipLaunchKernelGGL(k_coarse_list_c, dim3(kListWaves), dim3(64), 0, st, d_items, B.wl, n, zero);
         } else {
             const size_t lds = ((sizeof(int) * (size_t)B.NvMax + 15) & ~(size_t)15) +
                                sizeof(double) * 128 * kRing * kRowWaves;
@@ -4424,6 +4323,18 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     const size_t items_off = up.append(items.data(), items.size());
     up.flush();
     if (!B.small) launch_sets(ctx, p0, sets, sj, up);
+    // the stages after the coarse-map builds on the high-priority stream (the
+    // context's stream is restored when this function returns)
+    struct StreamRestore {
+        lgs_ctx* c;
+        hipStream_t s;
+        ~StreamRestore() { c->stream = s; }
+    } restore{ ctx, ctx->stream };
+    if (!B.small && ctx->prio_tail && ctx->hi) {
+        LGS_HIP_CHECK(hipEventRecord(ctx->split_ev[ctx->bank], ctx->stream));
+        LGS_HIP_CHECK(hipStreamWaitEvent(ctx->hi, ctx->split_ev[ctx->bank], 0));
+        ctx->stream = ctx->hi;
+    }
     enqueue_items(ctx, B, up.at<MatchItem>(items_off), items, ScanOptions{});
     F.post = ctx->post_records;
     if (F.post) {

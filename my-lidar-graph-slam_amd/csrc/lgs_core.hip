@@ -290,6 +290,7 @@ void lgs_ctx::wait_event(hipEvent_t ev)
 void lgs_ctx::release()
 {
     if (stream) hipStreamSynchronize(stream);
+    if (hi) hipStreamSynchronize(hi);
     for (int i = 0; i < S_NUM_SLOTS; ++i) {
         if (buf[i]) hipFree(buf[i]);
         buf[i] = nullptr;
@@ -330,6 +331,12 @@ void lgs_ctx::release()
     }
     if (stream) hipStreamDestroy(stream);
     stream = nullptr;
+    if (hi) hipStreamDestroy(hi);
+    hi = nullptr;
+    for (auto& e : split_ev) {
+        if (e) hipEventDestroy(e);
+        e = nullptr;
+    }
 }
 
 extern "C" int lgs_abi_version(void) { return LGS_ABI_VERSION; }
@@ -348,6 +355,15 @@ extern "C" int lgs_ctx_create(int device, lgs_ctx** out)
         hipMalloc(&ctx->zero, 32 * sizeof(double)) != hipSuccess ||
         hipMemsetAsync(ctx->zero, 0, 32 * sizeof(double), ctx->stream) != hipSuccess ||
         hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        delete ctx;
+        return LGS_ERR_HIP;
+    }
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->hi, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->split_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->split_ev[1], hipEventDisableTiming) != hipSuccess) {
+        ctx->release();
         delete ctx;
         return LGS_ERR_HIP;
     }
@@ -455,6 +471,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_SMALL_WINDOW: ctx->small_window = value != 0.0; return LGS_OK;
     case LGS_OPT_POST_RECORDS: ctx->post_records = value != 0.0; return LGS_OK;
     case LGS_OPT_FUSED_PLANES: ctx->fused_planes = value != 0.0; return LGS_OK;
+    case LGS_OPT_PRIORITY_TAIL: ctx->prio_tail = value != 0.0; return LGS_OK;
     case LGS_OPT_SORT_BARRIER_US:
         if (value < 0) return LGS_ERR_INVALID_ARG;
         ctx->sort_barrier_us = (long long)value;

@@ -273,7 +273,14 @@ struct lgs_ctx {
     bool peer_staged = false;    // cross-context copies through host memory (LGS_OPT_PEER_COPY)
     int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
     bool small_window = true;    // one-launch search of one-block windows (LGS_OPT_SMALL_WINDOW)
-    bool fused_planes = true;    // planes + superblock units in one pass (LGS_OPT_FUSED_PLANES)
+    bool fused_planes = true;    // superblock units by k_super_hv (LGS_OPT_FUSED_PLANES)
+    // a batch's stages after the coarse-map builds run on `hi`, a stream of
+    // the device's highest priority, behind an event on `stream`: the
+    // latency-bound tail of one context's chunk is not queued behind other
+    // contexts' plane builds (LGS_OPT_PRIORITY_TAIL)
+    bool prio_tail = false;   // measured r05: no gain (52.4k vs 52.3k scans/s), lone p50 +11 us
+    hipStream_t hi = nullptr;
+    hipEvent_t split_ev[2] = {};
     bool post_records = true;    // records written to pinned memory by k_post + a flag (LGS_OPT_POST_RECORDS)
     long long copies_direct = 0, copies_staged = 0;   // lgs_debug_copy_counters
     int lanes_min_batch = 2;     // pruned coarse stage: the work list (k_coarse_list) from this batch size on (LGS_OPT_LANES_MIN_BATCH)
