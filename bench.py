@@ -678,8 +678,19 @@ def run_loop(args, D, ctx):
         fn = loopbatch.hip_detect_fn_bb(ctx, maps, cands, abi.BBParams(*BB_PARAMS), cost, 0.6)
     else:
         fn = loopbatch.hip_detect_fn(ctx, maps, cands, abi.RtcsmParams(*LOOP_PARAMS), cost, 0.6)
+    # N > 1 on GPUs: the records' all-gather through the library's own RCCL
+    # collective (lgs_loop_records_allgather); the gloo rehearsal keeps torch
+    gather = None
+    if D.world > 1 and not D.rehearse:
+        gather = loopbatch.RcclGather(ctx, D.rank, D.world, D.d)
+
+    def one_step():
+        if gather is not None:
+            return loopbatch.run_sharded_rccl(cands, fn, gather)
+        return loopbatch.run_sharded(cands, fn, D.rank, D.world, D.d, D.device())
+
     for _ in range(args.warmup):
-        loopbatch.run_sharded(cands, fn, D.rank, D.world, D.d, D.device())
+        one_step()
     dominant = "k_bb_score" if bb else "k_coarse"
     set_timed_events(ctx, args, dominant, extra=() if bb else ("k_super",))
     D.barrier()
@@ -687,9 +698,11 @@ def run_loop(args, D, ctx):
     step_s = []
     for _ in range(args.steps):
         ts = time.perf_counter()
-        rec = loopbatch.run_sharded(cands, fn, D.rank, D.world, D.d, D.device())
+        rec = one_step()
         step_s.append(time.perf_counter() - ts)
     elapsed = D.max(time.perf_counter() - t0)
+    if gather is not None:
+        gather.close()
     stats = ctx.kernel_stats()
     ctx.set_option(abi.LGS_OPT_PROFILE, 0)
     found = len(loopbatch.loop_results(rec))
@@ -743,7 +756,8 @@ def run_loop(args, D, ctx):
         config=dict(workload=("config5 (f1): LoopDetectorBranchBound::Detect batch" if bb else
                               "config5: LoopDetectorRealTimeCorrelative::Detect batch"), candidates=len(cands),
                     found=found, parallelism=f"candidates sharded in contiguous blocks over {D.world} ranks + "
-                                             "RCCL all-gather of 176-B result records"),
+                                             "one all-gather of 176-B result records (N > 1: the library's "
+                                             "lgs_loop_records_allgather, RCCL)"),
         roofline=roofline_from(stats, dominant, args.pmc, "k_bb_score" if bb else "k_coarse_list", "l2-gather",
                                workload="loop_bb" if bb else "loop"),
         # config 5's largest kernel by time is the 9-row superblock-bound pass,

@@ -895,15 +895,23 @@ __device__ __forceinline__ unsigned pkmax(unsigned a, unsigned b)
 {
     return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
 }
+// NQ quads per thread: NQ = 1 stores the quad's halves (two 8-byte stores
+// per sub-phase, each unit's other half from the neighbouring quad's
+// thread); NQ = 2 (16-byte units) computes quads qt and qt + 1 and stores
+// unit qt whole (one 16-byte store per sub-phase, 64 consecutive units per
+// wave instruction), every quad's maxima computed by two threads.
+template <int NQ>
 __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ jobs, int nplanes, SuperGeom g)
 {
     const Blk wg = xcd_block();
     const PlaneJob& job = jobs[wg.z / nplanes];
     const int p = wg.z % nplanes;
-    const int tq = wg.x * 256 + threadIdx.x;        // (quad, unit column), column fastest
+    const int tq = wg.x * 256 + threadIdx.x;        // (quad or unit, unit column), column fastest
     const int qi = tq / g.ncol, c = tq - qi * g.ncol;
-    if (qi >= g.nqt) return;
-    const int X4 = g.X4lo + c, qt = g.qlo + qi;
+    // NQ = 2: units qlo - 1 .. qlo + nqt - 1 (unit u holds quads u, u + 1)
+    if (qi >= g.nqt + NQ - 1) return;
+    const int X4 = g.X4lo + c, qt = g.qlo + qi - (NQ - 1);
+    if (qt < 0) return;
     const int rx = p % g.lr, ry = p / g.lr;
     typedef unsigned long long u64;
     typedef const __attribute__((address_space(1))) u64 gu64_t;
@@ -912,20 +920,32 @@ __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ j
     const long long rowM = (long long)g.M * g.Wqp;
     // the column strip: column 3 of unit column (M - 1) / 4 in planes rx > 0
     const bool cstrip = rx > 0 && 4 * X4 + 3 == g.M - 1;
-    u64 hm[19];   // horizontal forward 4-max of columns 4 X4 + k, k < 4, per row
+    constexpr int NR = 16 * NQ + 3;
+    // every load first, from always-valid addresses (rows past the plane
+    // clamped to its last row, then zeroed; the strip column's value loaded
+    // by every thread, from its own row where it is not the strip): a load
+    // under a branch made the compiler wait for each row (19 round trips)
+    u64 la[NR], lb[NR];
+    unsigned short ls[NR];
 #pragma unroll
-    for (int k = 0; k < 19; ++k) {
-        const int Y = 16 * qt + k;
+    for (int k = 0; k < NR; ++k) {
+        const int Y = min(16 * qt + k, g.Hqp - 1);
         const bool rs = (Y == g.M - 1) && ry > 0;            // the row strip
         const unsigned short* row = rs ? P + rx * g.pstride + rowM : P + p * g.pstride + (long long)Y * g.Wqp;
-        const bool in = Y < g.Hqp;
-        u64 a = in ? *(gu64_t*)(row + 4 * X4) : 0ull;
-        const u64 b = in ? *(gu64_t*)(row + 4 * X4 + 4) : 0ull;
-        if (cstrip) {   // column M - 1 reads column M of plane (0, ry) (row strip: plane 0)
-            const unsigned short* src = rs ? P + rowM + g.M : P + ry * g.lr * g.pstride + (long long)Y * g.Wqp + g.M;
-            const u64 v = in ? (u64)*(gu16_t*)src : 0ull;
-            a = (a & 0x0000FFFFFFFFFFFFull) | (v << 48);
-        }
+        // column M - 1 reads column M of plane (0, ry) (row strip: plane 0)
+        const unsigned short* src = !cstrip ? row + 4 * X4
+                                  : rs ? P + rowM + g.M : P + ry * g.lr * g.pstride + (long long)Y * g.Wqp + g.M;
+        la[k] = *(gu64_t*)(row + 4 * X4);
+        lb[k] = *(gu64_t*)(row + 4 * X4 + 4);
+        ls[k] = *(gu16_t*)src;
+    }
+    u64 hm[NR];   // horizontal forward 4-max of columns 4 X4 + k, k < 4, per row
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const bool in = 16 * qt + k < g.Hqp;
+        u64 a = in ? la[k] : 0ull;
+        const u64 b = in ? lb[k] : 0ull;
+        if (cstrip) a = (a & 0x0000FFFFFFFFFFFFull) | ((u64)(in ? ls[k] : 0) << 48);
         // columns 0..7 as packed pairs: a = (c0 c1)(c2 c3), b = (c4 c5)(c6 c7)
         const unsigned a0 = (unsigned)a, a1 = (unsigned)(a >> 32), b0 = (unsigned)b, b1 = (unsigned)(b >> 32);
         const unsigned m01 = pkmax(a0, (a0 >> 16) | (a1 << 16));   // (max c0c1, max c1c2)
@@ -933,9 +953,9 @@ __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ j
         const unsigned m45 = pkmax(b0, (b0 >> 16) | (b1 << 16));   // (max c4c5, max c5c6)
         hm[k] = (u64)pkmax(m01, m23) | ((u64)pkmax(m23, m45) << 32);   // 4-max at columns 0, 1 | 2, 3
     }
-    unsigned vlo[16], vhi[16];   // vertical forward 4-max
+    unsigned vlo[16 * NQ], vhi[16 * NQ];   // vertical forward 4-max
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < 16 * NQ; ++k) {
         vlo[k] = pkmax(pkmax((unsigned)hm[k], (unsigned)hm[k + 1]), pkmax((unsigned)hm[k + 2], (unsigned)hm[k + 3]));
         vhi[k] = pkmax(pkmax((unsigned)(hm[k] >> 32), (unsigned)(hm[k + 1] >> 32)),
                        pkmax((unsigned)(hm[k + 2] >> 32), (unsigned)(hm[k + 3] >> 32)));
@@ -946,16 +966,28 @@ __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ j
     for (int cy = 0; cy < 4; ++cy) {
 #pragma unroll
         for (int cx = 0; cx < 4; ++cx) {
-            u64 h = 0;
+            u64 h[NQ];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const unsigned wv = (cx < 2) ? vlo[4 * i + cy] : vhi[4 * i + cy];
-                h |= (u64)((cx & 1) ? (wv >> 16) : (wv & 0xFFFFu)) << (16 * i);
+            for (int q = 0; q < NQ; ++q) {
+                h[q] = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const unsigned wv = (cx < 2) ? vlo[16 * q + 4 * i + cy] : vhi[16 * q + 4 * i + cy];
+                    h[q] |= (u64)((cx & 1) ? (wv >> 16) : (wv & 0xFFFFu)) << (16 * i);
+                }
             }
             const long long u = (cy * 4 + cx) * g.subO + (long long)qt * g.Wq4 + X4;
-            gstore(uo + u8 * u, h);                                          // rows 4 qt .. of unit qt
-            if (qt > 0) gstore(uo + (u8 * (u - g.Wq4) + 1), h);              // .. of unit qt - 1
-            if (u8 == 3 && qt > 1) gstore(uo + (3 * (u - 2 * g.Wq4) + 2), h);   // .. of unit qt - 2
+            if constexpr (NQ == 2) {   // unit qt whole (16-byte units)
+                typedef unsigned long long u64v2 __attribute__((ext_vector_type(2)));
+                u64v2 v;
+                v.x = h[0];
+                v.y = h[1];
+                gstore((u64v2*)(uo + 2 * u), v);
+            } else {
+                gstore(uo + u8 * u, h[0]);                                          // rows 4 qt .. of unit qt
+                if (qt > 0) gstore(uo + (u8 * (u - g.Wq4) + 1), h[0]);              // .. of unit qt - 1
+                if (u8 == 3 && qt > 1) gstore(uo + (3 * (u - 2 * g.Wq4) + 2), h[0]);   // .. of unit qt - 2
+            }
         }
     }
 }
@@ -3658,14 +3690,22 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
     if (sj.npj && sj.hv) {
         const int np = lp.low_res * lp.low_res;
         const SuperGeom g = super_geom(lp);
-        dim3 grid((g.ncol * g.nqt + 255) / 256, 1, np * (int)sj.npj);
+        const int nq = ctx->hv_full && lp.unit8 == 2 ? 2 : 1;   // threads per column: nqt quads or nqt + 1 units
+        dim3 grid((g.ncol * (g.nqt + nq - 1) + 255) / 256, 1, np * (int)sj.npj);
         // algorithmic bytes: the copies read once (2 B per padded cell of the
         // quads' rows and the units' columns) + the unit halves written (8 B x
         // 16 sub-phases x unit8 copies per quad and column)
         const double cq = (double)np * g.ncol * g.nqt * sj.npj;
         const int tok = ctx->timing_begin(K_SUPER_PLANES, cq * (16.0 * 4.0 * 2.0 + 16.0 * 8.0 * g.unit8));
         if (!ctx->skipped(K_SUPER_PLANES))
-            hipLaunchKernelGGL(k_super_hv, grid, dim3(256), 0, ctx->stream, up.at<PlaneJob>(sj.pj_off), np, g);
+        {
+            if (nq == 2)
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_hv<2>), grid, dim3(256), 0, ctx->stream,
+                                   up.at<PlaneJob>(sj.pj_off), np, g);
+            else
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_hv<1>), grid, dim3(256), 0, ctx->stream,
+                                   up.at<PlaneJob>(sj.pj_off), np, g);
+        }
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
     } else if (sj.npj) {
@@ -4504,6 +4544,7 @@ void run_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
 // Batches of at most kMaxBatch items (bounded scratch: ~20 MB per config-2
 // item), each with only the coarse maps its items reference.
 constexpr int kMaxBatch = kMaxBatchItems;
+constexpr int kSplitMin = 16;   // smallest chunk of a split call
 void run_chunked(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
                  const lgs_grid* const* grids, lgs_scan* const* scans, const lgs_pose2d* init, int n,
                  double nthr, const std::vector<PlaneSet>& sets_all, const int* set_of, lgs_rtcsm_summary* out)
@@ -4514,9 +4555,13 @@ void run_chunked(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge
     InFlight fl[2];
     bool busy[2] = { false, false };
     int c = 0;
+    // a call of 2 x kSplitMin .. kMaxBatch matches runs as two chunks, so that
+    // the two banks overlap even then (an 8-rank shard of the 512-candidate
+    // loop batch is 64 candidates)
+    const int step = (ctx->split_chunks && n <= kMaxBatch && n >= 2 * kSplitMin) ? (n + 1) / 2 : kMaxBatch;
     try {
-        for (int j0 = 0; j0 < n; j0 += kMaxBatch, ++c) {
-            const int m = std::min(kMaxBatch, n - j0);
+        for (int j0 = 0; j0 < n; j0 += step, ++c) {
+            const int m = std::min(step, n - j0);
             std::vector<PlaneSet> sets;
             std::vector<int> so((size_t)m), remap(sets_all.size(), -1);
             for (int k = 0; k < m; ++k) {

@@ -274,6 +274,8 @@ struct lgs_ctx {
     int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
     bool small_window = true;    // one-launch search of one-block windows (LGS_OPT_SMALL_WINDOW)
     bool fused_planes = true;    // superblock units by k_super_hv (LGS_OPT_FUSED_PLANES)
+    bool split_chunks = true;    // calls of 32..64 matches as two chunks (LGS_OPT_SPLIT_CHUNKS)
+    bool hv_full = false;        // k_super_hv stores 16-byte units whole (LGS_OPT_HV_FULL, A/B; measured r05: 0.24 vs 0.17 ms per 64 sets)
     // a batch's stages after the coarse-map builds run on `hi`, a stream of
     // the device's highest priority, behind an event on `stream`: the
     // latency-bound tail of one context's chunk is not queued behind other

@@ -157,6 +157,48 @@ def run_sharded(cands: Sequence[Candidate], detect_fn, rank: int = 0, world: int
     return np.concatenate(parts, axis=0)
 
 
+class RcclGather:
+    """The all-gather of the records through the library's C-ABI
+    (lgs_loop_records_allgather: one ncclAllGather of fixed-size rows on the
+    context's stream, RCCL over xGMI) instead of torch: one communicator per
+    rank, its unique id made on rank 0 and broadcast over `dist` once."""
+
+    def __init__(self, ctx: "abi.Context", rank: int, world: int, dist=None):
+        self.ctx, self.rank, self.world = ctx, rank, world
+        uid = None
+        if rank == 0:
+            buf = (C.c_ubyte * 128)()
+            ctx.check(ctx.lib.lgs_rccl_unique_id(buf), "rccl_unique_id")
+            uid = bytes(buf)
+        if world > 1:
+            box = [uid]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
+        self.comm = ctx.rccl_comm(world, rank, uid)
+
+    def __call__(self, n: int, lo: int, hi: int, local: np.ndarray) -> np.ndarray:
+        loc = (abi.LoopResult * max(1, hi - lo)).from_buffer_copy(
+            local.tobytes() if hi > lo else bytes(RECORD_BYTES))
+        out = (abi.LoopResult * max(1, n))()
+        self.ctx.check(self.ctx.lib.lgs_loop_records_allgather(self.ctx.h, self.comm, self.rank, self.world, n,
+                                                               loc, out), "loop_records_allgather")
+        return np.frombuffer(bytes(out), dtype=np.uint8)[: n * RECORD_BYTES].reshape(n, RECORD_BYTES)
+
+    def close(self):
+        if self.comm:
+            self.ctx.rccl_comm_destroy(self.comm)
+            self.comm = None
+
+
+def run_sharded_rccl(cands: Sequence[Candidate], detect_fn, gather: RcclGather) -> np.ndarray:
+    """run_sharded with the records gathered by the C-ABI collective."""
+    n = len(cands)
+    lo, hi = shard_bounds(n, gather.world, gather.rank)
+    local = detect_fn(sub_queries(cands, lo, hi), lo, hi) if hi > lo else np.zeros((0, RECORD_BYTES), np.uint8)
+    assert local.shape == (hi - lo, RECORD_BYTES)
+    return gather(n, lo, hi, local)
+
+
 def decode(records: np.ndarray) -> List[abi.LoopResult]:
     raw = records.tobytes()
     return [abi.LoopResult.from_buffer_copy(raw[i * RECORD_BYTES:(i + 1) * RECORD_BYTES])

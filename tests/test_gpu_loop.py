@@ -191,3 +191,19 @@ def test_loop_records_allgather_world1(ctx):
         assert bytes(ctx.loop_records_allgather(comm, 0, 1, 0, [])) == bytes(C.sizeof(abi.LoopResult))
     finally:
         ctx.rccl_comm_destroy(comm)
+
+
+def test_run_sharded_rccl_world1(ctx):
+    """bench.py's N > 1 loop line gathers through loopbatch.RcclGather (the
+    library's lgs_loop_records_allgather): at one rank it returns the records
+    run_sharded returns, byte for byte, call after call."""
+    maps, cands = small.make_problem()
+    p, c = abi.RtcsmParams(*small.PARAMS), abi.CostGEParams(*small.COST)
+    fn = loopbatch.hip_detect_fn(ctx, maps, cands, p, c, small.THR)
+    want = loopbatch.run_sharded(cands, fn)
+    gather = loopbatch.RcclGather(ctx, 0, 1)
+    try:
+        for _ in range(3):
+            assert loopbatch.run_sharded_rccl(cands, fn, gather).tobytes() == want.tobytes()
+    finally:
+        gather.close()

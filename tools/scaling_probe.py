@@ -119,6 +119,45 @@ def main():
             per.append(float(np.median(ts)))
         shards[w] = dict(candidates_per_rank=n // w, rank_ms=[round(1e3 * t, 4) for t in per],
                          max_rank_ms=round(1e3 * max(per), 4))
+    # the 8-rank block as ONE chunk (r04) vs two (r05 default, LGS_OPT_SPLIT_CHUNKS)
+    lo, hi = loopbatch.shard_bounds(n, 8, 0)
+    sq = loopbatch.sub_queries(cands, lo, hi)
+    split_ab = {}
+    for opt in (0, 1):
+        ctx.set_option(abi.LGS_OPT_SPLIT_CHUNKS, opt)
+        fn(sq, lo, hi)
+        ts = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            fn(sq, lo, hi)
+            ts.append(time.perf_counter() - t0)
+        split_ab["two_chunks" if opt else "one_chunk"] = round(1e3 * float(np.median(ts)), 4)
+    ctx.set_option(abi.LGS_OPT_SPLIT_CHUNKS, 1)
+    # per-rank overhead of an 8-rank step outside the kernels: the whole call
+    # (Python packaging + ctypes + lgs_loop_detect_rtcsm + record copy) vs the
+    # kernels' event-timed sum, and the C-ABI gather's own work at one rank
+    # (records host -> device, ncclAllGather, device -> host, synchronise)
+    ctx.set_option(abi.LGS_OPT_PROFILE, 1)
+    ctx.reset_stats()
+    reps = a.reps
+    for _ in range(reps):
+        fn(sq, lo, hi)
+    kern_ms = sum(v["total_ms"] for v in ctx.kernel_stats().values()) / reps
+    ctx.set_option(abi.LGS_OPT_PROFILE, 0)
+    gather = loopbatch.RcclGather(ctx, 0, 1)
+    rec = fn(sq, lo, hi)
+    ts = []
+    for _ in range(max(20, reps)):
+        t0 = time.perf_counter()
+        gather(hi - lo, 0, hi - lo, rec)
+        ts.append(time.perf_counter() - t0)
+    gather.close()
+    overhead = dict(block_call_ms=split_ab["two_chunks"], kernels_event_ms=round(kern_ms, 4),
+                    non_kernel_ms=round(split_ab["two_chunks"] - kern_ms, 4),
+                    capi_gather_world1_ms=round(1e3 * float(np.median(ts)), 4),
+                    note="kernels_event_ms: every kernel of the block's call HIP-event-timed on its stream "
+                         "(serialised: the profile mode times each launch), so non_kernel_ms is a lower bound "
+                         "of the host/launch share")
     t1 = shards[1]["max_rank_ms"]
     pred = {}
     for w in worlds:
@@ -127,7 +166,8 @@ def main():
         pred[w] = dict(step_ms=round(tw, 4), speedup=round(t1 / tw, 3), efficiency=round(t1 / tw / w, 3),
                        candidates_per_s=round(n / tw * 1e3, 1))
     out = dict(workload="config5: 512 candidates (32 maps x 16 nodes), 1081 beams, +-2.5 m / +-0.5 rad",
-               shard_on_one_gpu=shards, gloo_allgather_512_records=gloo, predicted=pred,
+               shard_on_one_gpu=shards, rank8_block_chunks_ms=split_ab, rank8_overhead=overhead,
+               gloo_allgather_512_records=gloo, predicted=pred,
                note="per-rank blocks timed one at a time on ONE MI355X (each rank owns a GPU on a node); "
                     "all-gather = gloo over host TCP (an upper bound of RCCL over xGMI)")
     s = json.dumps(out)
