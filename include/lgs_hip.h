@@ -181,7 +181,8 @@ int  lgs_abi_version(void);
 #define LGS_OPT_FUSED_PLANES  27  /* 1 (default) = the per-query coarse-map precompute writes the phase planes AND the octet superblock units in one pass from the fine map (k_planes_super, LowRes 5), 0 = the precompute + k_super_planes passes */
 #define LGS_OPT_PRIORITY_TAIL 28  /* 0 (default) = one stream; 1 = a correlative batch's stages after the coarse-map builds run on a second stream of the device's highest priority (behind an event), so that other contexts' plane builds cannot queue ahead of its latency-bound tail */
 #define LGS_OPT_HV_FULL       29  /* A/B: 1 = the superblock pass (k_super_hv) stores each 16-byte unit whole from two quads' maxima; 0 (default) = each quad's halves */
-#define LGS_OPT_SPLIT_CHUNKS  30  /* 1 (default) = a correlative call of 32..64 matches runs as two chunks of half the size, so that the two buffer banks overlap (one chunk per 64 otherwise); 0 = one chunk */
+#define LGS_OPT_SPLIT_CHUNKS  30  /* A/B: 1 = a correlative call of 32..64 matches runs as two chunks of half the size (the two buffer banks overlap); 0 (default) = one chunk per 64 */
+#define LGS_OPT_DEVICE_HITS   31  /* 1 (default) = lgs_maps_construct_from_scans / lgs_map_construct_global form the hit points (glibc sincos restated), boxes, ray cells and key offsets on the device; 0 = on the host */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

@@ -20,6 +20,7 @@
 //   k_apply    one thread per run applies the Bayes updates sequentially and
 //              counts hits/misses
 #include "lgs_internal.hpp"
+#include "glibc_math.hpp"
 
 #include <chrono>
 #include <cstdio>
@@ -161,6 +162,179 @@ __global__ __launch_bounds__(256) void k_emit(const int4* __restrict__ rays,
         out[k] = (cell << ksh) | tag | hit;
     }
     if (bad) *outside = 1;
+}
+
+// ---------------------------------------------------------------------------
+// Device hit points and ray cells (r05; the map rebuilds of many scans --
+// AfterLoopClosure, ConstructGlobalMap): ComputeBoundingBoxAndScanPoints'
+// hit points (C/mapping/grid_map_builder.cpp:335-380) with glibc's sincos
+// restated bit for bit (glibc_math.hpp gl_sincos), the boxes back to the host
+// for the maps' geometry (Resize), then the sensor / hit cells
+// (WorldCoordinateToGridCellIndex, H/grid_map/grid_map.hpp:779-790: a floor of
+// the IEEE quotient, as on the host), the ray lengths and key offsets -- the
+// host computed all of that (and staged 12 MB) in r04.
+struct HitUnit {              // one (map, scan) of the pass
+    const double* ranges;
+    const double* angles;
+    int n;                    // beams
+    int job;                  // map of the pass
+    double sx, sy, st;        // sensor pose (Compound on the host, glibc sincos)
+    double min_r, max_r;      // usable range (open interval)
+    long long beam0;          // the unit's region of the hit buffer (n slots)
+};
+struct MapGeo {
+    double min_x, min_y, res;
+};
+__device__ __forceinline__ double dmin_ref(double a, double b) { return (b < a) ? b : a; }  // std::min
+__device__ __forceinline__ double dmax_ref(double a, double b) { return (a < b) ? b : a; }  // std::max
+
+// Block-wide exclusive prefix of v over the 256 threads; returns it, *total = sum.
+template <class T>
+__device__ __forceinline__ T block_excl_scan(T v, T* sw, T* total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    T x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const T u = __shfl_up(x, off, 64);
+        if (lane >= off) x += u;
+    }
+    if (lane == 63) sw[w] = x;
+    __syncthreads();
+    T base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (i < w) base += sw[i];
+        tot += sw[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+// k_hits: one workgroup per unit: the usable beams' hit points, compacted in
+// beam order into the unit's region; the unit's count and box (sensor and
+// hits: min x, min y, max x, max y, with std::min / std::max).  bad |= 4 if
+// an angle lies outside gl_sincos's domain (the host path then runs).
+__global__ __launch_bounds__(256) void k_hits(const HitUnit* __restrict__ units, double2* __restrict__ hits,
+                                              int* __restrict__ counts, double4* __restrict__ boxes,
+                                              int* __restrict__ bad)
+{
+    const HitUnit U = units[blockIdx.x];
+    __shared__ int sw[4];
+    __shared__ double sb[4][256];
+    double b0 = U.sx, b1 = U.sy, b2 = U.sx, b3 = U.sy;
+    int base = 0, oob = 0;
+    for (int i0 = 0; i0 < U.n; i0 += 256) {
+        const int i = i0 + (int)threadIdx.x;
+        double r = 0.0, a = 0.0;
+        if (i < U.n) {
+            r = U.ranges[i];
+            a = U.angles[i];
+        }
+        const bool ok = i < U.n && !(r >= U.max_r || r <= U.min_r);
+        int tot = 0;
+        const int pos = base + block_excl_scan<int>(ok ? 1 : 0, sw, &tot);
+        if (ok) {
+            const double th = U.st + a;
+            double sn = 0.0, c = 0.0;
+            if (glm::gl_sincos_ok(th)) glm::gl_sincos(th, &sn, &c);
+            else oob = 1;
+            const double hx = U.sx + r * c, hy = U.sy + r * sn;
+            hits[U.beam0 + pos] = make_double2(hx, hy);
+            b0 = dmin_ref(b0, hx);
+            b1 = dmin_ref(b1, hy);
+            b2 = dmax_ref(b2, hx);
+            b3 = dmax_ref(b3, hy);
+        }
+        base += tot;
+    }
+    if (oob) *bad |= 4;
+    sb[0][threadIdx.x] = b0;
+    sb[1][threadIdx.x] = b1;
+    sb[2][threadIdx.x] = b2;
+    sb[3][threadIdx.x] = b3;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {   // min / max are exact: any order
+        if ((int)threadIdx.x < h) {
+            const int t = threadIdx.x;
+            sb[0][t] = dmin_ref(sb[0][t], sb[0][t + h]);
+            sb[1][t] = dmin_ref(sb[1][t], sb[1][t + h]);
+            sb[2][t] = dmax_ref(sb[2][t], sb[2][t + h]);
+            sb[3][t] = dmax_ref(sb[3][t], sb[3][t + h]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        counts[blockIdx.x] = base;
+        boxes[blockIdx.x] = make_double4(sb[0][0], sb[1][0], sb[2][0], sb[3][0]);
+    }
+}
+
+// k_raycells: one workgroup per unit: sensor and hit cells of its rays at
+// [ray0[u], ray0[u] + counts[u]) of the pass, the ray -> map index, and the
+// keys' offsets inside the unit (ray lengths max(|dx|, |dy|) + 1, prefix in
+// ray order); ukeys[u] = the unit's keys.
+__global__ __launch_bounds__(256) void k_raycells(const HitUnit* __restrict__ units, const double2* __restrict__ hits,
+                                                  const int* __restrict__ counts, const MapGeo* __restrict__ geo,
+                                                  const int* __restrict__ ray0, int4* __restrict__ rays,
+                                                  long long* __restrict__ offs, int* __restrict__ rmap,
+                                                  long long* __restrict__ ukeys)
+{
+    const int u = blockIdx.x;
+    const HitUnit U = units[u];
+    const MapGeo G = geo[U.job];
+    const int n = counts[u], r0 = ray0[u];
+    __shared__ long long sw[4];
+    const int sx = (int)floor((U.sx - G.min_x) / G.res), sy = (int)floor((U.sy - G.min_y) / G.res);
+    long long base = 0;
+    for (int j0 = 0; j0 < n; j0 += 256) {
+        const int j = j0 + (int)threadIdx.x;
+        long long len = 0;
+        int4 ry = make_int4(0, 0, 0, 0);
+        if (j < n) {
+            const double2 h = hits[U.beam0 + j];
+            const int hx = (int)floor((h.x - G.min_x) / G.res), hy = (int)floor((h.y - G.min_y) / G.res);
+            ry = make_int4(sx, sy, hx, hy);
+            len = (long long)max(abs(hx - sx), abs(hy - sy)) + 1;
+        }
+        long long tot = 0;
+        const long long pos = base + block_excl_scan<long long>(len, sw, &tot);
+        if (j < n) {
+            rays[r0 + j] = ry;
+            offs[r0 + j] = pos;
+            if (rmap) rmap[r0 + j] = U.job;
+        }
+        base += tot;
+    }
+    if (threadIdx.x == 0) ukeys[u] = base;
+}
+
+// The units' key bases (exclusive prefix over units, one workgroup; n small)
+// and the total (*total); then k_addbase moves every ray's offset by its
+// unit's base.
+__global__ __launch_bounds__(256) void k_unit_scan(const long long* __restrict__ ukeys, int nu,
+                                                   long long* __restrict__ kbase, long long* __restrict__ total)
+{
+    __shared__ long long sw[4];
+    long long base = 0;
+    for (int i0 = 0; i0 < nu; i0 += 256) {
+        const int i = i0 + (int)threadIdx.x;
+        const long long v = i < nu ? ukeys[i] : 0;
+        long long tot = 0;
+        const long long pos = base + block_excl_scan<long long>(v, sw, &tot);
+        if (i < nu) kbase[i] = pos;
+        base += tot;
+    }
+    if (threadIdx.x == 0) *total = base;
+}
+__global__ __launch_bounds__(256) void k_addbase(const int* __restrict__ counts, const int* __restrict__ ray0,
+                                                 const long long* __restrict__ kbase, long long* __restrict__ offs)
+{
+    const int u = blockIdx.x;
+    const long long b = kbase[u];
+    const int r0 = ray0[u], n = counts[u];
+    for (int j = threadIdx.x; j < n; j += 256) offs[r0 + j] += b;
 }
 
 // k_runmask: one thread per sorted key; each wavefront covers 64 consecutive
@@ -1169,6 +1343,7 @@ void hits_and_boxes(std::vector<MapJob>& jobs, const std::vector<int>& first, co
 void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_params* bp, TagPass* tp = nullptr)
 {
     hipStream_t st = ctx->stream;
+    const auto t_rc0 = std::chrono::steady_clock::now();
     struct Unit {
         int job;
         int tag;
@@ -1324,6 +1499,10 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
             });
         }
         char* d_stage = (char*)ctx->ensure(S_RAY6, mb + rb + ob + ib);
+        if (std::getenv("LGS_F2_TIMING"))
+            std::fprintf(stderr, "f2 raycast host prep (cells + staging) %.1f us, %zu bytes staged\n",
+                         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_rc0).count(),
+                         mb + rb + ob + ib);
         LGS_HIP_CHECK(hipMemcpyAsync(d_stage, pin, mb + rb + ob + ib, hipMemcpyHostToDevice, st));
         const BayesChains* d_chains = (const BayesChains*)d_stage;
         const RayMap* d_maps = (const RayMap*)(d_stage + cb);
@@ -1384,6 +1563,186 @@ void raycast_maps(lgs_ctx* ctx, std::vector<MapJob>& jobs, const lgs_builder_par
     if (apply_tok >= 0) ctx->pending[apply_tok].algo_bytes += 32.0 * (double)runs;
     if (ctx->profile) ctx->harvest();
     if (bad) throw Error(LGS_ERR_INTERNAL, bad_message(bad));
+}
+
+// ConstructMapFromScans of several maps (AfterLoopClosure; a global map) with
+// the hit points, boxes, ray cells and key offsets formed on the device
+// (k_hits, k_raycells): the host keeps the geometry
+// (Resize) between the two device phases, from the boxes k_hits returns --
+// identical values, so identical maps.  Returns false, with the maps as they
+// were or resized and reset for the same boxes, when the pass does not fit
+// one emit/sort/apply pass or an angle lies outside gl_sincos's domain: the
+// caller then runs the host path.
+bool construct_maps_device(lgs_ctx* ctx, lgs_map* const* maps, const int* first, const int* count, int n_maps,
+                           const lgs_scan* const* scans, const lgs_pose2d* poses, const lgs_builder_params* bp)
+{
+    hipStream_t st = ctx->stream;
+    std::vector<HitUnit> units;
+    std::vector<int> unit_scan;
+    long long beams = 0;
+    for (int j = 0; j < n_maps; ++j)
+        for (int k = 0; k < count[j]; ++k) {
+            const int i = first[j] + k;
+            const lgs_scan* sc = scans[i];
+            HitUnit U{};
+            const lgs_pose2d sp = compound(poses[i], sc->rel);   // :340-341
+            U.n = sc->n;
+            U.job = j;
+            U.sx = sp.x, U.sy = sp.y, U.st = sp.theta;
+            U.min_r = std::max(bp->usable_range_min, sc->min_range);
+            U.max_r = std::min(bp->usable_range_max, sc->max_range);
+            U.beam0 = beams;
+            beams += sc->n;
+            units.push_back(U);
+            unit_scan.push_back(i);
+        }
+    const int nu = (int)units.size();
+    if (nu == 0 || beams >= (1LL << 30)) return false;
+    {
+        std::vector<const lgs_scan*> sv;
+        for (int i : unit_scan) sv.push_back(scans[i]);
+        scans_to_device(ctx, sv.data(), (int)sv.size());
+    }
+    for (int u = 0; u < nu; ++u) {
+        units[u].ranges = scans[unit_scan[u]]->d_ranges;
+        units[u].angles = scans[unit_scan[u]]->d_angles;
+    }
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_hits = 0, o_rays = o_hits + al(16 * (size_t)beams), o_offs = o_rays + al(16 * (size_t)beams),
+                 o_rmap = o_offs + al(8 * (size_t)beams), o_cnt = o_rmap + al(4 * (size_t)beams),
+                 o_box = o_cnt + al(4 * (size_t)nu), o_ukeys = o_box + al(32 * (size_t)nu),
+                 o_kbase = o_ukeys + al(8 * (size_t)nu), o_total = o_kbase + al(8 * (size_t)nu),
+                 o_end = o_total + 256;
+    char* d = (char*)ctx->ensure(S_RAY8, o_end);
+    double2* d_hits = (double2*)(d + o_hits);
+    int4* d_rays = (int4*)(d + o_rays);
+    long long* d_offs = (long long*)(d + o_offs);
+    int* d_rmap = (int*)(d + o_rmap);
+    int* d_cnt = (int*)(d + o_cnt);
+    double4* d_box = (double4*)(d + o_box);
+    long long* d_ukeys = (long long*)(d + o_ukeys);
+    long long* d_kbase = (long long*)(d + o_kbase);
+    long long* d_total = (long long*)(d + o_total);
+    int* d_bad = (int*)ctx->ensure(S_RAY4, 16);
+    unsigned long long* d_runs = (unsigned long long*)(d_bad + 2);
+    LGS_HIP_CHECK(hipMemsetAsync(d_bad, 0, 16, st));
+    // phase 1: hit points, counts and boxes
+    {
+        Upload up(ctx);
+        const size_t uo = up.append(units.data(), units.size());
+        up.flush();
+        hipLaunchKernelGGL(k_hits, dim3(nu), dim3(256), 0, st, up.at<HitUnit>(uo), d_hits, d_cnt, d_box, d_bad);
+        LGS_HIP_CHECK(hipGetLastError());
+    }
+    std::vector<int> cnt(nu);
+    std::vector<std::array<double, 4>> ubox(nu);
+    int bad = 0;
+    {
+        char* pin = (char*)ctx->ensure_pinned(al(4 * (size_t)nu) + 32 * (size_t)nu + 16);
+        LGS_HIP_CHECK(hipMemcpyAsync(pin, d_cnt, 4 * (size_t)nu, hipMemcpyDeviceToHost, st));
+        LGS_HIP_CHECK(hipMemcpyAsync(pin + al(4 * (size_t)nu), d_box, 32 * (size_t)nu, hipMemcpyDeviceToHost, st));
+        LGS_HIP_CHECK(hipMemcpyAsync(pin + al(4 * (size_t)nu) + 32 * (size_t)nu, d_bad, 4, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        std::memcpy(cnt.data(), pin, 4 * (size_t)nu);
+        std::memcpy(ubox.data(), pin + al(4 * (size_t)nu), 32 * (size_t)nu);
+        std::memcpy(&bad, pin + al(4 * (size_t)nu) + 32 * (size_t)nu, 4);
+    }
+    if (bad) return false;
+    // the maps' boxes as ConstructMapFromScans accumulates them (:234-285;
+    // topRight starts at numeric_limits<double>::min()), then Resize + Reset
+    std::vector<std::array<double, 4>> box(n_maps, std::array<double, 4>{ DBL_MAX, DBL_MAX, DBL_MIN, DBL_MIN });
+    for (int u = 0; u < nu; ++u) {
+        auto& b = box[units[u].job];
+        b[0] = smin(b[0], ubox[u][0]);
+        b[1] = smin(b[1], ubox[u][1]);
+        b[2] = smax(b[2], ubox[u][2]);
+        b[3] = smax(b[3], ubox[u][3]);
+    }
+    for (int j = 0; j < n_maps; ++j) map_resize_reset(maps[j], box[j][0], box[j][1], box[j][2], box[j][3]);
+    // phase 2: ray cells, ray -> map, key offsets
+    std::vector<int> ray0(nu);
+    long long nr = 0;
+    for (int u = 0; u < nu; ++u) {
+        ray0[u] = (int)nr;
+        nr += cnt[u];
+    }
+    std::vector<RayMap> rm(n_maps);
+    std::vector<MapGeo> geo(n_maps);
+    unsigned long long cells = 0;
+    for (int j = 0; j < n_maps; ++j) {
+        const lgs_map* m = maps[j];
+        rm[j] = RayMap{ cells, m->w, m->h, m->d_cells, m->d_hit, m->d_miss, m->d_palloc, m->ps, m->npx };
+        geo[j] = MapGeo{ m->min_x, m->min_y, m->res };
+        cells += (unsigned long long)m->w * m->h;
+    }
+    if (nr == 0 || nr >= (1LL << 30) || cells >= (1ull << 31)) return false;
+    const bool multi = n_maps > 1;
+    const BayesChains chains = make_chains(bp->prob_hit, bp->prob_miss);
+    Upload up(ctx);
+    const size_t uo = up.append(units.data(), units.size());
+    const size_t go = up.append(geo.data(), geo.size());
+    const size_t ro = up.append(ray0.data(), ray0.size());
+    const size_t co = up.append(&chains, 1);
+    const size_t mo = up.append(rm.data(), rm.size());
+    up.flush();
+    hipLaunchKernelGGL(k_raycells, dim3(nu), dim3(256), 0, st, up.at<HitUnit>(uo), (const double2*)d_hits, d_cnt,
+                       up.at<MapGeo>(go), up.at<int>(ro), d_rays, d_offs, multi ? d_rmap : nullptr, d_ukeys);
+    hipLaunchKernelGGL(k_unit_scan, dim3(1), dim3(256), 0, st, d_ukeys, nu, d_kbase, d_total);
+    hipLaunchKernelGGL(k_addbase, dim3(nu), dim3(256), 0, st, d_cnt, up.at<int>(ro), d_kbase, d_offs);
+    LGS_HIP_CHECK(hipGetLastError());
+    long long keys = 0;
+    {
+        char* pin = (char*)ctx->ensure_pinned(16);
+        LGS_HIP_CHECK(hipMemcpyAsync(pin, d_total, 8, hipMemcpyDeviceToHost, st));
+        ctx->sync();
+        std::memcpy(&keys, pin, 8);
+    }
+    const long long budget = std::max(1LL, std::min(ctx->ray_chunk_keys, 1LL << 30));
+    if (keys > budget) return false;
+    // phase 3: emit, sort, runs, apply -- raycast_maps' pass
+    const RayMap* d_maps = up.at<RayMap>(mo);
+    const BayesChains* d_chains = up.at<BayesChains>(co);
+    unsigned* d_keys = (unsigned*)ctx->ensure(S_RAY2, sizeof(unsigned) * keys);
+    unsigned* d_sorted = (unsigned*)ctx->ensure(S_RAY3, sizeof(unsigned) * keys);
+    int tok = ctx->timing_begin(K_RAY_EMIT, 4.0 * (double)keys);
+    hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st, d_rays, d_offs,
+                       multi ? d_rmap : nullptr, (int)nr, d_maps, d_keys, d_bad, 1);
+    ctx->timing_end(tok);
+    LGS_HIP_CHECK(hipGetLastError());
+    int cell_bits = 1;
+    while (cell_bits < 32 && (1ull << cell_bits) < cells) ++cell_bits;
+    unsigned* d_tmp = (unsigned*)ctx->ensure(S_RAY5, sizeof(unsigned) * keys);
+    keysort(ctx, d_keys, d_sorted, d_tmp, keys, 1, cell_bits, d_bad);
+    tok = ctx->timing_begin(K_RAY_APPLY, 4.0 * (double)keys);
+    const long long nw = (keys + 63) / 64;
+    const long long nw2 = (nw + 63) / 64;
+    unsigned long long* d_hitw = (unsigned long long*)ctx->ensure(S_RAY7, sizeof(unsigned long long) * (2 * nw + 3 * nw2));
+    unsigned long long* d_endw = d_hitw + nw;
+    unsigned long long* d_hit2 = d_endw + nw;
+    unsigned long long* d_miss2 = d_hit2 + nw2;
+    unsigned long long* d_end2 = d_miss2 + nw2;
+    const unsigned blocks = (unsigned)((keys + 255) / 256);
+    hipLaunchKernelGGL(k_runmask, dim3(blocks), dim3(256), 0, st, d_sorted, keys, 1, d_hitw, d_endw, RunIndex{});
+    hipLaunchKernelGGL(k_runsummary, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, d_hitw, d_endw, nw, d_hit2,
+                       d_miss2, d_end2);
+    hipLaunchKernelGGL(k_apply, dim3(blocks), dim3(256), 0, st, d_sorted, keys,
+                       RunBits{ d_hitw, d_endw, d_hit2, d_miss2, d_end2, nw }, d_maps, n_maps, d_chains, bp->prob_hit,
+                       bp->prob_miss, 1);
+    ctx->timing_end(tok);
+    if (tok >= 0)
+        hipLaunchKernelGGL(k_count_runs, dim3((unsigned)std::min<long long>((nw + 255) / 256, 512)), dim3(256), 0, st,
+                           d_endw, nw, d_runs);
+    LGS_HIP_CHECK(hipGetLastError());
+    char* pin = (char*)ctx->ensure_pinned(16);
+    LGS_HIP_CHECK(hipMemcpyAsync(pin, d_bad, 16, hipMemcpyDeviceToHost, st));
+    ctx->sync();
+    unsigned long long runs = 0;
+    std::memcpy(&bad, pin, sizeof(int));
+    std::memcpy(&runs, pin + 8, sizeof(runs));
+    if (tok >= 0) ctx->pending[tok].algo_bytes += 32.0 * (double)runs;
+    if (ctx->profile) ctx->harvest();
+    if (bad) throw Error(LGS_ERR_INTERNAL, bad_message(bad));
+    return true;
 }
 
 void raycast(lgs_map* m, std::vector<HitsPtr>&& scans, const lgs_builder_params* bp)
@@ -2051,10 +2410,27 @@ extern "C" int lgs_maps_construct_from_scans(lgs_ctx* ctx, lgs_map* const* maps,
             first[i] = idx_min[i];
             count[i] = idx_max[i] - idx_min[i] + 1;
         }
+        // LGS_F2_TIMING=1: host phases of each call on stderr (diagnostics)
+        static const bool timing = std::getenv("LGS_F2_TIMING") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (ctx->device_hits && construct_maps_device(ctx, maps, first.data(), count.data(), n_maps, scans, poses, bp)) {
+            if (timing)
+                std::fprintf(stderr, "f2 call us (device hits): %.1f\n",
+                             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+            return;
+        }
         std::vector<std::array<double, 4>> box;
         hits_and_boxes(jobs, first, count, scans, poses, bp, box);
+        const auto t1 = std::chrono::steady_clock::now();
         for (int i = 0; i < n_maps; ++i) map_resize_reset(maps[i], box[i][0], box[i][1], box[i][2], box[i][3]);
+        const auto t2 = std::chrono::steady_clock::now();
         raycast_maps(ctx, jobs, bp);
+        if (timing) {
+            const auto t3 = std::chrono::steady_clock::now();
+            auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+            std::fprintf(stderr, "f2 call us: hits %.1f resize %.1f raycast(+sync) %.1f\n", us(t0, t1), us(t1, t2),
+                         us(t2, t3));
+        }
     });
 }
 
@@ -2068,7 +2444,22 @@ extern "C" int lgs_map_construct_global(lgs_ctx* ctx, double res, int ps, const 
     // GridMapType gridMap { res, patchSize, 0, 0, Point2D(0, 0) } (:89-90)
     int rc = lgs_map_create(ctx, res, ps, 0, 0, 0.0, 0.0, &m);
     if (rc != LGS_OK) return rc;
-    rc = lgs_map_construct_from_scans(ctx, m, scans, poses, n, bp);  // :91
+    // :91, with the hit points and ray cells on the device (the map is new:
+    // no latest-map window to keep)
+    bool done = false;
+    if (ctx->device_hits && n > 0) {
+        rc = guarded(ctx, [&] {
+            LGS_HIP_CHECK(hipSetDevice(ctx->device));
+            m->ctx = ctx;
+            const int f = 0;
+            done = construct_maps_device(ctx, &m, &f, &n, 1, scans, poses, bp);
+        });
+        if (rc != LGS_OK) {
+            lgs_map_destroy(m);
+            return rc;
+        }
+    }
+    if (!done) rc = lgs_map_construct_from_scans(ctx, m, scans, poses, n, bp);
     if (rc != LGS_OK) {
         lgs_map_destroy(m);
         return rc;

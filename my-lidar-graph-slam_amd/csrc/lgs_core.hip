@@ -474,6 +474,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_PRIORITY_TAIL: ctx->prio_tail = value != 0.0; return LGS_OK;
     case LGS_OPT_HV_FULL: ctx->hv_full = value != 0.0; return LGS_OK;
     case LGS_OPT_SPLIT_CHUNKS: ctx->split_chunks = value != 0.0; return LGS_OK;
+    case LGS_OPT_DEVICE_HITS: ctx->device_hits = value != 0.0; return LGS_OK;
     case LGS_OPT_SORT_BARRIER_US:
         if (value < 0) return LGS_ERR_INVALID_ARG;
         ctx->sort_barrier_us = (long long)value;

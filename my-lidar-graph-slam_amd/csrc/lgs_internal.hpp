@@ -70,6 +70,7 @@ enum Slot {
     S_TEDGE,        // int [items][T]: generation-stamped 'angle touches the low map edge' flags; holds
                     // nothing else, so stamps never need clearing (zeroed once when allocated)
     S_RAY0, S_RAY1, S_RAY2, S_RAY3, S_RAY4, S_RAY5, S_RAY6, S_RAY7,
+    S_RAY8,         // device hit points / ray cells of a map rebuild (k_raycast.hip construct_maps_device)
     S_LS0, S_LS1,
     S_LIN0, S_LIN1,   // K4 staging
     S_LIN2,           // K4 split refine: flags, timeout word, double-buffered per-beam terms
@@ -274,7 +275,8 @@ struct lgs_ctx {
     int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
     bool small_window = true;    // one-launch search of one-block windows (LGS_OPT_SMALL_WINDOW)
     bool fused_planes = true;    // superblock units by k_super_hv (LGS_OPT_FUSED_PLANES)
-    bool split_chunks = true;    // calls of 32..64 matches as two chunks (LGS_OPT_SPLIT_CHUNKS)
+    bool device_hits = true;     // map rebuilds of many scans: hit points / ray cells on the device (LGS_OPT_DEVICE_HITS)
+    bool split_chunks = false;   // calls of 32..64 matches as two chunks (LGS_OPT_SPLIT_CHUNKS; measured r05, 8-rank loop block: 1.007 vs 0.869 ms as one)
     bool hv_full = false;        // k_super_hv stores 16-byte units whole (LGS_OPT_HV_FULL, A/B; measured r05: 0.24 vs 0.17 ms per 64 sets)
     // a batch's stages after the coarse-map builds run on `hi`, a stream of
     // the device's highest priority, behind an event on `stream`: the

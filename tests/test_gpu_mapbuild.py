@@ -52,11 +52,13 @@ def _perturb(poses, seed=1):
             for x, y, t in poses]
 
 
+@pytest.mark.parametrize("dev", [1, 0])
 @pytest.mark.parametrize("chunk", [0, 20000, 1])
-def test_after_loop_closure_rebuild(ctx, world, chunk):
+def test_after_loop_closure_rebuild(ctx, world, chunk, dev):
     """Four local maps (overlapping node ranges, one single-node map) rebuilt
     after the poses moved; chunk > 0 forces ray-cast passes of that many keys
-    (1 = one ray per pass), so passes split maps and scans."""
+    (1 = one ray per pass), so passes split maps and scans (the device hit
+    points, dev = 1, then hand over to the host path after resizing the maps)."""
     n = 48 if chunk != 1 else 12
     poses = _trajectory(n)
     dscans, oscans = _nodes(ctx, world, poses, 361 if chunk != 1 else 91)
@@ -65,11 +67,13 @@ def test_after_loop_closure_rebuild(ctx, world, chunk):
     gms, oms = _local_maps(ctx, ranges, poses, dscans, oscans)
     new = _perturb(poses)
     try:
+        ctx.set_option(abi.LGS_OPT_DEVICE_HITS, dev)
         if chunk:
             ctx.set_option(abi.LGS_OPT_RAY_CHUNK_KEYS, chunk)
         ctx.construct_maps(gms, ranges, dscans, new, abi.BuilderParams(*BP))
     finally:
         ctx.set_option(abi.LGS_OPT_RAY_CHUNK_KEYS, 1 << 28)
+        ctx.set_option(abi.LGS_OPT_DEVICE_HITS, 1)
     obp = ob.BuilderParams(*BP)
     for i, ((lo, hi), gm, om) in enumerate(zip(ranges, gms, oms)):
         om.construct(new[lo:hi + 1], oscans[lo:hi + 1], obp)
@@ -94,17 +98,20 @@ def test_after_loop_closure_equals_one_by_one(ctx, world):
             assert np.array_equal(x, y), i
 
 
+@pytest.mark.parametrize("dev", [1, 0])
 @pytest.mark.parametrize("chunk", [0, 50000])
-def test_global_map(ctx, world, chunk):
+def test_global_map(ctx, world, chunk, dev):
     """ConstructGlobalMap: a fresh 0x0 map at (0, 0), every node, PatchSize 64."""
     poses = _trajectory(40, seed=2)
     dscans, oscans = _nodes(ctx, world, poses, 541)
     try:
+        ctx.set_option(abi.LGS_OPT_DEVICE_HITS, dev)
         if chunk:
             ctx.set_option(abi.LGS_OPT_RAY_CHUNK_KEYS, chunk)
         gm = ctx.construct_global_map(0.05, 64, dscans, poses, abi.BuilderParams(*BP))
     finally:
         ctx.set_option(abi.LGS_OPT_RAY_CHUNK_KEYS, 1 << 28)
+        ctx.set_option(abi.LGS_OPT_DEVICE_HITS, 1)
     om = ob.OMap(0.05, 64, 0, 0)
     om.construct(poses, oscans, ob.BuilderParams(*BP))
     same_map(gm, om, "global")
@@ -169,3 +176,26 @@ def test_render_gray_matches_drawmap(ctx, world):
     want = np.where((cells <= 0.0) | (cells > 1.0), 192, ((1.0 - cells) * 255.0).astype(np.uint8)).astype(np.uint8)
     assert np.array_equal(img, want[::-1])
     assert (img == 192).any() and (img < 192).any()
+
+
+def test_device_hits_scan_filters_and_empty_scans(ctx, world):
+    """Device hit points: beams at exactly the usable range limits, zero and
+    NaN-free short ranges, a scan with no usable beam (its sensor still in
+    the box, no rays), and maps of one node -- every map as the oracle's."""
+    poses = _trajectory(10, seed=9)
+    ang = scene.beam_angles(181)
+    rs = [scene.ray_cast(world, p, ang) for p in poses]
+    rs[2] = np.full(181, 25.0)                 # every beam beyond 20 m: no hit
+    rs[4][::7] = 20.0                          # at the usable maximum (excluded)
+    rs[4][3::11] = 0.01                        # at the usable minimum (excluded)
+    rs[5][::5] = 0.0
+    dscans = [ctx.scan(r, ang) for r in rs]
+    oscans = [ob.OScan(r, ang) for r in rs]
+    ranges = [(0, 3), (2, 2), (4, 9)]
+    gms = [ctx.map(0.05, 32, 0, 0, center=poses[lo][:2]) for lo, _ in ranges]
+    oms = [ob.OMap(0.05, 32, 0, 0, center=poses[lo][:2]) for lo, _ in ranges]
+    ctx.construct_maps(gms, ranges, dscans, poses, abi.BuilderParams(*BP))
+    obp = ob.BuilderParams(*BP)
+    for i, ((lo, hi), gm, om) in enumerate(zip(ranges, gms, oms)):
+        om.construct(poses[lo:hi + 1], oscans[lo:hi + 1], obp)
+        same_map(gm, om, f"map{i}")
