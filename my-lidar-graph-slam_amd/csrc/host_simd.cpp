@@ -10,6 +10,8 @@
 #include <cmath>
 #include <immintrin.h>
 
+#include "sincos_avx2.hpp"
+
 namespace lgs {
 namespace {
 // floor(a / res) through a * (1 / res): the product is within 3 * 2^-53
@@ -53,5 +55,23 @@ void cells_of_points(const double* xy, long long n2, double mx, double my, doubl
         return;
     }
     for (long long j = 0; j < n2; ++j) out[j] = cell_div(xy[j], (j & 1) ? my : mx, res);
+}
+
+// s[j], c[j] = glibc sincos(x[j]) bit for bit: four at a time through the
+// AVX2 restatement (sincos_avx2.hpp), libm for lanes outside its domain and
+// the tail
+void sincos_batch(const double* x, long long n, double* s, double* c)
+{
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    long long j = 0;
+    if (avx2) {
+        for (; j + 4 <= n; j += 4) {
+            const int bad = glm::avx2::sincos4(x + j, s + j, c + j);
+            if (bad)
+                for (int l = 0; l < 4; ++l)
+                    if (bad >> l & 1) ::sincos(x[j + l], s + j + l, c + j + l);
+        }
+    }
+    for (; j < n; ++j) ::sincos(x[j], s + j, c + j);
 }
 }  // namespace lgs

@@ -20,6 +20,8 @@
 //   k_apply    one thread per run applies the Bayes updates sequentially and
 //              counts hits/misses
 #include "lgs_internal.hpp"
+
+#include <atomic>
 #include "glibc_math.hpp"
 
 #include <chrono>
@@ -1195,14 +1197,25 @@ ScanHits scan_hits(const lgs_scan* s, lgs_pose2d robot, const lgs_builder_params
     h.sensor = compound(robot, s->rel);
     const double minRange = smax(bp->usable_range_min, s->min_range);
     const double maxRange = smin(bp->usable_range_max, s->max_range);
-    h.xy.reserve(2 * (size_t)s->n);
+    // the usable beams' angles, then their sincos four at a time (glibc bit
+    // for bit, sincos_batch), then the points
+    thread_local std::vector<double> th, rr, sn, cs;
+    th.clear();
+    rr.clear();
     for (int i = 0; i < s->n; ++i) {
         const double r = s->h_ranges[i];
         if (r >= maxRange || r <= minRange) continue;
-        double sn, c;
-        ref_sincos(h.sensor.theta + s->h_angles[i], sn, c);
-        h.xy.push_back(h.sensor.x + r * c);
-        h.xy.push_back(h.sensor.y + r * sn);
+        th.push_back(h.sensor.theta + s->h_angles[i]);
+        rr.push_back(r);
+    }
+    const size_t m = th.size();
+    sn.resize(m);
+    cs.resize(m);
+    sincos_batch(th.data(), (long long)m, sn.data(), cs.data());
+    h.xy.resize(2 * m);
+    for (size_t j = 0; j < m; ++j) {
+        h.xy[2 * j] = h.sensor.x + rr[j] * cs[j];
+        h.xy[2 * j + 1] = h.sensor.y + rr[j] * sn[j];
     }
     double b0 = h.sensor.x, b1 = h.sensor.y, b2 = h.sensor.x, b3 = h.sensor.y;
     for (size_t q = 0; q + 1 < h.xy.size(); q += 2) {
@@ -1849,7 +1862,7 @@ struct LatestCache {
     void finish()
     {
         if (pending) {
-            LGS_HIP_CHECK(hipEventSynchronize(wev->ev));
+            wev->wait();
             pending = false;
         }
         std::vector<KeyBufPtr> r;
@@ -1894,11 +1907,12 @@ LatestCache& cache_of(lgs_map* m)
         c->wev = std::make_shared<WriterEvent>();
         if (hipHostMalloc((void**)&c->h_bad, 16, hipHostMallocMapped) != hipSuccess ||
             hipHostGetDevicePointer((void**)&c->d_bad, c->h_bad, 0) != hipSuccess ||
-            hipEventCreateWithFlags(&c->wev->ev, hipEventDisableTiming) != hipSuccess) {
+            hipHostMalloc((void**)&c->wev->flag, sizeof(unsigned), hipHostMallocCoherent) != hipSuccess) {
             delete c;
             throw Error(LGS_ERR_OOM, "latest-map cache allocation failed");
         }
         *c->h_bad = 0;
+        *c->wev->flag = 0;
         m->cache = c;
     }
     return *m->cache;
@@ -1913,12 +1927,28 @@ void invalidate_cache(lgs_map* m)
 }
 
 
-// The step's device work stays queued when the call returns: readers of the
-// maps on other streams wait for this event (grid_acquire).
+// The step's device work stays queued when the call returns: its completion
+// word (k_writer_done after the work) tells the host; readers of the maps on
+// other streams order after it (grid_acquire, WriterEvent).
+// (no fence: the kernels before it on the stream have completed and released
+// their writes at their ends; the word is the only thing the host reads, a
+// system-scope store into uncached coherent memory)
+__global__ void k_writer_done(unsigned* flag, unsigned gen)
+{
+    __hip_atomic_store(flag, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 void record_writer(LatestCache& C, hipStream_t st, lgs_map* latest, lgs_map* local)
 {
-    LGS_HIP_CHECK(hipEventRecord(C.wev->ev, st));
-    C.wev->st = st;
+    static std::atomic<unsigned> counter{ 0 };
+    unsigned gen = ++counter;
+    if (gen == 0) gen = ++counter;   // 0: the word's initial value
+    {
+        std::lock_guard<std::mutex> lk(C.wev->mu);
+        C.wev->st = st;
+        C.wev->gen = gen;
+    }
+    hipLaunchKernelGGL(k_writer_done, dim3(1), dim3(1), 0, st, C.wev->flag, gen);
+    LGS_HIP_CHECK(hipGetLastError());
     C.pending = true;
     latest->view.writer = C.wev;
     if (local) local->view.writer = C.wev;
@@ -2310,7 +2340,13 @@ extern "C" void lgs_map_destroy(lgs_map* m)
     if (!m) return;
     hipSetDevice(m->device);
     if (m->cache) {
-        if (m->cache->pending) hipEventSynchronize(m->cache->wev->ev);
+        if (m->cache->pending) {
+            try {
+                m->cache->wev->wait();
+            } catch (...) {
+                hipStreamSynchronize(m->cache->wev->st);
+            }
+        }
         delete m->cache;
         m->cache = nullptr;
     }

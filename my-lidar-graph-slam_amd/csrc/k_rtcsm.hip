@@ -5051,7 +5051,7 @@ lgs_grid* clone_grid(lgs_ctx* ctx, const lgs_grid* src)
     const size_t bytes = sizeof(double) * (size_t)src->w * (size_t)src->h;
     try {
         if (bytes) {
-            if (src->writer) LGS_HIP_CHECK(hipEventSynchronize(src->writer->ev));
+            if (src->writer) src->writer->wait();
             if (!ctx->peer_staged && peer_access(ctx->device, src->device)) {
                 LGS_HIP_CHECK(hipMemcpyPeerAsync(g->d, ctx->device, src->d, src->device, bytes, ctx->stream));
                 ctx->sync();

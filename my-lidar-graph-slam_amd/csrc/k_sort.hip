@@ -19,6 +19,7 @@
 #include "lgs_internal.hpp"
 
 #include <algorithm>
+#include <cstring>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -270,7 +271,8 @@ __global__ __launch_bounds__(kWideThreads) void k_sort_wide(const unsigned* __re
                                                             long long n, int lo, int dbits, int bits, int passes,
                                                             unsigned* __restrict__ counts,
                                                             unsigned* __restrict__ bar, int* __restrict__ err,
-                                                            unsigned long long ticks)
+                                                            unsigned long long ticks, unsigned* done_flag,
+                                                            unsigned done_gen)
 {
     constexpr int NT = kWideThreads, NW = NT / 64, KPT = kWideKPT, TILE = kWideTile;
     constexpr int R = 1 << RB;
@@ -438,6 +440,9 @@ __global__ __launch_bounds__(kWideThreads) void k_sort_wide(const unsigned* __re
             __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(bar + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // every tile is past its last wait: the host may reuse the reservation
+            __threadfence_system();
+            *(volatile unsigned*)done_flag = done_gen;
         }
     }
 }
@@ -450,36 +455,44 @@ namespace lgs {
 // other, so the tiles of every k_sort_wide in flight on a device -- from any
 // lgs_ctx, on any stream -- must fit the device at once.  Each launch
 // reserves its tiles against the device's capacity (half its occupancy: a
-// margin for other streams' and processes' work) and holds them until an
-// event recorded after the launch has completed; a sort that does not fit
-// beside the others takes the reduce-then-scan passes.  Reserve, launch and
-// record happen under the device's lock, so no event is queried before it is
-// recorded.
+// margin for other streams' and processes' work) and holds them until the
+// launch's last workgroup has written the launch's generation into its slot
+// of a coherent pinned flag array (r05: an event recorded after each launch
+// cost a ~5 us gap before the next kernel of a config-4 step); a sort that
+// does not fit beside the others takes the reduce-then-scan passes.
+// Reserve and launch happen under the device's lock.
 struct CoopDevice {
+    static constexpr int kSlots = 64;
     std::mutex mu;
     long long cap = 0, used = 0;
-    std::vector<std::pair<hipEvent_t, long long>> live;   // (event after the launch, tiles)
-    std::vector<hipEvent_t> spare;
+    unsigned* flags = nullptr;   // coherent pinned; slot s = generation of the last launch done in it
+    unsigned gen = 0;
+    struct Live {
+        int slot;
+        unsigned gen;
+        long long tiles;
+    };
+    std::vector<Live> live;   // launch order
+    std::vector<int> free_slots;
+    bool done(const Live& l) const { return __atomic_load_n(&flags[l.slot], __ATOMIC_ACQUIRE) == l.gen; }
     void release(size_t i)
     {
-        used -= live[i].second;
-        spare.push_back(live[i].first);
+        used -= live[i].tiles;
+        free_slots.push_back(live[i].slot);
         live.erase(live.begin() + (ptrdiff_t)i);
     }
     // every completed launch (when the capacity is short)
     void reclaim()
     {
         for (size_t i = 0; i < live.size();) {
-            if (hipEventQuery(live[i].first) == hipSuccess) release(i);
+            if (done(live[i])) release(i);
             else ++i;
         }
     }
-    // the oldest launches, while completed: one event query per launch in
-    // the common case (querying all 16 live events before every launch cost
-    // ~6 us of host time on the config-4 step's dependency chain)
+    // the oldest launches, while completed
     void reclaim_front()
     {
-        while (!live.empty() && hipEventQuery(live.front().first) == hipSuccess) release(0);
+        while (!live.empty() && done(live.front())) release(0);
     }
 };
 CoopDevice g_coop[64];
@@ -497,29 +510,23 @@ bool coop_launch(lgs_ctx* ctx, long long tiles, Launch&& launch)
         int per_cu = 0, cus = 0;
         LGS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_wide<10>, kWideThreads, 0));
         LGS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        LGS_HIP_CHECK(hipHostMalloc((void**)&D.flags, sizeof(unsigned) * CoopDevice::kSlots, hipHostMallocCoherent));
+        std::memset(D.flags, 0, sizeof(unsigned) * CoopDevice::kSlots);
+        for (int i = CoopDevice::kSlots - 1; i >= 0; --i) D.free_slots.push_back(i);
         D.cap = std::max(1LL, (long long)per_cu * cus / 2);
     }
     const long long cap = ctx->coop_tiles >= 0 ? std::min(D.cap, ctx->coop_tiles) : D.cap;
     if (tiles > cap) return false;
     D.reclaim_front();
-    if (D.used + tiles > cap || D.live.size() >= 16) D.reclaim();
-    if (D.used + tiles > cap) return false;
-    hipEvent_t ev = nullptr;
-    if (!D.spare.empty()) {
-        ev = D.spare.back();
-        D.spare.pop_back();
-    } else {
-        LGS_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    }
-    launch();
-    const hipError_t le = hipGetLastError();
-    if (le != hipSuccess) {
-        D.spare.push_back(ev);
-        LGS_HIP_CHECK(le);
-    }
-    LGS_HIP_CHECK(hipEventRecord(ev, ctx->stream));
+    if (D.used + tiles > cap || D.free_slots.empty()) D.reclaim();
+    if (D.used + tiles > cap || D.free_slots.empty()) return false;
+    const int slot = D.free_slots.back();
+    if (++D.gen == 0) ++D.gen;   // 0: a slot never used
+    launch(D.flags + slot, D.gen);
+    LGS_HIP_CHECK(hipGetLastError());
+    D.free_slots.pop_back();
     D.used += tiles;
-    D.live.emplace_back(ev, tiles);
+    D.live.push_back(CoopDevice::Live{ slot, D.gen, tiles });
     return true;
 }
 
@@ -551,13 +558,15 @@ void keysort(lgs_ctx* ctx, const unsigned* in, unsigned* out, unsigned* tmp, lon
             const int rb = wd > 8 ? 10 : 8;
             unsigned* counts = (unsigned*)ctx->ensure(S_RAY1, sizeof(unsigned) * (size_t)ctiles * (1u << rb) * wp);
             const unsigned long long ticks = (unsigned long long)ctx->sort_barrier_us * 100ull;   // 100 MHz
-            const bool done = coop_launch(ctx, ctiles, [&] {
+            const bool done = coop_launch(ctx, ctiles, [&](unsigned* flag, unsigned gen) {
                 if (rb == 10)
                     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_wide<10>), dim3((unsigned)ctiles), dim3(kWideThreads), 0,
-                                       st, in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar, err, ticks);
+                                       st, in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar, err, ticks, flag,
+                                       gen);
                 else
                     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sort_wide<8>), dim3((unsigned)ctiles), dim3(kWideThreads), 0,
-                                       st, in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar, err, ticks);
+                                       st, in, out, tmp, n, lo, wd, bits, wp, counts, ctl + kCtlBar, err, ticks, flag,
+                                       gen);
             });
             if (done) return;
         }

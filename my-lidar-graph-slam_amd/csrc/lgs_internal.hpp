@@ -402,17 +402,47 @@ struct lgs_ctx {
 
 namespace lgs {
 // Device work still writing a map's cells when its call returned (the latest
-// map's asynchronous incremental rebuild, k_raycast.hip): an event on the
-// writer's stream.  Readers on another stream wait for it (grid_acquire).
+// map's asynchronous incremental rebuild, k_raycast.hip): a one-thread kernel
+// after the work stores the writer's generation into a coherent pinned word
+// (r05: an event recorded on the stream instead cost the next kernel a ~5 us
+// gap on the config-4 step's chain).  The host waits by spinning on the word;
+// a reader on another stream gets an event recorded on the writer's stream
+// only when it needs one (grid_acquire: everything queued there so far, so
+// the writer's work included).
 struct WriterEvent {
-    hipEvent_t ev = nullptr;
+    hipEvent_t ev = nullptr;      // created and recorded lazily, under mu
     hipStream_t st = nullptr;
+    unsigned* flag = nullptr;     // coherent pinned word (k_raycast.hip record_writer)
+    unsigned gen = 0;             // the pending writer's generation
+    std::mutex mu;
     WriterEvent() = default;
     WriterEvent(const WriterEvent&) = delete;
     WriterEvent& operator=(const WriterEvent&) = delete;
     ~WriterEvent()
     {
         if (ev) hipEventDestroy(ev);
+        if (flag) hipHostFree(flag);
+    }
+    bool done() const { return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == gen; }
+    // the host waits for the writer's work; a stream that went idle without
+    // the word (a fault, a lost store) is an error
+    void wait()
+    {
+        for (unsigned spins = 1; !done(); ++spins) {
+            if (spins % 4096) continue;
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess && !done()) throw Error(LGS_ERR_INTERNAL, "map writer: completion word lost");
+            if (e != hipSuccess && e != hipErrorNotReady) LGS_HIP_CHECK(e);
+        }
+    }
+    // reader's stream after the writer's work (a device-side wait)
+    void order_after(hipStream_t reader)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (done()) return;
+        if (!ev) LGS_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        LGS_HIP_CHECK(hipEventRecord(ev, st));
+        LGS_HIP_CHECK(hipStreamWaitEvent(reader, ev, 0));
     }
 };
 }  // namespace lgs
@@ -602,6 +632,8 @@ void fetch_list(lgs_ctx* ctx, const std::vector<FetchSeg>& segs);
 // above this, staging goes through hipMemcpyAsync (a kernel reading host
 // memory over the link is slower than the copy engine for bulk data)
 constexpr size_t kFetchMaxBytes = size_t(1) << 20;
+// glibc sincos of x[j], j < n, bit for bit (host_simd.cpp: AVX2 restatement)
+void sincos_batch(const double* x, long long n, double* s, double* c);
 // floor((xy[j] - (j odd ? my : mx)) / res) for j < n2 (host_simd.cpp)
 void cells_of_points(const double* xy, long long n2, double mx, double my, double res, int* out);
 inline void scan_to_device(lgs_ctx* ctx, const lgs_scan* s) { scans_to_device(ctx, &s, 1); }
@@ -610,8 +642,7 @@ inline void scan_to_device(lgs_ctx* ctx, const lgs_scan* s) { scans_to_device(ct
 // from another stream (a device-side wait, no host synchronisation).
 inline void grid_acquire(lgs_ctx* ctx, const lgs_grid* g)
 {
-    if (g && g->writer && g->writer->st != ctx->stream)
-        LGS_HIP_CHECK(hipStreamWaitEvent(ctx->stream, g->writer->ev, 0));
+    if (g && g->writer && g->writer->st != ctx->stream) g->writer->order_after(ctx->stream);
 }
 
 // Host staging of one batch's descriptors: appended to a pinned buffer, then

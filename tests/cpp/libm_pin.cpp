@@ -8,6 +8,7 @@
 #include <random>
 
 #include "glibc_math.hpp"
+#include "sincos_avx2.hpp"
 
 namespace {
 uint64_t bits(double x)
@@ -47,6 +48,38 @@ long pin_sincos(uint64_t seed, long n, double lo, double hi, int mode, double* b
         if (bits(s0) != bits(s1) || bits(c0) != bits(c1)) {
             if (mism == 0 && bad) *bad = x;
             ++mism;
+        }
+    }
+    return mism;
+}
+
+// The host's four-lane restatement (sincos_avx2.hpp, host_simd.cpp
+// sincos_batch) on the same inputs, four at a time; lanes it reports outside
+// its domain must be exactly those gl_sincos_ok rejects.
+long pin_sincos_avx2(uint64_t seed, long n, double lo, double hi, int mode, double* bad)
+{
+    std::mt19937_64 rng(seed);
+    std::uniform_real_distribution<double> U(lo, hi);
+    long mism = 0;
+    for (long j = 0; j + 4 <= n; j += 4) {
+        double x[4], s1[4], c1[4];
+        for (int l = 0; l < 4; ++l) {
+            x[l] = U(rng);
+            if (mode == 1) {
+                const int e = 30 + (int)(rng() % 23);
+                x[l] = std::ldexp(std::nearbyint(std::ldexp(x[l], e)), -e);
+            }
+        }
+        const int out = glm::avx2::sincos4(x, s1, c1);
+        for (int l = 0; l < 4; ++l) {
+            double s0, c0;
+            libm_sincos(x[l], &s0, &c0);
+            const bool dom = glm::gl_sincos_ok(x[l]);
+            const bool ok = (out >> l & 1) ? !dom : (dom && bits(s0) == bits(s1[l]) && bits(c0) == bits(c1[l]));
+            if (!ok) {
+                if (mism == 0 && bad) *bad = x[l];
+                ++mism;
+            }
         }
     }
     return mism;

@@ -28,7 +28,7 @@ LIBM_SHA256 = "e5141752c850ea45691513faadc577133fedf77bcbf19473f97e7247561254b2"
 def pin():
     assert os.path.exists(LIB), "build first: make -C <repo> all"
     lib = C.CDLL(LIB)
-    for f in (lib.pin_sincos, lib.pin_pow3):
+    for f in (lib.pin_sincos, lib.pin_sincos_avx2, lib.pin_pow3):
         f.restype = C.c_long
         f.argtypes = [C.c_uint64, C.c_long, C.c_double, C.c_double, C.c_int, C.POINTER(C.c_double)]
     return lib
@@ -45,6 +45,16 @@ def test_libm_is_the_pinned_build():
 def test_sincos_bit_exact(pin, lo, hi, mode):
     bad = C.c_double()
     n = pin.pin_sincos(11 + mode, 2_000_000, lo, hi, mode, C.byref(bad))
+    assert n == 0, f"{n} mismatches, first at x = {bad.value!r}"
+
+
+@pytest.mark.parametrize("lo,hi", [(-2.0 ** -27, 2.0 ** -27), (-0.13, 0.13), (-0.86, 0.86), (-2.43, 2.43),
+                                   (-7.0, 7.0), (-40.0, 40.0), (-1.05e8, 1.05e8), (-2e8, 2e8)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_sincos_avx2_bit_exact(pin, lo, hi, mode):
+    """The host's four-lane sincos (hit points of every map update) against libm."""
+    bad = C.c_double()
+    n = pin.pin_sincos_avx2(31 + mode, 2_000_000, lo, hi, mode, C.byref(bad))
     assert n == 0, f"{n} mismatches, first at x = {bad.value!r}"
 
 
