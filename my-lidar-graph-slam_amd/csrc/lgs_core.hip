@@ -1160,11 +1160,10 @@ extern "C" int lgs_scan_interpolate(lgs_ctx* ctx, const lgs_scan* in, double dis
                     "need 0 < dist_scans <= dist_threshold_empty, both finite");
         const int n = in->n;
         std::vector<double> px(n), py(n);
+        sincos_batch(in->h_angles.data(), n, py.data(), px.data());   // glibc's sincos, four at a time
         for (int i = 0; i < n; ++i) {
-            double sn, cs;
-            ref_sincos(in->h_angles[i], sn, cs);
-            px[i] = in->h_ranges[i] * cs;
-            py[i] = in->h_ranges[i] * sn;
+            px[i] = in->h_ranges[i] * px[i];
+            py[i] = in->h_ranges[i] * py[i];
             LGS_REQUIRE(std::isfinite(px[i]) && std::isfinite(py[i]), "non-finite range or angle");
         }
         rr.reserve(2 * (size_t)n);

@@ -1,0 +1,44 @@
+"""Diagnostics (GPU): how much of the config-2 coarse work the seed leaves.
+For one 64-query batch of the bench workload: the seed's lower bound L (max of
+k_seed_super's candidates), the final score, the superblocks kept with L (bound
+>= L) and with the final score as L (the best any seed could do), and the
+coarse blocks actually scored."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "my-lidar-graph-slam_amd"))
+import bench  # noqa: E402
+from lgs_amd import abi, scene  # noqa: E402
+
+ctx = abi.Context(0)
+world = scene.make_world()
+ang = scene.beam_angles(1081)
+cells, mx, my = bench.bench_map(world, ang)
+rng = np.random.default_rng(1000)
+scans, inits, _ = bench.random_scans(world, ang, rng, 64)
+g = ctx.grid_from_array(cells, mx, my, 0.05)
+ds = [ctx.scan(r, ang) for r in scans]
+P, cost = abi.RtcsmParams(*bench.PARAMS), abi.CostGEParams(*bench.COST)
+outs = ctx.optimize_pose_query_batch(g, P, cost, ds, inits)
+rows = []
+for j, o in enumerate(outs):
+    sb = ctx.debug_buffer("sbound", j)
+    Lb = ctx.debug_buffer("L", j)
+    L = float(np.max(Lb[8:12]))
+    best = o.score_max
+    thr = o.score_threshold
+    keep_L = int(np.sum((sb > thr) & (sb >= L)))
+    keep_best = int(np.sum((sb > thr) & (sb >= best)))
+    rows.append(dict(L=L, best=best, thr=thr, superblocks=int(sb.size), kept_L=keep_L, kept_best=keep_best,
+                     coarse_blocks=int(o.coarse_blocks), fine_blocks=int(o.fine_blocks)))
+a = {k: float(np.mean([r[k] for r in rows])) for k in rows[0]}
+a["L_equals_best"] = int(sum(r["L"] >= r["best"] for r in rows))
+print(json.dumps(a, indent=1))
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+with open(os.path.join(ROOT, "gpurun_out", "diag_seed.json"), "w") as f:
+    json.dump(dict(mean=a, items=rows), f, indent=1)
