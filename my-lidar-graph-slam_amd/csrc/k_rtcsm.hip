@@ -96,6 +96,8 @@ struct MatchItem {
     int nparts;
     double* Lp;
     double* Lc;
+    double* seedm;           // wide seed: nseedm (coarse score, block, sum of |terms|) triples
+    int nseedm;              // candidates of the wide seed (k_seed_members workgroups)
     double* sbound;
     double* poses7;
     int4* cidx;
@@ -478,6 +480,7 @@ __device__ __forceinline__ void stage_lds(T* dst, const T* __restrict__ src, int
 
 constexpr int kSB = 4;   // superblock = kSB x kSB coarse blocks
 constexpr int kSeedCands = 4;   // k_seed_super workgroups (candidate superblocks)
+constexpr int kSeedWide = 16;   // wide seed (batches): at most this many candidate superblocks' best members compared
 
 __device__ __forceinline__ bool better(double a, long long ka, double b, long long kb)
 {
@@ -1968,6 +1971,239 @@ constexpr int kSeedRegParts = 4;   // parts held in registers per thread
 // the fine stage (25 poses padded to 32 lanes)
 constexpr int kSeedB1 = 24, kSeedB2 = 36;
 
+// k_seed_super step 3: the fine scores of block mk (coarse score cmk, sum of
+// magnitudes cma) over its lr x lr poses, any order, rounding-bounded; returns
+// L_b = min(fine max, cmk), both lowered by their rounding bounds (uniform
+// over the workgroup).  sidx: the block's angle's beam cells in LDS.
+__device__ __forceinline__ double seed_fine(const RtcsmPlan& pl, const double* __restrict__ grid, const double* __restrict__ zero,
+                            const int2* sidx, long long mk, double cmk, double cma, double* red, double* reda,
+                            double* sv)
+{
+    const int tid = threadIdx.x;
+    const int Nv = pl.Nv;
+    // 3. fine scores of block mk, any order, rounding-bounded
+    const int rem = (int)(mk % pl.P);
+    const int bjx = rem / pl.ncy, bjy = rem % pl.ncy;
+    const int lr = pl.low_res, npose = lr * lr;
+    int QP = 1;
+    while (QP < npose) QP <<= 1;   // npose <= 1024
+    const int G = (int)blockDim.x / QP;
+    const int q = tid % QP, gq = tid / QP;
+    double fs = 0.0, fa = 0.0;
+    if (q < npose) {
+        const int xo = q % lr, yo = q / lr;
+        const int xf = -pl.win_x + bjx * lr + xo, yf = -pl.win_y + bjy * lr + yo;
+        const int W = pl.W, H = pl.H;
+        const int cnt = (gq < Nv) ? (Nv - gq + G - 1) / G : 0;   // beams gq, gq + G, ...
+        for (int i0 = 0; i0 < cnt; i0 += kSeedB2) {
+            double buf[kSeedB2];
+#pragma unroll
+            for (int j = 0; j < kSeedB2; ++j) {
+                const int2 c = sidx[gq + G * min(i0 + j, cnt - 1)];
+                const int x = c.x + xf, y = c.y + yf;
+                const bool inb = (i0 + j < cnt) & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
+                buf[j] = gload(inb ? grid + (unsigned)(y * W + x) : zero);
+            }
+#pragma unroll
+            for (int j = 0; j < kSeedB2; ++j) {
+                fs += buf[j];
+                fa += fabs(buf[j]);
+            }
+        }
+    }
+    __syncthreads();
+    // pose totals: lanes of a wave with equal q (QP < 64) by shuffles,
+    // then the waves through LDS
+    for (int off = QP; off < 64; off <<= 1) {
+        fs += __shfl_xor(fs, off, 64);
+        fa += __shfl_xor(fa, off, 64);
+    }
+    const int wq = min(QP, 64);
+    if ((tid & 63) < wq) {
+        red[(tid >> 6) * wq + (tid & 63)] = fs;
+        reda[(tid >> 6) * wq + (tid & 63)] = fa;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        double lv = -INFINITY;
+        // poses q: this lane's q (QP <= 64) or q = tid + 64 j (QP > 64)
+        for (int q0 = tid; q0 < npose; q0 += 64) {
+            double ts = 0.0, ta = 0.0;
+            if (QP <= 64) {
+                for (int j = 0; j < (int)(blockDim.x >> 6); ++j) {
+                    ts += red[j * wq + q0];
+                    ta += reda[j * wq + q0];
+                }
+            } else {   // QP > 64: a wave holds 64 poses of one group
+                for (int j = 0; j < (int)(blockDim.x >> 6); ++j)
+                    if (((j * 64) % QP) == (q0 / 64) * 64) {
+                        ts += red[j * wq + (q0 & 63)];
+                        ta += reda[j * wq + (q0 & 63)];
+                    }
+            }
+            lv = fmax(lv, ts - (4.0 * (double)(Nv + 2) * 0x1p-53) * ta);
+        }
+        for (int off = 32; off > 0; off >>= 1) lv = fmax(lv, __shfl_xor(lv, off, 64));
+        if (tid == 0) sv[0] = lv;
+    }
+    __syncthreads();
+    // s_final >= f_mk if the reference refines block mk, else >= c_mk
+    // (it skips the block only when c_mk <= scoreMax), so min(f, c) is a
+    // lower bound of the result for ANY block, unsafe ones included
+    // (their f may exceed c); both terms rounding-bounded from below
+    return fmin(sv[0], cmk - (4.0 * (double)(Nv + 2) * 0x1p-53) * cma);
+}
+
+// Wide seed for batches (r05, LGS_OPT_SEED_WIDE): k_seed_members, one
+// 256-thread workgroup per candidate superblock b < kSeedWide, runs steps 1-2
+// (the candidate as the b-th best of k_super's per-chunk bests by rank, the
+// parts staged in LDS) and publishes its best member (coarse score, block,
+// sum of magnitudes) to it.seedm; then k_seed_super MODE 2, kSeedCands
+// workgroups, takes the b-th best of those members by coarse score and runs
+// steps 3-4 on it (MODE 0: steps 1-4 as above).  The final best block was its
+// superblock's best member in every config-2 query measured, and that
+// superblock ranked 2-12 by bound where the four candidates missed it
+// (tools/diag_seed.py): a third of the queries then scored ~4.5x the coarse
+// blocks.  Sixteen candidates cost member sums, not fine scores.
+constexpr int kSeedMembersThreads = 256;
+constexpr int kSeedWideMaxParts = 1024;   // parts staged in LDS (larger searches: the narrow seed)
+__global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items items)
+{
+    const MatchItem& it = items[blockIdx.y];
+    const RtcsmPlan& pl = it.pl;
+    const double* __restrict__ cmap = it.cmap;
+    const int nparts = it.nparts;
+    if (blockIdx.x == 0 && threadIdx.x < 2 && it.keepc) it.keepc[threadIdx.x] = 0;   // before k_keep
+    extern __shared__ char smem[];
+    __shared__ double red[2][kSeedMembersThreads / 64][16];
+    __shared__ long long s_cand;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nsb2 = pl.nsbx * pl.nsby;
+    const int Nv = pl.Nv;
+    // 1. candidate b by wave 0: the parts in registers (16 per lane), b + 1
+    // rounds of a wave argmax, each taking the best part out (the narrow
+    // seed's order: bound, then block order); a candidate needs a bound
+    // above thr
+    if (w == 0) {
+        constexpr int R = kSeedWideMaxParts / 64;
+        double v[R];
+        long long k[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = lane + 64 * r;
+            v[r] = (i < nparts) ? it.part_c[i] : -INFINITY;
+            k[r] = (i < nparts) ? it.part_k[i] : LLONG_MAX;
+        }
+        long long pick = LLONG_MAX;
+        for (int round = 0; round <= (int)blockIdx.x; ++round) {
+            double bv = -INFINITY;
+            long long bk = LLONG_MAX;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (better(v[r], k[r], bv, bk)) {
+                    bv = v[r];
+                    bk = k[r];
+                }
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ov = __shfl_xor(bv, off, 64);
+                const long long ok = __shfl_xor(bk, off, 64);
+                if (better(ov, ok, bv, bk)) {
+                    bv = ov;
+                    bk = ok;
+                }
+            }
+            if (bk == LLONG_MAX || bv == -INFINITY || !(bv > pl.thr)) break;   // uniform: no candidate b
+            if (round == (int)blockIdx.x) pick = bk;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (k[r] == bk) v[r] = -INFINITY, k[r] = LLONG_MAX;
+        }
+        if (lane == 0) s_cand = pick;
+    }
+    __syncthreads();
+    double* out = it.seedm + 3 * blockIdx.x;
+    const long long ck = s_cand;
+    if (ck == LLONG_MAX) {   // no candidate b: an empty member
+        if (tid == 0) {
+            out[0] = -INFINITY;
+            out[1] = __builtin_bit_cast(double, (long long)LLONG_MAX);
+            out[2] = 0.0;
+        }
+        return;
+    }
+    const int ct = (int)(ck / nsb2), csb = (int)(ck % nsb2);
+    // 2. member sums: member m = tid % 16, beam group g = tid / 16 (16 groups)
+    int* srow = (int*)smem;   // [Nv]
+    stage_lds(srow, it.cbase + (size_t)ct * Nv, Nv);
+    __syncthreads();
+    constexpr int G = kSeedMembersThreads / 16;
+    const int m = tid & 15, g = tid >> 4;
+    const int jx = kSB * (csb % pl.nsbx) + (m & 3);
+    const int jy = kSB * (csb / pl.nsbx) + (m >> 2);
+    const bool valid = jx < pl.ncx && jy < pl.ncy;
+    double s = 0.0, sa = 0.0;   // member sum and its sum of magnitudes (any order)
+    if (valid) {
+        const double* __restrict__ lb = cmap + (jy * pl.Wqp + jx);
+        const int cnt = (g < Nv) ? (Nv - g + G - 1) / G : 0;   // beams g, g + G, ...
+        double acc[4] = { 0.0, 0.0, 0.0, 0.0 };
+        for (int i0 = 0; i0 < cnt; i0 += kSeedB1) {
+            double buf[kSeedB1];
+#pragma unroll
+            for (int j = 0; j < kSeedB1; ++j) {
+                const int i = min(i0 + j, cnt - 1);
+                buf[j] = (i0 + j < cnt) ? gload(lb + srow[g + G * i]) : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < kSeedB1; ++j) {
+                acc[j & 3] += buf[j];
+                sa += fabs(buf[j]);
+            }
+        }
+        s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    }
+    // member totals: the wave's 4 groups by shuffles, then the waves
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    sa += __shfl_xor(sa, 16, 64);
+    sa += __shfl_xor(sa, 32, 64);
+    if (lane < 16) {
+        red[0][w][m] = s;
+        red[1][w][m] = sa;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        double mv = -1.0, ma = 0.0;
+        long long mk = LLONG_MAX;
+        if (tid < 16 && valid) {
+            double tot = 0.0, tota = 0.0;
+#pragma unroll
+            for (int j = 0; j < kSeedMembersThreads / 64; ++j) {
+                tot += red[0][j][tid];
+                tota += red[1][j][tid];
+            }
+            mv = tot;
+            ma = tota;
+            mk = (long long)ct * pl.P + (long long)jx * pl.ncy + jy;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ov = __shfl_xor(mv, off, 64);
+            const double oa = __shfl_xor(ma, off, 64);
+            const long long ok = __shfl_xor(mk, off, 64);
+            if (better(ov, ok, mv, mk)) {
+                mv = ov;
+                ma = oa;
+                mk = ok;
+            }
+        }
+        if (tid == 0) {
+            out[0] = mv;
+            out[1] = __builtin_bit_cast(double, mk);
+            out[2] = ma;
+        }
+    }
+}
+
+template <int MODE>
 __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* __restrict__ zero)
 {
     const MatchItem& it = items[blockIdx.y];
@@ -1981,7 +2217,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
     const int nparts = it.nparts;
     double* __restrict__ Lc = it.Lc;
     RtcsmRecord* rec = it.rec;
-    if (blockIdx.x == 0 && threadIdx.x < 2 && it.keepc) it.keepc[threadIdx.x] = 0;   // before k_keep
+    if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < 2 && it.keepc) it.keepc[threadIdx.x] = 0;   // before k_keep
     extern __shared__ char smem[];
     __shared__ double sv[16];
     __shared__ long long sk[16];
@@ -1993,6 +2229,44 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
     const int Nv = pl.Nv;
     LGS_PROBE_DECL;
     LGS_PROBE_MARK();
+    double Lmine = -INFINITY;
+    if constexpr (MODE == 2) {
+        // the b-th best published member (coarse score, then block order)
+        if (tid < 64) {
+            const bool ok = tid < it.nseedm;
+            const double mv = ok ? it.seedm[3 * tid] : -INFINITY;
+            const long long mk = ok ? __builtin_bit_cast(long long, it.seedm[3 * tid + 1]) : LLONG_MAX;
+            const double ma = ok ? it.seedm[3 * tid + 2] : 0.0;
+            const bool valid = ok && mk != LLONG_MAX && mv > -INFINITY;
+            int rank = 0;
+            for (int j = 0; j < it.nseedm; ++j) {
+                const double ov = __shfl(mv, j, 64);
+                const long long okk = __shfl(mk, j, 64);
+                const bool ovalid = __shfl((int)valid, j, 64) != 0;
+                rank += (ovalid && j != tid && better(ov, okk, mv, mk)) ? 1 : 0;
+            }
+            if (tid == 0) sk[0] = LLONG_MAX;
+            __builtin_amdgcn_wave_barrier();
+            if (valid && rank == (int)blockIdx.x) {
+                sk[0] = mk;
+                sv[1] = mv;
+                sv[2] = ma;
+            }
+        }
+        __syncthreads();
+        if (sk[0] != LLONG_MAX) {
+            const int ct = (int)(sk[0] / pl.P);
+            int2* sidx = (int2*)(smem + ((sizeof(int) * (size_t)Nv + 15) & ~(size_t)15));   // [Nv]
+            stage_lds(sidx, idx + (size_t)ct * Nv, Nv);
+            __syncthreads();
+            Lmine = seed_fine(pl, grid, zero, sidx, sk[0], sv[1], sv[2], red, reda, sv);
+        }
+        if (tid == 0) {
+            Lc[blockIdx.x] = Lmine;
+            if (blockIdx.x == 0) rec->coarse_evals = 0ull;   // k_coarse_rows counts
+        }
+        return;
+    }
     double pv[kSeedRegParts];
     long long pk[kSeedRegParts];
 #pragma unroll
@@ -2027,7 +2301,6 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             if (pk[j] == bk) pv[j] = -INFINITY, pk[j] = LLONG_MAX;
         __syncthreads();
     }
-    double Lmine = -INFINITY;
     LGS_PROBE_MARK();
     if (nc > (int)blockIdx.x) {
         const long long ck = cand[blockIdx.x];
@@ -2107,81 +2380,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             }
         }
         __syncthreads();
-        const long long mk = sk[0];
-        const double cmk = sv[1], cma = sv[2];   // block mk's coarse score (any order), sum of |terms|
-        // 3. fine scores of block mk, any order, rounding-bounded
-        const int rem = (int)(mk % pl.P);
-        const int bjx = rem / pl.ncy, bjy = rem % pl.ncy;
-        const int lr = pl.low_res, npose = lr * lr;
-        LGS_PROBE_MARK();
-        int QP = 1;
-        while (QP < npose) QP <<= 1;   // npose <= 1024
-        const int G = (int)blockDim.x / QP;
-        const int q = tid % QP, gq = tid / QP;
-        double fs = 0.0, fa = 0.0;
-        if (q < npose) {
-            const int xo = q % lr, yo = q / lr;
-            const int xf = -pl.win_x + bjx * lr + xo, yf = -pl.win_y + bjy * lr + yo;
-            const int W = pl.W, H = pl.H;
-            const int cnt = (gq < Nv) ? (Nv - gq + G - 1) / G : 0;   // beams gq, gq + G, ...
-            for (int i0 = 0; i0 < cnt; i0 += kSeedB2) {
-                double buf[kSeedB2];
-#pragma unroll
-                for (int j = 0; j < kSeedB2; ++j) {
-                    const int2 c = sidx[gq + G * min(i0 + j, cnt - 1)];
-                    const int x = c.x + xf, y = c.y + yf;
-                    const bool inb = (i0 + j < cnt) & ((unsigned)x < (unsigned)W) & ((unsigned)y < (unsigned)H);
-                    buf[j] = gload(inb ? grid + (unsigned)(y * W + x) : zero);
-                }
-#pragma unroll
-                for (int j = 0; j < kSeedB2; ++j) {
-                    fs += buf[j];
-                    fa += fabs(buf[j]);
-                }
-            }
-        }
-        __syncthreads();
-        LGS_PROBE_MARK();
-        // pose totals: lanes of a wave with equal q (QP < 64) by shuffles,
-        // then the waves through LDS
-        for (int off = QP; off < 64; off <<= 1) {
-            fs += __shfl_xor(fs, off, 64);
-            fa += __shfl_xor(fa, off, 64);
-        }
-        const int wq = min(QP, 64);
-        if ((tid & 63) < wq) {
-            red[(tid >> 6) * wq + (tid & 63)] = fs;
-            reda[(tid >> 6) * wq + (tid & 63)] = fa;
-        }
-        __syncthreads();
-        if (tid < 64) {
-            double lv = -INFINITY;
-            // poses q: this lane's q (QP <= 64) or q = tid + 64 j (QP > 64)
-            for (int q0 = tid; q0 < npose; q0 += 64) {
-                double ts = 0.0, ta = 0.0;
-                if (QP <= 64) {
-                    for (int j = 0; j < (int)(blockDim.x >> 6); ++j) {
-                        ts += red[j * wq + q0];
-                        ta += reda[j * wq + q0];
-                    }
-                } else {   // QP > 64: a wave holds 64 poses of one group
-                    for (int j = 0; j < (int)(blockDim.x >> 6); ++j)
-                        if (((j * 64) % QP) == (q0 / 64) * 64) {
-                            ts += red[j * wq + (q0 & 63)];
-                            ta += reda[j * wq + (q0 & 63)];
-                        }
-                }
-                lv = fmax(lv, ts - (4.0 * (double)(Nv + 2) * 0x1p-53) * ta);
-            }
-            for (int off = 32; off > 0; off >>= 1) lv = fmax(lv, __shfl_xor(lv, off, 64));
-            if (tid == 0) sv[0] = lv;
-        }
-        __syncthreads();
-        // s_final >= f_mk if the reference refines block mk, else >= c_mk
-        // (it skips the block only when c_mk <= scoreMax), so min(f, c) is a
-        // lower bound of the result for ANY block, unsafe ones included
-        // (their f may exceed c); both terms rounding-bounded from below
-        Lmine = fmin(sv[0], cmk - (4.0 * (double)(Nv + 2) * 0x1p-53) * cma);
+        Lmine = seed_fine(pl, grid, zero, sidx, sk[0], sv[1], sv[2], red, reda, sv);
         LGS_PROBE_MARK();
     }
     // 4. publish
@@ -3475,7 +3674,7 @@ ItemLayout item_layout(int Tmax, int NvMax, int P, int nsb2, int chunks, int cb,
     L.poses7 = take(sizeof(double) * 21);
     L.cidx = take(sizeof(int4) * 7 * (size_t)Nmax);
     L.terms = take(sizeof(double) * 7 * (size_t)Nmax);
-    L.count = take(128);   // Lp, Lc[kSeedCands], nsel
+    L.count = take(128 + 24 * kSeedWide);   // Lp, Lc[kSeedCands], nsel | wide-seed members
     L.total = o;
     return L;
 }
@@ -3499,6 +3698,7 @@ void bind_workspace(MatchItem& it, char* base, const ItemLayout& L, int frows)
     it.Lp = (double*)(base + L.count);
     it.Lc = (double*)(base + L.count + 64);
     it.nsel = (int*)(base + L.count + 64 + 8 * kSeedCands);
+    it.seedm = (double*)(base + L.count + 128);
     it.dlist = (int*)(base + L.dlist);
     static_assert(64 + 8 * kSeedCands + 4 <= 128, "count block layout");
     it.frows = frows;
@@ -3897,8 +4097,20 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             const int tok = ctx->timing_begin(K_SEED, 8.0 * kSeedCands * (B.low_res * B.low_res + 16.0) * B.NvMax * n);
             const size_t lds = ((sizeof(int) * (size_t)std::max(B.NvMax, 1) + 15) & ~(size_t)15) +
                                sizeof(int2) * (size_t)std::max(B.NvMax, 1);   // coarse + fine beam rows
-            if (!ctx->skipped(K_SEED))
-                hipLaunchKernelGGL(k_seed_super, dim3(kSeedCands, n), dim3(1024), lds, st, d_items, zero);
+            // the wide seed for batches; a lone match keeps the one-launch seed
+            // (measured r05: lone p50 0.132 -> 0.140 ms with the extra launch,
+            // p90 0.155 -> 0.145)
+            const int nwide = std::min(ctx->seed_wide, kSeedWide);
+            bool wide = nwide > kSeedCands && n >= ctx->lanes_min_batch;
+            for (const auto& itm : items) wide = wide && itm.nparts <= kSeedWideMaxParts;
+            if (!ctx->skipped(K_SEED) && wide) {
+                hipLaunchKernelGGL(k_seed_members, dim3(nwide, n), dim3(kSeedMembersThreads),
+                                   sizeof(int) * (size_t)std::max(B.NvMax, 1), st, d_items);
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_seed_super<2>), dim3(kSeedCands, n), dim3(1024), lds, st,
+                                   d_items, zero);
+            } else if (!ctx->skipped(K_SEED))
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_seed_super<0>), dim3(kSeedCands, n), dim3(1024), lds, st,
+                                   d_items, zero);
             else if (B.wl.cnt)   // (diagnostics) the work-list counters k_seed_super zeroes
                 LGS_HIP_CHECK(hipMemsetAsync(B.wl.cnt, 0, sizeof(int) * 16 * (size_t)n, st));
             ctx->timing_end(tok);
@@ -4337,6 +4549,7 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
         it.rec = d_rec + j;
         it.keepc = B.wl.cnt ? B.wl.cnt + 16 * j : sctr ? sctr + j : nullptr;
         it.nparts = item_nparts(B, it.pl, B.pruned);
+        it.nseedm = std::min(ctx->seed_wide, kSeedWide);
     }
     ctx->dbg.assign((size_t)n, lgs_ctx::DbgItem{});
     for (int j = 0; j < n; ++j) {

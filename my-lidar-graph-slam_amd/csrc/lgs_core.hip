@@ -475,6 +475,10 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_HV_FULL: ctx->hv_full = value != 0.0; return LGS_OK;
     case LGS_OPT_SPLIT_CHUNKS: ctx->split_chunks = value != 0.0; return LGS_OK;
     case LGS_OPT_DEVICE_HITS: ctx->device_hits = value != 0.0; return LGS_OK;
+    case LGS_OPT_SEED_WIDE:
+        if (!(value >= 0.0 && value <= 16.0)) return LGS_ERR_INVALID_ARG;
+        ctx->seed_wide = (int)value;
+        return LGS_OK;
     case LGS_OPT_SORT_BARRIER_US:
         if (value < 0) return LGS_ERR_INVALID_ARG;
         ctx->sort_barrier_us = (long long)value;

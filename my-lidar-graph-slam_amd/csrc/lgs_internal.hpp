@@ -275,6 +275,7 @@ struct lgs_ctx {
     int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
     bool small_window = true;    // one-launch search of one-block windows (LGS_OPT_SMALL_WINDOW)
     bool fused_planes = true;    // superblock units by k_super_hv (LGS_OPT_FUSED_PLANES)
+    int seed_wide = 12;          // batches: candidate superblocks whose best members seed the bound (LGS_OPT_SEED_WIDE; <= 4: one launch)
     bool device_hits = true;     // map rebuilds of many scans: hit points / ray cells on the device (LGS_OPT_DEVICE_HITS)
     bool split_chunks = false;   // calls of 32..64 matches as two chunks (LGS_OPT_SPLIT_CHUNKS; measured r05, 8-rank loop block: 1.007 vs 0.869 ms as one)
     bool hv_full = false;        // k_super_hv stores 16-byte units whole (LGS_OPT_HV_FULL, A/B; measured r05: 0.24 vs 0.17 ms per 64 sets)

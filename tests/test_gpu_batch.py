@@ -344,3 +344,33 @@ def test_fine_staged_equals_gathers(ctx, world, n_cells, low_edge):
     assert [_record(b) for b in stag] == gath
     for j, ((r, init), b) in enumerate(zip(qs, stag)):
         assert_same(b, oracle_match(cells, mx, my, 0.05, params, r, ang, init), f"q{j}")
+
+
+def test_wide_seed_same_records_less_coarse_work(ctx, world, small_map):
+    """LGS_OPT_SEED_WIDE (the pruning bound seeded from 16 candidate
+    superblocks' best members, batches): every record field equal to the
+    4-candidate seed's but coarse_blocks / fine_blocks, the device's pruned
+    work, which may only shrink in total; and the oracle's answer (a
+    config-2-sized window)."""
+    cells, mx, my = small_map
+    rng = np.random.default_rng(33)
+    ang, qs = _queries(world, rng, 12, 541)
+    params = (5, 4.0, 4.0, 1.0, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    scans = [ctx.scan(r, ang) for r, _ in qs]
+    inits = [i for _, i in qs]
+    try:
+        ctx.set_option(abi.LGS_OPT_SEED_WIDE, 0)
+        narrow = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, inits)]
+        ctx.set_option(abi.LGS_OPT_SEED_WIDE, 1)
+        wide = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, inits)]
+    finally:
+        ctx.set_option(abi.LGS_OPT_SEED_WIDE, 1)
+    strip = lambda rec: rec[:6] + rec[8:]   # all but coarse_blocks / fine_blocks (the device's work)
+    assert [strip(r) for r in wide] == [strip(r) for r in narrow], _diff(wide, narrow)
+    for f in (6, 7):
+        assert sum(r[f] for r in wide) <= sum(r[f] for r in narrow), ([r[f] for r in wide], [r[f] for r in narrow])
+    for j in (0, 5, 11):
+        out = ctx.optimize_pose_query_batch(g, P, cost, scans, inits)[j]
+        assert_same(out, oracle_match(cells, mx, my, 0.05, params, qs[j][0], ang, inits[j]), f"q{j}")

@@ -111,14 +111,20 @@ def test_bench_configuration_three_contexts(ctx, bench_problem):
             ora = list(ex.map(oracle, pick))
         for (i, k, q), o in zip(pick, ora):
             assert_same(got[(i, k)][1][q], o, f"ctx{i} call{k} q{q}")
-        # every record against the lone call on its own context
+        # every record against the lone call on its own context (the batch's
+        # wide seed -- LGS_OPT_SEED_WIDE -- prunes more than the lone call's
+        # one-launch seed: the blocks scored may only shrink on the whole)
+        lone_blocks, batch_blocks = [], []
         for (i, k), (js, recs) in got.items():
             c, g, ds = state[i]
             for q, (j, b) in enumerate(zip(js, recs)):
                 one = c.optimize_pose_query(g, P, cost, ds[j], inits[j])
-                _lone_equal(b, one, f"ctx{i} call{k} q{q}")
+                _lone_equal(b, one, f"ctx{i} call{k} q{q}", blocks=False)
+                lone_blocks.append(one.coarse_blocks)
+                batch_blocks.append(b.coarse_blocks)
             # the superblock pruning scores a small fraction of the ~421 x 17 x 17 blocks
             assert np.mean([b.coarse_blocks for b in recs]) < 0.1 * 421 * 17 * 17
+        assert sum(batch_blocks) <= sum(lone_blocks), (sum(batch_blocks), sum(lone_blocks))
     finally:
         for c in ctxs[1:]:
             c.close()

@@ -34,10 +34,38 @@ for j, o in enumerate(outs):
     thr = o.score_threshold
     keep_L = int(np.sum((sb > thr) & (sb >= L)))
     keep_best = int(np.sum((sb > thr) & (sb >= best)))
-    rows.append(dict(L=L, best=best, thr=thr, superblocks=int(sb.size), kept_L=keep_L, kept_best=keep_best,
-                     coarse_blocks=int(o.coarse_blocks), fine_blocks=int(o.fine_blocks)))
+    # the best pose's superblock and its rank among all superblocks by bound
+    wx, wy, wt = o.win[0], o.win[1], o.win[2]
+    lr = bench.PARAMS[0]
+    ncx, ncy = 2 * wx // lr + 1, 2 * wy // lr + 1
+    nsbx, nsby = (ncx + 3) // 4, (ncy + 3) // 4
+    jx, jy, tt = (o.best_win[0] + wx) // lr, (o.best_win[1] + wy) // lr, o.best_win[2] + wt
+    k = tt * nsbx * nsby + (jy // 4) * nsbx + (jx // 4)
+    rank = int(np.sum(sb > sb[k]))
+    # the best per-angle superblock ranks (the seed's candidate pool: k_super's per-angle bests)
+    per_angle = sb.reshape(-1, nsbx * nsby).max(axis=1)
+    arank = int(np.sum(per_angle > per_angle[tt]))
+    # the best block's coarse-score rank among its superblock's members
+    cs = ctx.debug_buffer("cscore", j)
+    P_ = ncx * ncy
+    mem = []
+    for b_ in range(4):
+        for a_ in range(4):
+            mx_, my_ = 4 * (jx // 4) + a_, 4 * (jy // 4) + b_
+            if mx_ < ncx and my_ < ncy:
+                mem.append(cs[tt * P_ + mx_ * ncy + my_])
+    cbest = cs[tt * P_ + jx * ncy + jy]
+    mrank = int(np.sum(np.array(mem) > cbest))
+    rows.append(dict(member_rank=mrank, L=L, best=best, thr=thr, superblocks=int(sb.size), kept_L=keep_L, kept_best=keep_best,
+                     coarse_blocks=int(o.coarse_blocks), fine_blocks=int(o.fine_blocks), best_sb_rank=rank,
+                     best_angle_rank=arank, best_is_angle_max=int(sb[k] >= per_angle[tt])))
 a = {k: float(np.mean([r[k] for r in rows])) for k in rows[0]}
 a["L_equals_best"] = int(sum(r["L"] >= r["best"] for r in rows))
+for n in (1, 2, 3, 4, 6, 8):
+    a[f"member_in_top{n}"] = int(sum(r["member_rank"] < n for r in rows))
+for n in (4, 8, 16, 32, 64):
+    a[f"best_sb_in_top{n}"] = int(sum(r["best_sb_rank"] < n for r in rows))
+    a[f"best_angle_in_top{n}"] = int(sum(r["best_angle_rank"] < n for r in rows))
 print(json.dumps(a, indent=1))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 with open(os.path.join(ROOT, "gpurun_out", "diag_seed.json"), "w") as f:
