@@ -30,6 +30,7 @@ for j, o in enumerate(outs):
     sb = ctx.debug_buffer("sbound", j)
     Lb = ctx.debug_buffer("L", j)
     L = float(np.max(Lb[8:12]))
+    Lbest_b = int(np.argmax(Lb[8:12]))   # which of the 4 fine-scored members gave L (wide seed: by coarse rank)
     best = o.score_max
     thr = o.score_threshold
     keep_L = int(np.sum((sb > thr) & (sb >= L)))
@@ -56,11 +57,13 @@ for j, o in enumerate(outs):
                 mem.append(cs[tt * P_ + mx_ * ncy + my_])
     cbest = cs[tt * P_ + jx * ncy + jy]
     mrank = int(np.sum(np.array(mem) > cbest))
-    rows.append(dict(member_rank=mrank, L=L, best=best, thr=thr, superblocks=int(sb.size), kept_L=keep_L, kept_best=keep_best,
+    rows.append(dict(Lbest_b=Lbest_b, member_rank=mrank, L=L, best=best, thr=thr, superblocks=int(sb.size), kept_L=keep_L, kept_best=keep_best,
                      coarse_blocks=int(o.coarse_blocks), fine_blocks=int(o.fine_blocks), best_sb_rank=rank,
                      best_angle_rank=arank, best_is_angle_max=int(sb[k] >= per_angle[tt])))
 a = {k: float(np.mean([r[k] for r in rows])) for k in rows[0]}
 a["L_equals_best"] = int(sum(r["L"] >= r["best"] for r in rows))
+for n in range(4):
+    a[f"L_from_b{n}"] = int(sum(r["Lbest_b"] == n for r in rows))
 for n in (1, 2, 3, 4, 6, 8):
     a[f"member_in_top{n}"] = int(sum(r["member_rank"] < n for r in rows))
 for n in (4, 8, 16, 32, 64):

@@ -1,0 +1,21 @@
+#!/bin/bash
+# r05 final: full GPU suite, trace + PMC passes of the match bench
+# (pmc_summary.json for this library), the default bench line.  Usage: gpu_r05_final.sh <tag>
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+TAG=${1:-r05_vf}
+OUT=gpurun_out
+mkdir -p $OUT
+tools/gpu_step.sh "gputests|600|python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" || exit $?
+cp $OUT/gputests.log $OUT/${TAG}_gputests.log
+STEPS=200 bash tools/gpu_prof.sh $TAG || exit $?
+WORKLOAD=match python3 tools/pmc_summary.py $OUT/trace_$TAG $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG $OUT/pmc_l2_$TAG $OUT/$TAG > $OUT/${TAG}_summary.log 2>&1 || exit $?
+cp $OUT/${TAG}_pmc.json profiles/pmc_summary.json
+grep '^{' $OUT/trace_$TAG.log | tail -n 1 > $OUT/${TAG}_trace_run_bench.json
+ALGO=$(python3 -c "import json;print(json.loads(open('$OUT/${TAG}_trace_run_bench.json').read())['roofline']['algo_bytes_per_launch'])") || exit 1
+TR=$(find $OUT/trace_$TAG -name '*kernel_trace.csv' | head -1)
+python3 tools/trace_coarse.py $TR k_coarse_list $ALGO > $OUT/${TAG}_coarse_split.json || exit 1
+find $OUT/trace_$TAG -name '*kernel_stats.csv' -exec cp {} $OUT/${TAG}_run_kernel_stats.csv \;
+rm -rf $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG $OUT/pmc_l2_$TAG $OUT/trace_$TAG
+tools/gpu_step.sh "bench|600|python -u bench.py > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err" || exit $?
+python3 -c "import json;d=json.loads(open('$OUT/${TAG}_bench.json').read().strip().splitlines()[-1]);print(d['value'], d['roofline']['frac'], d['roofline']['traffic'], [(k, (d.get(k) or {}).get('value')) for k in ('config5_strong_scaling','config4_stream','config3_refine','f2_rebuild','config2_distinct_maps')])"
