@@ -544,6 +544,38 @@ __global__ __launch_bounds__(256) void k_decimate(const double* __restrict__ C, 
     D[plane * pstride + (long long)(qy + M) * Wqp + qx + M] = v;
 }
 
+// Supplied coarse maps of a batch in one launch (r05: one k_decimate and one
+// k_planes16 per map were 8 small launches per config-5 chunk): job
+// blockIdx.z / lr^2, plane blockIdx.z % lr^2; the interior of the padded
+// planes and, where the set has them, their fp16 round-up copies (the
+// margins of both are zero from planes_buffer).
+struct DecimJob {
+    const double* C;        // the supplied coarse map (W x H)
+    double* D;              // the set's padded phase planes
+    unsigned short* D16;    // their fp16 copies (null: no superblock bounds)
+    int* negflag;
+    int pgen;
+};
+__global__ __launch_bounds__(256) void k_decimate_jobs(const DecimJob* __restrict__ jobs, int W, int H, int lr,
+                                                       int Wq, int M, int Wqp, long long pstride)
+{
+    const int np = lr * lr;
+    const DecimJob& j = jobs[blockIdx.z / np];
+    const int plane = blockIdx.z % np;   // ry * lr + rx
+    const int qx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int qy = blockIdx.y;
+    if (qx >= Wq) return;
+    const int rx = plane % lr, ry = plane / lr;
+    const int x = lr * qx + rx, y = lr * qy + ry;
+    const double v = (x < W && y < H) ? j.C[(size_t)y * W + x] : 0.0;
+    const long long o = plane * pstride + (long long)(qy + M) * Wqp + qx + M;
+    j.D[o] = v;
+    if (j.D16) {
+        j.D16[o] = half_round_up_bits(v);
+        if (v < 0.0) *j.negflag = j.pgen;
+    }
+}
+
 // --------------------------------------------------------------------------
 // Sequential fp64 sum in beam order with the gathers software-pipelined:
 // batch k+1's loads are issued before batch k's values are added, so two
@@ -3455,14 +3487,28 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
 
 // --------------------------------------------------------------------------
 // k_post (LGS_OPT_POST_RECORDS): the batch's records straight into the pinned
-// (coherent) host copy, then the completion flag.  One wave: its system-scope
-// release orders its own record stores before the flag store.
+// (coherent) host copy, then the completion flag.  Every thread's loads are
+// issued before its stores (r05: one wave copying 16-byte words in a loop
+// waited a device round trip per word -- ~60 us for a 64-record chunk, 7% of
+// a config-5 batch); each thread's system-scope release orders its record
+// stores, the barrier puts all of them before the flag store.
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_post(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16,
-                                             unsigned* flag, unsigned gen)
+constexpr int kPostThreads = 256;
+__global__ __launch_bounds__(kPostThreads) void k_post(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16,
+                                                       unsigned* flag, unsigned gen)
 {
-    for (int i = threadIdx.x; i < n16; i += 64) dst[i] = src[i];
+    const int nt = blockDim.x;
+    for (int i0 = threadIdx.x; i0 < n16; i0 += 4 * nt) {
+        uint4 x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (i0 + j * nt < n16) x[j] = src[i0 + j * nt];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (i0 + j * nt < n16) dst[i0 + j * nt] = x[j];
+    }
     __threadfence_system();
+    __syncthreads();
     if (threadIdx.x == 0) *(volatile unsigned*)flag = gen;
 }
 
@@ -3769,7 +3815,7 @@ struct PlaneSet {
 // padded phase planes (query path) or a phase-plane copy of a supplied coarse
 // map, then the superblock planes of all sets in one launch.
 struct SetJobs {
-    size_t jobs_off = 0, njobs = 0, pj_off = 0, npj = 0;
+    size_t jobs_off = 0, njobs = 0, pj_off = 0, npj = 0, dj_off = 0, ndj = 0;
     bool hv = false;   // k_super_hv (else k_super_planes)
 };
 
@@ -3818,6 +3864,7 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
     // horizontal max into the precompute, sh mode.)
     std::vector<PrecompJob> jobs;
     std::vector<PlaneJob> pj;
+    std::vector<DecimJob> djobs;
     for (int s = 0; s < ns; ++s) {
         PlaneSet& ps = sets[s];
         ps.cmap = D + ssz * (size_t)s;
@@ -3853,7 +3900,10 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
             launch_precompute(ctx, ps.fine, lr, plain, nullptr);
             launch_decimate(plain, lp, D + ssz * (size_t)s, st);
         } else {
-            launch_decimate(ps.coarse->d, lp, D + ssz * (size_t)s, st);
+            DecimJob dj{ ps.coarse->d, D + ssz * (size_t)s, need_super ? ps.planes16 : nullptr,
+                         need_super ? neg + s : nullptr, ps.pgen };
+            djobs.push_back(dj);
+            ps.half_copy = false;   // k_decimate_jobs writes the copy
         }
         if (need_super) pj.push_back(j);
     }
@@ -3864,6 +3914,8 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
     sj.jobs_off = jobs.empty() ? 0 : up.append(jobs.data(), jobs.size());
     sj.npj = pj.size();
     sj.pj_off = pj.empty() ? 0 : up.append(pj.data(), pj.size());
+    sj.ndj = djobs.size();
+    sj.dj_off = djobs.empty() ? 0 : up.append(djobs.data(), djobs.size());
     sj.hv = hv_mode(ctx, lp);
     return sj;
 }
@@ -3880,6 +3932,13 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
         }
     if (sj.njobs)
         launch_precompute_jobs(ctx, up.at<PrecompJob>(sj.jobs_off), (int)sj.njobs, maxW, maxH, lp.low_res);
+    if (sj.ndj) {   // supplied coarse maps (all of the plan's size)
+        const int np = lp.low_res * lp.low_res;
+        hipLaunchKernelGGL(k_decimate_jobs, dim3((lp.Wq + 255) / 256, lp.Hq, np * (int)sj.ndj), dim3(256), 0,
+                           ctx->stream, up.at<DecimJob>(sj.dj_off), lp.W, lp.H, lp.low_res, lp.Wq, lp.M, lp.Wqp,
+                           lp.pstride);
+        LGS_HIP_CHECK(hipGetLastError());
+    }
     for (const auto& s : sets)
         if (s.half_copy) {   // planes the batched precompute did not write: their fp16 copy here
             const long long n = (long long)lp.low_res * lp.low_res * lp.pstride;
@@ -4595,7 +4654,9 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
         F.flag = h_flag;
         F.post_gen = (unsigned)ctx->next_stamp();
         *(volatile unsigned*)h_flag = 0u;   // before the launch: k_post's store comes after it
-        hipLaunchKernelGGL(k_post, dim3(1), dim3(64), 0, ctx->stream, (const uint4*)d_rec, (uint4*)h_rec,
+        const int n16 = (int)(rec_bytes / 16);   // one word per thread where it fits (a lone match: one wave)
+        hipLaunchKernelGGL(k_post, dim3(1), dim3(std::min(kPostThreads, (n16 + 63) / 64 * 64)), 0, ctx->stream,
+                           (const uint4*)d_rec, (uint4*)h_rec,
                            (int)(rec_bytes / 16), h_flag, F.post_gen);
         LGS_HIP_CHECK(hipGetLastError());
     } else {
