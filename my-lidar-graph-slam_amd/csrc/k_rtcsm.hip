@@ -2098,13 +2098,56 @@ __device__ __forceinline__ double seed_fine(const RtcsmPlan& pl, const double* _
 // (tools/diag_seed.py): a third of the queries then scored ~4.5x the coarse
 // blocks.  Sixteen candidates cost member sums, not fine scores.
 constexpr int kSeedMembersThreads = 256;
-constexpr int kSeedWideMaxParts = 1024;   // parts staged in LDS (larger searches: the narrow seed)
+constexpr int kSeedWideMaxParts = 1024;   // parts held in one wave's registers (larger searches: block rounds)
+// Candidate b of the seed, by one whole wave: the parts in registers (16 per
+// lane), b + 1 rounds of a wave argmax, each taking the best part out (the
+// seed's order: bound, then block order); a candidate needs a bound above
+// thr.  LLONG_MAX: no candidate b.  (r05: the block-wide argmax rounds, two
+// barriers each, were the seed's longest chain for its last workgroups.)
+__device__ __forceinline__ long long seed_pick_wave(const MatchItem& it, const RtcsmPlan& pl, int b)
+{
+    const int lane = (int)__lane_id();
+    const int nparts = it.nparts;
+    constexpr int R = kSeedWideMaxParts / 64;
+    double v[R];
+    long long k[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        v[r] = (i < nparts) ? it.part_c[i] : -INFINITY;
+        k[r] = (i < nparts) ? it.part_k[i] : LLONG_MAX;
+    }
+    long long pick = LLONG_MAX;
+    for (int round = 0; round <= b; ++round) {
+        double bv = -INFINITY;
+        long long bk = LLONG_MAX;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (better(v[r], k[r], bv, bk)) {
+                bv = v[r];
+                bk = k[r];
+            }
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ov = __shfl_xor(bv, off, 64);
+            const long long ok = __shfl_xor(bk, off, 64);
+            if (better(ov, ok, bv, bk)) {
+                bv = ov;
+                bk = ok;
+            }
+        }
+        if (bk == LLONG_MAX || bv == -INFINITY || !(bv > pl.thr)) break;   // uniform: no candidate b
+        if (round == b) pick = bk;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (k[r] == bk) v[r] = -INFINITY, k[r] = LLONG_MAX;
+    }
+    return pick;
+}
 __global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items items)
 {
     const MatchItem& it = items[blockIdx.y];
     const RtcsmPlan& pl = it.pl;
     const double* __restrict__ cmap = it.cmap;
-    const int nparts = it.nparts;
     if (blockIdx.x == 0 && threadIdx.x < 2 && it.keepc) it.keepc[threadIdx.x] = 0;   // before k_keep
     extern __shared__ char smem[];
     __shared__ double red[2][kSeedMembersThreads / 64][16];
@@ -2112,44 +2155,9 @@ __global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items item
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nsb2 = pl.nsbx * pl.nsby;
     const int Nv = pl.Nv;
-    // 1. candidate b by wave 0: the parts in registers (16 per lane), b + 1
-    // rounds of a wave argmax, each taking the best part out (the narrow
-    // seed's order: bound, then block order); a candidate needs a bound
-    // above thr
+    // 1. candidate b by wave 0 (seed_pick_wave)
     if (w == 0) {
-        constexpr int R = kSeedWideMaxParts / 64;
-        double v[R];
-        long long k[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int i = lane + 64 * r;
-            v[r] = (i < nparts) ? it.part_c[i] : -INFINITY;
-            k[r] = (i < nparts) ? it.part_k[i] : LLONG_MAX;
-        }
-        long long pick = LLONG_MAX;
-        for (int round = 0; round <= (int)blockIdx.x; ++round) {
-            double bv = -INFINITY;
-            long long bk = LLONG_MAX;
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (better(v[r], k[r], bv, bk)) {
-                    bv = v[r];
-                    bk = k[r];
-                }
-            for (int off = 32; off > 0; off >>= 1) {
-                const double ov = __shfl_xor(bv, off, 64);
-                const long long ok = __shfl_xor(bk, off, 64);
-                if (better(ov, ok, bv, bk)) {
-                    bv = ov;
-                    bk = ok;
-                }
-            }
-            if (bk == LLONG_MAX || bv == -INFINITY || !(bv > pl.thr)) break;   // uniform: no candidate b
-            if (round == (int)blockIdx.x) pick = bk;
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (k[r] == bk) v[r] = -INFINITY, k[r] = LLONG_MAX;
-        }
+        const long long pick = seed_pick_wave(it, pl, (int)blockIdx.x);
         if (lane == 0) s_cand = pick;
     }
     __syncthreads();
@@ -2299,39 +2307,52 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
         }
         return;
     }
-    double pv[kSeedRegParts];
-    long long pk[kSeedRegParts];
-#pragma unroll
-    for (int j = 0; j < kSeedRegParts; ++j) {
-        const int i = tid + j * 1024;
-        pv[j] = (i < nparts) ? part_c[i] : -INFINITY;
-        pk[j] = (i < nparts) ? part_k[i] : LLONG_MAX;
-    }
     int nc = 0;
-    for (; nc <= (int)blockIdx.x; ++nc) {   // candidates 0..blockIdx.x
-        double bv = -INFINITY;
-        long long bk = LLONG_MAX;
-#pragma unroll
-        for (int j = 0; j < kSeedRegParts; ++j)
-            if (better(pv[j], pk[j], bv, bk)) {
-                bv = pv[j];
-                bk = pk[j];
-            }
-        for (int i = tid + kSeedRegParts * 1024; i < nparts; i += 1024) {   // large searches only
-            bool taken = false;
-            for (int j = 0; j < nc; ++j) taken |= cand[j] == part_k[i];
-            if (!taken && better(part_c[i], part_k[i], bv, bk)) {
-                bv = part_c[i];
-                bk = part_k[i];
+    if (nparts <= kSeedWideMaxParts) {   // candidate b by one wave
+        __shared__ int s_nc;
+        if (tid < 64) {
+            const long long pick = seed_pick_wave(it, pl, (int)blockIdx.x);
+            if (tid == 0) {
+                cand[blockIdx.x] = pick;
+                s_nc = (pick != LLONG_MAX) ? (int)blockIdx.x + 1 : 0;
             }
         }
-        block_argmax(bv, bk, sv, sk);
-        if (bk == LLONG_MAX || bv == -INFINITY || !(bv > pl.thr)) break;   // uniform
-        if (tid == 0) cand[nc] = bk;
-#pragma unroll
-        for (int j = 0; j < kSeedRegParts; ++j)
-            if (pk[j] == bk) pv[j] = -INFINITY, pk[j] = LLONG_MAX;
         __syncthreads();
+        nc = s_nc;
+    } else {
+        double pv[kSeedRegParts];
+        long long pk[kSeedRegParts];
+#pragma unroll
+        for (int j = 0; j < kSeedRegParts; ++j) {
+            const int i = tid + j * 1024;
+            pv[j] = (i < nparts) ? part_c[i] : -INFINITY;
+            pk[j] = (i < nparts) ? part_k[i] : LLONG_MAX;
+        }
+        for (; nc <= (int)blockIdx.x; ++nc) {   // candidates 0..blockIdx.x
+            double bv = -INFINITY;
+            long long bk = LLONG_MAX;
+#pragma unroll
+            for (int j = 0; j < kSeedRegParts; ++j)
+                if (better(pv[j], pk[j], bv, bk)) {
+                    bv = pv[j];
+                    bk = pk[j];
+                }
+            for (int i = tid + kSeedRegParts * 1024; i < nparts; i += 1024) {   // large searches only
+                bool taken = false;
+                for (int j = 0; j < nc; ++j) taken |= cand[j] == part_k[i];
+                if (!taken && better(part_c[i], part_k[i], bv, bk)) {
+                    bv = part_c[i];
+                    bk = part_k[i];
+                }
+            }
+            block_argmax(bv, bk, sv, sk);
+            if (bk == LLONG_MAX || bv == -INFINITY || !(bv > pl.thr)) break;   // uniform
+            if (tid == 0) cand[nc] = bk;
+#pragma unroll
+            for (int j = 0; j < kSeedRegParts; ++j)
+                if (pk[j] == bk) pv[j] = -INFINITY, pk[j] = LLONG_MAX;
+            __syncthreads();
+        }
     }
     LGS_PROBE_MARK();
     if (nc > (int)blockIdx.x) {
