@@ -374,3 +374,33 @@ def test_wide_seed_same_records_less_coarse_work(ctx, world, small_map):
     for j in (0, 5, 11):
         out = ctx.optimize_pose_query_batch(g, P, cost, scans, inits)[j]
         assert_same(out, oracle_match(cells, mx, my, 0.05, params, qs[j][0], ang, inits[j]), f"q{j}")
+
+
+@pytest.mark.parametrize("wide,theta", [(5, 1.0), (16, 1.0), (12, 3.1)])
+def test_wide_seed_candidate_counts_and_large_searches(ctx, world, small_map, wide, theta):
+    """The wide seed with its fewest (5) and most (16) candidates, and a
+    search with more angle parts than one wave holds (+-3.1 rad: the batch
+    falls back to the one-launch seed): records equal the 4-candidate seed's
+    but for the device's work counters, which do not grow in total."""
+    cells, mx, my = small_map
+    rng = np.random.default_rng(51)
+    ang, qs = _queries(world, rng, 6, 541)
+    params = (5, 2.0, 2.0, theta, 20.0)
+    P, cost = abi.RtcsmParams(*params), launcher_cost()
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    scans = [ctx.scan(r, ang) for r, _ in qs]
+    inits = [i for _, i in qs]
+    try:
+        ctx.set_option(abi.LGS_OPT_SEED_WIDE, 0)
+        narrow = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, inits)]
+        ctx.set_option(abi.LGS_OPT_SEED_WIDE, wide)
+        got = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, inits)]
+    finally:
+        ctx.set_option(abi.LGS_OPT_SEED_WIDE, 12)
+    strip = lambda rec: rec[:6] + rec[8:]   # all but coarse_blocks / fine_blocks
+    assert [strip(r) for r in got] == [strip(r) for r in narrow], _diff(got, narrow)
+    assert sum(r[6] for r in got) <= sum(r[6] for r in narrow)
+    if theta > 3.0:   # the fallback: the very same seed, the very same work
+        assert got == narrow
+    out = ctx.optimize_pose_query_batch(g, P, cost, scans, inits)[2]
+    assert_same(out, oracle_match(cells, mx, my, 0.05, params, qs[2][0], ang, inits[2]), "q2")
