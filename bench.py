@@ -107,7 +107,7 @@ def parse():
     a = ap.parse_args()
     d_steps = dict(match=200, refine=200, loop=12, loop_bb=12, stream=10000 if a.driver == "cpp" else 500,
                    rebuild=20)[a.workload]
-    d_warm = dict(match=10, refine=5, loop=1, loop_bb=1, stream=10, rebuild=2)[a.workload]
+    d_warm = dict(match=10, refine=5, loop=1, loop_bb=2, stream=10, rebuild=2)[a.workload]
     a.steps = d_steps if a.steps is None else a.steps
     a.warmup = d_warm if a.warmup is None else a.warmup
     return a

@@ -537,9 +537,17 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         h_vidx.insert(h_vidx.end(), b.vidx.begin(), b.vidx.end());
         for (int h = 0; h <= Hm; ++h) it.maps[h] = pyr[j][h];
     }
-    if (!h_vidx.empty())
-        LGS_HIP_CHECK(hipMemcpyAsync(d_vidx_all, h_vidx.data(), sizeof(int) * h_vidx.size(), hipMemcpyHostToDevice,
+    // host <-> device copies of this path go through the context's pinned
+    // buffer (r05: copies to / from fresh pageable vectors stalled a call for
+    // 20-28 ms now and then -- the runtime pinning their new pages); each is
+    // consumed before the buffer is written again (the stream orders the
+    // device side, a sync precedes every host read)
+    if (!h_vidx.empty()) {
+        int* pv = (int*)ctx->ensure_pinned(sizeof(int) * h_vidx.size());
+        std::memcpy(pv, h_vidx.data(), sizeof(int) * h_vidx.size());
+        LGS_HIP_CHECK(hipMemcpyAsync(d_vidx_all, pv, sizeof(int) * h_vidx.size(), hipMemcpyHostToDevice,
                                      ctx->stream));
+    }
     // guards (shared by every level of the batch)
     // [0] guards, [1] children, [2] overflow; from byte 256 the per-match scored-node counters
     int* d_counts = (int*)ctx->ensure(S_BB3, 256 + sizeof(unsigned long long) * (size_t)n);
@@ -572,9 +580,10 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
                            up.at<int4>(poff), np, -1, d_pscores, d_guards, d_counts, gcap, ctx->guard_eps,
                            ctx->inject_index ? 1 : 0);
         LGS_HIP_CHECK(hipGetLastError());
-        LGS_HIP_CHECK(hipMemcpyAsync(pscores.data(), d_pscores, sizeof(double) * np, hipMemcpyDeviceToHost,
-                                     ctx->stream));
+        double* pp = (double*)ctx->ensure_pinned(sizeof(double) * (size_t)np);
+        LGS_HIP_CHECK(hipMemcpyAsync(pp, d_pscores, sizeof(double) * np, hipMemcpyDeviceToHost, ctx->stream));
         ctx->sync();
+        std::memcpy(pscores.data(), pp, sizeof(double) * (size_t)np);
     }
     // the path scores may carry unchecked guards: they only choose thr_exp,
     // and a wrong choice is caught below (a node missing from the table)
@@ -608,11 +617,14 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
             hipLaunchKernelGGL(k_bb_guard_nodes, dim3((ngc + 255) / 256), dim3(256), 0, ctx->stream,
                                ug.at<const int4*>(lo), d_guards + g0, ngc, d_gn);
             LGS_HIP_CHECK(hipGetLastError());
-            LGS_HIP_CHECK(hipMemcpyAsync(guards.data(), d_guards + g0, sizeof(BBGuard) * guards.size(),
-                                         hipMemcpyDeviceToHost, ctx->stream));
-            LGS_HIP_CHECK(hipMemcpyAsync(gnodes.data(), d_gn, sizeof(int4) * gnodes.size(), hipMemcpyDeviceToHost,
-                                         ctx->stream));
+            const size_t gb = sizeof(BBGuard) * guards.size(), nb = sizeof(int4) * gnodes.size();
+            const size_t gbo = (gb + 15) & ~(size_t)15;
+            char* pg = (char*)ctx->ensure_pinned(gbo + nb);
+            LGS_HIP_CHECK(hipMemcpyAsync(pg, d_guards + g0, gb, hipMemcpyDeviceToHost, ctx->stream));
+            LGS_HIP_CHECK(hipMemcpyAsync(pg + gbo, d_gn, nb, hipMemcpyDeviceToHost, ctx->stream));
             ctx->sync();
+            std::memcpy(guards.data(), pg, gb);
+            std::memcpy(gnodes.data(), pg + gbo, nb);
         }
         std::vector<std::pair<int, int>> dirty;   // (level id, node index)
         std::vector<int4> dnodes;
@@ -793,11 +805,14 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
                            ur.at<int>(to),
                            ur.at<double>(ho), n, d_res);
         LGS_HIP_CHECK(hipGetLastError());
-        LGS_HIP_CHECK(hipMemcpyAsync(res.data(), d_res, sizeof(BBResult) * (size_t)n, hipMemcpyDeviceToHost,
-                                     ctx->stream));
-        LGS_HIP_CHECK(hipMemcpyAsync(ncount.data(), d_ncount, sizeof(unsigned long long) * (size_t)n,
-                                     hipMemcpyDeviceToHost, ctx->stream));
+        const size_t rb = sizeof(BBResult) * (size_t)n, cb = sizeof(unsigned long long) * (size_t)n;
+        const size_t rbo = (rb + 15) & ~(size_t)15;
+        char* pr = (char*)ctx->ensure_pinned(rbo + cb);
+        LGS_HIP_CHECK(hipMemcpyAsync(pr, d_res, rb, hipMemcpyDeviceToHost, ctx->stream));
+        LGS_HIP_CHECK(hipMemcpyAsync(pr + rbo, d_ncount, cb, hipMemcpyDeviceToHost, ctx->stream));
         ctx->sync();
+        std::memcpy(res.data(), pr, rb);
+        std::memcpy(ncount.data(), pr + rbo, cb);
     }
     for (auto& L : levels) L.d_nodes = nullptr, L.d_scores = nullptr, L.d_child = nullptr;
     std::vector<lgs_pose2d> best((size_t)n);
