@@ -113,15 +113,12 @@ constexpr int kBBPipe = 16;
 // division: the product is within 1 ulp of the quotient (~1e-13 cells at
 // map sizes here), far inside guard_eps, so every cell whose floor could
 // differ from the reference's is guarded and re-checked on the host.
-__global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ items, const int4* __restrict__ nodes,
-                                                  int n, int level_id, double* __restrict__ scores,
-                                                  BBGuard* __restrict__ guards, int* __restrict__ nguard,
-                                                  int guard_cap, double guard_eps, int inject)
+// One node's score (one lane): the reference's beam-order sum over the
+// level's map, with the guard records of near-boundary cells.
+__device__ __forceinline__ void score_node(const BBItem& it, int4 nd, int i, int level_id, double* __restrict__ scores,
+                                           BBGuard* __restrict__ guards, int* __restrict__ nguard, int guard_cap,
+                                           double guard_eps, int inject)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int4 nd = nodes[i];
-    const BBItem& it = items[node_item(nd)];
     const int h = node_level(nd);
     // nodePose (:96-99)
     const double nx = it.sx + (double)nd.y * it.step_x;
@@ -176,6 +173,26 @@ __global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ ite
         for (int j = 0; j < kBBPipe; ++j) sum += val[j];
     }
     scores[i] = sum;
+}
+
+__global__ __launch_bounds__(256) void k_bb_score(const BBItem* __restrict__ items, const int4* __restrict__ nodes,
+                                                  int n, int level_id, double* __restrict__ scores,
+                                                  BBGuard* __restrict__ guards, int* __restrict__ nguard,
+                                                  int guard_cap, double guard_eps, int inject)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int4 nd = nodes[i];
+    // r05: a wave whose nodes all belong to one match (the common case: the
+    // top nodes are listed per match, children follow their parents) reads
+    // that match's fields and beam table through scalar loads -- the beam's
+    // rotation terms (rca, rsa) then cost no vector memory instruction, only
+    // the map gather does
+    const int j = node_item(nd);
+    const int j0 = __builtin_amdgcn_readfirstlane(j);
+    const bool uniform = __ballot(j != j0) == 0ull;
+    if (uniform) score_node(items[j0], nd, i, level_id, scores, guards, nguard, guard_cap, guard_eps, inject);
+    else score_node(items[j], nd, i, level_id, scores, guards, nguard, guard_cap, guard_eps, inject);
 }
 
 // child[i] = the index of node i's first child in the next level's list (its
