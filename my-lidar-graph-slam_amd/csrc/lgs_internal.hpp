@@ -283,7 +283,7 @@ struct lgs_ctx {
     // the device's highest priority, behind an event on `stream`: the
     // latency-bound tail of one context's chunk is not queued behind other
     // contexts' plane builds (LGS_OPT_PRIORITY_TAIL)
-    bool prio_tail = false;   // measured r05: no gain (52.4k vs 52.3k scans/s), lone p50 +11 us
+    bool prio_tail = false;   // measured r05: no gain (60.1k vs 59.6k scans/s), lone p50 +10 us, batch call +0.4 ms
     hipStream_t hi = nullptr;
     hipEvent_t split_ev[2] = {};
     bool post_records = true;    // records written to pinned memory by k_post + a flag (LGS_OPT_POST_RECORDS)
