@@ -184,6 +184,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_SPLIT_CHUNKS  30  /* A/B: 1 = a correlative call of 32..64 matches runs as two chunks of half the size (the two buffer banks overlap); 0 (default) = one chunk per 64 */
 #define LGS_OPT_DEVICE_HITS   31  /* 1 (default) = lgs_maps_construct_from_scans / lgs_map_construct_global form the hit points (glibc sincos restated), boxes, ray cells and key offsets on the device; 0 = on the host */
 #define LGS_OPT_SEED_WIDE     32  /* batches: the pruning bound seeded from the best members of this many candidate superblocks (5..16, default 12; the 4 best members fine-scored); 0..4 = 4 candidates in one launch */
+#define LGS_OPT_ZERO_TILES    33  /* 1 (default) = the per-map passes of a correlative batch skip the stores of a tile whose inputs are all +0 when that set's buffer already holds the tile's +0 outputs (per-tile words kept per bank, set and layout); 0 = every tile stored */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

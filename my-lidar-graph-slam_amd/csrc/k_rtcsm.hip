@@ -43,6 +43,7 @@ namespace lgs {
 void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, const PlaneGeom* planes);
 void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, int maxW, int maxH, int win);
 bool precompute_planes_ok(const lgs_grid* in, int win);
+void precompute_tile_grid(int maxW, int maxH, int win, int* gx, int* gy);
 }
 
 namespace {
@@ -132,6 +133,7 @@ struct PlaneJob {
     RtcsmPlan pl;            // layout fields (Wqp, Hqp, pstride, pstride4, sub4, Wq4)
     const unsigned short* planes16;   // the planes rounded up to fp16 (same layout)
     SuperT* super;
+    unsigned* zt;   // k_super_hv's zero-tile words of this set (null: none), see ZeroTiles
 };
 
 // The fp16 round-up copy of padded planes and the negative-cell stamp, for
@@ -944,9 +946,14 @@ __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ j
     const int tq = wg.x * 256 + threadIdx.x;        // (quad or unit, unit column), column fastest
     const int qi = tq / g.ncol, c = tq - qi * g.ncol;
     // NQ = 2: units qlo - 1 .. qlo + nqt - 1 (unit u holds quads u, u + 1)
-    if (qi >= g.nqt + NQ - 1) return;
-    const int X4 = g.X4lo + c, qt = g.qlo + qi - (NQ - 1);
-    if (qt < 0) return;
+    const int qt0 = g.qlo + qi - (NQ - 1);
+    const bool live = qi < g.nqt + NQ - 1 && qt0 >= 0;
+    // zero tiles (ZeroTiles): the workgroup's word says whether every unit
+    // half it stores holds +0 from its previous build; threads past the
+    // quads then load in-range rows and take part in the barrier only
+    unsigned* zw = job.zt ? job.zt + ((long long)p * gridDim.x + wg.x) : nullptr;   // uniform
+    if (!live && !zw) return;
+    const int X4 = g.X4lo + c, qt = min(max(qt0, 0), g.qlo + g.nqt - 1);
     const int rx = p % g.lr, ry = p / g.lr;
     typedef unsigned long long u64;
     typedef const __attribute__((address_space(1))) u64 gu64_t;
@@ -995,6 +1002,16 @@ __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ j
         vhi[k] = pkmax(pkmax((unsigned)(hm[k] >> 32), (unsigned)(hm[k + 1] >> 32)),
                        pkmax((unsigned)(hm[k + 2] >> 32), (unsigned)(hm[k + 3] >> 32)));
     }
+    if (zw) {
+        unsigned nzw = 0;
+#pragma unroll
+        for (int k = 0; k < 16 * NQ; ++k) nzw |= vlo[k] | vhi[k];
+        const unsigned zprev = *zw;                            // read by every thread before the
+        const int anynz = __syncthreads_or(live && nzw != 0);  // barrier, rewritten after it
+        if (!anynz && zprev == 1u) return;
+        if (threadIdx.x == 0 && zprev != (anynz ? 0u : 1u)) *zw = anynz ? 0u : 1u;
+    }
+    if (!live) return;
     u64* __restrict__ uo = (u64*)job.super + (long long)g.unit8 * p * g.pstrideO;
     const int u8 = g.unit8;
 #pragma unroll
@@ -3862,6 +3879,87 @@ SuperGeom super_geom(const RtcsmPlan& lp)
     return g;
 }
 
+// Zero tiles.  A map is mostly unknown space (+0 cells: the config-2 bench
+// map's room covers 23% of its 1000 x 1000 cells), and the per-map passes
+// write every plane, fp16 copy and superblock unit of it again for each
+// query.  k_precompute_planes (batched, 16-row tiles) and k_super_hv keep one
+// word per tile / workgroup and set: 1 = the outputs it stores were built
+// from all-(+0) inputs, so they hold +0; a tile whose inputs are still all +0
+// then stores nothing -- the same bits, without the writes.  The words are
+// kept valid here, per bank: a change of the plane layout, of a launch grid
+// or of a buffer clears them all (0 = build the tile), and a set whose planes
+// or units another path writes is marked stale, its words cleared before
+// their next use.  (Only writers that keep the words write the tiles they
+// cover; the zeroing of a whole buffer keeps them true.)
+void zero_tiles(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>& sets, std::vector<PrecompJob>& jobs,
+                const std::vector<int>& job_set, std::vector<PlaneJob>& pj, double* D, SuperT* S, bool need_super)
+{
+    const int b = ctx->bank, ns = (int)sets.size(), lr = lp.low_res;
+    std::vector<unsigned char>& pre_ok = ctx->zt_pre[b];
+    std::vector<unsigned char>& hv_ok = ctx->zt_hv[b];
+    if ((int)pre_ok.size() < ns) pre_ok.resize(ns, 0);
+    if ((int)hv_ok.size() < ns) hv_ok.resize(ns, 0);
+    const bool want = ctx->zero_tiles && need_super && lr <= 8 && hv_mode(ctx, lp);
+    const bool use_pre = want && jobs.size() > 1;   // one job: the lone precompute's 4-row tiles, no words
+    const bool use_hv = want;
+    // every set of this call is rewritten: stale unless a word-keeping pass covers it
+    std::vector<unsigned char> pre_now(ns, 0), hv_now(ns, 0);
+    int maxW = 0, maxH = 0;   // as launch_sets sizes the precompute's grid
+    for (auto& ps : sets)
+        if (ps.fine) {
+            maxW = std::max(maxW, ps.fine->w);
+            maxH = std::max(maxH, ps.fine->h);
+        }
+    int pgx = 0, pgy = 0;
+    if (use_pre) precompute_tile_grid(maxW, maxH, lr, &pgx, &pgy);
+    const SuperGeom g = super_geom(lp);
+    const int nq = ctx->hv_full && lp.unit8 == 2 ? 2 : 1;
+    const int hgx = (g.ncol * (g.nqt + nq - 1) + 255) / 256;
+    const long long pre_words = use_pre ? (long long)pgx * pgy : 0;
+    const long long hv_words = use_hv ? (long long)lr * lr * hgx : 0;
+    const long long per_set = pre_words + hv_words;
+    if (per_set > 0) {
+        unsigned* Z = (unsigned*)ctx->ensure(ctx->banked(S_ZTILE), sizeof(unsigned) * (size_t)(per_set * ns));
+        const long long key[12] = { (long long)(uintptr_t)D, (long long)(uintptr_t)S, (long long)(uintptr_t)Z,
+                                    lr, lp.Wq, lp.Hq, lp.M * 16 + lp.oct * 4 + lp.unit8, lp.pstride,
+                                    pgx, pgy, hgx, nq };
+        if (std::memcmp(key, ctx->zt_key[b], sizeof(key)) != 0) {
+            std::memcpy(ctx->zt_key[b], key, sizeof(key));
+            std::fill(pre_ok.begin(), pre_ok.end(), 0);
+            std::fill(hv_ok.begin(), hv_ok.end(), 0);
+        }
+        bool clear = false;
+        for (size_t k = 0; k < jobs.size() && use_pre; ++k) {
+            const int s = job_set[k];
+            // the word says "+0 outputs" for the tiles of this map size only
+            const bool ok = pre_ok[s] && ctx->zt_dims[b].size() > (size_t)s &&
+                            ctx->zt_dims[b][s] == ((long long)jobs[k].W << 32 | jobs[k].H);
+            clear |= !ok;
+            jobs[k].zt = Z + per_set * s;
+            pre_now[s] = 1;
+        }
+        for (int s = 0; s < ns && use_hv; ++s) {
+            clear |= !hv_ok[s];
+            pj[s].zt = Z + per_set * s + pre_words;
+            hv_now[s] = 1;
+        }
+        // (a cleared word only makes its tile build once more)
+        if (clear) LGS_HIP_CHECK(hipMemsetAsync(Z, 0, sizeof(unsigned) * (size_t)(per_set * ns), ctx->stream));
+        if (clear) {
+            std::fill(pre_ok.begin(), pre_ok.end(), 0);
+            std::fill(hv_ok.begin(), hv_ok.end(), 0);
+        }
+    }
+    if ((int)ctx->zt_dims[b].size() < ns) ctx->zt_dims[b].resize(ns, -1);
+    for (int s = 0; s < ns; ++s) {
+        pre_ok[s] = pre_now[s];
+        // units untouched when this call builds none (no superblock pass)
+        if (need_super) hv_ok[s] = hv_now[s];
+    }
+    for (size_t k = 0; k < jobs.size(); ++k)
+        ctx->zt_dims[b][job_set[k]] = ((long long)jobs[k].W << 32 | jobs[k].H);
+}
+
 void launch_decimate(const double* coarse, const RtcsmPlan& pl, double* D, hipStream_t st);
 SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& sets, bool need_super, Upload& up)
 {
@@ -3884,6 +3982,7 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
     // the serial strips of a workgroup; r05 keeps two passes and moves the
     // horizontal max into the precompute, sh mode.)
     std::vector<PrecompJob> jobs;
+    std::vector<int> job_set;
     std::vector<PlaneJob> pj;
     std::vector<DecimJob> djobs;
     for (int s = 0; s < ns; ++s) {
@@ -3914,6 +4013,7 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
                 ps.half_copy = false;
             }
             jobs.push_back(q);
+            job_set.push_back(s);
         } else if (ps.fine) {
             // rare (odd map sizes): one set at a time through the shared scratch
             const size_t cells = (size_t)lp.W * lp.H;
@@ -3928,6 +4028,7 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
         }
         if (need_super) pj.push_back(j);
     }
+    zero_tiles(ctx, lp, sets, jobs, job_set, pj, D, S, need_super);
     // the descriptors of this step go up with the batch's items (one copy):
     // the caller flushes before calling launch_sets
     SetJobs sj;

@@ -475,6 +475,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_HV_FULL: ctx->hv_full = value != 0.0; return LGS_OK;
     case LGS_OPT_SPLIT_CHUNKS: ctx->split_chunks = value != 0.0; return LGS_OK;
     case LGS_OPT_DEVICE_HITS: ctx->device_hits = value != 0.0; return LGS_OK;
+    case LGS_OPT_ZERO_TILES: ctx->zero_tiles = value != 0.0; return LGS_OK;
     case LGS_OPT_SEED_WIDE:
         if (!(value >= 0.0 && value <= 16.0)) return LGS_ERR_INVALID_ARG;
         ctx->seed_wide = (int)value;
@@ -792,8 +793,9 @@ __global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restri
 #endif
 // coarse columns per tile: the footprint (kPQX * LR + LR - 1 fine columns) fits
 // the 256 threads of the y pass, and kPQX is even (column pairs)
+constexpr int pqx_of(int LR) { return ((257 - LR) / LR) & ~1; }
 template <int LR>
-constexpr int pqx() { return ((257 - LR) / LR) & ~1; }
+constexpr int pqx() { return pqx_of(LR); }
 typedef double d2a16 __attribute__((ext_vector_type(2)));
 template <int LR, int kPTY = 16>
 __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __restrict__ jobs)
@@ -824,6 +826,7 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
     __shared__ double m1[kPTY][FW];
     const double* __restrict__ in = j.in;
     const int tid = threadIdx.x;
+    int nz = 0;   // a footprint value of this thread is not +0
     for (int c = tid; c < fw; c += 256) {   // one column per thread (FW <= 256)
         const int xx = sx0 + c;
         double v[FH];
@@ -832,6 +835,8 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
             const int yy = sy0 + k;
             v[k] = (xx < W && yy < H) ? gload(in + ((size_t)yy * W + xx)) : 0.0;   // reads past the end are 0
         }
+#pragma unroll
+        for (int k = 0; k < FH; ++k) nz |= __double_as_longlong(v[k]) != 0;
         // window maxima of every start row (static register indices), then row
         // oy takes the window starting at win_start(y0 + oy) - sy0 =
         // min(oy + d, st) (the tail repeats the last full window)
@@ -859,7 +864,19 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
             }
         }
     }
-    __syncthreads();
+    // zero tiles: an all-(+0) footprint gives +0 in every plane and fp16
+    // output of the tile; when the set's word says the tile already holds
+    // them (its previous build read an all-zero footprint too), nothing is
+    // stored -- an unknown map's empty patches cost their reads only
+    unsigned* zw = j.zt ? j.zt + (by * gx + bx) : nullptr;   // uniform per workgroup
+    if (zw) {
+        const unsigned zprev = *zw;              // every thread reads it before the barrier,
+        const int anynz = __syncthreads_or(nz);  // thread 0 rewrites it after
+        if (!anynz && zprev == 1u) return;
+        if (tid == 0 && zprev != (anynz ? 0u : 1u)) *zw = anynz ? 0u : 1u;
+    } else {
+        __syncthreads();
+    }
     const PlaneGeom& pg = j.pg;
     const int nq = (x1 - x0) / LR;        // coarse columns of this tile (W is a multiple of LR)
     const int np = (nq + 1) >> 1;         // column pairs
@@ -987,6 +1004,14 @@ void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, c
     }
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
+}
+// the tile grid of a batched plane precompute (win <= 8, more than one job:
+// 16-row tiles): k_rtcsm.hip's zero-tile words are indexed by it
+void precompute_tile_grid(int maxW, int maxH, int win, int* gx, int* gy)
+{
+    const int q = pqx_of(win) * win;
+    *gx = (maxW + q - 1) / q;
+    *gy = (maxH + 15) / 16;
 }
 void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, int maxW, int maxH, int win)
 {

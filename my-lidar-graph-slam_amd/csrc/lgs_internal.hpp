@@ -84,10 +84,11 @@ enum Slot {
     S_PRECOMP_TMP,  // double [W*H]: pass-1 result of the large-window precompute
     S_KEEP,         // int: kept-superblock work list of a batch (k_keep / k_coarse_list)
     S_COLL,         // lgs_loop_records_allgather: send block + gathered rows (lgs_coll.hip)
+    S_ZTILE,        // unsigned: zero-tile words of the per-map passes (k_rtcsm.hip ZeroTiles), per set
     // bank 1 of the per-batch buffers: a batched call keeps two 64-query
     // chunks in flight (the next chunk's launches go out before the host
     // finishes the previous one), each in its own bank (lgs_ctx::banked)
-    S_BATCH_WS_B, S_RECORDS_B, S_UPLOAD_B, S_DECIM_B, S_SUPER_B, S_NEGFLAG_B, S_TEDGE_B,
+    S_BATCH_WS_B, S_RECORDS_B, S_UPLOAD_B, S_DECIM_B, S_SUPER_B, S_NEGFLAG_B, S_TEDGE_B, S_ZTILE_B,
     S_NUM_SLOTS
 };
 
@@ -178,6 +179,12 @@ struct PrecompJob {
     unsigned short* out16;
     int* negflag;
     int pgen;
+    // zero-tile words of this set (k_precompute_planes<L, 16> only; null: none):
+    // word (by * gridDim.x + bx) is 1 when the tile's last build read an all-zero
+    // footprint, i.e. its plane and fp16 outputs hold +0 -- a tile whose
+    // footprint is still all zero then leaves them as they are (k_rtcsm.hip
+    // ZeroTiles keeps the words valid per bank, set and layout)
+    unsigned* zt;
 };
 
 // fp16 (bit pattern) of m rounded toward +inf; zeros as +0 (so nonnegative
@@ -275,7 +282,8 @@ struct lgs_ctx {
     int prune_min_super = 1;     // LGS_OPT_PRUNE_MIN_SUPER
     bool small_window = true;    // one-launch search of one-block windows (LGS_OPT_SMALL_WINDOW)
     bool fused_planes = true;    // superblock units by k_super_hv (LGS_OPT_FUSED_PLANES)
-    int seed_wide = 12;          // batches: candidate superblocks whose best members seed the bound (LGS_OPT_SEED_WIDE; <= 4: one launch)
+    int seed_wide = 12;
+    bool zero_tiles = true;   // LGS_OPT_ZERO_TILES          // batches: candidate superblocks whose best members seed the bound (LGS_OPT_SEED_WIDE; <= 4: one launch)
     bool device_hits = true;     // map rebuilds of many scans: hit points / ray cells on the device (LGS_OPT_DEVICE_HITS)
     bool split_chunks = false;   // calls of 32..64 matches as two chunks (LGS_OPT_SPLIT_CHUNKS; measured r05, 8-rank loop block: 1.007 vs 0.869 ms as one)
     bool hv_full = false;        // k_super_hv stores 16-byte units whole (LGS_OPT_HV_FULL, A/B; measured r05: 0.24 vs 0.17 ms per 64 sets)
@@ -341,6 +349,7 @@ struct lgs_ctx {
         case lgs::S_SUPER: return lgs::S_SUPER_B;
         case lgs::S_NEGFLAG: return lgs::S_NEGFLAG_B;
         case lgs::S_TEDGE: return lgs::S_TEDGE_B;
+        case lgs::S_ZTILE: return lgs::S_ZTILE_B;
         default: return slot;
         }
     }
@@ -359,6 +368,11 @@ struct lgs_ctx {
     void* super_ptr[2] = {};   // superblock planes zeroed with them
     int super_sets[2] = {};
     long long planes_key[2][4] = { { -1, -1, -1, -1 }, { -1, -1, -1, -1 } };
+    // zero-tile words of the per-map passes (k_rtcsm.hip ZeroTiles), per bank:
+    // the layout they were kept for and which sets' words are current
+    long long zt_key[2][12] = {};
+    std::vector<unsigned char> zt_pre[2], zt_hv[2];
+    std::vector<long long> zt_dims[2];   // per set: W << 32 | H of the map its precompute words describe
     double* zero = nullptr;      // 32 zero doubles: target of out-of-map gathers
     // profiling (LGS_OPT_PROFILE)
     bool profile = false;

@@ -404,3 +404,58 @@ def test_wide_seed_candidate_counts_and_large_searches(ctx, world, small_map, wi
         assert got == narrow
     out = ctx.optimize_pose_query_batch(g, P, cost, scans, inits)[2]
     assert_same(out, oracle_match(cells, mx, my, 0.05, params, qs[2][0], ang, inits[2]), "q2")
+
+
+def test_zero_tiles_follow_map_changes(ctx, world):
+    """LGS_OPT_ZERO_TILES: the per-map passes skip the stores of tiles whose
+    inputs are all +0 when the set's buffer already holds their +0 outputs.
+    One context with it (the default) and one without run the same calls --
+    batches whose sets switch between maps with erased regions, a blob and a
+    single nonzero cell in otherwise empty tiles, a lone query (its own
+    precompute tiling) and batches with fewer and more sets -- and must leave
+    the same records and bit-identical phase planes and superblock units."""
+    base, mx, my = build_map(world, 600, 0.05, 100, scene.arc_poses(5), n_beams=541)
+    a = base.copy()
+    a[:, :250] = 0.0                         # erased: whole zero tiles
+    b = base.copy()
+    b[:200, :] = 0.0
+    b[500:560, 20:80] = 0.7                  # a blob where a and base are empty
+    c = base.copy()
+    c[5, 5] = 0.3                            # one cell in an otherwise empty tile
+    c[590, 300] = 0.2
+    d = np.zeros_like(base)                  # nothing at all
+    d[300:310, 300:310] = 0.9
+    maps = {"a": a, "b": b, "c": c, "d": d, "base": base}
+    other = abi.Context(0)
+    try:
+        other.set_option(abi.LGS_OPT_ZERO_TILES, 0)
+        P, cost = abi.RtcsmParams(5, 1.0, 1.0, 0.6, 20.0), launcher_cost()
+        rng = np.random.default_rng(31)
+        ang, qs = _queries(world, rng, 6, 541)
+        state = []
+        for cx in (ctx, other):
+            grids = {k: cx.grid_from_array(v, mx, my, 0.05) for k, v in maps.items()}
+            scans = [cx.scan(r, ang) for r, _ in qs]
+            state.append((cx, grids, scans))
+        inits = [i for _, i in qs]
+        calls = [["a", "a", "b", "c"], ["b", "c", "a", "a"], ["c"], ["c", "b", "a", "b"], ["d", "d"],
+                 ["a", "c", "b"], ["base", "b", "c", "a", "d", "b"], ["a", "a", "b", "c"]]
+        for step, names in enumerate(calls):
+            res = []
+            for cx, grids, scans in state:
+                n = len(names)
+                if n == 1:
+                    out = [cx.optimize_pose_query(grids[names[0]], P, cost, scans[0], inits[0])]
+                else:
+                    out = cx.optimize_pose_query_batch([grids[k] for k in names], P, cost, scans[:n], inits[:n])
+                recs = [_record(o) for o in out]
+                bufs = [(cx.debug_buffer("planes", j), cx.debug_buffer("super", j)) for j in range(n)]
+                res.append((recs, bufs))
+            (r0, b0), (r1, b1) = res
+            assert r0 == r1, (step, _diff(r0, r1))
+            for j in range(len(names)):
+                for name, u, v in (("planes", b0[j][0], b1[j][0]), ("super", b0[j][1], b1[j][1])):
+                    assert u.shape == v.shape and np.array_equal(u.view(np.uint8), v.view(np.uint8)), \
+                        (step, j, names[j], name, int(np.argmax(u.view(np.uint8) != v.view(np.uint8))))
+    finally:
+        other.close()
