@@ -43,7 +43,7 @@ namespace lgs {
 void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, const PlaneGeom* planes);
 void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, int maxW, int maxH, int win);
 bool precompute_planes_ok(const lgs_grid* in, int win);
-void precompute_tile_grid(int maxW, int maxH, int win, int* gx, int* gy);
+void precompute_tile_grid(int maxW, int maxH, int win, int njobs, int* gx, int* gy, int* rows);
 }
 
 namespace {
@@ -927,6 +927,8 @@ struct SuperGeom {
     long long pstride, subO, pstrideO;
     int X4lo, ncol, qlo, nqt, lr;     // unit columns [X4lo, X4lo + ncol), quads [qlo, qlo + nqt)
 };
+// k_super_hv's grid (x): workgroups per plane
+inline int hv_grid_x(const SuperGeom& g, int nq) { return (g.ncol * (g.nqt + nq - 1) + 255) / 256; }
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pkmax(unsigned a, unsigned b)
 {
@@ -943,17 +945,21 @@ __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ j
     const Blk wg = xcd_block();
     const PlaneJob& job = jobs[wg.z / nplanes];
     const int p = wg.z % nplanes;
-    const int tq = wg.x * 256 + threadIdx.x;        // (quad or unit, unit column), column fastest
+    // (quad or unit, unit column), column fastest.  (Measured and rejected,
+    // r05: workgroups as tiles of 256 / n quads x n unit columns, n = 8-32,
+    // so that zero tiles would also cover empty columns: 0.145-0.165 vs
+    // 0.106 ms per 64 config-2 sets.)
+    const int tq = wg.x * 256 + threadIdx.x;
     const int qi = tq / g.ncol, c = tq - qi * g.ncol;
     // NQ = 2: units qlo - 1 .. qlo + nqt - 1 (unit u holds quads u, u + 1)
     const int qt0 = g.qlo + qi - (NQ - 1);
-    const bool live = qi < g.nqt + NQ - 1 && qt0 >= 0;
+    const bool live = qi < g.nqt + NQ - 1 && qt0 >= 0 && c < g.ncol;
     // zero tiles (ZeroTiles): the workgroup's word says whether every unit
     // half it stores holds +0 from its previous build; threads past the
     // quads then load in-range rows and take part in the barrier only
     unsigned* zw = job.zt ? job.zt + ((long long)p * gridDim.x + wg.x) : nullptr;   // uniform
     if (!live && !zw) return;
-    const int X4 = g.X4lo + c, qt = min(max(qt0, 0), g.qlo + g.nqt - 1);
+    const int X4 = g.X4lo + min(c, g.ncol - 1), qt = min(max(qt0, 0), g.qlo + g.nqt - 1);
     const int rx = p % g.lr, ry = p / g.lr;
     typedef unsigned long long u64;
     typedef const __attribute__((address_space(1))) u64 gu64_t;
@@ -3882,7 +3888,8 @@ SuperGeom super_geom(const RtcsmPlan& lp)
 // Zero tiles.  A map is mostly unknown space (+0 cells: the config-2 bench
 // map's room covers 23% of its 1000 x 1000 cells), and the per-map passes
 // write every plane, fp16 copy and superblock unit of it again for each
-// query.  k_precompute_planes (batched, 16-row tiles) and k_super_hv keep one
+// query.  k_precompute_planes (the launch's tiling: 16-row tiles, a lone
+// map's shorter ones) and k_super_hv keep one
 // word per tile / workgroup and set: 1 = the outputs it stores were built
 // from all-(+0) inputs, so they hold +0; a tile whose inputs are still all +0
 // then stores nothing -- the same bits, without the writes.  The words are
@@ -3900,7 +3907,7 @@ void zero_tiles(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>& 
     if ((int)pre_ok.size() < ns) pre_ok.resize(ns, 0);
     if ((int)hv_ok.size() < ns) hv_ok.resize(ns, 0);
     const bool want = ctx->zero_tiles && need_super && lr <= 8 && hv_mode(ctx, lp);
-    const bool use_pre = want && jobs.size() > 1;   // one job: the lone precompute's 4-row tiles, no words
+    const bool use_pre = want && !jobs.empty();
     const bool use_hv = want;
     // every set of this call is rewritten: stale unless a word-keeping pass covers it
     std::vector<unsigned char> pre_now(ns, 0), hv_now(ns, 0);
@@ -3910,11 +3917,11 @@ void zero_tiles(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>& 
             maxW = std::max(maxW, ps.fine->w);
             maxH = std::max(maxH, ps.fine->h);
         }
-    int pgx = 0, pgy = 0;
-    if (use_pre) precompute_tile_grid(maxW, maxH, lr, &pgx, &pgy);
+    int pgx = 0, pgy = 0, prows = 0;   // the launch's tiling (a lone map: its own, shorter tiles)
+    if (use_pre) precompute_tile_grid(maxW, maxH, lr, (int)jobs.size(), &pgx, &pgy, &prows);
     const SuperGeom g = super_geom(lp);
     const int nq = ctx->hv_full && lp.unit8 == 2 ? 2 : 1;
-    const int hgx = (g.ncol * (g.nqt + nq - 1) + 255) / 256;
+    const int hgx = hv_grid_x(g, nq);
     const long long pre_words = use_pre ? (long long)pgx * pgy : 0;
     const long long hv_words = use_hv ? (long long)lr * lr * hgx : 0;
     const long long per_set = pre_words + hv_words;
@@ -3922,7 +3929,7 @@ void zero_tiles(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>& 
         unsigned* Z = (unsigned*)ctx->ensure(ctx->banked(S_ZTILE), sizeof(unsigned) * (size_t)(per_set * ns));
         const long long key[12] = { (long long)(uintptr_t)D, (long long)(uintptr_t)S, (long long)(uintptr_t)Z,
                                     lr, lp.Wq, lp.Hq, lp.M * 16 + lp.oct * 4 + lp.unit8, lp.pstride,
-                                    pgx, pgy, hgx, nq };
+                                    pgx, (long long)pgy << 8 | prows, hgx, nq };
         if (std::memcmp(key, ctx->zt_key[b], sizeof(key)) != 0) {
             std::memcpy(ctx->zt_key[b], key, sizeof(key));
             std::fill(pre_ok.begin(), pre_ok.end(), 0);
@@ -4072,7 +4079,7 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
         const int np = lp.low_res * lp.low_res;
         const SuperGeom g = super_geom(lp);
         const int nq = ctx->hv_full && lp.unit8 == 2 ? 2 : 1;   // threads per column: nqt quads or nqt + 1 units
-        dim3 grid((g.ncol * (g.nqt + nq - 1) + 255) / 256, 1, np * (int)sj.npj);
+        dim3 grid(hv_grid_x(g, nq), 1, np * (int)sj.npj);
         // algorithmic bytes: the copies read once (2 B per padded cell of the
         // quads' rows and the units' columns) + the unit halves written (8 B x
         // 16 sub-phases x unit8 copies per quad and column)

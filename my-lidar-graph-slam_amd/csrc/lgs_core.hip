@@ -1005,13 +1005,15 @@ void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, c
     ctx->timing_end(tok);
     LGS_HIP_CHECK(hipGetLastError());
 }
-// the tile grid of a batched plane precompute (win <= 8, more than one job:
-// 16-row tiles): k_rtcsm.hip's zero-tile words are indexed by it
-void precompute_tile_grid(int maxW, int maxH, int win, int* gx, int* gy)
+// the tile grid of a plane precompute launch (win <= 8; one job: the lone
+// LGS_PTY_LONE-row tiles, else 16-row tiles): k_rtcsm.hip's zero-tile words
+// are indexed by it
+void precompute_tile_grid(int maxW, int maxH, int win, int njobs, int* gx, int* gy, int* rows)
 {
     const int q = pqx_of(win) * win;
+    *rows = njobs == 1 ? LGS_PTY_LONE : 16;
     *gx = (maxW + q - 1) / q;
-    *gy = (maxH + 15) / 16;
+    *gy = (maxH + *rows - 1) / *rows;
 }
 void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, int maxW, int maxH, int win)
 {
