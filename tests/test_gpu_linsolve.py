@@ -234,3 +234,30 @@ def test_linsolve_config3(ctx, world, big_map):
                 true[2] + rng.uniform(-0.03, 0.03))
         d, o = check_solve(ctx, g, og, CONFIG3, r, ang, init)
         assert d.iterations == 50
+
+
+def test_linsolve_batch_fills_device(ctx, world, small_map):
+    """A device-filling batch (more refines than CUs: 300 workgroups on 256
+    CUs, as bench.py's batched_refines_per_s_per_gpu_256 and more) gives
+    every refine the bits of the lone refine."""
+    cells, mx, my = small_map
+    g = ctx.grid_from_array(cells, mx, my, 0.05)
+    ang = scene.beam_angles(361)
+    rng = np.random.default_rng(17)
+    base = []
+    for _ in range(12):
+        true = (rng.uniform(-1, 1), rng.uniform(-1, 1), rng.uniform(-3, 3))
+        base.append((ctx.scan(scene.ray_cast(world, true, ang), ang), true))
+    scans, inits = [], []
+    for k in range(300):
+        s, true = base[k % len(base)]
+        scans.append(s)
+        inits.append((true[0] + 0.001 * (k % 7), true[1] - 0.002 * (k % 5), true[2] + 0.001 * (k % 3)))
+    lp = abi.LinsolveParams(*CONFIG3)
+    batch = ctx.linsolve_batch(g, lp, scans, inits)
+    for k in list(range(0, 300, 23)) + [299]:
+        one = ctx.linsolve(g, lp, scans[k], inits[k])
+        b = batch[k]
+        assert (one.estimated_pose.x, one.estimated_pose.y, one.estimated_pose.theta) == \
+            (b.estimated_pose.x, b.estimated_pose.y, b.estimated_pose.theta), k
+        assert one.normalized_cost == b.normalized_cost and one.iterations == b.iterations, k
