@@ -785,9 +785,13 @@ __global__ __launch_bounds__(256) void k_precompute_tiled(const double* __restri
 //     16-byte store (padded plane rows are even, so the pair is aligned); the
 //     lanes of a wave walk a plane row, so a wave writes 512-byte runs.
 // Same values as the reference's passes (max is exact).
-// tile rows: 16 for a batch's maps; a lone map (one job) takes 8-row tiles,
-// twice the workgroups for its ~250 tiles (latency, not bandwidth, bounds a
-// single 1000 x 1000 map)
+// tile rows: 8 for a batch's maps (r05: with zero tiles most workgroups only
+// read their footprint, and the shorter tiles' smaller LDS rows let more of
+// them run per CU); a lone map (one job) takes 4-row tiles, more workgroups
+// for its ~250 tiles (latency, not bandwidth, bounds a single 1000 x 1000 map)
+#ifndef LGS_PTY_BATCH
+#define LGS_PTY_BATCH 8   // measured (64 config-2 maps, zero tiles on): 32: 0.374 ms, 16: 0.189, 8: 0.150, 4: 0.173
+#endif
 #ifndef LGS_PTY_LONE
 #define LGS_PTY_LONE 4   // measured (lone config-2 map): 16: 16.4 us, 8: 13.3, 4: 11.5
 #endif
@@ -1011,7 +1015,7 @@ void launch_precompute(lgs_ctx* ctx, const lgs_grid* in, int win, double* out, c
 void precompute_tile_grid(int maxW, int maxH, int win, int njobs, int* gx, int* gy, int* rows)
 {
     const int q = pqx_of(win) * win;
-    *rows = njobs == 1 ? LGS_PTY_LONE : 16;
+    *rows = njobs == 1 ? LGS_PTY_LONE : LGS_PTY_BATCH;
     *gx = (maxW + q - 1) / q;
     *gy = (maxH + *rows - 1) / *rows;
 }
@@ -1030,8 +1034,8 @@ void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, i
                     dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + LGS_PTY_LONE - 1) / LGS_PTY_LONE, njobs), \
                     dim3(256), 0, ctx->stream, d_jobs); \
             else \
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_precompute_planes<L, 16>), \
-                    dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + 15) / 16, njobs), dim3(256), 0, ctx->stream, \
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_precompute_planes<L, LGS_PTY_BATCH>), \
+                    dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + LGS_PTY_BATCH - 1) / LGS_PTY_BATCH, njobs), dim3(256), 0, ctx->stream, \
                     d_jobs); \
             break;
         LGS_PP_CASE(1) LGS_PP_CASE(2) LGS_PP_CASE(3) LGS_PP_CASE(4) LGS_PP_CASE(5) LGS_PP_CASE(6)
