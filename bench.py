@@ -102,8 +102,14 @@ def parse():
                     help="match workload: also report configs 4 (config4_stream), 3 (config3_refine) and f2 "
                          "(f2_rebuild) after the timed region, each with its own CPU baseline and kernel times")
     ap.add_argument("--timed-events", default="dominant", choices=["dominant", "all", "none"],
-                    help="HIP-event timing inside the timed region: the roofline kernel only (default), "
-                         "every kernel, or none (A/B of the event overhead)")
+                    help="kernel timing inside the timed region: the roofline kernel only (default; with "
+                         "--device-timing 1 on the match workload: every kernel of the chunks, which costs two "
+                         "atomics per workgroup), every kernel, or none (A/B of the timing overhead)")
+    ap.add_argument("--device-timing", type=int, default=1,
+                    help="1 (default) = time the correlative chunks' kernels on the device (LGS_OPT_DEVICE_TIMING: "
+                         "first workgroup start to last workgroup end, s_memrealtime -- the span rocprofv3's kernel "
+                         "trace reports); 0 = HIP events on the stream (their begin fires when the stream reaches "
+                         "the launch, before the kernel gets its CUs)")
     a = ap.parse_args()
     d_steps = dict(match=200, refine=200, loop=12, loop_bb=12, stream=10000 if a.driver == "cpp" else 500,
                    rebuild=20)[a.workload]
@@ -253,18 +259,48 @@ def coarse_stage(stats):
                 frac=round(per / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
 
 
-def set_timed_events(ctx, args, dominant, extra=()):
-    """HIP-event timing during the timed region (LGS_OPT_PROFILE_MASK); the
+def set_timed_events(ctx, args, dominant, extra=(), chunk_kernels=False):
+    """Kernel timing during the timed region (LGS_OPT_PROFILE_MASK); the
     coarse kernel's work-list passes (k_coarse_aux) are timed with it, and
-    the `extra` kernels (config 5: k_super, which outweighs k_coarse there)."""
+    the `extra` kernels (config 5: k_super, which outweighs k_coarse there).
+    With --device-timing the correlative chunks' launches are timed on the
+    device (LGS_OPT_DEVICE_TIMING); chunk_kernels: then every kernel of the
+    chunks is timed (no events, two atomics per workgroup), so that the line
+    can name the largest kernel by its share of the timed region."""
     dom = 1 << abi.KERNEL_IDS.index(dominant)
     if dominant == "k_coarse":
         dom |= 1 << abi.KERNEL_IDS.index("k_coarse_aux")
     for k in extra:
         dom |= 1 << abi.KERNEL_IDS.index(k)
-    mask = {"dominant": dom, "all": (1 << len(abi.KERNEL_IDS)) - 1, "none": 0}[args.timed_events]
+    every = (1 << len(abi.KERNEL_IDS)) - 1
+    if args.device_timing and chunk_kernels:
+        dom = every
+    mask = {"dominant": dom, "all": every, "none": 0}[args.timed_events]
+    ctx.set_option(abi.LGS_OPT_DEVICE_TIMING, 1 if args.device_timing else 0)
     ctx.set_option(abi.LGS_OPT_PROFILE_MASK, mask)
     ctx.reset_stats()
+
+
+# the launched kernel(s) behind each timing id of a config-2 chunk (rocprofv3 names)
+TRACE_NAMES = dict(k_project="k_project<16>", k_super="k_super_oct<5, 2>", k_seed="k_seed_members + k_seed_super<2>",
+                   k_coarse_aux="k_keep + k_unsafe_list", k_coarse="k_coarse_list_c", k_select="k_select<256>",
+                   k_fine="k_fine_regs", k_replay="k_replay", k_cost="k_cost<1>",
+                   k_precompute="k_precompute_planes<5, 8>", k_super_planes="k_super_hv<1>")
+
+
+def timed_region_kernels(stats):
+    """Per-kernel device times of the timed region (every kernel of the
+    chunks, device-timed): launches, average ms, share of the summed kernel
+    time; and the largest kernel by that share."""
+    tot = sum(v["total_ms"] for v in stats.values() if v["launches"])
+    if tot <= 0:
+        return None, None
+    rows = {k: dict(trace_name=TRACE_NAMES.get(k, k), launches=v["launches"],
+                    avg_ms=round(v["total_ms"] / v["launches"], 5), share=round(v["total_ms"] / tot, 4))
+            for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["total_ms"]) if v["launches"]}
+    top = max(rows, key=lambda k: rows[k]["share"])
+    return rows, dict(kernel=top, trace_name=rows[top]["trace_name"], share=rows[top]["share"],
+                      avg_ms=rows[top]["avg_ms"])
 
 
 def bench_map(world, ang):
@@ -474,7 +510,7 @@ def run_match(args, D, ctx):
     for c, g, ds in state:
         for k in range(args.warmup):
             call(c, g, ds, k)
-        set_timed_events(c, args, "k_coarse")
+        set_timed_events(c, args, "k_coarse", chunk_kernels=True)
         if args.skip_kernels:   # after the warmup: skipped stages then read valid stale scratch
             c.set_option(abi.LGS_OPT_SKIP_MASK,
                          sum(1 << abi.KERNEL_IDS.index(k) for k in args.skip_kernels.split(",")))
@@ -520,6 +556,7 @@ def run_match(args, D, ctx):
         c0.optimize_pose_query(g0[0] if isinstance(g0, list) else g0, P, cost, ds0[j], inits[j])
         lat1.append(time.perf_counter() - ts)
     c0.set_option(abi.LGS_OPT_PROFILE, 1)
+    c0.set_option(abi.LGS_OPT_DEVICE_TIMING, 1 if args.device_timing else 0)
     # one stream: a chunk's tail on the priority stream would overlap the next
     # chunk's plane builds, and the table is of kernels alone
     prio = 1 if "28=1" in os.environ.get("LGS_CTX_OPTIONS", "") else 0   # the timed region's setting
@@ -557,6 +594,7 @@ def run_match(args, D, ctx):
                    single_core_scans_per_s=round(1.0 / float(np.median(times)), 4),
                    speedup_vs_single_core=round(value * float(np.median(times)), 1))
     lat_ms = np.array([x for l in lat for x in l]) * 1e3
+    trk, top = timed_region_kernels(stats) if args.device_timing else (None, None)
     line = dict(
         metric=METRIC, value=round(value, 2), unit="scans/s", n_gpus=D.world, steps=args.steps,
         warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 4), higher_is_better=True,
@@ -575,14 +613,22 @@ def run_match(args, D, ctx):
         p90_scan_match_ms=round(1e3 * float(np.percentile(lat1, 90)), 4) if lat1 else None,
         # latency of one batched call under the timed load
         p50_batch_call_ms=round(float(np.percentile(lat_ms, 50)), 4),
-        # the dominant kernel's HIP-event times over the timed region (the
+        # the correlative-score kernel's times over the timed region (the
         # rubric's basis: each launch shares the GPU with the other streams'
-        # kernels, so its duration includes their overlap); roofline_isolated
-        # is the same kernel timed alone, the one-stream pass after the timed
-        # region.  tools/trace_coarse.py splits a kernel trace
-        # of this command the same way (dispatches overlapping no other vs
-        # the rest).
+        # kernels, so its duration includes their overlap), device-timed by
+        # default: first workgroup start to last workgroup end, what the
+        # rocprofv3 kernel trace of the same command averages;
+        # roofline_isolated is the same kernel timed alone, the one-stream
+        # pass after the timed region.  tools/trace_coarse.py splits a kernel
+        # trace of this command (dispatches overlapping no other vs the rest).
         roofline=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"), cpu_baseline=cpu,
+        # the superblock-bound pass (2 B per angle x superblock x beam of the
+        # fp16 superblock planes), timed the same way
+        roofline_super=roofline_from(stats, "k_super", args.pmc, "k_super_oct<5, 2>", "l2-gather",
+                                     bytes_scale=0.25),
+        timing=("device: s_memrealtime span of each launch (LGS_OPT_DEVICE_TIMING)" if args.device_timing
+                else "HIP events on each launch's stream"),
+        timed_region_kernels=trk, largest_kernel=top,
         roofline_isolated=roofline_from(all_stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"),
         coarse_stage=coarse_stage(all_stats),
         pose_err_max_m=round(float(max(err)), 4), timed_events=args.timed_events,
@@ -1189,14 +1235,16 @@ def main():
     if args.workload == "match" and args.sub_lines:
         # configs 4 and 3 and f2 next to the headline, on the same run
         # (replicas over the ranks; CPU baselines on rank 0 at N = 1)
-        line["config4_stream"] = sub_line(args, D, ctx, "stream", 2000, 100, 8.0, oracle_steps=200, window="json",
+        # (BASELINE config 4: a 10k-scan trajectory -- every config-4 line
+        # times 10,000 steps after 100 warm-up steps)
+        line["config4_stream"] = sub_line(args, D, ctx, "stream", 10000, 100, 8.0, oracle_steps=200, window="json",
                                           interp=1, fused=1, driver="cpp", ctx_option=None)
         # SURVEY §8(d)'s config-4 variants: the per-scan match at the config-2
         # window (+-2 m / +-30 deg), and with the interpolator off (N = 1081)
-        line["config4_stream_config2_window"] = sub_line(args, D, ctx, "stream", 400, 20, 4.0, oracle_steps=200,
+        line["config4_stream_config2_window"] = sub_line(args, D, ctx, "stream", 10000, 20, 4.0, oracle_steps=200,
                                                          window="config2", interp=1, fused=1, driver="cpp",
                                                          ctx_option=None)
-        line["config4_stream_raw_scans"] = sub_line(args, D, ctx, "stream", 2000, 100, 4.0, oracle_steps=200,
+        line["config4_stream_raw_scans"] = sub_line(args, D, ctx, "stream", 10000, 100, 4.0, oracle_steps=200,
                                                     window="json", interp=0, fused=1, driver="cpp", ctx_option=None)
         line["config3_refine"] = sub_line(args, D, ctx, "refine", 100, 5, 3.0)
         line["f2_rebuild"] = sub_line(args, D, ctx, "rebuild", 10, 2, 3.0)

@@ -623,8 +623,10 @@ void run_bb(lgs_ctx* ctx, const lgs_bb_params* p, const lgs_cost_ge_params* cost
         const int ngc = std::max(0, std::min(g1, gcap) - g0);
         std::vector<BBGuard> guards((size_t)ngc);
         std::vector<int4> gnodes((size_t)ngc);
-        if (ngc > 0 && g1 <= gcap) {
-            // the guarded nodes' coordinates, gathered on the device
+        if (ngc > 0) {
+            // the guarded nodes' coordinates, gathered on the device (also
+            // past guard_cap: the first gcap records still credit their
+            // matches' guard_hits; the nodes are then all re-scored below)
             std::vector<const int4*> lists((size_t)Hm + 1, nullptr);
             for (int l = 0; l <= lv1; ++l) lists[(size_t)l] = levels[(size_t)l].d_nodes;
             Upload ug(ctx);

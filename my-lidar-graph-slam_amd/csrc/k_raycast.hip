@@ -1944,8 +1944,8 @@ void record_writer(LatestCache& C, hipStream_t st, lgs_map* latest, lgs_map* loc
     if (gen == 0) gen = ++counter;   // 0: the word's initial value
     {
         std::lock_guard<std::mutex> lk(C.wev->mu);
-        C.wev->st = st;
-        C.wev->gen = gen;
+        C.wev->st.store(st, std::memory_order_release);
+        C.wev->gen.store(gen, std::memory_order_release);
     }
     hipLaunchKernelGGL(k_writer_done, dim3(1), dim3(1), 0, st, C.wev->flag, gen);
     LGS_HIP_CHECK(hipGetLastError());
@@ -2344,7 +2344,7 @@ extern "C" void lgs_map_destroy(lgs_map* m)
             try {
                 m->cache->wev->wait();
             } catch (...) {
-                hipStreamSynchronize(m->cache->wev->st);
+                hipStreamSynchronize(m->cache->wev->st.load());
             }
         }
         delete m->cache;

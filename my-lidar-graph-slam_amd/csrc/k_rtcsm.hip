@@ -305,8 +305,9 @@ __device__ __forceinline__ bool strip_read(const double* __restrict__ cmap, int 
 constexpr int kProjRows = 16;
 constexpr int kProjRowsLone = 4;   // measured (lone config-2 scan): 16: 16.1 us, 8: 12.3, 4: 10.7, 2: 10.4
 template <int ROWS>
-__global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, double guard_eps, int inject)
+__global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, double guard_eps, int inject, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const Blk wg = xcd_block();
     const MatchItem& it = items[wg.z];
     const RtcsmPlan& pl = it.pl;
@@ -940,8 +941,9 @@ __device__ __forceinline__ unsigned pkmax(unsigned a, unsigned b)
 // unit qt whole (one 16-byte store per sub-phase, 64 consecutive units per
 // wave instruction), every quad's maxima computed by two threads.
 template <int NQ>
-__global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ jobs, int nplanes, SuperGeom g)
+__global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ jobs, int nplanes, SuperGeom g, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const Blk wg = xcd_block();
     const PlaneJob& job = jobs[wg.z / nplanes];
     const int p = wg.z % nplanes;
@@ -1163,8 +1165,9 @@ __device__ __forceinline__ float h16(unsigned long long bits)
 // third word holds rows 4q + 8 .. 4q + 11, read with the first two at once)
 typedef unsigned long long u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
 template <int NR, int U8>
-__global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const double* __restrict__ zero)
+__global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const double* __restrict__ zero, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const Blk wg = xcd_block();
     const MatchItem& it = items[wg.z];
     const RtcsmPlan& pl = it.pl;
@@ -1599,8 +1602,9 @@ constexpr int kListMaxNv = 4096;   // work-list batches: Nv bound (the unsafe te
 constexpr int kListWaves = LGS_LIST_WAVES;   // k_coarse_list workgroups (one wave each, grid-stride)
 constexpr int kUnsafeGroups = 4096;
 
-__global__ __launch_bounds__(64) void k_keep(Items items, WorkList W)
+__global__ __launch_bounds__(64) void k_keep(Items items, WorkList W, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const int j = blockIdx.y;
     const MatchItem& it = items[j];
     const RtcsmPlan& pl = it.pl;
@@ -1660,8 +1664,9 @@ __device__ __forceinline__ int list_prefix(const WorkList& W, int which, int n, 
 // (seq_sum_from).
 constexpr int kLC = 256;
 static_assert(kLC % 64 == 0, "whole waves per chunk row");
-__global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, int n, const double* __restrict__ zero)
+__global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, int n, const double* __restrict__ zero, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     __shared__ int s_cb[4][kLC + 2 * kPipe];
     const int lane = threadIdx.x, g4 = lane >> 4, m = lane & 15;
     int c;
@@ -1734,8 +1739,9 @@ __global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, i
 // The unsafe test of the listed edge angles (k_keep), one angle at a time per
 // workgroup (grid-stride).
 __global__ __launch_bounds__(64 * kLaneWaves) void k_unsafe_list(Items items, WorkList W, int n,
-                                                                 const double* __restrict__ zero)
+                                                                 const double* __restrict__ zero, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const int lane = threadIdx.x & 63;
     int c;
     const int total = list_prefix(W, 1, n, c);
@@ -2166,8 +2172,9 @@ __device__ __forceinline__ long long seed_pick_wave(const MatchItem& it, const R
     }
     return pick;
 }
-__global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items items)
+__global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items items, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const MatchItem& it = items[blockIdx.y];
     const RtcsmPlan& pl = it.pl;
     const double* __restrict__ cmap = it.cmap;
@@ -2267,8 +2274,9 @@ __global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items item
 }
 
 template <int MODE>
-__global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* __restrict__ zero)
+__global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* __restrict__ zero, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const MatchItem& it = items[blockIdx.y];
     const RtcsmPlan& pl = it.pl;
     const double* __restrict__ grid = it.grid;
@@ -2486,8 +2494,9 @@ constexpr int kSelSeg = 1024;
 // (batches: 256 threads, 36.4 -> 26.7 us per 64 scans; a lone scan keeps one
 // key per thread, 6.4 vs 8.3 us: its ~120 segments do not fill the GPU)
 template <int kSelThreads>
-__global__ __launch_bounds__(kSelThreads) void k_select(Items items, int use_sbound)
+__global__ __launch_bounds__(kSelThreads) void k_select(Items items, int use_sbound, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     static_assert(kSelSeg % kSelThreads == 0 && kSelThreads % 64 == 0, "whole chunks of whole waves");
     const MatchItem& it = items[blockIdx.y];
     if ((int)blockIdx.x >= it.nseg) return;   // past this item's segments (uniform)
@@ -2760,8 +2769,9 @@ __device__ __forceinline__ int2 unpack16(unsigned u)
 {
     return make_int2((int)(short)(u & 0xFFFFu), (int)(short)(u >> 16));
 }
-__global__ __launch_bounds__(64) void k_fine_regs(Items items, int n, const double* __restrict__ zero)
+__global__ __launch_bounds__(64) void k_fine_regs(Items items, int n, const double* __restrict__ zero, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     __shared__ int ipref[kMaxBatchItems + 1];
     __shared__ double stage[4 * kFrI * kFrBeam];
     extern __shared__ unsigned pidx[];   // [Nv + kFrPad] packed (x, y)
@@ -2881,8 +2891,9 @@ __global__ __launch_bounds__(64) void k_fine_regs(Items items, int n, const doub
 // strict update of :246) over the selected blocks in block order.  Lanes load
 // 64 consecutive entries at once; the acceptance itself walks them in lane
 // order with wave-uniform shuffles.  Then the 7 cost poses.
-__global__ __launch_bounds__(64) void k_replay(Items items)
+__global__ __launch_bounds__(64) void k_replay(Items items, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const MatchItem& it = items[blockIdx.x];
     const RtcsmPlan& pl = it.pl;
     const double* __restrict__ cscore = it.cscore;
@@ -3047,8 +3058,9 @@ __device__ __forceinline__ double min_sq_dist(const CostPlan& cp, const double* 
 // mode 1: read cells from cidx (after host patches).
 template <int KS>
 __global__ __launch_bounds__(kCostThreads) void k_cost(Items items, int guard_cap, double guard_eps, int inject,
-                                                       int mode)
+                                                       int mode, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const MatchItem& it = items[blockIdx.y];
     const CostPlan& cp = it.cp;
     const double* __restrict__ grid = it.grid;
@@ -3207,8 +3219,9 @@ template <int LR>
 __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int mode, int guard_cap,
                                                                double guard_eps, int inject,
                                                                const double* __restrict__ zero,
-                                                               const int4* __restrict__ patches, int npatch)
+                                                               const int4* __restrict__ patches, int npatch, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     constexpr int NT = 64 * (LR + 1), LD = 65;
     const MatchItem& it = items[blockIdx.y];
     const RtcsmPlan& pl = it.pl;
@@ -3538,8 +3551,9 @@ __global__ __launch_bounds__(64 * (LR + 1)) void k_match_small(Items items, int 
 // stores, the barrier puts all of them before the flag store.
 // --------------------------------------------------------------------------
 constexpr int kPostThreads = 256;
-__global__ __launch_bounds__(kPostThreads) void k_post(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16,
-                                                       unsigned* flag, unsigned gen)
+// A second segment (n2 words, LGS_OPT_DEVICE_TIMING: the chunk's timing
+// words) is copied the same way.
+__device__ __forceinline__ void post_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16)
 {
     const int nt = blockDim.x;
     for (int i0 = threadIdx.x; i0 < n16; i0 += 4 * nt) {
@@ -3551,6 +3565,13 @@ __global__ __launch_bounds__(kPostThreads) void k_post(const uint4* __restrict__
         for (int j = 0; j < 4; ++j)
             if (i0 + j * nt < n16) dst[i0 + j * nt] = x[j];
     }
+}
+__global__ __launch_bounds__(kPostThreads) void k_post(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16,
+                                                       unsigned* flag, unsigned gen, const uint4* __restrict__ src2,
+                                                       uint4* __restrict__ dst2, int n2)
+{
+    post_copy(src, dst, n16);
+    if (n2) post_copy(src2, dst2, n2);
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) *(volatile unsigned*)flag = gen;
@@ -4089,10 +4110,10 @@ void launch_sets(lgs_ctx* ctx, const RtcsmPlan& lp, const std::vector<PlaneSet>&
         {
             if (nq == 2)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_hv<2>), grid, dim3(256), 0, ctx->stream,
-                                   up.at<PlaneJob>(sj.pj_off), np, g);
+                                   up.at<PlaneJob>(sj.pj_off), np, g, ctx->dts(tok));
             else
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_hv<1>), grid, dim3(256), 0, ctx->stream,
-                                   up.at<PlaneJob>(sj.pj_off), np, g);
+                                   up.at<PlaneJob>(sj.pj_off), np, g, ctx->dts(tok));
         }
         ctx->timing_end(tok);
         LGS_HIP_CHECK(hipGetLastError());
@@ -4154,7 +4175,7 @@ void enqueue_cost_patches(lgs_ctx* ctx, const BatchShape& B, Items d_items, cons
     hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, st, items[0].cidx, dp, np);
     LGS_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, 1), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
-                       ctx->guard_eps, 0, 1);
+                       ctx->guard_eps, 0, 1, DevTs{});
     LGS_HIP_CHECK(hipGetLastError());
 }
 
@@ -4205,7 +4226,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
     case L:                                                                                                      \
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_match_small<L>), g, dim3(64 * (L + 1)),                              \
                            sizeof(int2) * nvp + sizeof(double) * small_buf_doubles<L>(), st, d_items, mode,       \
-                           ctx->guard_cap, ctx->guard_eps, inject, zero, dp, np);                                \
+                           ctx->guard_cap, ctx->guard_eps, inject, zero, dp, np, ctx->dts(tok));                 \
         break;
         if (!ctx->skipped(K_MATCH_SMALL)) switch (lr) {
             LGS_SMALL_CASE(2) LGS_SMALL_CASE(3) LGS_SMALL_CASE(4) LGS_SMALL_CASE(5) LGS_SMALL_CASE(6)
@@ -4221,7 +4242,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * nbeams);
         if (!ctx->skipped(K_COST))
             hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, n), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
-                               ctx->guard_eps, inject, 0);
+                               ctx->guard_eps, inject, 0, ctx->dts(tok_));
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
         if (opt.cost_patches && !opt.cost_patches->empty())
@@ -4246,10 +4267,10 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         if (ctx->skipped(K_PROJECT)) {
         } else if (lone)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_project<kProjRowsLone>), g, dim3(256), 0, st, d_items, ctx->guard_cap,
-                               ctx->guard_eps, inject);
+                               ctx->guard_eps, inject, ctx->dts(tok_));
         else
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_project<kProjRows>), g, dim3(256), 0, st, d_items, ctx->guard_cap,
-                               ctx->guard_eps, inject);
+                               ctx->guard_eps, inject, ctx->dts(tok_));
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
         if (opt.patches && !opt.patches->empty()) {
@@ -4269,11 +4290,11 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             dim3 g(B.chunks, B.Tmax, n);
             if (ctx->skipped(K_SUPER)) {
             } else if (B.oct && B.nsby <= 5)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<5, 2>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<5, 2>), g, dim3(64 * kSupWaves), lds, st, d_items, zero, ctx->dts(tok));
             else if (B.oct && B.unit8 == 3)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9, 3>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9, 3>), g, dim3(64 * kSupWaves), lds, st, d_items, zero, ctx->dts(tok));
             else if (B.oct)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9, 2>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9, 2>), g, dim3(64 * kSupWaves), lds, st, d_items, zero, ctx->dts(tok));
             else if (B.pair)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<1>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else
@@ -4293,12 +4314,12 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             for (const auto& itm : items) wide = wide && itm.nparts <= kSeedWideMaxParts;
             if (!ctx->skipped(K_SEED) && wide) {
                 hipLaunchKernelGGL(k_seed_members, dim3(nwide, n), dim3(kSeedMembersThreads),
-                                   sizeof(int) * (size_t)std::max(B.NvMax, 1), st, d_items);
+                                   sizeof(int) * (size_t)std::max(B.NvMax, 1), st, d_items, ctx->dts(tok));
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_seed_super<2>), dim3(kSeedCands, n), dim3(1024), lds, st,
-                                   d_items, zero);
+                                   d_items, zero, ctx->dts(tok));
             } else if (!ctx->skipped(K_SEED))
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_seed_super<0>), dim3(kSeedCands, n), dim3(1024), lds, st,
-                                   d_items, zero);
+                                   d_items, zero, ctx->dts(tok));
             else if (B.wl.cnt)   // (diagnostics) the work-list counters k_seed_super zeroes
                 LGS_HIP_CHECK(hipMemsetAsync(B.wl.cnt, 0, sizeof(int) * 16 * (size_t)n, st));
             ctx->timing_end(tok);
@@ -4309,7 +4330,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         const bool wl = n >= ctx->lanes_min_batch && B.wl.cnt && !ctx->skipped(K_COARSE);
         if (wl) {
             const int tk = ctx->timing_begin(K_COARSE_AUX, 8.0 * (double)B.Tmax * B.nsb2 * n);   // bound reads
-            hipLaunchKernelGGL(k_keep, dim3(B.Tmax, n), dim3(64), 0, st, d_items, B.wl);
+            hipLaunchKernelGGL(k_keep, dim3(B.Tmax, n), dim3(64), 0, st, d_items, B.wl, ctx->dts(tk));
             ctx->timing_end(tk);
             LGS_HIP_CHECK(hipGetLastError());
         }
@@ -4317,7 +4338,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         if (tok >= 0) ctx->pending[tok].coarse_evals = true;   // algorithmic bytes from the records
         if (ctx->skipped(K_COARSE)) {
         } else if (wl) {
-            hipLaunchKernelGGL(k_coarse_list_c, dim3(kListWaves), dim3(64), 0, st, d_items, B.wl, n, zero);
+            hipLaunchKernelGGL(k_coarse_list_c, dim3(kListWaves), dim3(64), 0, st, d_items, B.wl, n, zero, ctx->dts(tok));
         } else {
             const size_t lds = ((sizeof(int) * (size_t)B.NvMax + 15) & ~(size_t)15) +
                                sizeof(double) * 128 * kRing * kRowWaves;
@@ -4329,7 +4350,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         if (wl) {
             const int tk = ctx->timing_begin(K_COARSE_AUX, 0.0);
             hipLaunchKernelGGL(k_unsafe_list, dim3(std::min(kUnsafeGroups, n * B.Tmax)), dim3(64 * kLaneWaves), 0, st,
-                               d_items, B.wl, n, zero);
+                               d_items, B.wl, n, zero, ctx->dts(tk));
             ctx->timing_end(tk);
             LGS_HIP_CHECK(hipGetLastError());
         }
@@ -4356,10 +4377,10 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         if (!ctx->skipped(K_SELECT)) {
             if (n >= ctx->lanes_min_batch)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_select<256>), dim3((unsigned)B.nsegMax, n), dim3(256), 0, st,
-                                   d_items, B.pruned ? 1 : 0);
+                                   d_items, B.pruned ? 1 : 0, ctx->dts(tok_));
             else
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_select<kSelSeg>), dim3((unsigned)B.nsegMax, n), dim3(kSelSeg), 0,
-                                   st, d_items, B.pruned ? 1 : 0);
+                                   st, d_items, B.pruned ? 1 : 0, ctx->dts(tok_));
         }
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
@@ -4371,7 +4392,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         if (ctx->skipped(K_FINE)) {
         } else if (B.fine_staged && ctx->fine_staged) {
             hipLaunchKernelGGL(k_fine_regs, dim3(4096), dim3(64), sizeof(unsigned) * (size_t)(B.NvMax + kFrPad), st,
-                               d_items, n, zero);
+                               d_items, n, zero, ctx->dts(tok_));
         } else {
             hipLaunchKernelGGL(k_fine_lanes, dim3(4096), dim3(64 * kFineLanesWaves),
                                sizeof(int2) * (size_t)(B.NvMax + 4 * kPipe), st, d_items, n, zero);
@@ -4397,7 +4418,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
     {
         const int tok_ = ctx->timing_begin(K_REPLAY, 0.0);
         if (!ctx->skipped(K_REPLAY))
-            hipLaunchKernelGGL(k_replay, dim3(n), dim3(64), pref_bytes(B.nsegMax), st, d_items);
+            hipLaunchKernelGGL(k_replay, dim3(n), dim3(64), pref_bytes(B.nsegMax), st, d_items, ctx->dts(tok_));
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
     }
@@ -4409,7 +4430,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * nbeams);
         if (!ctx->skipped(K_COST))
             hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, n), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
-                               ctx->guard_eps, inject, 0);
+                               ctx->guard_eps, inject, 0, ctx->dts(tok_));
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
     }
@@ -4486,13 +4507,16 @@ bool check_projection_guards(lgs_ctx* ctx, const RtcsmPlan& pl, const lgs_scan* 
     use_host_idx = false;
     patches.clear();
     if (rec.guard_count == 0) return false;
+    int nvl = 0;   // this match's compaction (the list of its ScanRangeMax)
+    const int* vidx = scan_valid_indices(ctx, const_cast<lgs_scan*>(scan), pl.rmax, &nvl);
+    LGS_REQUIRE(nvl == pl.Nv, "scan compaction changed under a match");
     if (rec.guard_count > ctx->guard_cap) {
         // too many to inspect: full host projection (exact, slow path)
         host_idx.resize((size_t)pl.T * pl.Nv);
         for (int tt = 0; tt < pl.T; ++tt)
             for (int v = 0; v < pl.Nv; ++v) {
                 int ix, iy;
-                host_project(pl, scan, scan->h_vidx[v], tt, ix, iy);
+                host_project(pl, scan, vidx[v], tt, ix, iy);
                 host_idx[(size_t)tt * pl.Nv + v] = make_int2(ix, iy);
             }
         use_host_idx = true;
@@ -4501,7 +4525,7 @@ bool check_projection_guards(lgs_ctx* ctx, const RtcsmPlan& pl, const lgs_scan* 
     for (int k = 0; k < rec.guard_count; ++k) {
         const GuardRec& g = rec.guard[k];
         int ix, iy;
-        host_project(pl, scan, scan->h_vidx[g.v], g.t, ix, iy);
+        host_project(pl, scan, vidx[g.v], g.t, ix, iy);
         if (ix != g.ix || iy != g.iy) patches.push_back(make_int4(g.t, g.v, ix, iy));
     }
     return !patches.empty();
@@ -4704,9 +4728,30 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
     RtcsmRecord* d_rec = (RtcsmRecord*)ctx->ensure(ctx->banked(S_RECORDS), sizeof(RtcsmRecord) * (size_t)n);
     // the records' host copy, then (k_post) a completion flag
     const size_t rec_bytes = sizeof(RtcsmRecord) * (size_t)n;
-    RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned_rec(align256(rec_bytes) + 256);
+    // (pinned layout: records | flag (256 B) | the chunk's device-timing words)
+    constexpr size_t kDtsBytes = sizeof(unsigned long long) * 2 * kDtsSub * kDtsSlots;
+    RtcsmRecord* h_rec = (RtcsmRecord*)ctx->ensure_pinned_rec(align256(rec_bytes) + 256 + kDtsBytes);
     unsigned* h_flag = (unsigned*)((char*)h_rec + align256(rec_bytes));
     F.id = ++ctx->timing_batch;
+    // LGS_OPT_DEVICE_TIMING: the chain's launches stamp this bank's words,
+    // copied back with the records (k_post); reruns keep event timing
+    struct DtsScope {
+        lgs_ctx* c;
+        ~DtsScope() { c->dts_dev = nullptr; }
+    } dts_scope{ ctx };
+    if (ctx->profile && ctx->dev_timing) {
+        unsigned long long*& db = ctx->dts_buf[ctx->bank];
+        if (++ctx->dts_gen >= (1u << 24) || !db) {   // a new buffer, or the generations wrapped: zero the words
+            if (ctx->dts_gen >= (1u << 24)) ctx->dts_gen = 1;
+            for (int b = 0; b < 2; ++b) {
+                if (!ctx->dts_buf[b]) LGS_HIP_CHECK(hipMalloc((void**)&ctx->dts_buf[b], kDtsBytes));
+                LGS_HIP_CHECK(hipMemsetAsync(ctx->dts_buf[b], 0, kDtsBytes, ctx->stream));
+            }
+        }
+        ctx->dts_dev = db;
+        ctx->dts_host = (const unsigned long long*)((char*)h_flag + 256);
+        ctx->dts_used = 0;
+    }
     // The angle flags are only ever SET (k_project stamps an angle whose lattice
     // leaves the map low with the match's generation).  They live in a buffer
     // of their own that holds nothing but stamps, so a stale flag can never
@@ -4784,16 +4829,24 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
         F.post_gen = (unsigned)ctx->next_stamp();
         *(volatile unsigned*)h_flag = 0u;   // before the launch: k_post's store comes after it
         const int n16 = (int)(rec_bytes / 16);   // one word per thread where it fits (a lone match: one wave)
-        hipLaunchKernelGGL(k_post, dim3(1), dim3(std::min(kPostThreads, (n16 + 63) / 64 * 64)), 0, ctx->stream,
-                           (const uint4*)d_rec, (uint4*)h_rec,
-                           (int)(rec_bytes / 16), h_flag, F.post_gen);
+        const int n2 = ctx->dts_dev ? (int)(kDtsBytes / 16) : 0;
+        hipLaunchKernelGGL(k_post, dim3(1), dim3(std::min(kPostThreads, (std::max(n16, n2) + 63) / 64 * 64)), 0,
+                           ctx->stream, (const uint4*)d_rec, (uint4*)h_rec, (int)(rec_bytes / 16), h_flag, F.post_gen,
+                           (const uint4*)ctx->dts_dev, (uint4*)ctx->dts_host, n2);
         LGS_HIP_CHECK(hipGetLastError());
     } else {
         LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, rec_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        if (ctx->dts_dev)
+            LGS_HIP_CHECK(hipMemcpyAsync(const_cast<unsigned long long*>(ctx->dts_host), ctx->dts_dev, kDtsBytes,
+                                         hipMemcpyDeviceToHost, ctx->stream));
     }
     hipEvent_t& ev = ctx->bank_ev[ctx->bank];
     if (!ev) LGS_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     LGS_HIP_CHECK(hipEventRecord(ev, ctx->stream));
+    // the tail ran on the priority stream: the context's own stream waits for
+    // it, so every later synchronisation of that stream (sync(), a scratch
+    // regrow in ensure*) also covers the tail's reads of the scratch
+    if (ctx->stream != restore.s) LGS_HIP_CHECK(hipStreamWaitEvent(restore.s, ev, 0));
     F.items = std::move(items);
     F.B = B;
     F.gens = std::move(gens);
@@ -5049,7 +5102,7 @@ void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params
     Items d_items = up.at<MatchItem>(ioff);
     const int ks = cost->kernel_size;
     hipLaunchKernelGGL(KCOST(ks), dim3(7, n), dim3(kCostThreads), 0, ctx->stream, d_items, ctx->guard_cap,
-                       ctx->guard_eps, ctx->inject_index ? 1 : 0, 0);
+                       ctx->guard_eps, ctx->inject_index ? 1 : 0, 0, DevTs{});
     LGS_HIP_CHECK(hipGetLastError());
     LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
     ctx->sync();
@@ -5082,7 +5135,7 @@ void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params
             if (np) hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, ctx->stream,
                                        items[j].cidx, dp, np);
             hipLaunchKernelGGL(KCOST(ks), dim3(7, 1), dim3(kCostThreads), 0, ctx->stream, d_items + j,
-                               ctx->guard_cap, ctx->guard_eps, 0, 1);
+                               ctx->guard_cap, ctx->guard_eps, 0, 1, DevTs{});
             LGS_HIP_CHECK(hipGetLastError());
             LGS_HIP_CHECK(hipMemcpyAsync(&h_rec[j], d_rec + j, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                          ctx->stream));
@@ -5244,7 +5297,8 @@ extern "C" int lgs_rtcsm_dense_scores(lgs_ctx* ctx, const lgs_grid* grid, const 
         launch_sets(ctx, pl, sets, sj, up);
         Items d_items = up.at<MatchItem>(off);
         dim3 g(std::max(1, (nv + 255) / 256), (pl.T + kProjRows - 1) / kProjRows, 1);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_project<kProjRows>), g, dim3(256), 0, ctx->stream, d_items, 0, -1.0, 0);
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_project<kProjRows>), g, dim3(256), 0, ctx->stream, d_items, 0, -1.0, 0,
+                           DevTs{});
         LGS_HIP_CHECK(hipGetLastError());
         if (coarse_scores) {
             dim3 gc((pl.P + cb - 1) / cb, pl.T, 1);
@@ -5297,7 +5351,7 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
         up.flush();
         Items d_items = up.at<MatchItem>(off);
         hipLaunchKernelGGL(KCOST(cp.kernel_size), dim3(1, 1), dim3(kCostThreads), 0, ctx->stream, d_items,
-                           ctx->guard_cap, ctx->guard_eps, 0, 0);
+                           ctx->guard_cap, ctx->guard_eps, 0, 0, DevTs{});
         LGS_HIP_CHECK(hipGetLastError());
         LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                      ctx->stream));
@@ -5315,7 +5369,7 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
             LGS_HIP_CHECK(hipMemcpyAsync(it.cidx, row.data(), sizeof(int4) * row.size(),
                                          hipMemcpyHostToDevice, ctx->stream));
             hipLaunchKernelGGL(KCOST(cp.kernel_size), dim3(1, 1), dim3(kCostThreads), 0, ctx->stream, d_items,
-                               ctx->guard_cap, ctx->guard_eps, 0, 1);
+                               ctx->guard_cap, ctx->guard_eps, 0, 1, DevTs{});
             LGS_HIP_CHECK(hipGetLastError());
             LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
                                          ctx->stream));

@@ -220,6 +220,16 @@ void lgs_ctx::sync()
 int lgs_ctx::timing_begin(int kernel, double algo_bytes)
 {
     if (!profile || !((profile_mask >> kernel) & 1u)) return -1;
+    if (dev_timing && dts_dev && dts_used < kDtsSlots) {
+        // device-timed: a slot of the chunk's words, no events
+        PendingTiming t{ kernel, nullptr, nullptr, algo_bytes };
+        t.batch = timing_batch;
+        t.hw = dts_host + (size_t)dts_used * 2 * kDtsSub;
+        t.tag = (unsigned long long)dts_gen << 40;
+        ++dts_used;
+        pending.push_back(t);
+        return (int)pending.size() - 1;
+    }
     hipEvent_t ev[2];
     for (int i = 0; i < 2; ++i) {
         if (!event_pool.empty()) {
@@ -238,23 +248,39 @@ int lgs_ctx::timing_begin(int kernel, double algo_bytes)
 
 void lgs_ctx::timing_end(int token)
 {
-    if (token < 0) return;
+    if (token < 0 || !pending[token].b) return;   // device-timed: nothing to record
     LGS_HIP_CHECK(hipEventRecord(pending[token].b, stream));
 }
 
+namespace {
+// A device-timed launch's span from its words' host copy (first workgroup
+// start to last workgroup end, s_memrealtime at 100 MHz); false if no
+// workgroup of this generation stamped both (e.g. a launch skipped).
+bool dts_span_ms(const PendingTiming& p, float& ms)
+{
+    unsigned long long t0 = ~0ull, t1 = 0;
+    bool any0 = false, any1 = false;
+    for (int s = 0; s < kDtsSub; ++s) {
+        const unsigned long long w0 = __atomic_load_n(p.hw + 2 * s, __ATOMIC_ACQUIRE);
+        const unsigned long long w1 = __atomic_load_n(p.hw + 2 * s + 1, __ATOMIC_ACQUIRE);
+        if ((w0 & ~kDtsMask) == p.tag) {
+            t0 = std::min(t0, kDtsMask - (w0 & kDtsMask));
+            any0 = true;
+        }
+        if ((w1 & ~kDtsMask) == p.tag) {
+            t1 = std::max(t1, w1 & kDtsMask);
+            any1 = true;
+        }
+    }
+    if (!any0 || !any1 || t1 < t0) return false;   // (t1 < t0: the 40-bit clock wrapped, ~3 h)
+    ms = (float)((double)(t1 - t0) * 1e-5);
+    return true;
+}
+}  // namespace
+
 void lgs_ctx::harvest()
 {
-    for (auto& p : pending) {
-        float ms = 0.f;
-        LGS_HIP_CHECK(hipEventSynchronize(p.b));
-        LGS_HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
-        stat_launches[p.kernel] += 1;
-        stat_ms[p.kernel] += ms;
-        stat_bytes[p.kernel] += p.algo_bytes;
-        event_pool.push_back(p.a);
-        event_pool.push_back(p.b);
-    }
-    pending.clear();
+    harvest_upto(LLONG_MAX);
 }
 
 void lgs_ctx::harvest_upto(long long b)
@@ -263,13 +289,17 @@ void lgs_ctx::harvest_upto(long long b)
     for (; k < pending.size() && pending[k].batch <= b; ++k) {
         PendingTiming& p = pending[k];
         float ms = 0.f;
-        LGS_HIP_CHECK(hipEventSynchronize(p.b));
-        LGS_HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+        if (p.hw) {
+            if (!dts_span_ms(p, ms)) continue;
+        } else {
+            LGS_HIP_CHECK(hipEventSynchronize(p.b));
+            LGS_HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+            event_pool.push_back(p.a);
+            event_pool.push_back(p.b);
+        }
         stat_launches[p.kernel] += 1;
         stat_ms[p.kernel] += ms;
         stat_bytes[p.kernel] += p.algo_bytes;
-        event_pool.push_back(p.a);
-        event_pool.push_back(p.b);
     }
     pending.erase(pending.begin(), pending.begin() + (long)k);
 }
@@ -304,7 +334,12 @@ void lgs_ctx::release()
     aux_bytes.clear();
     if (zero) hipFree(zero);
     zero = nullptr;
+    for (int b = 0; b < 2; ++b) {
+        if (dts_buf[b]) hipFree(dts_buf[b]);
+        dts_buf[b] = nullptr;
+    }
     for (auto& p : pending) {
+        if (!p.a) continue;   // device-timed
         hipEventDestroy(p.a);
         hipEventDestroy(p.b);
     }
@@ -472,6 +507,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_POST_RECORDS: ctx->post_records = value != 0.0; return LGS_OK;
     case LGS_OPT_FUSED_PLANES: ctx->fused_planes = value != 0.0; return LGS_OK;
     case LGS_OPT_PRIORITY_TAIL: ctx->prio_tail = value != 0.0; return LGS_OK;
+    case LGS_OPT_DEVICE_TIMING: ctx->dev_timing = value != 0.0; return LGS_OK;
     case LGS_OPT_HV_FULL: ctx->hv_full = value != 0.0; return LGS_OK;
     case LGS_OPT_SPLIT_CHUNKS: ctx->split_chunks = value != 0.0; return LGS_OK;
     case LGS_OPT_DEVICE_HITS: ctx->device_hits = value != 0.0; return LGS_OK;
@@ -802,8 +838,9 @@ template <int LR>
 constexpr int pqx() { return pqx_of(LR); }
 typedef double d2a16 __attribute__((ext_vector_type(2)));
 template <int LR, int kPTY = 16>
-__global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __restrict__ jobs)
+__global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __restrict__ jobs, DevTs dts)
 {
+    const DtsScope dts_scope(dts);
     const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
     const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
     const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
@@ -1032,11 +1069,11 @@ void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, i
             if (njobs == 1) \
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_precompute_planes<L, LGS_PTY_LONE>), \
                     dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + LGS_PTY_LONE - 1) / LGS_PTY_LONE, njobs), \
-                    dim3(256), 0, ctx->stream, d_jobs); \
+                    dim3(256), 0, ctx->stream, d_jobs, ctx->dts(tok)); \
             else \
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_precompute_planes<L, LGS_PTY_BATCH>), \
                     dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + LGS_PTY_BATCH - 1) / LGS_PTY_BATCH, njobs), dim3(256), 0, ctx->stream, \
-                    d_jobs); \
+                    d_jobs, ctx->dts(tok)); \
             break;
         LGS_PP_CASE(1) LGS_PP_CASE(2) LGS_PP_CASE(3) LGS_PP_CASE(4) LGS_PP_CASE(5) LGS_PP_CASE(6)
         LGS_PP_CASE(7) LGS_PP_CASE(8)
@@ -1355,18 +1392,19 @@ void scans_to_device(lgs_ctx* ctx, const lgs_scan* const* scans, int n, Upload* 
 const int* scan_valid_indices(lgs_ctx* ctx, lgs_scan* s, double rmax, int* nv)
 {
     std::lock_guard<std::mutex> g(s->cache_mu);   // two contexts may match this scan at once
-    if (!(s->cached_rmax == rmax)) {
+    uint64_t key;
+    std::memcpy(&key, &rmax, sizeof(key));
+    if (std::isnan(rmax)) key = 0x7ff8000000000000ull;
+    auto it = s->vidx_by_rmax.find(key);
+    if (it == s->vidx_by_rmax.end()) {
         std::vector<int> v;
         for (int i = 0; i < s->n; ++i)
             if (!(s->h_ranges[i] >= rmax)) v.push_back(i);
-        if (!s->h_vidx.empty()) s->vidx_old.push_back(std::move(s->h_vidx));
-        s->h_vidx = std::move(v);
-        s->nv = (int)s->h_vidx.size();
-        s->cached_rmax = rmax;
+        it = s->vidx_by_rmax.emplace(key, std::move(v)).first;
     }
     (void)ctx;
-    *nv = s->nv;   // the device compacts the same beams itself (k_project)
-    return s->h_vidx.data();
+    *nv = (int)it->second.size();   // the device compacts the same beams itself (k_project)
+    return it->second.data();
 }
 
 namespace {

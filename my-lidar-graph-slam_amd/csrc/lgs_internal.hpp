@@ -9,6 +9,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -16,6 +17,7 @@
 #include <stdexcept>
 #include <string>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <atomic>
 #include <condition_variable>
@@ -256,6 +258,50 @@ struct PendingTiming {
     // actually scored x 8 B x Nv) once their host copy is known
     bool coarse_evals = false;
     long long batch = 0;   // lgs_ctx::timing_batch when launched
+    // device-timed launch (LGS_OPT_DEVICE_TIMING): the slot's host copy and tag
+    const unsigned long long* hw = nullptr;
+    unsigned long long tag = 0;
+};
+
+// Device timing of a launch (LGS_OPT_DEVICE_TIMING): kDtsSub sub-slots of two
+// words (start, end), each word gen << 40 | 40-bit value, raised by relaxed
+// agent-scope atomic maxima (vector atomics).  The start word holds
+// kDtsMask - t, so its maximum is the earliest start of this generation;
+// older generations' values are smaller, so the words need no reset between
+// launches (only zero at allocation).  Sub-slot = linear workgroup id & 7 (the
+// workgroup's XCD under round-robin dispatch): 8 addresses share the atomics.
+constexpr int kDtsSub = 8;
+constexpr int kDtsSlots = 32;   // device-timed launches per chunk
+constexpr unsigned long long kDtsMask = (1ull << 40) - 1ull;
+struct DevTs {
+    unsigned long long* w;   // this launch's 2 x kDtsSub words (null: not device-timed)
+    unsigned long long tag;  // gen << 40
+};
+__device__ __forceinline__ int dts_sub()
+{
+    return (int)((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & (kDtsSub - 1));
+}
+__device__ __forceinline__ void dts_begin(const DevTs& d)
+{
+    if (d.w && threadIdx.x == 0 && threadIdx.y == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime() & kDtsMask;
+        __hip_atomic_fetch_max(d.w + 2 * dts_sub(), d.tag | (kDtsMask - t), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+__device__ __forceinline__ void dts_end(const DevTs& d)
+{
+    if (d.w && threadIdx.x == 0 && threadIdx.y == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime() & kDtsMask;
+        __hip_atomic_fetch_max(d.w + 2 * dts_sub() + 1, d.tag | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// start stamp at construction (the kernel's first statement), end stamp at
+// every exit of thread 0
+struct DtsScope {
+    const DevTs d;
+    __device__ explicit DtsScope(const DevTs& x) : d(x) { dts_begin(d); }
+    __device__ ~DtsScope() { dts_end(d); }
 };
 }  // namespace lgs
 
@@ -389,6 +435,22 @@ struct lgs_ctx {
     // after a stream synchronisation.
     int timing_begin(int kernel, double algo_bytes);
     void timing_end(int token);
+    // LGS_OPT_DEVICE_TIMING: per-bank device words of a chunk's launches (zeroed
+    // at allocation), the chunk's region while its chain is enqueued (null
+    // otherwise: event timing), its host copy (written by k_post) and slots used
+    bool dev_timing = false;
+    unsigned long long* dts_buf[2] = {};
+    unsigned long long* dts_dev = nullptr;
+    const unsigned long long* dts_host = nullptr;
+    int dts_used = 0;
+    unsigned dts_gen = 0;   // 24-bit generations, per context (monotonic per bank region)
+    // the launch's device-timing words for a timing token (DevTs{} = none)
+    lgs::DevTs dts(int token) const
+    {
+        if (token < 0 || !pending[(size_t)token].hw) return lgs::DevTs{ nullptr, 0ull };
+        const size_t slot = (size_t)(pending[(size_t)token].hw - dts_host) / (2 * lgs::kDtsSub);
+        return lgs::DevTs{ dts_dev + slot * 2 * lgs::kDtsSub, pending[(size_t)token].tag };
+    }
     void harvest();
     // timings of the launches tagged with batch <= b only (the next chunk's
     // may still be running)
@@ -426,9 +488,13 @@ namespace lgs {
 // the writer's work included).
 struct WriterEvent {
     hipEvent_t ev = nullptr;      // created and recorded lazily, under mu
-    hipStream_t st = nullptr;
+    // (st, gen) are set together under mu by the owner's record_writer;
+    // readers in other contexts (grid_acquire, clone_grid) load them without
+    // the lock, so both are atomics: a reader sees either pair member of a
+    // newer writer, which only makes it wait for more work, never less
+    std::atomic<hipStream_t> st{ nullptr };
     unsigned* flag = nullptr;     // coherent pinned word (k_raycast.hip record_writer)
-    unsigned gen = 0;             // the pending writer's generation
+    std::atomic<unsigned> gen{ 0 };   // the pending writer's generation
     std::mutex mu;
     WriterEvent() = default;
     WriterEvent(const WriterEvent&) = delete;
@@ -438,14 +504,14 @@ struct WriterEvent {
         if (ev) hipEventDestroy(ev);
         if (flag) hipHostFree(flag);
     }
-    bool done() const { return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == gen; }
+    bool done() const { return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == gen.load(std::memory_order_acquire); }
     // the host waits for the writer's work; a stream that went idle without
     // the word (a fault, a lost store) is an error
     void wait()
     {
         for (unsigned spins = 1; !done(); ++spins) {
             if (spins % 4096) continue;
-            const hipError_t e = hipStreamQuery(st);
+            const hipError_t e = hipStreamQuery(st.load(std::memory_order_acquire));
             if (e == hipSuccess && !done()) throw Error(LGS_ERR_INTERNAL, "map writer: completion word lost");
             if (e != hipSuccess && e != hipErrorNotReady) LGS_HIP_CHECK(e);
         }
@@ -456,7 +522,7 @@ struct WriterEvent {
         std::lock_guard<std::mutex> lk(mu);
         if (done()) return;
         if (!ev) LGS_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        LGS_HIP_CHECK(hipEventRecord(ev, st));
+        LGS_HIP_CHECK(hipEventRecord(ev, st.load(std::memory_order_acquire)));
         LGS_HIP_CHECK(hipStreamWaitEvent(reader, ev, 0));
     }
 };
@@ -560,15 +626,15 @@ struct lgs_scan {
     double min_range = 0, max_range = 0;
     double max_elem = 0;                 // *std::max_element(ranges)
     std::vector<double> h_ranges, h_angles;
-    // compaction cache: beams with range < scan_range_max, in beam order
-    double cached_rmax = NAN;
-    int nv = 0;
-    std::vector<int> h_vidx;      // host copy (guard re-projection); the device compacts itself
-    // the compaction is built once per ScanRangeMax, under cache_mu: contexts
-    // may match one scan at the same time; a replaced list stays alive (its
-    // readers may still hold it) in vidx_old.  cache_mu also guards hits_cache.
+    // compaction cache: beams with range < scan_range_max, in beam order, one
+    // list per distinct ScanRangeMax (the frontend's and the loop detector's
+    // matchers may alternate on one scan), built once under cache_mu and never
+    // modified after: a reader's pointer stays valid for the scan's lifetime
+    // and the set of lists is bounded by the matchers' distinct values (host
+    // copy for the guard re-projection; the device compacts itself).
+    // cache_mu also guards hits_cache.
     mutable std::mutex cache_mu;
-    std::vector<std::vector<int>> vidx_old;
+    std::map<uint64_t, std::vector<int>> vidx_by_rmax;   // keyed by the bits of ScanRangeMax (any NaN: one key)
     // hit points of the last (robot pose, usable range) they were computed for
     // (k_raycast.hip scan_hits): the frontend inserts a scan at its estimated
     // pose and then rebuilds the latest map from it at that same pose 10 times
@@ -657,7 +723,8 @@ inline void scan_to_device(lgs_ctx* ctx, const lgs_scan* s) { scans_to_device(ct
 // from another stream (a device-side wait, no host synchronisation).
 inline void grid_acquire(lgs_ctx* ctx, const lgs_grid* g)
 {
-    if (g && g->writer && g->writer->st != ctx->stream) g->writer->order_after(ctx->stream);
+    if (g && g->writer && g->writer->st.load(std::memory_order_acquire) != ctx->stream)
+        g->writer->order_after(ctx->stream);
 }
 
 // Host staging of one batch's descriptors: appended to a pinned buffer, then

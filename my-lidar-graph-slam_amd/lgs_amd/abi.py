@@ -44,6 +44,7 @@ LGS_OPT_SPLIT_CHUNKS = 30
 LGS_OPT_DEVICE_HITS = 31
 LGS_OPT_SEED_WIDE = 32
 LGS_OPT_ZERO_TILES = 33
+LGS_OPT_DEVICE_TIMING = 34   # correlative chunks' kernels timed on the device (s_memrealtime spans)
 KERNEL_IDS = ["k_project", "k_coarse", "k_seed", "k_select", "k_fine", "k_replay", "k_cost", "k_precompute",
               "k_linsolve", "k_ray_emit", "k_ray_apply", "k_super", "k_super_planes", "k_bb_score",
               "k_bb_expand", "k_coarse_aux", "k_match_small"]   # lgs_ctx_kernel_stats order

@@ -363,10 +363,10 @@ def test_wide_seed_same_records_less_coarse_work(ctx, world, small_map):
     try:
         ctx.set_option(abi.LGS_OPT_SEED_WIDE, 0)
         narrow = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, inits)]
-        ctx.set_option(abi.LGS_OPT_SEED_WIDE, 1)
+        ctx.set_option(abi.LGS_OPT_SEED_WIDE, 16)   # > 4 candidates: the two-launch wide seed runs
         wide = [_record(b) for b in ctx.optimize_pose_query_batch(g, P, cost, scans, inits)]
     finally:
-        ctx.set_option(abi.LGS_OPT_SEED_WIDE, 1)
+        ctx.set_option(abi.LGS_OPT_SEED_WIDE, 12)   # the library default
     strip = lambda rec: rec[:6] + rec[8:]   # all but coarse_blocks / fine_blocks (the device's work)
     assert [strip(r) for r in wide] == [strip(r) for r in narrow], _diff(wide, narrow)
     for f in (6, 7):

@@ -1,6 +1,6 @@
 #!/bin/bash
-# r05 final: full GPU suite, trace + PMC passes of the match bench
-# (pmc_summary.json for this library), the default bench line.  Usage: gpu_r05_final.sh <tag>
+# Final profile of THIS build: full GPU suite, trace + PMC passes of the match bench
+# (pmc_summary.json for this library), the default bench line.  Usage: tools/gpu_final.sh <tag>; then tools/gpu_prof_workloads.sh <tag> loop loop_bb rebuild
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 TAG=${1:-r05_vf}
