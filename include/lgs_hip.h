@@ -186,6 +186,7 @@ int  lgs_abi_version(void);
 #define LGS_OPT_SEED_WIDE     32  /* batches: the pruning bound seeded from the best members of this many candidate superblocks (5..16, default 12; the 4 best members fine-scored); 0..4 = 4 candidates in one launch */
 #define LGS_OPT_ZERO_TILES    33  /* 1 (default) = the per-map passes of a correlative batch skip the stores of a tile whose inputs are all +0 when that set's buffer already holds the tile's +0 outputs (per-tile words kept per bank, set and layout); 0 = every tile stored */
 #define LGS_OPT_DEVICE_TIMING 34  /* 1 = while LGS_OPT_PROFILE(_MASK) times a kernel of a correlative batch chunk, time it on the device instead of with stream events: its workgroups stamp s_memrealtime (100 MHz) at start and end into per-chunk words (two relaxed atomic maxima per workgroup), copied back with the chunk's records; a launch's time is its first workgroup's start to its last workgroup's end (the execution span rocprofv3 reports, not the wait of a stream event for the CUs).  Launches outside a chunk's main chain keep event timing.  0 (default) = events */
+#define LGS_OPT_LEAN_PROJECT  35  /* 1 (default) = batched pruned correlative chunks (work list, wide seed, staged fine evaluation) write only the superblock base of every (angle, beam) plus per-beam / per-angle trig tables, and the kernels that stage a coarse-base or cell row form it themselves with the projection's own arithmetic (bit-identical); 0 = every row materialised (the guard fix-up reruns and lone matches always materialise) */
 #define LGS_OPT_POISON_WS     15  /* diagnostics: 1 = fill every match workspace and record with 0xFF bytes before the batch runs (any read-before-write shows up) */
 int  lgs_ctx_set_option(lgs_ctx* ctx, int option, double value);
 

@@ -103,6 +103,15 @@ struct MatchItem {
     double* poses7;
     int4* cidx;
     double* terms;
+    // lean projection (LGS_OPT_LEAN_PROJECT): k_project
+    // writes only the superblock bases of every (angle, beam) plus these two
+    // tables, and every consumer of a coarse-base or cell row forms the rows
+    // it stages itself (lean_cell: k_project's arithmetic, bit for bit)
+    double4* btab;           // per valid beam v: range, cos, sin of its angle (glibc-free ocml sincos, as k_project)
+    double2* atab;           // per search angle t: cos, sin of the sensor angle
+    int lean;                // 1: the coarse-base and cell rows (idx, cbase[0, T Nv)) are NOT written
+    int inject;              // LGS_OPT_INJECT_INDEX (tests): a guarded projection's x index + 1
+    double geps;             // the projection guard's epsilon (near_boundary)
 };
 typedef const MatchItem* __restrict__ Items;
 
@@ -326,6 +335,7 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     __shared__ int s_wsum[4];
     __shared__ double s_ct[ROWS], s_st[ROWS];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool lean = it.lean != 0;
     if (tid < ROWS) {
         // currentSensorPose.mTheta = sensorPose.mTheta + stepTheta * t (:90-91)
         const int t = wg.y * ROWS + tid - pl.win_t;
@@ -334,6 +344,7 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
         sincos(th, &sn, &cs);
         s_ct[tid] = cs;
         s_st[tid] = sn;
+        if (lean && wg.x == 0 && wg.y * ROWS + tid < pl.T) it.atab[wg.y * ROWS + tid] = make_double2(cs, sn);
     }
     const int v0 = wg.x * 256;
     const int chunk = (pl.N + 255) / 256;
@@ -369,6 +380,7 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     const double a = angles[i];
     double sa, ca;
     sincos(a, &sa, &ca);
+    if (lean && wg.y == 0) it.btab[v] = make_double4(r, ca, sa, 0.0);
     const int tt1 = min(pl.T, (wg.y + 1) * ROWS);
     const double inv_res = 1.0 / pl.res;
     const double inv_lr = 1.0 / pl.low_res;
@@ -401,9 +413,11 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
         ix += inject;
     }
     const size_t o = (size_t)tt * pl.Nv + v;
-    idx[o] = ((unsigned long long)(unsigned)iy << 32) | (unsigned)ix;
     const BeamLattice bl = beam_lattice(ix, iy, pl, inv_lr);
-    cbase[o] = coarse_base_l(bl, pl);
+    if (!lean) {   // lean: the consumers form these rows themselves (lean_cell)
+        idx[o] = ((unsigned long long)(unsigned)iy << 32) | (unsigned)ix;
+        cbase[o] = coarse_base_l(bl, pl);
+    }
     cbase[pl.sb_off + o] = super_base_l(bl, pl);
     // this angle has a beam whose coarse lattice starts left of / below the
     // map: k_coarse must run its unsafe-block check (generation-stamped flag)
@@ -411,6 +425,35 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     }
 }
 
+// Lean projection: the cell of (angle t, valid beam v)
+// from the tables k_project wrote, with k_project's arithmetic operation for
+// operation (-ffp-contract=off: the same roundings, so the same bits), its
+// guard test included (LGS_OPT_INJECT_INDEX shifts a guarded x index here
+// exactly as there).  Only batches whose every consumer forms its rows this
+// way run lean (lean_rows on the host); guard fix-up reruns and lone matches
+// materialise the rows.
+__device__ __forceinline__ int2 lean_cell(const MatchItem& it, int t, int v)
+{
+    const RtcsmPlan& pl = it.pl;
+    const double4 b = it.btab[v];   // r, cos a, sin a
+    const double2 a = it.atab[t];   // cos th_t, sin th_t
+    const double c = a.x * b.y - a.y * b.z;
+    const double s = a.y * b.y + a.x * b.z;
+    const double hx = pl.sx + b.x * c;
+    const double hy = pl.sy + b.x * s;
+    const double inv_res = 1.0 / pl.res;
+    const double qx = (hx - pl.min_x) * inv_res;
+    const double qy = (hy - pl.min_y) * inv_res;
+    int ix = (int)floor(qx);
+    const int iy = (int)floor(qy);
+    if (it.inject && (near_boundary(qx, it.geps) || near_boundary(qy, it.geps))) ix += it.inject;
+    return make_int2(ix, iy);
+}
+__device__ __forceinline__ int lean_coarse_base(const MatchItem& it, int t, int v)
+{
+    const int2 q = lean_cell(it, t, v);
+    return coarse_base_l(beam_lattice(q.x, q.y, it.pl, 1.0 / it.pl.low_res), it.pl);
+}
 __global__ void k_patch(Items items, const int4* __restrict__ patches, int n)
 {
     const RtcsmPlan& pl = items[0].pl;
@@ -478,6 +521,25 @@ __device__ __forceinline__ void stage_lds(T* dst, const T* __restrict__ src, int
             if (v < n) dst[v] = x[j];
         }
     }
+}
+
+// Block-wide row staging (stage_lds's replacement for lean items): the angle
+// row of coarse bases / cells into LDS.
+__device__ __forceinline__ void stage_cbase_row(int* dst, const MatchItem& it, int t, int n)
+{
+    if (!it.lean) {
+        stage_lds(dst, it.cbase + (size_t)t * it.pl.Nv, n);
+        return;
+    }
+    for (int v = threadIdx.x; v < n; v += blockDim.x) dst[v] = lean_coarse_base(it, t, v);
+}
+__device__ __forceinline__ void stage_idx_row(int2* dst, const MatchItem& it, int t, int n)
+{
+    if (!it.lean) {
+        stage_lds(dst, it.idx + (size_t)t * it.pl.Nv, n);
+        return;
+    }
+    for (int v = threadIdx.x; v < n; v += blockDim.x) dst[v] = lean_cell(it, t, v);
 }
 
 
@@ -1513,11 +1575,12 @@ __device__ __forceinline__ void unsafe_angle(const MatchItem& it, int t)
     __shared__ int s_ccnt[kEdgeMaxNv / 64];
     int ne = -1;   // -1: walk every beam
     const int2* __restrict__ idr = idx + (size_t)t * pl.Nv;
+    const bool lean = it.lean != 0;   // the cells formed here (lean_cell), not read
     if (te && cnt > 0 && pl.Nv <= kEdgeMaxNv) {
         const int nch = (pl.Nv + 63) / 64;
         for (int c = w; c < nch; c += kLaneWaves) {
             const int v = c * 64 + lane;
-            const int2 q = v < pl.Nv ? idr[v] : make_int2(pl.win_x, pl.win_y);
+            const int2 q = v < pl.Nv ? (lean ? lean_cell(it, t, v) : idr[v]) : make_int2(pl.win_x, pl.win_y);
             const bool e = (q.x - pl.win_x < 0) | (q.y - pl.win_y < 0);
             const unsigned long long bal = __ballot(e);
             if (lane == 0) s_ccnt[c] = __popcll(bal);
@@ -1529,7 +1592,7 @@ __device__ __forceinline__ void unsafe_angle(const MatchItem& it, int t)
             int off = 0;
             for (int k = 0; k < c; ++k) off += s_ccnt[k];
             const int v = c * 64 + lane;
-            const int2 q = v < pl.Nv ? idr[v] : make_int2(pl.win_x, pl.win_y);
+            const int2 q = v < pl.Nv ? (lean ? lean_cell(it, t, v) : idr[v]) : make_int2(pl.win_x, pl.win_y);
             const bool e = (q.x - pl.win_x < 0) | (q.y - pl.win_y < 0);
             const unsigned long long bal = __ballot(e);
             if (e) s_edge[off + __popcll(bal & ((1ull << lane) - 1ull))] = q;
@@ -1560,7 +1623,7 @@ __device__ __forceinline__ void unsafe_angle(const MatchItem& it, int t)
                 }
             } else {
                 for (int v = 0; v < pl.Nv; ++v) {
-                    const int2 q = idr[v];
+                    const int2 q = lean ? lean_cell(it, t, v) : idr[v];
                     if (q.x - pl.win_x < 0 || q.y - pl.win_y < 0)
                         unsafe |= strip_read(cmap, q.x + x0, q.y + y0, pl, ext);
                 }
@@ -1671,6 +1734,7 @@ __global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, i
     const int lane = threadIdx.x, g4 = lane >> 4, m = lane & 15;
     int c;
     const int total = list_prefix(W, 0, n, c);
+    const bool lean = items[0].lean != 0;   // the batch's items all run lean or none
     constexpr int kOff = -(1 << 30);
     constexpr int PER = kLC / 64;
     for (int e0 = 4 * blockIdx.x; e0 < total; e0 += 4 * gridDim.x) {   // wave-uniform
@@ -1703,6 +1767,17 @@ __global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, i
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int nq = __shfl(Nv, 16 * q, 64);
+                if (lean) {   // the group's row formed here (lean_cell), its item and angle wave-uniform
+                    const int jq = __builtin_amdgcn_readfirstlane(__shfl(j, 16 * q, 64));
+                    const int tq = __builtin_amdgcn_readfirstlane(__shfl(t, 16 * q, 64));
+                    const MatchItem& iq = items[jq];
+#pragma unroll
+                    for (int i = 0; i < PER; ++i) {
+                        const int v = v0 + lane + 64 * i;
+                        pre[q][i] = v < nq ? lean_coarse_base(iq, tq, v) : kOff;
+                    }
+                    continue;
+                }
                 const int* row = (const int*)__shfl((unsigned long long)cbr, 16 * q, 64);
 #pragma unroll
                 for (int i = 0; i < PER; ++i) {
@@ -2204,7 +2279,7 @@ __global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items item
     const int ct = (int)(ck / nsb2), csb = (int)(ck % nsb2);
     // 2. member sums: member m = tid % 16, beam group g = tid / 16 (16 groups)
     int* srow = (int*)smem;   // [Nv]
-    stage_lds(srow, it.cbase + (size_t)ct * Nv, Nv);
+    stage_cbase_row(srow, it, ct, Nv);
     __syncthreads();
     constexpr int G = kSeedMembersThreads / 16;
     const int m = tid & 15, g = tid >> 4;
@@ -2280,9 +2355,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
     const MatchItem& it = items[blockIdx.y];
     const RtcsmPlan& pl = it.pl;
     const double* __restrict__ grid = it.grid;
-    const int2* __restrict__ idx = it.idx;
     const double* __restrict__ cmap = it.cmap;
-    const int* __restrict__ cbase = it.cbase;
     const double* __restrict__ part_c = it.part_c;
     const long long* __restrict__ part_k = it.part_k;
     const int nparts = it.nparts;
@@ -2328,7 +2401,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
         if (sk[0] != LLONG_MAX) {
             const int ct = (int)(sk[0] / pl.P);
             int2* sidx = (int2*)(smem + ((sizeof(int) * (size_t)Nv + 15) & ~(size_t)15));   // [Nv]
-            stage_lds(sidx, idx + (size_t)ct * Nv, Nv);
+            stage_idx_row(sidx, it, ct, Nv);
             __syncthreads();
             Lmine = seed_fine(pl, grid, zero, sidx, sk[0], sv[1], sv[2], red, reda, sv);
         }
@@ -2394,8 +2467,8 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
         // (one memory round trip less on this latency chain)
         int* srow = (int*)smem;   // [Nv]
         int2* sidx = (int2*)(smem + ((sizeof(int) * (size_t)Nv + 15) & ~(size_t)15));   // [Nv]
-        stage_lds(srow, cbase + (size_t)ct * Nv, Nv);
-        stage_lds(sidx, idx + (size_t)ct * Nv, Nv);
+        stage_cbase_row(srow, it, ct, Nv);
+        stage_idx_row(sidx, it, ct, Nv);
         __syncthreads();
         const int m = tid & 15, g = tid >> 4;
         const int jx = kSB * (csb % pl.nsbx) + (m & 3);
@@ -2814,8 +2887,9 @@ __global__ __launch_bounds__(64) void k_fine_regs(Items items, int n, const doub
         const double* __restrict__ grid = it.grid;
         const int2* __restrict__ src_idx = it.idx + (size_t)tt * Nv;
         __syncthreads();   // the previous block's row is read
+        const bool lean = it.lean != 0;
         for (int v = lane; v < Nv + kFrPad; v += 64) {
-            int2 c = v < Nv ? src_idx[v] : make_int2(-(1 << 28), -(1 << 28));
+            int2 c = v < Nv ? (lean ? lean_cell(it, tt, v) : src_idx[v]) : make_int2(-(1 << 28), -(1 << 28));
             c.x = min(max(c.x, -16384), 16383);   // far outside the map either way (W, H <= 8192)
             c.y = min(max(c.y, -16384), 16383);
             pidx[v] = (unsigned)(c.x & 0xFFFF) | ((unsigned)c.y << 16);
@@ -3755,7 +3829,7 @@ inline bool uses_super(const lgs_ctx* ctx, int nv_max, int nsb2, bool dense)
 // (sized for the batch's largest plan), field offsets below.
 struct ItemLayout {
     size_t idx, cbase, cscore, cflag, list, segcnt, dlist, fval, fpos, part_c, part_k, sbound, poses7, cidx,
-        terms, count, total;
+        terms, count, btab, atab, total;
 };
 ItemLayout item_layout(int Tmax, int NvMax, int P, int nsb2, int chunks, int cb, int frows, int Nmax)
 {
@@ -3786,6 +3860,8 @@ ItemLayout item_layout(int Tmax, int NvMax, int P, int nsb2, int chunks, int cb,
     L.cidx = take(sizeof(int4) * 7 * (size_t)Nmax);
     L.terms = take(sizeof(double) * 7 * (size_t)Nmax);
     L.count = take(128 + 24 * kSeedWide);   // Lp, Lc[kSeedCands], nsel | wide-seed members
+    L.btab = take(sizeof(double4) * (size_t)std::max(NvMax, 1));
+    L.atab = take(sizeof(double2) * (size_t)std::max(Tmax, 1));
     L.total = o;
     return L;
 }
@@ -3811,6 +3887,8 @@ void bind_workspace(MatchItem& it, char* base, const ItemLayout& L, int frows)
     it.nsel = (int*)(base + L.count + 64 + 8 * kSeedCands);
     it.seedm = (double*)(base + L.count + 128);
     it.dlist = (int*)(base + L.dlist);
+    it.btab = (double4*)(base + L.btab);
+    it.atab = (double2*)(base + L.atab);
     static_assert(64 + 8 * kSeedCands + 4 <= 128, "count block layout");
     it.frows = frows;
     it.nseg = (int)((it.pl.K + kSelSeg - 1) / kSelSeg);
@@ -4654,6 +4732,23 @@ struct InFlight {
     unsigned post_gen = 0;
 };
 
+// Lean projection (LGS_OPT_LEAN_PROJECT): only when every kernel enqueue_items
+// will launch on this batch forms its coarse-base and cell rows itself -- the
+// pruned work-list chain with the wide seed and the staged fine evaluator
+// (k_super_oct, k_seed_members + k_seed_super<2>, k_keep, k_coarse_list_c,
+// k_unsafe_list, k_fine_regs) -- the same decisions enqueue_items makes.
+bool lean_rows(const lgs_ctx* ctx, const BatchShape& B, const std::vector<MatchItem>& items)
+{
+    const int n = B.n;
+    if (!ctx->lean_project || B.small || !B.pruned || !B.oct || n < ctx->lanes_min_batch || !B.wl.cnt) return false;
+    if (ctx->skip_mask) return false;   // (diagnostics: skipped stages leave stale rows either way)
+    if (!(B.fine_lanes && B.fine_staged && ctx->fine_staged)) return false;
+    if (!(std::min(ctx->seed_wide, kSeedWide) > kSeedCands)) return false;
+    for (const auto& it : items)
+        if (it.nparts > kSeedWideMaxParts) return false;
+    return true;
+}
+
 // The device part of a batch, on ctx->bank's buffers: every stage launched,
 // the records' copy to the host queued and the bank's event recorded.
 void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost_ge_params* cost,
@@ -4783,7 +4878,11 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
         it.keepc = B.wl.cnt ? B.wl.cnt + 16 * j : sctr ? sctr + j : nullptr;
         it.nparts = item_nparts(B, it.pl, B.pruned);
         it.nseedm = std::min(ctx->seed_wide, kSeedWide);
+        it.inject = ctx->inject_index ? 1 : 0;
+        it.geps = ctx->guard_eps;
     }
+    const bool lean = lean_rows(ctx, B, items);
+    for (auto& it : items) it.lean = lean ? 1 : 0;
     ctx->dbg.assign((size_t)n, lgs_ctx::DbgItem{});
     for (int j = 0; j < n; ++j) {
         // every item's intermediates for lgs_debug_item_buffer (diagnostics)
@@ -4960,6 +5059,7 @@ void finish_matches(lgs_ctx* ctx, InFlight& F)
             B1.pruned = pruned = !B.small && uses_super(ctx, B.NvMax, B.nsb2, opt.dense);
             std::vector<MatchItem> one(1, items[j]);
             one[0].nparts = item_nparts(B1, one[0].pl, B1.pruned);
+            one[0].lean = 0;   // a rerun materialises its rows (k_patch / the host's rows patch them)
             const int g = one[0].gen = ctx->generation = ctx->next_stamp();
             if ((size_t)j < ctx->dbg.size()) ctx->dbg[j].gen = g;
             Upload u1(ctx);

@@ -512,6 +512,7 @@ extern "C" int lgs_ctx_set_option(lgs_ctx* ctx, int option, double value)
     case LGS_OPT_SPLIT_CHUNKS: ctx->split_chunks = value != 0.0; return LGS_OK;
     case LGS_OPT_DEVICE_HITS: ctx->device_hits = value != 0.0; return LGS_OK;
     case LGS_OPT_ZERO_TILES: ctx->zero_tiles = value != 0.0; return LGS_OK;
+    case LGS_OPT_LEAN_PROJECT: ctx->lean_project = value != 0.0; return LGS_OK;
     case LGS_OPT_SEED_WIDE:
         if (!(value >= 0.0 && value <= 16.0)) return LGS_ERR_INVALID_ARG;
         ctx->seed_wide = (int)value;

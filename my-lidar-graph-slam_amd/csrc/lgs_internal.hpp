@@ -268,32 +268,41 @@ struct PendingTiming {
 // agent-scope atomic maxima (vector atomics).  The start word holds
 // kDtsMask - t, so its maximum is the earliest start of this generation;
 // older generations' values are smaller, so the words need no reset between
-// launches (only zero at allocation).  Sub-slot = linear workgroup id & 7 (the
-// workgroup's XCD under round-robin dispatch): 8 addresses share the atomics.
+// launches (only zero at allocation).  Atomics on one address serialise at
+// the memory side (~50 ns each: one pair per workgroup took a 27k-workgroup
+// launch from 10 to 358 us), so only a sample of workgroups stamps: the
+// first kDtsSub dispatched (workgroups are dispatched in linear-id order, so
+// one of them starts first) stamp the start; the last kDtsSub dispatched and
+// every kDtsEvery-th stamp the end (the last workgroup to finish is one of
+// the last dispatched when workgroups carry even work).
 constexpr int kDtsSub = 8;
+constexpr int kDtsEvery = 32;
 constexpr int kDtsSlots = 32;   // device-timed launches per chunk
 constexpr unsigned long long kDtsMask = (1ull << 40) - 1ull;
 struct DevTs {
     unsigned long long* w;   // this launch's 2 x kDtsSub words (null: not device-timed)
     unsigned long long tag;  // gen << 40
 };
-__device__ __forceinline__ int dts_sub()
-{
-    return (int)((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & (kDtsSub - 1));
-}
 __device__ __forceinline__ void dts_begin(const DevTs& d)
 {
     if (d.w && threadIdx.x == 0 && threadIdx.y == 0) {
-        const unsigned long long t = __builtin_amdgcn_s_memrealtime() & kDtsMask;
-        __hip_atomic_fetch_max(d.w + 2 * dts_sub(), d.tag | (kDtsMask - t), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        if (b < (unsigned)kDtsSub) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime() & kDtsMask;
+            __hip_atomic_fetch_max(d.w + 2 * b, d.tag | (kDtsMask - t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 __device__ __forceinline__ void dts_end(const DevTs& d)
 {
     if (d.w && threadIdx.x == 0 && threadIdx.y == 0) {
-        const unsigned long long t = __builtin_amdgcn_s_memrealtime() & kDtsMask;
-        __hip_atomic_fetch_max(d.w + 2 * dts_sub() + 1, d.tag | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        const unsigned nwg = gridDim.x * gridDim.y * gridDim.z;
+        if (b + (unsigned)kDtsSub >= nwg || b % (unsigned)kDtsEvery == 0u) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime() & kDtsMask;
+            const unsigned sub = (b + b / (unsigned)kDtsEvery) & (unsigned)(kDtsSub - 1);
+            __hip_atomic_fetch_max(d.w + 2 * sub + 1, d.tag | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 // start stamp at construction (the kernel's first statement), end stamp at
@@ -329,6 +338,7 @@ struct lgs_ctx {
     bool small_window = true;    // one-launch search of one-block windows (LGS_OPT_SMALL_WINDOW)
     bool fused_planes = true;    // superblock units by k_super_hv (LGS_OPT_FUSED_PLANES)
     int seed_wide = 12;
+    bool lean_project = true;    // LGS_OPT_LEAN_PROJECT (k_rtcsm.hip lean_rows)
     bool zero_tiles = true;   // LGS_OPT_ZERO_TILES          // batches: candidate superblocks whose best members seed the bound (LGS_OPT_SEED_WIDE; <= 4: one launch)
     bool device_hits = true;     // map rebuilds of many scans: hit points / ray cells on the device (LGS_OPT_DEVICE_HITS)
     bool split_chunks = false;   // calls of 32..64 matches as two chunks (LGS_OPT_SPLIT_CHUNKS; measured r05, 8-rank loop block: 1.007 vs 0.869 ms as one)

@@ -45,6 +45,7 @@ LGS_OPT_DEVICE_HITS = 31
 LGS_OPT_SEED_WIDE = 32
 LGS_OPT_ZERO_TILES = 33
 LGS_OPT_DEVICE_TIMING = 34   # correlative chunks' kernels timed on the device (s_memrealtime spans)
+LGS_OPT_LEAN_PROJECT = 35    # batched chunks: only superblock bases projected; consumers form their rows
 KERNEL_IDS = ["k_project", "k_coarse", "k_seed", "k_select", "k_fine", "k_replay", "k_cost", "k_precompute",
               "k_linsolve", "k_ray_emit", "k_ray_apply", "k_super", "k_super_planes", "k_bb_score",
               "k_bb_expand", "k_coarse_aux", "k_match_small"]   # lgs_ctx_kernel_stats order
