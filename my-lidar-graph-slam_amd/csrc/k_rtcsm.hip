@@ -134,7 +134,11 @@ __device__ __forceinline__ Blk xcd_block()
     const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
     const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
     const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-    return { l % gx, (l / gx) % gy, l / (gx * gy) };
+    // uniform by construction; readfirstlane tells the compiler, so that a
+    // descriptor indexed by it is read with scalar loads (hoisted out of
+    // loops) instead of per-iteration vector loads (seen in k_project)
+    return { __builtin_amdgcn_readfirstlane(l % gx), __builtin_amdgcn_readfirstlane((l / gx) % gy),
+             __builtin_amdgcn_readfirstlane(l / (gx * gy)) };
 }
 
 // Per-set superblock-plane job: one coarse map's padded phase planes.
@@ -420,8 +424,10 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     }
     cbase[pl.sb_off + o] = super_base_l(bl, pl);
     // this angle has a beam whose coarse lattice starts left of / below the
-    // map: k_coarse must run its unsafe-block check (generation-stamped flag)
-    if (ix - pl.win_x < 0 || iy - pl.win_y < 0) tedge[tt] = gen;
+    // map: k_coarse must run its unsafe-block check (generation-stamped flag;
+    // one store per wave and angle)
+    const unsigned long long edge = __ballot(ix - pl.win_x < 0 || iy - pl.win_y < 0);
+    if (edge && lane == __ffsll((long long)edge) - 1) tedge[tt] = gen;
     }
 }
 
@@ -1216,6 +1222,9 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 #endif
 template <int NR>
 constexpr int oct_pipe() { return NR > 5 ? LGS_OCT_PIPE9 : LGS_OCT_PIPE5; }
+// entries past the staged superblock-base row that k_super_oct's batched
+// row reads may touch (64 beam slots x the deepest pipeline)
+constexpr int kOctRowPad = 64 * (LGS_OCT_PIPE5 > LGS_OCT_PIPE9 ? LGS_OCT_PIPE5 : LGS_OCT_PIPE9);
 __device__ __forceinline__ float h16(unsigned long long bits)
 {
     return (float)__builtin_bit_cast(SuperT, (unsigned short)(bits & 0xFFFFu));
@@ -1264,11 +1273,17 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
         u64x2 x[kOctPipe];
         unsigned long long y[kOctPipe];
         int sh[kOctPipe];
+        // the batch's row entries first, unconditionally (the LDS row is
+        // padded by kOctRowPad entries): one LDS wait per batch instead of
+        // one per load (a masked read before each gather serialised them)
+        int cv[kOctPipe];
+#pragma unroll
+        for (int j = 0; j < kOctPipe; ++j) cv[j] = row[nb * (i0 + j) + q];
 #pragma unroll
         for (int j = 0; j < kOctPipe; ++j) {
             const int v = nb * (i0 + j) + q;
             const bool ok = act && v < cnt;
-            const int c = ok ? row[v] : 0;
+            const int c = ok ? cv[j] : 0;
             sh[j] = 16 * (c & 3);
             const long long u = (long long)(c >> 2) + a;
             typedef const __attribute__((address_space(1))) u64x2a8 gu64x2a8_t;
@@ -1287,8 +1302,10 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
 #pragma unroll
         for (int j = 0; j < kOctPipe; ++j) {
             const int k = sh[j];
-            // rows 0..3 of the beam's window from bits k.. of (x.x, x.y, y)
-            const unsigned long long w0 = k ? ((x[j].x >> k) | (x[j].y << (64 - k))) : x[j].x;
+            // rows 0..3 of the beam's window from bits k.. of (x.x, x.y, y);
+            // (x.y << (63 - k)) << 1 is x.y << (64 - k) for k in [1, 63] and 0
+            // for k = 0: no branch on k
+            const unsigned long long w0 = (x[j].x >> k) | ((x[j].y << (63 - k)) << 1);
             sr[0] += h16(w0);
             sr[1] += h16(w0 >> 16);
             sr[2] += h16(w0 >> 32);
@@ -1296,7 +1313,7 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
             if constexpr (NR == 5) {
                 sr[4] += h16(x[j].y >> k);
             } else {
-                const unsigned long long w1 = k ? ((x[j].y >> k) | (y[j] << (64 - k))) : x[j].y;
+                const unsigned long long w1 = (x[j].y >> k) | ((y[j] << (63 - k)) << 1);
                 sr[4] += h16(w1);
                 sr[5] += h16(w1 >> 16);
                 sr[6] += h16(w1 >> 32);
@@ -4364,7 +4381,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
     if (B.pruned) {
         {
             const int tok = ctx->timing_begin(K_SUPER, 8.0 * B.nsb2 * beams_T);
-            const size_t lds = sizeof(int) * (size_t)std::max(B.NvMax, 1);
+            const size_t lds = sizeof(int) * ((size_t)std::max(B.NvMax, 1) + kOctRowPad);
             dim3 g(B.chunks, B.Tmax, n);
             if (ctx->skipped(K_SUPER)) {
             } else if (B.oct && B.nsby <= 5)
