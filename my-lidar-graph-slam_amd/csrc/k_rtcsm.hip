@@ -104,13 +104,14 @@ struct MatchItem {
     int4* cidx;
     double* terms;
     // lean projection (LGS_OPT_LEAN_PROJECT): k_project
-    // writes only the superblock bases of every (angle, beam) plus these two
-    // tables, and every consumer of a coarse-base or cell row forms the rows
-    // it stages itself (lean_cell: k_project's arithmetic, bit for bit)
+    // does not run; k_beams writes these two tables and every kernel that
+    // stages a superblock-base, coarse-base or cell row forms it itself
+    // (lean_super_row / lean_cell: k_project's arithmetic, bit for bit)
     double4* btab;           // per valid beam v: range, cos, sin of its angle (glibc-free ocml sincos, as k_project)
     double2* atab;           // per search angle t: cos, sin of the sensor angle
-    int lean;                // 1: the coarse-base and cell rows (idx, cbase[0, T Nv)) are NOT written
+    int lean;                // 1: no (angle, beam) row (idx, cbase) is written
     int inject;              // LGS_OPT_INJECT_INDEX (tests): a guarded projection's x index + 1
+    int gcap;                // guard records the record holds (guard_cap)
     double geps;             // the projection guard's epsilon (near_boundary)
 };
 typedef const MatchItem* __restrict__ Items;
@@ -339,7 +340,6 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     __shared__ int s_wsum[4];
     __shared__ double s_ct[ROWS], s_st[ROWS];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const bool lean = it.lean != 0;
     if (tid < ROWS) {
         // currentSensorPose.mTheta = sensorPose.mTheta + stepTheta * t (:90-91)
         const int t = wg.y * ROWS + tid - pl.win_t;
@@ -348,7 +348,6 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
         sincos(th, &sn, &cs);
         s_ct[tid] = cs;
         s_st[tid] = sn;
-        if (lean && wg.x == 0 && wg.y * ROWS + tid < pl.T) it.atab[wg.y * ROWS + tid] = make_double2(cs, sn);
     }
     const int v0 = wg.x * 256;
     const int chunk = (pl.N + 255) / 256;
@@ -384,7 +383,6 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
     const double a = angles[i];
     double sa, ca;
     sincos(a, &sa, &ca);
-    if (lean && wg.y == 0) it.btab[v] = make_double4(r, ca, sa, 0.0);
     const int tt1 = min(pl.T, (wg.y + 1) * ROWS);
     const double inv_res = 1.0 / pl.res;
     const double inv_lr = 1.0 / pl.low_res;
@@ -417,11 +415,9 @@ __global__ __launch_bounds__(256) void k_project(Items items, int guard_cap, dou
         ix += inject;
     }
     const size_t o = (size_t)tt * pl.Nv + v;
+    idx[o] = ((unsigned long long)(unsigned)iy << 32) | (unsigned)ix;
     const BeamLattice bl = beam_lattice(ix, iy, pl, inv_lr);
-    if (!lean) {   // lean: the consumers form these rows themselves (lean_cell)
-        idx[o] = ((unsigned long long)(unsigned)iy << 32) | (unsigned)ix;
-        cbase[o] = coarse_base_l(bl, pl);
-    }
+    cbase[o] = coarse_base_l(bl, pl);
     cbase[pl.sb_off + o] = super_base_l(bl, pl);
     // this angle has a beam whose coarse lattice starts left of / below the
     // map: k_coarse must run its unsafe-block check (generation-stamped flag;
@@ -459,6 +455,104 @@ __device__ __forceinline__ int lean_coarse_base(const MatchItem& it, int t, int 
 {
     const int2 q = lean_cell(it, t, v);
     return coarse_base_l(beam_lattice(q.x, q.y, it.pl, 1.0 / it.pl.low_res), it.pl);
+}
+
+// Lean batches (r06): k_beams replaces k_project -- per item, the valid-beam
+// compaction (ComputeScanIndices' filter, :192-193) and the two tables
+// (range, cos, sin per valid beam: one sincos per beam; cos, sin per search
+// angle) -- and k_super_oct forms each angle's superblock-base row in LDS
+// with k_project's arithmetic (lean_super_row), records its guarded
+// projections and the angle's edge flag: no (angle, beam) row is written to
+// memory at all (k_project wrote 4-16 B per (angle, beam), 0.085-0.106 ms
+// per 64 config-2 queries).  Grid (ceil(NvMax / 256), 1, items).
+__global__ __launch_bounds__(256) void k_beams(Items items, DevTs dts)
+{
+    const DtsScope dts_scope(dts);
+    const MatchItem& it = items[blockIdx.z];
+    const RtcsmPlan& pl = it.pl;
+    const double* __restrict__ ranges = it.ranges;
+    const double* __restrict__ angles = it.angles;
+    __shared__ int s_map[256];
+    __shared__ int s_wsum[4];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (blockIdx.x == 0)
+        for (int tt = tid; tt < pl.T; tt += 256) {
+            // currentSensorPose.mTheta = sensorPose.mTheta + stepTheta * t (:90-91), as k_project
+            const double th = pl.st + pl.step_t * (double)(tt - pl.win_t);
+            double sn, cs;
+            sincos(th, &sn, &cs);
+            it.atab[tt] = make_double2(cs, sn);
+        }
+    const int v0 = blockIdx.x * 256;
+    if (v0 >= pl.Nv) return;   // past this item's valid beams (uniform)
+    const int chunk = (pl.N + 255) / 256;
+    const int lo = min(tid * chunk, pl.N), hi = min(lo + chunk, pl.N);
+    int nvalid = 0;
+    for (int i = lo; i < hi; ++i) nvalid += !(ranges[i] >= pl.rmax);
+    int incl = nvalid;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += u;
+    }
+    if (lane == 63) s_wsum[wid] = incl;
+    __syncthreads();
+    int pos = incl - nvalid;
+    for (int j = 0; j < wid; ++j) pos += s_wsum[j];
+    for (int i = lo; i < hi; ++i)
+        if (!(ranges[i] >= pl.rmax)) {
+            const int r = pos - v0;
+            if (r >= 0 && r < 256) s_map[r] = i;
+            ++pos;
+        }
+    __syncthreads();
+    const int v = v0 + tid;
+    if (v >= pl.Nv) return;
+    const int i = s_map[tid];
+    double sa, ca;
+    sincos(angles[i], &sa, &ca);
+    it.btab[v] = make_double4(ranges[i], ca, sa, 0.0);
+}
+
+// The superblock-base row of angle t into LDS (block-wide), with k_project's
+// guard records (gen-tagged slots of the item's record, the injected index
+// shift of LGS_OPT_INJECT_INDEX) and the angle's edge flag.  Every thread of
+// the block must call it (a barrier inside).
+__device__ __forceinline__ void lean_super_row(const MatchItem& it, int t, int* srow)
+{
+    const RtcsmPlan& pl = it.pl;
+    RtcsmRecord* rec = it.rec;
+    const double inv_res = 1.0 / pl.res, inv_lr = 1.0 / pl.low_res;
+    const double2 at = it.atab[t];
+    int edge = 0;
+    for (int v = threadIdx.x; v < pl.Nv; v += blockDim.x) {
+        const double4 b = it.btab[v];
+        const double c = at.x * b.y - at.y * b.z;
+        const double s = at.y * b.y + at.x * b.z;
+        const double hx = pl.sx + b.x * c;
+        const double hy = pl.sy + b.x * s;
+        const double qx = (hx - pl.min_x) * inv_res;
+        const double qy = (hy - pl.min_y) * inv_res;
+        int ix = (int)floor(qx);
+        const int iy = (int)floor(qy);
+        const bool guarded = near_boundary(qx, it.geps) || near_boundary(qy, it.geps);
+        const int slot = tagged_slot_wave(&rec->guard_word, (unsigned)it.gen, guarded);
+        if (guarded) {
+            if (slot < it.gcap) {
+                GuardRec g;
+                g.t = t;
+                g.v = v;
+                g.ix = ix + it.inject;
+                g.iy = iy;
+                rec->guard[slot] = g;
+            }
+            ix += it.inject;
+        }
+        srow[v] = super_base_l(beam_lattice(ix, iy, pl, inv_lr), pl);
+        edge |= (ix - pl.win_x < 0 || iy - pl.win_y < 0) ? 1 : 0;
+    }
+    // this angle has a beam whose coarse lattice starts left of / below the
+    // map: the unsafe-block check runs for it (generation-stamped flag)
+    if (__syncthreads_or(edge) && threadIdx.x == 0) it.tedge[t] = it.gen;
 }
 __global__ void k_patch(Items items, const int4* __restrict__ patches, int n)
 {
@@ -1254,8 +1348,12 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
     const int nb = 64 / nsbx;               // beam slots per wave instruction
     const int q = lane / nsbx, a = lane - nsbx * q;
     const bool act = q < nb;
-    const int* __restrict__ cbrow = it.cbase + pl.sb_off + (size_t)t * pl.Nv;
-    stage_lds(srow, cbrow, pl.Nv);
+    if (it.lean) {   // the row formed here (lean_super_row), k_project does not run
+        lean_super_row(it, t, srow);
+    } else {
+        const int* __restrict__ cbrow = it.cbase + pl.sb_off + (size_t)t * pl.Nv;
+        stage_lds(srow, cbrow, pl.Nv);
+    }
     __syncthreads();
     const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
     const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
@@ -4358,9 +4456,13 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         const bool lone = n < ctx->lanes_min_batch;
         const int rows = lone ? kProjRowsLone : kProjRows;
         dim3 g(std::max(1, (B.NvMax + 255) / 256), (B.Tmax + rows - 1) / rows, n);
-        const int tok_ = ctx->timing_begin(K_PROJECT, 24.0 * beams_T);
+        // lean batches: the beam / angle tables only (k_super_oct projects)
+        const int tok_ = ctx->timing_begin(K_PROJECT, items[0].lean ? 32.0 * B.NvMax * n : 24.0 * beams_T);
         if (ctx->skipped(K_PROJECT)) {
-        } else if (lone)
+        } else if (items[0].lean)
+            hipLaunchKernelGGL(k_beams, dim3(std::max(1, (B.NvMax + 255) / 256), 1, n), dim3(256), 0, st, d_items,
+                               ctx->dts(tok_));
+        else if (lone)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_project<kProjRowsLone>), g, dim3(256), 0, st, d_items, ctx->guard_cap,
                                ctx->guard_eps, inject, ctx->dts(tok_));
         else
@@ -4897,6 +4999,7 @@ void launch_matches(lgs_ctx* ctx, const lgs_rtcsm_params* params, const lgs_cost
         it.nseedm = std::min(ctx->seed_wide, kSeedWide);
         it.inject = ctx->inject_index ? 1 : 0;
         it.geps = ctx->guard_eps;
+        it.gcap = ctx->guard_cap;
     }
     const bool lean = lean_rows(ctx, B, items);
     for (auto& it : items) it.lean = lean ? 1 : 0;

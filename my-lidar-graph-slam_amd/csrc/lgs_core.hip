@@ -850,7 +850,10 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
     const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     (void)l;
 #else
-    const int bx = l % gx, by = (l / gx) % gy, bz = l / (gx * gy);
+    // wave-uniform by construction: readfirstlane lets the job descriptor be
+    // read with scalar loads (the divisions put them in vector registers)
+    const int bx = __builtin_amdgcn_readfirstlane(l % gx), by = __builtin_amdgcn_readfirstlane((l / gx) % gy),
+              bz = __builtin_amdgcn_readfirstlane(l / (gx * gy));
 #endif
     const PrecompJob& j = jobs[bz];
     const int W = j.W, H = j.H;
@@ -974,7 +977,8 @@ __global__ __launch_bounds__(256) void k_precompute_jobs(const PrecompJob* __res
     const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     (void)l;
 #else
-    const int bx = l % gx, by = (l / gx) % gy, bz = l / (gx * gy);
+    const int bx = __builtin_amdgcn_readfirstlane(l % gx), by = __builtin_amdgcn_readfirstlane((l / gx) % gy),
+              bz = __builtin_amdgcn_readfirstlane(l / (gx * gy));
 #endif
     const PrecompJob& j = jobs[bz];
     if (bx * kTileX >= j.W || by * kTileY >= j.H) return;
