@@ -225,7 +225,7 @@ def roofline_from(stats, kernel, pmc_path, trace_kernel, bound, workload="match"
     8 TB/s HBM peak.  frac_hbm_counters = the PMC-counted HBM bytes of the same
     kernel (from this build's profile) over the same time; null without one.
     bytes_scale rescales the library's per-launch accounting (k_super counts
-    8 B per superblock lookup, the fp64 planes' width; the fp16 planes read 2 B)."""
+    8 B per superblock lookup, the fp64 planes' width; the 8-bit units read 1 B)."""
     k = stats.get(kernel)
     if not k or not k["launches"] or not k["algo_bytes"]:
         return None
@@ -622,10 +622,10 @@ def run_match(args, D, ctx):
         # pass after the timed region.  tools/trace_coarse.py splits a kernel
         # trace of this command (dispatches overlapping no other vs the rest).
         roofline=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"), cpu_baseline=cpu,
-        # the superblock-bound pass (2 B per angle x superblock x beam of the
-        # fp16 superblock planes), timed the same way
+        # the superblock-bound pass (1 B per angle x superblock x beam of the
+        # 8-bit superblock units, r06), timed the same way
         roofline_super=roofline_from(stats, "k_super", args.pmc, "k_super_oct<5, 2>", "l2-gather",
-                                     bytes_scale=0.25),
+                                     bytes_scale=0.125),
         timing=("device: s_memrealtime span of each launch (LGS_OPT_DEVICE_TIMING)" if args.device_timing
                 else "HIP events on each launch's stream"),
         timed_region_kernels=trk, largest_kernel=top,
@@ -812,9 +812,10 @@ def run_loop(args, D, ctx):
         roofline=roofline_from(stats, dominant, args.pmc, "k_bb_score" if bb else "k_coarse_list", "l2-gather",
                                workload="loop_bb" if bb else "loop"),
         # config 5's largest kernel by time is the 9-row superblock-bound pass,
-        # not the coarse sums: its own roofline (2 B per angle x superblock x beam)
+        # not the coarse sums: its own roofline (1 B per angle x superblock x
+        # beam of the 8-bit superblock units, r06)
         roofline_super=None if bb else roofline_from(stats, "k_super", args.pmc, "k_super_oct<9, 3>", "l2-gather",
-                                                     workload="loop", bytes_scale=0.25),
+                                                     workload="loop", bytes_scale=0.125),
         coarse_stage=None if bb else coarse_stage(stats),
         step_ms_p10_p50_p90=[round(1e3 * float(np.percentile(step_s, q)), 4) for q in (10, 50, 90)],
         step_spread=round(float((np.percentile(step_s, 90) - np.percentile(step_s, 10)) / np.median(step_s)), 4),

@@ -148,7 +148,29 @@ struct PlaneJob {
     const unsigned short* planes16;   // the planes rounded up to fp16 (same layout)
     SuperT* super;
     unsigned* zt;   // k_super_hv's zero-tile words of this set (null: none), see ZeroTiles
+    int* negflag;   // stamped with pgen when a bound value exceeds 1 (8-bit units cannot hold it)
+    int pgen;
 };
+
+// 8-bit superblock units (r06, octet layouts): 4 fp16 round-up maxima (bits
+// 16 i of v, i < 4) -> 4 bytes ceil(255 h) (exact: h has 11 significant
+// bits, so 255 h is exact in fp32, and ceil(255 h) / 255 >= h).  The bound is
+// then an exact integer sum / 255 (no fp32 partials).  A value above 1 (not an
+// occupancy probability) sets *over: the set's bounds are disabled (negflag,
+// as for negative cells).  Bit patterns of +0 and positive fp16 values order
+// like the values, so the maxima taken on them stay maxima here.
+__device__ __forceinline__ unsigned quad_u8(unsigned long long v, bool& over)
+{
+    unsigned r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float h = (float)__builtin_bit_cast(_Float16, (unsigned short)(v >> (16 * i)));
+        over |= h > 1.0f;
+        const float q = fminf(fmaxf(ceilf(h * 255.0f), 0.0f), 255.0f);
+        r |= (unsigned)q << (8 * i);
+    }
+    return r;
+}
 
 // The fp16 round-up copy of padded planes and the negative-cell stamp, for
 // planes the batched precompute did not write (phase-plane copies of
@@ -1028,8 +1050,9 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
         // of (qt - 1, X)
         static_assert(kSPY % 16 == 0, "whole quads of sub-phase rows per tile");
         typedef unsigned long long u64;
-        const int u8 = pl.unit8;   // 2: 16-byte units (8 rows), 3: 24-byte units (12 rows)
-        u64* __restrict__ uo = (u64*)(S + 4 * u8 * plane * pl.pstrideO);
+        const int u8 = pl.unit8;   // 8-bit units: 2 dwords (8 rows) or 3 (12 rows), as k_super_hv
+        unsigned* __restrict__ uo = (unsigned*)S + (long long)u8 * plane * pl.pstrideO;
+        bool over = false;
         for (int k = tid; k < kSPY * kQ; k += blockDim.x) {   // (quad, sub-phase, column), column fastest
             const int h = k / (16 * kQ), sp = (k / kQ) % 16, X = k % kQ;
             const int qt = (y0 >> 4) + h;
@@ -1039,11 +1062,13 @@ __global__ __launch_bounds__((SPX + 3 + 63) / 64 * 64) void k_super_planes(const
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 v |= (u64)__builtin_bit_cast(unsigned short, hs[16 * h + 4 * i + cy][sx][X]) << (16 * i);
+            const unsigned b4 = quad_u8(v, over);
             const long long u = sp * pl.subO + (long long)qt * pl.Wq4 + Xg;
-            gstore(uo + u8 * u, v);                                          // rows 4 qt .. of unit qt
-            if (qt > 0) gstore(uo + (u8 * (u - pl.Wq4) + 1), v);             // .. of unit qt - 1
-            if (u8 == 3 && qt > 1) gstore(uo + (3 * (u - 2 * pl.Wq4) + 2), v);   // .. of unit qt - 2
+            gstore(uo + u8 * u, b4);                                          // rows 4 qt .. of unit qt
+            if (qt > 0) gstore(uo + (u8 * (u - pl.Wq4) + 1), b4);             // .. of unit qt - 1
+            if (u8 == 3 && qt > 1) gstore(uo + (3 * (u - 2 * pl.Wq4) + 2), b4);   // .. of unit qt - 2
         }
+        if (over && job.negflag) gstore(job.negflag, job.pgen);
         return;
     }
     // one 16-byte store of 8 consecutive superblocks of a sub-phase row per
@@ -1182,29 +1207,29 @@ __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ j
         if (threadIdx.x == 0 && zprev != (anynz ? 0u : 1u)) *zw = anynz ? 0u : 1u;
     }
     if (!live) return;
-    u64* __restrict__ uo = (u64*)job.super + (long long)g.unit8 * p * g.pstrideO;
+    // 8-bit units of unit8 dwords: a quad's 4 rows are dword 0 of unit qt,
+    // dword 1 of unit qt - 1 (and dword 2 of unit qt - 2)
+    unsigned* __restrict__ uo = (unsigned*)job.super + (long long)g.unit8 * p * g.pstrideO;
     const int u8 = g.unit8;
+    bool over = false;
 #pragma unroll
     for (int cy = 0; cy < 4; ++cy) {
 #pragma unroll
         for (int cx = 0; cx < 4; ++cx) {
-            u64 h[NQ];
+            unsigned h[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                h[q] = 0;
+                u64 hh = 0;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const unsigned wv = (cx < 2) ? vlo[16 * q + 4 * i + cy] : vhi[16 * q + 4 * i + cy];
-                    h[q] |= (u64)((cx & 1) ? (wv >> 16) : (wv & 0xFFFFu)) << (16 * i);
+                    hh |= (u64)((cx & 1) ? (wv >> 16) : (wv & 0xFFFFu)) << (16 * i);
                 }
+                h[q] = quad_u8(hh, over);
             }
             const long long u = (cy * 4 + cx) * g.subO + (long long)qt * g.Wq4 + X4;
-            if constexpr (NQ == 2) {   // unit qt whole (16-byte units)
-                typedef unsigned long long u64v2 __attribute__((ext_vector_type(2)));
-                u64v2 v;
-                v.x = h[0];
-                v.y = h[1];
-                gstore((u64v2*)(uo + 2 * u), v);
+            if constexpr (NQ == 2) {   // unit qt whole (8-row units)
+                gstore((u64*)(uo + 2 * u), (u64)h[0] | ((u64)h[1] << 32));
             } else {
                 gstore(uo + u8 * u, h[0]);                                          // rows 4 qt .. of unit qt
                 if (qt > 0) gstore(uo + (u8 * (u - g.Wq4) + 1), h[0]);              // .. of unit qt - 1
@@ -1212,6 +1237,7 @@ __global__ __launch_bounds__(256) void k_super_hv(const PlaneJob* __restrict__ j
             }
         }
     }
+    if (over && job.negflag) gstore(job.negflag, job.pgen);
 }
 
 // k_super: one workgroup (kSupWaves waves) per (chunk of superblocks, search
@@ -1319,29 +1345,25 @@ constexpr int oct_pipe() { return NR > 5 ? LGS_OCT_PIPE9 : LGS_OCT_PIPE5; }
 // entries past the staged superblock-base row that k_super_oct's batched
 // row reads may touch (64 beam slots x the deepest pipeline)
 constexpr int kOctRowPad = 64 * (LGS_OCT_PIPE5 > LGS_OCT_PIPE9 ? LGS_OCT_PIPE5 : LGS_OCT_PIPE9);
-__device__ __forceinline__ float h16(unsigned long long bits)
-{
-    return (float)__builtin_bit_cast(SuperT, (unsigned short)(bits & 0xFFFFu));
-}
 // NR = the superblock rows a lane sums per beam: 5 (nsby <= 5: the beam's
 // rows sit in one unit) or 9 (nsby <= 9: one unit + the high half of the next
 // unit, rows 4q + 8 .. 4q + 11).
 // U8: the unit size in 8-byte words (2: 16-byte units, 3: 24-byte units whose
 // third word holds rows 4q + 8 .. 4q + 11, read with the first two at once)
-typedef unsigned long long u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
 template <int NR, int U8>
 __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const double* __restrict__ zero, DevTs dts)
 {
+    static_assert((NR == 5 && U8 == 2) || (NR == 9 && U8 == 3), "8-bit units: 8 rows for 5-row windows, 12 for 9");
     const DtsScope dts_scope(dts);
     const Blk wg = xcd_block();
     const MatchItem& it = items[wg.z];
     const RtcsmPlan& pl = it.pl;
     if (wg.y >= pl.T) return;   // past this item's angles (uniform)
-    const u64x2* __restrict__ units = (const u64x2*)it.super;
-    const u64x2* __restrict__ z2 = (const u64x2*)zero;
-    const unsigned long long* __restrict__ hi8 = (const unsigned long long*)it.super;   // unit words
-    extern __shared__ int srow[];   // [Nv]
-    __shared__ double part[kSupWaves][64][NR];
+    typedef unsigned long long u64;
+    const unsigned* __restrict__ ub = (const unsigned*)it.super;   // 8-bit units of U8 dwords
+    const unsigned* __restrict__ z4 = (const unsigned*)zero;
+    extern __shared__ int srow[];   // [Nv + kOctRowPad]
+    __shared__ int part[kSupWaves][64][NR];
     const int t = wg.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nsbx = pl.nsbx, nsb2 = nsbx * pl.nsby;
@@ -1359,17 +1381,17 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
     const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
     const int* row = srow + lo;
     const int nq = (cnt + nb - 1) / nb;     // slot q takes beams nb i + q
-    const long long wq4 = pl.Wq4;
-    // fp32 partial sums of the fp16 values (exact conversions; the rounding
-    // of up to Nv nonnegative fp32 additions is covered by the bound's
-    // factor m32 below)
-    float sr[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) sr[r] = 0.0f;
+    // exact integer sums of the 8-bit values, SWAR: two u64 of four 16-bit
+    // fields, window rows (0, 2, 4, 6) and (1, 3, 5, 7), + row 8 (NR = 9).
+    // A lane sums at most ceil(Nv / (kSupWaves nb)) <= 74 beams (Nv <= 2048 on
+    // the pruned path, nb >= 7): <= 74 x 255 < 2^16, no field overflows.
+    constexpr u64 kM = 0x00FF00FF00FF00FFull;
+    u64 ae = 0, ao = 0;
+    unsigned a8 = 0;
     constexpr int kOctPipe = oct_pipe<NR>();
     for (int i0 = 0; i0 < nq; i0 += kOctPipe) {
-        u64x2 x[kOctPipe];
-        unsigned long long y[kOctPipe];
+        u64 x[kOctPipe];
+        unsigned y[kOctPipe];
         int sh[kOctPipe];
         // the batch's row entries first, unconditionally (the LDS row is
         // padded by kOctRowPad entries): one LDS wait per batch instead of
@@ -1382,60 +1404,56 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
             const int v = nb * (i0 + j) + q;
             const bool ok = act && v < cnt;
             const int c = ok ? cv[j] : 0;
-            sh[j] = 16 * (c & 3);
-            const long long u = (long long)(c >> 2) + a;
-            typedef const __attribute__((address_space(1))) u64x2a8 gu64x2a8_t;
-            typedef const __attribute__((address_space(1))) u64x2 gu64x2_t;
-            typedef const __attribute__((address_space(1))) unsigned long long gu64c_t;
-            if constexpr (U8 == 3) {   // one contiguous 24-byte unit: rows 4q .. 4q + 11
-                const u64x2a8 t = *(gu64x2a8_t*)(ok ? hi8 + 3 * u : (const unsigned long long*)z2);
-                x[j].x = t.x;
-                x[j].y = t.y;
-                y[j] = ok ? *(gu64c_t*)(hi8 + 3 * u + 2) : 0ull;
-            } else {
-                x[j] = *(gu64x2_t*)(ok ? units + u : z2);
-                if constexpr (NR > 5) y[j] = ok ? *(gu64c_t*)(hi8 + 2 * (u + wq4) + 1) : 0ull;
+            sh[j] = 8 * (c & 3);                      // the window's first row in the unit
+            const unsigned* pu = ok ? ub + (size_t)U8 * (size_t)((c >> 2) + a) : z4;
+            if constexpr (U8 == 2) {   // one 8-byte unit: rows 4q .. 4q + 7
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                typedef const __attribute__((address_space(1))) u32x2 gu32x2_t;
+                const u32x2 d = *(gu32x2_t*)pu;
+                x[j] = (u64)d.x | ((u64)d.y << 32);
+                y[j] = 0u;
+            } else {                   // one 12-byte unit: rows 4q .. 4q + 11
+                typedef unsigned u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+                typedef const __attribute__((address_space(1))) u32x3 gu32x3_t;
+                const u32x3 d = *(gu32x3_t*)pu;
+                x[j] = (u64)d.x | ((u64)d.y << 32);
+                y[j] = d.z;
             }
         }
 #pragma unroll
         for (int j = 0; j < kOctPipe; ++j) {
             const int k = sh[j];
-            // rows 0..3 of the beam's window from bits k.. of (x.x, x.y, y);
-            // (x.y << (63 - k)) << 1 is x.y << (64 - k) for k in [1, 63] and 0
-            // for k = 0: no branch on k
-            const unsigned long long w0 = (x[j].x >> k) | ((x[j].y << (63 - k)) << 1);
-            sr[0] += h16(w0);
-            sr[1] += h16(w0 >> 16);
-            sr[2] += h16(w0 >> 32);
-            sr[3] += h16(w0 >> 48);
+            u64 wl;
             if constexpr (NR == 5) {
-                sr[4] += h16(x[j].y >> k);
+                wl = (x[j] >> k) & 0xFFFFFFFFFFull;   // rows 0..4 of the window
             } else {
-                const unsigned long long w1 = (x[j].y >> k) | ((y[j] << (63 - k)) << 1);
-                sr[4] += h16(w1);
-                sr[5] += h16(w1 >> 16);
-                sr[6] += h16(w1 >> 32);
-                sr[7] += h16(w1 >> 48);
-                sr[8] += h16(y[j] >> k);
+                // rows 0..7 from bytes k/8 .. of (x, y); (y << (63 - k)) << 1 is
+                // y << (64 - k) for k > 0 and 0 for k = 0: no branch on k
+                wl = (x[j] >> k) | (((u64)y[j] << (63 - k)) << 1);
+                a8 += (y[j] >> k) & 0xFFu;          // row 8
             }
+            ae += wl & kM;
+            ao += (wl >> 8) & kM;
         }
     }
 #pragma unroll
-    for (int r = 0; r < NR; ++r) part[w][lane][r] = (double)sr[r];
+    for (int r = 0; r < NR && r < 8; ++r) part[w][lane][r] = (int)(((r & 1) ? ao : ae) >> (16 * (r >> 1)) & 0xFFFFu);
+    if constexpr (NR == 9) part[w][lane][8] = (int)a8;
     __syncthreads();
     if (w != 0) return;
     const int sbi = lane;
     const bool own = sbi < nsb2;
-    double tot = 0.0;
+    int tot = 0;   // <= Nv x 255 (Nv <= 2048 on the pruned path): exact
     if (own) {
         const int ca = sbi % nsbx, rb = sbi / nsbx;
         for (int j = 0; j < kSupWaves; ++j)
             for (int s = 0; s < nb; ++s) tot += part[j][s * nsbx + ca][rb];
     }
-    // fp32 slack: a sum of m <= Nv nonnegative fp32 terms is at least the
-    // real sum times 1 - (m - 1) 2^-24 (to first order); twice that covers it
-    const double m32 = 1.0 + 2.0 * (double)(pl.Nv + 1) * 0x1p-24;
-    const double bound = (*it.negflag == it.pgen) ? INFINITY : tot * pl.sb_mult * m32;
+    // the sum of the units / 255 >= the sum of the fp16 round-ups >= the sum
+    // of the members' coarse values; the division's rounding (<= 2^-53
+    // relative) is covered by 1 + 2^-50, the reference order by sb_mult
+    const double bound =
+        (*it.negflag == it.pgen) ? INFINITY : ((double)tot / 255.0) * (1.0 + 0x1p-50) * pl.sb_mult;
     if (own) it.sbound[(size_t)t * nsb2 + sbi] = bound;
     const bool seedable = own;   // k_seed_super skips unsafe members
     double bv = seedable ? bound : -INFINITY;
@@ -3821,13 +3839,12 @@ void set_plane_layout(RtcsmPlan& pl)
     pl.pstride4 = 16 * pl.sub4;
     LGS_REQUIRE((long long)pl.low_res * pl.low_res * pl.pstride4 < (1LL << 31),
                 "coarse map too large for 32-bit plane offsets");
-    // octet layout: one 16-byte unit holds 5 superblock rows of a beam's
-    // window (nsby <= 5), one unit + the high half of the next holds 9
+    // octet layout (8-bit units, r06): unit (q, X) holds sub-phase rows 4q ..
+    // 4q + 4 unit8 - 1 of column X, one byte each: 8 rows (unit8 = 2) hold
+    // the 5 superblock rows of a window with nsby <= 5 at any of the 4 row
+    // offsets, 12 rows (unit8 = 3) the 9 rows of nsby <= 9
     pl.oct = pl.nsbx <= 9 && pl.nsby <= 9 && pl.nsbx * pl.nsby <= 64;
-#ifndef LGS_OCT12
-#define LGS_OCT12 1
-#endif
-    pl.unit8 = (LGS_OCT12 && pl.oct && pl.nsby > 5) ? 3 : 2;
+    pl.unit8 = (pl.oct && pl.nsby > 5) ? 3 : 2;
     pl.Qo = (pl.Hq4 + 3) / 4 + 1;
     pl.subO = (long long)pl.Qo * pl.Wq4;
     pl.pstrideO = 16 * pl.subO;
@@ -4026,7 +4043,7 @@ inline size_t plane16_bytes(const RtcsmPlan& pl)
 inline size_t set_bytes(const RtcsmPlan& pl) { return plane_bytes(pl) + plane16_bytes(pl); }
 inline size_t super_bytes(const RtcsmPlan& pl)
 {
-    if (pl.oct) return align256(8 * (size_t)pl.unit8 * pl.low_res * pl.low_res * (size_t)pl.pstrideO);
+    if (pl.oct) return align256(4 * (size_t)pl.unit8 * pl.low_res * pl.low_res * (size_t)pl.pstrideO);
     return align256(sizeof(SuperT) * (size_t)pl.low_res * pl.low_res * (size_t)pl.pstride4);
 }
 double* planes_buffer(lgs_ctx* ctx, const RtcsmPlan& pl, int nsets, bool with_super)
@@ -4219,6 +4236,8 @@ SetJobs build_sets(lgs_ctx* ctx, const RtcsmPlan& lp, std::vector<PlaneSet>& set
             ps.super = j.super;
             ps.negflag = neg + s;
             ps.pgen = ctx->next_stamp();
+            j.negflag = neg + s;
+            j.pgen = ps.pgen;
         }
         if (ps.fine && precompute_planes_ok(ps.fine, lr)) {
             PrecompJob q{};
@@ -4488,10 +4507,8 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             if (ctx->skipped(K_SUPER)) {
             } else if (B.oct && B.nsby <= 5)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<5, 2>), g, dim3(64 * kSupWaves), lds, st, d_items, zero, ctx->dts(tok));
-            else if (B.oct && B.unit8 == 3)
+            else if (B.oct)   // nsby 6..9: 12-row units (set_plane_layout)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9, 3>), g, dim3(64 * kSupWaves), lds, st, d_items, zero, ctx->dts(tok));
-            else if (B.oct)
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super_oct<9, 2>), g, dim3(64 * kSupWaves), lds, st, d_items, zero, ctx->dts(tok));
             else if (B.pair)
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_super<1>), g, dim3(64 * kSupWaves), lds, st, d_items, zero);
             else

@@ -26,8 +26,8 @@ def layout(W, H, res, lr, rx, ry):
     Hqp = Hq + 2 * M
     Wq4, Hq4 = ((-(-Wqp // 4)) + 7) & ~7, -(-Hqp // 4)
     # octet layout (k_rtcsm.hip set_plane_layout) for windows of <= 9 x 9
-    # superblocks: 16-byte units (rows 4q .. 4q + 7), 24-byte units (rows
-    # 4q .. 4q + 11) for windows of more than 5 superblock rows
+    # superblocks: 8-bit units (r06) of 8 rows (4q .. 4q + 7, 8 bytes) or,
+    # for windows of more than 5 superblock rows, 12 rows (12 bytes)
     oct = nsbx <= 9 and nsby <= 9 and nsbx * nsby <= 64
     u8 = 3 if oct and nsby > 5 else 2
     Qo = (Hq4 + 3) // 4 + 1
@@ -72,25 +72,33 @@ def clamp_strip(P, lr, M):
     return Q
 
 
+def unit_u8(h):
+    """the 8-bit unit value of an fp16 round-up h (k_rtcsm.hip quad_u8):
+    ceil(255 h), exact in fp32 (h has 11 significant bits)"""
+    return np.clip(np.ceil(h.astype(np.float32) * np.float32(255.0)), 0, 255).astype(np.uint8)
+
+
 def check_super(P, S, lr, L):
-    """S (fp16, sub-phase layout) == the forward 4x4 max of every (strip-clamped)
+    """S (sub-phase layout) == the forward 4x4 max of every (strip-clamped)
     plane rounded up to fp16 (bit-exact: round-up is monotone, so the max of the
-    round-ups is the round-up of the max)"""
+    round-ups is the round-up of the max); octet layouts hold the 8-bit
+    round-up ceil(255 h) of that fp16 value"""
     Hqp, Wqp = L["Hqp"], L["Wqp"]
     pad = np.zeros((lr * lr, Hqp + 3, Wqp + 3))
     pad[:, :Hqp, :Wqp] = clamp_strip(P, lr, L["M"])
     m = np.max([pad[:, j:j + Hqp, i:i + Wqp] for j in range(4) for i in range(4)], axis=0)
     pstride4 = 16 * L["sub4"]
+    B = S.view(np.uint8)
     for p in range(lr * lr):
         got = np.zeros((Hqp, Wqp))
         for sy in range(4):
             for sx in range(4):
                 if L["oct"]:
-                    # units (q, X) of 8 halfs = rows 4q .. 4q + 7: rows from the low
-                    # halves, and every high half equals the next unit's low half
-                    h = 4 * L["u8"]   # halfs per unit
+                    # units (q, X) of 4 u8 bytes = rows 4q .. 4q + 4 u8 - 1: rows
+                    # from the first dword, and dword d equals unit q + d's first
+                    h = 4 * L["u8"]   # bytes per unit
                     o = (p * 16 + sy * 4 + sx) * L["subO"] * h
-                    u = S[o:o + L["subO"] * h].reshape(L["Qo"], L["Wq4"], h)
+                    u = B[o:o + L["subO"] * h].reshape(L["Qo"], L["Wq4"], h)
                     blk = u[:, :, :4].transpose(0, 2, 1).reshape(4 * L["Qo"], L["Wq4"])[:L["Hq4"]]
                     assert np.array_equal(u[:-2, :, 4:8], u[1:-1, :, :4]), (p, sy, sx)
                     if L["u8"] == 3:
@@ -99,7 +107,8 @@ def check_super(P, S, lr, L):
                     blk = S[p * pstride4 + (sy * 4 + sx) * L["sub4"]:][:L["sub4"]].reshape(L["Hq4"], L["Wq4"])
                 ys, xs = np.arange(sy, Hqp, 4), np.arange(sx, Wqp, 4)
                 got[np.ix_(ys, xs)] = blk[:len(ys), :len(xs)].astype(np.float64)
-        want = half_round_up(m[p]).astype(np.float64)
+        want = half_round_up(m[p])
+        want = (unit_u8(want) if L["oct"] else want).astype(np.float64)
         assert np.array_equal(got, want), (p, np.argwhere(got != want)[:4])
 
 
