@@ -219,7 +219,8 @@ def pmc_for(pmc_path, trace_kernel, workload):
                 l2_hit_rate=e.get("l2_hit_rate"), profile=os.path.relpath(pmc_path, ROOT))
 
 
-def roofline_from(stats, kernel, pmc_path, trace_kernel, bound, workload="match", bytes_scale=1.0):
+def roofline_from(stats, kernel, pmc_path, trace_kernel, bound, workload="match", bytes_scale=1.0,
+                  time_key="total_ms"):
     """Roofline of the dominant kernel: achieved = ALGORITHMIC bytes per launch
      / event-timed average launch duration; frac against the
     8 TB/s HBM peak.  frac_hbm_counters = the PMC-counted HBM bytes of the same
@@ -227,10 +228,10 @@ def roofline_from(stats, kernel, pmc_path, trace_kernel, bound, workload="match"
     bytes_scale rescales the library's per-launch accounting (k_super counts
     8 B per superblock lookup, the fp64 planes' width; the 8-bit units read 1 B)."""
     k = stats.get(kernel)
-    if not k or not k["launches"] or not k["algo_bytes"]:
+    if not k or not k["launches"] or not k["algo_bytes"] or not k.get(time_key):
         return None
     per_launch = bytes_scale * k["algo_bytes"] / k["launches"]
-    avg_ms = k["total_ms"] / k["launches"]
+    avg_ms = k[time_key] / k["launches"]
     achieved = per_launch / (avg_ms * 1e-3) / 1e9
     p = pmc_for(pmc_path, trace_kernel, workload)
     traffic = round(p["traffic"]) if p else None
@@ -542,7 +543,7 @@ def run_match(args, D, ctx):
     stats = {}
     for c, _, _ in state:            # k_coarse launches of every stream, event-timed on their own streams
         for k, v in c.kernel_stats().items():
-            a = stats.setdefault(k, dict(launches=0, total_ms=0.0, algo_bytes=0.0))
+            a = stats.setdefault(k, dict(launches=0, total_ms=0.0, algo_bytes=0.0, dispatch_ms=0.0))
             for f in a:
                 a[f] += v[f]
     # single-stream latency and the per-kernel table: a separate, fully
@@ -626,6 +627,13 @@ def run_match(args, D, ctx):
         # 8-bit superblock units, r06), timed the same way
         roofline_super=roofline_from(stats, "k_super", args.pmc, "k_super_oct<5, 2>", "l2-gather",
                                      bytes_scale=0.125),
+        # the same launches dispatch-inclusive: from the end of the chunk's
+        # previous launch on the stream (k_keep) to the kernel's end, what a
+        # stream event and rocprofv3's dispatch duration count (the execution
+        # plus the wait for CUs held by the other streams' kernels):
+        # tools/trace_coarse.py's "timed" group of the committed trace
+        roofline_dispatch=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather",
+                                        time_key="dispatch_ms") if args.device_timing else None,
         timing=("device: s_memrealtime span of each launch (LGS_OPT_DEVICE_TIMING)" if args.device_timing
                 else "HIP events on each launch's stream"),
         timed_region_kernels=trk, largest_kernel=top,

@@ -217,12 +217,19 @@ int  lgs_debug_copy_counters(const lgs_ctx* ctx, long long* direct, long long* s
 
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is
  * the algorithmic byte count of DESIGN.md §Roofline (e.g. 8 B per coarse-score
- * lookup), summed over launches; total_ms sums hipEventElapsedTime. */
+ * lookup), summed over launches; total_ms sums hipEventElapsedTime, or with
+ * LGS_OPT_DEVICE_TIMING each launch's execution span (first workgroup start to
+ * last workgroup end); dispatch_ms (device timing only, else = total_ms) sums
+ * the span from the end of the chunk's previous device-timed launch on the
+ * same stream to the launch's end -- what a stream event or a rocprofv3
+ * dispatch duration counts: the execution plus the wait for CUs held by other
+ * streams' kernels (r06). */
 typedef struct {
     char name[32];
     int64_t launches;
     double total_ms;
     double algo_bytes;
+    double dispatch_ms;
 } lgs_kernel_stat;
 int  lgs_ctx_kernel_stats(lgs_ctx* ctx, lgs_kernel_stat* out, int cap);  /* returns count (>=0) or -status */
 int  lgs_ctx_reset_stats(lgs_ctx* ctx);

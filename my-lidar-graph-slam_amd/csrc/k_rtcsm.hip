@@ -2335,6 +2335,9 @@ __device__ __forceinline__ double seed_fine(const RtcsmPlan& pl, const double* _
 // (tools/diag_seed.py): a third of the queries then scored ~4.5x the coarse
 // blocks.  Sixteen candidates cost member sums, not fine scores.
 constexpr int kSeedMembersThreads = 256;
+#ifndef LGS_SEED2_THREADS
+#define LGS_SEED2_THREADS 1024   // k_seed_super<2> workgroup (MODE 2 takes any multiple of 64 up to 1024)
+#endif
 constexpr int kSeedWideMaxParts = 1024;   // parts held in one wave's registers (larger searches: block rounds)
 // Candidate b of the seed, by one whole wave: the parts in registers (16 per
 // lane), b + 1 rounds of a wave argmax, each taking the best part out (the
@@ -3207,6 +3210,16 @@ __global__ __launch_bounds__(64) void k_replay(Items items, DevTs dts)
 // --------------------------------------------------------------------------
 constexpr int kCostThreads = 1024;
 constexpr int kCostLdsTerms = 8192;
+// dynamic LDS of a k_cost launch: the terms of its largest item (r06: a
+// static 64 KB array held two workgroups per CU and made the 7 x n
+// workgroups wait for whole CUs under other streams' work)
+template <class V>
+inline size_t cost_lds(const V& items)
+{
+    int n = 1;
+    for (const auto& it : items) n = std::max(n, it.cp.N);
+    return sizeof(double) * (size_t)std::min(n, kCostLdsTerms);
+}
 
 __device__ __forceinline__ double gval(const CostPlan& cp, const double* __restrict__ g, int x,
                                        int y)
@@ -3278,7 +3291,7 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(Items items, int guard_ca
     double* __restrict__ gterms = it.terms;
     RtcsmRecord* rec = it.rec;
     const int gen = it.gen;
-    __shared__ double lterms[kCostLdsTerms];
+    extern __shared__ double lterms[];   // [min(max N of the launch, kCostLdsTerms)] (cost_lds)
     const int pi = blockIdx.x;
     const bool in_lds = cp.N <= kCostLdsTerms;
     double* __restrict__ tm = in_lds ? lterms : gterms + (size_t)pi * cp.N;
@@ -4386,8 +4399,8 @@ void enqueue_cost_patches(lgs_ctx* ctx, const BatchShape& B, Items d_items, cons
                                  hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, st, items[0].cidx, dp, np);
     LGS_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, 1), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
-                       ctx->guard_eps, 0, 1, DevTs{});
+    hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, 1), dim3(kCostThreads), cost_lds(items), st, d_items,
+                       ctx->guard_cap, ctx->guard_eps, 0, 1, DevTs{});
     LGS_HIP_CHECK(hipGetLastError());
 }
 
@@ -4453,7 +4466,8 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
         for (auto& it : items) nbeams += it.cp.N;
         const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * nbeams);
         if (!ctx->skipped(K_COST))
-            hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, n), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
+            hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, n), dim3(kCostThreads), cost_lds(items), st, d_items,
+                               ctx->guard_cap,
                                ctx->guard_eps, inject, 0, ctx->dts(tok_));
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
@@ -4529,7 +4543,7 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
             if (!ctx->skipped(K_SEED) && wide) {
                 hipLaunchKernelGGL(k_seed_members, dim3(nwide, n), dim3(kSeedMembersThreads),
                                    sizeof(int) * (size_t)std::max(B.NvMax, 1), st, d_items, ctx->dts(tok));
-                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_seed_super<2>), dim3(kSeedCands, n), dim3(1024), lds, st,
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_seed_super<2>), dim3(kSeedCands, n), dim3(LGS_SEED2_THREADS), lds, st,
                                    d_items, zero, ctx->dts(tok));
             } else if (!ctx->skipped(K_SEED))
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_seed_super<0>), dim3(kSeedCands, n), dim3(1024), lds, st,
@@ -4643,7 +4657,8 @@ void enqueue_items(lgs_ctx* ctx, const BatchShape& B, Items d_items, const std::
     {
         const int tok_ = ctx->timing_begin(K_COST, 8.0 * 7.0 * 2.0 * kk * nbeams);
         if (!ctx->skipped(K_COST))
-            hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, n), dim3(kCostThreads), 0, st, d_items, ctx->guard_cap,
+            hipLaunchKernelGGL(KCOST(B.kernel_size), dim3(7, n), dim3(kCostThreads), cost_lds(items), st, d_items,
+                               ctx->guard_cap,
                                ctx->guard_eps, inject, 0, ctx->dts(tok_));
         ctx->timing_end(tok_);
         LGS_HIP_CHECK(hipGetLastError());
@@ -5338,7 +5353,8 @@ void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params
     up.copy();
     Items d_items = up.at<MatchItem>(ioff);
     const int ks = cost->kernel_size;
-    hipLaunchKernelGGL(KCOST(ks), dim3(7, n), dim3(kCostThreads), 0, ctx->stream, d_items, ctx->guard_cap,
+    hipLaunchKernelGGL(KCOST(ks), dim3(7, n), dim3(kCostThreads), cost_lds(items), ctx->stream, d_items,
+                       ctx->guard_cap,
                        ctx->guard_eps, ctx->inject_index ? 1 : 0, 0, DevTs{});
     LGS_HIP_CHECK(hipGetLastError());
     LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
@@ -5371,7 +5387,7 @@ void cost_summaries(lgs_ctx* ctx, const lgs_grid* grid, const lgs_cost_ge_params
                                          ctx->stream));
             if (np) hipLaunchKernelGGL(k_cost_patch, dim3((np + 255) / 256), dim3(256), 0, ctx->stream,
                                        items[j].cidx, dp, np);
-            hipLaunchKernelGGL(KCOST(ks), dim3(7, 1), dim3(kCostThreads), 0, ctx->stream, d_items + j,
+            hipLaunchKernelGGL(KCOST(ks), dim3(7, 1), dim3(kCostThreads), cost_lds(items), ctx->stream, d_items + j,
                                ctx->guard_cap, ctx->guard_eps, 0, 1, DevTs{});
             LGS_HIP_CHECK(hipGetLastError());
             LGS_HIP_CHECK(hipMemcpyAsync(&h_rec[j], d_rec + j, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
@@ -5587,7 +5603,8 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
         const size_t off = up.append(&it, 1);
         up.flush();
         Items d_items = up.at<MatchItem>(off);
-        hipLaunchKernelGGL(KCOST(cp.kernel_size), dim3(1, 1), dim3(kCostThreads), 0, ctx->stream, d_items,
+        hipLaunchKernelGGL(KCOST(cp.kernel_size), dim3(1, 1), dim3(kCostThreads), cost_lds(std::vector<MatchItem>{ it }),
+                           ctx->stream, d_items,
                            ctx->guard_cap, ctx->guard_eps, 0, 0, DevTs{});
         LGS_HIP_CHECK(hipGetLastError());
         LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,
@@ -5605,7 +5622,8 @@ extern "C" int lgs_cost_greedy_endpoint(lgs_ctx* ctx, const lgs_grid* grid,
             }
             LGS_HIP_CHECK(hipMemcpyAsync(it.cidx, row.data(), sizeof(int4) * row.size(),
                                          hipMemcpyHostToDevice, ctx->stream));
-            hipLaunchKernelGGL(KCOST(cp.kernel_size), dim3(1, 1), dim3(kCostThreads), 0, ctx->stream, d_items,
+            hipLaunchKernelGGL(KCOST(cp.kernel_size), dim3(1, 1), dim3(kCostThreads), cost_lds(std::vector<MatchItem>{ it }),
+                           ctx->stream, d_items,
                                ctx->guard_cap, ctx->guard_eps, 0, 1, DevTs{});
             LGS_HIP_CHECK(hipGetLastError());
             LGS_HIP_CHECK(hipMemcpyAsync(h_rec, d_rec, sizeof(RtcsmRecord), hipMemcpyDeviceToHost,

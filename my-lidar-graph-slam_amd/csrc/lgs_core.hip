@@ -255,8 +255,10 @@ void lgs_ctx::timing_end(int token)
 namespace {
 // A device-timed launch's span from its words' host copy (first workgroup
 // start to last workgroup end, s_memrealtime at 100 MHz); false if no
-// workgroup of this generation stamped both (e.g. a launch skipped).
-bool dts_span_ms(const PendingTiming& p, float& ms)
+// workgroup of this generation stamped both (e.g. a launch skipped).  *t0,
+// *t1: the ticks.
+bool dts_span_ms(const PendingTiming& p, float& ms, unsigned long long* t0p = nullptr,
+                 unsigned long long* t1p = nullptr)
 {
     unsigned long long t0 = ~0ull, t1 = 0;
     bool any0 = false, any1 = false;
@@ -274,6 +276,8 @@ bool dts_span_ms(const PendingTiming& p, float& ms)
     }
     if (!any0 || !any1 || t1 < t0) return false;   // (t1 < t0: the 40-bit clock wrapped, ~3 h)
     ms = (float)((double)(t1 - t0) * 1e-5);
+    if (t0p) *t0p = t0;
+    if (t1p) *t1p = t1;
     return true;
 }
 }  // namespace
@@ -286,20 +290,30 @@ void lgs_ctx::harvest()
 void lgs_ctx::harvest_upto(long long b)
 {
     size_t k = 0;
+    long long prev_batch = -1;
+    unsigned long long prev_end = 0;   // the end tick of the chunk's previous device-timed launch
     for (; k < pending.size() && pending[k].batch <= b; ++k) {
         PendingTiming& p = pending[k];
         float ms = 0.f;
+        double disp = 0.0;
         if (p.hw) {
-            if (!dts_span_ms(p, ms)) continue;
+            unsigned long long t0 = 0, t1 = 0;
+            if (!dts_span_ms(p, ms, &t0, &t1)) continue;
+            const bool chained = prev_batch == p.batch && prev_end <= t1 && prev_end != 0;
+            disp = chained ? (double)(t1 - std::min(prev_end, t0)) * 1e-5 : (double)ms;
+            prev_batch = p.batch;
+            prev_end = t1;
         } else {
             LGS_HIP_CHECK(hipEventSynchronize(p.b));
             LGS_HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
             event_pool.push_back(p.a);
             event_pool.push_back(p.b);
+            disp = ms;
         }
         stat_launches[p.kernel] += 1;
         stat_ms[p.kernel] += ms;
         stat_bytes[p.kernel] += p.algo_bytes;
+        stat_disp_ms[p.kernel] += disp;
     }
     pending.erase(pending.begin(), pending.begin() + (long)k);
 }
@@ -442,6 +456,7 @@ extern "C" int lgs_ctx_kernel_stats(lgs_ctx* ctx, lgs_kernel_stat* out, int cap)
             out[n].launches = ctx->stat_launches[k];
             out[n].total_ms = ctx->stat_ms[k];
             out[n].algo_bytes = ctx->stat_bytes[k];
+            out[n].dispatch_ms = ctx->stat_disp_ms[k];
         }
         ++n;
     }
@@ -458,6 +473,7 @@ extern "C" int lgs_ctx_reset_stats(lgs_ctx* ctx)
             ctx->stat_launches[k] = 0;
             ctx->stat_ms[k] = 0;
             ctx->stat_bytes[k] = 0;
+            ctx->stat_disp_ms[k] = 0;
         }
         ctx->count_matches = ctx->count_coarse_blocks = ctx->count_coarse_blocks_dense = ctx->count_pruned = 0;
     });

@@ -438,6 +438,7 @@ struct lgs_ctx {
     int64_t stat_launches[lgs::K_NUM_KERNELS] = {};
     double stat_ms[lgs::K_NUM_KERNELS] = {};
     double stat_bytes[lgs::K_NUM_KERNELS] = {};
+    double stat_disp_ms[lgs::K_NUM_KERNELS] = {};   // device timing: from the previous launch's end (lgs_kernel_stat)
     // correlative matches since the last lgs_ctx_reset_stats (lgs_ctx_match_counters)
     int64_t count_matches = 0, count_coarse_blocks = 0, count_coarse_blocks_dense = 0, count_pruned = 0;
 

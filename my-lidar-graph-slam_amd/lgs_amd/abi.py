@@ -172,7 +172,7 @@ LOOP_RESULT_DOUBLES = 22   # sizeof(lgs_loop_result) / 8
 
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double),
-                ("algo_bytes", C.c_double)]
+                ("algo_bytes", C.c_double), ("dispatch_ms", C.c_double)]
 
 
 # (name, restype, argtypes) for every symbol of include/lgs_hip.h
@@ -335,7 +335,8 @@ class Context:
         if n < 0:
             self.check(-n, "kernel_stats")
         return {buf[i].name.decode(): dict(launches=buf[i].launches, total_ms=buf[i].total_ms,
-                                           algo_bytes=buf[i].algo_bytes) for i in range(n)}
+                                           algo_bytes=buf[i].algo_bytes, dispatch_ms=buf[i].dispatch_ms)
+                for i in range(n)}
 
     def reset_stats(self):
         self.check(self.lib.lgs_ctx_reset_stats(self.h), "reset_stats")
