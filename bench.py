@@ -283,7 +283,7 @@ def set_timed_events(ctx, args, dominant, extra=(), chunk_kernels=False):
 
 
 # the launched kernel(s) behind each timing id of a config-2 chunk (rocprofv3 names)
-TRACE_NAMES = dict(k_project="k_project<16>", k_super="k_super_oct<5, 2>", k_seed="k_seed_members + k_seed_super<2>",
+TRACE_NAMES = dict(k_project="k_beams (lean batches; k_project<16> materialises)", k_super="k_super_oct<5, 2>", k_seed="k_seed_members + k_seed_super<2>",
                    k_coarse_aux="k_keep + k_unsafe_list", k_coarse="k_coarse_list_c", k_select="k_select<256>",
                    k_fine="k_fine_regs", k_replay="k_replay", k_cost="k_cost<1>",
                    k_precompute="k_precompute_planes<5, 8>", k_super_planes="k_super_hv<1>")

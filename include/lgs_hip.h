@@ -215,6 +215,15 @@ int  lgs_debug_keysort(lgs_ctx* ctx, const unsigned* keys, unsigned* out, long l
  * access over xGMI) and staged through pinned host memory. */
 int  lgs_debug_copy_counters(const lgs_ctx* ctx, long long* direct, long long* staged);
 
+/* Diagnostics, checked build only (liblgs_hip_checked.so, compiled with
+ * LGS_CHECK_OFFSETS): the correlative consumers test every
+ * coarse / superblock plane offset they form or read against its padded
+ * plane.  out[0] = offsets checked, out[1] = violations, out[2] = the first
+ * violation (kind << 60 | angle << 32 | beam; kind 1 coarse, 2 superblock),
+ * out[3] = its offset; since the last reset (reset != 0 zeroes them after
+ * the read).  The product build returns LGS_ERR_INVALID_ARG (no checks). */
+int  lgs_debug_offset_checks(lgs_ctx* ctx, int reset, unsigned long long* out);
+
 /* Per-kernel statistics gathered while LGS_OPT_PROFILE is on.  algo_bytes is
  * the algorithmic byte count of DESIGN.md §Roofline (e.g. 8 B per coarse-score
  * lookup), summed over launches; total_ms sums hipEventElapsedTime, or with

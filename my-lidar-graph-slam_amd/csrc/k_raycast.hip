@@ -1992,6 +1992,7 @@ struct StepTiming {
     bool on = std::getenv("LGS_STEP_TIMING") != nullptr;
     std::chrono::steady_clock::time_point prev;
     double us[8] = {};
+    double keys = 0, rays = 0, longq = 0;
     long long steps = 0;
     void start()
     {
@@ -2008,9 +2009,11 @@ struct StepTiming {
     {
         if (!on || ++steps % 500) return;
         std::fprintf(stderr, "latest step host us: finish %.1f hits %.1f geom %.1f pre %.1f rays(latest) %.1f "
-                     "rays(local)+shift %.1f stage %.1f launch %.1f\n", us[0] / 500, us[1] / 500, us[2] / 500,
-                     us[6] / 500, us[7] / 500, us[3] / 500, us[4] / 500, us[5] / 500);
+                     "rays(local)+shift %.1f stage %.1f launch %.1f; keys %.0f rays %.0f L-keys %.0f\n", us[0] / 500,
+                     us[1] / 500, us[2] / 500, us[6] / 500, us[7] / 500, us[3] / 500, us[4] / 500, us[5] / 500,
+                     keys / 500, rays / 500, longq / 500);
         for (double& u : us) u = 0;
+        keys = rays = longq = 0;
     }
 };
 StepTiming& step_timing()
@@ -2165,6 +2168,7 @@ void latest_step(lgs_ctx* ctx, LatestCache& C, lgs_map* latest, lgs_map* local, 
                            nw, buf->hit2, buf->miss2, buf->end2);
     }
     const long long nthreads = nE + nloc + nL;
+    if (tm.on) tm.keys += (double)keys, tm.rays += (double)nr, tm.longq += (double)nL;
     const LongList ll{ C.d_long, C.d_long + 2 };
     if (nthreads > 0) {
         hipLaunchKernelGGL(k_apply_window, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, st,

@@ -295,6 +295,59 @@ __device__ __forceinline__ int super_base_l(const BeamLattice& b, const RtcsmPla
                    : 0;
 }
 
+// Checked build (LGS_CHECK_OFFSETS: liblgs_hip_checked.so, VERDICT r05 item
+// 5): the consumers test every coarse / superblock base they form or read
+// against its padded plane before using it -- the window a base opens must
+// lie inside one plane (coarse: ncx x ncy cells from the base; superblock:
+// nsbx units from the base's unit).  Checks are counted per wave; a
+// violation is counted and the first one kept (kind << 60 | t << 32 | v, base),
+// read back by lgs_debug_offset_checks.  Round 5's "nowrite" variant read
+// unwritten rows as bases and faulted: such a row would
+// land here as a counted violation, not as an illegal address.
+#ifdef LGS_CHECK_OFFSETS
+__device__ unsigned long long g_offchk[4];   // checked, violations, first (kind|t|v), first base
+__device__ __forceinline__ void offchk_note(bool ok, int kind, int t, int v, long long base)
+{
+    const unsigned long long act = __ballot(1), bad = __ballot(!ok);
+    const int lane = (int)__lane_id();
+    if (lane == __ffsll((long long)act) - 1) {
+        atomicAdd(&g_offchk[0], (unsigned long long)__popcll(act));
+        if (bad) atomicAdd(&g_offchk[1], (unsigned long long)__popcll(bad));
+    }
+    if (!ok && atomicCAS(&g_offchk[2], 0ull,
+                         ((unsigned long long)kind << 60) | ((unsigned long long)(unsigned)t << 32) | (unsigned)v) == 0ull)
+        g_offchk[3] = (unsigned long long)base;
+}
+__device__ __forceinline__ void chk_coarse(const RtcsmPlan& pl, int b, int t, int v)
+{
+    const long long all = (long long)pl.low_res * pl.low_res * pl.pstride;
+    bool ok = b >= 0 && b < all;
+    if (ok) {
+        const long long o = b % pl.pstride;
+        ok = o / pl.Wqp + pl.ncy <= pl.Hqp && o % pl.Wqp + pl.ncx <= pl.Wqp;
+    }
+    offchk_note(ok, 1, t, v, b);
+}
+__device__ __forceinline__ void chk_super(const RtcsmPlan& pl, int c, int t, int v)
+{
+    bool ok;
+    if (pl.oct) {
+        const long long u = (long long)(c >> 2), all = (long long)pl.low_res * pl.low_res * pl.pstrideO;
+        ok = c >= 0 && u + pl.nsbx <= all && u % pl.Wq4 + pl.nsbx <= pl.Wq4;
+    } else {
+        const long long all = (long long)pl.low_res * pl.low_res * pl.pstride4;
+        ok = c >= 0 && (long long)c + (long long)(pl.nsby - 1) * pl.Wq4 + pl.nsbx <= all &&
+             c % pl.Wq4 + pl.nsbx <= pl.Wq4;
+    }
+    offchk_note(ok, 2, t, v, c);
+}
+#define LGS_CHK_COARSE(pl, b, t, v) chk_coarse(pl, b, t, v)
+#define LGS_CHK_SUPER(pl, c, t, v) chk_super(pl, c, t, v)
+#else
+#define LGS_CHK_COARSE(pl, b, t, v) ((void)0)
+#define LGS_CHK_SUPER(pl, c, t, v) ((void)0)
+#endif
+
 __device__ __forceinline__ int coarse_base(int ix, int iy, const RtcsmPlan& pl)
 {
     return coarse_base_l(beam_lattice(ix, iy, pl, 1.0 / pl.low_res), pl);
@@ -570,6 +623,7 @@ __device__ __forceinline__ void lean_super_row(const MatchItem& it, int t, int* 
             ix += it.inject;
         }
         srow[v] = super_base_l(beam_lattice(ix, iy, pl, inv_lr), pl);
+        LGS_CHK_SUPER(pl, srow[v], t, v);
         edge |= (ix - pl.win_x < 0 || iy - pl.win_y < 0) ? 1 : 0;
     }
     // this angle has a beam whose coarse lattice starts left of / below the
@@ -651,9 +705,16 @@ __device__ __forceinline__ void stage_cbase_row(int* dst, const MatchItem& it, i
 {
     if (!it.lean) {
         stage_lds(dst, it.cbase + (size_t)t * it.pl.Nv, n);
+#ifdef LGS_CHECK_OFFSETS
+        __syncthreads();
+        for (int v = threadIdx.x; v < n; v += blockDim.x) LGS_CHK_COARSE(it.pl, dst[v], t, v);
+#endif
         return;
     }
-    for (int v = threadIdx.x; v < n; v += blockDim.x) dst[v] = lean_coarse_base(it, t, v);
+    for (int v = threadIdx.x; v < n; v += blockDim.x) {
+        dst[v] = lean_coarse_base(it, t, v);
+        LGS_CHK_COARSE(it.pl, dst[v], t, v);
+    }
 }
 __device__ __forceinline__ void stage_idx_row(int2* dst, const MatchItem& it, int t, int n)
 {
@@ -901,6 +962,10 @@ __global__ __launch_bounds__(1024) void k_coarse(Items items, const double* __re
     const size_t o = (size_t)tt * pl.Nv;
     const int2* __restrict__ id = idx + o;
     const int* __restrict__ cb = cbase + o;
+#ifdef LGS_CHECK_OFFSETS
+    if (blockIdx.x == 0)
+        for (int v = threadIdx.x; v < pl.Nv; v += blockDim.x) LGS_CHK_COARSE(pl, cb[v], tt, v);
+#endif
 
     const double* __restrict__ lane_base = cmap + (jy * pl.Wqp + jx);
     const double sum =
@@ -1281,6 +1346,9 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super(Items items, const dou
     const int* __restrict__ cbrow = cbase + pl.sb_off + (size_t)t * pl.Nv;
     stage_lds(srow, cbrow, pl.Nv);
     __syncthreads();
+#ifdef LGS_CHECK_OFFSETS
+    for (int v = threadIdx.x; v < pl.Nv; v += blockDim.x) LGS_CHK_SUPER(pl, srow[v], t, v);
+#endif
     LGS_PROBE_MARK();
     const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
     const int lo = min(w * per, pl.Nv), cnt = min(per, pl.Nv - lo);
@@ -1375,6 +1443,10 @@ __global__ __launch_bounds__(64 * kSupWaves) void k_super_oct(Items items, const
     } else {
         const int* __restrict__ cbrow = it.cbase + pl.sb_off + (size_t)t * pl.Nv;
         stage_lds(srow, cbrow, pl.Nv);
+#ifdef LGS_CHECK_OFFSETS
+        __syncthreads();
+        for (int v = threadIdx.x; v < pl.Nv; v += blockDim.x) LGS_CHK_SUPER(pl, srow[v], t, v);
+#endif
     }
     __syncthreads();
     const int per = (pl.Nv + kSupWaves - 1) / kSupWaves;
@@ -1561,6 +1633,9 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_coarse_rows(Items items, con
     double* ring = (double*)(smem + srow_bytes) + (size_t)w * kRing * 128;   // [kRing][32 beams][4 blocks]
     stage_lds(srow, cbase + (size_t)t * Nv, Nv);
     __syncthreads();
+#ifdef LGS_CHECK_OFFSETS
+    for (int v = threadIdx.x; v < Nv; v += blockDim.x) LGS_CHK_COARSE(pl, srow[v], t, v);
+#endif
     LGS_PROBE_MARK();
     // gather lane: beam lane / 2 of the instruction's 32, blocks 2 (lane % 2)
     // and + 1 of the patch row; adder lane c < 4: block c of the patch row
@@ -1918,6 +1993,19 @@ __global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, i
                     pre[q][i] = v < nq ? gload(row + v) : kOff;   // past a row: the zero cell
                 }
             }
+#ifdef LGS_CHECK_OFFSETS
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int jq = __builtin_amdgcn_readfirstlane(__shfl(j, 16 * q, 64));
+                const int tq = __builtin_amdgcn_readfirstlane(__shfl(t, 16 * q, 64));
+                const int nq = __shfl(Nv, 16 * q, 64);
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int v = v0 + lane + 64 * i;
+                    if (v < nq) LGS_CHK_COARSE(items[jq].pl, pre[q][i], tq, v);
+                }
+            }
+#endif
         };
         fetch_chunk(0);
         double sum = 0.0;
@@ -5924,6 +6012,25 @@ extern "C" int lgs_loop_detect_rtcsm_multi(lgs_ctx* const* ctxs, int num_ctx, co
         // a result's start_node_index etc. come from its query, which each
         // shard saw clipped but unchanged: nothing to remap
     });
+}
+
+extern "C" int lgs_debug_offset_checks(lgs_ctx* ctx, int reset, unsigned long long* out)
+{
+    if (!ctx || !out) return LGS_ERR_INVALID_ARG;
+#ifdef LGS_CHECK_OFFSETS
+    return guarded(ctx, [&] {
+        LGS_HIP_CHECK(hipSetDevice(ctx->device));
+        LGS_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        LGS_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_offchk), sizeof(unsigned long long) * 4));
+        if (reset) {
+            const unsigned long long z[4] = { 0, 0, 0, 0 };
+            LGS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_offchk), z, sizeof(z)));
+        }
+    });
+#else
+    (void)reset;
+    return LGS_ERR_INVALID_ARG;   // product build: no checks compiled in
+#endif
 }
 
 extern "C" int lgs_debug_copy_counters(const lgs_ctx* ctx, long long* direct, long long* staged)

@@ -269,6 +269,7 @@ _PROTOS = [
     ("lgs_debug_keysort", C.c_int, [_P, _P, _P, C.c_longlong, C.c_int, C.c_int]),
     ("lgs_debug_map_rebuilds", C.c_int, [_P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     ("lgs_debug_copy_counters", C.c_int, [_P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
+    ("lgs_debug_offset_checks", C.c_int, [_P, C.c_int, C.POINTER(C.c_ulonglong)]),
     ("lgs_debug_item_buffer", C.c_int, [_P, C.c_int, C.c_int, _P, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("lgs_debug_libm", C.c_int, [_P, C.c_int, _P, C.c_int, _P]),
 ]
@@ -653,6 +654,14 @@ class Context:
         a, b = C.c_longlong(), C.c_longlong()
         self.check(self.lib.lgs_debug_copy_counters(self.h, C.byref(a), C.byref(b)), "debug_copy_counters")
         return {"direct": a.value, "staged": b.value}
+
+    def offset_checks(self, reset: bool = True) -> dict:
+        """Checked build only (liblgs_hip_checked.so): plane-offset checks and
+        violations of the correlative consumers since the last reset
+        (lgs_debug_offset_checks); raises in the product build."""
+        out = (C.c_ulonglong * 4)()
+        self.check(self.lib.lgs_debug_offset_checks(self.h, 1 if reset else 0, out), "debug_offset_checks")
+        return {"checked": out[0], "violations": out[1], "first": out[2], "first_base": out[3]}
 
     def debug_keysort(self, keys, lo: int, bits: int) -> np.ndarray:
         """Diagnostics: the K3 stable radix sort (csrc/k_sort.hip) of host u32
