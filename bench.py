@@ -220,13 +220,16 @@ def pmc_for(pmc_path, trace_kernel, workload):
 
 
 def roofline_from(stats, kernel, pmc_path, trace_kernel, bound, workload="match", bytes_scale=1.0,
-                  time_key="total_ms"):
+                  time_key="total_ms", exec_key=None):
     """Roofline of the dominant kernel: achieved = ALGORITHMIC bytes per launch
      / event-timed average launch duration; frac against the
     8 TB/s HBM peak.  frac_hbm_counters = the PMC-counted HBM bytes of the same
     kernel (from this build's profile) over the same time; null without one.
     bytes_scale rescales the library's per-launch accounting (k_super counts
-    8 B per superblock lookup, the fp64 planes' width; the 8-bit units read 1 B)."""
+    8 B per superblock lookup, the fp64 planes' width; the 8-bit units read 1 B).
+    time_key: "total_ms" (events, or the device execution span) or
+    "dispatch_ms" (device-timed, dispatch-inclusive); exec_key adds the
+    execution-span figure beside it."""
     k = stats.get(kernel)
     if not k or not k["launches"] or not k["algo_bytes"] or not k.get(time_key):
         return None
@@ -236,8 +239,12 @@ def roofline_from(stats, kernel, pmc_path, trace_kernel, bound, workload="match"
     p = pmc_for(pmc_path, trace_kernel, workload)
     traffic = round(p["traffic"]) if p else None
     frac_hbm = round(traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if p else None
+    ex = None
+    if exec_key and k.get(exec_key):
+        ex_ms = k[exec_key] / k["launches"]
+        ex = dict(avg_launch_ms=round(ex_ms, 5), frac=round(per_launch / (ex_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
     return dict(bound=bound, achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, time_basis=time_key, execution=ex,
                 frac_algorithmic=round(achieved / HBM_PEAK_GBS, 4), frac_hbm_counters=frac_hbm,
                 traffic_raw_fetch_plus_write=round(p["raw"]) if p else None,
                 l2_hit_rate=p["l2_hit_rate"] if p else None, pmc_profile=p["profile"] if p else None,
@@ -614,28 +621,29 @@ def run_match(args, D, ctx):
         p90_scan_match_ms=round(1e3 * float(np.percentile(lat1, 90)), 4) if lat1 else None,
         # latency of one batched call under the timed load
         p50_batch_call_ms=round(float(np.percentile(lat_ms, 50)), 4),
-        # the correlative-score kernel's times over the timed region (the
-        # rubric's basis: each launch shares the GPU with the other streams'
-        # kernels, so its duration includes their overlap), device-timed by
-        # default: first workgroup start to last workgroup end, what the
-        # rocprofv3 kernel trace of the same command averages;
-        # roofline_isolated is the same kernel timed alone, the one-stream
-        # pass after the timed region.  tools/trace_coarse.py splits a kernel
-        # trace of this command (dispatches overlapping no other vs the rest).
-        roofline=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"), cpu_baseline=cpu,
+        # the correlative-score kernel over the timed region (the rubric's
+        # basis), device-timed by default (LGS_OPT_DEVICE_TIMING, DESIGN.md
+        # §6): `avg_launch_ms` is dispatch-inclusive -- from the end of the
+        # chunk's previous launch on the stream (k_keep) to the kernel's last
+        # workgroup, i.e. its execution plus the wait for CUs held by the
+        # other streams' kernels, what rocprofv3's dispatch duration counts
+        # (tools/trace_coarse.py's "timed" group of the committed trace) --
+        # and `execution` is the first-workgroup-start to last-workgroup-end
+        # span of the same launches; roofline_isolated is the same kernel
+        # timed alone, the one-stream pass after the timed region (the
+        # trace's "alone" group).  Events when device timing is off.
+        roofline=(roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather", time_key="dispatch_ms",
+                                exec_key="total_ms") if args.device_timing
+                  else roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather")), cpu_baseline=cpu,
         # the superblock-bound pass (1 B per angle x superblock x beam of the
         # 8-bit superblock units, r06), timed the same way
-        roofline_super=roofline_from(stats, "k_super", args.pmc, "k_super_oct<5, 2>", "l2-gather",
-                                     bytes_scale=0.125),
-        # the same launches dispatch-inclusive: from the end of the chunk's
-        # previous launch on the stream (k_keep) to the kernel's end, what a
-        # stream event and rocprofv3's dispatch duration count (the execution
-        # plus the wait for CUs held by the other streams' kernels):
-        # tools/trace_coarse.py's "timed" group of the committed trace
-        roofline_dispatch=roofline_from(stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather",
-                                        time_key="dispatch_ms") if args.device_timing else None,
-        timing=("device: s_memrealtime span of each launch (LGS_OPT_DEVICE_TIMING)" if args.device_timing
-                else "HIP events on each launch's stream"),
+        roofline_super=(roofline_from(stats, "k_super", args.pmc, "k_super_oct<5, 2>", "l2-gather",
+                                      bytes_scale=0.125, time_key="dispatch_ms", exec_key="total_ms")
+                        if args.device_timing else
+                        roofline_from(stats, "k_super", args.pmc, "k_super_oct<5, 2>", "l2-gather", bytes_scale=0.125)),
+        timing=("device: s_memrealtime stamps of sampled workgroups per launch (LGS_OPT_DEVICE_TIMING); "
+                "avg_launch_ms dispatch-inclusive, execution = first start to last end"
+                if args.device_timing else "HIP events on each launch's stream"),
         timed_region_kernels=trk, largest_kernel=top,
         roofline_isolated=roofline_from(all_stats, "k_coarse", args.pmc, "k_coarse_list", "l2-gather"),
         coarse_stage=coarse_stage(all_stats),

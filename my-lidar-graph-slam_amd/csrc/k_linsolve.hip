@@ -594,9 +594,94 @@ struct alignas(16) SplitLds {
 // behind it); a full group is one fully unrolled block of 32 16-byte loads and
 // 64 adds, so the compiler pipelines the loads against the add chain without
 // loop-carried copies.  Returns 0 early if another wave set *abort.
+//
+// LGS_SEQ_PIPE (r06, default): the operands in a ring of four 8-term
+// register chunks (half a group).  Each chunk is reloaded with the next half
+// group's terms as soon as its adds are issued, so the LDS loads run half a
+// group ahead of the chain instead of every group's loads (and flag) waiting
+// in front of its adds.  The next group's flag is read between a group's two
+// halves: LDS operations of a wave complete in order, so waiting for the flag
+// costs only the wait for the second half's loads, which its adds need next
+// anyway; the loads of the next group are issued after the flag read that
+// saw it staged (in-order LDS, the staging wave's release), hence see its
+// rows.  No load sits under a branch (a conditional reload made the compiler
+// copy every chunk and drain the loads at each half), and an empty volatile
+// asm on s after each half keeps its adds ahead of the next flag wait.  The last group is
+// added in full: lanes past n publish +0.0 terms (beam_acc of an unused beam)
+// and s + 0.0 == s bit for bit here (s starts at +0.0 and a sum is -0.0 only
+// if both addends are).
+#ifndef LGS_SEQ_PIPE
+#define LGS_SEQ_PIPE 1
+#endif
+constexpr int kPipeC = 4;   // double2 per chunk: 8 terms, 4 chunks per half group
+__device__ __forceinline__ void pipe_load(double2 (&v)[kPipeC], const double* __restrict__ p)
+{
+#pragma unroll
+    for (int q = 0; q < kPipeC; ++q) v[q] = *(const double2*)(p + 2 * q);
+}
+__device__ __forceinline__ double pipe_add(double s, const double2 (&v)[kPipeC])
+{
+#pragma unroll
+    for (int q = 0; q < kPipeC; ++q) {
+        s = s + v[q].x;
+        s = s + v[q].y;
+    }
+    return s;
+}
 __device__ __forceinline__ double seq_add_staged(const double* __restrict__ row, int m, const unsigned* ready,
                                                  const int* abort, unsigned epoch)
 {
+#if LGS_SEQ_PIPE
+    static_assert(8 * 2 * kPipeC == kGroup, "four chunks per half group");
+    const int G = (m + kGroup - 1) / kGroup;
+    auto wait_staged = [&](int gg) {
+        while (__hip_atomic_load(&ready[gg], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != epoch)
+            if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+        return true;
+    };
+    double2 v0[kPipeC], v1[kPipeC], v2[kPipeC], v3[kPipeC];
+    if (!wait_staged(0)) return 0.0;
+    pipe_load(v0, row);
+    pipe_load(v1, row + 8);
+    pipe_load(v2, row + 16);
+    pipe_load(v3, row + 24);
+    double s = 0.0;
+    for (int gg = 0; gg < G; ++gg) {
+        const double* h1 = row + gg * kGroup + 32;
+        __builtin_amdgcn_sched_barrier(0);
+        s = pipe_add(s, v0);
+        pipe_load(v0, h1);
+        __builtin_amdgcn_sched_barrier(0);
+        s = pipe_add(s, v1);
+        pipe_load(v1, h1 + 8);
+        __builtin_amdgcn_sched_barrier(0);
+        s = pipe_add(s, v2);
+        pipe_load(v2, h1 + 16);
+        __builtin_amdgcn_sched_barrier(0);
+        s = pipe_add(s, v3);
+        pipe_load(v3, h1 + 24);
+        // the first half's adds before the flag wait (the compiler would
+        // otherwise sink them past the spin loop: they have no side effects)
+        asm volatile("" : "+v"(s)::"memory");
+        const bool more = gg + 1 < G;
+        if (more && !wait_staged(gg + 1)) return 0.0;
+        const double* n0 = more ? row + (gg + 1) * kGroup : row;   // (past the last group: a harmless reload)
+        __builtin_amdgcn_sched_barrier(0);
+        s = pipe_add(s, v0);
+        pipe_load(v0, n0);
+        __builtin_amdgcn_sched_barrier(0);
+        s = pipe_add(s, v1);
+        pipe_load(v1, n0 + 8);
+        __builtin_amdgcn_sched_barrier(0);
+        s = pipe_add(s, v2);
+        pipe_load(v2, n0 + 16);
+        __builtin_amdgcn_sched_barrier(0);
+        s = pipe_add(s, v3);
+        pipe_load(v3, n0 + 24);
+        asm volatile("" : "+v"(s)::"memory");
+    }
+    return s;
+#else
     double s = 0.0;
     for (int gg = 0; gg * kGroup < m; ++gg) {
         while (__hip_atomic_load(&ready[gg], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != epoch)
@@ -617,6 +702,7 @@ __device__ __forceinline__ double seq_add_staged(const double* __restrict__ row,
         }
     }
     return s;
+#endif
 }
 
 __device__ __forceinline__ bool spin_expired(unsigned long long t0, unsigned long long limit)
