@@ -142,6 +142,10 @@ class Dist:
         if self.world > 1 or force:
             import torch
             import torch.distributed as tdist
+            if self.world == 1:   # LGS_BENCH_DIST without a launcher: a one-rank env:// rendezvous
+                for k, v in (("RANK", "0"), ("LOCAL_RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"),
+                             ("MASTER_PORT", "29531")):
+                    os.environ.setdefault(k, v)
             if self.rehearse:
                 tdist.init_process_group("gloo")
             else:

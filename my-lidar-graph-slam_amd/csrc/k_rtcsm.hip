@@ -1871,6 +1871,13 @@ constexpr int kListMaxNv = 4096;   // work-list batches: Nv bound (the unsafe te
 #define LGS_LIST_WAVES 4096
 #endif
 constexpr int kListWaves = LGS_LIST_WAVES;   // k_coarse_list workgroups (one wave each, grid-stride)
+#ifndef LGS_LIST_XCD
+#define LGS_LIST_XCD 1
+#endif
+#ifndef LGS_XCD2
+#define LGS_XCD2 1   // the same for k_fine_regs, and xcd_block() for the seed kernels
+#endif
+static_assert(kListWaves % 8 == 0, "whole workgroups per XCD");
 constexpr int kUnsafeGroups = 4096;
 
 __global__ __launch_bounds__(64) void k_keep(Items items, WorkList W, DevTs dts)
@@ -1945,7 +1952,18 @@ __global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, i
     const bool lean = items[0].lean != 0;   // the batch's items all run lean or none
     constexpr int kOff = -(1 << 30);
     constexpr int PER = kLC / 64;
+#if LGS_LIST_XCD
+    // XCD-aware split (r06): workgroups go to the 8 XCDs round-robin, so
+    // consecutive quads -- one item's superblocks -- landed on every XCD and
+    // each XCD's L2 held every item's planes; XCD x now takes the x-th eighth
+    // of the list (items contiguous), its workgroups grid-striding over it
+    const int nq = (total + 3) >> 2, xcd = blockIdx.x & 7, per = gridDim.x >> 3;
+    const int qe = (int)(((long long)nq * (xcd + 1)) >> 3);
+    for (int qd = (int)(((long long)nq * xcd) >> 3) + (int)(blockIdx.x >> 3); qd < qe; qd += per) {
+        const int e0 = 4 * qd;   // wave-uniform
+#else
     for (int e0 = 4 * blockIdx.x; e0 < total; e0 += 4 * gridDim.x) {   // wave-uniform
+#endif
         const int e = e0 + g4;
         const bool has = e < total;
         int j = 0;
@@ -2473,11 +2491,16 @@ __device__ __forceinline__ long long seed_pick_wave(const MatchItem& it, const R
 }
 __global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items items, DevTs dts)
 {
+#if LGS_XCD2
+    const Blk sbk = xcd_block();   // an item's workgroups on one XCD (its planes in one L2)
+#else
+    const Blk sbk{ (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z };
+#endif
     const DtsScope dts_scope(dts);
-    const MatchItem& it = items[blockIdx.y];
+    const MatchItem& it = items[sbk.y];
     const RtcsmPlan& pl = it.pl;
     const double* __restrict__ cmap = it.cmap;
-    if (blockIdx.x == 0 && threadIdx.x < 2 && it.keepc) it.keepc[threadIdx.x] = 0;   // before k_keep
+    if (sbk.x == 0 && threadIdx.x < 2 && it.keepc) it.keepc[threadIdx.x] = 0;   // before k_keep
     extern __shared__ char smem[];
     __shared__ double red[2][kSeedMembersThreads / 64][16];
     __shared__ long long s_cand;
@@ -2486,11 +2509,11 @@ __global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items item
     const int Nv = pl.Nv;
     // 1. candidate b by wave 0 (seed_pick_wave)
     if (w == 0) {
-        const long long pick = seed_pick_wave(it, pl, (int)blockIdx.x);
+        const long long pick = seed_pick_wave(it, pl, (int)sbk.x);
         if (lane == 0) s_cand = pick;
     }
     __syncthreads();
-    double* out = it.seedm + 3 * blockIdx.x;
+    double* out = it.seedm + 3 * sbk.x;
     const long long ck = s_cand;
     if (ck == LLONG_MAX) {   // no candidate b: an empty member
         if (tid == 0) {
@@ -2575,8 +2598,13 @@ __global__ __launch_bounds__(kSeedMembersThreads) void k_seed_members(Items item
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* __restrict__ zero, DevTs dts)
 {
+#if LGS_XCD2
+    const Blk sbk = xcd_block();   // an item's workgroups on one XCD (its planes in one L2)
+#else
+    const Blk sbk{ (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z };
+#endif
     const DtsScope dts_scope(dts);
-    const MatchItem& it = items[blockIdx.y];
+    const MatchItem& it = items[sbk.y];
     const RtcsmPlan& pl = it.pl;
     const double* __restrict__ grid = it.grid;
     const double* __restrict__ cmap = it.cmap;
@@ -2585,7 +2613,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
     const int nparts = it.nparts;
     double* __restrict__ Lc = it.Lc;
     RtcsmRecord* rec = it.rec;
-    if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < 2 && it.keepc) it.keepc[threadIdx.x] = 0;   // before k_keep
+    if (MODE == 0 && sbk.x == 0 && threadIdx.x < 2 && it.keepc) it.keepc[threadIdx.x] = 0;   // before k_keep
     extern __shared__ char smem[];
     __shared__ double sv[16];
     __shared__ long long sk[16];
@@ -2615,7 +2643,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             }
             if (tid == 0) sk[0] = LLONG_MAX;
             __builtin_amdgcn_wave_barrier();
-            if (valid && rank == (int)blockIdx.x) {
+            if (valid && rank == (int)sbk.x) {
                 sk[0] = mk;
                 sv[1] = mv;
                 sv[2] = ma;
@@ -2630,8 +2658,8 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             Lmine = seed_fine(pl, grid, zero, sidx, sk[0], sv[1], sv[2], red, reda, sv);
         }
         if (tid == 0) {
-            Lc[blockIdx.x] = Lmine;
-            if (blockIdx.x == 0) rec->coarse_evals = 0ull;   // k_coarse_rows counts
+            Lc[sbk.x] = Lmine;
+            if (sbk.x == 0) rec->coarse_evals = 0ull;   // k_coarse_rows counts
         }
         return;
     }
@@ -2639,10 +2667,10 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
     if (nparts <= kSeedWideMaxParts) {   // candidate b by one wave
         __shared__ int s_nc;
         if (tid < 64) {
-            const long long pick = seed_pick_wave(it, pl, (int)blockIdx.x);
+            const long long pick = seed_pick_wave(it, pl, (int)sbk.x);
             if (tid == 0) {
-                cand[blockIdx.x] = pick;
-                s_nc = (pick != LLONG_MAX) ? (int)blockIdx.x + 1 : 0;
+                cand[sbk.x] = pick;
+                s_nc = (pick != LLONG_MAX) ? (int)sbk.x + 1 : 0;
             }
         }
         __syncthreads();
@@ -2656,7 +2684,7 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
             pv[j] = (i < nparts) ? part_c[i] : -INFINITY;
             pk[j] = (i < nparts) ? part_k[i] : LLONG_MAX;
         }
-        for (; nc <= (int)blockIdx.x; ++nc) {   // candidates 0..blockIdx.x
+        for (; nc <= (int)sbk.x; ++nc) {   // candidates 0..sbk.x
             double bv = -INFINITY;
             long long bk = LLONG_MAX;
 #pragma unroll
@@ -2683,8 +2711,8 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
         }
     }
     LGS_PROBE_MARK();
-    if (nc > (int)blockIdx.x) {
-        const long long ck = cand[blockIdx.x];
+    if (nc > (int)sbk.x) {
+        const long long ck = cand[sbk.x];
         const int ct = (int)(ck / nsb2), csb = (int)(ck % nsb2);
         // 2. member sums: member m = tid % 16, beam group tid / 16 (64 groups);
         // the fine stage's beam row is staged together with the coarse one
@@ -2766,8 +2794,8 @@ __global__ __launch_bounds__(1024) void k_seed_super(Items items, const double* 
     }
     // 4. publish
     if (tid == 0) {
-        Lc[blockIdx.x] = Lmine;
-        if (blockIdx.x == 0) rec->coarse_evals = 0ull;   // k_coarse_rows counts
+        Lc[sbk.x] = Lmine;
+        if (sbk.x == 0) rec->coarse_evals = 0ull;   // k_coarse_rows counts
     }
     LGS_PROBE_MARK();
     LGS_PROBE_PRINT("seed(b0: cand, members, argmax, stage, fine, reduce, publish)");
@@ -3092,7 +3120,15 @@ __global__ __launch_bounds__(64) void k_fine_regs(Items items, int n, const doub
     const bool act = lane < LR * LR;
     const int xo = lane / LR, yo = lane - (lane / LR) * LR;
     typedef double d2v __attribute__((ext_vector_type(2)));
+#if LGS_XCD2
+    // XCD-aware split of the list (as k_coarse_list_c): XCD x takes the x-th
+    // eighth, items contiguous, so an item's map rows stay in one XCD's L2
+    const int xcd = blockIdx.x & 7, per = gridDim.x >> 3;
+    const int ge = (int)(((long long)total * (xcd + 1)) >> 3);
+    for (int g = (int)(((long long)total * xcd) >> 3) + (int)(blockIdx.x >> 3); g < ge; g += per) {
+#else
     for (int g = blockIdx.x; g < total; g += gridDim.x) {   // workgroup-uniform
+#endif
         int lo = 0, hi = n - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
