@@ -928,6 +928,30 @@ __device__ __forceinline__ double seq_sum4(int n, Fetch fetch, Addr addr)
     return s;
 }
 
+// seq_sum4 continuing a sum (k_coarse_list_c's chunks, LGS_LIST_PIPE4)
+template <class Rec, class Fetch, class Addr>
+__device__ __forceinline__ double seq_sum_from4(double s, int n, Fetch fetch, Addr addr)
+{
+    double a[kPipe], b[kPipe], c[kPipe], d[kPipe];
+    issue_batch<Rec>(0, fetch, addr, a);
+    issue_batch<Rec>(kPipe, fetch, addr, b);
+    issue_batch<Rec>(2 * kPipe, fetch, addr, c);
+    for (int v0 = 0; v0 < n; v0 += 4 * kPipe) {
+        issue_batch<Rec>(v0 + 3 * kPipe, fetch, addr, d);
+        add_batch(s, a, n - v0);
+        if (v0 + kPipe >= n) break;
+        issue_batch<Rec>(v0 + 4 * kPipe, fetch, addr, a);
+        add_batch(s, b, n - v0 - kPipe);
+        if (v0 + 2 * kPipe >= n) break;
+        issue_batch<Rec>(v0 + 5 * kPipe, fetch, addr, b);
+        add_batch(s, c, n - v0 - 2 * kPipe);
+        if (v0 + 3 * kPipe >= n) break;
+        issue_batch<Rec>(v0 + 6 * kPipe, fetch, addr, c);
+        add_batch(s, d, n - v0 - 3 * kPipe);
+    }
+    return s;
+}
+
 // --------------------------------------------------------------------------
 // k_coarse: one lane per coarse block (t, jx, jy) of one search angle t per
 // workgroup (blockDim = P rounded up to 64); lanes sweep jx fastest.  Each lane
@@ -1940,12 +1964,19 @@ __device__ __forceinline__ int list_prefix(const WorkList& W, int which, int n, 
 // CU): the next chunk is loaded into registers while the current one is
 // summed, then written to LDS; the sum carries over the chunks in beam order
 // (seq_sum_from).
-constexpr int kLC = 256;
+#ifndef LGS_LC
+#define LGS_LC 256
+#endif
+#ifndef LGS_LIST_PIPE4
+#define LGS_LIST_PIPE4 0   // 1: four gather batches in flight per lane (seq_sum_from4)
+#endif
+constexpr int kLC = LGS_LC;
+constexpr int kLCPad = (LGS_LIST_PIPE4 ? 4 : 2) * kPipe;   // look-ahead entries past a staged chunk
 static_assert(kLC % 64 == 0, "whole waves per chunk row");
 __global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, int n, const double* __restrict__ zero, DevTs dts)
 {
     const DtsScope dts_scope(dts);
-    __shared__ int s_cb[4][kLC + 2 * kPipe];
+    __shared__ int s_cb[4][kLC + kLCPad];
     const int lane = threadIdx.x, g4 = lane >> 4, m = lane & 15;
     int c;
     const int total = list_prefix(W, 0, n, c);
@@ -2034,13 +2065,18 @@ __global__ __launch_bounds__(64) void k_coarse_list_c(Items items, WorkList W, i
             for (int q = 0; q < 4; ++q) {
 #pragma unroll
                 for (int i = 0; i < PER; ++i) s_cb[q][lane + 64 * i] = pre[q][i];
-                if (lane < 2 * kPipe) s_cb[q][kLC + lane] = kOff;   // seq_sum's look-ahead
+                if (lane < kLCPad) s_cb[q][kLC + lane] = kOff;   // seq_sum's look-ahead
             }
             if (v0 + kLC < nmax) fetch_chunk(v0 + kLC);
             const int cnt = min(kLC, nmax - v0);
             const int* __restrict__ my = s_cb[g4];
+#if LGS_LIST_PIPE4
+            sum = seq_sum_from4<int>(sum, cnt, [&](int v) { return my[v]; },
+                                     [&](const int& cc) { return (active && cc != kOff) ? lane_base + cc : zero; });
+#else
             sum = seq_sum_from<int>(sum, cnt, [&](int v) { return my[v]; },
                                     [&](const int& cc) { return (active && cc != kOff) ? lane_base + cc : zero; });
+#endif
         }
         if (active) {
             const long long k = (long long)t * pl.P + (long long)jx * pl.ncy + jy;
