@@ -62,7 +62,7 @@ def parse():
                     help="diagnostics only: comma-separated kernel names not launched (results invalid)")
     ap.add_argument("--super-prune", type=int, default=1,
                     help="A/B: 1 superblock pruning of the coarse stage, 0 score every coarse block")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=2,
                     help="match workload: concurrent HIP streams (lgs contexts) per GPU, one host thread each")
     ap.add_argument("--batch", type=int, default=128,
                     help="match workload: queries per call (lgs_rtcsm_optimize_pose_query_batch runs them as "

@@ -276,7 +276,7 @@ struct PendingTiming {
 // every kDtsEvery-th stamp the end (the last workgroup to finish is one of
 // the last dispatched when workgroups carry even work).
 constexpr int kDtsSub = 8;
-constexpr int kDtsEvery = 32;
+constexpr int kDtsEvery = 31;   // odd: a multiple of 8 would sample only blockIdx % 8 == 0 (XCD 0)
 constexpr int kDtsSlots = 32;   // device-timed launches per chunk
 constexpr unsigned long long kDtsMask = (1ull << 40) - 1ull;
 struct DevTs {

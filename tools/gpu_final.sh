@@ -19,11 +19,12 @@ for ph in $PHASES; do
     WORKLOAD=match python3 tools/pmc_summary.py $OUT/trace_$TAG $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG $OUT/pmc_l2_$TAG $OUT/$TAG > $OUT/${TAG}_summary.log 2>&1 || exit $?
     cp $OUT/${TAG}_pmc.json profiles/pmc_summary.json
     grep '^{' $OUT/trace_$TAG.log | tail -n 1 > $OUT/${TAG}_trace_run_bench.json
-    # the timed region's dispatches: 3 streams x 10 warm-up calls x 2 chunks before it, the 8-call one-stream pass after
+    # the timed region's dispatches: streams (bench default 2) x 10 warm-up calls x 2 chunks before it, the
+    # 8-call one-stream pass after (HEAD / TAIL override)
     read ALGO ALGOS < <(python3 -c "import json;d=json.loads(open('$OUT/${TAG}_trace_run_bench.json').read());print(d['roofline']['algo_bytes_per_launch'], d['roofline_super']['algo_bytes_per_launch'])") || exit 1
     TR=$(find $OUT/trace_$TAG -name '*kernel_trace.csv' | head -1)
-    python3 tools/trace_coarse.py $TR k_coarse_list $ALGO 60 16 > $OUT/${TAG}_coarse_split.json || exit 1
-    python3 tools/trace_coarse.py $TR "k_super_oct<5" $ALGOS 60 16 > $OUT/${TAG}_super_split.json || exit 1
+    python3 tools/trace_coarse.py $TR k_coarse_list $ALGO ${HEAD:-40} ${TAIL:-16} > $OUT/${TAG}_coarse_split.json || exit 1
+    python3 tools/trace_coarse.py $TR "k_super_oct<5" $ALGOS ${HEAD:-40} ${TAIL:-16} > $OUT/${TAG}_super_split.json || exit 1
     find $OUT/trace_$TAG -name '*kernel_stats.csv' -exec cp {} $OUT/${TAG}_run_kernel_stats.csv \;
     rm -rf $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG $OUT/pmc_l2_$TAG $OUT/trace_$TAG ;;
   bench)
