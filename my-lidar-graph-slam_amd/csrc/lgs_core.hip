@@ -980,6 +980,157 @@ __global__ __launch_bounds__(256) void k_precompute_planes(const PrecompJob* __r
     }
 }
 
+// Column-streaming batched precompute: one workgroup walks kSub consecutive
+// kPTY-row tiles of one tile column, so a footprint row is loaded once (the
+// LR - 1 halo rows carry over in registers) and the next tile's rows are in
+// flight while this tile's x pass runs.  Tiles, zero-tile words and outputs
+// are those of k_precompute_planes<LR, kPTY> (tile row by = blockIdx.y *
+// kSub + s of gyt).
+#ifndef LGS_PTY_SUB
+#define LGS_PTY_SUB 2   // measured (64 config-2 maps, one stream): 1: 0.145 ms, 2: 0.116, 3: 0.124, 4: 0.120, 8: 0.122
+#endif
+template <int LR, int kPTY, int kSub>
+__global__ __launch_bounds__(256) void k_precompute_planes_s(const PrecompJob* __restrict__ jobs, int gyt, DevTs dts)
+{
+    const DtsScope dts_scope(dts);
+    const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
+    const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    const int bx = __builtin_amdgcn_readfirstlane(l % gx), bys = __builtin_amdgcn_readfirstlane((l / gx) % gy),
+              bz = __builtin_amdgcn_readfirstlane(l / (gx * gy));
+    const PrecompJob& j = jobs[bz];
+    const int W = j.W, H = j.H;
+    constexpr int kPQX = pqx<LR>();
+    constexpr int FW = kPQX * LR + LR - 1;
+    static_assert(FW <= 256, "one footprint column per thread");
+    constexpr int FH = kPTY + LR - 1;
+    const int x0 = bx * kPQX * LR;
+    if (x0 >= W) return;   // past this job's map (uniform)
+    const int x1 = min(x0 + kPQX * LR, W);
+    const int sx0 = win_start(x0, W, LR);
+    const int fw = win_start(x1 - 1, W, LR) + LR - sx0;
+    __shared__ double m1[kPTY][FW];
+    const double* __restrict__ in = j.in;
+    const int tid = threadIdx.x;
+    const int xx = sx0 + tid;
+    const bool col = tid < fw, cin = col && xx < W;   // reads past the end are 0
+    const int nq = (x1 - x0) / LR, np = (nq + 1) >> 1;
+    const PlaneGeom& pg = j.pg;
+    double* __restrict__ out = j.out;
+    double v[FH];
+    const int by0 = bys * kSub;
+    // prologue: the first tile's footprint rows
+    int sy0 = win_start(by0 * kPTY, H, LR);
+    if (by0 >= gyt || by0 * kPTY >= H) return;
+#pragma unroll
+    for (int k = 0; k < FH; ++k) {
+        const int yy = sy0 + k;
+        v[k] = (cin && yy < H) ? gload(in + ((size_t)yy * W + xx)) : 0.0;
+    }
+    for (int s = 0; s < kSub; ++s) {
+        const int by = by0 + s, y0 = by * kPTY;
+        if (by >= gyt || y0 >= H) break;   // uniform
+        const int y1 = min(y0 + kPTY, H), oh = y1 - y0;
+        int nz = 0;
+#pragma unroll
+        for (int k = 0; k < FH; ++k) nz |= __double_as_longlong(v[k]) != 0;
+        double wm[kPTY];
+#pragma unroll
+        for (int k = 0; k < kPTY; ++k) {
+            double m = v[k];
+#pragma unroll
+            for (int i = 1; i < LR; ++i) m = dmax(m, v[k + i]);
+            wm[k] = m;
+        }
+        if (s > 0) __syncthreads();   // the previous tile's x pass is done with m1
+        const int d = y0 - sy0, st = max(0, H - LR - sy0);
+        if (col) {
+            if (d == 0 && st >= kPTY - 1) {
+#pragma unroll
+                for (int oy = 0; oy < kPTY; ++oy)
+                    if (oy < oh) m1[oy][tid] = wm[oy];
+            } else {
+#pragma unroll
+                for (int oy = 0; oy < kPTY; ++oy) {
+                    const int sr = min(oy + d, st);
+                    double m = wm[0];
+#pragma unroll
+                    for (int k = 1; k < kPTY; ++k) m = (k == sr) ? wm[k] : m;
+                    if (oy < oh) m1[oy][tid] = m;
+                }
+            }
+        }
+        // the next tile's rows go in flight now (its halo rows carry over when
+        // its footprint continues this one's), under this tile's x pass
+        const int nby = by + 1;
+        if (s + 1 < kSub && nby < gyt && nby * kPTY < H) {
+            const int nsy0 = win_start(nby * kPTY, H, LR);
+            if (nsy0 == sy0 + kPTY) {
+#pragma unroll
+                for (int k = 0; k < LR - 1; ++k) v[k] = v[k + kPTY];
+#pragma unroll
+                for (int k = LR - 1; k < FH; ++k) {
+                    const int yy = nsy0 + k;
+                    v[k] = (cin && yy < H) ? gload(in + ((size_t)yy * W + xx)) : 0.0;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < FH; ++k) {
+                    const int yy = nsy0 + k;
+                    v[k] = (cin && yy < H) ? gload(in + ((size_t)yy * W + xx)) : 0.0;
+                }
+            }
+            sy0 = nsy0;
+        }
+        unsigned* zw = j.zt ? j.zt + (by * gx + bx) : nullptr;   // uniform per workgroup
+        if (zw) {
+            const unsigned zprev = *zw;
+            const int anynz = __syncthreads_or(nz);
+            if (tid == 0 && zprev != (anynz ? 0u : 1u)) *zw = anynz ? 0u : 1u;
+            if (!anynz && zprev == 1u) continue;
+        } else {
+            __syncthreads();
+        }
+        for (int k = tid; k < oh * LR * (kPQX / 2); k += 256) {   // as k_precompute_planes
+            const int oy = k / (LR * (kPQX / 2)), rem = k % (LR * (kPQX / 2));
+            const int rx = rem / (kPQX / 2), p = rem % (kPQX / 2);
+            if (p >= np) continue;
+            const int qxl = 2 * p;
+            const int xa = x0 + qxl * LR + rx;
+            const double* ca = &m1[oy][win_start(xa, W, LR) - sx0];
+            double ma = ca[0];
+#pragma unroll
+            for (int i = 1; i < LR; ++i) ma = dmax(ma, ca[i]);
+            const int y = y0 + oy, qy = y / LR, ry = y - qy * LR;
+            const long long o = (ry * LR + rx) * pg.pstride + (long long)(qy + pg.M) * pg.Wqp + (x0 / LR + qxl) + pg.M;
+            double* dst = out + o;
+            if (qxl + 1 < nq) {
+                const int xb = xa + LR;
+                const double* cb = &m1[oy][win_start(xb, W, LR) - sx0];
+                double mb = cb[0];
+#pragma unroll
+                for (int i = 1; i < LR; ++i) mb = dmax(mb, cb[i]);
+                d2a16 vv;
+                vv.x = ma;
+                vv.y = mb;
+                gstore((d2a16*)dst, vv);
+                if (j.out16) {
+                    gstore((unsigned*)(j.out16 + o),
+                           (unsigned)half_round_up_bits(ma) | ((unsigned)half_round_up_bits(mb) << 16));
+                    if (ma < 0.0 || mb < 0.0) gstore(j.negflag, j.pgen);
+                }
+            } else {
+                gstore(dst, ma);
+                if (j.out16) {
+                    gstore(j.out16 + o, half_round_up_bits(ma));
+                    if (ma < 0.0) gstore(j.negflag, j.pgen);
+                }
+            }
+        }
+    }
+}
+
 // Batched: job blockIdx.z (maps of a batch may differ in size; the grid
 // covers the largest, tiles past a job's map exit).
 // XCD-aware order (speed only): one map's tiles on one XCD (see k_rtcsm.hip xcd_block)
@@ -1091,7 +1242,12 @@ void launch_precompute_jobs(lgs_ctx* ctx, const PrecompJob* d_jobs, int njobs, i
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_precompute_planes<L, LGS_PTY_LONE>), \
                     dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + LGS_PTY_LONE - 1) / LGS_PTY_LONE, njobs), \
                     dim3(256), 0, ctx->stream, d_jobs, ctx->dts(tok)); \
-            else \
+            else if (LGS_PTY_SUB > 1) { \
+                const int gyt = (maxH + LGS_PTY_BATCH - 1) / LGS_PTY_BATCH; \
+                hipLaunchKernelGGL(HIP_KERNEL_NAME(k_precompute_planes_s<L, LGS_PTY_BATCH, LGS_PTY_SUB>), \
+                    dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (gyt + LGS_PTY_SUB - 1) / LGS_PTY_SUB, njobs), \
+                    dim3(256), 0, ctx->stream, d_jobs, gyt, ctx->dts(tok)); \
+            } else \
                 hipLaunchKernelGGL(HIP_KERNEL_NAME(k_precompute_planes<L, LGS_PTY_BATCH>), \
                     dim3((maxW + pqx<L>() * L - 1) / (pqx<L>() * L), (maxH + LGS_PTY_BATCH - 1) / LGS_PTY_BATCH, njobs), dim3(256), 0, ctx->stream, \
                     d_jobs, ctx->dts(tok)); \

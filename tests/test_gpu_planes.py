@@ -119,7 +119,11 @@ def check_super(P, S, lr, L):
     # planes + units in one pass (k_planes_super) and in two (precompute +
     # k_super_planes); maps not a multiple of 16 coarse rows, 80-row quads
     (5, 400, 2, (4.0, 4.0), 1), (5, 400, 2, (4.0, 4.0), 0), (5, 455, 2, (5.0, 5.4), 1), (5, 455, 2, (5.0, 5.4), 0),
-    (5, 1000, 2, (4.0, 4.0), 1), (5, 35, 2, (1.0, 1.2), 1)])
+    (5, 1000, 2, (4.0, 4.0), 1), (5, 35, 2, (1.0, 1.2), 1),
+    # last 8-row tile starting inside the final window (1008 > 1010 - 5): its
+    # footprint does not continue the previous tile's (the streaming batched
+    # precompute reloads instead of carrying the halo rows)
+    (5, 1010, 2, (1.0, 1.2), 1)])
 def test_device_coarse_planes(ctx, world, lr, n, batch, rxy, fused):
     rng = np.random.default_rng(lr * 100 + n)
     cells = np.where(rng.random((n, n)) < 0.3, rng.choice([0.001, 0.3, 0.45, 0.6, 0.999], (n, n)), 0.0)
